@@ -1,0 +1,505 @@
+#!/usr/bin/env python3
+"""Generate golden vectors by importing the *reference* implementation.
+
+This script runs ONLY in the build container (where /root/reference exists). It
+imports the reference's Python modules (read-only, never copied) and records
+inputs/outputs as small .npz fixtures under tests/golden/. The fixtures are data
+(inputs and expected outputs); the reference source itself never ships.
+
+Missing third-party packages that the reference imports but never calls on the
+hot path (gymnasium.spaces.Discrete, torch_geometric names, tensorboard) are
+replaced by tiny stubs written to a temporary directory.
+
+Usage:  python tests/golden/make_golden.py [--ref /root/reference/src]
+"""
+import argparse
+import copy
+import hashlib
+import os
+import sys
+import tempfile
+import textwrap
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+def write_stubs(root):
+    files = {
+        "gymnasium/__init__.py": "",
+        "gymnasium/spaces.py": textwrap.dedent(
+            """
+            import numpy as np
+            class Discrete:
+                def __init__(self, n, start=0):
+                    self.n = n
+                    self.start = start
+                def sample(self):
+                    return self.start + np.random.randint(self.n)
+            """
+        ),
+        "torch_geometric/__init__.py": "",
+        "torch_geometric/nn/__init__.py": textwrap.dedent(
+            """
+            class _Missing:
+                def __init__(self, *a, **k):
+                    raise ImportError("torch_geometric is not installed")
+            GCNConv = SAGEConv = AntiSymmetricConv = GraphSAGE = _Missing
+            """
+        ),
+        "torch_geometric/nn/summary.py": "def summary(model, *a, **k):\n    return 'summary'\n",
+        "torch_geometric/utils/__init__.py": textwrap.dedent(
+            """
+            def dense_to_sparse(*a, **k):
+                raise ImportError("torch_geometric is not installed")
+            """
+        ),
+    }
+    for rel, txt in files.items():
+        p = os.path.join(root, rel)
+        os.makedirs(os.path.dirname(p), exist_ok=True)
+        with open(p, "w") as f:
+            f.write(txt)
+
+
+def sha(a):
+    return hashlib.sha1(np.ascontiguousarray(a).tobytes()).hexdigest()
+
+
+# ---------------------------------------------------------------------------
+# RNG goldens (numpy legacy MT19937 as the reference uses it)
+# ---------------------------------------------------------------------------
+def gen_rng(out):
+    seeds = [0, 1, 42, 476, 923430603, 2**32 - 1]
+    d = {"seeds": np.array(seeds, dtype=np.uint64)}
+    for s in seeds:
+        rs = np.random.RandomState(s)
+        d[f"key_{s}"] = rs.get_state()[1].astype(np.uint32)
+        rs = np.random.RandomState(s)
+        d[f"raw_{s}"] = rs.randint(0, 2**32, size=1500, dtype=np.uint64).astype(np.uint32)
+        rs = np.random.RandomState(s)
+        # the exact call pattern of Routing.reset_packet for N=20
+        mix = []
+        for _ in range(100):
+            mix.append(float(rs.randint(20)))
+            mix.append(float(rs.randint(20)))
+            mix.append(rs.random())
+        d[f"packet20_{s}"] = np.array(mix, dtype=np.float64)
+        rs = np.random.RandomState(s)
+        d[f"randint31_{s}"] = np.array([rs.randint(2**31 - 1) for _ in range(64)], dtype=np.int64)
+        rs = np.random.RandomState(s)
+        eg = []
+        for _ in range(40):
+            eg.append(rs.randint(4, size=20).astype(np.float64))
+            eg.append(rs.rand(20))
+        d[f"egreedy_{s}"] = np.stack(eg)
+        rs = np.random.RandomState(s)
+        d[f"randint_n_{s}"] = np.array(
+            [rs.randint(n) for n in [1, 2, 3, 5, 7, 10, 13, 20, 33, 50, 64, 100, 1000] * 20],
+            dtype=np.int64,
+        )
+    np.savez_compressed(out, **d)
+
+
+# ---------------------------------------------------------------------------
+# Topology goldens
+# ---------------------------------------------------------------------------
+def topo_record(net):
+    n = net.n_nodes
+    pos = np.array([[nd.x, nd.y] for nd in net.nodes], dtype=np.float64)
+    edges = np.array([[e.start, e.end, e.length] for e in net.edges], dtype=np.int64)
+    node_edges = np.array([nd.edges for nd in net.nodes], dtype=np.int64)
+    neighbors = np.array([nd.neighbors for nd in net.nodes], dtype=np.int64)
+    apsp = np.array(
+        [[net.shortest_paths_weights[i][j] for j in range(n)] for i in range(n)], dtype=np.int64
+    )
+    return dict(
+        seed=int(net.current_topology_seed),
+        repetitions=int(net.repetitions),
+        pos=pos,
+        edges=edges,
+        node_edges=node_edges,
+        neighbors=neighbors,
+        apsp=apsp,
+        adj=net.adj_matrix.astype(np.int8),
+    )
+
+
+def gen_topology(out, Network, EVAL_SEEDS):
+    d = {}
+    # random topologies drawn through the main stream (training path), EVAL_SEEDS excluded
+    for n, main_seed, count in [(10, 11, 24), (20, 12, 24), (30, 13, 12), (40, 14, 12), (50, 15, 12), (100, 16, 6)]:
+        np.random.seed(main_seed)
+        net = Network(n_nodes=n, random_topology=True, excluded_seeds=EVAL_SEEDS)
+        recs = []
+        for _ in range(count):
+            net.reset()
+            recs.append(topo_record(net))
+        # main stream position after the resets: next raw draws
+        post = np.random.randint(0, 2**32, size=4, dtype=np.uint64).astype(np.uint32)
+        key = f"rand_n{n}"
+        d[key + "_main_seed"] = np.int64(main_seed)
+        d[key + "_post_raw"] = post
+        for k in ["seed", "repetitions"]:
+            d[key + "_" + k] = np.array([r[k] for r in recs], dtype=np.int64)
+        for k in ["pos", "edges", "node_edges", "neighbors", "apsp", "adj"]:
+            d[key + "_" + k] = np.stack([r[k] for r in recs])
+    # fixed seeds
+    for s in [476, 923430603] + list(EVAL_SEEDS[:30]):
+        net = Network(n_nodes=20, random_topology=False, topology_init_seed=s)
+        np.random.seed(0)
+        net.reset()
+        r = topo_record(net)
+        for k, v in r.items():
+            d[f"fixed_{s}_{k}"] = np.asarray(v)
+    d["fixed_seeds"] = np.array([476, 923430603] + list(EVAL_SEEDS[:30]), dtype=np.int64)
+    # build_seed_list (used for --num-topologies-train and EVAL_SEEDS)
+    for n, init, cnt in [(20, 476, 40), (20, 1234, 16), (10, 99, 16), (50, 7, 8)]:
+        net = Network(n_nodes=n, random_topology=True, n_random_seeds=cnt, topology_init_seed=init)
+        d[f"seedlist_n{n}_i{init}"] = np.array(net.seeds, dtype=np.int64)
+    np.savez_compressed(out, **d)
+
+
+# ---------------------------------------------------------------------------
+# Environment traces
+# ---------------------------------------------------------------------------
+ENV_CONFIGS = [
+    # name, n_nodes, n_data, topology mode, topo arg, congestion, action mask, ttl, env seed, steps, episode steps, egreedy eps (None = tape)
+    dict(name="fixed476", n=20, a=20, mode="fixed", topo=476, cong=True, mask=False, ttl=0, seed=0, T=300, ep=300, eps=None),
+    dict(name="fixed923", n=20, a=20, mode="fixed", topo=923430603, cong=True, mask=False, ttl=0, seed=7, T=300, ep=300, eps=None),
+    dict(name="rand20", n=20, a=20, mode="random", topo=476, cong=True, mask=False, ttl=0, seed=3, T=200, ep=50, eps=None),
+    dict(name="rand10_nocong", n=10, a=30, mode="random", topo=476, cong=False, mask=False, ttl=0, seed=5, T=150, ep=50, eps=None),
+    dict(name="rand50", n=50, a=20, mode="random", topo=476, cong=True, mask=False, ttl=0, seed=9, T=100, ep=50, eps=None),
+    dict(name="fixed476_ttl_mask", n=20, a=20, mode="fixed", topo=476, cong=True, mask=True, ttl=10, seed=1, T=200, ep=100, eps=None),
+    dict(name="list5", n=20, a=20, mode="list", topo=1234, cong=True, mask=False, ttl=0, seed=2, T=120, ep=20, eps=None),
+    dict(name="evalseq", n=20, a=20, mode="sequential", topo=476, cong=True, mask=False, ttl=0, seed=4, T=100, ep=20, eps=None),
+    dict(name="egreedy_rand20", n=20, a=20, mode="random", topo=476, cong=True, mask=False, ttl=0, seed=11, T=150, ep=50, eps=0.3),
+    dict(name="fixed476_a1", n=20, a=1, mode="fixed", topo=476, cong=True, mask=False, ttl=0, seed=13, T=60, ep=60, eps=None),
+]
+FULL_STEPS = (0, 1, 2, 3, 26, 52)  # snapshot indices with full arrays
+
+
+def gen_env(out_dir, Network, Routing, EVAL_SEEDS):
+    """Per config: a snapshot stream. Snapshot 0 is the initial reset; then every
+    env.step(t) appends a snapshot, and an episode reset (episode_steps reached)
+    appends another snapshot with kind=1 right after the step's snapshot."""
+    for cfg in ENV_CONFIGS:
+        n, a = cfg["n"], cfg["a"]
+        if cfg["mode"] == "fixed":
+            net = Network(n_nodes=n, random_topology=False, topology_init_seed=cfg["topo"])
+        elif cfg["mode"] == "random":
+            net = Network(n_nodes=n, random_topology=True, topology_init_seed=cfg["topo"], excluded_seeds=EVAL_SEEDS)
+        elif cfg["mode"] == "list":
+            net = Network(n_nodes=n, random_topology=True, n_random_seeds=5, topology_init_seed=cfg["topo"], excluded_seeds=EVAL_SEEDS)
+        elif cfg["mode"] == "sequential":
+            net = Network(n_nodes=n, random_topology=True, provided_seeds=list(EVAL_SEEDS[:8]), sequential_topology_seeds=True)
+        else:
+            raise ValueError(cfg["mode"])
+        env = Routing(net, a, 1, enable_congestion=cfg["cong"], enable_action_mask=cfg["mask"], ttl=cfg["ttl"])
+        tape_rng = np.random.RandomState(1000 + cfg["seed"])
+        np.random.seed(cfg["seed"])
+        snap_keys = ["kind", "step", "now", "target", "edge", "time", "ttl", "size", "start", "spw", "visited",
+                     "agent_steps", "loads", "topo_seed", "action_mask", "obs_sha", "nodeobs_sha", "adj_sha",
+                     "nodeagent_sha"]
+        step_keys = ["reward", "done", "actions", "q", "info_looped", "info_throughput", "info_dropped",
+                     "info_blocked", "info_ndelays", "info_narrived"]
+        rec = {k: [] for k in snap_keys + step_keys}
+        lists = {"delays": [], "delays_arrived": [], "spr": []}
+        full = {}
+        topo = []
+        final_info = []
+
+        def snap(kind, t, obs, adj):
+            E = len(env.network.edges)
+            si = len(rec["kind"])
+            rec["kind"].append(kind)
+            rec["step"].append(t)
+            rec["now"].append([p.now for p in env.data])
+            rec["target"].append([p.target for p in env.data])
+            rec["edge"].append([p.edge for p in env.data])
+            rec["time"].append([p.time for p in env.data])
+            rec["ttl"].append([p.ttl for p in env.data])
+            rec["size"].append([p.size for p in env.data])
+            rec["start"].append([p.start for p in env.data])
+            rec["spw"].append([p.shortest_path_weight for p in env.data])
+            rec["visited"].append([sum(1 << v for v in p.visited_nodes) for p in env.data])
+            rec["agent_steps"].append(env.agent_steps.copy())
+            loads = np.zeros(3 * n // 2, dtype=np.float64)
+            loads[:E] = [float(e.load) for e in env.network.edges]
+            rec["loads"].append(loads)
+            rec["topo_seed"].append(int(env.network.current_topology_seed))
+            rec["action_mask"].append(env.action_mask.astype(np.int8).copy())
+            nobs = env.get_node_observation()
+            nagent = env.get_node_agent_matrix()
+            rec["obs_sha"].append(sha(obs.astype(np.float32)))
+            rec["nodeobs_sha"].append(sha(nobs.astype(np.float32)))
+            rec["adj_sha"].append(sha(adj.astype(np.int8)))
+            rec["nodeagent_sha"].append(sha(nagent.astype(np.int8)))
+            if si in FULL_STEPS:
+                full[f"obs_{si}"] = obs.astype(np.float32)
+                full[f"nodeobs_{si}"] = nobs.astype(np.float32)
+                full[f"adj_{si}"] = adj.astype(np.int8)
+                full[f"nodeagent_{si}"] = nagent.astype(np.int8)
+            if kind == 1:
+                r = topo_record(env.network)
+                r["aux"] = env.get_node_aux()
+                topo.append(r)
+
+        obs, adj = env.reset()
+        snap(1, 0, obs, adj)
+        ep_step = 0
+        for t in range(1, cfg["T"] + 1):
+            if cfg["eps"] is None:
+                act = tape_rng.randint(4, size=a)
+                q = np.zeros((a, 4), dtype=np.float32)
+            else:
+                q = tape_rng.standard_normal((a, 4)).astype(np.float32)
+                ra = np.random.randint(4, size=a)
+                rf = np.random.rand(a) < cfg["eps"]
+                act = np.argmax(q, axis=-1) * ~rf + rf * ra
+            rec["q"].append(q)
+            rec["actions"].append(np.asarray(act, dtype=np.int64))
+            obs, adj, reward, done, info = env.step(act)
+            rec["reward"].append(reward.copy())
+            rec["done"].append(done.astype(np.int8))
+            rec["info_looped"].append(float(info["looped"]))
+            rec["info_throughput"].append(int(info["throughput"]))
+            rec["info_dropped"].append(int(info["dropped"]))
+            rec["info_blocked"].append(int(info["blocked"]))
+            rec["info_ndelays"].append(len(info["delays"]))
+            rec["info_narrived"].append(len(info["delays_arrived"]))
+            for k in lists:
+                lists[k].extend([float(x) for x in info[k]])
+            snap(0, t, obs, adj)
+            ep_step += 1
+            if ep_step >= cfg["ep"]:
+                fi = env.get_final_info({"delays": []})
+                final_info.append([float(x) for x in fi["delays"]] + [-1.0])
+                obs, adj = env.reset()
+                ep_step = 0
+                snap(1, t, obs, adj)
+
+        d = {}
+        for k, v in rec.items():
+            if k.endswith("_sha"):
+                d[k] = np.array(v)
+            elif k == "visited":
+                d[k] = np.array(v, dtype=np.uint64)
+            elif k in ("size", "loads", "agent_steps", "info_looped"):
+                d[k] = np.array(v, dtype=np.float64)
+            elif k in ("reward", "q"):
+                d[k] = np.array(v, dtype=np.float32)
+            else:
+                d[k] = np.array(v, dtype=np.int64)
+        for k, v in lists.items():
+            d["list_" + k] = np.array(v, dtype=np.float64)
+        d["final_delays"] = np.array(sum(final_info, []), dtype=np.float64)
+        for k, v in full.items():
+            d["full_" + k] = v
+        for i, r in enumerate(topo):
+            for k in ["seed", "edges", "node_edges", "apsp", "adj", "aux"]:
+                d[f"topo{i}_{k}"] = np.asarray(r[k])
+        d["n_topo"] = np.int64(len(topo))
+        for k, v in cfg.items():
+            d[f"cfg_{k}"] = np.array(-1 if v is None else v)
+        np.savez_compressed(os.path.join(out_dir, f"env_{cfg['name']}.npz"), **d)
+        print("env", cfg["name"], "done", flush=True)
+
+
+# ---------------------------------------------------------------------------
+# NetMon / DQN / training-step goldens
+# ---------------------------------------------------------------------------
+def collect_graph_inputs(Network, Routing, EVAL_SEEDS, n, a, B, steps, seed):
+    """node obs / adj / node-agent for B independent envs over `steps` consecutive steps."""
+    obs_l, adj_l, na_l, aobs_l = [], [], [], []
+    rng = np.random.RandomState(seed + 77)
+    envs = []
+    for b in range(B):
+        np.random.seed(seed + b)
+        net = Network(n_nodes=n, random_topology=True, excluded_seeds=EVAL_SEEDS)
+        env = Routing(net, a, 1)
+        env.reset()
+        envs.append(env)
+    for t in range(steps):
+        o, ad, na, ao = [], [], [], []
+        for env in envs:
+            o.append(env.get_node_observation())
+            ad.append(env.get_nodes_adjacency().astype(np.float32))
+            na.append(env.get_node_agent_matrix().astype(np.float32))
+            ao.append(env._get_observation())
+            env.step(rng.randint(4, size=a))
+        obs_l.append(np.stack(o))
+        adj_l.append(np.stack(ad))
+        na_l.append(np.stack(na))
+        aobs_l.append(np.stack(ao))
+    return np.stack(obs_l), np.stack(adj_l), np.stack(na_l), np.stack(aobs_l)
+
+
+def sd_to_npz(prefix, sd, d):
+    for k, v in sd.items():
+        d[f"{prefix}{k}"] = v.detach().cpu().numpy()
+
+
+def gen_netmon(out, Network, Routing, EVAL_SEEDS, NetMon, DQN):
+    import torch
+    import torch.nn.functional as F
+
+    d = {}
+    n, a, B, steps = 20, 20, 4, 3
+    node_obs, node_adj, node_agent, agent_obs = collect_graph_inputs(Network, Routing, EVAL_SEEDS, n, a, B, steps, 100)
+    d["node_obs"], d["node_adj"], d["node_agent"], d["agent_obs"] = node_obs, node_adj, node_agent, agent_obs
+    # variant 0 is the production configuration (H=128, encoder 512,256); the rest use
+    # small dimensions to keep the fixture small (the kernels are dimension-generic)
+    variants = [
+        ("lstm", "sum", 1, 128, (512, 256)), ("lstm", "sum", 3, 32, (64, 48)),
+        ("lstm", "mean", 2, 32, (64, 48)), ("lnlstm", "sum", 1, 32, (64, 48)),
+        ("lnlstm", "mean", 3, 32, (64, 48)), ("gru", "sum", 2, 32, (64, 48)),
+    ]
+    d["variants"] = np.array([f"{r}|{g}|{k}|{h}|{e[0]},{e[1]}" for r, g, k, h, e in variants])
+    for vi, (rnn, agg, K, H, enc) in enumerate(variants):
+        torch.manual_seed(vi)
+        nm = NetMon(node_obs.shape[-1], H, list(enc), K, F.leaky_relu, rnn_type=rnn,
+                    rnn_carryover=True, agg_type=agg, output_neighbor_hidden=True,
+                    output_global_hidden=False)
+        nm.eval()
+        sd_to_npz(f"v{vi}_w_", nm.state_dict(), d)
+        nm.state = None
+        with torch.no_grad():
+            for t in range(steps):
+                x = torch.tensor(node_obs[t])
+                m = torch.tensor(node_adj[t])
+                na = torch.tensor(node_agent[t])
+                state_in = None if nm.state is None else nm.state.clone()
+                h = nm(x, m, na, no_agent_mapping=True)
+                mapped = NetMon.output_to_network_obs(h, na)
+                d[f"v{vi}_h_{t}"] = h.numpy()
+                d[f"v{vi}_mapped_{t}"] = mapped.numpy()
+                d[f"v{vi}_state_{t}"] = nm.state.numpy()
+                if state_in is not None:
+                    d[f"v{vi}_statein_{t}"] = state_in.numpy()
+    # DQN policy network on the joint observation (agent obs ++ NetMon graph obs)
+    torch.manual_seed(42)
+    joint = np.concatenate([agent_obs[0], d["v0_mapped_0"]], axis=-1).astype(np.float32)
+    dqn = DQN(joint.shape[-1], [512, 256], 4, F.leaky_relu)
+    sd_to_npz("dqn_w_", dqn.state_dict(), d)
+    with torch.no_grad():
+        q = dqn(torch.tensor(joint), None)
+    d["dqn_obs"] = joint
+    d["dqn_q"] = q.numpy()
+    np.savez_compressed(out, **d)
+
+
+def gen_train(out, Network, Routing, EVAL_SEEDS, NetMon, DQN, interpolate_model):
+    """One DQN+NetMon update exactly as src/main.py:832-1022 performs it (sequence replay)."""
+    import torch
+    import torch.nn.functional as F
+    import torch.optim as optim
+
+    d = {}
+    n, a, B, L = 20, 20, 3, 3
+    node_obs, node_adj, node_agent, agent_obs = collect_graph_inputs(Network, Routing, EVAL_SEEDS, n, a, B, L + 1, 200)
+    rng = np.random.RandomState(5)
+    torch.manual_seed(3)
+    netmon = NetMon(node_obs.shape[-1], 32, [64, 48], 1, F.leaky_relu, rnn_type="lstm",
+                    rnn_carryover=True, agg_type="sum", output_neighbor_hidden=True)
+    obs_dim = agent_obs.shape[-1] + netmon.get_out_features()
+    model = DQN(obs_dim, [64, 32], 4, F.leaky_relu)
+    model_tar = copy.deepcopy(model)
+    # perturb target so that it differs from the online model
+    with torch.no_grad():
+        for p in model_tar.parameters():
+            p.add_(0.01 * torch.randn_like(p))
+    sd_to_npz("netmon_", netmon.state_dict(), d)
+    sd_to_npz("model_", model.state_dict(), d)
+    sd_to_npz("target_", model_tar.state_dict(), d)
+    node_state0 = (0.1 * rng.standard_normal((B, n, netmon.get_state_size()))).astype(np.float32)
+    actions = rng.randint(4, size=(L, B, a))
+    reward = rng.choice(np.array([0.0, -0.2, 10.0, -10.0, 9.8], dtype=np.float32), size=(L, B, a)).astype(np.float32)
+    done = rng.rand(L, B, a) < 0.1
+    episode_done = rng.rand(L, B) < 0.3
+    d.update(node_obs=node_obs, node_adj=node_adj, node_agent=node_agent, agent_obs=agent_obs,
+             node_state0=node_state0, actions=actions, reward=reward, done=done.astype(np.int8),
+             episode_done=episode_done.astype(np.int8))
+    gamma, lr, tau = 0.9, 1e-3, 0.01
+    d["gamma"], d["lr"], d["tau"] = np.float64(gamma), np.float64(lr), np.float64(tau)
+    parameters = list(model.parameters()) + list(netmon.parameters())
+    optimizer = optim.AdamW(parameters, lr=lr)
+    netmon.train()
+    model.train()
+    loss_q = torch.zeros(1)
+    for t in range(L):
+        obs = np.concatenate([agent_obs[t], np.zeros((B, a, netmon.get_out_features()), np.float32)], -1)
+        next_obs = np.concatenate([agent_obs[t + 1], np.zeros((B, a, netmon.get_out_features()), np.float32)], -1)
+        obs = torch.tensor(obs)
+        next_obs = torch.tensor(next_obs)
+        if t == 0:
+            netmon.state = torch.tensor(node_state0)
+        else:
+            netmon.state = last_netmon_state * (~last_ep_done).view(-1, 1, 1)  # noqa: F821
+        network_obs = netmon(torch.tensor(node_obs[t]), torch.tensor(node_adj[t]), torch.tensor(node_agent[t]))
+        obs[:, :, -network_obs.shape[-1]:] = network_obs
+        last_netmon_state = netmon.state
+        last_ep_done = torch.tensor(episode_done[t])
+        q_values = model(obs, None)
+        with torch.no_grad():
+            nno = netmon(torch.tensor(node_obs[t + 1]), torch.tensor(node_adj[t + 1]), torch.tensor(node_agent[t + 1]))
+            next_obs[:, :, -nno.shape[-1]:] = nno
+            next_q = model_tar(next_obs, None)
+            next_q_max = next_q.max(dim=2)[0]
+        tgt = torch.tensor(reward[t]) + (~torch.tensor(done[t])) * gamma * next_q_max
+        q_target = torch.scatter(q_values.detach(), -1, torch.tensor(actions[t]).unsqueeze(-1), tgt.unsqueeze(-1))
+        loss_q = loss_q + torch.mean((q_values - q_target).pow(2)) / L
+        d[f"q_{t}"] = q_values.detach().numpy()
+        d[f"qtarget_{t}"] = q_target.numpy()
+    optimizer.zero_grad()
+    loss_q.backward()
+    d["loss"] = loss_q.detach().numpy()
+    names = [f"model_{k}" for k, _ in model.named_parameters()] + [f"netmon_{k}" for k, _ in netmon.named_parameters()]
+    for nm_, p in zip(names, parameters):
+        d["grad_raw_" + nm_] = p.grad.detach().numpy().copy()
+    torch.nn.utils.clip_grad_value_(parameters, 0.5)
+    torch.nn.utils.clip_grad_norm_(parameters, 1.0)
+    for nm_, p in zip(names, parameters):
+        d["grad_clip_" + nm_] = p.grad.detach().numpy().copy()
+    optimizer.step()
+    for nm_, p in zip(names, parameters):
+        d["param_after_" + nm_] = p.detach().numpy().copy()
+    interpolate_model(model, model_tar, tau, model_tar)
+    sd_to_npz("target_after_", model_tar.state_dict(), d)
+    d["param_names"] = np.array(names)
+    np.savez_compressed(out, **d)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--ref", default="/root/reference/src")
+    ap.add_argument("--only", default="")
+    args = ap.parse_args()
+    stub_dir = tempfile.mkdtemp(prefix="gm_ref_stubs_")
+    write_stubs(stub_dir)
+    sys.path[:0] = [stub_dir, args.ref]
+
+    from env.network import Network  # noqa: E402
+    from env.routing import Routing  # noqa: E402
+    from env.constants import EVAL_SEEDS  # noqa: E402
+    from model import NetMon, DQN  # noqa: E402
+    from util import interpolate_model  # noqa: E402
+
+    only = set(args.only.split(",")) if args.only else None
+    if only is None or "seeds" in only:
+        np.save(os.path.join(HERE, "eval_seeds.npy"), np.array(EVAL_SEEDS, dtype=np.int64))
+    if only is None or "rng" in only:
+        gen_rng(os.path.join(HERE, "rng.npz"))
+    if only is None or "topology" in only:
+        gen_topology(os.path.join(HERE, "topology.npz"), Network, EVAL_SEEDS)
+    if only is None or "env" in only:
+        gen_env(HERE, Network, Routing, EVAL_SEEDS)
+    if only is None or "netmon" in only:
+        gen_netmon(os.path.join(HERE, "netmon.npz"), Network, Routing, EVAL_SEEDS, NetMon, DQN)
+    if only is None or "train" in only:
+        gen_train(os.path.join(HERE, "train.npz"), Network, Routing, EVAL_SEEDS, NetMon, DQN, interpolate_model)
+
+
+if __name__ == "__main__":
+    main()
