@@ -1,0 +1,112 @@
+"""ctypes binding of libgraphmarl_amd.so (the C ABI in include/graph_marl_amd.h).
+
+torch is imported first so that the library binds to the HIP runtime torch already
+loaded (same libamdhip64.so.7 soname) and torch streams/tensors are usable as
+plain hipStream_t / device pointers. There is no CPU fallback: if the library is
+missing or no GPU is present the product path raises.
+"""
+import ctypes as C
+import os
+
+import torch  # noqa: F401  (must precede the HIP library load)
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "lib", "libgraphmarl_amd.so")
+
+GM_OK = 0
+GM_INFO_FIELDS = 9
+INFO_KEYS = ["looped", "throughput", "dropped", "blocked", "n_delays", "sum_delays", "n_arrived",
+             "sum_delays_arrived", "sum_spr"]
+TOPO_FIXED, TOPO_RANDOM, TOPO_LIST, TOPO_SEQUENTIAL = 0, 1, 2, 3
+
+# every symbol the header declares (checked by tests/test_capi.py)
+EXPORTS = [
+    "gm_last_error", "gm_version", "gm_env_create", "gm_env_destroy", "gm_env_dims", "gm_env_reset",
+    "gm_env_step", "gm_env_observe", "gm_env_topology", "gm_env_final_info", "gm_policy_egreedy",
+    "gm_env_get_state", "gm_build_seed_list", "gm_mp_aggregate", "gm_mp_aggregate_bwd", "gm_netmon_readout",
+    "gm_netmon_readout_bwd", "gm_lstm_pointwise", "gm_lstm_pointwise_bwd", "gm_linear_f32",
+]
+
+
+class EnvConfig(C.Structure):
+    _fields_ = [
+        ("n_env", C.c_int32), ("n_nodes", C.c_int32), ("n_data", C.c_int32), ("env_var", C.c_int32),
+        ("congestion", C.c_int32), ("action_mask", C.c_int32), ("ttl", C.c_int32), ("topo_mode", C.c_int32),
+        ("topo_seed", C.c_int64), ("seed_list", C.POINTER(C.c_int64)), ("n_seed_list", C.c_int32),
+        ("excluded", C.POINTER(C.c_int64)), ("n_excluded", C.c_int32), ("device", C.c_int32),
+    ]
+
+
+class ObsBuffers(C.Structure):
+    _fields_ = [("obs", C.c_void_p), ("obs_row_stride", C.c_int64), ("node_obs", C.c_void_p),
+                ("agent_node", C.c_void_p), ("agent_adj", C.c_void_p)]
+
+
+class StepDetail(C.Structure):
+    _fields_ = [("done_steps", C.c_void_p), ("done_opt", C.c_void_p), ("success", C.c_void_p)]
+
+
+class EnvState(C.Structure):
+    _fields_ = [(k, C.c_void_p) for k in [
+        "now", "target", "edge", "time", "ttl", "start", "spw", "agent_steps", "size", "visited", "amask",
+        "loads", "topo_seed", "topo_reps", "edge_a", "edge_b", "edge_len", "nbr_edge", "apsp", "rng_key",
+        "rng_pos"]]
+
+
+class GMError(RuntimeError):
+    pass
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise GMError(f"{LIB_PATH} not built: run `make -C graph-marl_amd/csrc` (or __graft_entry__.build())")
+    L = C.CDLL(LIB_PATH)
+    vp, i32, i64 = C.c_void_p, C.c_int32, C.c_int64
+    L.gm_last_error.restype = C.c_char_p
+    L.gm_env_create.argtypes = [C.POINTER(EnvConfig), vp, C.POINTER(vp)]
+    L.gm_env_destroy.argtypes = [vp]
+    L.gm_env_dims.argtypes = [vp] + [C.POINTER(i32)] * 5
+    L.gm_env_reset.argtypes = [vp, vp, C.POINTER(ObsBuffers), vp]
+    L.gm_env_step.argtypes = [vp, vp, vp, vp, vp, C.POINTER(StepDetail), C.POINTER(ObsBuffers), vp]
+    L.gm_env_observe.argtypes = [vp, C.POINTER(ObsBuffers), vp]
+    L.gm_env_topology.argtypes = [vp, vp, vp, vp, vp, vp]
+    L.gm_env_final_info.argtypes = [vp, vp, vp]
+    L.gm_policy_egreedy.argtypes = [vp, vp, C.c_double, vp, vp]
+    L.gm_env_get_state.argtypes = [vp, C.POINTER(EnvState)]
+    L.gm_build_seed_list.argtypes = [i32, i64, i32, vp, i32, i32, vp]
+    L.gm_mp_aggregate.argtypes = [vp, vp, i32, i32, i32, i32, i32, vp, vp]
+    L.gm_mp_aggregate_bwd.argtypes = [vp, vp, i32, i32, i32, i32, i32, vp, vp]
+    L.gm_netmon_readout.argtypes = [vp, vp, vp, vp, i32, i32, i32, i32, i32, vp, i64, vp]
+    L.gm_netmon_readout_bwd.argtypes = [vp, i64, vp, vp, i32, i32, i32, i32, i32, vp, vp, vp]
+    L.gm_lstm_pointwise.argtypes = [vp, vp, i32, i32, vp, vp, vp, vp]
+    L.gm_lstm_pointwise_bwd.argtypes = [vp, vp, vp, vp, vp, i32, i32, vp, vp, vp]
+    L.gm_linear_f32.argtypes = [vp, i64, vp, i64, vp, i32, i32, i32, i32, vp, i64, vp]
+    _lib = L
+    return L
+
+
+def check(rc):
+    if rc != GM_OK:
+        raise GMError(f"graph_marl_amd error {rc}: {lib().gm_last_error().decode()}")
+
+
+def ptr(t):
+    """Device pointer of a tensor (None -> NULL)."""
+    if t is None:
+        return None
+    return C.c_void_p(t.data_ptr())
+
+
+def stream_ptr(device=None):
+    return C.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+def require_gpu():
+    if not torch.cuda.is_available():
+        raise GMError("graph-marl_amd needs a ROCm GPU (torch.cuda.is_available() is False); there is no CPU path")

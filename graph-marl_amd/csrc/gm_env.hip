@@ -1,0 +1,1117 @@
+// gm_env.hip — batched routing environment (reference src/env/routing.py,
+// src/env/network.py) as HIP kernels for gfx950, plus its C ABI.
+//
+// Layout in HBM (library-owned, SoA per field, env-major):
+//   packets  int32 [n_env][A] now/target/edge/time/ttl/start/spw/steps,
+//            f64 size[n_env][A], u64 visited[n_env][A][2], u8 amask[n_env][A][4]
+//   loads    f64 [n_env][E]            (E = 3N/2)
+//   topology int32 nbr/nbr_edge [n_env][N][3] (ascending neighbour id),
+//            int32 edge_a/edge_b/edge_len [n_env][E], int16 apsp [n_env][N][N]
+//   rng      u32 [n_env][2][624] + cur/pos/has_next (numpy legacy MT19937 ring)
+// One 64-lane wavefront per env: lane a owns packet a, lane e owns edge e (and
+// e+64), so the order-dependent fp64 load updates are exact per-edge scans in
+// packet-id order and every RNG draw happens in reference order.
+//
+// Compiled with -ffp-contract=off: the env is bit-exact against the reference.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/graph_marl_amd.h"
+#include "gm_device.hpp"
+
+using namespace gm;
+
+namespace {
+thread_local std::string g_err;
+}
+
+extern "C" const char* gm_last_error(void) { return g_err.c_str(); }
+extern "C" int gm_version(void) { return 1; }
+
+int gm_fail(int code, const std::string& msg) {
+    g_err = msg;
+    return code;
+}
+
+#define GM_HIP(call)                                                                         \
+    do {                                                                                     \
+        hipError_t e_ = (call);                                                              \
+        if (e_ != hipSuccess)                                                                \
+            return gm_fail(GM_ERR_HIP, std::string(#call) + ": " + hipGetErrorString(e_)); \
+    } while (0)
+
+struct EnvDev {
+    int n_env, N, A, E;
+    int cong, amask_on, ttl, topo_mode, n_list, n_excl;
+    int64_t fixed_seed;
+    const int64_t* list;
+    const int64_t* excl;
+    int32_t *nbr, *nbr_edge, *edge_a, *edge_b, *edge_len;
+    int16_t* apsp;
+    int64_t* topo_seed;
+    int32_t *topo_reps, *topo_ready, *seq_index;
+    int32_t *now, *target, *edge, *time, *ttl_, *start, *spw, *steps;
+    double* size;
+    uint64_t* visited;
+    uint8_t* amask;
+    double* load;
+    uint32_t* mt;
+    int32_t *mt_cur, *mt_pos, *mt_has_next;
+    int32_t* err;
+};
+
+struct gm_env {
+    gm_env_config cfg;
+    std::vector<int64_t> list, excl;
+    EnvDev d;
+    std::vector<void*> allocs;
+    int device;
+};
+
+namespace {
+
+// ---------------------------------------------------------------------------
+// Shared per-block LDS image of one env
+// ---------------------------------------------------------------------------
+struct EnvLds {
+    int32_t now[MAX_AGENTS], target[MAX_AGENTS], edge[MAX_AGENTS], time[MAX_AGENTS];
+    double size[MAX_AGENTS];
+    double load[MAX_EDGES];
+    uint8_t nbr[MAX_NODES * 3], nbr_edge[MAX_NODES * 3];
+    uint8_t ea[MAX_EDGES], eb[MAX_EDGES], elen[MAX_EDGES];
+    uint64_t nbrmask[MAX_NODES];
+    float node_cnt[MAX_NODES], node_load[MAX_NODES];
+    uint32_t rbuf[RNG_BUF];
+    uint32_t rtmp[MT_N];
+};
+
+__device__ void load_topology_lds(const EnvDev& d, int env, EnvLds& s) {
+    const int l = lane_id();
+    const int N = d.N, E = d.E;
+    for (int i = l; i < N * 3; i += WAVE) {
+        s.nbr[i] = (uint8_t)d.nbr[(size_t)env * N * 3 + i];
+        s.nbr_edge[i] = (uint8_t)d.nbr_edge[(size_t)env * N * 3 + i];
+    }
+    for (int e = l; e < E; e += WAVE) {
+        s.ea[e] = (uint8_t)d.edge_a[(size_t)env * E + e];
+        s.eb[e] = (uint8_t)d.edge_b[(size_t)env * E + e];
+        s.elen[e] = (uint8_t)d.edge_len[(size_t)env * E + e];
+    }
+    __syncthreads();
+    if (l < N) {
+        uint64_t m = 0;
+        for (int k = 0; k < 3; k++) m |= 1ull << s.nbr[l * 3 + k];
+        s.nbrmask[l] = m;
+    }
+    __syncthreads();
+}
+
+__device__ __forceinline__ MainRng open_rng(const EnvDev& d, int env, EnvLds& s) {
+    MainRng r;
+    r.g = d.mt + (size_t)env * 2 * MT_N;
+    r.buf = s.rbuf;
+    r.tmp = s.rtmp;
+    r.cur = d.mt_cur[env];
+    r.pos = d.mt_pos[env];
+    r.has_next = d.mt_has_next[env];
+    r.n = 0;
+    r.k = 0;
+    return r;
+}
+
+__device__ __forceinline__ void close_rng(const EnvDev& d, int env, MainRng& r) {
+    r.commit();
+    if (lane_id() == 0) {
+        d.mt_cur[env] = r.cur;
+        d.mt_pos[env] = r.pos;
+        d.mt_has_next[env] = r.has_next;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Observation emission (routing.py:187-358, 522-539), packet state in LDS.
+// ---------------------------------------------------------------------------
+__device__ void emit_obs(const EnvDev& d, int env, EnvLds& s, const gm_obs_buffers& o) {
+    const int l = lane_id();
+    const int N = d.N, A = d.A;
+    if (o.node_obs) {
+        // packets waiting at node j (not on an edge) and the sum of their sizes in id order
+        if (l < N) {
+            int cnt = 0;
+            double tl = 0.0;
+            for (int i = 0; i < A; i++) {
+                if (s.now[i] == l && s.edge[i] == -1) {
+                    cnt++;
+                    tl += s.size[i];
+                }
+            }
+            s.node_cnt[l] = (float)cnt;
+            s.node_load[l] = (float)tl;
+        }
+        __syncthreads();
+        const int ND = 4 * N + 8;
+        float* base = o.node_obs + (size_t)env * N * ND;
+        for (int j = 0; j < N; j++) {
+            for (int c = l; c < ND; c += WAVE) {
+                float v;
+                if (c < N) v = (float)(c == j);
+                else if (c == N) v = s.node_cnt[j];
+                else if (c == N + 1) v = s.node_load[j];
+                else {
+                    int r = c - (N + 2), k = r / (N + 2), q = r - k * (N + 2);
+                    if (q < N) v = (float)(s.nbr[j * 3 + k] == q);
+                    else if (q == N) v = (float)s.elen[s.nbr_edge[j * 3 + k]];
+                    else v = (float)s.load[s.nbr_edge[j * 3 + k]];
+                }
+                base[(size_t)j * ND + c] = v;
+            }
+        }
+    }
+    if (o.obs) {
+        const int D = 6 * N + 10;
+        float* base = o.obs + (size_t)env * A * o.obs_row_stride;
+        for (int a = 0; a < A; a++) {
+            const int now = s.now[a], e = s.edge[a];
+            const int other = e >= 0 ? (s.ea[e] ^ s.eb[e] ^ now) : -1;
+            for (int c = l; c < D; c += WAVE) {
+                float v;
+                if (c < N) v = (float)(c == now);
+                else if (c < 2 * N) v = (float)(c - N == s.target[a]);
+                else if (c == 2 * N) v = (float)(e != -1);
+                else if (c < 3 * N + 1) v = (float)(c - (2 * N + 1) == other);
+                else if (c == 3 * N + 1) v = (float)s.time[a];
+                else if (c == 3 * N + 2) v = (float)s.size[a];
+                else if (c == 3 * N + 3) v = (float)a;
+                else {
+                    int r = c - (3 * N + 4), k = r / (N + 2), q = r - k * (N + 2);
+                    if (q < N) v = (float)(s.nbr[now * 3 + k] == q);
+                    else if (q == N) v = (float)s.elen[s.nbr_edge[now * 3 + k]];
+                    else v = (float)s.load[s.nbr_edge[now * 3 + k]];
+                }
+                base[(size_t)a * o.obs_row_stride + c] = v;
+            }
+        }
+    }
+    if (o.agent_node && l < A) o.agent_node[(size_t)env * A + l] = s.now[l];
+    if (o.agent_adj) {
+        int8_t* base = o.agent_adj + (size_t)env * A * A;
+        for (int idx = l; idx < A * A; idx += WAVE) {
+            int i = idx / A, j = idx - i * A;
+            int ni = s.now[i], nj = s.now[j];
+            base[idx] = (int8_t)(i == j || ni == nj || ((s.nbrmask[ni] >> nj) & 1ull));
+        }
+    }
+}
+
+__device__ void load_packets_lds(const EnvDev& d, int env, EnvLds& s) {
+    const int l = lane_id();
+    if (l < d.A) {
+        size_t p = (size_t)env * d.A + l;
+        s.now[l] = d.now[p];
+        s.target[l] = d.target[p];
+        s.edge[l] = d.edge[p];
+        s.time[l] = d.time[p];
+        s.size[l] = d.size[p];
+    }
+    for (int e = l; e < d.E; e += WAVE) s.load[e] = d.load[(size_t)env * d.E + e];
+    __syncthreads();
+}
+
+// ---------------------------------------------------------------------------
+// Topology generation (network.py:122-272), one wave per env, state in LDS.
+// ---------------------------------------------------------------------------
+struct TopoLds {
+    double x[MAX_NODES], y[MAX_NODES], d2[MAX_NODES];
+    uint32_t tkey[MT_N];
+    int32_t deg[MAX_NODES];
+    uint64_t adj[MAX_NODES];
+    int32_t node_edges[MAX_NODES * 3];
+    int32_t ea[MAX_EDGES], eb[MAX_EDGES], elen[MAX_EDGES];
+    int32_t n_edges;
+    int32_t cand_at_rank[MAX_NODES];
+    uint8_t ok_at_rank[MAX_NODES];
+    int16_t dist[MAX_NODES * MAX_NODES];
+};
+
+__device__ __forceinline__ bool is_excluded(const EnvDev& d, int64_t sd) {
+    int lo = 0, hi = d.n_excl - 1;
+    while (lo <= hi) {
+        int m = (lo + hi) >> 1;
+        int64_t v = d.excl[m];
+        if (v == sd) return true;
+        if (v < sd) lo = m + 1;
+        else hi = m - 1;
+    }
+    return false;
+}
+
+template <class R>
+__device__ int64_t draw_topology_seed(const EnvDev& d, R& r) {  // network.py:230-232, 252-254
+    int64_t sd = r.randint(2147483647LL);
+    while (d.n_excl > 0 && is_excluded(d, sd)) sd = r.randint(2147483647LL);
+    return sd;
+}
+
+// One _create_random_topology attempt from the LDS stream t.tkey (fresh after seeding).
+__device__ bool topology_attempt(const EnvDev& d, TopoLds& t, LocalRng& tr) {
+    const int l = lane_id();
+    const int N = d.N;
+    // positions: node i draws x then y (network.py:134-138) = tempered words 4i..4i+3
+    if (tr.pos == MT_N) {
+        mt_twist_lds(tr.key);
+        tr.pos = 0;
+    }
+    if (l < N) {
+        uint32_t w0 = mt_temper(tr.key[tr.pos + 4 * l]), w1 = mt_temper(tr.key[tr.pos + 4 * l + 1]);
+        uint32_t w2 = mt_temper(tr.key[tr.pos + 4 * l + 2]), w3 = mt_temper(tr.key[tr.pos + 4 * l + 3]);
+        t.x[l] = ((int32_t)(w0 >> 5) * 67108864.0 + (int32_t)(w1 >> 6)) / 9007199254740992.0;
+        t.y[l] = ((int32_t)(w2 >> 5) * 67108864.0 + (int32_t)(w3 >> 6)) / 9007199254740992.0;
+        t.deg[l] = 0;
+        t.adj[l] = 0;
+    }
+    tr.pos += 4 * N;
+    if (l == 0) t.n_edges = 0;
+    __syncthreads();
+    for (int i = 0; i < N; i++) {
+        // squared distances of row i (network.py:143-150) and stable ranks (153)
+        double my = 0.0;
+        if (l < N) {
+            double dx = t.x[l] - t.x[i], dy = t.y[l] - t.y[i];
+            double a = dx * dx, b = dy * dy;
+            my = a + b;
+            t.d2[l] = my;
+        }
+        __syncthreads();
+        int rank = 0;
+        if (l < N) {
+            for (int k = 0; k < N; k++) {
+                double dk = t.d2[k];
+                rank += (dk < my) || (dk == my && k < l);
+            }
+        }
+        const int need = 3 - t.deg[i];
+        if (need > 0) {
+            // candidate at sorted position r >= 1 is taken iff its degree < 3 and it is
+            // not already linked to i (network.py:157-170), first `need` in rank order
+            if (l < N) {
+                bool ok = rank >= 1 && t.deg[l] < 3 && !((t.adj[l] >> i) & 1ull);
+                t.ok_at_rank[rank] = (uint8_t)ok;
+                t.cand_at_rank[rank] = l;
+            }
+            __syncthreads();
+            uint64_t okm = ballot(l < N && t.ok_at_rank[l]);
+            int take = 0;
+            while (okm && take < need) {
+                int r = __builtin_ctzll(okm);
+                okm &= okm - 1;
+                take++;
+                int c = t.cand_at_rank[r];
+                double dc = t.d2[c];
+                double sq = sqrt(dc);
+                double s10 = sq * 10.0;
+                int32_t len = ((int32_t)s10) / 2 + 1;  // network.py:173
+                if (l == 0) {
+                    int e = t.n_edges;
+                    t.ea[e] = i < c ? i : c;
+                    t.eb[e] = i < c ? c : i;
+                    t.elen[e] = len;
+                    t.node_edges[c * 3 + t.deg[c]] = e;  // candidate first (180-181)
+                    t.deg[c] += 1;
+                    t.node_edges[i * 3 + t.deg[i]] = e;
+                    t.deg[i] += 1;
+                    t.adj[c] |= 1ull << i;
+                    t.adj[i] |= 1ull << c;
+                    t.n_edges = e + 1;
+                }
+                __syncthreads();
+            }
+        }
+        __syncthreads();
+    }
+    // validity (network.py:197-213): all degrees 3 and connected
+    bool deg_ok = !(ballot(l < N && t.deg[l] != 3));
+    if (!deg_ok) return false;
+    uint64_t full = N == 64 ? ~0ull : ((1ull << N) - 1);
+    uint64_t reach = 1ull, prev = 0;
+    uint64_t myadj = l < N ? t.adj[l] : 0ull;
+    while (reach != prev) {
+        prev = reach;
+        uint64_t contrib = ((reach >> l) & 1ull) ? myadj : 0ull;
+        reach |= wave_or_u64(contrib);
+    }
+    return reach == full;
+}
+
+__device__ void topology_finish(const EnvDev& d, int env, TopoLds& t, int64_t seed, int reps) {
+    const int l = lane_id();
+    const int N = d.N, E = d.E;
+    // per-node edges sorted by neighbour id (network.py:191-195)
+    if (l < N) {
+        int ee[3], nb[3];
+        for (int k = 0; k < 3; k++) {
+            ee[k] = t.node_edges[l * 3 + k];
+            nb[k] = t.ea[ee[k]] ^ t.eb[ee[k]] ^ l;
+        }
+        for (int a = 1; a < 3; a++)
+            for (int b = a; b > 0 && nb[b - 1] > nb[b]; b--) {
+                int tn = nb[b]; nb[b] = nb[b - 1]; nb[b - 1] = tn;
+                int te = ee[b]; ee[b] = ee[b - 1]; ee[b - 1] = te;
+            }
+        for (int k = 0; k < 3; k++) {
+            d.nbr[((size_t)env * N + l) * 3 + k] = nb[k];
+            d.nbr_edge[((size_t)env * N + l) * 3 + k] = ee[k];
+        }
+    }
+    for (int e = l; e < E; e += WAVE) {
+        d.edge_a[(size_t)env * E + e] = t.ea[e];
+        d.edge_b[(size_t)env * E + e] = t.eb[e];
+        d.edge_len[(size_t)env * E + e] = t.elen[e];
+    }
+    // all-pairs shortest path weights (network.py:274-290) by Floyd-Warshall
+    const int16_t INF = 0x3fff;
+    for (int idx = l; idx < N * N; idx += WAVE) t.dist[idx] = (idx / N == idx % N) ? 0 : INF;
+    __syncthreads();
+    if (l < E) {
+        int a = t.ea[l], b = t.eb[l];
+        t.dist[a * N + b] = (int16_t)t.elen[l];
+        t.dist[b * N + a] = (int16_t)t.elen[l];
+    }
+    if (E > WAVE && l + WAVE < E) {
+        int e = l + WAVE, a = t.ea[e], b = t.eb[e];
+        t.dist[a * N + b] = (int16_t)t.elen[e];
+        t.dist[b * N + a] = (int16_t)t.elen[e];
+    }
+    __syncthreads();
+    for (int k = 0; k < N; k++) {
+        for (int idx = l; idx < N * N; idx += WAVE) {
+            int i = idx / N, j = idx - i * N;
+            int v = t.dist[i * N + k] + t.dist[k * N + j];
+            if (v < t.dist[idx]) t.dist[idx] = (int16_t)v;
+        }
+        __syncthreads();
+    }
+    for (int idx = l; idx < N * N; idx += WAVE) d.apsp[(size_t)env * N * N + idx] = t.dist[idx];
+    if (l == 0) {
+        d.topo_seed[env] = seed;
+        d.topo_reps[env] = reps;
+        d.topo_ready[env] = 1;
+    }
+}
+
+// network.py:242-258: fresh stream per topology seed, reseed on invalid topology
+__device__ void generate_topology(const EnvDev& d, int env, TopoLds& t, int64_t seed, bool allow_retry) {
+    LocalRng tr;
+    tr.key = t.tkey;
+    tr.seed((uint32_t)seed);
+    int reps = 0;
+    for (;;) {
+        bool ok = topology_attempt(d, t, tr);
+        reps++;
+        if (ok) break;
+        if (!allow_retry || reps > 100000) {
+            if (lane_id() == 0) atomicExch(d.err, GM_ERR_TOPOLOGY);
+            break;
+        }
+        seed = draw_topology_seed(d, tr);
+        tr.seed((uint32_t)seed);
+    }
+    __syncthreads();
+    topology_finish(d, env, t, seed, reps);
+    __syncthreads();
+}
+
+struct ResetLds {
+    EnvLds env;
+    TopoLds topo;
+};
+
+// src/env/routing.py:160-178 (+ network.py:366-371): new topology (per mode), zero
+// loads, respawn every packet in id order (reset_packet, routing.py:119-144).
+__global__ __launch_bounds__(64) void k_env_reset(EnvDev d, const uint8_t* mask, gm_obs_buffers o) {
+    const int env = blockIdx.x;
+    if (mask && !mask[env]) return;
+    const int l = lane_id();
+    __shared__ ResetLds S;
+    EnvLds& s = S.env;
+    MainRng r = open_rng(d, env, s);
+    const int N = d.N, A = d.A;
+
+    int64_t seed = -1;
+    bool gen = true;
+    if (d.topo_mode == GM_TOPO_FIXED) {
+        gen = d.topo_ready[env] == 0;  // same topology every reset; no draw
+        seed = d.fixed_seed;
+    } else if (d.topo_mode == GM_TOPO_RANDOM) {
+        seed = draw_topology_seed(d, r);
+    } else if (d.topo_mode == GM_TOPO_LIST) {
+        seed = d.list[r.randint(d.n_list)];  // np.random.choice(seed_list)
+    } else {
+        int idx = 0;
+        if (d.n_list > 1) {
+            idx = d.seq_index[env];
+            __syncthreads();
+            if (l == 0) d.seq_index[env] = (idx + 1) % d.n_list;
+        }
+        seed = d.list[idx];
+    }
+    if (gen) generate_topology(d, env, S.topo, seed, d.topo_mode == GM_TOPO_RANDOM);
+    __syncthreads();
+
+    // packets
+    int p_now = 0, p_target = 0;
+    double p_size = 0.0;
+    for (int i = 0; i < A; i++) {
+        int st = (int)r.randint(N);
+        int tg = (int)r.randint(N);
+        double sz = r.random();
+        if (l == i) {
+            p_now = st;
+            p_target = tg;
+            p_size = sz;
+        }
+    }
+    close_rng(d, env, r);
+    if (l < A) {
+        size_t p = (size_t)env * A + l;
+        d.now[p] = p_now;
+        d.target[p] = p_target;
+        d.start[p] = p_now;
+        d.size[p] = p_size;
+        d.edge[p] = -1;
+        d.time[p] = 0;
+        d.ttl_[p] = d.ttl;
+        d.steps[p] = 0;
+        d.spw[p] = d.apsp[((size_t)env * N + p_now) * N + p_target];
+        d.visited[p * 2 + 0] = p_now < 64 ? (1ull << p_now) : 0ull;
+        d.visited[p * 2 + 1] = 0ull;
+        uint32_t m = d.amask_on ? (uint32_t)(p_now != p_target) : 0u;
+        reinterpret_cast<uint32_t*>(d.amask)[p] = m;
+        s.now[l] = p_now;
+        s.target[l] = p_target;
+        s.edge[l] = -1;
+        s.time[l] = 0;
+        s.size[l] = p_size;
+    }
+    for (int e = l; e < d.E; e += WAVE) {
+        d.load[(size_t)env * d.E + e] = 0.0;
+        s.load[e] = 0.0;
+    }
+    __syncthreads();
+    if (o.obs || o.node_obs || o.agent_node || o.agent_adj) {
+        load_topology_lds(d, env, s);
+        emit_obs(d, env, s, o);
+    }
+}
+
+struct StepOut {
+    float* reward;
+    uint8_t* done;
+    double* info;
+    gm_step_detail det;
+};
+
+// src/env/routing.py:360-520
+__global__ __launch_bounds__(64) void k_env_step(EnvDev d, const int32_t* act, StepOut out, gm_obs_buffers o) {
+    const int env = blockIdx.x;
+    const int l = lane_id();
+    const int N = d.N, A = d.A, E = d.E;
+    __shared__ EnvLds s;
+    load_topology_lds(d, env, s);
+
+    // packet a in lane a (registers)
+    const bool own = l < A;
+    const size_t p = (size_t)env * A + l;
+    int now = 0, target = 0, edge = -1, time = 0, ttl = 0, steps = 0, spw = 0, start = 0, a_t = 0;
+    double size = 0.0;
+    uint64_t vis = 0;
+    if (own) {
+        now = d.now[p]; target = d.target[p]; edge = d.edge[p]; time = d.time[p];
+        ttl = d.ttl_[p]; steps = d.steps[p]; spw = d.spw[p]; start = d.start[p];
+        size = d.size[p]; vis = d.visited[p * 2];
+        a_t = act[p];
+        if (a_t < 0 || a_t > 3) {  // the reference raises IndexError; flag and idle
+            atomicExch(d.err, GM_ERR_INVALID_ARG);
+            a_t = 0;
+        }
+    }
+    // edge e in lane e (and e+64)
+    double ld0 = l < E ? d.load[(size_t)env * E + l] : 0.0;
+    double ld1 = l + WAVE < E ? d.load[(size_t)env * E + l + WAVE] : 0.0;
+
+    steps += 1;  // routing.py:371
+    float reward = 0.0f;
+
+    // ---- phase 1 (routing.py:380-412): admission, lower packet id first ----
+    int chosen = -1;
+    if (own && edge == -1 && a_t != 0) chosen = s.nbr_edge[now * 3 + (a_t - 1)];
+    uint64_t admit = 0, block = 0;
+    for (int i = 0; i < A; i++) {
+        int c = readlane(chosen, i);
+        if (c < 0) continue;  // uniform
+        double si = readlane_f64(size, i);
+        if (c == l || c == l + WAVE) {
+            double ld = c == l ? ld0 : ld1;
+            if (d.cong && ld + si > 1.0) {
+                block |= 1ull << i;
+            } else {
+                ld = ld + si;
+                admit |= 1ull << i;
+                if (c == l) ld0 = ld; else ld1 = ld;
+            }
+        }
+    }
+    admit = wave_or_u64(admit);
+    block = wave_or_u64(block);
+    bool looped = false;
+    if (own) {
+        if ((block >> l) & 1ull) reward = reward - 0.2f;
+        if ((admit >> l) & 1ull) {
+            edge = chosen;
+            time = s.elen[chosen];
+            now = s.ea[chosen] ^ s.eb[chosen] ^ now;
+            if ((vis >> now) & 1ull) looped = true;
+            else vis |= 1ull << now;
+        }
+    }
+
+    // ---- phase 2 (routing.py:444-495) ----
+    int sub_edge = -1;
+    bool drop = false, fin = false, reached = false;
+    uint32_t am = 0;
+    if (own) {
+        am = reinterpret_cast<const uint32_t*>(d.amask)[p];
+        ttl -= 1;
+        if (edge != -1) {
+            time -= 1;
+            if (time <= 0) {
+                sub_edge = edge;
+                edge = -1;
+            }
+        }
+        drop = d.ttl > 0 && ttl <= 0;
+        if (d.amask_on) {
+            if (edge != -1) {
+                am = 0;
+            } else {
+                am = 1u;
+                int cnt = 1;
+                for (int k = 0; k < 3; k++) {
+                    uint32_t b = (uint32_t)((vis >> s.nbr[now * 3 + k]) & 1ull);
+                    am |= b << (8 * (k + 1));
+                    cnt += (int)b;
+                }
+                if (cnt == 4) drop = true;
+            }
+        }
+        reached = edge == -1 && now == target;
+        fin = reached || drop;
+        if (fin) {
+            reward = reward + (reached ? 10.0f : -10.0f);
+            if (edge != -1) sub_edge = edge;  // reset_packet frees its edge (125-127)
+        }
+    }
+    // loads: per-edge subtraction in packet order
+    for (int i = 0; i < A; i++) {
+        int c = readlane(sub_edge, i);
+        if (c < 0) continue;
+        double si = readlane_f64(size, i);
+        if (c == l) ld0 = ld0 - si;
+        else if (c == l + WAVE) ld1 = ld1 - si;
+    }
+    // statistics of finished packets (before respawn)
+    const int opt = spw > 1 ? spw : 1;
+    const int done_steps = fin ? steps : 0;
+    uint64_t finm = ballot(own && fin);
+    uint64_t succm = ballot(own && fin && reached);
+    uint64_t loopm = ballot(own && looped);
+    if (out.det.done_steps && own) out.det.done_steps[p] = done_steps;
+    if (out.det.done_opt && own) out.det.done_opt[p] = fin ? opt : 0;
+    if (out.det.success && own) out.det.success[p] = (uint8_t)(fin && reached);
+    if (out.info) {
+        int sd = wave_sum_i32(fin ? steps : 0);
+        int sda = wave_sum_i32(fin && reached ? steps : 0);
+        double spr_sum = 0.0;
+        for (int i = 0; i < A; i++) {  // in packet order, like the reference's list
+            if (!((succm >> i) & 1ull)) continue;
+            int st = readlane(steps, i), op = readlane(opt, i);
+            spr_sum += (double)st / (double)op;
+        }
+        if (l == 0) {
+            double* inf = out.info + (size_t)env * GM_INFO_FIELDS;
+            inf[GM_INFO_LOOPED] = (double)__popcll(loopm);
+            inf[GM_INFO_THROUGHPUT] = (double)__popcll(succm);
+            inf[GM_INFO_DROPPED] = (double)__popcll(finm & ~succm);
+            inf[GM_INFO_BLOCKED] = (double)__popcll(block);
+            inf[GM_INFO_N_DELAYS] = (double)__popcll(finm);
+            inf[GM_INFO_SUM_DELAYS] = (double)sd;
+            inf[GM_INFO_N_ARRIVED] = (double)__popcll(succm);
+            inf[GM_INFO_SUM_DELAYS_ARRIVED] = (double)sda;
+            inf[GM_INFO_SUM_SPR] = spr_sum;
+        }
+    }
+    if (own) {
+        out.reward[p] = reward;
+        out.done[p] = (uint8_t)fin;
+    }
+    // respawn finished packets in id order (reset_packet draws, routing.py:130-134)
+    if (finm) {
+        MainRng r = open_rng(d, env, s);
+        r.prefetch(6 * __popcll(finm) + 8);
+        uint64_t m = finm;
+        while (m) {
+            int i = __builtin_ctzll(m);
+            m &= m - 1;
+            int st = (int)r.randint(N);
+            int tg = (int)r.randint(N);
+            double sz = r.random();
+            if (l == i) {
+                now = st;
+                target = tg;
+                size = sz;
+                start = st;
+            }
+        }
+        close_rng(d, env, r);
+        if (own && fin) {
+            time = 0;
+            edge = -1;
+            ttl = d.ttl;
+            steps = 0;
+            spw = d.apsp[((size_t)env * N + now) * N + target];
+            vis = 1ull << now;
+            am = d.amask_on ? (uint32_t)(now != target) : 0u;
+        }
+    }
+    // write back
+    if (own) {
+        d.now[p] = now; d.target[p] = target; d.edge[p] = edge; d.time[p] = time;
+        d.ttl_[p] = ttl; d.steps[p] = steps; d.spw[p] = spw; d.start[p] = start;
+        d.size[p] = size; d.visited[p * 2] = vis;
+        reinterpret_cast<uint32_t*>(d.amask)[p] = am;
+        s.now[l] = now; s.target[l] = target; s.edge[l] = edge; s.time[l] = time; s.size[l] = size;
+    }
+    if (l < E) { d.load[(size_t)env * E + l] = ld0; s.load[l] = ld0; }
+    if (l + WAVE < E) { d.load[(size_t)env * E + l + WAVE] = ld1; s.load[l + WAVE] = ld1; }
+    __syncthreads();
+    if (o.obs || o.node_obs || o.agent_node || o.agent_adj) emit_obs(d, env, s, o);
+}
+
+__global__ __launch_bounds__(64) void k_env_observe(EnvDev d, gm_obs_buffers o) {
+    const int env = blockIdx.x;
+    __shared__ EnvLds s;
+    load_topology_lds(d, env, s);
+    load_packets_lds(d, env, s);
+    emit_obs(d, env, s, o);
+}
+
+// EpsilonGreedy.__call__ (src/policy.py:20-64): randint(4, size=A) then rand(A)
+// from the env's stream every call; argmax (first maximum) unless the draw < eps.
+__global__ __launch_bounds__(64) void k_policy_egreedy(EnvDev d, const float* q, double eps, int32_t* actions) {
+    const int env = blockIdx.x;
+    const int l = lane_id();
+    const int A = d.A;
+    __shared__ uint32_t rbuf[RNG_BUF];
+    __shared__ uint32_t rtmp[MT_N];
+    MainRng r;
+    r.g = d.mt + (size_t)env * 2 * MT_N;
+    r.buf = rbuf;
+    r.tmp = rtmp;
+    r.cur = d.mt_cur[env];
+    r.pos = d.mt_pos[env];
+    r.has_next = d.mt_has_next[env];
+    r.n = 0;
+    r.k = 0;
+    r.prefetch(3 * A);
+    if (l < A) {
+        size_t p = (size_t)env * A + l;
+        float4 qv = reinterpret_cast<const float4*>(q)[p];
+        float v[4] = {qv.x, qv.y, qv.z, qv.w};
+        if (d.amask_on) {
+            uint32_t m = reinterpret_cast<const uint32_t*>(d.amask)[p];
+            for (int k = 0; k < 4; k++)
+                if ((m >> (8 * k)) & 0xffu) v[k] = -__builtin_inff();
+        }
+        int best = 0;
+        for (int k = 1; k < 4; k++)
+            if (v[k] > v[best]) best = k;
+        int ra = (int)(rbuf[l] & 3u);
+        uint32_t w0 = rbuf[A + 2 * l], w1 = rbuf[A + 2 * l + 1];
+        double u = ((int32_t)(w0 >> 5) * 67108864.0 + (int32_t)(w1 >> 6)) / 9007199254740992.0;
+        actions[p] = u < eps ? ra : best;
+    }
+    r.k = 3 * A;
+    r.commit();
+    if (l == 0) {
+        d.mt_cur[env] = r.cur;
+        d.mt_pos[env] = r.pos;
+        d.mt_has_next[env] = r.has_next;
+    }
+}
+
+__global__ void k_rng_seed(EnvDev d, const uint32_t* seeds) {
+    int env = blockIdx.x * blockDim.x + threadIdx.x;
+    if (env >= d.n_env) return;
+    uint32_t* k = d.mt + (size_t)env * 2 * MT_N;
+    uint32_t v = seeds[env];
+    k[0] = v;
+    for (int i = 1; i < MT_N; i++) {
+        v = 1812433253u * (v ^ (v >> 30)) + (uint32_t)i;
+        k[i] = v;
+    }
+    d.mt_cur[env] = 0;
+    d.mt_pos[env] = MT_N;
+    d.mt_has_next[env] = 0;
+    d.seq_index[env] = 0;
+    d.topo_ready[env] = 0;
+}
+
+__global__ void k_topology_out(EnvDev d, int32_t* nbr, int8_t* node_adj, float* node_aux, int64_t* seeds) {
+    const int env = blockIdx.x;
+    const int l = threadIdx.x;
+    const int N = d.N;
+    if (nbr)
+        for (int i = l; i < N * 3; i += blockDim.x) nbr[(size_t)env * N * 3 + i] = d.nbr[(size_t)env * N * 3 + i];
+    if (node_adj) {
+        for (int idx = l; idx < N * N; idx += blockDim.x) {
+            int i = idx / N, j = idx % N;
+            const int32_t* nb = d.nbr + ((size_t)env * N + i) * 3;
+            node_adj[(size_t)env * N * N + idx] = (int8_t)(i == j || nb[0] == j || nb[1] == j || nb[2] == j);
+        }
+    }
+    if (node_aux)
+        for (int idx = l; idx < N * N; idx += blockDim.x)
+            node_aux[(size_t)env * N * N + idx] = (float)d.apsp[(size_t)env * N * N + idx];
+    if (seeds && l == 0) seeds[env] = d.topo_seed[env];
+}
+
+__global__ void k_final_info(EnvDev d, double* out) {
+    const int env = blockIdx.x * blockDim.x + threadIdx.x;
+    if (env >= d.n_env) return;
+    double s = 0.0, c = 0.0;
+    for (int a = 0; a < d.A; a++) {
+        int st = d.steps[(size_t)env * d.A + a];
+        if (st != 0) {
+            s += st;
+            c += 1.0;
+        }
+    }
+    out[env * 2] = s;
+    out[env * 2 + 1] = c;
+}
+
+// src/env/network.py:100-120 build_seed_list: main stream seeded with the init seed;
+// each candidate seed is a main-stream draw (exclusions re-drawn), its topology chain
+// (reseeding on invalid graphs) gives the final seed; unique seeds in order.
+__global__ __launch_bounds__(64) void k_build_seed_list(EnvDev d, int count, int64_t* out) {
+    __shared__ ResetLds S;
+    MainRng r = open_rng(d, 0, S.env);
+    int have = 0;
+    while (have < count) {
+        int64_t cand = draw_topology_seed(d, r);
+        r.commit();
+        LocalRng tr;
+        tr.key = S.topo.tkey;
+        tr.seed((uint32_t)cand);
+        int64_t seed = cand;
+        int reps = 0;
+        for (;;) {
+            bool ok = topology_attempt(d, S.topo, tr);
+            reps++;
+            if (ok || reps > 100000) break;
+            seed = draw_topology_seed(d, tr);
+            tr.seed((uint32_t)seed);
+        }
+        bool dup = false;
+        for (int i = 0; i < have; i++) dup |= out[i] == seed;
+        __syncthreads();
+        if (!dup) {
+            if (lane_id() == 0) out[have] = seed;
+            have++;
+        }
+        __syncthreads();
+    }
+    close_rng(d, 0, r);
+}
+
+bool has_obs(const gm_obs_buffers* o) {
+    return o && (o->obs || o->node_obs || o->agent_node || o->agent_adj);
+}
+
+int check_launch() {
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return gm_fail(GM_ERR_HIP, std::string("kernel launch: ") + hipGetErrorString(e));
+    return GM_OK;
+}
+
+template <class T>
+int dalloc(gm_env* env, T** p, size_t n) {
+    void* q = nullptr;
+    if (n == 0) n = 1;
+    hipError_t e = hipMalloc(&q, n * sizeof(T));
+    if (e != hipSuccess) return gm_fail(GM_ERR_OOM, std::string("hipMalloc: ") + hipGetErrorString(e));
+    env->allocs.push_back(q);
+    *p = (T*)q;
+    return GM_OK;
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------------------
+// C ABI
+// ---------------------------------------------------------------------------
+extern "C" int gm_env_destroy(gm_env* env) {
+    if (!env) return GM_OK;
+    (void)hipSetDevice(env->device);
+    for (void* p : env->allocs) (void)hipFree(p);
+    delete env;
+    return GM_OK;
+}
+
+extern "C" int gm_env_create(const gm_env_config* cfg, const uint32_t* env_seeds, gm_env** out) {
+    if (!cfg || !env_seeds || !out) return gm_fail(GM_ERR_INVALID_ARG, "null argument");
+    *out = nullptr;
+    const int N = cfg->n_nodes, A = cfg->n_data;
+    if (cfg->n_env <= 0) return gm_fail(GM_ERR_INVALID_ARG, "n_env must be > 0");
+    if (N < 4 || N > MAX_NODES || (N % 2) != 0)
+        return gm_fail(GM_ERR_INVALID_ARG, "n_nodes must be even and in [4, 64] (3-regular topology generator)");
+    if (A < 1 || A > MAX_AGENTS) return gm_fail(GM_ERR_INVALID_ARG, "n_data must be in [1, 64]");
+    if (cfg->env_var != 1) return gm_fail(GM_ERR_UNSUPPORTED, "only env_var=1 (INDEPENDENT) is implemented");
+    if ((cfg->topo_mode == GM_TOPO_LIST || cfg->topo_mode == GM_TOPO_SEQUENTIAL) &&
+        (cfg->n_seed_list <= 0 || !cfg->seed_list))
+        return gm_fail(GM_ERR_INVALID_ARG, "seed list required for LIST/SEQUENTIAL topology mode");
+    if (cfg->topo_mode < 0 || cfg->topo_mode > 3) return gm_fail(GM_ERR_INVALID_ARG, "bad topo_mode");
+    GM_HIP(hipSetDevice(cfg->device));
+    gm_env* env = new gm_env();
+    env->cfg = *cfg;
+    env->device = cfg->device;
+    if (cfg->seed_list) env->list.assign(cfg->seed_list, cfg->seed_list + cfg->n_seed_list);
+    if (cfg->excluded) {
+        env->excl.assign(cfg->excluded, cfg->excluded + cfg->n_excluded);
+        std::sort(env->excl.begin(), env->excl.end());
+    }
+    env->cfg.seed_list = nullptr;
+    env->cfg.excluded = nullptr;
+    EnvDev& d = env->d;
+    memset(&d, 0, sizeof(d));
+    const size_t B = (size_t)cfg->n_env;
+    d.n_env = cfg->n_env;
+    d.N = N;
+    d.A = A;
+    d.E = 3 * N / 2;
+    d.cong = cfg->congestion != 0;
+    d.amask_on = cfg->action_mask != 0;
+    d.ttl = cfg->ttl;
+    d.topo_mode = cfg->topo_mode;
+    d.fixed_seed = cfg->topo_seed;
+    d.n_list = (int)env->list.size();
+    d.n_excl = (int)env->excl.size();
+    int rc = GM_OK;
+#define ALLOC(ptr, n) \
+    if ((rc = dalloc(env, &(ptr), (n))) != GM_OK) { gm_env_destroy(env); return rc; }
+    int64_t *list_d = nullptr, *excl_d = nullptr;
+    ALLOC(list_d, env->list.size());
+    ALLOC(excl_d, env->excl.size());
+    d.list = list_d;
+    d.excl = excl_d;
+    ALLOC(d.nbr, B * N * 3);
+    ALLOC(d.nbr_edge, B * N * 3);
+    ALLOC(d.edge_a, B * d.E);
+    ALLOC(d.edge_b, B * d.E);
+    ALLOC(d.edge_len, B * d.E);
+    ALLOC(d.apsp, B * N * N);
+    ALLOC(d.topo_seed, B);
+    ALLOC(d.topo_reps, B);
+    ALLOC(d.topo_ready, B);
+    ALLOC(d.seq_index, B);
+    ALLOC(d.now, B * A);
+    ALLOC(d.target, B * A);
+    ALLOC(d.edge, B * A);
+    ALLOC(d.time, B * A);
+    ALLOC(d.ttl_, B * A);
+    ALLOC(d.start, B * A);
+    ALLOC(d.spw, B * A);
+    ALLOC(d.steps, B * A);
+    ALLOC(d.size, B * A);
+    ALLOC(d.visited, B * A * 2);
+    ALLOC(d.amask, B * A * 4);
+    ALLOC(d.load, B * d.E);
+    ALLOC(d.mt, B * 2 * MT_N);
+    ALLOC(d.mt_cur, B);
+    ALLOC(d.mt_pos, B);
+    ALLOC(d.mt_has_next, B);
+    ALLOC(d.err, 1);
+    uint32_t* seeds_d = nullptr;
+    ALLOC(seeds_d, B);
+#undef ALLOC
+    GM_HIP(hipMemcpy(seeds_d, env_seeds, B * sizeof(uint32_t), hipMemcpyHostToDevice));
+    if (!env->list.empty())
+        GM_HIP(hipMemcpy(list_d, env->list.data(), env->list.size() * sizeof(int64_t), hipMemcpyHostToDevice));
+    if (!env->excl.empty())
+        GM_HIP(hipMemcpy(excl_d, env->excl.data(), env->excl.size() * sizeof(int64_t), hipMemcpyHostToDevice));
+    GM_HIP(hipMemset(d.err, 0, sizeof(int32_t)));
+    GM_HIP(hipMemset(d.edge, 0xff, B * A * sizeof(int32_t)));
+    GM_HIP(hipMemset(d.load, 0, B * d.E * sizeof(double)));
+    GM_HIP(hipMemset(d.steps, 0, B * A * sizeof(int32_t)));
+    GM_HIP(hipMemset(d.amask, 0, B * A * 4));
+    hipLaunchKernelGGL(k_rng_seed, dim3((unsigned)((B + 63) / 64)), dim3(64), 0, 0, d, seeds_d);
+    if ((rc = check_launch()) != GM_OK) { gm_env_destroy(env); return rc; }
+    GM_HIP(hipDeviceSynchronize());
+    *out = env;
+    return GM_OK;
+}
+
+extern "C" int gm_env_dims(const gm_env* env, int32_t* n_env, int32_t* n_nodes, int32_t* n_data, int32_t* obs_dim,
+                           int32_t* node_obs_dim) {
+    if (!env) return gm_fail(GM_ERR_INVALID_ARG, "null env");
+    if (n_env) *n_env = env->d.n_env;
+    if (n_nodes) *n_nodes = env->d.N;
+    if (n_data) *n_data = env->d.A;
+    if (obs_dim) *obs_dim = 6 * env->d.N + 10;
+    if (node_obs_dim) *node_obs_dim = 4 * env->d.N + 8;
+    return GM_OK;
+}
+
+static int check_obs(const gm_env* env, const gm_obs_buffers* o) {
+    if (o && o->obs && o->obs_row_stride < 6 * env->d.N + 10)
+        return gm_fail(GM_ERR_INVALID_ARG, "obs_row_stride smaller than the observation size");
+    return GM_OK;
+}
+
+extern "C" int gm_env_reset(gm_env* env, const uint8_t* reset_mask, const gm_obs_buffers* obs, void* stream) {
+    if (!env) return gm_fail(GM_ERR_INVALID_ARG, "null env");
+    int rc = check_obs(env, obs);
+    if (rc) return rc;
+    gm_obs_buffers o = obs ? *obs : gm_obs_buffers{};
+    hipLaunchKernelGGL(k_env_reset, dim3(env->d.n_env), dim3(64), 0, (hipStream_t)stream, env->d, reset_mask, o);
+    return check_launch();
+}
+
+extern "C" int gm_env_step(gm_env* env, const int32_t* actions, float* reward, uint8_t* done, double* info,
+                           const gm_step_detail* detail, const gm_obs_buffers* obs, void* stream) {
+    if (!env || !actions || !reward || !done) return gm_fail(GM_ERR_INVALID_ARG, "null argument");
+    int rc = check_obs(env, obs);
+    if (rc) return rc;
+    StepOut so;
+    so.reward = reward;
+    so.done = done;
+    so.info = info;
+    so.det = detail ? *detail : gm_step_detail{};
+    gm_obs_buffers o = obs ? *obs : gm_obs_buffers{};
+    hipLaunchKernelGGL(k_env_step, dim3(env->d.n_env), dim3(64), 0, (hipStream_t)stream, env->d, actions, so, o);
+    return check_launch();
+}
+
+extern "C" int gm_env_observe(gm_env* env, const gm_obs_buffers* obs, void* stream) {
+    if (!env) return gm_fail(GM_ERR_INVALID_ARG, "null env");
+    if (!has_obs(obs)) return GM_OK;
+    int rc = check_obs(env, obs);
+    if (rc) return rc;
+    hipLaunchKernelGGL(k_env_observe, dim3(env->d.n_env), dim3(64), 0, (hipStream_t)stream, env->d, *obs);
+    return check_launch();
+}
+
+extern "C" int gm_env_topology(gm_env* env, int32_t* nbr, int8_t* node_adj, float* node_aux, int64_t* topo_seed,
+                               void* stream) {
+    if (!env) return gm_fail(GM_ERR_INVALID_ARG, "null env");
+    hipLaunchKernelGGL(k_topology_out, dim3(env->d.n_env), dim3(64), 0, (hipStream_t)stream, env->d, nbr, node_adj,
+                       node_aux, topo_seed);
+    return check_launch();
+}
+
+extern "C" int gm_env_final_info(gm_env* env, double* out, void* stream) {
+    if (!env || !out) return gm_fail(GM_ERR_INVALID_ARG, "null argument");
+    hipLaunchKernelGGL(k_final_info, dim3((env->d.n_env + 63) / 64), dim3(64), 0, (hipStream_t)stream, env->d, out);
+    return check_launch();
+}
+
+extern "C" int gm_policy_egreedy(gm_env* env, const float* q, double epsilon, int32_t* actions, void* stream) {
+    if (!env || !q || !actions) return gm_fail(GM_ERR_INVALID_ARG, "null argument");
+    if ((reinterpret_cast<uintptr_t>(q) & 15) != 0) return gm_fail(GM_ERR_INVALID_ARG, "q must be 16-byte aligned");
+    hipLaunchKernelGGL(k_policy_egreedy, dim3(env->d.n_env), dim3(64), 0, (hipStream_t)stream, env->d, q, epsilon,
+                       actions);
+    return check_launch();
+}
+
+extern "C" int gm_build_seed_list(int32_t n_nodes, int64_t init_seed, int32_t count, const int64_t* excluded,
+                                  int32_t n_excluded, int32_t device, int64_t* out) {
+    if (!out || count <= 0) return gm_fail(GM_ERR_INVALID_ARG, "gm_build_seed_list: bad arguments");
+    gm_env_config c;
+    memset(&c, 0, sizeof(c));
+    c.n_env = 1;
+    c.n_nodes = n_nodes;
+    c.n_data = 1;
+    c.env_var = 1;
+    c.topo_mode = GM_TOPO_RANDOM;
+    c.excluded = excluded;
+    c.n_excluded = n_excluded;
+    c.device = device;
+    uint32_t s0 = (uint32_t)init_seed;
+    gm_env* env = nullptr;
+    int rc = gm_env_create(&c, &s0, &env);
+    if (rc) return rc;
+    int64_t* dout = nullptr;
+    if ((rc = dalloc(env, &dout, (size_t)count)) != GM_OK) {
+        gm_env_destroy(env);
+        return rc;
+    }
+    hipLaunchKernelGGL(k_build_seed_list, dim3(1), dim3(64), 0, 0, env->d, count, dout);
+    rc = check_launch();
+    if (rc == GM_OK) {
+        hipError_t e = hipMemcpy(out, dout, (size_t)count * sizeof(int64_t), hipMemcpyDeviceToHost);
+        if (e != hipSuccess) rc = gm_fail(GM_ERR_HIP, std::string("gm_build_seed_list: ") + hipGetErrorString(e));
+    }
+    gm_env_destroy(env);
+    return rc;
+}
+
+template <class T>
+static int d2h(T* host, const T* dev, size_t n) {
+    if (!host) return GM_OK;
+    GM_HIP(hipMemcpy(host, dev, n * sizeof(T), hipMemcpyDeviceToHost));
+    return GM_OK;
+}
+
+extern "C" int gm_env_get_state(gm_env* env, gm_env_state* st) {
+    if (!env || !st) return gm_fail(GM_ERR_INVALID_ARG, "null argument");
+    GM_HIP(hipSetDevice(env->device));
+    GM_HIP(hipDeviceSynchronize());
+    int32_t err = 0;
+    GM_HIP(hipMemcpy(&err, env->d.err, sizeof(err), hipMemcpyDeviceToHost));
+    if (err) return gm_fail(err, "device reported an invalid topology seed / generator failure");
+    const EnvDev& d = env->d;
+    const size_t B = d.n_env, A = d.A, N = d.N, E = d.E;
+    int rc = 0;
+    if ((rc = d2h(st->now, d.now, B * A)) || (rc = d2h(st->target, d.target, B * A)) ||
+        (rc = d2h(st->edge, d.edge, B * A)) || (rc = d2h(st->time, d.time, B * A)) ||
+        (rc = d2h(st->ttl, d.ttl_, B * A)) || (rc = d2h(st->start, d.start, B * A)) ||
+        (rc = d2h(st->spw, d.spw, B * A)) || (rc = d2h(st->agent_steps, d.steps, B * A)) ||
+        (rc = d2h(st->size, d.size, B * A)) || (rc = d2h(st->visited, d.visited, B * A * 2)) ||
+        (rc = d2h(st->amask, d.amask, B * A * 4)) || (rc = d2h(st->loads, d.load, B * E)) ||
+        (rc = d2h(st->topo_seed, d.topo_seed, B)) || (rc = d2h(st->topo_reps, d.topo_reps, B)) ||
+        (rc = d2h(st->edge_a, d.edge_a, B * E)) || (rc = d2h(st->edge_b, d.edge_b, B * E)) ||
+        (rc = d2h(st->edge_len, d.edge_len, B * E)) || (rc = d2h(st->nbr_edge, d.nbr_edge, B * N * 3)))
+        return rc;
+    if (st->apsp) {
+        std::vector<int16_t> tmp(B * N * N);
+        GM_HIP(hipMemcpy(tmp.data(), d.apsp, tmp.size() * sizeof(int16_t), hipMemcpyDeviceToHost));
+        for (size_t i = 0; i < tmp.size(); i++) st->apsp[i] = tmp[i];
+    }
+    if (st->rng_key || st->rng_pos) {
+        // numpy's view of the stream: the block being consumed and the position in it
+        std::vector<uint32_t> mt(B * 2 * MT_N);
+        std::vector<int32_t> cur(B), pos(B);
+        GM_HIP(hipMemcpy(mt.data(), d.mt, mt.size() * sizeof(uint32_t), hipMemcpyDeviceToHost));
+        GM_HIP(hipMemcpy(cur.data(), d.mt_cur, B * sizeof(int32_t), hipMemcpyDeviceToHost));
+        GM_HIP(hipMemcpy(pos.data(), d.mt_pos, B * sizeof(int32_t), hipMemcpyDeviceToHost));
+        for (size_t b = 0; b < B; b++) {
+            if (st->rng_key) memcpy(st->rng_key + b * MT_N, mt.data() + (b * 2 + cur[b]) * MT_N, MT_N * 4);
+            if (st->rng_pos) st->rng_pos[b] = pos[b];
+        }
+    }
+    return GM_OK;
+}

@@ -1,0 +1,453 @@
+"""NetMon and DQN on the HIP kernels (reference src/model.py, src/layernormlstm.py).
+
+Parameter names match the reference's state_dicts (MLP.linear_layers.*,
+nn.LSTMCell weight_ih/weight_hh/bias_ih/bias_hh, q_net.fc.*), so reference
+checkpoints load unchanged. The forward arithmetic runs in libgraphmarl_amd:
+  * gm_linear_f32          every nn.Linear (+ MLP leaky_relu), fp32 MFMA
+  * gm_lstm_pointwise      nn.LSTMCell gate math
+  * gm_mp_aggregate        SimpleAggregation (sum / mean over I + A)
+  * gm_netmon_readout      [h, last neighbour h] readout fused with the agent gather
+Backward passes use the matching HIP backward kernels; weight/input gradients of
+the dense layers use library GEMMs (torch.mm -> hipBLASLt).
+"""
+import math
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from . import _lib as L
+
+SUM, MEAN = 0, 1
+
+
+def _s():
+    return L.stream_ptr()
+
+
+def _pad_stride(k):
+    return (k + 3) // 4 * 4
+
+
+class _WeightCache:
+    """fp32 weight with its row stride padded to a multiple of 4 (16-byte rows)."""
+
+    def __init__(self):
+        self.key = None
+        self.val = None
+
+    def get(self, w):
+        n, k = w.shape
+        kp = _pad_stride(k)
+        if kp == k and w.is_contiguous():
+            return w, k
+        key = (w.data_ptr(), w._version, kp)
+        if self.key != key:
+            self.val = F.pad(w.detach(), (0, kp - k)).contiguous()
+            self.key = key
+        return self.val, kp
+
+
+def linear_raw(x2d, ldx, k, w, b, act, out=None, ldy=None, wcache=None):
+    """y = act(x @ w^T + b) on the MFMA kernel. x2d: row-major rows with stride ldx."""
+    m = x2d.shape[0]
+    n = w.shape[0]
+    wp, ldw = (wcache.get(w) if wcache is not None else _WeightCache().get(w))
+    if out is None:
+        out = torch.empty(m, n, device=x2d.device, dtype=torch.float32)
+        ldy = n
+    L.check(L.lib().gm_linear_f32(L.ptr(x2d), ldx, L.ptr(wp), ldw, L.ptr(b), m, n, k, act, L.ptr(out), ldy, _s()))
+    return out
+
+
+def _as_rows(x):
+    """(2-D view, row stride, K) of a tensor whose last dim is contiguous."""
+    k = x.shape[-1]
+    x2 = x.reshape(-1, k) if x.dim() != 2 else x
+    if x2.stride(-1) != 1 or (x2.stride(0) % 4) != 0 or (x2.data_ptr() % 16) != 0:
+        x2 = F.pad(x2, (0, _pad_stride(k) - k)).contiguous()
+        return x2, x2.stride(0), k
+    return x2, x2.stride(0), k
+
+
+class LinearFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, b, act, wcache):
+        x2, ldx, k = _as_rows(x)
+        y = linear_raw(x2, ldx, k, w, b, act, wcache=wcache)
+        ctx.act = act
+        ctx.save_for_backward(x2[:, :k] if x2.shape[1] != k else x2, w, y)
+        return y.reshape(*x.shape[:-1], w.shape[0])
+
+    @staticmethod
+    def backward(ctx, gy):
+        x2, w, y = ctx.saved_tensors
+        gy = gy.reshape(-1, w.shape[0])
+        if ctx.act == 1:
+            gy = torch.where(y >= 0, gy, 0.01 * gy)
+        gx = gy @ w if ctx.needs_input_grad[0] else None
+        gw = gy.t() @ x2 if ctx.needs_input_grad[1] else None
+        gb = gy.sum(0) if ctx.needs_input_grad[2] else None
+        if gx is not None:
+            gx = gx.reshape(*ctx.saved_tensors[0].shape[:-1], w.shape[1])
+        return gx, gw, gb, None, None
+
+
+class Linear(nn.Linear):
+    """nn.Linear whose forward runs the fused fp32 MFMA kernel (act: 0 none, 1 leaky_relu)."""
+
+    def __init__(self, in_features, out_features, bias=True, act=0):
+        super().__init__(in_features, out_features, bias)
+        self.act = act
+        self._wc = _WeightCache()
+
+    def forward(self, x):
+        if x.shape[-1] != self.in_features:
+            raise ValueError(f"Linear expects {self.in_features} features, got {x.shape[-1]}")
+        lead = x.shape[:-1]
+        y = LinearFn.apply(x.reshape(-1, x.shape[-1]), self.weight, self.bias, self.act, self._wc)
+        return y.reshape(*lead, self.out_features)
+
+
+class MLP(nn.Module):
+    """src/model.py:13-42 (leaky_relu after every layer, including the output by default)."""
+
+    def __init__(self, in_features, mlp_units, activation_on_output=True):
+        super().__init__()
+        if isinstance(mlp_units, int):
+            mlp_units = [mlp_units]
+        self.linear_layers = nn.ModuleList()
+        prev = in_features
+        for i, u in enumerate(mlp_units):
+            last = i == len(mlp_units) - 1
+            self.linear_layers.append(Linear(prev, u, act=0 if (last and not activation_on_output) else 1))
+            prev = u
+        self.out_features = prev
+
+    def forward(self, x):
+        for lin in self.linear_layers:
+            x = lin(x)
+        return x
+
+    def forward_into(self, x2d, ldx, k, scratch):
+        """no-grad fast path over a strided row buffer (e.g. the joint observation)."""
+        h, ld, kk = x2d, ldx, k
+        for i, lin in enumerate(self.linear_layers):
+            out = scratch(i, x2d.shape[0], lin.out_features)
+            linear_raw(h, ld, kk, lin.weight, lin.bias, lin.act, out=out, ldy=out.stride(0), wcache=lin._wc)
+            h, ld, kk = out, out.stride(0), lin.out_features
+        return h
+
+
+class _Aggregate(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, h, nbr, mode):
+        G, N, deg = nbr.shape
+        H = h.shape[-1]
+        out = torch.empty_like(h)
+        L.check(L.lib().gm_mp_aggregate(L.ptr(h), L.ptr(nbr), G, N, deg, H, mode, L.ptr(out), _s()))
+        ctx.save_for_backward(nbr)
+        ctx.mode = mode
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        (nbr,) = ctx.saved_tensors
+        G, N, deg = nbr.shape
+        g = g.contiguous()
+        dh = torch.empty_like(g)
+        L.check(L.lib().gm_mp_aggregate_bwd(L.ptr(g), L.ptr(nbr), G, N, deg, g.shape[-1], ctx.mode, L.ptr(dh), _s()))
+        return dh, None, None
+
+
+def mp_aggregate(h, nbr, mode=SUM):
+    """SimpleAggregation (src/model.py:206-229): rows of h [G*N, H] summed over {n} ∪ nbr(n)."""
+    return _Aggregate.apply(h.contiguous(), nbr, mode)
+
+
+class _Readout(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, hf, hp, nbr, agent_node, out, col0):
+        G, N, deg = nbr.shape
+        H = hf.shape[-1]
+        R = N if agent_node is None else agent_node.shape[1]
+        if out is None:
+            res = torch.empty(G * R, (deg + 1) * H, device=hf.device)
+            dst, stride = res, res.stride(0)
+        else:
+            res = None
+            dst = out.view(-1, out.shape[-1])[:, col0:]
+            stride = out.shape[-1]
+        L.check(L.lib().gm_netmon_readout(L.ptr(hf), L.ptr(hp), L.ptr(nbr), L.ptr(agent_node), G, N, R, deg, H,
+                                          L.ptr(dst), stride, _s()))
+        ctx.save_for_backward(nbr, agent_node if agent_node is not None else torch.empty(0))
+        ctx.has_map = agent_node is not None
+        ctx.H = H
+        return res if res is not None else out
+
+    @staticmethod
+    def backward(ctx, g):
+        nbr, an = ctx.saved_tensors
+        an = an if ctx.has_map else None
+        G, N, deg = nbr.shape
+        R = N if an is None else an.shape[1]
+        g = g.contiguous()
+        dhf = torch.empty(G * N, ctx.H, device=g.device)
+        dhp = torch.empty(G * N, ctx.H, device=g.device)
+        L.check(L.lib().gm_netmon_readout_bwd(L.ptr(g), g.shape[-1], L.ptr(nbr), L.ptr(an), G, N, R, deg, ctx.H,
+                                              L.ptr(dhf), L.ptr(dhp), _s()))
+        return dhf, dhp, None, None, None, None
+
+
+def netmon_readout(h_final, h_prev, nbr, agent_node=None, out=None, col0=0):
+    """NetMon readout (src/model.py:457-474, 582-631): rows [h(v), h_prev(nbr(v, 0..2))]
+    for v = agent_node[g, r] (output_to_network_obs) or every node. With `out` the rows
+    are written into columns [col0, col0 + 4H) of an existing buffer (no-grad path)."""
+    return _Readout.apply(h_final.contiguous(), h_prev.contiguous(), nbr, agent_node, out, col0)
+
+
+class _LSTMPointwise(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, gates, c):
+        M, H4 = gates.shape
+        H = H4 // 4
+        h1 = torch.empty(M, H, device=gates.device)
+        c1 = torch.empty(M, H, device=gates.device)
+        need = torch.is_grad_enabled() and (gates.requires_grad or c.requires_grad)
+        act = torch.empty_like(gates) if need else None
+        L.check(L.lib().gm_lstm_pointwise(L.ptr(gates), L.ptr(c), M, H, L.ptr(h1), L.ptr(c1), L.ptr(act), _s()))
+        if need:
+            ctx.save_for_backward(act, c, c1)
+        return h1, c1
+
+    @staticmethod
+    def backward(ctx, dh1, dc1):
+        act, c, c1 = ctx.saved_tensors
+        M, H = c.shape
+        dg = torch.empty(M, 4 * H, device=c.device)
+        dc = torch.empty(M, H, device=c.device)
+        dh1 = None if dh1 is None else dh1.contiguous()
+        dc1 = None if dc1 is None else dc1.contiguous()
+        L.check(L.lib().gm_lstm_pointwise_bwd(L.ptr(dh1), L.ptr(dc1), L.ptr(act), L.ptr(c), L.ptr(c1), M, H,
+                                              L.ptr(dg), L.ptr(dc), _s()))
+        return dg, dc
+
+
+class LSTMCell(nn.Module):
+    """nn.LSTMCell parameters/semantics; gates = [x|h] @ [W_ih|W_hh]^T + (b_ih + b_hh)
+    in one MFMA GEMM, gate math in gm_lstm_pointwise."""
+
+    def __init__(self, input_size, hidden_size):
+        super().__init__()
+        self.input_size, self.hidden_size = input_size, hidden_size
+        self.weight_ih = nn.Parameter(torch.empty(4 * hidden_size, input_size))
+        self.weight_hh = nn.Parameter(torch.empty(4 * hidden_size, hidden_size))
+        self.bias_ih = nn.Parameter(torch.empty(4 * hidden_size))
+        self.bias_hh = nn.Parameter(torch.empty(4 * hidden_size))
+        stdv = 1.0 / math.sqrt(hidden_size)
+        for p in self.parameters():
+            nn.init.uniform_(p, -stdv, stdv)
+        self._wc = _WeightCache()
+
+    def forward(self, x, state):
+        h, c = state
+        xh = torch.cat([x, h], -1)
+        w = torch.cat([self.weight_ih, self.weight_hh], 1)
+        b = self.bias_ih + self.bias_hh
+        if torch.is_grad_enabled() and (w.requires_grad or xh.requires_grad):
+            gates = LinearFn.apply(xh, w, b, 0, None)
+        else:
+            gates = linear_raw(xh, xh.stride(0), xh.shape[1], w, b, 0)
+        return _LSTMPointwise.apply(gates, c.contiguous())
+
+
+class LayerNormLSTMCell(nn.Module):
+    """src/layernormlstm.py:8-42 (LN on the input and hidden gate pre-activations and on
+    the cell, single bias). GEMMs on the MFMA kernel; the normalisations use torch."""
+
+    def __init__(self, input_size, hidden_size):
+        super().__init__()
+        self.input_size, self.hidden_size = input_size, hidden_size
+        self.weight_ih = nn.Parameter(torch.empty(4 * hidden_size, input_size))
+        self.weight_hh = nn.Parameter(torch.empty(4 * hidden_size, hidden_size))
+        self.bias_ih = nn.Parameter(torch.empty(4 * hidden_size))
+        stdv = 1.0 / math.sqrt(hidden_size)
+        for p in self.parameters():
+            nn.init.uniform_(p, -stdv, stdv)
+        self.ln_input = nn.LayerNorm(4 * hidden_size)
+        self.ln_hidden = nn.LayerNorm(4 * hidden_size)
+        self.ln_cell = nn.LayerNorm(hidden_size)
+
+    def forward(self, x, state):
+        hx, cx = state
+        gi = self.ln_input(LinearFn.apply(x, self.weight_ih, None, 0, None))
+        gh = self.ln_hidden(LinearFn.apply(hx, self.weight_hh, None, 0, None))
+        g = gi + gh + self.bias_ih
+        H = self.hidden_size
+        i, f, gg, o = torch.sigmoid(g[:, :H]), torch.sigmoid(g[:, H:2 * H]), torch.tanh(g[:, 2 * H:3 * H]), \
+            torch.sigmoid(g[:, 3 * H:])
+        cy = self.ln_cell(f * cx + i * gg)
+        return o * torch.tanh(cy), cy
+
+
+class GRUCell(nn.Module):
+    """nn.GRUCell semantics (r, z, n) with the GEMMs on the MFMA kernel."""
+
+    def __init__(self, input_size, hidden_size):
+        super().__init__()
+        self.input_size, self.hidden_size = input_size, hidden_size
+        self.weight_ih = nn.Parameter(torch.empty(3 * hidden_size, input_size))
+        self.weight_hh = nn.Parameter(torch.empty(3 * hidden_size, hidden_size))
+        self.bias_ih = nn.Parameter(torch.empty(3 * hidden_size))
+        self.bias_hh = nn.Parameter(torch.empty(3 * hidden_size))
+        stdv = 1.0 / math.sqrt(hidden_size)
+        for p in self.parameters():
+            nn.init.uniform_(p, -stdv, stdv)
+
+    def forward(self, x, h):
+        gi = LinearFn.apply(x, self.weight_ih, self.bias_ih, 0, None)
+        gh = LinearFn.apply(h, self.weight_hh, self.bias_hh, 0, None)
+        H = self.hidden_size
+        r = torch.sigmoid(gi[:, :H] + gh[:, :H])
+        z = torch.sigmoid(gi[:, H:2 * H] + gh[:, H:2 * H])
+        n = torch.tanh(gi[:, 2 * H:] + r * gh[:, 2 * H:])
+        return (1 - z) * n + z * h
+
+
+def dense_to_nbr(mask):
+    """(I + A) float mask [B, N, N] -> neighbour table int32 [B, N, deg] (ascending, -1 pad)."""
+    B, N, _ = mask.shape
+    m = (mask != 0) & ~torch.eye(N, dtype=torch.bool, device=mask.device)
+    deg = int(m.sum(-1).max().item()) if m.numel() else 0
+    deg = max(deg, 1)
+    ids = torch.arange(N, device=mask.device).expand(B, N, N)
+    key = torch.where(m, ids, ids + N)
+    srt = key.sort(-1).values[..., :deg]
+    return torch.where(srt < N, srt, torch.full_like(srt, -1)).to(torch.int32).contiguous()
+
+
+def node_agent_to_index(node_agent):
+    """node-agent matrix [B, N, A] -> node index of every agent int32 [B, A]."""
+    return node_agent.argmax(1).to(torch.int32).contiguous()
+
+
+class NetMon(nn.Module):
+    """src/model.py:256-650 for agg_type sum|mean, rnn lstm|lnlstm|gru, carry-over state.
+
+    forward(x, mask, node_agent_matrix, max_degree=None, no_agent_mapping=False) keeps the
+    reference signature (dense (I+A) mask / node-agent matrix); forward_graph() is the
+    native entry point taking the neighbour table nbr [B, N, 3] and agent_node [B, A].
+    """
+
+    def __init__(self, in_features, hidden_features, encoder_units, iterations, rnn_type="lstm",
+                 rnn_carryover=True, agg_type="sum", output_neighbor_hidden=True, output_global_hidden=False):
+        super().__init__()
+        if agg_type not in ("sum", "mean"):
+            raise NotImplementedError(f"agg_type {agg_type!r}: only sum/mean are built (torch_geometric variants "
+                                      "are out of scope)")
+        if not rnn_carryover:
+            raise NotImplementedError("rnn_carryover=False is not built")
+        if output_global_hidden:
+            raise NotImplementedError("--netmon-global readout is not built")
+        self.encode = MLP(in_features, (*encoder_units, hidden_features))
+        self.state = None
+        self.iterations = iterations
+        self.output_neighbor_hidden = output_neighbor_hidden
+        self.output_global_hidden = output_global_hidden
+        self.rnn_carryover = rnn_carryover
+        self.agg_type_str = agg_type
+        self.agg_mode = SUM if agg_type == "sum" else MEAN
+        self.rnn_type = rnn_type
+        if rnn_type == "lstm":
+            self.rnn_obs = LSTMCell(hidden_features, hidden_features)
+            self.rnn_update = LSTMCell(hidden_features, hidden_features)
+            self.num_states = 2
+        elif rnn_type == "lnlstm":
+            self.rnn_obs = LayerNormLSTMCell(hidden_features, hidden_features)
+            self.rnn_update = LayerNormLSTMCell(hidden_features, hidden_features)
+            self.num_states = 2
+        elif rnn_type == "gru":
+            self.rnn_obs = GRUCell(hidden_features, hidden_features)
+            self.rnn_update = GRUCell(hidden_features, hidden_features)
+            self.num_states = 1
+        else:
+            raise NotImplementedError(f"rnn_type {rnn_type!r}")
+        self.hidden_features = hidden_features
+        self.state_size = hidden_features * self.num_states
+
+    def get_out_features(self):
+        return self.hidden_features * (4 if self.output_neighbor_hidden else 1)
+
+    def get_state_size(self):
+        return self.state_size
+
+    def _cell(self, cell, x, h, c):
+        if self.rnn_type == "gru":
+            return cell(x, h), None
+        return cell(x, (h, c))
+
+    def forward_graph(self, x, nbr, agent_node=None, out=None, out_col=0):
+        """x [B, N, F] node observations, nbr int32 [B, N, deg], agent_node int32 [B, A] or None.
+        Returns [B, A or N, 4H] (or writes into `out` [B, A, W] at column out_col)."""
+        B, N, Fdim = x.shape
+        H = self.hidden_features
+        if self.state is None:
+            self.state = torch.zeros(B, N, self.state_size, device=x.device)
+        st = self.state.reshape(B * N, self.num_states, H)
+        h = self.encode(x.reshape(B * N, Fdim))
+        hs, cs = st[:, 0], (st[:, 1] if self.num_states == 2 else None)
+        h, c = self._cell(self.rnn_obs, h, hs.contiguous(), None if cs is None else cs.contiguous())
+        last_nbr = torch.zeros_like(h) if self.iterations <= 0 else None
+        for it in range(self.iterations):
+            if it == self.iterations - 1:
+                last_nbr = h
+            M = mp_aggregate(h, nbr, self.agg_mode)
+            h, c = self._cell(self.rnn_update, M, h, c)
+        self.state = (torch.stack((h, c), 1) if c is not None else h.unsqueeze(1)).reshape(B, N, self.state_size)
+        if not self.output_neighbor_hidden:
+            hv = h.reshape(B, N, H)
+            if agent_node is None:
+                return hv
+            return torch.gather(hv, 1, agent_node.long().unsqueeze(-1).expand(-1, -1, H))
+        res = netmon_readout(h, last_nbr, nbr, agent_node, out=out, col0=out_col)
+        if out is not None:
+            return out
+        R = N if agent_node is None else agent_node.shape[1]
+        return res.reshape(B, R, -1)
+
+    def forward(self, x, mask, node_agent_matrix=None, max_degree=None, no_agent_mapping=False):
+        nbr = dense_to_nbr(mask)
+        an = None if (no_agent_mapping or node_agent_matrix is None) else node_agent_to_index(node_agent_matrix)
+        return self.forward_graph(x, nbr, an)
+
+    @staticmethod
+    def output_to_network_obs(netmon_out, node_agent_matrix):
+        return torch.bmm(netmon_out.transpose(1, 2), node_agent_matrix).transpose(1, 2)
+
+
+class Q_Net(nn.Module):
+    def __init__(self, in_features, actions):
+        super().__init__()
+        self.fc = Linear(in_features, actions, act=0)
+
+    def forward(self, x):
+        return self.fc(x)
+
+
+class DQN(nn.Module):
+    """src/model.py:187-203: MLP encoder (activation on output) + linear Q head."""
+
+    def __init__(self, in_features, mlp_units, num_actions):
+        super().__init__()
+        self.encoder = MLP(in_features, mlp_units)
+        self.q_net = Q_Net(self.encoder.out_features, num_actions)
+
+    def forward(self, x, mask=None):
+        return self.q_net(self.encoder(x))
+
+    def forward_rows(self, x2d, ldx, k, scratch):
+        """no-grad fast path: q [rows, actions] from a strided observation buffer."""
+        h = self.encoder.forward_into(x2d, ldx, k, scratch)
+        out = scratch(len(self.encoder.linear_layers), x2d.shape[0], self.q_net.fc.out_features)
+        return linear_raw(h, h.stride(0), h.shape[1], self.q_net.fc.weight, self.q_net.fc.bias, 0, out=out,
+                          ldy=out.stride(0), wcache=self.q_net.fc._wc)

@@ -1,0 +1,67 @@
+"""ε-greedy action selection on the device (reference src/policy.py:7-87 EpsilonGreedy).
+
+Q-values come from the DQN on the HIP linear kernels; the random draws
+(randint(4, size=A) then rand(A), every call, from each env's numpy-legacy stream)
+and the argmax/mix run in gm_policy_egreedy.
+"""
+import torch
+
+from . import _lib as L
+
+
+class EpsilonGreedy:
+    def __init__(self, env, model, action_space=4, args=None, epsilon=None, epsilon_decay=None,
+                 epsilon_update_freq=None, step_before_train=None):
+        self._env = env.get() if hasattr(env, "get") else env
+        self._model = model
+        self._action_space = action_space
+        self._epsilon = epsilon if epsilon is not None else getattr(args, "epsilon", 0.6)
+        self._decay = epsilon_decay if epsilon_decay is not None else getattr(args, "epsilon_decay", 0.996)
+        self._freq = epsilon_update_freq if epsilon_update_freq is not None else getattr(args, "epsilon_update_freq",
+                                                                                          100)
+        self._before = step_before_train if step_before_train is not None else getattr(args, "step_before_train",
+                                                                                        2000)
+        self._step = 0
+        self._eps_tmp = None
+        e = self._env
+        self.actions = torch.zeros(e.n_env, e.n_data, dtype=torch.int32, device=e.device)
+        self._scratch = {}
+
+    def _buf(self, i, m, n):
+        key = (i, m, n)
+        b = self._scratch.get(key)
+        if b is None:
+            b = torch.empty(m, n, device=self._env.device)
+            self._scratch[key] = b
+        return b
+
+    def q_values(self, obs):
+        """q [n_env, A, 4] for a joint observation view [n_env, A, D] (strided rows ok)."""
+        e = self._env
+        with torch.no_grad():
+            x2 = obs.reshape(-1, obs.shape[-1])
+            q = self._model.forward_rows(x2, x2.stride(0), obs.shape[-1], self._buf)
+        return q.view(e.n_env, e.n_data, -1)
+
+    def select(self, q):
+        """ε-greedy mix of argmax(q) and uniform actions, drawn from each env's stream."""
+        e = self._env
+        L.check(L.lib().gm_policy_egreedy(e._h, L.ptr(q), float(self._epsilon), L.ptr(self.actions),
+                                          L.stream_ptr(e.device)))
+        return self.actions
+
+    def __call__(self, obs, adj=None):
+        self._step += 1
+        actions = self.select(self.q_values(obs))
+        if self._epsilon > 0 and self._step > self._before and self._step % self._freq == 0:
+            self._epsilon = max(self._epsilon * self._decay, 0.01)
+        return actions
+
+    def eval(self):
+        self._eps_tmp = self._epsilon
+        self._epsilon = 0
+
+    def train(self):
+        if self._eps_tmp is not None:
+            self._epsilon = self._eps_tmp
+            self._eps_tmp = None

@@ -1,0 +1,297 @@
+"""Batched routing environment with the reference's NetworkEnv API.
+
+Mirrors `Network` + `Routing` (reference src/env/network.py:42-389,
+src/env/routing.py:43-552) for `n_env` independent graph instances resident in
+HBM. Every method returns torch tensors on the GPU with a leading env dimension;
+the arithmetic runs in the HIP kernels of libgraphmarl_amd.so (gm_env_*).
+Per-env behaviour is bit-identical to the reference given the same numpy seed.
+"""
+import ctypes as C
+import os
+from dataclasses import dataclass, field
+from typing import List, Optional
+
+import numpy as np
+import torch
+
+from . import _lib as L
+
+EVAL_SEEDS = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "data", "eval_seeds.npy"))
+
+
+class Discrete:
+    """Stand-in for gymnasium.spaces.Discrete as the reference uses it (.n only)."""
+
+    def __init__(self, n, start=0):
+        self.n, self.start = n, start
+
+
+@dataclass
+class Network:
+    """Topology configuration (reference Network.__init__, src/env/network.py:47-98).
+
+    Seeds are resolved exactly like the reference: a fixed topology seed, a list of
+    `n_random_seeds` valid seeds built from `topology_init_seed` (device
+    build_seed_list), provided seeds, or a fresh random seed per reset."""
+
+    n_nodes: int = 20
+    random_topology: bool = False
+    n_random_seeds: Optional[int] = None
+    sequential_topology_seeds: bool = False
+    topology_init_seed: int = 476
+    excluded_seeds: Optional[List[int]] = None
+    provided_seeds: Optional[List[int]] = None
+    device: int = 0
+    seeds: List[int] = field(default_factory=list)
+
+    def __post_init__(self):
+        if self.n_nodes % 2:
+            raise ValueError("n_nodes must be even (random 3-regular topologies)")
+        if self.provided_seeds is not None and len(self.provided_seeds) > 0:
+            self.seeds = list(self.provided_seeds)
+        elif not self.random_topology:
+            self.seeds = [self.topology_init_seed]
+        elif self.n_random_seeds is None or self.n_random_seeds <= 0:
+            self.seeds = []
+        else:
+            self.seeds = build_seed_list(self.n_nodes, self.topology_init_seed, self.n_random_seeds,
+                                         self.excluded_seeds, self.device)
+        if self.excluded_seeds is not None:
+            ex = set(int(s) for s in self.excluded_seeds)
+            assert all(int(s) not in ex for s in self.seeds)
+
+    def mode(self):
+        if not self.random_topology and not (self.provided_seeds and len(self.provided_seeds) > 0):
+            return L.TOPO_FIXED, self.topology_init_seed, None
+        if len(self.seeds) == 0:
+            return L.TOPO_RANDOM, self.topology_init_seed, None
+        if self.sequential_topology_seeds and len(self.seeds) > 1:
+            return L.TOPO_SEQUENTIAL, self.topology_init_seed, self.seeds
+        return L.TOPO_LIST, self.topology_init_seed, self.seeds
+
+
+def build_seed_list(n_nodes, init_seed, count, excluded=None, device=0):
+    """Network.build_seed_list (src/env/network.py:100-120), computed on the GPU."""
+    L.require_gpu()
+    out = np.zeros(count, dtype=np.int64)
+    ex = None if excluded is None else np.ascontiguousarray(np.sort(np.asarray(excluded, np.int64)))
+    L.check(L.lib().gm_build_seed_list(n_nodes, init_seed, count, None if ex is None else ex.ctypes.data,
+                                       0 if ex is None else len(ex), device, out.ctypes.data))
+    return [int(s) for s in out]
+
+
+class Routing:
+    """n_env routing environments (reference Routing, src/env/routing.py:43).
+
+    :param network: topology configuration (`Network`)
+    :param n_data: packets (agents) per env
+    :param env_var: environment variant; 1 (INDEPENDENT) is implemented
+    :param n_env: number of parallel graph instances
+    :param seeds: per-env numpy-legacy seeds (default: seed + env index)
+    :param obs_extra: extra zero columns reserved after each agent observation (the
+        NetMon wrapper writes its 4H graph features there, fusing the reference's concat)
+    :param agent_adjacency: compute the agent adjacency every step (the reference
+        returns it from step(); the DQN ignores it, the hot path turns it off)
+    """
+
+    def __init__(self, network: Network, n_data=20, env_var=1, k=3, enable_congestion=True,
+                 enable_action_mask=False, ttl=0, n_env=1, seeds=None, seed=0, obs_extra=0,
+                 agent_adjacency=True, device=None):
+        L.require_gpu()
+        self.network = network
+        self.n_data = n_data
+        self.n_env = n_env
+        self.env_var = env_var
+        self.k = k
+        self.enable_congestion = enable_congestion
+        self.enable_action_mask = enable_action_mask
+        self.ttl = ttl
+        self.action_space = Discrete(4, start=0)
+        self.agent_adjacency = agent_adjacency
+        self.device = torch.device("cuda", network.device if device is None else device)
+        self.eval_info_enabled = False
+        mode, tseed, lst = network.mode()
+        cfg = L.EnvConfig()
+        cfg.n_env, cfg.n_nodes, cfg.n_data, cfg.env_var = n_env, network.n_nodes, n_data, env_var
+        cfg.congestion, cfg.action_mask, cfg.ttl = int(enable_congestion), int(enable_action_mask), int(ttl)
+        cfg.topo_mode, cfg.topo_seed = mode, int(tseed)
+        self._keep = []
+        if lst is not None:
+            arr = np.ascontiguousarray(np.asarray(lst, np.int64))
+            self._keep.append(arr)
+            cfg.seed_list, cfg.n_seed_list = arr.ctypes.data_as(C.POINTER(C.c_int64)), len(arr)
+        if network.excluded_seeds is not None:
+            ex = np.ascontiguousarray(np.sort(np.asarray(network.excluded_seeds, np.int64)))
+            self._keep.append(ex)
+            cfg.excluded, cfg.n_excluded = ex.ctypes.data_as(C.POINTER(C.c_int64)), len(ex)
+        cfg.device = self.device.index or 0
+        if seeds is None:
+            seeds = [(seed + i) & 0xFFFFFFFF for i in range(n_env)]
+        seeds_arr = np.ascontiguousarray(np.asarray(seeds, dtype=np.uint32))
+        assert len(seeds_arr) == n_env
+        h = C.c_void_p()
+        with torch.cuda.device(self.device):
+            L.check(L.lib().gm_env_create(C.byref(cfg), seeds_arr.ctypes.data, C.byref(h)))
+        self._h = h
+        N, A = network.n_nodes, n_data
+        self.n_nodes = N
+        self.obs_dim = 6 * N + 10
+        self.node_obs_dim = 4 * N + 8
+        self.obs_stride = ((self.obs_dim + obs_extra + 3) // 4) * 4
+        dev = self.device
+        # persistent device buffers (filled in place by the kernels; no allocation per step)
+        self.obs_buf = torch.zeros(n_env, A, self.obs_stride, device=dev)
+        self.node_obs = torch.zeros(n_env, N, self.node_obs_dim, device=dev)
+        self.agent_node = torch.zeros(n_env, A, dtype=torch.int32, device=dev)
+        self.agent_adj = torch.zeros(n_env, A, A, dtype=torch.int8, device=dev)
+        self.reward = torch.zeros(n_env, A, device=dev)
+        self.done = torch.zeros(n_env, A, dtype=torch.uint8, device=dev)
+        self.info = torch.zeros(n_env, L.GM_INFO_FIELDS, dtype=torch.float64, device=dev)
+        self.nbr = torch.zeros(n_env, N, 3, dtype=torch.int32, device=dev)
+        self._actions = torch.zeros(n_env, A, dtype=torch.int32, device=dev)
+        self._obsbufs = self._make_obsbufs(self.agent_adjacency)
+
+    # -- plumbing ---------------------------------------------------------------
+    def _make_obsbufs(self, adj):
+        o = L.ObsBuffers()
+        o.obs = self.obs_buf.data_ptr()
+        o.obs_row_stride = self.obs_stride
+        o.node_obs = self.node_obs.data_ptr()
+        o.agent_node = self.agent_node.data_ptr()
+        o.agent_adj = self.agent_adj.data_ptr() if adj else None
+        return o
+
+    def _stream(self):
+        return L.stream_ptr(self.device)
+
+    def close(self):
+        if getattr(self, "_h", None):
+            L.lib().gm_env_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def obs(self):
+        """agent observations [n_env, A, 6N+10] (view of the persistent buffer)."""
+        return self.obs_buf[..., : self.obs_dim]
+
+    def __str__(self):
+        return (f"Routing environment (graph-marl_amd, {self.n_env} parallel envs)\n"
+                f"> Network: {self.n_nodes} nodes\n> Number of packets: {self.n_data}\n"
+                f"> Congestion: {self.enable_congestion}\n> Action mask: {self.enable_action_mask}\n"
+                f"> TTL: {self.ttl if self.ttl > 0 else 'disabled'}")
+
+    # -- NetworkEnv API -----------------------------------------------------------
+    def set_eval_info(self, val):
+        self.eval_info_enabled = val
+
+    def reset_(self, mask=None):
+        """Reset envs in place (mask: bool/uint8 [n_env] on device, None = all)."""
+        m = None if mask is None else mask.to(torch.uint8)
+        L.check(L.lib().gm_env_reset(self._h, L.ptr(m), C.byref(self._obsbufs), self._stream()))
+        L.check(L.lib().gm_env_topology(self._h, L.ptr(self.nbr), None, None, None, self._stream()))
+
+    def reset(self):
+        """Routing.reset (routing.py:160-178) for every env -> (obs, agent adjacency)."""
+        self.reset_()
+        return self.obs, self.agent_adj
+
+    def step_(self, actions, detail=None):
+        """Routing.step in place; results in self.obs/reward/done/info."""
+        a = actions
+        if a.dtype != torch.int32 or not a.is_contiguous():
+            self._actions.copy_(a)
+            a = self._actions
+        det = None
+        if detail is not None:
+            det = L.StepDetail()
+            det.done_steps, det.done_opt, det.success = (detail["done_steps"].data_ptr(),
+                                                         detail["done_opt"].data_ptr(),
+                                                         detail["success"].data_ptr())
+        L.check(L.lib().gm_env_step(self._h, L.ptr(a), L.ptr(self.reward), L.ptr(self.done), L.ptr(self.info),
+                                    None if det is None else C.byref(det), C.byref(self._obsbufs),
+                                    self._stream()))
+
+    def step(self, act):
+        """Routing.step (routing.py:360-520) -> (obs, adj, reward, done, info) with a
+        leading env dim; info holds per-env sums (see _lib.INFO_KEYS)."""
+        if not torch.is_tensor(act):
+            act = torch.as_tensor(np.asarray(act), device=self.device)
+        self.step_(act.to(self.device))
+        info = {k: self.info[:, i] for i, k in enumerate(L.INFO_KEYS)}
+        return self.obs, self.agent_adj, self.reward, self.done.bool(), info
+
+    def get_nodes_adjacency(self):
+        out = torch.empty(self.n_env, self.n_nodes, self.n_nodes, dtype=torch.int8, device=self.device)
+        L.check(L.lib().gm_env_topology(self._h, None, L.ptr(out), None, None, self._stream()))
+        return out
+
+    def get_node_observation(self):
+        return self.node_obs
+
+    def get_node_aux(self):
+        out = torch.empty(self.n_env, self.n_nodes, self.n_nodes, device=self.device)
+        L.check(L.lib().gm_env_topology(self._h, None, None, L.ptr(out), None, self._stream()))
+        return out
+
+    def get_node_agent_matrix(self):
+        m = torch.zeros(self.n_env, self.n_nodes, self.n_data, dtype=torch.int8, device=self.device)
+        m.scatter_(1, self.agent_node.long().unsqueeze(1), 1)
+        return m
+
+    def get_topology_seeds(self):
+        out = torch.empty(self.n_env, dtype=torch.int64, device=self.device)
+        L.check(L.lib().gm_env_topology(self._h, None, None, None, L.ptr(out), self._stream()))
+        return out
+
+    def get_final_info(self, info):
+        """Routing.get_final_info: adds the still-running packets' steps to the delays."""
+        out = torch.empty(self.n_env, 2, dtype=torch.float64, device=self.device)
+        L.check(L.lib().gm_env_final_info(self._h, L.ptr(out), self._stream()))
+        info = dict(info)
+        info["sum_delays"] = info["sum_delays"] + out[:, 0]
+        info["n_delays"] = info["n_delays"] + out[:, 1]
+        return info
+
+    def observe(self):
+        L.check(L.lib().gm_env_observe(self._h, C.byref(self._make_obsbufs(True)), self._stream()))
+
+    def get_num_agents(self):
+        return self.n_data
+
+    def get_num_nodes(self):
+        return self.n_nodes
+
+    def get(self):
+        return self
+
+    # -- parity / debugging ---------------------------------------------------------
+    def get_state(self):
+        """Copy the full env state to host numpy arrays (synchronous)."""
+        B, A, N, E = self.n_env, self.n_data, self.n_nodes, 3 * self.n_nodes // 2
+        arrs = dict(
+            now=np.zeros((B, A), np.int32), target=np.zeros((B, A), np.int32), edge=np.zeros((B, A), np.int32),
+            time=np.zeros((B, A), np.int32), ttl=np.zeros((B, A), np.int32), start=np.zeros((B, A), np.int32),
+            spw=np.zeros((B, A), np.int32), agent_steps=np.zeros((B, A), np.int32),
+            size=np.zeros((B, A), np.float64), visited=np.zeros((B, A, 2), np.uint64),
+            amask=np.zeros((B, A, 4), np.uint8), loads=np.zeros((B, E), np.float64),
+            topo_seed=np.zeros(B, np.int64), topo_reps=np.zeros(B, np.int32), edge_a=np.zeros((B, E), np.int32),
+            edge_b=np.zeros((B, E), np.int32), edge_len=np.zeros((B, E), np.int32),
+            nbr_edge=np.zeros((B, N, 3), np.int32), apsp=np.zeros((B, N, N), np.int32),
+            rng_key=np.zeros((B, 624), np.uint32), rng_pos=np.zeros(B, np.int32),
+        )
+        st = L.EnvState()
+        for k, v in arrs.items():
+            setattr(st, k, v.ctypes.data)
+        torch.cuda.synchronize(self.device)
+        L.check(L.lib().gm_env_get_state(self._h, C.byref(st)))
+        return arrs
+
+    @property
+    def action_mask(self):
+        return torch.as_tensor(self.get_state()["amask"].astype(bool), device=self.device)

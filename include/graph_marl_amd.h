@@ -1,0 +1,176 @@
+/* graph_marl_amd.h — C ABI of the MI355X-native graph-marl hot path.
+ *
+ * One handle = one batch of n_env independent routing environments resident in
+ * HBM of one device. Every entry point takes plain device pointers, sizes and a
+ * hipStream_t (passed as void*); nothing here allocates on the step path.
+ * Return value: 0 on success, a negative gm_status otherwise; gm_last_error()
+ * returns a message for the calling thread's last failure.
+ *
+ * Reference interfaces replaced (paths relative to the reference repo root):
+ *   gm_env_create / gm_env_destroy   Routing.__init__ + Network.__init__   src/env/routing.py:55-109, src/env/network.py:47-98
+ *   gm_env_reset                     Routing.reset (+ Network.reset)        src/env/routing.py:160-178, src/env/network.py:366-371
+ *   gm_env_step                      Routing.step                           src/env/routing.py:360-520
+ *   gm_env_observe                   _get_observation / get_node_observation / get_node_agent_matrix /
+ *                                    _get_data_adjacency / get_node_aux     src/env/routing.py:187-358, 522-539
+ *   gm_env_topology                  get_nodes_adjacency (+ neighbour table) src/env/routing.py:184-185, src/env/network.py:385-389
+ *   gm_env_final_info                Routing.get_final_info                 src/env/routing.py:541-546
+ *   gm_build_seed_list               Network.build_seed_list                src/env/network.py:100-120
+ *   gm_policy_egreedy                EpsilonGreedy.__call__ (draws + select) src/policy.py:20-64
+ *   gm_mp_aggregate(_bwd)            SimpleAggregation.forward              src/model.py:206-229
+ *   gm_netmon_readout(_bwd)          NetMon._get_neighbor_h + output_to_network_obs src/model.py:582-631
+ *   gm_lstm_pointwise(_bwd)          nn.LSTMCell gate math / LayerNorm-free part    src/model.py:379-382, 491, 543
+ *   gm_linear_f32                    nn.Linear (+ leaky_relu of MLP)        src/model.py:13-42, 119-125
+ */
+#ifndef GRAPH_MARL_AMD_H
+#define GRAPH_MARL_AMD_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef enum {
+    GM_OK = 0,
+    GM_ERR_INVALID_ARG = -1,
+    GM_ERR_OOM = -2,
+    GM_ERR_HIP = -3,
+    GM_ERR_TOPOLOGY = -4, /* a provided topology seed is invalid / generator retry limit hit */
+    GM_ERR_UNSUPPORTED = -5
+} gm_status;
+
+/* topology modes: Network seed handling, src/env/network.py:215-272, 356-371 */
+typedef enum {
+    GM_TOPO_FIXED = 0,      /* --random-topology=0: one seed, no main-stream draw            */
+    GM_TOPO_RANDOM = 1,     /* --random-topology=1 --num-topologies-train=0: fresh seed/reset */
+    GM_TOPO_LIST = 2,       /* seed list, np.random.choice per reset                          */
+    GM_TOPO_SEQUENTIAL = 3  /* seed list walked in order per env (evaluation over EVAL_SEEDS) */
+} gm_topo_mode;
+
+typedef struct {
+    int32_t n_env;
+    int32_t n_nodes;        /* --n-router, even, <= 64          */
+    int32_t n_data;         /* --n-data (agents), <= 64          */
+    int32_t env_var;        /* --env-var; only 1 (INDEPENDENT)   */
+    int32_t congestion;     /* !--no-congestion                  */
+    int32_t action_mask;    /* --action-mask                     */
+    int32_t ttl;            /* --ttl (0 disables)                */
+    int32_t topo_mode;      /* gm_topo_mode                      */
+    int64_t topo_seed;      /* --topology-init-seed (FIXED)      */
+    const int64_t* seed_list;  /* host, LIST / SEQUENTIAL        */
+    int32_t n_seed_list;
+    const int64_t* excluded;   /* host, seeds never used (EVAL_SEEDS); may be NULL */
+    int32_t n_excluded;
+    int32_t device;         /* HIP device ordinal                */
+} gm_env_config;
+
+/* Optional observation outputs (any pointer may be NULL). */
+typedef struct {
+    float* obs;             /* [n_env, A, obs_row_stride]; columns [0, 6N+10) written     */
+    int64_t obs_row_stride; /* floats between agent rows (>= 6N+10; 6N+10+512 with NetMon) */
+    float* node_obs;        /* [n_env, N, 4N+8]                                           */
+    int32_t* agent_node;    /* [n_env, A] node index of every agent (node-agent matrix)   */
+    int8_t* agent_adj;      /* [n_env, A, A] agent adjacency                              */
+} gm_obs_buffers;
+
+/* Per-env statistics of one step (src/env/routing.py:499-508), float64 [n_env, GM_INFO_FIELDS]. */
+enum {
+    GM_INFO_LOOPED = 0, GM_INFO_THROUGHPUT, GM_INFO_DROPPED, GM_INFO_BLOCKED,
+    GM_INFO_N_DELAYS, GM_INFO_SUM_DELAYS, GM_INFO_N_ARRIVED, GM_INFO_SUM_DELAYS_ARRIVED,
+    GM_INFO_SUM_SPR, GM_INFO_FIELDS
+};
+
+/* Optional per-packet step outputs for exact info lists (NULL to skip). */
+typedef struct {
+    int32_t* done_steps;    /* [n_env, A] agent steps of a packet that finished this step, else 0 */
+    int32_t* done_opt;      /* [n_env, A] max(shortest path weight, 1) of that packet             */
+    uint8_t* success;       /* [n_env, A] reached its target                                      */
+} gm_step_detail;
+
+typedef struct gm_env gm_env;
+
+const char* gm_last_error(void);
+int gm_version(void);
+
+int gm_env_create(const gm_env_config* cfg, const uint32_t* env_seeds /* host [n_env] */, gm_env** out);
+int gm_env_destroy(gm_env* env);
+int gm_env_dims(const gm_env* env, int32_t* n_env, int32_t* n_nodes, int32_t* n_data, int32_t* obs_dim,
+                int32_t* node_obs_dim);
+
+/* reset_mask: device uint8 [n_env] (NULL = every env). */
+int gm_env_reset(gm_env* env, const uint8_t* reset_mask, const gm_obs_buffers* obs, void* stream);
+/* actions: device int32 [n_env, A] in {0..3}; reward float32 [n_env, A]; done uint8 [n_env, A];
+ * info float64 [n_env, GM_INFO_FIELDS] (nullable); detail nullable; obs nullable. */
+int gm_env_step(gm_env* env, const int32_t* actions, float* reward, uint8_t* done, double* info,
+                const gm_step_detail* detail, const gm_obs_buffers* obs, void* stream);
+int gm_env_observe(gm_env* env, const gm_obs_buffers* obs, void* stream);
+/* nbr: int32 [n_env, N, 3] neighbour ids ascending (= order of actions 1..3);
+ * node_adj: int8 [n_env, N, N] (I + A); node_aux: float32 [n_env, N, N] APSP weights;
+ * topo_seed: int64 [n_env]. Any may be NULL. */
+int gm_env_topology(gm_env* env, int32_t* nbr, int8_t* node_adj, float* node_aux, int64_t* topo_seed,
+                    void* stream);
+/* Sum and count of non-zero agent steps per env (get_final_info), float64 [n_env, 2]. */
+int gm_env_final_info(gm_env* env, double* out, void* stream);
+
+/* Network.build_seed_list (src/env/network.py:100-120) on the device: `count` unique
+ * valid topology seeds from `init_seed` (EVAL_SEEDS = (20, 476, 1000)). out: host. */
+int gm_build_seed_list(int32_t n_nodes, int64_t init_seed, int32_t count, const int64_t* excluded,
+                       int32_t n_excluded, int32_t device, int64_t* out);
+
+/* ε-greedy action selection: q float32 [n_env, A, 4]; epsilon as the reference's
+ * float64; draws randint(4,size=A) then rand(A) from every env's stream. */
+int gm_policy_egreedy(gm_env* env, const float* q, double epsilon, int32_t* actions, void* stream);
+
+/* Host-side state export/import for parity tests (synchronous). Arrays are host
+ * pointers sized [n_env, ...]; any may be NULL. */
+typedef struct {
+    int32_t *now, *target, *edge, *time, *ttl, *start, *spw, *agent_steps; /* [n_env, A] */
+    double* size;                                                          /* [n_env, A] */
+    uint64_t* visited;                                                     /* [n_env, A, 2] */
+    uint8_t* amask;                                                        /* [n_env, A, 4] */
+    double* loads;                                                         /* [n_env, 3N/2] */
+    int64_t* topo_seed;                                                    /* [n_env] */
+    int32_t* topo_reps;                                                    /* [n_env] */
+    int32_t *edge_a, *edge_b, *edge_len;                                   /* [n_env, 3N/2] */
+    int32_t* nbr_edge;                                                     /* [n_env, N, 3] */
+    int32_t* apsp;                                                         /* [n_env, N, N] */
+    uint32_t* rng_key;   /* [n_env, 624] current MT block  */
+    int32_t* rng_pos;    /* [n_env]                          */
+} gm_env_state;
+int gm_env_get_state(gm_env* env, gm_env_state* st);
+
+/* ---- NetMon message passing (graphs of fixed max degree, ELL neighbour table) ----
+ * h: float32 [G*N, H] rows; nbr: int32 [G, N, deg] neighbour ids (-1 = none).
+ * out[n] = Σ over {n} ∪ nbr(n) in ascending node order (mode 0 = sum, 1 = mean). */
+int gm_mp_aggregate(const float* h, const int32_t* nbr, int32_t n_graphs, int32_t n_nodes, int32_t deg,
+                    int32_t hidden, int32_t mode, float* out, void* stream);
+/* Backward of gm_mp_aggregate for symmetric adjacency: dh[j] = Σ_{n ∈ {j} ∪ nbr(j)} dout[n] / cnt(n). */
+int gm_mp_aggregate_bwd(const float* dout, const int32_t* nbr, int32_t n_graphs, int32_t n_nodes, int32_t deg,
+                        int32_t hidden, int32_t mode, float* dh, void* stream);
+/* Readout (NetMon.forward with output_neighbor_hidden) fused with the agent gather:
+ * row r of graph g maps to node v = agent_node[g*R + r] (or v = r when agent_node is NULL, R = N);
+ * out[g*R + r] = [h_final[v], h_prev[nbr(v,0)], ..., h_prev[nbr(v,deg-1)]] (zeros for -1),
+ * written at out + (g*R + r) * out_stride (floats). */
+int gm_netmon_readout(const float* h_final, const float* h_prev, const int32_t* nbr, const int32_t* agent_node,
+                      int32_t n_graphs, int32_t n_nodes, int32_t n_rows, int32_t deg, int32_t hidden, float* out,
+                      int64_t out_stride, void* stream);
+int gm_netmon_readout_bwd(const float* dout, int64_t dout_stride, const int32_t* nbr, const int32_t* agent_node,
+                          int32_t n_graphs, int32_t n_nodes, int32_t n_rows, int32_t deg, int32_t hidden,
+                          float* dh_final, float* dh_prev, void* stream);
+/* LSTM gate math: gates [M, 4H] pre-activations (i,f,g,o, biases included), c [M, H]
+ * -> h_new, c_new [M, H]; saves sigmoid/tanh activations in act [M, 4H] if non-NULL. */
+int gm_lstm_pointwise(const float* gates, const float* c, int32_t m, int32_t hidden, float* h_new, float* c_new,
+                      float* act, void* stream);
+/* Backward: given dh_new, dc_new (nullable = 0), act, c, c_new -> dgates [M,4H], dc [M,H]. */
+int gm_lstm_pointwise_bwd(const float* dh_new, const float* dc_new, const float* act, const float* c,
+                          const float* c_new, int32_t m, int32_t hidden, float* dgates, float* dc, void* stream);
+/* Fused f32 MFMA linear layer: y[M,N] = act(x[M,K] @ w[N,K]^T + b[N]); row strides ldx, ldw
+ * (multiples of 4 floats, 16-byte aligned bases), ldy; K may be ragged; b nullable;
+ * act 0 = none, 1 = leaky_relu(0.01). */
+int gm_linear_f32(const float* x, int64_t ldx, const float* w, int64_t ldw, const float* b, int32_t m, int32_t n,
+                  int32_t k, int32_t act, float* y, int64_t ldy, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

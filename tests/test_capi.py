@@ -1,0 +1,56 @@
+"""CPU tests of the C-ABI boundary: the shared library loads and exports every
+entry point include/graph_marl_amd.h declares (no compute without a GPU)."""
+import ctypes
+import os
+import re
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "graph_marl_amd.h")
+
+
+def declared_functions():
+    txt = open(HEADER).read()
+    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    return set(re.findall(r"\b(gm_[a-z0-9_]+)\s*\(", txt))
+
+
+def test_header_and_binding_agree(gm):
+    assert declared_functions() == set(gm._lib.EXPORTS)
+
+
+def test_library_exports_every_declared_symbol(gm):
+    path = gm._lib.LIB_PATH
+    if not os.path.exists(path):
+        subprocess.check_call(["make", "-s", "-C", os.path.join(ROOT, "graph-marl_amd", "csrc")])
+    L = gm._lib.lib()
+    for name in declared_functions():
+        assert hasattr(L, name), name
+    out = subprocess.check_output(["nm", "-D", "--defined-only", path]).decode()
+    syms = set(re.findall(r"\bT (gm_[a-z0-9_]+)\b", out))
+    assert declared_functions() <= syms
+
+
+def test_error_path_without_device(gm):
+    """Invalid arguments are rejected before any device call, with a message."""
+    L = gm._lib.lib()
+    cfg = gm._lib.EnvConfig()
+    cfg.n_env, cfg.n_nodes, cfg.n_data, cfg.env_var = 1, 21, 20, 1  # odd node count
+    h = ctypes.c_void_p()
+    seeds = (ctypes.c_uint32 * 1)(0)
+    rc = L.gm_env_create(ctypes.byref(cfg), ctypes.cast(seeds, ctypes.c_void_p), ctypes.byref(h))
+    assert rc == -1
+    assert b"even" in L.gm_last_error()
+    rc = L.gm_linear_f32(None, 0, None, 0, None, 0, 0, 0, 0, None, 0, None)
+    assert rc == -1
+
+
+def test_product_refuses_cpu(gm):
+    import torch
+
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    with pytest.raises(gm._lib.GMError):
+        gm.Routing(gm.Network(20), n_env=2)

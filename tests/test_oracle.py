@@ -1,0 +1,139 @@
+"""CPU tests: pin the oracle against the reference's golden vectors.
+
+The golden files were produced by importing the reference (tests/golden/make_golden.py).
+"""
+import numpy as np
+import pytest
+
+import golden_replay as R
+import netmon_ref
+
+
+def test_mt19937_streams(oracle_mod):
+    g = np.load(f"{R.GOLDEN}/rng.npz")
+    for s in g["seeds"]:
+        s = int(s)
+        m = oracle_mod.MTStream(s)
+        np.testing.assert_array_equal(m.key, g[f"key_{s}"])
+        raw = np.array([m.next32() for _ in range(1500)], dtype=np.uint32)
+        np.testing.assert_array_equal(raw, g[f"raw_{s}"])
+        m = oracle_mod.MTStream(s)
+        mix = []
+        for _ in range(100):
+            mix += [m.randint(20), m.randint(20), m.random()]
+        np.testing.assert_array_equal(np.array(mix), g[f"packet20_{s}"])
+        m = oracle_mod.MTStream(s)
+        np.testing.assert_array_equal([m.randint(2**31 - 1) for _ in range(64)], g[f"randint31_{s}"])
+        m = oracle_mod.MTStream(s)
+        ns = [1, 2, 3, 5, 7, 10, 13, 20, 33, 50, 64, 100, 1000] * 20
+        np.testing.assert_array_equal([m.randint(n) for n in ns], g[f"randint_n_{s}"])
+        m = oracle_mod.MTStream(s)
+        eg = []
+        for _ in range(40):
+            eg.append([m.randint(4) for _ in range(20)])
+            eg.append([m.random() for _ in range(20)])
+        np.testing.assert_array_equal(np.array(eg, dtype=np.float64), g[f"egreedy_{s}"])
+
+
+def test_eval_seeds_are_the_generator_output(oracle_mod):
+    """EVAL_SEEDS (src/env/constants.py) = first 1000 valid seeds from init seed 476."""
+    ev = np.load(f"{R.GOLDEN}/eval_seeds.npy")
+    np.testing.assert_array_equal(oracle_mod.build_seed_list(20, 476, 1000), ev)
+
+
+def test_product_eval_seed_table_matches_reference():
+    import os
+
+    prod = np.load(os.path.join(R.GOLDEN, "..", "..", "graph-marl_amd", "data", "eval_seeds.npy"))
+    np.testing.assert_array_equal(prod, np.load(f"{R.GOLDEN}/eval_seeds.npy"))
+
+
+@pytest.mark.parametrize("n", [10, 20, 30, 40, 50, 100])
+def test_random_topologies(oracle_mod, n):
+    t = np.load(f"{R.GOLDEN}/topology.npz")
+    k = f"rand_n{n}"
+    cfg = oracle_mod.make_config(n, 1, topo_mode=oracle_mod.TOPO_RANDOM, excluded=R.EVAL_SEEDS)
+    m = oracle_mod.MTStream(int(t[k + "_main_seed"]))
+    for r in range(len(t[k + "_seed"])):
+        s, tp = oracle_mod.create_valid(cfg, m)
+        a = tp.arrays()
+        assert s == t[k + "_seed"][r]
+        assert a["repetitions"] == t[k + "_repetitions"][r]
+        for f in ["pos", "edges", "node_edges", "neighbors", "apsp"]:
+            np.testing.assert_array_equal(a[f], t[k + "_" + f][r], err_msg=f)
+    np.testing.assert_array_equal([m.next32() for _ in range(4)], t[k + "_post_raw"])
+
+
+def test_fixed_topologies_and_seed_lists(oracle_mod):
+    t = np.load(f"{R.GOLDEN}/topology.npz")
+    for s in t["fixed_seeds"]:
+        cfg = oracle_mod.make_config(20, 1, topo_mode=oracle_mod.TOPO_FIXED, topo_seed=int(s))
+        seed, tp = oracle_mod.create_valid(cfg, oracle_mod.MTStream(0))
+        a = tp.arrays()
+        assert seed == s
+        np.testing.assert_array_equal(a["edges"], t[f"fixed_{s}_edges"])
+        np.testing.assert_array_equal(a["apsp"], t[f"fixed_{s}_apsp"])
+    for key in [k for k in t.files if k.startswith("seedlist_")]:
+        _, n, i = key.split("_")
+        got = oracle_mod.build_seed_list(int(n[1:]), int(i[1:]), len(t[key]))
+        np.testing.assert_array_equal(got, t[key])
+
+
+class OracleAdapter:
+    def __init__(self, oracle_mod, cfg, spec):
+        O = oracle_mod
+        mode, seed, lst = spec
+        m = {"fixed": O.TOPO_FIXED, "random": O.TOPO_RANDOM, "list": O.TOPO_LIST,
+             "sequential": O.TOPO_SEQUENTIAL}[mode]
+        self.c = O.make_config(int(cfg["n"]), int(cfg["a"]), bool(cfg["cong"]), bool(cfg["mask"]), int(cfg["ttl"]),
+                               m, seed, seed_list=lst,
+                               excluded=R.EVAL_SEEDS if mode in ("random", "list") else None)
+        self.env = O.OracleEnv(self.c, int(cfg["seed"]))
+
+    def reset(self):
+        self.env.reset()
+
+    def egreedy(self, q, eps):
+        return self.env.draw_egreedy(q, eps)
+
+    def step(self, a):
+        return self.env.step(a)
+
+    def state(self):
+        return self.env.state()
+
+    def observe(self):
+        return self.env.observe()
+
+    def final_delays(self):
+        return self.env.final_delays()
+
+
+@pytest.mark.parametrize("path", R.env_golden_files(), ids=lambda p: p.split("/")[-1])
+def test_env_trace_bit_exact(oracle_mod, path):
+    n = R.replay(path, lambda cfg, spec: OracleAdapter(oracle_mod, cfg, spec))
+    assert n > 10
+
+
+def test_netmon_restatement_matches_reference():
+    g = np.load(f"{R.GOLDEN}/netmon.npz")
+    for vi, v in enumerate(g["variants"]):
+        rnn, agg, K = v.split("|")[:3]
+        W = netmon_ref.weights_from_npz(g, f"v{vi}_w_")
+        state = None
+        for t in range(3):
+            out, state = netmon_ref.netmon_forward(W, g["node_obs"][t], g["node_adj"][t], state, rnn, agg, int(K))
+            np.testing.assert_allclose(out, g[f"v{vi}_h_{t}"], atol=1e-5, rtol=0)
+            np.testing.assert_allclose(state, g[f"v{vi}_state_{t}"], atol=1e-5, rtol=0)
+            mapped = netmon_ref.to_network_obs(out, g["node_agent"][t])
+            np.testing.assert_allclose(mapped, g[f"v{vi}_mapped_{t}"], atol=1e-5, rtol=0)
+    W = netmon_ref.weights_from_npz(g, "dqn_w_")
+    np.testing.assert_allclose(netmon_ref.dqn_forward(W, g["dqn_obs"]), g["dqn_q"], atol=1e-5, rtol=0)
+
+
+def test_oracle_bench_driver_runs(oracle_mod):
+    cfg = oracle_mod.make_config(20, 20, topo_mode=oracle_mod.TOPO_RANDOM, excluded=R.EVAL_SEEDS)
+    sec, obs, nobs = oracle_mod.bench_rollout(cfg, 16, 60, 50, 2)
+    assert sec > 0 and obs.shape == (16, 20, 130) and nobs.shape == (16, 20, 88)
+    # every agent observation has exactly one "now" and one "target" one-hot
+    assert (obs[..., :20].sum(-1) == 1).all() and (obs[..., 20:40].sum(-1) == 1).all()
