@@ -1,0 +1,201 @@
+#!/usr/bin/env python3
+"""Benchmark: routing env-steps/s with NetMon on MI355X (BASELINE.json metric).
+
+One step = one vectorised rollout step over n_env graph instances on each GPU:
+DQN Q-values on the joint observation -> ε-greedy draws -> Routing.step ->
+NetMon step (encoder, LSTM obs cell, K x (aggregate + LSTM update), readout into
+the joint observation), plus the episode resets (new random topology + NetMon
+start-up) every --episode-steps steps, exactly like the reference's training
+rollout (src/main.py:667-748) with NetMonWrapper (src/env/wrapper.py).
+
+Multi-GPU: one process per GPU (torchrun), env shards with disjoint seeds, no
+collective on the rollout path (weak scaling); barrier + max-over-ranks timing.
+Rank 0 prints ONE JSON line.
+"""
+import argparse
+import importlib
+import json
+import os
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "env-steps/sec (routing, --netmon, 20-node graphs) at 1/2/4/8 MI355X"
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8 TB/s spec
+F32_MFMA_PEAK_TFS = 157.3  # MI355X_MICROARCH.md: f32-input MFMA dense peak
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=200)
+    p.add_argument("--warmup", type=int, default=20)
+    p.add_argument("--n-env", type=int, default=4096)
+    p.add_argument("--n-router", type=int, default=20)
+    p.add_argument("--n-data", type=int, default=20)
+    p.add_argument("--netmon-iterations", type=int, default=1)
+    p.add_argument("--episode-steps", type=int, default=50)
+    p.add_argument("--random-topology", type=int, default=1)
+    p.add_argument("--epsilon", type=float, default=0.5)
+    p.add_argument("--no-kernel-timers", action="store_true")
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--cpu-envs", type=int, default=256)
+    p.add_argument("--cpu-steps", type=int, default=20)
+    return p.parse_args()
+
+
+def kernel_cost(tag, n_env, N, A, E):
+    """(bound, algorithmic units per launch) for a timer tag — DESIGN.md §4."""
+    kind = tag.split(":")[0]
+    if kind == "linear":
+        m, n, k = (int(v) for v in tag.split(":")[2].split("x"))
+        return "mfma", 2.0 * m * n * k
+    if kind == "mp_aggregate":
+        rows, H = (int(v) for v in tag.split(":")[1].split("x"))
+        return "hbm", rows * H * 4 * 2 + rows * 3 * 4  # read h, write M, read nbr
+    if kind == "netmon_readout":
+        rows, w = (int(v) for v in tag.split(":")[1].split("x"))
+        return "hbm", rows * w * 4 * 2 + rows * 4  # gather-read + write + index
+    if kind == "lstm_pointwise":
+        rows, H = (int(v) for v in tag.split(":")[1].split("x"))
+        return "hbm", rows * H * 4 * (4 + 1 + 2)  # gates, c in; h, c out
+    if kind == "env_step":
+        # compact state (78A + 22E + 12N) + materialised fp32 obs
+        b_state = 78 * A + 22 * E + 12 * N
+        b_obs = 4 * A * (6 * N + 10) + 4 * N * (4 * N + 8)
+        return "hbm", float(n_env * (b_state + b_obs))
+    if kind == "egreedy":
+        return "hbm", float(n_env * A * (16 + 4 + 12))
+    return None, None
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(0)
+    dev = torch.device("cuda", torch.cuda.current_device())
+    gm = importlib.import_module("graph-marl_amd")
+    M = importlib.import_module("graph-marl_amd.model")
+    W = importlib.import_module("graph-marl_amd.wrapper")
+    P = importlib.import_module("graph-marl_amd.policy")
+    L = gm._lib
+
+    N, A, B, K = args.n_router, args.n_data, args.n_env, args.netmon_iterations
+    E = 3 * N // 2
+    net = gm.Network(N, random_topology=bool(args.random_topology), excluded_seeds=gm.EVAL_SEEDS,
+                     device=dev.index)
+    env = gm.Routing(net, A, n_env=B, seed=rank * B, obs_extra=512, agent_adjacency=False, device=dev.index)
+    torch.manual_seed(0)
+    netmon = M.NetMon(4 * N + 8, 128, [512, 256], K).to(dev)
+    dqn = M.DQN(6 * N + 10 + netmon.get_out_features(), [512, 256], 4).to(dev)
+    M.tag_modules(netmon, "netmon.")
+    M.tag_modules(dqn, "dqn.")
+    wenv = W.NetMonWrapper(env, netmon, 1)
+    policy = P.EpsilonGreedy(wenv, dqn, epsilon=args.epsilon, epsilon_decay=1.0, epsilon_update_freq=100,
+                             step_before_train=0)
+    state = {"ep": 0}
+
+    def step():
+        act = policy(wenv.obs)
+        wenv.step_(act)
+        state["ep"] += 1
+        if state["ep"] >= args.episode_steps:
+            wenv.reset()
+            state["ep"] = 0
+
+    with torch.no_grad():
+        wenv.reset()
+        for _ in range(args.warmup):
+            step()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        if not args.no_kernel_timers:
+            L.PROF = {}
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            step()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        elapsed = time.perf_counter() - t0
+        prof, L.PROF = L.PROF, None
+    el = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(el, op=dist.ReduceOp.MAX)
+    elapsed = float(el.item())
+    total = B * world * args.steps
+    value = total / elapsed
+
+    kernels = {}
+    if prof:
+        for tag, evs in prof.items():
+            ts = [s.elapsed_time(e) for s, e in evs]
+            kernels[tag] = {"launches": len(ts), "avg_us": 1e3 * sum(ts) / len(ts), "total_ms": sum(ts)}
+    roof = None
+    if kernels:
+        dom = max(kernels, key=lambda k: kernels[k]["total_ms"])
+        bound, units = kernel_cost(dom, B, N, A, E)
+        sec = kernels[dom]["avg_us"] * 1e-6
+        if bound == "mfma":
+            ach = units / sec / 1e12
+            roof = {"kernel": dom, "bound": "mfma", "achieved": round(ach, 2), "peak": F32_MFMA_PEAK_TFS,
+                    "unit": "TFLOP/s", "frac": round(ach / F32_MFMA_PEAK_TFS, 4), "traffic": None}
+        else:
+            ach = units / sec / 1e9
+            roof = {"kernel": dom, "bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None}
+        for tag, kv in kernels.items():
+            bound, units = kernel_cost(tag, B, N, A, E)
+            if bound:
+                s = kv["avg_us"] * 1e-6
+                kv["achieved"] = round(units / s / (1e12 if bound == "mfma" else 1e9), 2)
+                kv["unit"] = "TFLOP/s" if bound == "mfma" else "GB/s"
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        try:
+            sys.path.insert(0, os.path.join(ROOT, "oracle"))
+            import cpu_baseline
+
+            threads = int(os.environ.get("OMP_NUM_THREADS", str(min(16, os.cpu_count() or 1))))
+            v, dt = cpu_baseline.measure(args.cpu_envs, args.cpu_steps, threads, K=K,
+                                         episode_steps=args.episode_steps)
+            cpu = {"value": round(v, 1), "unit": "env-steps/s", "cores": threads, "kind": "port",
+                   "sample": f"{args.cpu_envs} envs x {args.cpu_steps} steps ({dt:.1f} s): C oracle env (OpenMP) "
+                             f"+ NumPy fp32 NetMon(K={K}) + DQN eps-greedy, same shapes"}
+        except Exception as ex:  # the baseline must never break the GPU line
+            cpu = {"value": None, "error": repr(ex)[:200]}
+
+    if rank == 0:
+        line = {
+            "metric": METRIC, "value": round(value, 1), "unit": "env-steps/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(1e3 * elapsed / args.steps, 4),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+            "data": "synthetic: random-init NetMon+DQN weights, on-device random topologies and packets",
+            "config": {"workload": f"routing rollout --netmon (NetMon K={K}, H=128, enc 512,256, lstm, sum) + "
+                                   f"DQN 512,256 eps-greedy, {'random' if args.random_topology else 'fixed'} "
+                                   f"{N}-node topologies, episode {args.episode_steps} steps",
+                       "n_env_per_gpu": B, "n_nodes": N, "n_data": A, "netmon_iterations": K,
+                       "parallelism": f"dp{world} (env shards, no rollout collective)"},
+            "roofline": roof, "cpu_baseline": cpu, "kernels": kernels,
+        }
+        print(json.dumps(line))
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

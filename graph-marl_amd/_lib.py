@@ -110,3 +110,31 @@ def stream_ptr(device=None):
 def require_gpu():
     if not torch.cuda.is_available():
         raise GMError("graph-marl_amd needs a ROCm GPU (torch.cuda.is_available() is False); there is no CPU path")
+
+
+# ---------------------------------------------------------------------------
+# Optional per-kernel timing (bench.py): when PROF is a dict, every wrapped launch
+# records a pair of HIP events on the launch stream under its tag.
+# ---------------------------------------------------------------------------
+PROF = None
+
+
+class timed:
+    __slots__ = ("tag", "s")
+
+    def __init__(self, tag):
+        self.tag = tag
+        self.s = None
+
+    def __enter__(self):
+        if PROF is not None and self.tag:
+            self.s = torch.cuda.Event(enable_timing=True)
+            self.s.record()
+        return self
+
+    def __exit__(self, *exc):
+        if self.s is not None:
+            e = torch.cuda.Event(enable_timing=True)
+            e.record()
+            PROF.setdefault(self.tag, []).append((self.s, e))
+        return False

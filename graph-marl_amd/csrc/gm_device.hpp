@@ -123,11 +123,13 @@ struct MainRng {
         __syncthreads();
         has_next = 1;
     }
+    // pos == 624 without a generated next block means "twist before the next draw"
+    // (a freshly seeded numpy stream); only a generated next block can be entered.
     __device__ void commit() {
         pos += k;
         n = 0;
         k = 0;
-        if (pos >= MT_N) {
+        if (pos >= MT_N && has_next) {
             pos -= MT_N;
             cur = 1 - cur;
             has_next = 0;
@@ -157,8 +159,9 @@ struct MainRng {
         uint32_t rng = (uint32_t)(high - 1);
         if (rng == 0) return 0;
         uint32_t m = mask_for(rng), v;
-        while ((v = (next32() & m)) > rng) {
-        }
+        // acceptance >= 1/2 per draw: 4096 rejections in a row means a broken stream
+        for (int guard = 0; (v = (next32() & m)) > rng; guard++)
+            if (guard > 4096) return 0;
         return (int64_t)v;
     }
     __device__ __forceinline__ double random() {
@@ -186,8 +189,8 @@ struct LocalRng {
         uint32_t rng = (uint32_t)(high - 1);
         if (rng == 0) return 0;
         uint32_t m = mask_for(rng), v;
-        while ((v = (next32() & m)) > rng) {
-        }
+        for (int guard = 0; (v = (next32() & m)) > rng; guard++)
+            if (guard > 4096) return 0;
         return (int64_t)v;
     }
 };

@@ -253,7 +253,7 @@ __device__ __forceinline__ bool is_excluded(const EnvDev& d, int64_t sd) {
 template <class R>
 __device__ int64_t draw_topology_seed(const EnvDev& d, R& r) {  // network.py:230-232, 252-254
     int64_t sd = r.randint(2147483647LL);
-    while (d.n_excl > 0 && is_excluded(d, sd)) sd = r.randint(2147483647LL);
+    for (int guard = 0; d.n_excl > 0 && is_excluded(d, sd) && guard < 4096; guard++) sd = r.randint(2147483647LL);
     return sd;
 }
 
@@ -807,11 +807,20 @@ __global__ void k_final_info(EnvDev d, double* out) {
 // src/env/network.py:100-120 build_seed_list: main stream seeded with the init seed;
 // each candidate seed is a main-stream draw (exclusions re-drawn), its topology chain
 // (reseeding on invalid graphs) gives the final seed; unique seeds in order.
+constexpr int MAX_SEED_LIST = 4096;
+
 __global__ __launch_bounds__(64) void k_build_seed_list(EnvDev d, int count, int64_t* out) {
     __shared__ ResetLds S;
+    __shared__ int64_t found[MAX_SEED_LIST];
     MainRng r = open_rng(d, 0, S.env);
     int have = 0;
-    while (have < count) {
+    // duplicates are rare (2^31 seeds); a bounded candidate budget keeps a broken
+    // stream from spinning forever
+    for (int cands = 0; have < count; cands++) {
+        if (cands > 64 * count + 1024) {
+            if (lane_id() == 0) atomicExch(d.err, GM_ERR_TOPOLOGY);
+            break;
+        }
         int64_t cand = draw_topology_seed(d, r);
         r.commit();
         LocalRng tr;
@@ -827,14 +836,15 @@ __global__ __launch_bounds__(64) void k_build_seed_list(EnvDev d, int count, int
             tr.seed((uint32_t)seed);
         }
         bool dup = false;
-        for (int i = 0; i < have; i++) dup |= out[i] == seed;
+        for (int i = 0; i < have; i++) dup |= found[i] == seed;
         __syncthreads();
         if (!dup) {
-            if (lane_id() == 0) out[have] = seed;
+            if (lane_id() == 0) found[have] = seed;
             have++;
         }
         __syncthreads();
     }
+    for (int i = lane_id(); i < have; i += WAVE) out[i] = found[i];
     close_rng(d, 0, r);
 }
 
@@ -1039,7 +1049,8 @@ extern "C" int gm_policy_egreedy(gm_env* env, const float* q, double epsilon, in
 
 extern "C" int gm_build_seed_list(int32_t n_nodes, int64_t init_seed, int32_t count, const int64_t* excluded,
                                   int32_t n_excluded, int32_t device, int64_t* out) {
-    if (!out || count <= 0) return gm_fail(GM_ERR_INVALID_ARG, "gm_build_seed_list: bad arguments");
+    if (!out || count <= 0 || count > 4096)
+        return gm_fail(GM_ERR_INVALID_ARG, "gm_build_seed_list: count must be in [1, 4096]");
     gm_env_config c;
     memset(&c, 0, sizeof(c));
     c.n_env = 1;
@@ -1064,6 +1075,9 @@ extern "C" int gm_build_seed_list(int32_t n_nodes, int64_t init_seed, int32_t co
     if (rc == GM_OK) {
         hipError_t e = hipMemcpy(out, dout, (size_t)count * sizeof(int64_t), hipMemcpyDeviceToHost);
         if (e != hipSuccess) rc = gm_fail(GM_ERR_HIP, std::string("gm_build_seed_list: ") + hipGetErrorString(e));
+        int32_t err = 0;
+        if (rc == GM_OK && hipMemcpy(&err, env->d.err, sizeof(err), hipMemcpyDeviceToHost) == hipSuccess && err)
+            rc = gm_fail(GM_ERR_TOPOLOGY, "gm_build_seed_list: candidate budget exhausted");
     }
     gm_env_destroy(env);
     return rc;

@@ -48,7 +48,7 @@ class _WeightCache:
         return self.val, kp
 
 
-def linear_raw(x2d, ldx, k, w, b, act, out=None, ldy=None, wcache=None):
+def linear_raw(x2d, ldx, k, w, b, act, out=None, ldy=None, wcache=None, tag=None):
     """y = act(x @ w^T + b) on the MFMA kernel. x2d: row-major rows with stride ldx."""
     m = x2d.shape[0]
     n = w.shape[0]
@@ -56,7 +56,9 @@ def linear_raw(x2d, ldx, k, w, b, act, out=None, ldy=None, wcache=None):
     if out is None:
         out = torch.empty(m, n, device=x2d.device, dtype=torch.float32)
         ldy = n
-    L.check(L.lib().gm_linear_f32(L.ptr(x2d), ldx, L.ptr(wp), ldw, L.ptr(b), m, n, k, act, L.ptr(out), ldy, _s()))
+    with L.timed(tag and f"linear:{tag}:{m}x{n}x{k}"):
+        L.check(L.lib().gm_linear_f32(L.ptr(x2d), ldx, L.ptr(wp), ldw, L.ptr(b), m, n, k, act, L.ptr(out), ldy,
+                                      _s()))
     return out
 
 
@@ -72,9 +74,9 @@ def _as_rows(x):
 
 class LinearFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, w, b, act, wcache):
+    def forward(ctx, x, w, b, act, wcache, tag=None):
         x2, ldx, k = _as_rows(x)
-        y = linear_raw(x2, ldx, k, w, b, act, wcache=wcache)
+        y = linear_raw(x2, ldx, k, w, b, act, wcache=wcache, tag=tag)
         ctx.act = act
         ctx.save_for_backward(x2[:, :k] if x2.shape[1] != k else x2, w, y)
         return y.reshape(*x.shape[:-1], w.shape[0])
@@ -90,7 +92,7 @@ class LinearFn(torch.autograd.Function):
         gb = gy.sum(0) if ctx.needs_input_grad[2] else None
         if gx is not None:
             gx = gx.reshape(*ctx.saved_tensors[0].shape[:-1], w.shape[1])
-        return gx, gw, gb, None, None
+        return gx, gw, gb, None, None, None
 
 
 class Linear(nn.Linear):
@@ -100,12 +102,13 @@ class Linear(nn.Linear):
         super().__init__(in_features, out_features, bias)
         self.act = act
         self._wc = _WeightCache()
+        self.tag = None
 
     def forward(self, x):
         if x.shape[-1] != self.in_features:
             raise ValueError(f"Linear expects {self.in_features} features, got {x.shape[-1]}")
         lead = x.shape[:-1]
-        y = LinearFn.apply(x.reshape(-1, x.shape[-1]), self.weight, self.bias, self.act, self._wc)
+        y = LinearFn.apply(x.reshape(-1, x.shape[-1]), self.weight, self.bias, self.act, self._wc, self.tag)
         return y.reshape(*lead, self.out_features)
 
 
@@ -134,7 +137,8 @@ class MLP(nn.Module):
         h, ld, kk = x2d, ldx, k
         for i, lin in enumerate(self.linear_layers):
             out = scratch(i, x2d.shape[0], lin.out_features)
-            linear_raw(h, ld, kk, lin.weight, lin.bias, lin.act, out=out, ldy=out.stride(0), wcache=lin._wc)
+            linear_raw(h, ld, kk, lin.weight, lin.bias, lin.act, out=out, ldy=out.stride(0), wcache=lin._wc,
+                       tag=lin.tag)
             h, ld, kk = out, out.stride(0), lin.out_features
         return h
 
@@ -145,7 +149,8 @@ class _Aggregate(torch.autograd.Function):
         G, N, deg = nbr.shape
         H = h.shape[-1]
         out = torch.empty_like(h)
-        L.check(L.lib().gm_mp_aggregate(L.ptr(h), L.ptr(nbr), G, N, deg, H, mode, L.ptr(out), _s()))
+        with L.timed(f"mp_aggregate:{G * N}x{H}"):
+            L.check(L.lib().gm_mp_aggregate(L.ptr(h), L.ptr(nbr), G, N, deg, H, mode, L.ptr(out), _s()))
         ctx.save_for_backward(nbr)
         ctx.mode = mode
         return out
@@ -178,8 +183,9 @@ class _Readout(torch.autograd.Function):
             res = None
             dst = out.view(-1, out.shape[-1])[:, col0:]
             stride = out.shape[-1]
-        L.check(L.lib().gm_netmon_readout(L.ptr(hf), L.ptr(hp), L.ptr(nbr), L.ptr(agent_node), G, N, R, deg, H,
-                                          L.ptr(dst), stride, _s()))
+        with L.timed(f"netmon_readout:{G * R}x{(deg + 1) * H}"):
+            L.check(L.lib().gm_netmon_readout(L.ptr(hf), L.ptr(hp), L.ptr(nbr), L.ptr(agent_node), G, N, R, deg, H,
+                                              L.ptr(dst), stride, _s()))
         ctx.save_for_backward(nbr, agent_node if agent_node is not None else torch.empty(0))
         ctx.has_map = agent_node is not None
         ctx.H = H
@@ -213,9 +219,10 @@ class _LSTMPointwise(torch.autograd.Function):
         H = H4 // 4
         h1 = torch.empty(M, H, device=gates.device)
         c1 = torch.empty(M, H, device=gates.device)
-        need = torch.is_grad_enabled() and (gates.requires_grad or c.requires_grad)
+        need = ctx.needs_input_grad[0] or ctx.needs_input_grad[1]
         act = torch.empty_like(gates) if need else None
-        L.check(L.lib().gm_lstm_pointwise(L.ptr(gates), L.ptr(c), M, H, L.ptr(h1), L.ptr(c1), L.ptr(act), _s()))
+        with L.timed(f"lstm_pointwise:{M}x{H}"):
+            L.check(L.lib().gm_lstm_pointwise(L.ptr(gates), L.ptr(c), M, H, L.ptr(h1), L.ptr(c1), L.ptr(act), _s()))
         if need:
             ctx.save_for_backward(act, c, c1)
         return h1, c1
@@ -248,6 +255,7 @@ class LSTMCell(nn.Module):
         for p in self.parameters():
             nn.init.uniform_(p, -stdv, stdv)
         self._wc = _WeightCache()
+        self.tag = None
 
     def forward(self, x, state):
         h, c = state
@@ -255,9 +263,9 @@ class LSTMCell(nn.Module):
         w = torch.cat([self.weight_ih, self.weight_hh], 1)
         b = self.bias_ih + self.bias_hh
         if torch.is_grad_enabled() and (w.requires_grad or xh.requires_grad):
-            gates = LinearFn.apply(xh, w, b, 0, None)
+            gates = LinearFn.apply(xh, w, b, 0, None, self.tag)
         else:
-            gates = linear_raw(xh, xh.stride(0), xh.shape[1], w, b, 0)
+            gates = linear_raw(xh, xh.stride(0), xh.shape[1], w, b, 0, tag=self.tag)
         return _LSTMPointwise.apply(gates, c.contiguous())
 
 
@@ -450,4 +458,11 @@ class DQN(nn.Module):
         h = self.encoder.forward_into(x2d, ldx, k, scratch)
         out = scratch(len(self.encoder.linear_layers), x2d.shape[0], self.q_net.fc.out_features)
         return linear_raw(h, h.stride(0), h.shape[1], self.q_net.fc.weight, self.q_net.fc.bias, 0, out=out,
-                          ldy=out.stride(0), wcache=self.q_net.fc._wc)
+                          ldy=out.stride(0), wcache=self.q_net.fc._wc, tag=self.q_net.fc.tag)
+
+
+def tag_modules(root, prefix=""):
+    """Name every Linear/LSTMCell by its module path (kernel timer tags)."""
+    for name, m in root.named_modules():
+        if isinstance(m, (Linear, LSTMCell)):
+            m.tag = prefix + name

@@ -46,8 +46,9 @@ class EpsilonGreedy:
     def select(self, q):
         """ε-greedy mix of argmax(q) and uniform actions, drawn from each env's stream."""
         e = self._env
-        L.check(L.lib().gm_policy_egreedy(e._h, L.ptr(q), float(self._epsilon), L.ptr(self.actions),
-                                          L.stream_ptr(e.device)))
+        with L.timed("egreedy"):
+            L.check(L.lib().gm_policy_egreedy(e._h, L.ptr(q), float(self._epsilon), L.ptr(self.actions),
+                                              L.stream_ptr(e.device)))
         return self.actions
 
     def __call__(self, obs, adj=None):

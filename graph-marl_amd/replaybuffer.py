@@ -1,0 +1,111 @@
+"""Device-resident replay memory for n_env parallel envs (reference
+src/replaybuffer.py:34-287 ReplayBuffer).
+
+Differences from the reference, by design:
+  * one ring slot = one vector step = n_env transitions, all tensors stay in HBM
+    (the reference copies 17 host arrays to the device per sampled step);
+  * the 4H NetMon part of the agent observation is not stored: the update re-runs
+    NetMon over the sampled sequence and overwrites it anyway (src/main.py:865-880,
+    909-915); the graph is stored as its neighbour table and the node-agent matrix
+    as the agent -> node index, the NetMon input state as in the reference
+    (the state *before* the NetMon call that produced obs, wrapper.py:99-104);
+  * sampling draws from a torch device generator seeded with `seed` — uniform like
+    the reference's np.random.default_rng(seed).choice, but a different stream
+    (sampling indices are not part of the parity contract).
+"""
+from collections import namedtuple
+
+import torch
+
+TransitionBatch = namedtuple(
+    "TransitionBatch",
+    ["idx", "obs", "action", "reward", "next_obs", "done", "episode_done", "node_obs", "nbr", "node_state",
+     "agent_node", "next_node_obs", "next_agent_node"],
+)
+
+
+class ReplayBuffer:
+    def __init__(self, seed, capacity, n_env, n_agents, obs_dim, n_nodes, node_obs_dim, node_state_size,
+                 device, half_precision=False):
+        """capacity: transitions (env-steps) like the reference; the ring holds
+        ceil(capacity / n_env) vector steps."""
+        self.n_env, self.A, self.N = n_env, n_agents, n_nodes
+        self.slots = max(1, -(-int(capacity) // n_env))
+        self.capacity = self.slots * n_env
+        self.count = 0  # filled slots
+        self.index = 0  # next slot
+        self.device = device
+        ft = torch.float16 if half_precision else torch.float32
+        S, B, A, N = self.slots, n_env, n_agents, n_nodes
+
+        def z(*shape, dtype=ft):
+            return torch.zeros(*shape, dtype=dtype, device=device)
+
+        self.obs = z(S, B, A, obs_dim)
+        self.next_obs = z(S, B, A, obs_dim)
+        self.action = z(S, B, A, dtype=torch.int8)
+        self.reward = z(S, B, A)
+        self.done = z(S, B, A, dtype=torch.bool)
+        self.episode_done = z(S, dtype=torch.bool)
+        self.node_obs = z(S, B, N, node_obs_dim)
+        self.next_node_obs = z(S, B, N, node_obs_dim)
+        self.nbr = z(S, B, N, 3, dtype=torch.int8)
+        self.agent_node = z(S, B, A, dtype=torch.int8)
+        self.next_agent_node = z(S, B, A, dtype=torch.int8)
+        self.node_state = z(S, B, N, node_state_size)
+        self.gen = torch.Generator(device=device)
+        self.gen.manual_seed(seed)
+
+    def nbytes(self):
+        return sum(t.numel() * t.element_size() for t in self.__dict__.values() if torch.is_tensor(t))
+
+    def add(self, obs, action, reward, next_obs, done, episode_done, node_state, node_obs, nbr, agent_node,
+            next_node_obs, next_agent_node):
+        """One vector step (every argument has a leading n_env dim; node_state may be None = zeros)."""
+        i = self.index
+        self.obs[i].copy_(obs)
+        self.action[i].copy_(action)
+        self.reward[i].copy_(reward)
+        self.next_obs[i].copy_(next_obs)
+        self.done[i].copy_(done)
+        self.episode_done[i] = bool(episode_done)
+        if node_state is None:
+            self.node_state[i].zero_()
+        else:
+            self.node_state[i].copy_(node_state)
+        self.node_obs[i].copy_(node_obs)
+        self.nbr[i].copy_(nbr)
+        self.agent_node[i].copy_(agent_node)
+        self.next_node_obs[i].copy_(next_node_obs)
+        self.next_agent_node[i].copy_(next_agent_node)
+        if self.count < self.slots:
+            self.count += 1
+        self.index = (self.index + 1) % self.slots
+
+    def _gather(self, slot, env):
+        f = torch.float32
+        return TransitionBatch(
+            (slot, env), self.obs[slot, env].to(f), self.action[slot, env].long(), self.reward[slot, env].to(f),
+            self.next_obs[slot, env].to(f), self.done[slot, env], self.episode_done[slot],
+            self.node_obs[slot, env].to(f), self.nbr[slot, env].int().contiguous(),
+            self.node_state[slot, env].to(f), self.agent_node[slot, env].int().contiguous(),
+            self.next_node_obs[slot, env].to(f), self.next_agent_node[slot, env].int().contiguous(),
+        )
+
+    def get_batch(self, batch_size, sequence_length=1):
+        """Yields sequence_length TransitionBatches of batch_size transitions
+        (src/replaybuffer.py:103-130): uniform env and start slot; sequences are
+        consecutive slots of one env, starting from the oldest slot and wrapping."""
+        dev = self.device
+        env = torch.randint(0, self.n_env, (batch_size,), device=dev, generator=self.gen)
+        if sequence_length <= 1:
+            slot = torch.randint(0, self.count, (batch_size,), device=dev, generator=self.gen)
+            yield self._gather(slot, env)
+            return
+        if self.count <= sequence_length:
+            raise ValueError("not enough transitions for the requested sequence length")
+        start = self.index % self.count
+        off = torch.randint(0, self.count - sequence_length, (batch_size,), device=dev, generator=self.gen)
+        first = (start + off) % self.count
+        for o in range(sequence_length):
+            yield self._gather((first + o) % self.count, env)

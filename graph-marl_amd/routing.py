@@ -193,7 +193,8 @@ class Routing:
     def reset_(self, mask=None):
         """Reset envs in place (mask: bool/uint8 [n_env] on device, None = all)."""
         m = None if mask is None else mask.to(torch.uint8)
-        L.check(L.lib().gm_env_reset(self._h, L.ptr(m), C.byref(self._obsbufs), self._stream()))
+        with L.timed("env_reset"):
+            L.check(L.lib().gm_env_reset(self._h, L.ptr(m), C.byref(self._obsbufs), self._stream()))
         L.check(L.lib().gm_env_topology(self._h, L.ptr(self.nbr), None, None, None, self._stream()))
 
     def reset(self):
@@ -213,9 +214,10 @@ class Routing:
             det.done_steps, det.done_opt, det.success = (detail["done_steps"].data_ptr(),
                                                          detail["done_opt"].data_ptr(),
                                                          detail["success"].data_ptr())
-        L.check(L.lib().gm_env_step(self._h, L.ptr(a), L.ptr(self.reward), L.ptr(self.done), L.ptr(self.info),
-                                    None if det is None else C.byref(det), C.byref(self._obsbufs),
-                                    self._stream()))
+        with L.timed("env_step"):
+            L.check(L.lib().gm_env_step(self._h, L.ptr(a), L.ptr(self.reward), L.ptr(self.done), L.ptr(self.info),
+                                        None if det is None else C.byref(det), C.byref(self._obsbufs),
+                                        self._stream()))
 
     def step(self, act):
         """Routing.step (routing.py:360-520) -> (obs, adj, reward, done, info) with a

@@ -1,0 +1,104 @@
+"""DQN + NetMon update on the device (reference src/main.py:819-1026) and the
+data-parallel gradient exchange across GPUs.
+
+Per update: for each step of the sampled sequence, NetMon re-runs with gradient
+from the stored input state (reset on episode boundaries), its readout replaces
+the graph part of the observation, the online DQN gives Q, the target DQN (online
+NetMon, no grad) gives max Q of the next observation, the TD target is written
+into the chosen action only (loss over all 4 actions, unchosen terms 0), loss
+averaged over the sequence; then clip_grad_value(0.5), clip_grad_norm(1.0),
+AdamW, soft target update. With world_size > 1 the gradients of all parameters
+are averaged in ONE flattened RCCL all-reduce before clipping, so every rank
+clips and steps on the global gradient and the replicas stay identical.
+"""
+import torch
+import torch.distributed as dist
+
+
+def allreduce_gradients(params, group=None):
+    """Average .grad over the process group with one bucketed all-reduce."""
+    if not dist.is_available() or not dist.is_initialized() or dist.get_world_size(group) == 1:
+        return
+    grads = [p.grad for p in params if p.grad is not None]
+    if not grads:
+        return
+    flat = torch.cat([g.reshape(-1) for g in grads])
+    dist.all_reduce(flat, group=group)
+    flat.div_(dist.get_world_size(group))
+    off = 0
+    for g in grads:
+        n = g.numel()
+        g.copy_(flat[off:off + n].view_as(g))
+        off += n
+
+
+def shard_seeds(rank, world, n_env, base=0):
+    """Per-env numpy-legacy seeds of one rank's env shard: disjoint across ranks."""
+    return [(base + rank * n_env + i) & 0xFFFFFFFF for i in range(n_env)]
+
+
+def broadcast_parameters(modules, src=0, group=None):
+    if not dist.is_available() or not dist.is_initialized() or dist.get_world_size(group) == 1:
+        return
+    for m in modules:
+        for t in list(m.parameters()) + list(m.buffers()):
+            dist.broadcast(t.data, src=src, group=group)
+
+
+@torch.no_grad()
+def interpolate_model(a, b, a_weight, target):
+    """src/util.py:8-23: target <- a_weight * a + (1 - a_weight) * b (all state entries)."""
+    sa, sb, st = a.state_dict(), b.state_dict(), target.state_dict()
+    for k in sa:
+        st[k].copy_(a_weight * sa[k] + (1 - a_weight) * sb[k])
+
+
+def joint_obs(env_obs, network_obs):
+    return torch.cat([env_obs, network_obs], -1)
+
+
+def dqn_loss(netmon, model, model_tar, batches, gamma):
+    """Sequence loss of src/main.py:840-954 (no DGN attention / aux terms).
+    Returns (loss, list of q, list of q_target)."""
+    L = len(batches)
+    loss_q = None
+    qs, qts = [], []
+    last_state = last_ep_done = None
+    for t, batch in enumerate(batches):
+        if t == 0:
+            netmon.state = batch.node_state
+        else:
+            netmon.state = last_state * (~last_ep_done).view(-1, 1, 1)
+        network_obs = netmon.forward_graph(batch.node_obs, batch.nbr, batch.agent_node)
+        obs = joint_obs(batch.obs, network_obs)
+        last_state = netmon.state
+        last_ep_done = batch.episode_done.expand(batch.obs.shape[0]) if batch.episode_done.dim() == 0 \
+            else batch.episode_done
+        q = model(obs)
+        with torch.no_grad():
+            nno = netmon.forward_graph(batch.next_node_obs, batch.nbr, batch.next_agent_node)
+            next_q = model_tar(joint_obs(batch.next_obs, nno))
+            next_q_max = next_q.max(dim=2)[0]
+        target = batch.reward + (~batch.done) * gamma * next_q_max
+        q_target = torch.scatter(q.detach(), -1, batch.action.unsqueeze(-1), target.unsqueeze(-1))
+        term = torch.mean((q - q_target).pow(2)) / L
+        loss_q = term if loss_q is None else loss_q + term
+        qs.append(q)
+        qts.append(q_target)
+    return loss_q, qs, qts
+
+
+def dqn_update(netmon, model, model_tar, optimizer, params, batches, gamma, tau, target_update_steps=0,
+               iteration=1, group=None):
+    loss, qs, qts = dqn_loss(netmon, model, model_tar, batches, gamma)
+    optimizer.zero_grad(set_to_none=False)
+    loss.backward()
+    allreduce_gradients(params, group)
+    torch.nn.utils.clip_grad_value_(params, 0.5)
+    torch.nn.utils.clip_grad_norm_(params, 1.0)
+    optimizer.step()
+    if target_update_steps <= 0:
+        interpolate_model(model, model_tar, tau, model_tar)
+    elif iteration % target_update_steps == 0:
+        model_tar.load_state_dict(model.state_dict())
+    return loss.detach(), qs, qts

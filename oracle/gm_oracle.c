@@ -539,3 +539,40 @@ double gmo_bench_rollout(const gmo_config* c, int32_t n_env, int32_t steps, int3
     free(envs);
     return (double)(t1.tv_sec - t0.tv_sec) + 1e-9 * (double)(t1.tv_nsec - t0.tv_nsec);
 }
+
+/* ---------------------------------------------------------------------------
+ * Batched driver for the CPU baseline (bench.py cpu_baseline leg): n_env
+ * independent envs stepped with OpenMP; observations written to flat arrays.
+ * ------------------------------------------------------------------------- */
+gmo_env* gmo_batch_create(const gmo_config* c, int32_t n_env, uint32_t seed_base) {
+    gmo_env* envs = (gmo_env*)malloc(sizeof(gmo_env) * (size_t)n_env);
+#pragma omp parallel for schedule(static)
+    for (int b = 0; b < n_env; b++) gmo_env_init(&envs[b], c, seed_base + (uint32_t)b);
+    return envs;
+}
+
+void gmo_batch_free(gmo_env* envs) { free(envs); }
+
+void gmo_batch_run(gmo_env* envs, int32_t n_env, int32_t do_reset, const int32_t* act, float* reward, uint8_t* done,
+                   float* obs, int64_t obs_stride, float* node_obs, int32_t* agent_node, int32_t* nbr) {
+    int A = envs[0].cfg.n_data, n = envs[0].cfg.n_nodes;
+    int D = gmo_obs_dim(n), ND = gmo_node_obs_dim(n);
+#pragma omp parallel for schedule(static)
+    for (int b = 0; b < n_env; b++) {
+        gmo_env* e = &envs[b];
+        if (do_reset) {
+            gmo_env_reset(e);
+        } else {
+            gmo_info info;
+            gmo_env_step(e, act + (size_t)b * A, reward + (size_t)b * A, done + (size_t)b * A, &info);
+        }
+        float tmp[GMO_MAXA * (6 * GMO_MAXN + 10)];
+        gmo_env_observe(e, tmp, node_obs + (size_t)b * n * ND, NULL, NULL, NULL);
+        for (int a = 0; a < A; a++) {
+            memcpy(obs + ((size_t)b * A + a) * obs_stride, tmp + (size_t)a * D, sizeof(float) * D);
+            agent_node[(size_t)b * A + a] = e->now[a];
+        }
+        for (int j = 0; j < n; j++)
+            for (int k = 0; k < 3; k++) nbr[((size_t)b * n + j) * 3 + k] = e->topo.nbr[j][k];
+    }
+}

@@ -97,4 +97,9 @@ size_t gmo_env_sizeof(void);
  * actions (action tape from a splitmix stream), OpenMP over envs. Returns seconds. */
 double gmo_bench_rollout(const gmo_config* c, int32_t n_env, int32_t steps, int32_t episode_steps,
                          int32_t n_threads, float* obs_out, float* node_obs_out);
+/* batched CPU-baseline driver (OpenMP over envs) */
+gmo_env* gmo_batch_create(const gmo_config* c, int32_t n_env, uint32_t seed_base);
+void gmo_batch_free(gmo_env* envs);
+void gmo_batch_run(gmo_env* envs, int32_t n_env, int32_t do_reset, const int32_t* act, float* reward, uint8_t* done,
+                   float* obs, int64_t obs_stride, float* node_obs, int32_t* agent_node, int32_t* nbr);
 #endif

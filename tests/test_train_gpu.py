@@ -1,0 +1,115 @@
+"""GPU parity of one DQN + NetMon update (src/main.py:832-1022) against the
+reference's golden update: loss, raw and clipped gradients, AdamW step, soft
+target update — and the device replay buffer's sequence sampling semantics."""
+import importlib
+
+import numpy as np
+import pytest
+import torch
+
+import golden_replay as R
+
+pytestmark = pytest.mark.gpu
+
+
+def mods():
+    return (importlib.import_module("graph-marl_amd.model"), importlib.import_module("graph-marl_amd.train"),
+            importlib.import_module("graph-marl_amd.replaybuffer"))
+
+
+def _sd(g, prefix):
+    return {k[len(prefix):]: torch.as_tensor(g[k]) for k in g.files if k.startswith(prefix)}
+
+
+def test_update_matches_reference_golden():
+    M, T, RB = mods()
+    g = np.load(f"{R.GOLDEN}/train.npz")
+    dev = torch.device("cuda")
+    nd = g["node_obs"].shape[-1]
+    netmon = M.NetMon(nd, 32, [64, 48], 1).to(dev)
+    netmon.load_state_dict(_sd(g, "netmon_"))
+    obs_dim = g["agent_obs"].shape[-1] + netmon.get_out_features()
+    model = M.DQN(obs_dim, [64, 32], 4).to(dev)
+    model.load_state_dict(_sd(g, "model_"))
+    target = M.DQN(obs_dim, [64, 32], 4).to(dev)
+    target.load_state_dict(_sd(g, "target_"))
+    L = g["actions"].shape[0]
+    f = lambda a: torch.as_tensor(a, device=dev)  # noqa: E731
+    batches = []
+    for t in range(L):
+        batches.append(RB.TransitionBatch(
+            None, f(g["agent_obs"][t]), f(g["actions"][t]).long(), f(g["reward"][t]), f(g["agent_obs"][t + 1]),
+            f(g["done"][t]).bool(), f(g["episode_done"][t]).bool(), f(g["node_obs"][t]),
+            M.dense_to_nbr(f(g["node_adj"][t])), f(g["node_state0"]), M.node_agent_to_index(f(g["node_agent"][t])),
+            f(g["node_obs"][t + 1]), M.node_agent_to_index(f(g["node_agent"][t + 1]))))
+    params = list(model.parameters()) + list(netmon.parameters())
+    names = [f"model_{k}" for k, _ in model.named_parameters()] + [f"netmon_{k}" for k, _ in
+                                                                    netmon.named_parameters()]
+    assert names == list(g["param_names"])
+    opt = torch.optim.AdamW(params, lr=float(g["lr"]))
+    netmon.train()
+    model.train()
+    loss, qs, qts = T.dqn_loss(netmon, model, target, batches, float(g["gamma"]))
+    np.testing.assert_allclose(loss.item(), g["loss"].item(), rtol=1e-5, atol=1e-6)
+    for t in range(L):
+        np.testing.assert_allclose(qs[t].detach().cpu().numpy(), g[f"q_{t}"], atol=1e-5, rtol=0)
+        np.testing.assert_allclose(qts[t].cpu().numpy(), g[f"qtarget_{t}"], atol=1e-5, rtol=0)
+    opt.zero_grad()
+    loss.backward()
+    for n, p in zip(names, params):
+        np.testing.assert_allclose(p.grad.cpu().numpy(), g["grad_raw_" + n], atol=1e-5, rtol=1e-4, err_msg=n)
+    torch.nn.utils.clip_grad_value_(params, 0.5)
+    torch.nn.utils.clip_grad_norm_(params, 1.0)
+    for n, p in zip(names, params):
+        np.testing.assert_allclose(p.grad.cpu().numpy(), g["grad_clip_" + n], atol=1e-5, rtol=1e-4, err_msg=n)
+    opt.step()
+    for n, p in zip(names, params):
+        np.testing.assert_allclose(p.detach().cpu().numpy(), g["param_after_" + n], atol=1e-6, rtol=0, err_msg=n)
+    T.interpolate_model(model, target, float(g["tau"]), target)
+    for k, v in target.state_dict().items():
+        np.testing.assert_allclose(v.cpu().numpy(), g["target_after_" + k], atol=1e-6, rtol=0, err_msg=k)
+
+
+def test_replay_sequences_and_full_update_on_env_data():
+    """Collect a rollout into the device replay buffer, sample sequences, run
+    dqn_update: sequences are consecutive slots of one env, loss is finite, and
+    parameters move."""
+    gm = importlib.import_module("graph-marl_amd")
+    M, T, RB = mods()
+    W = importlib.import_module("graph-marl_amd.wrapper")
+    P = importlib.import_module("graph-marl_amd.policy")
+    B, N, A = 64, 20, 20
+    env = gm.Routing(gm.Network(N, random_topology=True, excluded_seeds=gm.EVAL_SEEDS), A, n_env=B, seed=3,
+                     obs_extra=512, agent_adjacency=False)
+    torch.manual_seed(0)
+    netmon = M.NetMon(4 * N + 8, 128, [512, 256], 1).cuda()
+    model = M.DQN(6 * N + 10 + 512, [512, 256], 4).cuda()
+    target = M.DQN(6 * N + 10 + 512, [512, 256], 4).cuda()
+    target.load_state_dict(model.state_dict())
+    wenv = W.NetMonWrapper(env, netmon, 1)
+    pol = P.EpsilonGreedy(wenv, model, epsilon=1.0, epsilon_decay=1.0, epsilon_update_freq=100,
+                          step_before_train=0)
+    rb = RB.ReplayBuffer(0, 40 * B, B, A, env.obs_dim, N, 4 * N + 8, netmon.get_state_size(), "cuda")
+    wenv.reset()
+    for t in range(30):
+        obs = env.obs.clone()
+        node_obs, agent_node = env.node_obs.clone(), env.agent_node.clone()
+        state_in = wenv.last_netmon_state
+        act = pol(wenv.obs)
+        wenv.step_(act)
+        rb.add(obs, act, env.reward, env.obs, env.done.bool(), (t + 1) % 10 == 0, state_in, node_obs, env.nbr,
+               agent_node, env.node_obs, env.agent_node)
+        if (t + 1) % 10 == 0:
+            wenv.reset()
+    assert rb.count == 30
+    seqs = list(rb.get_batch(16, sequence_length=4))
+    slots = torch.stack([s.idx[0] for s in seqs])
+    envs = torch.stack([s.idx[1] for s in seqs])
+    assert (envs == envs[0]).all()
+    assert ((slots[1:] - slots[:-1]) % rb.count == 1).all()
+    params = list(model.parameters()) + list(netmon.parameters())
+    before = [p.detach().clone() for p in params]
+    opt = torch.optim.AdamW(params, lr=1e-3)
+    loss, _, _ = T.dqn_update(netmon, model, target, opt, params, seqs, 0.9, 0.01)
+    assert torch.isfinite(loss)
+    assert any(not torch.equal(a, p) for a, p in zip(before, params))

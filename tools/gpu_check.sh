@@ -1,0 +1,29 @@
+#!/bin/bash
+# GPU validation chain (run through gpurun). Each step has its own time limit and
+# the chain stops at the first failure, so a fault/timeout never starts more GPU work.
+#   tools/gpu_check.sh [smoke] [tests] [bench] [prof]
+cd "$(dirname "$0")/.." || exit 1
+mkdir -p gpurun_out
+step() {  # name, seconds, command...
+    local name=$1 secs=$2
+    shift 2
+    echo "== $name ($(date +%T))" | tee -a gpurun_out/chain.log
+    timeout -k 10 "$secs" "$@" > "gpurun_out/$name.log" 2>&1
+    local rc=$?
+    echo "== $name rc=$rc" | tee -a gpurun_out/chain.log
+    tail -5 "gpurun_out/$name.log"
+    return $rc
+}
+rc=0
+for s in "$@"; do
+    case $s in
+        smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" || exit $? ;;
+        tests) step gpu_tests 900 python -m pytest tests -m gpu -x -q --tb=short --timeout=300 -p no:cacheprovider || exit $? ;;
+        envtests) step env_tests 600 python -m pytest tests/test_env_gpu.py -x -q --tb=short --timeout=300 -p no:cacheprovider || exit $? ;;
+        nettests) step net_tests 600 python -m pytest tests/test_netmon_gpu.py tests/test_train_gpu.py -x -q --tb=short --timeout=300 -p no:cacheprovider || exit $? ;;
+        bench) step bench 600 python bench.py || exit $? ;;
+        benchq) step bench 300 python bench.py --no-cpu-baseline --steps 100 || exit $? ;;
+        *) echo "unknown step $s"; exit 2 ;;
+    esac
+done
+exit $rc
