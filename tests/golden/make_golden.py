@@ -338,7 +338,7 @@ def collect_graph_inputs(Network, Routing, EVAL_SEEDS, n, a, B, steps, seed):
 
 def sd_to_npz(prefix, sd, d):
     for k, v in sd.items():
-        d[f"{prefix}{k}"] = v.detach().cpu().numpy()
+        d[f"{prefix}{k}"] = v.detach().cpu().numpy().copy()  # copy: params are updated in place later
 
 
 def gen_netmon(out, Network, Routing, EVAL_SEEDS, NetMon, DQN):

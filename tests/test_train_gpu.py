@@ -18,7 +18,8 @@ def mods():
 
 
 def _sd(g, prefix):
-    return {k[len(prefix):]: torch.as_tensor(g[k]) for k in g.files if k.startswith(prefix)}
+    return {k[len(prefix):]: torch.as_tensor(g[k]) for k in g.files
+            if k.startswith(prefix) and not k.startswith(prefix + "after_")}
 
 
 def test_update_matches_reference_golden():
@@ -50,10 +51,11 @@ def test_update_matches_reference_golden():
     netmon.train()
     model.train()
     loss, qs, qts = T.dqn_loss(netmon, model, target, batches, float(g["gamma"]))
-    np.testing.assert_allclose(loss.item(), g["loss"].item(), rtol=1e-5, atol=1e-6)
     for t in range(L):
-        np.testing.assert_allclose(qs[t].detach().cpu().numpy(), g[f"q_{t}"], atol=1e-5, rtol=0)
-        np.testing.assert_allclose(qts[t].cpu().numpy(), g[f"qtarget_{t}"], atol=1e-5, rtol=0)
+        np.testing.assert_allclose(qs[t].detach().cpu().numpy(), g[f"q_{t}"], atol=1e-5, rtol=0, err_msg=f"q_{t}")
+        np.testing.assert_allclose(qts[t].cpu().numpy(), g[f"qtarget_{t}"], atol=1e-5, rtol=0,
+                                   err_msg=f"qtarget_{t}")
+    np.testing.assert_allclose(loss.item(), g["loss"].item(), rtol=1e-5, atol=1e-6)
     opt.zero_grad()
     loss.backward()
     for n, p in zip(names, params):
