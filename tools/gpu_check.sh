@@ -23,6 +23,12 @@ for s in "$@"; do
         nettests) step net_tests 600 python -m pytest tests/test_netmon_gpu.py tests/test_train_gpu.py -x -q --tb=short --timeout=300 -p no:cacheprovider || exit $? ;;
         bench) step bench 600 python bench.py || exit $? ;;
         benchq) step bench 300 python bench.py --no-cpu-baseline --steps 100 || exit $? ;;
+        prof) step prof 600 rocprofv3 --kernel-trace --stats -T --output-format csv -d gpurun_out/prof -o bench \
+                  -- python bench.py --steps 100 --no-cpu-baseline || exit $? ;;
+        pmc) step pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE -T --output-format csv -d gpurun_out/pmc -o fetch \
+                 -- python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-kernel-timers || exit $?
+             step pmc_write 600 rocprofv3 --pmc WRITE_SIZE -T --output-format csv -d gpurun_out/pmc -o write \
+                 -- python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-kernel-timers || exit $? ;;
         *) echo "unknown step $s"; exit 2 ;;
     esac
 done

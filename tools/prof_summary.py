@@ -1,0 +1,91 @@
+#!/usr/bin/env python3
+"""Summarise rocprofv3 CSVs (kernel trace + PMC FETCH_SIZE/WRITE_SIZE passes) per
+kernel and launch shape. Usage:
+  python tools/prof_summary.py --trace gpurun_out/prof/bench_kernel_trace.csv \
+      [--fetch gpurun_out/pmc/fetch_counter_collection.csv --write gpurun_out/pmc/write_counter_collection.csv]
+HBM bytes follow MI355X_MICROARCH.md §HBM: counters are KiB; FETCH_SIZE reads 1/2 of
+a wide (16 B/lane) coalesced stream on gfx950, so the corrected read figure is 2x.
+"""
+import argparse
+import csv
+from collections import defaultdict
+
+
+def load(path):
+    with open(path) as f:
+        return list(csv.DictReader(f))
+
+
+def key(r):
+    g = r.get("Grid_Size") or r.get("Grid_Size_X")
+    w = r.get("Workgroup_Size") or r.get("Workgroup_Size_X")
+    return r["Kernel_Name"], int(g), int(w)
+
+
+NETMON = ["netmon.enc0(K=88)", "netmon.enc1(K=512)", "netmon.enc2(K=256)", "netmon.rnn_obs(K=256)",
+          "netmon.rnn_update(K=256)"]
+DQN = ["dqn.enc0(K=642)", "dqn.enc1(K=512)", "dqn.q(K=256)"]
+
+
+def linear_labels(n_dispatch, episode_steps, netmon_iters=1):
+    """Call-site names of the k_linear_f32 dispatches of one bench.py process, in
+    launch order: reset (NetMon start-up step), then per step 3 DQN + 1 NetMon step,
+    and a reset after every `episode_steps` steps."""
+    nm = NETMON[:4] + [NETMON[4]] * netmon_iters
+    out = list(nm)
+    step = 0
+    while len(out) < n_dispatch:
+        out += DQN + nm
+        step += 1
+        if step % episode_steps == 0:
+            out += nm
+    return out[:n_dispatch]
+
+
+def relabel(rows, episode_steps):
+    lin = [r for r in rows if r["Kernel_Name"].startswith("k_linear_f32")]
+    for r, lab in zip(lin, linear_labels(len(lin), episode_steps)):
+        r["Kernel_Name"] = f"k_linear_f32[{lab}]"
+    return rows
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--trace", required=True)
+    ap.add_argument("--fetch")
+    ap.add_argument("--write")
+    ap.add_argument("--top", type=int, default=20)
+    ap.add_argument("--episode-steps", type=int, default=50)
+    a = ap.parse_args()
+    dur = defaultdict(list)
+    trace = load(a.trace)
+    trace.sort(key=lambda r: int(r["Start_Timestamp"]))
+    for r in relabel(trace, a.episode_steps):
+        dur[key(r)].append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
+    pmc = defaultdict(dict)
+    for name, path in (("FETCH_SIZE", a.fetch), ("WRITE_SIZE", a.write)):
+        if not path:
+            continue
+        acc = defaultdict(list)
+        rows = [r for r in load(path) if r["Counter_Name"] == name]
+        rows.sort(key=lambda r: int(r["Dispatch_Id"]))
+        for r in relabel(rows, a.episode_steps):
+            if r["Counter_Name"] == name:
+                acc[key(r)].append(float(r["Counter_Value"]))
+        for k, v in acc.items():
+            pmc[k][name] = sum(v) / len(v)
+    total = sum(sum(v) for v in dur.values())
+    rows = sorted(dur.items(), key=lambda kv: -sum(kv[1]))[: a.top]
+    print("| kernel | grid (threads) | wg | calls | avg us | share % | FETCH KiB/launch (x2 corr.) | WRITE KiB/launch |")
+    print("|---|---|---|---|---|---|---|---|")
+    for (n, g, w), v in rows:
+        p = pmc.get((n, g, w), {})
+        fe = p.get("FETCH_SIZE")
+        wr = p.get("WRITE_SIZE")
+        fes = "" if fe is None else f"{fe:.0f} ({2 * fe:.0f})"
+        wrs = "" if wr is None else f"{wr:.0f}"
+        print(f"| {n} | {g} | {w} | {len(v)} | {sum(v) / len(v) / 1e3:.1f} | {100 * sum(v) / total:.1f} | {fes} | {wrs} |")
+
+
+if __name__ == "__main__":
+    main()
