@@ -43,6 +43,7 @@ def parse():
     p.add_argument("--random-topology", type=int, default=1)
     p.add_argument("--epsilon", type=float, default=0.5)
     p.add_argument("--no-kernel-timers", action="store_true")
+    p.add_argument("--unfused", action="store_true", help="materialise the joint obs; separate LSTM/aggregate kernels")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-envs", type=int, default=256)
     p.add_argument("--cpu-steps", type=int, default=20)
@@ -52,7 +53,7 @@ def parse():
 def kernel_cost(tag, n_env, N, A, E):
     """(bound, algorithmic units per launch) for a timer tag — DESIGN.md §4."""
     kind = tag.split(":")[0]
-    if kind == "linear":
+    if kind in ("linear", "lstm", "lstm_agg"):
         m, n, k = (int(v) for v in tag.split(":")[2].split("x"))
         return "mfma", 2.0 * m * n * k
     if kind == "mp_aggregate":
@@ -101,13 +102,13 @@ def main():
     dqn = M.DQN(6 * N + 10 + netmon.get_out_features(), [512, 256], 4).to(dev)
     M.tag_modules(netmon, "netmon.")
     M.tag_modules(dqn, "dqn.")
-    wenv = W.NetMonWrapper(env, netmon, 1)
+    wenv = W.NetMonWrapper(env, netmon, 1, fused=not args.unfused)
     policy = P.EpsilonGreedy(wenv, dqn, epsilon=args.epsilon, epsilon_decay=1.0, epsilon_update_freq=100,
                              step_before_train=0)
     state = {"ep": 0}
 
     def step():
-        act = policy(wenv.obs)
+        act = policy.act(wenv)
         wenv.step_(act)
         state["ep"] += 1
         if state["ep"] >= args.episode_steps:

@@ -24,7 +24,7 @@ EXPORTS = [
     "gm_last_error", "gm_version", "gm_env_create", "gm_env_destroy", "gm_env_dims", "gm_env_reset",
     "gm_env_step", "gm_env_observe", "gm_env_topology", "gm_env_final_info", "gm_policy_egreedy",
     "gm_env_get_state", "gm_build_seed_list", "gm_mp_aggregate", "gm_mp_aggregate_bwd", "gm_netmon_readout",
-    "gm_netmon_readout_bwd", "gm_lstm_pointwise", "gm_lstm_pointwise_bwd", "gm_linear_f32",
+    "gm_netmon_readout_bwd", "gm_lstm_pointwise", "gm_lstm_pointwise_bwd", "gm_linear_f32", "gm_gemm_f32",
 ]
 
 

@@ -1,0 +1,433 @@
+// gm_gemm.hip — fp32 MFMA GEMM with gathered A operands and fused epilogues for the
+// NetMon / DQN layers (reference src/model.py:13-42 MLP, 119-125 Q_Net, 187-203 DQN,
+// 206-229 SimpleAggregation, 379-382/491/543 LSTMCell, 582-631 readout).
+//
+//   y = epi( A @ W^T + b ),  A = [ src0 (k0 cols) | src1 (k1 cols) ]   (K concatenation)
+//
+// A sources (per row of A):
+//   DENSE     row-major rows (any stride) — plain layer input, [x | h] of the LSTM, env obs
+//   AGGREGATE Σ_{m ∈ {n} ∪ nbr(n)} h[m] (ascending node id; /count for mean) — the
+//             message-passing aggregate is computed while the tile is loaded
+//   READOUT   [h_final[v], h_prev[nbr(v,0)], h_prev[nbr(v,1)], h_prev[nbr(v,2)]] with
+//             v = agent_node[row] — NetMon readout + agent gather (output_to_network_obs)
+// Epilogues: bias (+ leaky_relu), or LSTM gates (weights packed so one 128-wide tile holds
+// i,f,g,o of 32 hidden units): c' = σ(f)c + σ(i)tanh(g), h' = σ(o)tanh(c').
+//
+// Exact fp32 (v_mfma_f32_32x32x2_f32 = fmaf chain per k). All operand loads are
+// unconditional buffer_load_dwordx4 (hardware bounds check returns 0: missing
+// neighbours use an out-of-range offset, rows are clamped), so the load stream has
+// no per-lane branches; the ragged K tail is zeroed in the LDS store of the last tile
+// (wave-uniform branch). LDS is double-buffered: one barrier per 32-deep K tile while
+// the next tile's loads are in flight in registers. Blocks are remapped so that tiles
+// sharing A rows run on one XCD.
+#include <hip/hip_runtime.h>
+
+#include <cstring>
+#include <string>
+
+#include "../../include/graph_marl_amd.h"
+
+int gm_fail(int code, const std::string& msg);
+
+namespace {
+
+typedef float floatx16 __attribute__((ext_vector_type(16)));
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int BK = 32;
+constexpr int LDP = BK + 4;           // padded LDS row (floats): conflict-free ds_read_b128
+constexpr int OOB = 0x7ff00000;       // byte offset beyond any buffer: load returns 0
+enum { EPI_BIAS = 0, EPI_LSTM = 1 };
+
+struct ASrc {
+    int mode;                 // GM_A_DENSE / GM_A_AGGREGATE / GM_A_READOUT
+    const float* p0;          // dense rows | node rows h | h_final rows
+    const float* p1;          // READOUT: h_prev rows
+    long long ld0, ld1;       // row strides (floats)
+    const int* nbr;           // [G][N][deg]
+    const int* agent_node;    // READOUT: [G*R]
+    int n_nodes, deg, mean, rows_per_graph, k, hidden;
+    unsigned bytes0, bytes1;  // buffer extents for the bounds check
+};
+
+struct Epi {
+    const float* bias;
+    int act;                  // EPI_BIAS: 0 none, 1 leaky_relu(0.01)
+    float* y;
+    long long ldy;
+    float* y2;                // EPI_LSTM: c' out
+    long long ldy2;
+    const float* c_in;        // EPI_LSTM: c in
+    long long ldc;
+    float* act_out;           // EPI_LSTM: [M][4H] activations i,f,g,o (optional)
+    int hidden;
+};
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const float* p, unsigned bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc((void*)p, (short)0, (int)bytes, 0x00020000);
+}
+__device__ __forceinline__ float4 bload(__amdgpu_buffer_rsrc_t r, int byte_off) {
+    u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(r, byte_off, 0, 0);
+    return make_float4(__uint_as_float(v.x), __uint_as_float(v.y), __uint_as_float(v.z), __uint_as_float(v.w));
+}
+__device__ __forceinline__ float4 f4add(float4 a, float4 b) {
+    return make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w);
+}
+__device__ __forceinline__ float sigm(float x) { return 1.0f / (1.0f + expf(-x)); }
+
+template <int WGM, int WGN, int TM, int TN>
+struct Cfg {
+    static constexpr int BM = WGM * TM * 32;
+    static constexpr int BN = WGN * TN * 32;
+    static constexpr int THREADS = WGM * WGN * 64;
+    static constexpr int AQ = BM * BK / 4 / THREADS;  // float4 per thread per A tile
+    static constexpr int BQ = BN * BK / 4 / THREADS;
+    static constexpr int RSTEP = THREADS / (BK / 4);   // rows between a thread's A rows
+};
+
+template <int WGM, int WGN, int TM, int TN, int AMODE, int EPI>
+__global__ __launch_bounds__(WGM* WGN * 64, 2) void k_gemm(ASrc a0, ASrc a1, const float* __restrict__ w,
+                                                            long long ldw, unsigned wbytes, int M, int N, int K,
+                                                            Epi ep) {
+    using C = Cfg<WGM, WGN, TM, TN>;
+    __shared__ __attribute__((aligned(16))) float As[2][C::BM * LDP];
+    __shared__ __attribute__((aligned(16))) float Bs[2][C::BN * LDP];
+
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wr = wave / WGN, wc = wave % WGN;
+    const int nM = (M + C::BM - 1) / C::BM, nN = (N + C::BN - 1) / C::BN;
+    const int T = nM * nN;
+    int bid = blockIdx.x;
+    {
+        const int q = T / 8, r = T % 8, xcd = bid % 8, loc = bid / 8;
+        bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + loc;
+    }
+    const int m0 = (bid / nN) * C::BM, n0 = (bid % nN) * C::BN;
+
+    // ---- per-thread A rows (fixed over K) and their source rows ----
+    const int c4 = tid % (BK / 4);
+    const int rbase = tid / (BK / 4);
+    int rowoff0[C::AQ], rowoff1[C::AQ];
+    int src[C::AQ][4];  // AGGREGATE: member rows; READOUT: segment source rows (-1 = none)
+    float scale[C::AQ];
+#pragma unroll
+    for (int q = 0; q < C::AQ; q++) {
+        int row = min(m0 + rbase + q * C::RSTEP, M - 1);
+        rowoff0[q] = (int)(row * a0.ld0);
+        rowoff1[q] = (int)(row * a1.ld0);
+        scale[q] = 1.0f;
+        if (AMODE == GM_A_AGGREGATE) {
+            const int g = row / a0.n_nodes, n = row - g * a0.n_nodes;
+            const int* nb = a0.nbr + (size_t)row * a0.deg;
+            int cnt = 0, self_done = 0;
+#pragma unroll
+            for (int j = 0; j < 4; j++) src[q][j] = -1;
+            for (int j = 0; j < a0.deg; j++) {
+                int v = nb[j];
+                if (v < 0) continue;
+                if (!self_done && n < v) { src[q][cnt++] = g * a0.n_nodes + n; self_done = 1; }
+                src[q][cnt++] = g * a0.n_nodes + v;
+            }
+            if (!self_done) src[q][cnt++] = g * a0.n_nodes + n;
+            if (a0.mean) scale[q] = 1.0f / (float)cnt;
+        } else if (AMODE == GM_A_READOUT) {
+            const int g = row / a0.rows_per_graph;
+            const int v = a0.agent_node[row];
+            const int* nb = a0.nbr + ((size_t)g * a0.n_nodes + v) * a0.deg;
+            src[q][0] = g * a0.n_nodes + v;
+#pragma unroll
+            for (int j = 1; j < 4; j++) {
+                int m = j - 1 < a0.deg ? nb[j - 1] : -1;
+                src[q][j] = m >= 0 ? g * a0.n_nodes + m : -1;
+            }
+        }
+    }
+    int woff[C::BQ];
+#pragma unroll
+    for (int q = 0; q < C::BQ; q++) woff[q] = (int)(min(n0 + rbase + q * C::RSTEP, N - 1) * ldw);
+
+    const __amdgpu_buffer_rsrc_t r0a = rsrc(a0.p0, a0.bytes0);
+    const __amdgpu_buffer_rsrc_t r0b = rsrc(a0.p1 ? a0.p1 : a0.p0, a0.p1 ? a0.bytes1 : a0.bytes0);
+    const __amdgpu_buffer_rsrc_t r1 = rsrc(a1.p0 ? a1.p0 : a0.p0, a1.p0 ? a1.bytes0 : 0u);
+    const __amdgpu_buffer_rsrc_t rw = rsrc(w, wbytes);
+
+    float4 ra[C::AQ], rb[C::BQ];
+    auto gload = [&](int k0) {
+        if (k0 < a0.k) {
+            const int kl = k0 + 4 * c4;
+            if (AMODE == GM_A_DENSE) {
+#pragma unroll
+                for (int q = 0; q < C::AQ; q++) ra[q] = bload(r0a, (rowoff0[q] + kl) * 4);
+            } else if (AMODE == GM_A_AGGREGATE) {
+                const long long ld = a0.ld0;
+#pragma unroll
+                for (int q = 0; q < C::AQ; q++) {
+                    float4 v = bload(r0a, src[q][0] >= 0 ? (int)(src[q][0] * ld + kl) * 4 : OOB);
+#pragma unroll
+                    for (int j = 1; j < 4; j++)
+                        v = f4add(v, bload(r0a, src[q][j] >= 0 ? (int)(src[q][j] * ld + kl) * 4 : OOB));
+                    ra[q] = make_float4(v.x * scale[q], v.y * scale[q], v.z * scale[q], v.w * scale[q]);
+                }
+            } else {  // READOUT: the K tile lies inside one H-wide segment
+                const int seg = k0 / a0.hidden, ko = kl - seg * a0.hidden;
+                if (seg == 0) {
+#pragma unroll
+                    for (int q = 0; q < C::AQ; q++) ra[q] = bload(r0a, (int)(src[q][0] * a0.ld0 + ko) * 4);
+                } else {
+#pragma unroll
+                    for (int q = 0; q < C::AQ; q++) {
+                        int s = seg == 1 ? src[q][1] : seg == 2 ? src[q][2] : src[q][3];
+                        ra[q] = bload(r0b, s >= 0 ? (int)(s * a0.ld1 + ko) * 4 : OOB);
+                    }
+                }
+            }
+        } else {
+            const int kl = k0 - a0.k + 4 * c4;
+#pragma unroll
+            for (int q = 0; q < C::AQ; q++) ra[q] = bload(r1, (rowoff1[q] + kl) * 4);
+        }
+#pragma unroll
+        for (int q = 0; q < C::BQ; q++) rb[q] = bload(rw, (woff[q] + k0 + 4 * c4) * 4);
+    };
+    auto lstore = [&](int buf, int k0) {
+        // zero the columns past the end of the current source on its last (ragged) tile
+        const int kend = k0 < a0.k ? a0.k : K;
+        if (k0 + BK > kend) {
+            const int kk = k0 + 4 * c4;
+#pragma unroll
+            for (int q = 0; q < C::AQ; q++) {
+                if (kk + 0 >= kend) ra[q].x = 0.f;
+                if (kk + 1 >= kend) ra[q].y = 0.f;
+                if (kk + 2 >= kend) ra[q].z = 0.f;
+                if (kk + 3 >= kend) ra[q].w = 0.f;
+            }
+#pragma unroll
+            for (int q = 0; q < C::BQ; q++) {
+                if (kk + 0 >= K) rb[q].x = 0.f;
+                if (kk + 1 >= K) rb[q].y = 0.f;
+                if (kk + 2 >= K) rb[q].z = 0.f;
+                if (kk + 3 >= K) rb[q].w = 0.f;
+            }
+        }
+#pragma unroll
+        for (int q = 0; q < C::AQ; q++)
+            *reinterpret_cast<float4*>(&As[buf][(rbase + q * C::RSTEP) * LDP + 4 * c4]) = ra[q];
+#pragma unroll
+        for (int q = 0; q < C::BQ; q++)
+            *reinterpret_cast<float4*>(&Bs[buf][(rbase + q * C::RSTEP) * LDP + 4 * c4]) = rb[q];
+    };
+
+    floatx16 acc[TM][TN];
+#pragma unroll
+    for (int i = 0; i < TM; i++)
+#pragma unroll
+        for (int j = 0; j < TN; j++)
+#pragma unroll
+            for (int r = 0; r < 16; r++) acc[i][j][r] = 0.f;
+
+    const int h = lane >> 5, l32 = lane & 31;
+    const int nk = (K + BK - 1) / BK;
+    gload(0);
+    lstore(0, 0);
+    __syncthreads();
+    for (int kt = 0; kt < nk; kt++) {
+        const int cur = kt & 1;
+        if (kt + 1 < nk) gload((kt + 1) * BK);
+        const float* as = As[cur];
+        const float* bs = Bs[cur];
+#pragma unroll
+        for (int s4 = 0; s4 < 4; s4++) {
+            float4 af[TM], bf[TN];
+#pragma unroll
+            for (int i = 0; i < TM; i++)
+                af[i] = *reinterpret_cast<const float4*>(&as[(wr * TM * 32 + i * 32 + l32) * LDP + h * 16 + 4 * s4]);
+#pragma unroll
+            for (int j = 0; j < TN; j++)
+                bf[j] = *reinterpret_cast<const float4*>(&bs[(wc * TN * 32 + j * 32 + l32) * LDP + h * 16 + 4 * s4]);
+#pragma unroll
+            for (int e = 0; e < 4; e++)
+#pragma unroll
+                for (int i = 0; i < TM; i++)
+#pragma unroll
+                    for (int j = 0; j < TN; j++) {
+                        float a = e == 0 ? af[i].x : e == 1 ? af[i].y : e == 2 ? af[i].z : af[i].w;
+                        float b = e == 0 ? bf[j].x : e == 1 ? bf[j].y : e == 2 ? bf[j].z : bf[j].w;
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, acc[i][j], 0, 0, 0);
+                    }
+        }
+        if (kt + 1 < nk) lstore(cur ^ 1, (kt + 1) * BK);
+        __syncthreads();
+    }
+
+    // ---- epilogue: C/D map col = lane & 31, row = (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5) ----
+    if (EPI == EPI_BIAS) {
+#pragma unroll
+        for (int j = 0; j < TN; j++) {
+            const int col = n0 + wc * TN * 32 + j * 32 + l32;
+            const float bv = (ep.bias && col < N) ? ep.bias[col] : 0.f;
+#pragma unroll
+            for (int i = 0; i < TM; i++) {
+                const int rb0 = m0 + wr * TM * 32 + i * 32 + 4 * h;
+#pragma unroll
+                for (int r = 0; r < 16; r++) {
+                    const int row = rb0 + (r & 3) + 8 * (r >> 2);
+                    float v = acc[i][j][r] + bv;
+                    if (ep.act == 1) v = v >= 0.f ? v : 0.01f * v;
+                    if (row < M && col < N) ep.y[(long long)row * ep.ldy + col] = v;
+                }
+            }
+        }
+    } else {  // EPI_LSTM: TN == 4 gate tiles (i, f, g, o) of 32 hidden units
+        const int H = ep.hidden;
+        const int unit = (n0 >> 2) + l32;
+        float bgate[4];
+#pragma unroll
+        for (int g = 0; g < 4; g++) bgate[g] = ep.bias ? ep.bias[n0 + g * 32 + l32] : 0.f;
+#pragma unroll
+        for (int i = 0; i < TM; i++) {
+            const int rb0 = m0 + wr * TM * 32 + i * 32 + 4 * h;
+#pragma unroll
+            for (int r = 0; r < 16; r++) {
+                const int row = rb0 + (r & 3) + 8 * (r >> 2);
+                if (row >= M || unit >= H) continue;
+                float gi = sigm(acc[i][0][r] + bgate[0]);
+                float gf = sigm(acc[i][1][r] + bgate[1]);
+                float gg = tanhf(acc[i][2][r] + bgate[2]);
+                float go = sigm(acc[i][3][r] + bgate[3]);
+                float cn = gf * ep.c_in[(long long)row * ep.ldc + unit] + gi * gg;
+                float hn = go * tanhf(cn);
+                ep.y[(long long)row * ep.ldy + unit] = hn;
+                ep.y2[(long long)row * ep.ldy2 + unit] = cn;
+                if (ep.act_out) {
+                    float* ao = ep.act_out + (long long)row * 4 * H;
+                    ao[unit] = gi;
+                    ao[H + unit] = gf;
+                    ao[2 * H + unit] = gg;
+                    ao[3 * H + unit] = go;
+                }
+            }
+        }
+    }
+}
+
+template <int WGM, int WGN, int TM, int TN, int AMODE, int EPI>
+int launch(const ASrc& a0, const ASrc& a1, const float* w, long long ldw, unsigned wbytes, int M, int N, int K,
+           const Epi& ep, hipStream_t st) {
+    using C = Cfg<WGM, WGN, TM, TN>;
+    const int T = ((M + C::BM - 1) / C::BM) * ((N + C::BN - 1) / C::BN);
+    hipLaunchKernelGGL((k_gemm<WGM, WGN, TM, TN, AMODE, EPI>), dim3(T), dim3(C::THREADS), 0, st, a0, a1, w, ldw,
+                       wbytes, M, N, K, ep);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return gm_fail(GM_ERR_HIP, std::string("gm_gemm launch: ") + hipGetErrorString(e));
+    return GM_OK;
+}
+
+bool fits(long long bytes) { return bytes >= 0 && bytes < (1ll << 31) - (1 << 24); }
+
+int to_asrc(const gm_a_src* s, int M, ASrc& o) {
+    memset(&o, 0, sizeof(o));
+    if (!s) return GM_OK;
+    o.mode = s->mode;
+    o.p0 = s->p0;
+    o.p1 = s->p1;
+    o.ld0 = s->ld0;
+    o.ld1 = s->ld1;
+    o.nbr = s->nbr;
+    o.agent_node = s->agent_node;
+    o.n_nodes = s->n_nodes;
+    o.deg = s->deg;
+    o.mean = s->mean;
+    o.rows_per_graph = s->rows_per_graph;
+    o.k = s->k;
+    o.hidden = s->hidden;
+    if (!s->p0 || s->k <= 0 || (s->ld0 & 3) || (reinterpret_cast<uintptr_t>(s->p0) & 15))
+        return gm_fail(GM_ERR_INVALID_ARG, "gm_gemm_f32: A source needs p0, k > 0, ld0 % 4 == 0, 16-byte base");
+    long long rows0 = M;
+    if (s->mode == GM_A_DENSE) {
+        if (s->ld0 < s->k) return gm_fail(GM_ERR_INVALID_ARG, "gm_gemm_f32: dense ld0 < k");
+    } else {
+        if (!s->nbr || s->n_nodes <= 0 || s->deg < 0 || s->deg > 3)
+            return gm_fail(GM_ERR_INVALID_ARG, "gm_gemm_f32: gather source needs nbr, n_nodes, deg <= 3");
+        if (s->mode == GM_A_AGGREGATE) {
+            if (s->ld0 < s->k) return gm_fail(GM_ERR_INVALID_ARG, "gm_gemm_f32: aggregate ld0 < k");
+        } else if (s->mode == GM_A_READOUT) {
+            if (!s->p1 || !s->agent_node || s->rows_per_graph <= 0 || s->hidden <= 0 || (s->hidden % BK) ||
+                s->k != (s->deg + 1) * s->hidden || (s->ld1 & 3) || (reinterpret_cast<uintptr_t>(s->p1) & 15) ||
+                (M % s->rows_per_graph))
+                return gm_fail(GM_ERR_INVALID_ARG, "gm_gemm_f32: readout source: hidden % 32 == 0, k = (deg+1)*hidden");
+            rows0 = (long long)(M / s->rows_per_graph) * s->n_nodes;
+            long long b1 = ((rows0 - 1) * s->ld1 + s->hidden) * 4;
+            if (!fits(b1)) return gm_fail(GM_ERR_UNSUPPORTED, "gm_gemm_f32: source larger than 2 GB");
+            o.bytes1 = (unsigned)b1;
+        } else {
+            return gm_fail(GM_ERR_INVALID_ARG, "gm_gemm_f32: unknown A source mode");
+        }
+    }
+    long long width = s->mode == GM_A_READOUT ? s->hidden : s->k;
+    long long b0 = ((rows0 - 1) * s->ld0 + width) * 4;
+    if (!fits(b0)) return gm_fail(GM_ERR_UNSUPPORTED, "gm_gemm_f32: source larger than 2 GB (split M)");
+    o.bytes0 = (unsigned)b0;
+    return GM_OK;
+}
+
+}  // namespace
+
+extern "C" int gm_gemm_f32(const gm_a_src* a0, const gm_a_src* a1, const float* w, int64_t ldw, const float* b,
+                           int32_t m, int32_t n, int32_t epilogue, float* y, int64_t ldy, float* y2, int64_t ldy2,
+                           const float* c_in, int64_t ldc, float* act_out, void* stream) {
+    if (!a0 || !w || !y || m <= 0 || n <= 0 || (ldw & 3) || (reinterpret_cast<uintptr_t>(w) & 15))
+        return gm_fail(GM_ERR_INVALID_ARG, "gm_gemm_f32: bad arguments");
+    ASrc s0, s1;
+    int rc = to_asrc(a0, m, s0);
+    if (rc) return rc;
+    rc = to_asrc(a1, m, s1);
+    if (rc) return rc;
+    if (a1 && (a1->mode != GM_A_DENSE || (s0.k % BK)))
+        return gm_fail(GM_ERR_INVALID_ARG, "gm_gemm_f32: second A source must be dense and the first k % 32 == 0");
+    const int K = s0.k + (a1 ? s1.k : 0);
+    if (ldw < K) return gm_fail(GM_ERR_INVALID_ARG, "gm_gemm_f32: ldw < K");
+    long long wb = ((long long)(n - 1) * ldw + ((K + 3) & ~3)) * 4;
+    if (!fits(wb)) return gm_fail(GM_ERR_UNSUPPORTED, "gm_gemm_f32: weights larger than 2 GB");
+    Epi ep;
+    memset(&ep, 0, sizeof(ep));
+    ep.bias = b;
+    ep.y = y;
+    ep.ldy = ldy;
+    ep.y2 = y2;
+    ep.ldy2 = ldy2;
+    ep.c_in = c_in;
+    ep.ldc = ldc;
+    ep.act_out = act_out;
+    hipStream_t st = (hipStream_t)stream;
+    if (epilogue == GM_EPI_LSTM) {
+        if (n % 128 || !y2 || !c_in) return gm_fail(GM_ERR_INVALID_ARG, "gm_gemm_f32: LSTM epilogue needs 4H % 128 == 0");
+        ep.hidden = n / 4;
+        if (s0.mode == GM_A_DENSE) return launch<4, 1, 1, 4, GM_A_DENSE, EPI_LSTM>(s0, s1, w, ldw, (unsigned)wb, m, n, K, ep, st);
+        if (s0.mode == GM_A_AGGREGATE)
+            return launch<4, 1, 1, 4, GM_A_AGGREGATE, EPI_LSTM>(s0, s1, w, ldw, (unsigned)wb, m, n, K, ep, st);
+        return gm_fail(GM_ERR_UNSUPPORTED, "gm_gemm_f32: LSTM epilogue with readout source");
+    }
+    if (epilogue != GM_EPI_BIAS && epilogue != GM_EPI_BIAS_LEAKY)
+        return gm_fail(GM_ERR_INVALID_ARG, "gm_gemm_f32: unknown epilogue");
+    if (ldy < n) return gm_fail(GM_ERR_INVALID_ARG, "gm_gemm_f32: ldy < n");
+    ep.act = epilogue == GM_EPI_BIAS_LEAKY ? 1 : 0;
+    if (s0.mode == GM_A_READOUT)
+        return launch<2, 2, 2, 2, GM_A_READOUT, EPI_BIAS>(s0, s1, w, ldw, (unsigned)wb, m, n, K, ep, st);
+    if (s0.mode == GM_A_AGGREGATE)
+        return launch<2, 2, 2, 2, GM_A_AGGREGATE, EPI_BIAS>(s0, s1, w, ldw, (unsigned)wb, m, n, K, ep, st);
+    if (n <= 32) return launch<4, 1, 1, 1, GM_A_DENSE, EPI_BIAS>(s0, s1, w, ldw, (unsigned)wb, m, n, K, ep, st);
+    return launch<2, 2, 2, 2, GM_A_DENSE, EPI_BIAS>(s0, s1, w, ldw, (unsigned)wb, m, n, K, ep, st);
+}
+
+extern "C" int gm_linear_f32(const float* x, int64_t ldx, const float* w, int64_t ldw, const float* b, int32_t m,
+                             int32_t n, int32_t k, int32_t act, float* y, int64_t ldy, void* stream) {
+    if (!x || !w || !y || act < 0 || act > 1) return gm_fail(GM_ERR_INVALID_ARG, "gm_linear_f32: bad arguments");
+    gm_a_src a;
+    memset(&a, 0, sizeof(a));
+    a.mode = GM_A_DENSE;
+    a.p0 = x;
+    a.ld0 = ldx;
+    a.k = k;
+    return gm_gemm_f32(&a, nullptr, w, ldw, b, m, n, act ? GM_EPI_BIAS_LEAKY : GM_EPI_BIAS, y, ldy, nullptr, 0,
+                       nullptr, 0, nullptr, stream);
+}

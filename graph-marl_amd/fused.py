@@ -1,0 +1,198 @@
+"""Fused no-grad rollout path over gm_gemm_f32 (include/graph_marl_amd.h).
+
+NetMon step (reference src/model.py:476-580):
+  x  = MLP encoder(node_obs)                                   gm_linear_f32 x3
+  S1 = LSTM_obs([x | h_state], c_state)                        one GEMM, gate math in epilogue
+  S2 = LSTM_upd([Σ_{I+A} h(S1) | h(S1)], c(S1))  (K times)     aggregate folded into the A load
+state = S_K ([h | c] per node, the reference's (B, N, 2H) layout), h_prev = h before the
+last update (readout's neighbour features, src/model.py:510-519).
+
+DQN Q (src/model.py:187-203) on the joint observation without materialising it:
+  h1 = leaky(W1 @ [readout(h_final, h_prev, nbr, agent_node) | env_obs] + b1)
+so the NetMon readout + agent gather (src/model.py:582-631) happen in the GEMM's A load.
+Weights are packed once per parameter version (LSTM gate interleave, W1 column order).
+"""
+import ctypes as C
+
+import torch
+import torch.nn.functional as F
+
+from . import _lib as L
+
+GM_A_DENSE, GM_A_AGGREGATE, GM_A_READOUT = 0, 1, 2
+GM_EPI_BIAS, GM_EPI_BIAS_LEAKY, GM_EPI_LSTM = 0, 1, 2
+
+
+class ASrc(C.Structure):
+    _fields_ = [
+        ("mode", C.c_int32), ("p0", C.c_void_p), ("p1", C.c_void_p), ("ld0", C.c_int64), ("ld1", C.c_int64),
+        ("nbr", C.c_void_p), ("agent_node", C.c_void_p), ("n_nodes", C.c_int32), ("deg", C.c_int32),
+        ("mean", C.c_int32), ("rows_per_graph", C.c_int32), ("k", C.c_int32), ("hidden", C.c_int32),
+    ]
+
+
+def _setup():
+    lib = L.lib()
+    if not getattr(lib, "_gemm_ready", False):
+        vp = C.c_void_p
+        lib.gm_gemm_f32.argtypes = [C.POINTER(ASrc), C.POINTER(ASrc), vp, C.c_int64, vp, C.c_int32, C.c_int32,
+                                    C.c_int32, vp, C.c_int64, vp, C.c_int64, vp, C.c_int64, vp, vp]
+        lib._gemm_ready = True
+    return lib
+
+
+def dense(p, ld, k):
+    s = ASrc()
+    s.mode, s.p0, s.ld0, s.k = GM_A_DENSE, p, ld, k
+    return s
+
+
+def aggregate(p, ld, k, nbr, n_nodes, mean=False):
+    s = ASrc()
+    s.mode, s.p0, s.ld0, s.k = GM_A_AGGREGATE, p, ld, k
+    s.nbr, s.n_nodes, s.deg, s.mean = nbr.data_ptr(), n_nodes, nbr.shape[-1], int(mean)
+    return s
+
+
+def readout(h_final, ld_f, h_prev, ld_p, nbr, agent_node, n_nodes, hidden):
+    s = ASrc()
+    s.mode, s.p0, s.ld0, s.p1, s.ld1 = GM_A_READOUT, h_final, ld_f, h_prev, ld_p
+    s.nbr, s.agent_node, s.n_nodes, s.deg = nbr.data_ptr(), agent_node.data_ptr(), n_nodes, nbr.shape[-1]
+    s.rows_per_graph, s.hidden, s.k = agent_node.shape[-1], hidden, (nbr.shape[-1] + 1) * hidden
+    return s
+
+
+def gemm(a0, a1, w, ldw, b, m, n, epi, y, ldy, y2=None, ldy2=0, c_in=None, ldc=0, act_out=None, tag=None):
+    lib = _setup()
+    with L.timed(tag):
+        L.check(lib.gm_gemm_f32(C.byref(a0), None if a1 is None else C.byref(a1), w, ldw, b, m, n, epi, y, ldy,
+                                y2, ldy2, c_in, ldc, act_out, L.stream_ptr()))
+
+
+def _key(*ts):
+    return tuple((t.data_ptr(), t._version) for t in ts)
+
+
+class Packed:
+    """Per-module cache of packed weights, refreshed when a parameter changes."""
+
+    def __init__(self):
+        self.key = None
+        self.val = None
+
+    def get(self, key, fn):
+        if key != self.key:
+            self.val = fn()
+            self.key = key
+        return self.val
+
+
+def _pad_cols(w):
+    k = w.shape[1]
+    kp = (k + 3) // 4 * 4
+    return F.pad(w, (0, kp - k)).contiguous(), kp
+
+
+def pack_lstm(cell):
+    """[W_ih | W_hh] with rows interleaved per 32 hidden units: row 128t + 32g + u holds gate g
+    of unit 32t + u (original row g*H + 32t + u); bias b_ih + b_hh in the same order."""
+    if not hasattr(cell, "_packed"):
+        cell._packed = Packed()
+
+    def build():
+        with torch.no_grad():
+            H = cell.hidden_size
+            assert H % 32 == 0, "fused LSTM needs H % 32 == 0"
+            w = torch.cat([cell.weight_ih, cell.weight_hh], 1)
+            b = cell.bias_ih + cell.bias_hh
+            t = torch.arange(H // 32, device=w.device)
+            g = torch.arange(4, device=w.device)
+            u = torch.arange(32, device=w.device)
+            orig = (g[None, :, None] * H + 32 * t[:, None, None] + u[None, None, :]).reshape(-1)
+            wp, ldw = _pad_cols(w[orig])
+            return wp, ldw, b[orig].contiguous()
+
+    return cell._packed.get(_key(cell.weight_ih, cell.weight_hh, cell.bias_ih, cell.bias_hh), build)
+
+
+def pack_dqn_first(lin, obs_dim):
+    """W1 columns reordered to [graph part | env obs part] to match A = [readout | env obs]."""
+    if not hasattr(lin, "_packed_first"):
+        lin._packed_first = Packed()
+
+    def build():
+        with torch.no_grad():
+            w = torch.cat([lin.weight[:, obs_dim:], lin.weight[:, :obs_dim]], 1)
+            wp, ldw = _pad_cols(w)
+            return wp, ldw, lin.bias.contiguous()
+
+    return lin._packed_first.get(_key(lin.weight, lin.bias) + (obs_dim,), build)
+
+
+def _linear(x, ldx, k, lin, out):
+    wp, ldw = lin._wc.get(lin.weight)
+    a = dense(x.data_ptr(), ldx, k)
+    gemm(a, None, wp.data_ptr(), ldw, lin.bias.data_ptr(), x.shape[0], lin.out_features,
+         GM_EPI_BIAS_LEAKY if lin.act == 1 else GM_EPI_BIAS, out.data_ptr(), out.stride(0),
+         tag=lin.tag and f"linear:{lin.tag}:{x.shape[0]}x{lin.out_features}x{k}")
+    return out
+
+
+@torch.no_grad()
+def netmon_step(netmon, node_obs, nbr, state):
+    """One NetMon step for B graphs. node_obs [B, N, F]; nbr int32 [B, N, deg]; state
+    [B, N, 2H] or None. Returns (new state [B, N, 2H], h_prev rows [B*N, 2H] whose first
+    H columns are the last pre-aggregation h)."""
+    if netmon.rnn_type != "lstm":
+        raise NotImplementedError("fused NetMon step: lstm only (lnlstm/gru use NetMon.forward_graph)")
+    B, N, Fd = node_obs.shape
+    H = netmon.hidden_features
+    M = B * N
+    dev = node_obs.device
+    x = node_obs.reshape(M, Fd)
+    for lin in netmon.encode.linear_layers:
+        x = _linear(x, x.stride(0), x.shape[1], lin, torch.empty(M, lin.out_features, device=dev))
+    if state is None:
+        state = torch.zeros(B, N, 2 * H, device=dev)
+    st = state.reshape(M, 2 * H)
+    wp, ldw, bp = pack_lstm(netmon.rnn_obs)
+    S = torch.empty(M, 2 * H, device=dev)
+    gemm(dense(x.data_ptr(), x.stride(0), H), dense(st.data_ptr(), 2 * H, H), wp.data_ptr(), ldw, bp.data_ptr(),
+         M, 4 * H, GM_EPI_LSTM, S.data_ptr(), 2 * H, S[:, H:].data_ptr(), 2 * H, st[:, H:].data_ptr(), 2 * H,
+         tag=netmon.rnn_obs.tag and f"lstm:{netmon.rnn_obs.tag}:{M}x{4 * H}x{2 * H}")
+    wu, ldu, bu = pack_lstm(netmon.rnn_update)
+    last = S
+    mean = netmon.agg_mode == 1
+    for it in range(netmon.iterations):
+        last = S
+        S2 = torch.empty(M, 2 * H, device=dev)
+        gemm(aggregate(S.data_ptr(), 2 * H, H, nbr, N, mean), dense(S.data_ptr(), 2 * H, H), wu.data_ptr(), ldu,
+             bu.data_ptr(), M, 4 * H, GM_EPI_LSTM, S2.data_ptr(), 2 * H, S2[:, H:].data_ptr(), 2 * H,
+             S[:, H:].data_ptr(), 2 * H,
+             tag=netmon.rnn_update.tag and f"lstm_agg:{netmon.rnn_update.tag}:{M}x{4 * H}x{2 * H}")
+        S = S2
+    if netmon.iterations <= 0:
+        last = torch.zeros_like(S)
+    netmon.state = S.view(B, N, 2 * H)
+    return netmon.state, last
+
+
+@torch.no_grad()
+def dqn_q(dqn, env_obs, obs_dim, state, h_prev, nbr, agent_node, scratch):
+    """Q [B*A, actions] of the DQN on [env obs | NetMon readout] with the readout gathered
+    inside the first GEMM. env_obs: [B, A, stride] (first obs_dim columns used)."""
+    B, A, stride = env_obs.shape
+    N = nbr.shape[1]
+    H = state.shape[-1] // 2
+    M = B * A
+    lin0 = dqn.encoder.linear_layers[0]
+    wp, ldw, b = pack_dqn_first(lin0, obs_dim)
+    h1 = scratch(0, M, lin0.out_features)
+    a0 = readout(state.data_ptr(), 2 * H, h_prev.data_ptr(), h_prev.stride(0), nbr, agent_node, N, H)
+    gemm(a0, dense(env_obs.data_ptr(), stride, obs_dim), wp.data_ptr(), ldw, b.data_ptr(), M, lin0.out_features,
+         GM_EPI_BIAS_LEAKY if lin0.act == 1 else GM_EPI_BIAS, h1.data_ptr(), h1.stride(0),
+         tag=lin0.tag and f"linear:{lin0.tag}:{M}x{lin0.out_features}x{a0.k + obs_dim}")
+    h = h1
+    for i, lin in enumerate(list(dqn.encoder.linear_layers[1:]) + [dqn.q_net.fc]):
+        h = _linear(h, h.stride(0), h.shape[1], lin, scratch(i + 1, M, lin.out_features))
+    return h

@@ -51,11 +51,28 @@ class EpsilonGreedy:
                                               L.stream_ptr(e.device)))
         return self.actions
 
-    def __call__(self, obs, adj=None):
+    def _decay_step(self):
         self._step += 1
-        actions = self.select(self.q_values(obs))
         if self._epsilon > 0 and self._step > self._before and self._step % self._freq == 0:
             self._epsilon = max(self._epsilon * self._decay, 0.01)
+
+    def __call__(self, obs, adj=None):
+        actions = self.select(self.q_values(obs))
+        self._decay_step()
+        return actions
+
+    def act(self, wenv):
+        """Fast path for a fused NetMonWrapper: the DQN's first GEMM gathers the NetMon
+        readout from the node state tables instead of reading a materialised joint obs."""
+        from . import fused as FU
+
+        if not getattr(wenv, "fused", False):
+            return self(wenv.obs)
+        e = wenv.env
+        q = FU.dqn_q(self._model, e.obs_buf, e.obs_dim, wenv.current_netmon_state, wenv.h_prev, e.nbr,
+                     e.agent_node, self._buf)
+        actions = self.select(q.view(e.n_env, e.n_data, -1))
+        self._decay_step()
         return actions
 
     def eval(self):

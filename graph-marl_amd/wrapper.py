@@ -1,17 +1,23 @@
 """NetMon graph observations for the batched routing env (reference
 src/env/wrapper.py:7-109 NetMonWrapper).
 
-After every env step one NetMon step runs on the device over all n_env graphs;
-its readout is written straight into columns [6N+10, 6N+10+4H) of the env's
-joint observation buffer (the reference's np.concatenate of obs and graph obs).
+After every env step one NetMon step runs on the device over all n_env graphs.
+Fused mode (lstm NetMon, default): the step is three encoder GEMMs plus one GEMM per LSTM
+cell with the aggregate and gate math fused (fused.netmon_step); the graph part of the joint
+observation is NOT materialised — the DQN gathers it inside its first GEMM
+(policy.EpsilonGreedy.act). Reading `.obs` (the reference API) materialises the joint
+observation [env obs | readout] on demand. Unfused mode runs NetMon.forward_graph and writes
+the readout into the joint observation buffer after every step.
 """
 import torch
 
-from .model import NetMon
+from . import _lib as L
+from . import fused as FU
+from .model import NetMon, netmon_readout
 
 
 class NetMonWrapper:
-    def __init__(self, env, netmon: NetMon, startup_iterations=1):
+    def __init__(self, env, netmon: NetMon, startup_iterations=1, fused=None):
         assert startup_iterations >= 1, "Number of startup iterations must be >= 1"
         need = env.obs_dim + netmon.get_out_features()
         if env.obs_stride < need:
@@ -21,7 +27,10 @@ class NetMonWrapper:
         self.startup_iterations = startup_iterations
         self.last_netmon_state = None
         self.current_netmon_state = None
+        self.h_prev = None
         self.obs_dim = need
+        self.fused = (netmon.rnn_type == "lstm" and netmon.output_neighbor_hidden) if fused is None else fused
+        self._dirty = False
 
     def __getattr__(self, name):
         return getattr(self.env, name)
@@ -31,15 +40,32 @@ class NetMonWrapper:
 
     @property
     def obs(self):
+        """joint observation [n_env, A, 6N+10+4H] (reference: concat of obs and graph obs)."""
+        if self._dirty:
+            self._materialize()
         return self.env.obs_buf[..., : self.obs_dim]
 
+    def _materialize(self):
+        e, H = self.env, self.netmon.hidden_features
+        B, N = e.n_env, e.n_nodes
+        hf = self.current_netmon_state.reshape(B * N, -1)[:, :H].contiguous()
+        hp = self.h_prev[:, :H].contiguous()
+        with torch.no_grad():
+            netmon_readout(hf, hp, e.nbr, e.agent_node, out=e.obs_buf, col0=e.obs_dim)
+        self._dirty = False
+
     def _netmon_step(self):
+        e = self.env
         with torch.no_grad():
             self.last_netmon_state = self.current_netmon_state
-            self.netmon.state = self.current_netmon_state
-            self.netmon.forward_graph(self.env.node_obs, self.env.nbr, self.env.agent_node,
-                                      out=self.env.obs_buf, out_col=self.env.obs_dim)
-            self.current_netmon_state = self.netmon.state
+            if self.fused:
+                state, self.h_prev = FU.netmon_step(self.netmon, e.node_obs, e.nbr, self.current_netmon_state)
+                self.current_netmon_state = state
+                self._dirty = True
+            else:
+                self.netmon.state = self.current_netmon_state
+                self.netmon.forward_graph(e.node_obs, e.nbr, e.agent_node, out=e.obs_buf, out_col=e.obs_dim)
+                self.current_netmon_state = self.netmon.state
 
     def reset(self):
         self.current_netmon_state = None

@@ -20,6 +20,7 @@
  *   gm_netmon_readout(_bwd)          NetMon._get_neighbor_h + output_to_network_obs src/model.py:582-631
  *   gm_lstm_pointwise(_bwd)          nn.LSTMCell gate math / LayerNorm-free part    src/model.py:379-382, 491, 543
  *   gm_linear_f32                    nn.Linear (+ leaky_relu of MLP)        src/model.py:13-42, 119-125
+ *   gm_gemm_f32                      Linear / LSTMCell GEMMs with aggregate, readout and gate math fused
  */
 #ifndef GRAPH_MARL_AMD_H
 #define GRAPH_MARL_AMD_H
@@ -169,6 +170,31 @@ int gm_lstm_pointwise_bwd(const float* dh_new, const float* dc_new, const float*
  * act 0 = none, 1 = leaky_relu(0.01). */
 int gm_linear_f32(const float* x, int64_t ldx, const float* w, int64_t ldw, const float* b, int32_t m, int32_t n,
                   int32_t k, int32_t act, float* y, int64_t ldy, void* stream);
+
+/* ---- General fused GEMM: y = epilogue(A @ W^T + b), A = [src0 | src1] along K ----
+ * Replaces the reference's Linear layers of MLP/DQN (src/model.py:13-42, 187-203) and the
+ * LSTMCell gate GEMM (src/model.py:379-382) with the aggregate (206-229) and the readout +
+ * agent gather (582-631) folded into the A-operand load. */
+enum { GM_A_DENSE = 0, GM_A_AGGREGATE = 1, GM_A_READOUT = 2 };
+enum { GM_EPI_BIAS = 0, GM_EPI_BIAS_LEAKY = 1, GM_EPI_LSTM = 2 };
+typedef struct {
+    int32_t mode;              /* GM_A_*                                                           */
+    const float* p0;           /* DENSE: rows; AGGREGATE: node rows h; READOUT: h_final node rows  */
+    const float* p1;           /* READOUT: h_prev node rows (the last pre-aggregation h)           */
+    int64_t ld0, ld1;          /* row strides in floats (multiples of 4)                           */
+    const int32_t* nbr;        /* AGGREGATE / READOUT: [G][n_nodes][deg] ascending, -1 = none      */
+    const int32_t* agent_node; /* READOUT: [G * rows_per_graph] node of every row                  */
+    int32_t n_nodes, deg, mean, rows_per_graph;
+    int32_t k;                 /* columns this source contributes (READOUT: (deg + 1) * hidden)    */
+    int32_t hidden;            /* READOUT: H (multiple of 32)                                      */
+} gm_a_src;
+/* src1 (nullable) must be DENSE and src0->k a multiple of 32. W: [n][ldw] (ldw >= K, zero
+ * padded to a multiple of 4). GM_EPI_LSTM: W rows packed so that rows [128t, 128t+128) are
+ * gates i,f,g,o (32 rows each) of hidden units [32t, 32t+32); n = 4H; writes h' to y, c' to y2,
+ * reads c from c_in, optional activations [M][4H] (original gate order) to act_out. */
+int gm_gemm_f32(const gm_a_src* src0, const gm_a_src* src1, const float* w, int64_t ldw, const float* b, int32_t m,
+                int32_t n, int32_t epilogue, float* y, int64_t ldy, float* y2, int64_t ldy2, const float* c_in,
+                int64_t ldc, float* act_out, void* stream);
 
 #ifdef __cplusplus
 }

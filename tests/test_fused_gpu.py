@@ -1,0 +1,113 @@
+"""GPU parity of the fused GEMM path (gm_gemm_f32): dense/ragged GEMMs and the LSTM
+epilogue vs torch fp32, the fused NetMon step and DQN readout-gather vs the unfused
+(golden-validated) path, and the reference goldens through the fused path."""
+import importlib
+
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+import golden_replay as R
+
+pytestmark = pytest.mark.gpu
+
+
+def mods():
+    return (importlib.import_module("graph-marl_amd"), importlib.import_module("graph-marl_amd.model"),
+            importlib.import_module("graph-marl_amd.fused"), importlib.import_module("graph-marl_amd.wrapper"))
+
+
+@pytest.mark.parametrize("m,n,k,ldx", [(81920, 512, 642, 644), (1000, 256, 512, 512), (777, 130, 90, 92),
+                                       (5, 3, 7, 8), (4097, 33, 129, 132), (64, 4, 256, 256)])
+@pytest.mark.parametrize("epi", [0, 1])
+def test_gemm_dense_vs_torch(m, n, k, ldx, epi):
+    gm, M, FU, W = mods()
+    torch.manual_seed(m + n + k)
+    buf = torch.randn(m, ldx, device="cuda")
+    x = buf[:, :k]
+    w = torch.randn(n, k, device="cuda") / k ** 0.5
+    b = torch.randn(n, device="cuda")
+    wp, ldw = FU._pad_cols(w)
+    y = torch.empty(m, n, device="cuda")
+    FU.gemm(FU.dense(buf.data_ptr(), ldx, k), None, wp.data_ptr(), ldw, b.data_ptr(), m, n, epi, y.data_ptr(), n)
+    ref = F.linear(x.double(), w.double(), b.double())
+    if epi == 1:
+        ref = F.leaky_relu(ref)
+    assert (y.double() - ref).abs().max().item() < 1e-5 * max(1.0, k ** 0.5 / 8)
+
+
+def test_gemm_two_sources_and_lstm_epilogue():
+    gm, M, FU, W = mods()
+    torch.manual_seed(0)
+    Mr, H = 5000, 128
+    cell = M.LSTMCell(H, H).cuda()
+    x = torch.randn(Mr, H, device="cuda")
+    st = torch.randn(Mr, 2 * H, device="cuda")
+    h, c = st[:, :H], st[:, H:]
+    wp, ldw, bp = FU.pack_lstm(cell)
+    S = torch.empty(Mr, 2 * H, device="cuda")
+    FU.gemm(FU.dense(x.data_ptr(), H, H), FU.dense(st.data_ptr(), 2 * H, H), wp.data_ptr(), ldw, bp.data_ptr(), Mr,
+            4 * H, FU.GM_EPI_LSTM, S.data_ptr(), 2 * H, S[:, H:].data_ptr(), 2 * H, c.data_ptr(), 2 * H)
+    ref = torch.nn.LSTMCell(H, H).cuda()
+    ref.load_state_dict(cell.state_dict())
+    rh, rc = ref(x, (h.contiguous(), c.contiguous()))
+    torch.testing.assert_close(S[:, :H], rh, atol=1e-5, rtol=0)
+    torch.testing.assert_close(S[:, H:], rc, atol=1e-5, rtol=0)
+
+
+def _setup_env(gm, W, M, B=64, seed=5, fused=True):
+    N, A = 20, 20
+    env = gm.Routing(gm.Network(N, random_topology=True, excluded_seeds=gm.EVAL_SEEDS), A, n_env=B, seed=seed,
+                     obs_extra=512, agent_adjacency=False)
+    torch.manual_seed(1)
+    nm = M.NetMon(4 * N + 8, 128, [512, 256], 1).cuda()
+    return env, nm, W.NetMonWrapper(env, nm, 1, fused=fused)
+
+
+def test_fused_rollout_matches_unfused_path():
+    gm, M, FU, W = mods()
+    P = importlib.import_module("graph-marl_amd.policy")
+    e1, nm1, w1 = _setup_env(gm, W, M, fused=True)
+    e2, nm2, w2 = _setup_env(gm, W, M, fused=False)
+    torch.manual_seed(2)
+    dqn = M.DQN(e1.obs_dim + 512, [512, 256], 4).cuda()
+    p1 = P.EpsilonGreedy(w1, dqn, epsilon=0.5, epsilon_decay=1.0, step_before_train=0)
+    p2 = P.EpsilonGreedy(w2, dqn, epsilon=0.5, epsilon_decay=1.0, step_before_train=0)
+    w1.reset()
+    w2.reset()
+    for t in range(6):
+        q1 = FU.dqn_q(dqn, e1.obs_buf, e1.obs_dim, w1.current_netmon_state, w1.h_prev, e1.nbr, e1.agent_node,
+                      p1._buf).view(e1.n_env, e1.n_data, -1).clone()
+        q2 = p2.q_values(w2.obs)
+        torch.testing.assert_close(q1, q2, atol=1e-5, rtol=0)
+        a1 = p1.select(q1).clone()
+        a2 = p2.select(q2).clone()
+        # identical draws; argmax may only differ on exact near-ties
+        assert (a1 != a2).float().mean().item() < 1e-3
+        w1.step_(a2)
+        w2.step_(a2)
+        torch.testing.assert_close(w1.current_netmon_state, w2.current_netmon_state, atol=1e-5, rtol=0)
+        torch.testing.assert_close(w1.obs, w2.obs, atol=1e-5, rtol=0)
+
+
+@pytest.mark.parametrize("vi", [0, 1, 2])
+def test_fused_netmon_vs_reference_golden(vi):
+    gm, M, FU, W = mods()
+    g = np.load(f"{R.GOLDEN}/netmon.npz")
+    rnn, agg, K, H, enc = g["variants"][vi].split("|")
+    nm = M.NetMon(g["node_obs"].shape[-1], int(H), [int(e) for e in enc.split(",")], int(K), rnn_type=rnn,
+                  agg_type=agg).cuda()
+    nm.load_state_dict({k[len(f"v{vi}_w_"):]: torch.as_tensor(g[k]) for k in g.files if k.startswith(f"v{vi}_w_")})
+    state = None
+    for t in range(3):
+        x = torch.as_tensor(g["node_obs"][t], device="cuda")
+        nbr = M.dense_to_nbr(torch.as_tensor(g["node_adj"][t], device="cuda"))
+        na = torch.as_tensor(g["node_agent"][t], device="cuda")
+        an = M.node_agent_to_index(na)
+        state, hprev = FU.netmon_step(nm, x, nbr, state)
+        np.testing.assert_allclose(state.cpu().numpy(), g[f"v{vi}_state_{t}"], atol=1e-5, rtol=0)
+        B, N = x.shape[:2]
+        Hh = int(H)
+        out = M.netmon_readout(state.reshape(B * N, -1)[:, :Hh].contiguous(), hprev[:, :Hh].contiguous(), nbr, an)
+        np.testing.assert_allclose(out.view(B, -1, 4 * Hh).cpu().numpy(), g[f"v{vi}_mapped_{t}"], atol=1e-5, rtol=0)
