@@ -25,6 +25,7 @@ EXPORTS = [
     "gm_env_step", "gm_env_observe", "gm_env_topology", "gm_env_final_info", "gm_policy_egreedy",
     "gm_env_get_state", "gm_build_seed_list", "gm_mp_aggregate", "gm_mp_aggregate_bwd", "gm_netmon_readout",
     "gm_netmon_readout_bwd", "gm_lstm_pointwise", "gm_lstm_pointwise_bwd", "gm_linear_f32", "gm_gemm_f32",
+    "gm_gemm_set_tile",
 ]
 
 
@@ -87,6 +88,7 @@ def lib():
     L.gm_lstm_pointwise.argtypes = [vp, vp, i32, i32, vp, vp, vp, vp]
     L.gm_lstm_pointwise_bwd.argtypes = [vp, vp, vp, vp, vp, i32, i32, vp, vp, vp]
     L.gm_linear_f32.argtypes = [vp, i64, vp, i64, vp, i32, i32, i32, i32, vp, i64, vp]
+    L.gm_gemm_set_tile.argtypes = [i32]
     _lib = L
     return L
 

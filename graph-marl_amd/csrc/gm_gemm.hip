@@ -34,8 +34,7 @@ namespace {
 typedef float floatx16 __attribute__((ext_vector_type(16)));
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
-constexpr int BK = 32;
-constexpr int LDP = BK + 4;           // padded LDS row (floats): conflict-free ds_read_b128
+constexpr int BKMAX = 32;            // largest K tile of any configuration (host-side checks)
 constexpr int OOB = 0x7ff00000;       // byte offset beyond any buffer: load returns 0
 enum { EPI_BIAS = 0, EPI_LSTM = 1 };
 
@@ -75,8 +74,11 @@ __device__ __forceinline__ float4 f4add(float4 a, float4 b) {
 }
 __device__ __forceinline__ float sigm(float x) { return 1.0f / (1.0f + expf(-x)); }
 
-template <int WGM, int WGN, int TM, int TN>
+template <int WGM, int WGN, int TM, int TN, int BK_>
 struct Cfg {
+    static constexpr int BK = BK_;
+    static constexpr int LDP = BK + 4;  // padded LDS row (floats): conflict-free ds_read_b128
+    static constexpr int KH = BK / 2;   // k per lane half: MFMA k pair {s, KH + s}
     static constexpr int BM = WGM * TM * 32;
     static constexpr int BN = WGN * TN * 32;
     static constexpr int THREADS = WGM * WGN * 64;
@@ -85,11 +87,12 @@ struct Cfg {
     static constexpr int RSTEP = THREADS / (BK / 4);   // rows between a thread's A rows
 };
 
-template <int WGM, int WGN, int TM, int TN, int AMODE, int EPI>
+template <int WGM, int WGN, int TM, int TN, int BK_, int AMODE, int EPI>
 __global__ __launch_bounds__(WGM* WGN * 64, 2) void k_gemm(ASrc a0, ASrc a1, const float* __restrict__ w,
                                                             long long ldw, unsigned wbytes, int M, int N, int K,
                                                             Epi ep) {
-    using C = Cfg<WGM, WGN, TM, TN>;
+    using C = Cfg<WGM, WGN, TM, TN, BK_>;
+    constexpr int BK = C::BK, LDP = C::LDP, KH = C::KH;
     __shared__ __attribute__((aligned(16))) float As[2][C::BM * LDP];
     __shared__ __attribute__((aligned(16))) float Bs[2][C::BN * LDP];
 
@@ -236,14 +239,14 @@ __global__ __launch_bounds__(WGM* WGN * 64, 2) void k_gemm(ASrc a0, ASrc a1, con
         const float* as = As[cur];
         const float* bs = Bs[cur];
 #pragma unroll
-        for (int s4 = 0; s4 < 4; s4++) {
+        for (int s4 = 0; s4 < KH / 4; s4++) {
             float4 af[TM], bf[TN];
 #pragma unroll
             for (int i = 0; i < TM; i++)
-                af[i] = *reinterpret_cast<const float4*>(&as[(wr * TM * 32 + i * 32 + l32) * LDP + h * 16 + 4 * s4]);
+                af[i] = *reinterpret_cast<const float4*>(&as[(wr * TM * 32 + i * 32 + l32) * LDP + h * KH + 4 * s4]);
 #pragma unroll
             for (int j = 0; j < TN; j++)
-                bf[j] = *reinterpret_cast<const float4*>(&bs[(wc * TN * 32 + j * 32 + l32) * LDP + h * 16 + 4 * s4]);
+                bf[j] = *reinterpret_cast<const float4*>(&bs[(wc * TN * 32 + j * 32 + l32) * LDP + h * KH + 4 * s4]);
 #pragma unroll
             for (int e = 0; e < 4; e++)
 #pragma unroll
@@ -310,17 +313,19 @@ __global__ __launch_bounds__(WGM* WGN * 64, 2) void k_gemm(ASrc a0, ASrc a1, con
     }
 }
 
-template <int WGM, int WGN, int TM, int TN, int AMODE, int EPI>
+template <int WGM, int WGN, int TM, int TN, int BK_, int AMODE, int EPI>
 int launch(const ASrc& a0, const ASrc& a1, const float* w, long long ldw, unsigned wbytes, int M, int N, int K,
            const Epi& ep, hipStream_t st) {
-    using C = Cfg<WGM, WGN, TM, TN>;
+    using C = Cfg<WGM, WGN, TM, TN, BK_>;
     const int T = ((M + C::BM - 1) / C::BM) * ((N + C::BN - 1) / C::BN);
-    hipLaunchKernelGGL((k_gemm<WGM, WGN, TM, TN, AMODE, EPI>), dim3(T), dim3(C::THREADS), 0, st, a0, a1, w, ldw,
-                       wbytes, M, N, K, ep);
+    hipLaunchKernelGGL((k_gemm<WGM, WGN, TM, TN, BK_, AMODE, EPI>), dim3(T), dim3(C::THREADS), 0, st, a0, a1, w,
+                       ldw, wbytes, M, N, K, ep);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return gm_fail(GM_ERR_HIP, std::string("gm_gemm launch: ") + hipGetErrorString(e));
     return GM_OK;
 }
+
+int g_tile = -1;  // tile configuration override (gm_gemm_set_tile), -1 = per-shape default
 
 bool fits(long long bytes) { return bytes >= 0 && bytes < (1ll << 31) - (1 << 24); }
 
@@ -351,7 +356,7 @@ int to_asrc(const gm_a_src* s, int M, ASrc& o) {
         if (s->mode == GM_A_AGGREGATE) {
             if (s->ld0 < s->k) return gm_fail(GM_ERR_INVALID_ARG, "gm_gemm_f32: aggregate ld0 < k");
         } else if (s->mode == GM_A_READOUT) {
-            if (!s->p1 || !s->agent_node || s->rows_per_graph <= 0 || s->hidden <= 0 || (s->hidden % BK) ||
+            if (!s->p1 || !s->agent_node || s->rows_per_graph <= 0 || s->hidden <= 0 || (s->hidden % BKMAX) ||
                 s->k != (s->deg + 1) * s->hidden || (s->ld1 & 3) || (reinterpret_cast<uintptr_t>(s->p1) & 15) ||
                 (M % s->rows_per_graph))
                 return gm_fail(GM_ERR_INVALID_ARG, "gm_gemm_f32: readout source: hidden % 32 == 0, k = (deg+1)*hidden");
@@ -382,7 +387,7 @@ extern "C" int gm_gemm_f32(const gm_a_src* a0, const gm_a_src* a1, const float* 
     if (rc) return rc;
     rc = to_asrc(a1, m, s1);
     if (rc) return rc;
-    if (a1 && (a1->mode != GM_A_DENSE || (s0.k % BK)))
+    if (a1 && (a1->mode != GM_A_DENSE || (s0.k % BKMAX)))
         return gm_fail(GM_ERR_INVALID_ARG, "gm_gemm_f32: second A source must be dense and the first k % 32 == 0");
     const int K = s0.k + (a1 ? s1.k : 0);
     if (ldw < K) return gm_fail(GM_ERR_INVALID_ARG, "gm_gemm_f32: ldw < K");
@@ -399,24 +404,48 @@ extern "C" int gm_gemm_f32(const gm_a_src* a0, const gm_a_src* a1, const float* 
     ep.ldc = ldc;
     ep.act_out = act_out;
     hipStream_t st = (hipStream_t)stream;
+    const int tile = g_tile;
+#define GM_L(WGM, WGN, TM, TN, BK_, AM, EP) \
+    launch<WGM, WGN, TM, TN, BK_, AM, EP>(s0, s1, w, ldw, (unsigned)wb, m, n, K, ep, st)
     if (epilogue == GM_EPI_LSTM) {
         if (n % 128 || !y2 || !c_in) return gm_fail(GM_ERR_INVALID_ARG, "gm_gemm_f32: LSTM epilogue needs 4H % 128 == 0");
         ep.hidden = n / 4;
-        if (s0.mode == GM_A_DENSE) return launch<4, 1, 1, 4, GM_A_DENSE, EPI_LSTM>(s0, s1, w, ldw, (unsigned)wb, m, n, K, ep, st);
-        if (s0.mode == GM_A_AGGREGATE)
-            return launch<4, 1, 1, 4, GM_A_AGGREGATE, EPI_LSTM>(s0, s1, w, ldw, (unsigned)wb, m, n, K, ep, st);
+        if (s0.mode == GM_A_DENSE) {
+            if (tile == 2) return GM_L(4, 1, 2, 4, 16, GM_A_DENSE, EPI_LSTM);
+            return GM_L(4, 1, 1, 4, 32, GM_A_DENSE, EPI_LSTM);
+        }
+        if (s0.mode == GM_A_AGGREGATE) {
+            if (tile == 2) return GM_L(4, 1, 2, 4, 16, GM_A_AGGREGATE, EPI_LSTM);
+            return GM_L(4, 1, 1, 4, 32, GM_A_AGGREGATE, EPI_LSTM);
+        }
         return gm_fail(GM_ERR_UNSUPPORTED, "gm_gemm_f32: LSTM epilogue with readout source");
     }
     if (epilogue != GM_EPI_BIAS && epilogue != GM_EPI_BIAS_LEAKY)
         return gm_fail(GM_ERR_INVALID_ARG, "gm_gemm_f32: unknown epilogue");
     if (ldy < n) return gm_fail(GM_ERR_INVALID_ARG, "gm_gemm_f32: ldy < n");
     ep.act = epilogue == GM_EPI_BIAS_LEAKY ? 1 : 0;
-    if (s0.mode == GM_A_READOUT)
-        return launch<2, 2, 2, 2, GM_A_READOUT, EPI_BIAS>(s0, s1, w, ldw, (unsigned)wb, m, n, K, ep, st);
-    if (s0.mode == GM_A_AGGREGATE)
-        return launch<2, 2, 2, 2, GM_A_AGGREGATE, EPI_BIAS>(s0, s1, w, ldw, (unsigned)wb, m, n, K, ep, st);
-    if (n <= 32) return launch<4, 1, 1, 1, GM_A_DENSE, EPI_BIAS>(s0, s1, w, ldw, (unsigned)wb, m, n, K, ep, st);
-    return launch<2, 2, 2, 2, GM_A_DENSE, EPI_BIAS>(s0, s1, w, ldw, (unsigned)wb, m, n, K, ep, st);
+    // per-shape default (tools/gemm_bench.py on MI355X): BK=16 wins for short K (enc.l0),
+    // narrow N (enc.l2) and the K=642 readout layer; BK=32 for K=512, N>=256
+    const int t = tile >= 0 ? tile : ((s0.mode == GM_A_READOUT || K <= 128 || n <= 128) ? 3 : 0);
+    if (s0.mode == GM_A_READOUT) {
+        if (t == 1) return GM_L(2, 2, 2, 4, 16, GM_A_READOUT, EPI_BIAS);
+        if (t == 2) return GM_L(2, 2, 4, 2, 16, GM_A_READOUT, EPI_BIAS);
+        if (t == 3) return GM_L(2, 2, 2, 2, 16, GM_A_READOUT, EPI_BIAS);
+        return GM_L(2, 2, 2, 2, 32, GM_A_READOUT, EPI_BIAS);
+    }
+    if (s0.mode == GM_A_AGGREGATE) return GM_L(2, 2, 2, 2, 32, GM_A_AGGREGATE, EPI_BIAS);
+    if (n <= 32) return GM_L(4, 1, 1, 1, 32, GM_A_DENSE, EPI_BIAS);
+    if (t == 1) return GM_L(2, 2, 2, 4, 16, GM_A_DENSE, EPI_BIAS);
+    if (t == 2) return GM_L(2, 2, 4, 2, 16, GM_A_DENSE, EPI_BIAS);
+    if (t == 3) return GM_L(2, 2, 2, 2, 16, GM_A_DENSE, EPI_BIAS);
+    return GM_L(2, 2, 2, 2, 32, GM_A_DENSE, EPI_BIAS);
+#undef GM_L
+}
+
+extern "C" int gm_gemm_set_tile(int32_t tile) {
+    if (tile < -1 || tile > 3) return gm_fail(GM_ERR_INVALID_ARG, "gm_gemm_set_tile: tile in [-1, 3]");
+    g_tile = tile;
+    return GM_OK;
 }
 
 extern "C" int gm_linear_f32(const float* x, int64_t ldx, const float* w, int64_t ldw, const float* b, int32_t m,

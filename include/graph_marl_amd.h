@@ -195,6 +195,9 @@ typedef struct {
 int gm_gemm_f32(const gm_a_src* src0, const gm_a_src* src1, const float* w, int64_t ldw, const float* b, int32_t m,
                 int32_t n, int32_t epilogue, float* y, int64_t ldy, float* y2, int64_t ldy2, const float* c_in,
                 int64_t ldc, float* act_out, void* stream);
+/* Tuning knob: tile configuration of gm_gemm_f32 (-1 = per-shape default; 0 = 128x128x32;
+ * 1 = 128x256x16; 2 = 256x128x16 (LSTM: 256x128x16); 3 = 128x128x16). Process-wide. */
+int gm_gemm_set_tile(int32_t tile);
 
 #ifdef __cplusplus
 }

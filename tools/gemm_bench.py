@@ -1,0 +1,100 @@
+#!/usr/bin/env python3
+"""GEMM microbenchmark on the rollout's layer shapes: gm_gemm_f32 vs hipBLASLt fp32
+(torch.nn.functional.linear), interleaved rounds in one process (cdna guide rule 24)."""
+import importlib
+import json
+import os
+import sys
+
+import torch
+import torch.nn.functional as F
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+FU = importlib.import_module("graph-marl_amd.fused")
+
+SHAPES = [  # name, M, N, K
+    ("dqn.l1", 81920, 512, 642), ("dqn.l2", 81920, 256, 512), ("enc.l0", 81920, 512, 88),
+    ("enc.l1", 81920, 256, 512), ("enc.l2", 81920, 128, 256), ("lstm", 81920, 512, 256),
+]
+
+
+TILES = [int(t) for t in os.environ.get("TILES", "-1,0,1,2,3").split(",")]
+
+
+def timeit(fn, reps=20):
+    fn()
+    torch.cuda.synchronize()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(reps):
+        fn()
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) / reps * 1e3  # us
+
+
+def main():
+    torch.manual_seed(0)
+    out = {}
+    for name, m, n, k in SHAPES:
+        ldx = (k + 3) // 4 * 4
+        buf = torch.randn(m, ldx, device="cuda")
+        x = buf[:, :k]
+        w = torch.randn(n, k, device="cuda") / k ** 0.5
+        b = torch.randn(n, device="cuda")
+        wp, ldw = FU._pad_cols(w)
+        y = torch.empty(m, n, device="cuda")
+        xc = x.contiguous()
+
+        def mine():
+            FU.gemm(FU.dense(buf.data_ptr(), ldx, k), None, wp.data_ptr(), ldw, b.data_ptr(), m, n, 1, y.data_ptr(), n)
+
+        def blas():
+            F.linear(xc, w, b)
+
+        lib = FU._setup()
+        r = {f"tile{t}": [] for t in TILES}
+        r["hipblaslt"] = []
+        for _ in range(3):
+            for t in TILES:
+                lib.gm_gemm_set_tile(t)
+                r[f"tile{t}"].append(timeit(mine))
+            r["hipblaslt"].append(timeit(blas))
+        lib.gm_gemm_set_tile(-1)
+        fl = 2.0 * m * n * k
+        out[name] = {k2: {"us": round(min(v), 1), "tflops": round(fl / (min(v) * 1e-6) / 1e12, 1)} for k2, v in r.items()}
+        print(name, json.dumps(out[name]), flush=True)
+    # fused LSTM cell GEMM (dense [x|h] source, gate epilogue)
+    M_ = importlib.import_module("graph-marl_amd.model")
+    H, m = 128, 81920
+    cell = M_.LSTMCell(H, H).cuda()
+    x = torch.randn(m, H, device="cuda")
+    st = torch.randn(m, 2 * H, device="cuda")
+    wp, ldw, bp = FU.pack_lstm(cell)
+    S = torch.empty(m, 2 * H, device="cuda")
+    nbr = torch.randint(0, 20, (m // 20, 20, 3), device="cuda", dtype=torch.int32)
+
+    def lstm_dense():
+        FU.gemm(FU.dense(x.data_ptr(), H, H), FU.dense(st.data_ptr(), 2 * H, H), wp.data_ptr(), ldw, bp.data_ptr(),
+                m, 4 * H, FU.GM_EPI_LSTM, S.data_ptr(), 2 * H, S[:, H:].data_ptr(), 2 * H, st[:, H:].data_ptr(), 2 * H)
+
+    def lstm_agg():
+        FU.gemm(FU.aggregate(st.data_ptr(), 2 * H, H, nbr, 20), FU.dense(st.data_ptr(), 2 * H, H), wp.data_ptr(),
+                ldw, bp.data_ptr(), m, 4 * H, FU.GM_EPI_LSTM, S.data_ptr(), 2 * H, S[:, H:].data_ptr(), 2 * H,
+                st[:, H:].data_ptr(), 2 * H)
+
+    lib = FU._setup()
+    for name, fn in (("lstm_fused", lstm_dense), ("lstm_agg_fused", lstm_agg)):
+        r = {0: [], 2: []}
+        for _ in range(3):
+            for t in r:
+                lib.gm_gemm_set_tile(t)
+                r[t].append(timeit(fn))
+        lib.gm_gemm_set_tile(-1)
+        fl = 2.0 * m * 4 * H * 2 * H
+        print(name, json.dumps({f"tile{t}": {"us": round(min(v), 1), "tflops": round(fl / (min(v) * 1e-6) / 1e12, 1)}
+                                for t, v in r.items()}), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -21,6 +21,7 @@ for s in "$@"; do
         tests) step gpu_tests 900 python -m pytest tests -m gpu -x -q --tb=short --timeout=300 -p no:cacheprovider || exit $? ;;
         envtests) step env_tests 600 python -m pytest tests/test_env_gpu.py -x -q --tb=short --timeout=300 -p no:cacheprovider || exit $? ;;
         nettests) step net_tests 600 python -m pytest tests/test_netmon_gpu.py tests/test_train_gpu.py -x -q --tb=short --timeout=300 -p no:cacheprovider || exit $? ;;
+        gemm) step gemm 300 python tools/gemm_bench.py || exit $? ;;
         bench) step bench 600 python bench.py || exit $? ;;
         benchq) step bench 300 python bench.py --no-cpu-baseline --steps 100 || exit $? ;;
         prof) step prof 600 rocprofv3 --kernel-trace --stats -T --output-format csv -d gpurun_out/prof -o bench \
