@@ -18,6 +18,8 @@ GM_INFO_FIELDS = 9
 INFO_KEYS = ["looped", "throughput", "dropped", "blocked", "n_delays", "sum_delays", "n_arrived",
              "sum_delays_arrived", "sum_spr"]
 TOPO_FIXED, TOPO_RANDOM, TOPO_LIST, TOPO_SEQUENTIAL = 0, 1, 2, 3
+GM_EVAL_FIELDS = 5
+EVAL_KEYS = ["total_edge_load", "occupied_edges", "packets_on_edges", "total_packet_size", "sum_packet_distances"]
 
 # every symbol the header declares (checked by tests/test_capi.py)
 EXPORTS = [
@@ -25,7 +27,9 @@ EXPORTS = [
     "gm_env_step", "gm_env_observe", "gm_env_topology", "gm_env_final_info", "gm_policy_egreedy",
     "gm_env_get_state", "gm_build_seed_list", "gm_mp_aggregate", "gm_mp_aggregate_bwd", "gm_netmon_readout",
     "gm_netmon_readout_bwd", "gm_lstm_pointwise", "gm_lstm_pointwise_bwd", "gm_linear_f32", "gm_gemm_f32",
-    "gm_gemm_set_tile",
+    "gm_gemm_set_tile", "gm_simple_create", "gm_simple_destroy", "gm_simple_reset", "gm_simple_step",
+    "gm_simple_observe", "gm_simple_policy_egreedy", "gm_simple_get_state", "gm_env_set_topology",
+    "gm_policy_shortest_path",
 ]
 
 
@@ -44,7 +48,7 @@ class ObsBuffers(C.Structure):
 
 
 class StepDetail(C.Structure):
-    _fields_ = [("done_steps", C.c_void_p), ("done_opt", C.c_void_p), ("success", C.c_void_p)]
+    _fields_ = [("done_steps", C.c_void_p), ("done_opt", C.c_void_p), ("success", C.c_void_p), ("eval", C.c_void_p)]
 
 
 class EnvState(C.Structure):
@@ -89,6 +93,8 @@ def lib():
     L.gm_lstm_pointwise_bwd.argtypes = [vp, vp, vp, vp, vp, i32, i32, vp, vp, vp]
     L.gm_linear_f32.argtypes = [vp, i64, vp, i64, vp, i32, i32, i32, i32, vp, i64, vp]
     L.gm_gemm_set_tile.argtypes = [i32]
+    L.gm_env_set_topology.argtypes = [vp, i32, i64, vp, i32, i32]
+    L.gm_policy_shortest_path.argtypes = [vp, vp, vp]
     _lib = L
     return L
 

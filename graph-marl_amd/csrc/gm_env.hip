@@ -47,7 +47,7 @@ int gm_fail(int code, const std::string& msg) {
 
 struct EnvDev {
     int n_env, N, A, E;
-    int cong, amask_on, ttl, topo_mode, n_list, n_excl;
+    int cong, amask_on, ttl, topo_mode, n_list, n_excl, seq_stride;
     int64_t fixed_seed;
     const int64_t* list;
     const int64_t* excl;
@@ -455,7 +455,7 @@ __global__ __launch_bounds__(64) void k_env_reset(EnvDev d, const uint8_t* mask,
         if (d.n_list > 1) {
             idx = d.seq_index[env];
             __syncthreads();
-            if (l == 0) d.seq_index[env] = (idx + 1) % d.n_list;
+            if (l == 0) d.seq_index[env] = (idx + d.seq_stride) % d.n_list;
         }
         seed = d.list[idx];
     }
@@ -576,6 +576,28 @@ __global__ __launch_bounds__(64) void k_env_step(EnvDev d, const int32_t* act, S
             now = s.ea[chosen] ^ s.eb[chosen] ^ now;
             if ((vis >> now) & 1ull) looped = true;
             else vis |= 1ull << now;
+        }
+    }
+
+    // eval-only statistics after admission (routing.py:414-441): sums in edge / packet order
+    if (out.det.eval) {
+        double tel = 0.0, tps = 0.0;
+        int occ = 0;
+        for (int e = 0; e < E; e++) {
+            double le = e < WAVE ? readlane_f64(ld0, e) : readlane_f64(ld1, e - WAVE);
+            tel = tel + le;
+            occ += le > 0.0;
+        }
+        for (int i = 0; i < A; i++) tps = tps + readlane_f64(size, i);
+        const int on_edges = __popcll(ballot(own && edge != -1));
+        const int dist = wave_sum_i32(own ? (int)d.apsp[((size_t)env * N + now) * N + target] : 0);
+        if (l == 0) {
+            double* ev = out.det.eval + (size_t)env * GM_EVAL_FIELDS;
+            ev[GM_EVAL_TOTAL_EDGE_LOAD] = tel;
+            ev[GM_EVAL_OCCUPIED_EDGES] = (double)occ;
+            ev[GM_EVAL_PACKETS_ON_EDGES] = (double)on_edges;
+            ev[GM_EVAL_TOTAL_PACKET_SIZE] = tps;
+            ev[GM_EVAL_SUM_PACKET_DISTANCES] = (double)dist;
         }
     }
 
@@ -753,6 +775,85 @@ __global__ __launch_bounds__(64) void k_policy_egreedy(EnvDev d, const float* q,
     }
 }
 
+// ShortestPath heuristic (src/policy.py:90-139): each packet takes the first hop of
+// networkx's weighted shortest path (nx.shortest_path(G, weight="weight"),
+// src/env/network.py:279) towards its target. Lane s runs networkx's Dijkstra from
+// source s with its exact tie-breaking: the heap pops the smallest (distance, push
+// counter); a node's path is replaced only on a strictly shorter distance; neighbours
+// are relaxed in G's adjacency order = edge creation order (network.py:179-186).
+// Only the latest push of a node can be live, so the heap is the per-node
+// (seen, counter) pair. first[s][t] = first hop on the s -> t path.
+__global__ __launch_bounds__(64) void k_policy_shortest_path(EnvDev d, int32_t* actions) {
+    const int env = blockIdx.x;
+    const int l = lane_id();
+    const int N = d.N, A = d.A;
+    __shared__ EnvLds s;
+    __shared__ uint8_t first[MAX_NODES * MAX_NODES];
+    __shared__ int16_t seen[MAX_NODES * WAVE];
+    __shared__ int16_t cnt[MAX_NODES * WAVE];
+    load_topology_lds(d, env, s);
+    constexpr int16_t INF = 0x7fff;
+    if (l < N) {
+        const int src = l;
+        for (int u = 0; u < N; u++) seen[u * WAVE + l] = INF;
+        seen[src * WAVE + l] = 0;
+        cnt[src * WAVE + l] = 0;
+        first[src * N + src] = (uint8_t)src;
+        int c = 1;
+        uint64_t done = 0;
+        for (int it = 0; it < N; it++) {
+            int v = -1, bd = INF, bc = 0;
+            for (int u = 0; u < N; u++) {
+                if ((done >> u) & 1ull) continue;
+                const int du = seen[u * WAVE + l];
+                if (du == INF) continue;
+                const int cu = cnt[u * WAVE + l];
+                if (v < 0 || du < bd || (du == bd && cu < bc)) {
+                    v = u;
+                    bd = du;
+                    bc = cu;
+                }
+            }
+            if (v < 0) break;
+            done |= 1ull << v;
+            int e3[3] = {s.nbr_edge[v * 3], s.nbr_edge[v * 3 + 1], s.nbr_edge[v * 3 + 2]};
+            for (int i = 1; i < 3; i++)  // incident edges in creation (edge id) order
+                for (int j = i; j > 0 && e3[j] < e3[j - 1]; j--) {
+                    int t = e3[j];
+                    e3[j] = e3[j - 1];
+                    e3[j - 1] = t;
+                }
+            for (int k = 0; k < 3; k++) {
+                const int e = e3[k];
+                const int u = s.ea[e] ^ s.eb[e] ^ v;
+                if ((done >> u) & 1ull) continue;
+                const int vu = bd + (int)s.elen[e];
+                const int su = seen[u * WAVE + l];
+                if (su == INF || vu < su) {
+                    seen[u * WAVE + l] = (int16_t)vu;
+                    cnt[u * WAVE + l] = (int16_t)c++;
+                    first[src * N + u] = v == src ? (uint8_t)u : first[src * N + v];
+                }
+            }
+        }
+    }
+    __syncthreads();
+    if (l < A) {
+        const size_t p = (size_t)env * A + l;
+        const int now = d.now[p], target = d.target[p];
+        int a = 0;
+        if (now != target) {
+            const int nx = first[now * N + target];
+            for (int k = 0; k < 3; k++)
+                if (s.nbr[now * 3 + k] == nx) {
+                    a = k + 1;
+                    break;
+                }
+        }
+        actions[p] = a;
+    }
+}
+
 __global__ void k_rng_seed(EnvDev d, const uint32_t* seeds) {
     int env = blockIdx.x * blockDim.x + threadIdx.x;
     if (env >= d.n_env) return;
@@ -920,6 +1021,7 @@ extern "C" int gm_env_create(const gm_env_config* cfg, const uint32_t* env_seeds
     d.fixed_seed = cfg->topo_seed;
     d.n_list = (int)env->list.size();
     d.n_excl = (int)env->excl.size();
+    d.seq_stride = 1;
     int rc = GM_OK;
 #define ALLOC(ptr, n) \
     if ((rc = dalloc(env, &(ptr), (n))) != GM_OK) { gm_env_destroy(env); return rc; }
@@ -1014,6 +1116,49 @@ extern "C" int gm_env_step(gm_env* env, const int32_t* actions, float* reward, u
     gm_obs_buffers o = obs ? *obs : gm_obs_buffers{};
     hipLaunchKernelGGL(k_env_step, dim3(env->d.n_env), dim3(64), 0, (hipStream_t)stream, env->d, actions, so, o);
     return check_launch();
+}
+
+__global__ void k_topology_rewind(EnvDev d, int interleave) {
+    const int env = blockIdx.x * blockDim.x + threadIdx.x;
+    if (env >= d.n_env) return;
+    d.seq_index[env] = interleave ? env % d.n_list : 0;
+    d.topo_ready[env] = 0;
+}
+
+extern "C" int gm_policy_shortest_path(gm_env* env, int32_t* actions, void* stream) {
+    if (!env || !actions) return gm_fail(GM_ERR_INVALID_ARG, "gm_policy_shortest_path: null argument");
+    hipLaunchKernelGGL(k_policy_shortest_path, dim3(env->d.n_env), dim3(64), 0, (hipStream_t)stream, env->d, actions);
+    return check_launch();
+}
+
+extern "C" int gm_env_set_topology(gm_env* env, int32_t topo_mode, int64_t topo_seed, const int64_t* seed_list,
+                                   int32_t n_seed_list, int32_t interleave) {
+    if (!env || topo_mode < 0 || topo_mode > 3) return gm_fail(GM_ERR_INVALID_ARG, "gm_env_set_topology: bad mode");
+    if ((topo_mode == GM_TOPO_LIST || topo_mode == GM_TOPO_SEQUENTIAL) && (n_seed_list <= 0 || !seed_list))
+        return gm_fail(GM_ERR_INVALID_ARG, "gm_env_set_topology: seed list required for LIST/SEQUENTIAL");
+    GM_HIP(hipSetDevice(env->device));
+    GM_HIP(hipDeviceSynchronize());  // no reset in flight reads the old list
+    EnvDev& d = env->d;
+    if (n_seed_list > 0 && seed_list) {
+        env->list.assign(seed_list, seed_list + n_seed_list);
+        int64_t* list_d = nullptr;
+        int rc = dalloc(env, &list_d, env->list.size());
+        if (rc != GM_OK) return rc;
+        GM_HIP(hipMemcpy(list_d, env->list.data(), env->list.size() * sizeof(int64_t), hipMemcpyHostToDevice));
+        d.list = list_d;
+        d.n_list = (int)env->list.size();
+    }
+    d.topo_mode = topo_mode;
+    d.fixed_seed = topo_seed;
+    env->cfg.topo_mode = topo_mode;
+    env->cfg.topo_seed = topo_seed;
+    d.seq_stride = interleave ? d.n_env : 1;
+    hipLaunchKernelGGL(k_topology_rewind, dim3((unsigned)((d.n_env + 63) / 64)), dim3(64), 0, 0, d,
+                       (int)(interleave && d.n_list > 0));
+    int rc = check_launch();
+    if (rc != GM_OK) return rc;
+    GM_HIP(hipDeviceSynchronize());
+    return GM_OK;
 }
 
 extern "C" int gm_env_observe(gm_env* env, const gm_obs_buffers* obs, void* stream) {

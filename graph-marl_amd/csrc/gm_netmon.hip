@@ -1,7 +1,7 @@
 // gm_netmon.hip — NetMon message passing (reference src/model.py:206-229,
 // 476-631) as HBM-bound HIP kernels for gfx950.
 //
-// Graph layout: node rows h[G*N][H] (fp32, row-major, H % 4 == 0), neighbour
+// Graph layout: node rows h[G*N][H] (fp32, row-major; float4 lanes when H % 4 == 0), neighbour
 // table nbr[G][N][deg] (ELL, ascending ids, -1 = none). The reference multiplies a
 // dense (I+A) mask with h (bmm); with deg 3 that reads 4 rows per output row, so
 // the aggregate is a gather of 4 contiguous 512-byte rows per node with float4
@@ -19,10 +19,32 @@ namespace {
 
 constexpr int MAXDEG = 8;
 
-__device__ __forceinline__ float4 f4add(float4 a, float4 b) {
-    return make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w);
+// V-wide fp32 vectors (V = 4, 2 or 1 chosen from H's alignment on the host)
+template <int V> struct Vec { float v[V]; };
+template <int V> __device__ __forceinline__ Vec<V> ldv(const float* p) {
+    Vec<V> r;
+    if constexpr (V == 4) {
+        float4 t = *reinterpret_cast<const float4*>(p);
+        r.v[0] = t.x; r.v[1] = t.y; r.v[2] = t.z; r.v[3] = t.w;
+    } else if constexpr (V == 2) {
+        float2 t = *reinterpret_cast<const float2*>(p);
+        r.v[0] = t.x; r.v[1] = t.y;
+    } else {
+        r.v[0] = *p;
+    }
+    return r;
 }
-__device__ __forceinline__ float4 f4scale(float4 a, float s) { return make_float4(a.x * s, a.y * s, a.z * s, a.w * s); }
+template <int V> __device__ __forceinline__ void stv(float* p, const Vec<V>& a) {
+    if constexpr (V == 4) *reinterpret_cast<float4*>(p) = make_float4(a.v[0], a.v[1], a.v[2], a.v[3]);
+    else if constexpr (V == 2) *reinterpret_cast<float2*>(p) = make_float2(a.v[0], a.v[1]);
+    else *p = a.v[0];
+}
+template <int V> __device__ __forceinline__ Vec<V> zerov() {
+    Vec<V> r;
+#pragma unroll
+    for (int i = 0; i < V; i++) r.v[i] = 0.f;
+    return r;
+}
 
 // sorted member list {n} ∪ nbr(n) (ascending node id) — the summation order of a
 // sequential dense row product (I+A)[n,:] · h
@@ -44,95 +66,101 @@ __device__ __forceinline__ int members(const int32_t* nb, int deg, int n, int* o
 
 // forward: out[n] = Σ_{m ∈ {n} ∪ nbr(n)} h[m]  (/ count for mean)
 // backward (symmetric adjacency): dh[j] = Σ_{n ∈ {j} ∪ nbr(j)} dout[n] * scale(n)
-template <bool BWD>
+template <bool BWD, int V>
 __global__ __launch_bounds__(256) void k_mp_aggregate(const float* __restrict__ h, const int32_t* __restrict__ nbr,
                                                       int G, int N, int deg, int H, int mode, float* __restrict__ out) {
-    const int H4 = H >> 2;
+    const int HV = H / V;
     const long long gid = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-    const long long total = (long long)G * N * H4;
+    const long long total = (long long)G * N * HV;
     if (gid >= total) return;
-    const int c4 = (int)(gid % H4);
-    const long long row = gid / H4;
+    const int cv = (int)(gid % HV);
+    const long long row = gid / HV;
     const int g = (int)(row / N), n = (int)(row % N);
     const int32_t* nb = nbr + ((size_t)g * N + n) * deg;
     int mem[MAXDEG + 1];
     const int cnt = members(nb, deg, n, mem);
-    const float4* src = reinterpret_cast<const float4*>(h) + (size_t)g * N * H4 + c4;
-    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    const float* src = h + (size_t)g * N * H + (size_t)cv * V;
+    Vec<V> acc = zerov<V>();
     for (int q = 0; q < cnt; q++) {
-        float4 v = src[(size_t)mem[q] * H4];
+        Vec<V> x = ldv<V>(src + (size_t)mem[q] * H);
         if (BWD && mode == 1) {
             const int32_t* nbm = nbr + ((size_t)g * N + mem[q]) * deg;
             int cm = 1;
             for (int k = 0; k < deg; k++) cm += nbm[k] >= 0;
-            v = f4scale(v, 1.0f / (float)cm);
+#pragma unroll
+            for (int i = 0; i < V; i++) x.v[i] = x.v[i] * (1.0f / (float)cm);
         }
-        acc = q == 0 ? v : f4add(acc, v);
+#pragma unroll
+        for (int i = 0; i < V; i++) acc.v[i] = q == 0 ? x.v[i] : acc.v[i] + x.v[i];
     }
-    if (!BWD && mode == 1) acc = make_float4(acc.x / cnt, acc.y / cnt, acc.z / cnt, acc.w / cnt);
-    reinterpret_cast<float4*>(out)[row * H4 + c4] = acc;
+    if (!BWD && mode == 1) {
+#pragma unroll
+        for (int i = 0; i < V; i++) acc.v[i] = acc.v[i] / cnt;
+    }
+    stv<V>(out + row * H + (size_t)cv * V, acc);
 }
 
 // readout: out row r of graph g = [h_final[v], h_prev[nbr(v,0..deg-1)]], v = agent_node or r.
-// Output rows may sit inside a wider joint observation (stride, 8-byte aligned) so
-// stores are float2.
+// Output rows may sit inside a wider joint observation (stride); V-wide stores.
+template <int V>
 __global__ __launch_bounds__(256) void k_readout(const float* __restrict__ hf, const float* __restrict__ hp,
                                                  const int32_t* __restrict__ nbr, const int32_t* __restrict__ agent_node,
                                                  int G, int N, int R, int deg, int H, float* __restrict__ out,
                                                  long long stride) {
-    const int H2 = H >> 1;
-    const int W2 = (deg + 1) * H2;
+    const int HV = H / V;
+    const int WV = (deg + 1) * HV;
     const long long gid = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-    const long long total = (long long)G * R * W2;
+    const long long total = (long long)G * R * WV;
     if (gid >= total) return;
-    const int c2 = (int)(gid % W2);
-    const long long row = gid / W2;
+    const int cv = (int)(gid % WV);
+    const long long row = gid / WV;
     const int g = (int)(row / R), r = (int)(row % R);
     const int v = agent_node ? agent_node[(size_t)g * R + r] : r;
-    const int seg = c2 / H2, off = c2 - seg * H2;
-    float2 val;
+    const int seg = cv / HV, off = (cv - seg * HV) * V;
+    Vec<V> val;
     if (seg == 0) {
-        val = reinterpret_cast<const float2*>(hf)[((size_t)g * N + v) * H2 + off];
+        val = ldv<V>(hf + ((size_t)g * N + v) * H + off);
     } else {
         int m = nbr[((size_t)g * N + v) * deg + seg - 1];
-        val = m >= 0 ? reinterpret_cast<const float2*>(hp)[((size_t)g * N + m) * H2 + off] : make_float2(0.f, 0.f);
+        val = m >= 0 ? ldv<V>(hp + ((size_t)g * N + m) * H + off) : zerov<V>();
     }
-    *reinterpret_cast<float2*>(out + row * stride + 2 * c2) = val;
+    stv<V>(out + row * stride + (size_t)cv * V, val);
 }
 
 // readout backward, deterministic (no atomics): node v of graph g gathers the
 // gradient of every row that read it, rows in ascending order.
+template <int V>
 __global__ __launch_bounds__(256) void k_readout_bwd(const float* __restrict__ dout, long long stride,
                                                      const int32_t* __restrict__ nbr,
                                                      const int32_t* __restrict__ agent_node, int G, int N, int R,
                                                      int deg, int H, float* __restrict__ dhf, float* __restrict__ dhp) {
-    const int H2 = H >> 1;
+    const int HV = H / V;
     const long long gid = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-    const long long total = (long long)G * N * H2;
+    const long long total = (long long)G * N * HV;
     if (gid >= total) return;
-    const int off = (int)(gid % H2);
-    const long long node = gid / H2;
+    const int off = (int)(gid % HV) * V;
+    const long long node = gid / HV;
     const int g = (int)(node / N), v = (int)(node % N);
-    float2 af = make_float2(0.f, 0.f), ap = make_float2(0.f, 0.f);
+    Vec<V> af = zerov<V>(), ap = zerov<V>();
     for (int r = 0; r < R; r++) {
         const int u = agent_node ? agent_node[(size_t)g * R + r] : r;
         const float* drow = dout + ((size_t)g * R + r) * stride;
         if (u == v) {
-            float2 x = *reinterpret_cast<const float2*>(drow + 2 * off);
-            af.x += x.x;
-            af.y += x.y;
+            Vec<V> x = ldv<V>(drow + off);
+#pragma unroll
+            for (int i = 0; i < V; i++) af.v[i] += x.v[i];
         }
         const int32_t* nb = nbr + ((size_t)g * N + u) * deg;
         for (int k = 0; k < deg; k++) {
             if (nb[k] == v) {
-                float2 x = *reinterpret_cast<const float2*>(drow + (size_t)(k + 1) * H + 2 * off);
-                ap.x += x.x;
-                ap.y += x.y;
+                Vec<V> x = ldv<V>(drow + (size_t)(k + 1) * H + off);
+#pragma unroll
+                for (int i = 0; i < V; i++) ap.v[i] += x.v[i];
             }
         }
     }
-    if (dhf) reinterpret_cast<float2*>(dhf)[node * H2 + off] = af;
-    if (dhp) reinterpret_cast<float2*>(dhp)[node * H2 + off] = ap;
+    if (dhf) stv<V>(dhf + node * H + off, af);
+    if (dhp) stv<V>(dhp + node * H + off, ap);
 }
 
 __device__ __forceinline__ float sigm(float x) { return 1.0f / (1.0f + expf(-x)); }
@@ -191,48 +219,75 @@ int launched() {
 
 }  // namespace
 
+// widest vector that divides H and keeps every access aligned (base pointers are
+// torch allocations; strides are checked)
+static int vec_width(int H, long long stride, const void* p) {
+    if (H % 4 == 0 && stride % 4 == 0 && (reinterpret_cast<uintptr_t>(p) & 15) == 0) return 4;
+    if (H % 2 == 0 && stride % 2 == 0 && (reinterpret_cast<uintptr_t>(p) & 7) == 0) return 2;
+    return 1;
+}
+
+#define GM_VLAUNCH(KER, V, GRID, ...)                                                                  \
+    do {                                                                                               \
+        if ((V) == 4) hipLaunchKernelGGL(KER<4>, GRID, dim3(256), 0, (hipStream_t)stream, __VA_ARGS__); \
+        else if ((V) == 2) hipLaunchKernelGGL(KER<2>, GRID, dim3(256), 0, (hipStream_t)stream, __VA_ARGS__); \
+        else hipLaunchKernelGGL(KER<1>, GRID, dim3(256), 0, (hipStream_t)stream, __VA_ARGS__);        \
+    } while (0)
+
+template <bool BWD>
+static int launch_agg(const float* h, const int32_t* nbr, int32_t G, int32_t N, int32_t deg, int32_t H, int32_t mode,
+                      float* out, void* stream) {
+    const int V = vec_width(H, H, h) < vec_width(H, H, out) ? vec_width(H, H, h) : vec_width(H, H, out);
+    long long total = (long long)G * N * (H / V);
+    dim3 grid(nblocks(total, 256));
+    if (V == 4) hipLaunchKernelGGL((k_mp_aggregate<BWD, 4>), grid, dim3(256), 0, (hipStream_t)stream, h, nbr, G, N, deg, H, mode, out);
+    else if (V == 2) hipLaunchKernelGGL((k_mp_aggregate<BWD, 2>), grid, dim3(256), 0, (hipStream_t)stream, h, nbr, G, N, deg, H, mode, out);
+    else hipLaunchKernelGGL((k_mp_aggregate<BWD, 1>), grid, dim3(256), 0, (hipStream_t)stream, h, nbr, G, N, deg, H, mode, out);
+    return launched();
+}
+
 extern "C" int gm_mp_aggregate(const float* h, const int32_t* nbr, int32_t G, int32_t N, int32_t deg, int32_t H,
                                int32_t mode, float* out, void* stream) {
-    if (!h || !nbr || !out || G <= 0 || N <= 0 || deg < 0 || deg > MAXDEG || H <= 0 || (H & 3) || mode < 0 || mode > 1)
-        return gm_fail(GM_ERR_INVALID_ARG, "gm_mp_aggregate: bad arguments (H % 4 == 0, deg <= 8)");
-    long long total = (long long)G * N * (H / 4);
-    hipLaunchKernelGGL(k_mp_aggregate<false>, dim3(nblocks(total, 256)), dim3(256), 0, (hipStream_t)stream, h, nbr, G,
-                       N, deg, H, mode, out);
-    return launched();
+    if (!h || !nbr || !out || G <= 0 || N <= 0 || deg < 0 || deg > MAXDEG || H <= 0 || mode < 0 || mode > 1)
+        return gm_fail(GM_ERR_INVALID_ARG, "gm_mp_aggregate: bad arguments (deg <= 8)");
+    return launch_agg<false>(h, nbr, G, N, deg, H, mode, out, stream);
 }
 
 extern "C" int gm_mp_aggregate_bwd(const float* dout, const int32_t* nbr, int32_t G, int32_t N, int32_t deg,
                                    int32_t H, int32_t mode, float* dh, void* stream) {
-    if (!dout || !nbr || !dh || G <= 0 || N <= 0 || deg < 0 || deg > MAXDEG || H <= 0 || (H & 3) || mode < 0 ||
-        mode > 1)
+    if (!dout || !nbr || !dh || G <= 0 || N <= 0 || deg < 0 || deg > MAXDEG || H <= 0 || mode < 0 || mode > 1)
         return gm_fail(GM_ERR_INVALID_ARG, "gm_mp_aggregate_bwd: bad arguments");
-    long long total = (long long)G * N * (H / 4);
-    hipLaunchKernelGGL(k_mp_aggregate<true>, dim3(nblocks(total, 256)), dim3(256), 0, (hipStream_t)stream, dout, nbr, G,
-                       N, deg, H, mode, dh);
-    return launched();
+    return launch_agg<true>(dout, nbr, G, N, deg, H, mode, dh, stream);
 }
 
 extern "C" int gm_netmon_readout(const float* hf, const float* hp, const int32_t* nbr, const int32_t* agent_node,
                                  int32_t G, int32_t N, int32_t R, int32_t deg, int32_t H, float* out, int64_t stride,
                                  void* stream) {
-    if (!hf || !hp || !nbr || !out || G <= 0 || N <= 0 || R <= 0 || deg < 0 || H <= 0 || (H & 1) || (stride & 1) ||
-        (reinterpret_cast<uintptr_t>(out) & 7) || stride < (int64_t)(deg + 1) * H)
-        return gm_fail(GM_ERR_INVALID_ARG, "gm_netmon_readout: bad arguments (even H/stride, 8-byte aligned out)");
+    if (!hf || !hp || !nbr || !out || G <= 0 || N <= 0 || R <= 0 || deg < 0 || H <= 0 ||
+        stride < (int64_t)(deg + 1) * H)
+        return gm_fail(GM_ERR_INVALID_ARG, "gm_netmon_readout: bad arguments");
     if (!agent_node && R != N) return gm_fail(GM_ERR_INVALID_ARG, "gm_netmon_readout: R must equal N without agent map");
-    long long total = (long long)G * R * (deg + 1) * (H / 2);
-    hipLaunchKernelGGL(k_readout, dim3(nblocks(total, 256)), dim3(256), 0, (hipStream_t)stream, hf, hp, nbr, agent_node,
-                       G, N, R, deg, H, out, (long long)stride);
+    int V = vec_width(H, stride, out);
+    int v2 = vec_width(H, H, hf), v3 = vec_width(H, H, hp);
+    V = V < v2 ? V : v2;
+    V = V < v3 ? V : v3;
+    long long total = (long long)G * R * (deg + 1) * (H / V);
+    GM_VLAUNCH(k_readout, V, dim3(nblocks(total, 256)), hf, hp, nbr, agent_node, G, N, R, deg, H, out,
+               (long long)stride);
     return launched();
 }
 
 extern "C" int gm_netmon_readout_bwd(const float* dout, int64_t stride, const int32_t* nbr, const int32_t* agent_node,
                                      int32_t G, int32_t N, int32_t R, int32_t deg, int32_t H, float* dhf, float* dhp,
                                      void* stream) {
-    if (!dout || !nbr || G <= 0 || N <= 0 || R <= 0 || deg < 0 || H <= 0 || (H & 1) || (stride & 1))
+    if (!dout || !nbr || G <= 0 || N <= 0 || R <= 0 || deg < 0 || H <= 0)
         return gm_fail(GM_ERR_INVALID_ARG, "gm_netmon_readout_bwd: bad arguments");
-    long long total = (long long)G * N * (H / 2);
-    hipLaunchKernelGGL(k_readout_bwd, dim3(nblocks(total, 256)), dim3(256), 0, (hipStream_t)stream, dout,
-                       (long long)stride, nbr, agent_node, G, N, R, deg, H, dhf, dhp);
+    int V = vec_width(H, stride, dout);
+    if (dhf) { int v = vec_width(H, H, dhf); V = V < v ? V : v; }
+    if (dhp) { int v = vec_width(H, H, dhp); V = V < v ? V : v; }
+    long long total = (long long)G * N * (H / V);
+    GM_VLAUNCH(k_readout_bwd, V, dim3(nblocks(total, 256)), dout, (long long)stride, nbr, agent_node, G, N, R, deg, H,
+               dhf, dhp);
     return launched();
 }
 

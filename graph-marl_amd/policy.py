@@ -1,12 +1,12 @@
 """ε-greedy action selection on the device (reference src/policy.py:7-87 EpsilonGreedy).
 
 Q-values come from the DQN on the HIP linear kernels; the random draws
-(randint(4, size=A) then rand(A), every call, from each env's numpy-legacy stream)
-and the argmax/mix run in gm_policy_egreedy.
+(randint(n_actions, size=A) then rand(A), every call, from each env's numpy-legacy
+stream) and the argmax/mix run in the env's egreedy kernel (gm_policy_egreedy /
+gm_simple_policy_egreedy).
 """
 import torch
 
-from . import _lib as L
 
 
 class EpsilonGreedy:
@@ -45,11 +45,7 @@ class EpsilonGreedy:
 
     def select(self, q):
         """ε-greedy mix of argmax(q) and uniform actions, drawn from each env's stream."""
-        e = self._env
-        with L.timed("egreedy"):
-            L.check(L.lib().gm_policy_egreedy(e._h, L.ptr(q), float(self._epsilon), L.ptr(self.actions),
-                                              L.stream_ptr(e.device)))
-        return self.actions
+        return self._env.egreedy(q.contiguous(), self._epsilon, self.actions)
 
     def _decay_step(self):
         self._step += 1

@@ -26,7 +26,7 @@ TransitionBatch = namedtuple(
 
 class ReplayBuffer:
     def __init__(self, seed, capacity, n_env, n_agents, obs_dim, n_nodes, node_obs_dim, node_state_size,
-                 device, half_precision=False):
+                 device, half_precision=False, nbr_width=3):
         """capacity: transitions (env-steps) like the reference; the ring holds
         ceil(capacity / n_env) vector steps."""
         self.n_env, self.A, self.N = n_env, n_agents, n_nodes
@@ -47,49 +47,66 @@ class ReplayBuffer:
         self.reward = z(S, B, A)
         self.done = z(S, B, A, dtype=torch.bool)
         self.episode_done = z(S, dtype=torch.bool)
-        self.node_obs = z(S, B, N, node_obs_dim)
-        self.next_node_obs = z(S, B, N, node_obs_dim)
-        self.nbr = z(S, B, N, 3, dtype=torch.int8)
-        self.agent_node = z(S, B, A, dtype=torch.int8)
-        self.next_agent_node = z(S, B, A, dtype=torch.int8)
-        self.node_state = z(S, B, N, node_state_size)
+        self.graph = node_state_size > 0  # NetMon transitions carry the graph inputs
+        if self.graph:
+            self.node_obs = z(S, B, N, node_obs_dim)
+            self.next_node_obs = z(S, B, N, node_obs_dim)
+            self.nbr = z(S, B, N, nbr_width, dtype=torch.int8)
+            self.agent_node = z(S, B, A, dtype=torch.int8)
+            self.next_agent_node = z(S, B, A, dtype=torch.int8)
+            self.node_state = z(S, B, N, node_state_size)
         self.gen = torch.Generator(device=device)
         self.gen.manual_seed(seed)
 
     def nbytes(self):
         return sum(t.numel() * t.element_size() for t in self.__dict__.values() if torch.is_tensor(t))
 
-    def add(self, obs, action, reward, next_obs, done, episode_done, node_state, node_obs, nbr, agent_node,
-            next_node_obs, next_agent_node):
-        """One vector step (every argument has a leading n_env dim; node_state may be None = zeros)."""
+    def add_pre(self, obs, node_state=None, node_obs=None, nbr=None, agent_node=None):
+        """First half of a transition, recorded before the env step: the observation and the
+        NetMon inputs that produced it (node_state = the NetMon state before that call)."""
         i = self.index
         self.obs[i].copy_(obs)
+        if self.graph:
+            if node_state is None:
+                self.node_state[i].zero_()
+            else:
+                self.node_state[i].copy_(node_state)
+            self.node_obs[i].copy_(node_obs)
+            self.nbr[i].copy_(nbr)
+            self.agent_node[i].copy_(agent_node)
+
+    def add_post(self, action, reward, next_obs, done, episode_done, next_node_obs=None, next_agent_node=None):
+        """Second half, after the step; commits the slot."""
+        i = self.index
         self.action[i].copy_(action)
         self.reward[i].copy_(reward)
         self.next_obs[i].copy_(next_obs)
         self.done[i].copy_(done)
         self.episode_done[i] = bool(episode_done)
-        if node_state is None:
-            self.node_state[i].zero_()
-        else:
-            self.node_state[i].copy_(node_state)
-        self.node_obs[i].copy_(node_obs)
-        self.nbr[i].copy_(nbr)
-        self.agent_node[i].copy_(agent_node)
-        self.next_node_obs[i].copy_(next_node_obs)
-        self.next_agent_node[i].copy_(next_agent_node)
+        if self.graph:
+            self.next_node_obs[i].copy_(next_node_obs)
+            self.next_agent_node[i].copy_(next_agent_node)
         if self.count < self.slots:
             self.count += 1
         self.index = (self.index + 1) % self.slots
 
+    def add(self, obs, action, reward, next_obs, done, episode_done, node_state, node_obs, nbr, agent_node,
+            next_node_obs, next_agent_node):
+        """One vector step (every argument has a leading n_env dim; node_state may be None = zeros)."""
+        self.add_pre(obs, node_state, node_obs, nbr, agent_node)
+        self.add_post(action, reward, next_obs, done, episode_done, next_node_obs, next_agent_node)
+
     def _gather(self, slot, env):
         f = torch.float32
+        g = self.graph
         return TransitionBatch(
             (slot, env), self.obs[slot, env].to(f), self.action[slot, env].long(), self.reward[slot, env].to(f),
             self.next_obs[slot, env].to(f), self.done[slot, env], self.episode_done[slot],
-            self.node_obs[slot, env].to(f), self.nbr[slot, env].int().contiguous(),
-            self.node_state[slot, env].to(f), self.agent_node[slot, env].int().contiguous(),
-            self.next_node_obs[slot, env].to(f), self.next_agent_node[slot, env].int().contiguous(),
+            self.node_obs[slot, env].to(f) if g else None, self.nbr[slot, env].int().contiguous() if g else None,
+            self.node_state[slot, env].to(f) if g else None,
+            self.agent_node[slot, env].int().contiguous() if g else None,
+            self.next_node_obs[slot, env].to(f) if g else None,
+            self.next_agent_node[slot, env].int().contiguous() if g else None,
         )
 
     def get_batch(self, batch_size, sequence_length=1):

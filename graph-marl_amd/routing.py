@@ -188,7 +188,22 @@ class Routing:
 
     # -- NetworkEnv API -----------------------------------------------------------
     def set_eval_info(self, val):
-        self.eval_info_enabled = val
+        """Enable the eval-only step statistics (routing.py:414-441) in step()'s info."""
+        self.eval_info_enabled = bool(val)
+        if self.eval_info_enabled and not hasattr(self, "eval_stats"):
+            self.eval_stats = torch.zeros(self.n_env, L.GM_EVAL_FIELDS, dtype=torch.float64, device=self.device)
+
+    def set_topology_seeds(self, seeds, sequential=True, interleave=False):
+        """network.seeds = seeds; network.sequential_topology_seeds = sequential (the reference's
+        switch to EVAL_SEEDS before evaluation, src/main.py:553-560). interleave: env b starts at
+        seeds[b] and advances by n_env (n_env envs walk the list like consecutive episodes)."""
+        seeds = [int(x) for x in seeds]
+        self.network.seeds = seeds
+        self.network.sequential_topology_seeds = sequential
+        mode, tseed, lst = self.network.mode()
+        arr = None if lst is None else np.ascontiguousarray(np.asarray(lst, np.int64))
+        L.check(L.lib().gm_env_set_topology(self._h, mode, int(tseed), None if arr is None else arr.ctypes.data,
+                                            0 if arr is None else len(arr), int(interleave)))
 
     def reset_(self, mask=None):
         """Reset envs in place (mask: bool/uint8 [n_env] on device, None = all)."""
@@ -209,11 +224,14 @@ class Routing:
             self._actions.copy_(a)
             a = self._actions
         det = None
-        if detail is not None:
+        if detail is not None or self.eval_info_enabled:
             det = L.StepDetail()
-            det.done_steps, det.done_opt, det.success = (detail["done_steps"].data_ptr(),
-                                                         detail["done_opt"].data_ptr(),
-                                                         detail["success"].data_ptr())
+            if detail is not None:
+                det.done_steps, det.done_opt, det.success = (detail["done_steps"].data_ptr(),
+                                                             detail["done_opt"].data_ptr(),
+                                                             detail["success"].data_ptr())
+            if self.eval_info_enabled:
+                det.eval = self.eval_stats.data_ptr()
         with L.timed("env_step"):
             L.check(L.lib().gm_env_step(self._h, L.ptr(a), L.ptr(self.reward), L.ptr(self.done), L.ptr(self.info),
                                         None if det is None else C.byref(det), C.byref(self._obsbufs),
@@ -226,7 +244,22 @@ class Routing:
             act = torch.as_tensor(np.asarray(act), device=self.device)
         self.step_(act.to(self.device))
         info = {k: self.info[:, i] for i, k in enumerate(L.INFO_KEYS)}
+        if self.eval_info_enabled:
+            info.update({k: self.eval_stats[:, i] for i, k in enumerate(L.EVAL_KEYS)})
         return self.obs, self.agent_adj, self.reward, self.done.bool(), info
+
+    def egreedy(self, q, epsilon, actions):
+        """EpsilonGreedy draws (src/policy.py:44-50) from each env's stream; q [n_env, A, 4]."""
+        with L.timed("egreedy"):
+            L.check(L.lib().gm_policy_egreedy(self._h, L.ptr(q), float(epsilon), L.ptr(actions),
+                                              L.stream_ptr(self.device)))
+        return actions
+
+    def shortest_path_actions(self, actions):
+        """ShortestPath policy (src/policy.py:90-139) for every packet of every env."""
+        with L.timed("shortest_path"):
+            L.check(L.lib().gm_policy_shortest_path(self._h, L.ptr(actions), L.stream_ptr(self.device)))
+        return actions
 
     def get_nodes_adjacency(self):
         out = torch.empty(self.n_env, self.n_nodes, self.n_nodes, dtype=torch.int8, device=self.device)
@@ -251,10 +284,15 @@ class Routing:
         L.check(L.lib().gm_env_topology(self._h, None, None, None, L.ptr(out), self._stream()))
         return out
 
-    def get_final_info(self, info):
-        """Routing.get_final_info: adds the still-running packets' steps to the delays."""
+    def final_info(self):
+        """[n_env, 2] float64: sum and count of the non-zero agent steps (get_final_info)."""
         out = torch.empty(self.n_env, 2, dtype=torch.float64, device=self.device)
         L.check(L.lib().gm_env_final_info(self._h, L.ptr(out), self._stream()))
+        return out
+
+    def get_final_info(self, info):
+        """Routing.get_final_info: adds the still-running packets' steps to the delays."""
+        out = self.final_info()
         info = dict(info)
         info["sum_delays"] = info["sum_delays"] + out[:, 0]
         info["n_delays"] = info["n_delays"] + out[:, 1]

@@ -58,27 +58,32 @@ def joint_obs(env_obs, network_obs):
 
 
 def dqn_loss(netmon, model, model_tar, batches, gamma):
-    """Sequence loss of src/main.py:840-954 (no DGN attention / aux terms).
+    """Sequence loss of src/main.py:840-954 (no DGN attention / aux terms); netmon may be None.
     Returns (loss, list of q, list of q_target)."""
     L = len(batches)
     loss_q = None
     qs, qts = [], []
     last_state = last_ep_done = None
     for t, batch in enumerate(batches):
-        if t == 0:
-            netmon.state = batch.node_state
+        if netmon is None:
+            q = model(batch.obs)
+            with torch.no_grad():
+                next_q_max = model_tar(batch.next_obs).max(dim=2)[0]
         else:
-            netmon.state = last_state * (~last_ep_done).view(-1, 1, 1)
-        network_obs = netmon.forward_graph(batch.node_obs, batch.nbr, batch.agent_node)
-        obs = joint_obs(batch.obs, network_obs)
-        last_state = netmon.state
-        last_ep_done = batch.episode_done.expand(batch.obs.shape[0]) if batch.episode_done.dim() == 0 \
-            else batch.episode_done
-        q = model(obs)
-        with torch.no_grad():
-            nno = netmon.forward_graph(batch.next_node_obs, batch.nbr, batch.next_agent_node)
-            next_q = model_tar(joint_obs(batch.next_obs, nno))
-            next_q_max = next_q.max(dim=2)[0]
+            if t == 0:
+                netmon.state = batch.node_state
+            else:
+                netmon.state = last_state * (~last_ep_done).view(-1, 1, 1)
+            network_obs = netmon.forward_graph(batch.node_obs, batch.nbr, batch.agent_node)
+            obs = joint_obs(batch.obs, network_obs)
+            last_state = netmon.state
+            last_ep_done = batch.episode_done.expand(batch.obs.shape[0]) if batch.episode_done.dim() == 0 \
+                else batch.episode_done
+            q = model(obs)
+            with torch.no_grad():
+                nno = netmon.forward_graph(batch.next_node_obs, batch.nbr, batch.next_agent_node)
+                next_q = model_tar(joint_obs(batch.next_obs, nno))
+                next_q_max = next_q.max(dim=2)[0]
         target = batch.reward + (~batch.done) * gamma * next_q_max
         q_target = torch.scatter(q.detach(), -1, batch.action.unsqueeze(-1), target.unsqueeze(-1))
         term = torch.mean((q - q_target).pow(2)) / L

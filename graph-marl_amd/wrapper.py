@@ -19,9 +19,13 @@ from .model import NetMon, netmon_readout
 class NetMonWrapper:
     def __init__(self, env, netmon: NetMon, startup_iterations=1, fused=None):
         assert startup_iterations >= 1, "Number of startup iterations must be >= 1"
-        need = env.obs_dim + netmon.get_out_features()
+        # the readout is [h, h_prev of deg neighbours] with deg = the graph's max degree
+        # (src/model.py:582-589), so the graph part is (deg + 1) H wide (4H on routing graphs)
+        H = netmon.hidden_features
+        self.graph_features = (env.nbr.shape[-1] + 1) * H if netmon.output_neighbor_hidden else H
+        need = env.obs_dim + self.graph_features
         if env.obs_stride < need:
-            raise ValueError(f"env obs buffer too narrow: create Routing with obs_extra={netmon.get_out_features()}")
+            raise ValueError(f"env obs buffer too narrow: create the env with obs_extra={self.graph_features}")
         self.env = env
         self.netmon = netmon
         self.startup_iterations = startup_iterations
@@ -29,7 +33,9 @@ class NetMonWrapper:
         self.current_netmon_state = None
         self.h_prev = None
         self.obs_dim = need
-        self.fused = (netmon.rnn_type == "lstm" and netmon.output_neighbor_hidden) if fused is None else fused
+        if fused is None:
+            fused = netmon.rnn_type == "lstm" and netmon.output_neighbor_hidden and H % 32 == 0
+        self.fused = fused
         self._dirty = False
 
     def __getattr__(self, name):
@@ -40,7 +46,7 @@ class NetMonWrapper:
 
     @property
     def obs(self):
-        """joint observation [n_env, A, 6N+10+4H] (reference: concat of obs and graph obs)."""
+        """joint observation [n_env, A, obs_dim + (deg+1)H] (reference: concat of obs and graph obs)."""
         if self._dirty:
             self._materialize()
         return self.env.obs_buf[..., : self.obs_dim]

@@ -81,11 +81,20 @@ enum {
     GM_INFO_SUM_SPR, GM_INFO_FIELDS
 };
 
+/* Eval-only statistics after the admission phase (src/env/routing.py:414-441, enabled by
+ * set_eval_info), float64 [n_env, GM_EVAL_FIELDS]; the per-packet lists packet_sizes and
+ * packet_distances are reported as sums over the A packets. */
+enum {
+    GM_EVAL_TOTAL_EDGE_LOAD = 0, GM_EVAL_OCCUPIED_EDGES, GM_EVAL_PACKETS_ON_EDGES, GM_EVAL_TOTAL_PACKET_SIZE,
+    GM_EVAL_SUM_PACKET_DISTANCES, GM_EVAL_FIELDS
+};
+
 /* Optional per-packet step outputs for exact info lists (NULL to skip). */
 typedef struct {
     int32_t* done_steps;    /* [n_env, A] agent steps of a packet that finished this step, else 0 */
     int32_t* done_opt;      /* [n_env, A] max(shortest path weight, 1) of that packet             */
     uint8_t* success;       /* [n_env, A] reached its target                                      */
+    double* eval;           /* [n_env, GM_EVAL_FIELDS] eval-only statistics                       */
 } gm_step_detail;
 
 typedef struct gm_env gm_env;
@@ -110,6 +119,17 @@ int gm_env_observe(gm_env* env, const gm_obs_buffers* obs, void* stream);
  * topo_seed: int64 [n_env]. Any may be NULL. */
 int gm_env_topology(gm_env* env, int32_t* nbr, int8_t* node_adj, float* node_aux, int64_t* topo_seed,
                     void* stream);
+/* ShortestPath heuristic (src/policy.py:90-139): actions int32 [n_env, A] = 1 + index (by
+ * neighbour id) of the first hop of networkx's weighted shortest path now -> target
+ * (Dijkstra with networkx's tie-breaking, src/env/network.py:279), 0 at the target. */
+int gm_policy_shortest_path(gm_env* env, int32_t* actions, void* stream);
+/* Switch the topology source between resets (the reference's evaluation sets
+ * network.seeds = EVAL_SEEDS and sequential_topology_seeds = True, src/main.py:553-560,
+ * 1049-1053). The sequential index restarts at 0 (network.py:87); with interleave, env b
+ * starts at seed b and advances by n_env, so n_env envs walk the list like one env's
+ * consecutive episodes. Synchronous. */
+int gm_env_set_topology(gm_env* env, int32_t topo_mode, int64_t topo_seed, const int64_t* seed_list,
+                        int32_t n_seed_list, int32_t interleave);
 /* Sum and count of non-zero agent steps per env (get_final_info), float64 [n_env, 2]. */
 int gm_env_final_info(gm_env* env, double* out, void* stream);
 
@@ -198,6 +218,43 @@ int gm_gemm_f32(const gm_a_src* src0, const gm_a_src* src1, const float* w, int6
 /* Tuning knob: tile configuration of gm_gemm_f32 (-1 = per-shape default; 0 = 128x128x32;
  * 1 = 128x256x16; 2 = 256x128x16 (LSTM: 256x128x16); 3 = 128x128x16). Process-wide. */
 int gm_gemm_set_tile(int32_t tile);
+
+/* ---------------------------------------------------------------------------
+ * SimpleEnvironment (src/env/simple_environment.py:45-334; BASELINE config 1):
+ * 3 routers on a line, 1 packet at the middle router, actions {0, 1}, reward = score
+ * (-1/+1) of the router reached, done every step. Batched over n_env envs, each with
+ * its own numpy-legacy stream (seeds[env]); reset draws exactly the reference's
+ * sequence (_build_network 123-209), gm_simple_policy_egreedy draws EpsilonGreedy's
+ * randint(2, size=1) + rand(1) (src/policy.py:44-50) from the same stream.
+ * ------------------------------------------------------------------------- */
+typedef struct gm_simple_env gm_simple_env;
+typedef struct {
+    float* obs;              /* [n_env][1][obs_row_stride]: [now] (+ adjacency 9 + scores 3 if env_var != 1) */
+    int64_t obs_row_stride;
+    float* node_obs;         /* [n_env][3][1] router scores (get_node_observation) */
+    int8_t* node_adj;        /* [n_env][3][3] I + A (get_nodes_adjacency) */
+    int32_t* nbr;            /* [n_env][3][2] neighbour ids ascending, -1 padded */
+    int32_t* agent_node;     /* [n_env][1] router of the packet (get_node_agent_matrix) */
+} gm_simple_obs;
+typedef struct { /* host buffers, any may be NULL */
+    int32_t* score;          /* [n_env][3] */
+    int32_t* router_edge;    /* [n_env][3][2] Router.edge lists (-1 = none) */
+    int32_t* edge_end;       /* [n_env][2][2] Edge (start, end) */
+    int32_t* start;          /* [n_env] */
+    int32_t* now;            /* [n_env] */
+} gm_simple_state;
+int gm_simple_create(int32_t n_env, int32_t env_var, int32_t random_topology, const uint32_t* seeds_host,
+                     int32_t device, gm_simple_env** out);
+int gm_simple_destroy(gm_simple_env* env);
+/* SimpleEnvironment.reset (simple_environment.py:211-213); reset_mask (device u8 [n_env]) or NULL = all */
+int gm_simple_reset(gm_simple_env* env, const uint8_t* reset_mask, const gm_simple_obs* obs, void* stream);
+/* SimpleEnvironment.step (simple_environment.py:283-315): actions int32 [n_env] in {0, 1} */
+int gm_simple_step(gm_simple_env* env, const int32_t* actions, float* reward, uint8_t* done,
+                   const gm_simple_obs* obs, void* stream);
+int gm_simple_observe(gm_simple_env* env, const gm_simple_obs* obs, void* stream);
+int gm_simple_policy_egreedy(gm_simple_env* env, const float* q, double epsilon, int32_t* actions, void* stream);
+/* synchronous; fails with GM_ERR_INVALID_ARG if an invalid action was stepped since the last call */
+int gm_simple_get_state(gm_simple_env* env, gm_simple_state* st);
 
 #ifdef __cplusplus
 }

@@ -471,6 +471,160 @@ def gen_train(out, Network, Routing, EVAL_SEEDS, NetMon, DQN, interpolate_model)
     np.savez_compressed(out, **d)
 
 
+# ---------------------------------------------------------------------------
+# SimpleEnvironment traces (src/env/simple_environment.py) with EpsilonGreedy
+# draws (src/policy.py:44-50) on the same global stream
+# ---------------------------------------------------------------------------
+SIMPLE_CONFIGS = [(0, 1, 1), (1, 1, 0), (42, 3, 1), (7, 2, 1), (123, 1, 1), (5, 3, 0)]
+
+
+def simple_snapshot(env):
+    score = np.array([r.score for r in env.router], np.int32)
+    redge = np.full((3, 2), -1, np.int32)
+    for i, r in enumerate(env.router):
+        for k, e in enumerate(r.edge):
+            redge[i, k] = int(e)
+    ends = np.array([[e.start, e.end] for e in env.edges], np.int32)
+    return score, redge, ends, np.int32(env.start_node)
+
+
+def gen_simple(out, SimpleEnvironment):
+    d = {"configs": np.array(SIMPLE_CONFIGS, np.int64)}
+    T, eps = 40, 0.5
+    for ci, (seed, env_var, rt) in enumerate(SIMPLE_CONFIGS):
+        np.random.seed(seed)
+        env = SimpleEnvironment(env_var=env_var, random_topology=bool(rt))
+        qrng = np.random.RandomState(1000 + seed)
+        rec = {k: [] for k in ("reset", "q", "act", "obs", "reward", "score", "redge", "ends", "start",
+                               "node_obs", "node_adj", "node_agent")}
+        for t in range(T):
+            if t % 3 == 0:
+                obs, adj = env.reset()
+                rec["reset"].append(1)
+            else:
+                rec["reset"].append(0)
+            sc, re_, en, st = simple_snapshot(env)
+            rec["score"].append(sc)
+            rec["redge"].append(re_)
+            rec["ends"].append(en)
+            rec["start"].append(st)
+            rec["node_obs"].append(env.get_node_observation())
+            rec["node_adj"].append(env.get_nodes_adjacency().copy())
+            rec["node_agent"].append(env.get_node_agent_matrix())
+            q = qrng.standard_normal((1, 2)).astype(np.float32)
+            random_actions = np.random.randint(2, size=1)
+            random_filter = np.random.rand(1) < eps
+            act = np.argmax(q, axis=-1) * ~random_filter + random_filter * random_actions
+            obs, adj, reward, done, info = env.step(act)
+            assert done[0]
+            rec["q"].append(q)
+            rec["act"].append(act.astype(np.int32))
+            rec["obs"].append(np.asarray(obs, np.float32))
+            rec["reward"].append(np.asarray(reward, np.float32))
+        for k, v in rec.items():
+            d[f"c{ci}_{k}"] = np.array(v)
+    np.savez_compressed(out, **d)
+    print("simple:", out)
+
+
+# ---------------------------------------------------------------------------
+# ShortestPath heuristic (src/policy.py:90-139): networkx first hops and traces
+# ---------------------------------------------------------------------------
+def first_hops(net):
+    n = net.n_nodes
+    f = np.zeros((n, n), np.int32)
+    for i in range(n):
+        for j in range(n):
+            f[i, j] = i if i == j else net.shortest_paths[i][j][1]
+    return f
+
+
+def gen_shortest(out, Network, Routing, EVAL_SEEDS, ShortestPath):
+    d = {}
+    nets = []
+    for s in [476, 923430603] + list(EVAL_SEEDS[:30]):
+        net = Network(n_nodes=20, random_topology=False, topology_init_seed=s)
+        net.reset()
+        nets.append(net)
+    for n, main_seed, count in [(10, 21, 8), (50, 22, 6), (64, 23, 4)]:
+        np.random.seed(main_seed)
+        net = Network(n_nodes=n, random_topology=True, excluded_seeds=EVAL_SEEDS)
+        for _ in range(count):
+            net.reset()
+            nets.append(copy.deepcopy(net))
+    for i, net in enumerate(nets):
+        d[f"t{i}_edges"] = np.array([[e.start, e.end, e.length] for e in net.edges], np.int64)
+        d[f"t{i}_first"] = first_hops(net)
+    d["n_tables"] = np.int64(len(nets))
+
+    class _Args:
+        pass
+
+    for name, mode, seed, T, ep in [("fixed476", "fixed", 0, 100, 100), ("rand20", "random", 3, 100, 25)]:
+        if mode == "fixed":
+            net = Network(n_nodes=20, random_topology=False, topology_init_seed=476)
+        else:
+            net = Network(n_nodes=20, random_topology=True, topology_init_seed=476, excluded_seeds=EVAL_SEEDS)
+        env = Routing(net, 20, 1, enable_congestion=True, enable_action_mask=False, ttl=0)
+        pol = ShortestPath(env, None, 4, _Args())
+        np.random.seed(seed)
+        env.reset()
+        acts, rews = [], []
+        for t in range(T):
+            a = pol(None, None)
+            _, _, r, _, _ = env.step(a)
+            acts.append(np.asarray(a, np.int32))
+            rews.append(np.asarray(r, np.float32))
+            if (t + 1) % ep == 0:
+                env.reset()
+        d[f"trace_{name}_actions"] = np.stack(acts)
+        d[f"trace_{name}_reward"] = np.stack(rews)
+        d[f"trace_{name}_cfg"] = np.array([seed, T, ep], np.int64)
+    np.savez_compressed(out, **d)
+    print("shortest:", out)
+
+
+# ---------------------------------------------------------------------------
+# Evaluation reducer (src/eval.py) with the ShortestPath policy on EVAL_SEEDS, set up
+# like `main.py --eval --policy=heuristic` (src/main.py:409-575), and the CLI flags
+# ---------------------------------------------------------------------------
+EVAL_CONFIGS = [(0, 6, 40, 20, 20), (5, 4, 60, 20, 12), (9, 3, 30, 20, 8)]  # seed, episodes, steps, N, A
+
+
+def gen_eval(out, Network, Routing, EVAL_SEEDS, ShortestPath, evaluate):
+    d = {"configs": np.array(EVAL_CONFIGS, np.int64)}
+
+    class _Args:
+        pass
+
+    for ci, (seed, episodes, steps, n, a) in enumerate(EVAL_CONFIGS):
+        np.random.seed(seed)
+        net = Network(n_nodes=n, random_topology=True, n_random_seeds=0, topology_init_seed=476,
+                      excluded_seeds=EVAL_SEEDS)
+        env = Routing(net, a, 1, enable_congestion=True, enable_action_mask=False, ttl=0)
+        env.reset()  # reset_and_get_sizes
+        pol = ShortestPath(env, None, 4, _Args())
+        env.network.seeds = EVAL_SEEDS
+        env.network.sequential_topology_seeds = True
+        m = evaluate(env, pol, episodes, steps, True)
+        keys = sorted(m)
+        d[f"c{ci}_keys"] = np.array(keys)
+        d[f"c{ci}_values"] = np.array([float(m[k]) for k in keys], np.float64)
+    np.savez_compressed(out, **d)
+    print("eval:", out)
+
+
+def gen_cli_flags(out, ref):
+    import json
+    import re
+
+    src = open(os.path.join(ref, "main.py")).read()
+    flags = sorted(set(re.findall(r'add_argument\(\s*"(--[a-z0-9-]+)"', src)))
+    with open(out, "w") as f:
+        json.dump(flags, f, indent=1)
+    print("cli flags:", len(flags))
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--ref", default="/root/reference/src")
@@ -485,6 +639,9 @@ def main():
     from env.constants import EVAL_SEEDS  # noqa: E402
     from model import NetMon, DQN  # noqa: E402
     from util import interpolate_model  # noqa: E402
+    from env.simple_environment import SimpleEnvironment  # noqa: E402
+    from policy import ShortestPath  # noqa: E402
+    from eval import evaluate  # noqa: E402
 
     only = set(args.only.split(",")) if args.only else None
     if only is None or "seeds" in only:
@@ -499,6 +656,14 @@ def main():
         gen_netmon(os.path.join(HERE, "netmon.npz"), Network, Routing, EVAL_SEEDS, NetMon, DQN)
     if only is None or "train" in only:
         gen_train(os.path.join(HERE, "train.npz"), Network, Routing, EVAL_SEEDS, NetMon, DQN, interpolate_model)
+    if only is None or "shortest" in only:
+        gen_shortest(os.path.join(HERE, "shortest.npz"), Network, Routing, EVAL_SEEDS, ShortestPath)
+    if only is None or "eval" in only:
+        gen_eval(os.path.join(HERE, "eval.npz"), Network, Routing, EVAL_SEEDS, ShortestPath, evaluate)
+    if only is None or "cli" in only:
+        gen_cli_flags(os.path.join(HERE, "cli_flags.json"), args.ref)
+    if only is None or "simple" in only:
+        gen_simple(os.path.join(HERE, "simple.npz"), SimpleEnvironment)
 
 
 if __name__ == "__main__":

@@ -1,0 +1,45 @@
+"""End-to-end CLI training runs (src/main.py flow) on the device."""
+import importlib
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+CI_FLAGS = ("--model=dqn --hidden-dim=8 --random-topology=1 --mini-batch-size=32 --device=cpu --episode-steps=1 "
+            "--eval-episode-steps=1 --lr=0.001 --tau=0.01 --netmon --netmon-encoder-dim=4 --hidden-dim=4 "
+            "--netmon-dim=2 --netmon-iterations=1 --sequence-length=1 --step-before-train=1_000 --capacity=10_000 "
+            "--eval-episodes=100 --total-steps=5_000 --env-type=simple --epsilon=0.1 --epsilon-decay=1.0 --seed=0 "
+            "--disable-progress")
+
+
+def test_reference_ci_train_example(tmp_path):
+    """The reference's CI check (.github/workflows/train-example.yml): train DQN + NetMon on
+    the simple env, then evaluation must report reward_mean 1.0."""
+    main = importlib.import_module("graph-marl_amd.main")
+    m = main.main(CI_FLAGS.split() + [f"--log-dir={tmp_path}"])
+    assert m["reward_mean"] == 1.0
+    assert os.path.exists(tmp_path / "model_last.pt")
+
+
+def test_routing_netmon_train_checkpoint_and_reload(tmp_path):
+    main = importlib.import_module("graph-marl_amd.main")
+    common = ["--env-type=routing", "--model=dqn", "--netmon", "--netmon-iterations=1", "--n-env=64",
+              "--episode-steps=50", "--eval-episodes=64", "--eval-episode-steps=20", "--disable-progressbar"]
+    m = main.main(common + ["--total-steps=300", "--step-before-train=100", "--mini-batch-size=32",
+                            "--sequence-length=4", "--capacity=20000", f"--log-dir={tmp_path}"])
+    for k in ("reward_mean", "delays_mean", "throughput_mean", "spr_mean"):
+        assert np.isfinite(m[k]), k
+    ck = tmp_path / "model_last.pt"
+    assert ck.exists()
+    m2 = main.main(common + ["--eval", f"--model-load-path={ck}", "--policy=trained"])
+    assert np.isfinite(m2["reward_mean"])
+
+
+def test_routing_no_netmon_train(tmp_path):
+    main = importlib.import_module("graph-marl_amd.main")
+    m = main.main(["--env-type=routing", "--model=dqn", "--random-topology=0", "--n-env=32", "--total-steps=200",
+                   "--step-before-train=50", "--mini-batch-size=16", "--episode-steps=100", "--eval-episodes=8",
+                   "--eval-episode-steps=20", "--disable-progressbar", f"--log-dir={tmp_path}"])
+    assert np.isfinite(m["reward_mean"])
