@@ -40,7 +40,8 @@ class EpsilonGreedy:
         e = self._env
         with torch.no_grad():
             x2 = obs.reshape(-1, obs.shape[-1])
-            q = self._model.forward_rows(x2, x2.stride(0), obs.shape[-1], self._buf)
+            # rows are spaced by the agent-dim stride (reshape may renormalise size-1 dims)
+            q = self._model.forward_rows(x2, obs.stride(-2), obs.shape[-1], self._buf)
         return q.view(e.n_env, e.n_data, -1)
 
     def select(self, q):
