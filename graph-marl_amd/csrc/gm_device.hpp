@@ -13,7 +13,7 @@ namespace gm {
 constexpr int WAVE = 64;
 constexpr int MT_N = 624;
 constexpr int MT_M = 397;
-constexpr int MAX_NODES = 64;
+constexpr int MAX_NODES = 128;  // node-indexed work runs in lanes v = l, l + 64
 constexpr int MAX_AGENTS = 64;
 constexpr int MAX_EDGES = MAX_NODES * 3 / 2;
 constexpr int RNG_BUF = 256;
@@ -34,6 +34,10 @@ __device__ __forceinline__ uint64_t readlane_u64(uint64_t v, int l) {
     return ((uint64_t)hi << 32) | lo;
 }
 __device__ __forceinline__ uint64_t ballot(bool p) { return __ballot(p); }
+
+// 128-bit node sets (N <= 128): word v >> 6, bit v & 63
+__device__ __forceinline__ bool bit128(const uint64_t* m, int v) { return (m[v >> 6] >> (v & 63)) & 1ull; }
+__device__ __forceinline__ void set128(uint64_t* m, int v) { m[v >> 6] |= 1ull << (v & 63); }
 
 __device__ __forceinline__ uint64_t wave_or_u64(uint64_t v) {
     uint32_t lo = (uint32_t)v, hi = (uint32_t)(v >> 32);

@@ -84,7 +84,7 @@ struct EnvLds {
     double load[MAX_EDGES];
     uint8_t nbr[MAX_NODES * 3], nbr_edge[MAX_NODES * 3];
     uint8_t ea[MAX_EDGES], eb[MAX_EDGES], elen[MAX_EDGES];
-    uint64_t nbrmask[MAX_NODES];
+    uint64_t nbrmask[MAX_NODES][2];
     float node_cnt[MAX_NODES], node_load[MAX_NODES];
     uint32_t rbuf[RNG_BUF];
     uint32_t rtmp[MT_N];
@@ -103,10 +103,11 @@ __device__ void load_topology_lds(const EnvDev& d, int env, EnvLds& s) {
         s.elen[e] = (uint8_t)d.edge_len[(size_t)env * E + e];
     }
     __syncthreads();
-    if (l < N) {
-        uint64_t m = 0;
-        for (int k = 0; k < 3; k++) m |= 1ull << s.nbr[l * 3 + k];
-        s.nbrmask[l] = m;
+    for (int v = l; v < N; v += WAVE) {
+        uint64_t m[2] = {0ull, 0ull};
+        for (int k = 0; k < 3; k++) set128(m, s.nbr[v * 3 + k]);
+        s.nbrmask[v][0] = m[0];
+        s.nbrmask[v][1] = m[1];
     }
     __syncthreads();
 }
@@ -141,17 +142,17 @@ __device__ void emit_obs(const EnvDev& d, int env, EnvLds& s, const gm_obs_buffe
     const int N = d.N, A = d.A;
     if (o.node_obs) {
         // packets waiting at node j (not on an edge) and the sum of their sizes in id order
-        if (l < N) {
+        for (int v = l; v < N; v += WAVE) {
             int cnt = 0;
             double tl = 0.0;
             for (int i = 0; i < A; i++) {
-                if (s.now[i] == l && s.edge[i] == -1) {
+                if (s.now[i] == v && s.edge[i] == -1) {
                     cnt++;
                     tl += s.size[i];
                 }
             }
-            s.node_cnt[l] = (float)cnt;
-            s.node_load[l] = (float)tl;
+            s.node_cnt[v] = (float)cnt;
+            s.node_load[v] = (float)tl;
         }
         __syncthreads();
         const int ND = 4 * N + 8;
@@ -203,7 +204,7 @@ __device__ void emit_obs(const EnvDev& d, int env, EnvLds& s, const gm_obs_buffe
         for (int idx = l; idx < A * A; idx += WAVE) {
             int i = idx / A, j = idx - i * A;
             int ni = s.now[i], nj = s.now[j];
-            base[idx] = (int8_t)(i == j || ni == nj || ((s.nbrmask[ni] >> nj) & 1ull));
+            base[idx] = (int8_t)(i == j || ni == nj || bit128(s.nbrmask[ni], nj));
         }
     }
 }
@@ -229,13 +230,12 @@ struct TopoLds {
     double x[MAX_NODES], y[MAX_NODES], d2[MAX_NODES];
     uint32_t tkey[MT_N];
     int32_t deg[MAX_NODES];
-    uint64_t adj[MAX_NODES];
+    uint64_t adj[MAX_NODES][2];
     int32_t node_edges[MAX_NODES * 3];
     int32_t ea[MAX_EDGES], eb[MAX_EDGES], elen[MAX_EDGES];
     int32_t n_edges;
     int32_t cand_at_rank[MAX_NODES];
     uint8_t ok_at_rank[MAX_NODES];
-    int16_t dist[MAX_NODES * MAX_NODES];
 };
 
 __device__ __forceinline__ bool is_excluded(const EnvDev& d, int64_t sd) {
@@ -258,57 +258,76 @@ __device__ int64_t draw_topology_seed(const EnvDev& d, R& r) {  // network.py:23
 }
 
 // One _create_random_topology attempt from the LDS stream t.tkey (fresh after seeding).
+// Node-indexed work runs in lanes v = l and v = l + 64 (N <= 128).
 __device__ bool topology_attempt(const EnvDev& d, TopoLds& t, LocalRng& tr) {
     const int l = lane_id();
     const int N = d.N;
     // positions: node i draws x then y (network.py:134-138) = tempered words 4i..4i+3
+    // (4N <= 512 words: one fresh 624-word block)
     if (tr.pos == MT_N) {
         mt_twist_lds(tr.key);
         tr.pos = 0;
     }
-    if (l < N) {
-        uint32_t w0 = mt_temper(tr.key[tr.pos + 4 * l]), w1 = mt_temper(tr.key[tr.pos + 4 * l + 1]);
-        uint32_t w2 = mt_temper(tr.key[tr.pos + 4 * l + 2]), w3 = mt_temper(tr.key[tr.pos + 4 * l + 3]);
-        t.x[l] = ((int32_t)(w0 >> 5) * 67108864.0 + (int32_t)(w1 >> 6)) / 9007199254740992.0;
-        t.y[l] = ((int32_t)(w2 >> 5) * 67108864.0 + (int32_t)(w3 >> 6)) / 9007199254740992.0;
-        t.deg[l] = 0;
-        t.adj[l] = 0;
+    for (int v = l; v < N; v += WAVE) {
+        uint32_t w0 = mt_temper(tr.key[tr.pos + 4 * v]), w1 = mt_temper(tr.key[tr.pos + 4 * v + 1]);
+        uint32_t w2 = mt_temper(tr.key[tr.pos + 4 * v + 2]), w3 = mt_temper(tr.key[tr.pos + 4 * v + 3]);
+        t.x[v] = ((int32_t)(w0 >> 5) * 67108864.0 + (int32_t)(w1 >> 6)) / 9007199254740992.0;
+        t.y[v] = ((int32_t)(w2 >> 5) * 67108864.0 + (int32_t)(w3 >> 6)) / 9007199254740992.0;
+        t.deg[v] = 0;
+        t.adj[v][0] = 0;
+        t.adj[v][1] = 0;
     }
     tr.pos += 4 * N;
     if (l == 0) t.n_edges = 0;
     __syncthreads();
     for (int i = 0; i < N; i++) {
         // squared distances of row i (network.py:143-150) and stable ranks (153)
-        double my = 0.0;
-        if (l < N) {
-            double dx = t.x[l] - t.x[i], dy = t.y[l] - t.y[i];
-            double a = dx * dx, b = dy * dy;
-            my = a + b;
-            t.d2[l] = my;
+        double my[2] = {0.0, 0.0};
+        for (int h = 0; h < 2; h++) {
+            const int v = l + h * WAVE;
+            if (v < N) {
+                double dx = t.x[v] - t.x[i], dy = t.y[v] - t.y[i];
+                double a = dx * dx, b = dy * dy;
+                my[h] = a + b;
+                t.d2[v] = my[h];
+            }
         }
         __syncthreads();
-        int rank = 0;
-        if (l < N) {
-            for (int k = 0; k < N; k++) {
-                double dk = t.d2[k];
-                rank += (dk < my) || (dk == my && k < l);
+        int rank[2] = {0, 0};
+        for (int h = 0; h < 2; h++) {
+            const int v = l + h * WAVE;
+            if (v < N) {
+                for (int k = 0; k < N; k++) {
+                    double dk = t.d2[k];
+                    rank[h] += (dk < my[h]) || (dk == my[h] && k < v);
+                }
             }
         }
         const int need = 3 - t.deg[i];
         if (need > 0) {
             // candidate at sorted position r >= 1 is taken iff its degree < 3 and it is
             // not already linked to i (network.py:157-170), first `need` in rank order
-            if (l < N) {
-                bool ok = rank >= 1 && t.deg[l] < 3 && !((t.adj[l] >> i) & 1ull);
-                t.ok_at_rank[rank] = (uint8_t)ok;
-                t.cand_at_rank[rank] = l;
+            for (int h = 0; h < 2; h++) {
+                const int v = l + h * WAVE;
+                if (v < N) {
+                    bool ok = rank[h] >= 1 && t.deg[v] < 3 && !bit128(t.adj[v], i);
+                    t.ok_at_rank[rank[h]] = (uint8_t)ok;
+                    t.cand_at_rank[rank[h]] = v;
+                }
             }
             __syncthreads();
-            uint64_t okm = ballot(l < N && t.ok_at_rank[l]);
+            uint64_t okm0 = ballot(l < N && t.ok_at_rank[l]);
+            uint64_t okm1 = ballot(l + WAVE < N && t.ok_at_rank[l + WAVE]);
             int take = 0;
-            while (okm && take < need) {
-                int r = __builtin_ctzll(okm);
-                okm &= okm - 1;
+            while ((okm0 | okm1) && take < need) {
+                int r;
+                if (okm0) {
+                    r = __builtin_ctzll(okm0);
+                    okm0 &= okm0 - 1;
+                } else {
+                    r = WAVE + __builtin_ctzll(okm1);
+                    okm1 &= okm1 - 1;
+                }
                 take++;
                 int c = t.cand_at_rank[r];
                 double dc = t.d2[c];
@@ -324,8 +343,8 @@ __device__ bool topology_attempt(const EnvDev& d, TopoLds& t, LocalRng& tr) {
                     t.deg[c] += 1;
                     t.node_edges[i * 3 + t.deg[i]] = e;
                     t.deg[i] += 1;
-                    t.adj[c] |= 1ull << i;
-                    t.adj[i] |= 1ull << c;
+                    set128(t.adj[c], i);
+                    set128(t.adj[i], c);
                     t.n_edges = e + 1;
                 }
                 __syncthreads();
@@ -334,28 +353,37 @@ __device__ bool topology_attempt(const EnvDev& d, TopoLds& t, LocalRng& tr) {
         __syncthreads();
     }
     // validity (network.py:197-213): all degrees 3 and connected
-    bool deg_ok = !(ballot(l < N && t.deg[l] != 3));
+    bool deg_ok = !(ballot(l < N && t.deg[l] != 3) | ballot(l + WAVE < N && t.deg[l + WAVE] != 3));
     if (!deg_ok) return false;
-    uint64_t full = N == 64 ? ~0ull : ((1ull << N) - 1);
-    uint64_t reach = 1ull, prev = 0;
-    uint64_t myadj = l < N ? t.adj[l] : 0ull;
-    while (reach != prev) {
-        prev = reach;
-        uint64_t contrib = ((reach >> l) & 1ull) ? myadj : 0ull;
-        reach |= wave_or_u64(contrib);
+    uint64_t full0 = N >= 64 ? ~0ull : ((1ull << N) - 1);
+    uint64_t full1 = N <= 64 ? 0ull : (N == 128 ? ~0ull : ((1ull << (N - 64)) - 1));
+    uint64_t reach[2] = {1ull, 0ull}, prev[2] = {0ull, 0ull};
+    while (reach[0] != prev[0] || reach[1] != prev[1]) {
+        prev[0] = reach[0];
+        prev[1] = reach[1];
+        uint64_t c0 = 0, c1 = 0;
+        for (int h = 0; h < 2; h++) {
+            const int v = l + h * WAVE;
+            if (v < N && bit128(prev, v)) {
+                c0 |= t.adj[v][0];
+                c1 |= t.adj[v][1];
+            }
+        }
+        reach[0] |= wave_or_u64(c0);
+        reach[1] |= wave_or_u64(c1);
     }
-    return reach == full;
+    return reach[0] == full0 && reach[1] == full1;
 }
 
-__device__ void topology_finish(const EnvDev& d, int env, TopoLds& t, int64_t seed, int reps) {
+__device__ void topology_finish(const EnvDev& d, int env, TopoLds& t, int16_t* dist, int64_t seed, int reps) {
     const int l = lane_id();
     const int N = d.N, E = d.E;
     // per-node edges sorted by neighbour id (network.py:191-195)
-    if (l < N) {
+    for (int v = l; v < N; v += WAVE) {
         int ee[3], nb[3];
         for (int k = 0; k < 3; k++) {
-            ee[k] = t.node_edges[l * 3 + k];
-            nb[k] = t.ea[ee[k]] ^ t.eb[ee[k]] ^ l;
+            ee[k] = t.node_edges[v * 3 + k];
+            nb[k] = t.ea[ee[k]] ^ t.eb[ee[k]] ^ v;
         }
         for (int a = 1; a < 3; a++)
             for (int b = a; b > 0 && nb[b - 1] > nb[b]; b--) {
@@ -363,8 +391,8 @@ __device__ void topology_finish(const EnvDev& d, int env, TopoLds& t, int64_t se
                 int te = ee[b]; ee[b] = ee[b - 1]; ee[b - 1] = te;
             }
         for (int k = 0; k < 3; k++) {
-            d.nbr[((size_t)env * N + l) * 3 + k] = nb[k];
-            d.nbr_edge[((size_t)env * N + l) * 3 + k] = ee[k];
+            d.nbr[((size_t)env * N + v) * 3 + k] = nb[k];
+            d.nbr_edge[((size_t)env * N + v) * 3 + k] = ee[k];
         }
     }
     for (int e = l; e < E; e += WAVE) {
@@ -374,28 +402,23 @@ __device__ void topology_finish(const EnvDev& d, int env, TopoLds& t, int64_t se
     }
     // all-pairs shortest path weights (network.py:274-290) by Floyd-Warshall
     const int16_t INF = 0x3fff;
-    for (int idx = l; idx < N * N; idx += WAVE) t.dist[idx] = (idx / N == idx % N) ? 0 : INF;
+    for (int idx = l; idx < N * N; idx += WAVE) dist[idx] = (idx / N == idx % N) ? 0 : INF;
     __syncthreads();
-    if (l < E) {
-        int a = t.ea[l], b = t.eb[l];
-        t.dist[a * N + b] = (int16_t)t.elen[l];
-        t.dist[b * N + a] = (int16_t)t.elen[l];
-    }
-    if (E > WAVE && l + WAVE < E) {
-        int e = l + WAVE, a = t.ea[e], b = t.eb[e];
-        t.dist[a * N + b] = (int16_t)t.elen[e];
-        t.dist[b * N + a] = (int16_t)t.elen[e];
+    for (int e = l; e < E; e += WAVE) {
+        int a = t.ea[e], b = t.eb[e];
+        dist[a * N + b] = (int16_t)t.elen[e];
+        dist[b * N + a] = (int16_t)t.elen[e];
     }
     __syncthreads();
     for (int k = 0; k < N; k++) {
         for (int idx = l; idx < N * N; idx += WAVE) {
             int i = idx / N, j = idx - i * N;
-            int v = t.dist[i * N + k] + t.dist[k * N + j];
-            if (v < t.dist[idx]) t.dist[idx] = (int16_t)v;
+            int v = dist[i * N + k] + dist[k * N + j];
+            if (v < dist[idx]) dist[idx] = (int16_t)v;
         }
         __syncthreads();
     }
-    for (int idx = l; idx < N * N; idx += WAVE) d.apsp[(size_t)env * N * N + idx] = t.dist[idx];
+    for (int idx = l; idx < N * N; idx += WAVE) d.apsp[(size_t)env * N * N + idx] = dist[idx];
     if (l == 0) {
         d.topo_seed[env] = seed;
         d.topo_reps[env] = reps;
@@ -404,7 +427,8 @@ __device__ void topology_finish(const EnvDev& d, int env, TopoLds& t, int64_t se
 }
 
 // network.py:242-258: fresh stream per topology seed, reseed on invalid topology
-__device__ void generate_topology(const EnvDev& d, int env, TopoLds& t, int64_t seed, bool allow_retry) {
+__device__ void generate_topology(const EnvDev& d, int env, TopoLds& t, int16_t* dist, int64_t seed,
+                                  bool allow_retry) {
     LocalRng tr;
     tr.key = t.tkey;
     tr.seed((uint32_t)seed);
@@ -421,13 +445,14 @@ __device__ void generate_topology(const EnvDev& d, int env, TopoLds& t, int64_t 
         tr.seed((uint32_t)seed);
     }
     __syncthreads();
-    topology_finish(d, env, t, seed, reps);
+    topology_finish(d, env, t, dist, seed, reps);
     __syncthreads();
 }
 
 struct ResetLds {
     EnvLds env;
     TopoLds topo;
+    int16_t dist[MAX_NODES * MAX_NODES];  // Floyd-Warshall APSP
 };
 
 // src/env/routing.py:160-178 (+ network.py:366-371): new topology (per mode), zero
@@ -459,7 +484,7 @@ __global__ __launch_bounds__(64) void k_env_reset(EnvDev d, const uint8_t* mask,
         }
         seed = d.list[idx];
     }
-    if (gen) generate_topology(d, env, S.topo, seed, d.topo_mode == GM_TOPO_RANDOM);
+    if (gen) generate_topology(d, env, S.topo, S.dist, seed, d.topo_mode == GM_TOPO_RANDOM);
     __syncthreads();
 
     // packets
@@ -488,7 +513,7 @@ __global__ __launch_bounds__(64) void k_env_reset(EnvDev d, const uint8_t* mask,
         d.steps[p] = 0;
         d.spw[p] = d.apsp[((size_t)env * N + p_now) * N + p_target];
         d.visited[p * 2 + 0] = p_now < 64 ? (1ull << p_now) : 0ull;
-        d.visited[p * 2 + 1] = 0ull;
+        d.visited[p * 2 + 1] = p_now >= 64 ? (1ull << (p_now - 64)) : 0ull;
         uint32_t m = d.amask_on ? (uint32_t)(p_now != p_target) : 0u;
         reinterpret_cast<uint32_t*>(d.amask)[p] = m;
         s.now[l] = p_now;
@@ -528,20 +553,21 @@ __global__ __launch_bounds__(64) void k_env_step(EnvDev d, const int32_t* act, S
     const size_t p = (size_t)env * A + l;
     int now = 0, target = 0, edge = -1, time = 0, ttl = 0, steps = 0, spw = 0, start = 0, a_t = 0;
     double size = 0.0;
-    uint64_t vis = 0;
+    uint64_t vis[2] = {0ull, 0ull};  // visited node set (N <= 128)
     if (own) {
         now = d.now[p]; target = d.target[p]; edge = d.edge[p]; time = d.time[p];
         ttl = d.ttl_[p]; steps = d.steps[p]; spw = d.spw[p]; start = d.start[p];
-        size = d.size[p]; vis = d.visited[p * 2];
+        size = d.size[p]; vis[0] = d.visited[p * 2]; vis[1] = d.visited[p * 2 + 1];
         a_t = act[p];
         if (a_t < 0 || a_t > 3) {  // the reference raises IndexError; flag and idle
             atomicExch(d.err, GM_ERR_INVALID_ARG);
             a_t = 0;
         }
     }
-    // edge e in lane e (and e+64)
+    // edge e in lane e % 64, slot e / 64 (E <= 192)
     double ld0 = l < E ? d.load[(size_t)env * E + l] : 0.0;
     double ld1 = l + WAVE < E ? d.load[(size_t)env * E + l + WAVE] : 0.0;
+    double ld2 = l + 2 * WAVE < E ? d.load[(size_t)env * E + l + 2 * WAVE] : 0.0;
 
     steps += 1;  // routing.py:371
     float reward = 0.0f;
@@ -554,14 +580,17 @@ __global__ __launch_bounds__(64) void k_env_step(EnvDev d, const int32_t* act, S
         int c = readlane(chosen, i);
         if (c < 0) continue;  // uniform
         double si = readlane_f64(size, i);
-        if (c == l || c == l + WAVE) {
-            double ld = c == l ? ld0 : ld1;
+        if ((c & (WAVE - 1)) == l) {
+            const int slot = c >> 6;
+            double ld = slot == 0 ? ld0 : (slot == 1 ? ld1 : ld2);
             if (d.cong && ld + si > 1.0) {
                 block |= 1ull << i;
             } else {
                 ld = ld + si;
                 admit |= 1ull << i;
-                if (c == l) ld0 = ld; else ld1 = ld;
+                if (slot == 0) ld0 = ld;
+                else if (slot == 1) ld1 = ld;
+                else ld2 = ld;
             }
         }
     }
@@ -574,8 +603,8 @@ __global__ __launch_bounds__(64) void k_env_step(EnvDev d, const int32_t* act, S
             edge = chosen;
             time = s.elen[chosen];
             now = s.ea[chosen] ^ s.eb[chosen] ^ now;
-            if ((vis >> now) & 1ull) looped = true;
-            else vis |= 1ull << now;
+            if (bit128(vis, now)) looped = true;
+            else set128(vis, now);
         }
     }
 
@@ -584,7 +613,8 @@ __global__ __launch_bounds__(64) void k_env_step(EnvDev d, const int32_t* act, S
         double tel = 0.0, tps = 0.0;
         int occ = 0;
         for (int e = 0; e < E; e++) {
-            double le = e < WAVE ? readlane_f64(ld0, e) : readlane_f64(ld1, e - WAVE);
+            double le = e < WAVE ? readlane_f64(ld0, e)
+                                 : (e < 2 * WAVE ? readlane_f64(ld1, e - WAVE) : readlane_f64(ld2, e - 2 * WAVE));
             tel = tel + le;
             occ += le > 0.0;
         }
@@ -623,7 +653,7 @@ __global__ __launch_bounds__(64) void k_env_step(EnvDev d, const int32_t* act, S
                 am = 1u;
                 int cnt = 1;
                 for (int k = 0; k < 3; k++) {
-                    uint32_t b = (uint32_t)((vis >> s.nbr[now * 3 + k]) & 1ull);
+                    uint32_t b = (uint32_t)bit128(vis, s.nbr[now * 3 + k]);
                     am |= b << (8 * (k + 1));
                     cnt += (int)b;
                 }
@@ -644,6 +674,7 @@ __global__ __launch_bounds__(64) void k_env_step(EnvDev d, const int32_t* act, S
         double si = readlane_f64(size, i);
         if (c == l) ld0 = ld0 - si;
         else if (c == l + WAVE) ld1 = ld1 - si;
+        else if (c == l + 2 * WAVE) ld2 = ld2 - si;
     }
     // statistics of finished packets (before respawn)
     const int opt = spw > 1 ? spw : 1;
@@ -705,7 +736,9 @@ __global__ __launch_bounds__(64) void k_env_step(EnvDev d, const int32_t* act, S
             ttl = d.ttl;
             steps = 0;
             spw = d.apsp[((size_t)env * N + now) * N + target];
-            vis = 1ull << now;
+            vis[0] = 0ull;
+            vis[1] = 0ull;
+            set128(vis, now);
             am = d.amask_on ? (uint32_t)(now != target) : 0u;
         }
     }
@@ -713,12 +746,13 @@ __global__ __launch_bounds__(64) void k_env_step(EnvDev d, const int32_t* act, S
     if (own) {
         d.now[p] = now; d.target[p] = target; d.edge[p] = edge; d.time[p] = time;
         d.ttl_[p] = ttl; d.steps[p] = steps; d.spw[p] = spw; d.start[p] = start;
-        d.size[p] = size; d.visited[p * 2] = vis;
+        d.size[p] = size; d.visited[p * 2] = vis[0]; d.visited[p * 2 + 1] = vis[1];
         reinterpret_cast<uint32_t*>(d.amask)[p] = am;
         s.now[l] = now; s.target[l] = target; s.edge[l] = edge; s.time[l] = time; s.size[l] = size;
     }
     if (l < E) { d.load[(size_t)env * E + l] = ld0; s.load[l] = ld0; }
     if (l + WAVE < E) { d.load[(size_t)env * E + l + WAVE] = ld1; s.load[l + WAVE] = ld1; }
+    if (l + 2 * WAVE < E) { d.load[(size_t)env * E + l + 2 * WAVE] = ld2; s.load[l + 2 * WAVE] = ld2; }
     __syncthreads();
     if (o.obs || o.node_obs || o.agent_node || o.agent_adj) emit_obs(d, env, s, o);
 }
@@ -783,6 +817,7 @@ __global__ __launch_bounds__(64) void k_policy_egreedy(EnvDev d, const float* q,
 // are relaxed in G's adjacency order = edge creation order (network.py:179-186).
 // Only the latest push of a node can be live, so the heap is the per-node
 // (seen, counter) pair. first[s][t] = first hop on the s -> t path.
+// LDS: first 16 KB + seen/cnt 32 KB + the topology image.
 __global__ __launch_bounds__(64) void k_policy_shortest_path(EnvDev d, int32_t* actions) {
     const int env = blockIdx.x;
     const int l = lane_id();
@@ -793,18 +828,17 @@ __global__ __launch_bounds__(64) void k_policy_shortest_path(EnvDev d, int32_t* 
     __shared__ int16_t cnt[MAX_NODES * WAVE];
     load_topology_lds(d, env, s);
     constexpr int16_t INF = 0x7fff;
-    if (l < N) {
-        const int src = l;
+    for (int src = l; src < N; src += WAVE) {  // lane l runs sources l and l + 64
         for (int u = 0; u < N; u++) seen[u * WAVE + l] = INF;
         seen[src * WAVE + l] = 0;
         cnt[src * WAVE + l] = 0;
         first[src * N + src] = (uint8_t)src;
         int c = 1;
-        uint64_t done = 0;
+        uint64_t done[2] = {0ull, 0ull};
         for (int it = 0; it < N; it++) {
             int v = -1, bd = INF, bc = 0;
             for (int u = 0; u < N; u++) {
-                if ((done >> u) & 1ull) continue;
+                if (bit128(done, u)) continue;
                 const int du = seen[u * WAVE + l];
                 if (du == INF) continue;
                 const int cu = cnt[u * WAVE + l];
@@ -815,7 +849,7 @@ __global__ __launch_bounds__(64) void k_policy_shortest_path(EnvDev d, int32_t* 
                 }
             }
             if (v < 0) break;
-            done |= 1ull << v;
+            set128(done, v);
             int e3[3] = {s.nbr_edge[v * 3], s.nbr_edge[v * 3 + 1], s.nbr_edge[v * 3 + 2]};
             for (int i = 1; i < 3; i++)  // incident edges in creation (edge id) order
                 for (int j = i; j > 0 && e3[j] < e3[j - 1]; j--) {
@@ -826,7 +860,7 @@ __global__ __launch_bounds__(64) void k_policy_shortest_path(EnvDev d, int32_t* 
             for (int k = 0; k < 3; k++) {
                 const int e = e3[k];
                 const int u = s.ea[e] ^ s.eb[e] ^ v;
-                if ((done >> u) & 1ull) continue;
+                if (bit128(done, u)) continue;
                 const int vu = bd + (int)s.elen[e];
                 const int su = seen[u * WAVE + l];
                 if (su == INF || vu < su) {
@@ -910,8 +944,13 @@ __global__ void k_final_info(EnvDev d, double* out) {
 // (reseeding on invalid graphs) gives the final seed; unique seeds in order.
 constexpr int MAX_SEED_LIST = 4096;
 
+struct SeedListLds {
+    EnvLds env;
+    TopoLds topo;
+};
+
 __global__ __launch_bounds__(64) void k_build_seed_list(EnvDev d, int count, int64_t* out) {
-    __shared__ ResetLds S;
+    __shared__ SeedListLds S;
     __shared__ int64_t found[MAX_SEED_LIST];
     MainRng r = open_rng(d, 0, S.env);
     int have = 0;
@@ -989,7 +1028,7 @@ extern "C" int gm_env_create(const gm_env_config* cfg, const uint32_t* env_seeds
     const int N = cfg->n_nodes, A = cfg->n_data;
     if (cfg->n_env <= 0) return gm_fail(GM_ERR_INVALID_ARG, "n_env must be > 0");
     if (N < 4 || N > MAX_NODES || (N % 2) != 0)
-        return gm_fail(GM_ERR_INVALID_ARG, "n_nodes must be even and in [4, 64] (3-regular topology generator)");
+        return gm_fail(GM_ERR_INVALID_ARG, "n_nodes must be even and in [4, 128] (3-regular topology generator)");
     if (A < 1 || A > MAX_AGENTS) return gm_fail(GM_ERR_INVALID_ARG, "n_data must be in [1, 64]");
     if (cfg->env_var != 1) return gm_fail(GM_ERR_UNSUPPORTED, "only env_var=1 (INDEPENDENT) is implemented");
     if ((cfg->topo_mode == GM_TOPO_LIST || cfg->topo_mode == GM_TOPO_SEQUENTIAL) &&

@@ -115,6 +115,8 @@ BATCH_CASES = [
     (64, 64, "random", True, False, 0, 8, 60, 30),
     (50, 20, "random", True, True, 12, 16, 90, 45),
     (4, 1, "random", True, False, 0, 16, 40, 20),
+    (100, 20, "random", True, False, 0, 8, 60, 30),
+    (128, 64, "random", True, True, 16, 4, 40, 20),
 ]
 
 
@@ -147,7 +149,7 @@ def test_batch_vs_oracle(gm, oracle_mod, case):
             np.testing.assert_array_equal(st["loads"][b].view(np.uint64), s["loads"].view(np.uint64),
                                           err_msg=f"{tag} env {b} loads")
             np.testing.assert_array_equal(st["agent_steps"][b], s["agent_steps"])
-            np.testing.assert_array_equal(st["visited"][b][:, 0], s["visited"][:, 0])
+            np.testing.assert_array_equal(st["visited"][b], s["visited"], err_msg=f"{tag} env {b} visited")
             assert st["topo_seed"][b] == s["topo_seed"]
             np.testing.assert_array_equal(st["rng_key"][b], s["rng_key"], err_msg=f"{tag} env {b} rng")
             assert st["rng_pos"][b] == s["rng_pos"]
@@ -247,3 +249,25 @@ def test_large_batch_invariants(gm, oracle_mod):
                 np.testing.assert_array_equal(st["now"][b], s["now"])
                 np.testing.assert_array_equal(st["loads"][b].view(np.uint64), s["loads"].view(np.uint64))
                 np.testing.assert_array_equal(obs[b], o.observe()["obs"])
+
+
+@pytest.mark.parametrize("n", [10, 20, 50, 100])
+def test_topology_from_seed_matches_reference_golden(gm, n):
+    """Topologies generated on the device from the reference's recorded (valid) seeds:
+    edges in creation order, lengths and APSP equal the reference's networkx output
+    (tests/golden/topology.npz, rand_n*), up to N = 100 (BASELINE config 5)."""
+    g = np.load(f"{R.GOLDEN}/topology.npz")
+    seeds = g[f"rand_n{n}_seed"]
+    B = len(seeds)
+    env = gm.Routing(gm.Network(n, random_topology=True, excluded_seeds=gm.EVAL_SEEDS), 4, n_env=B, seed=1)
+    env.set_topology_seeds(seeds, sequential=True, interleave=True)
+    env.reset_()
+    st = env.get_state()
+    E = 3 * n // 2
+    for b in range(B):
+        ge = g[f"rand_n{n}_edges"][b]
+        np.testing.assert_array_equal(st["edge_a"][b, :E], ge[:, 0], err_msg=f"n={n} topology {b}")
+        np.testing.assert_array_equal(st["edge_b"][b, :E], ge[:, 1])
+        np.testing.assert_array_equal(st["edge_len"][b, :E], ge[:, 2])
+        np.testing.assert_array_equal(st["apsp"][b], g[f"rand_n{n}_apsp"][b])
+        assert st["topo_seed"][b] == seeds[b]

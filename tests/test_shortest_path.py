@@ -79,7 +79,7 @@ def test_device_trace_matches_reference(name):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("n", [10, 20, 50, 64])
+@pytest.mark.parametrize("n", [10, 20, 50, 64, 100, 128])
 def test_device_actions_match_restatement_on_random_graphs(n):
     """512 envs of random N-node topologies with random packets: every packet's action
     equals the restated networkx first hop."""
