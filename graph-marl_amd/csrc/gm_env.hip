@@ -818,14 +818,20 @@ __global__ __launch_bounds__(64) void k_policy_egreedy(EnvDev d, const float* q,
 // Only the latest push of a node can be live, so the heap is the per-node
 // (seen, counter) pair. first[s][t] = first hop on the s -> t path.
 // LDS: first 16 KB + seen/cnt 32 KB + the topology image.
-__global__ __launch_bounds__(64) void k_policy_shortest_path(EnvDev d, int32_t* actions) {
-    const int env = blockIdx.x;
+struct FirstHopLds {
+    EnvLds s;
+    uint8_t first[MAX_NODES * MAX_NODES];
+    int16_t seen[MAX_NODES * WAVE];
+    int16_t cnt[MAX_NODES * WAVE];
+};
+
+__device__ void first_hops_lds(const EnvDev& d, int env, FirstHopLds& F) {
     const int l = lane_id();
-    const int N = d.N, A = d.A;
-    __shared__ EnvLds s;
-    __shared__ uint8_t first[MAX_NODES * MAX_NODES];
-    __shared__ int16_t seen[MAX_NODES * WAVE];
-    __shared__ int16_t cnt[MAX_NODES * WAVE];
+    const int N = d.N;
+    EnvLds& s = F.s;
+    uint8_t* first = F.first;
+    int16_t* seen = F.seen;
+    int16_t* cnt = F.cnt;
     load_topology_lds(d, env, s);
     constexpr int16_t INF = 0x7fff;
     for (int src = l; src < N; src += WAVE) {  // lane l runs sources l and l + 64
@@ -872,6 +878,16 @@ __global__ __launch_bounds__(64) void k_policy_shortest_path(EnvDev d, int32_t* 
         }
     }
     __syncthreads();
+}
+
+__global__ __launch_bounds__(64) void k_policy_shortest_path(EnvDev d, int32_t* actions) {
+    const int env = blockIdx.x;
+    const int l = lane_id();
+    const int N = d.N, A = d.A;
+    __shared__ FirstHopLds F;
+    first_hops_lds(d, env, F);
+    EnvLds& s = F.s;
+    const uint8_t* first = F.first;
     if (l < A) {
         const size_t p = (size_t)env * A + l;
         const int now = d.now[p], target = d.target[p];
@@ -886,6 +902,14 @@ __global__ __launch_bounds__(64) void k_policy_shortest_path(EnvDev d, int32_t* 
         }
         actions[p] = a;
     }
+}
+
+__global__ __launch_bounds__(64) void k_env_first_hops(EnvDev d, int32_t* out) {
+    const int env = blockIdx.x;
+    __shared__ FirstHopLds F;
+    first_hops_lds(d, env, F);
+    const int N = d.N;
+    for (int i = lane_id(); i < N * N; i += WAVE) out[(size_t)env * N * N + i] = F.first[i];
 }
 
 __global__ void k_rng_seed(EnvDev d, const uint32_t* seeds) {
@@ -1167,6 +1191,12 @@ __global__ void k_topology_rewind(EnvDev d, int interleave) {
 extern "C" int gm_policy_shortest_path(gm_env* env, int32_t* actions, void* stream) {
     if (!env || !actions) return gm_fail(GM_ERR_INVALID_ARG, "gm_policy_shortest_path: null argument");
     hipLaunchKernelGGL(k_policy_shortest_path, dim3(env->d.n_env), dim3(64), 0, (hipStream_t)stream, env->d, actions);
+    return check_launch();
+}
+
+extern "C" int gm_env_first_hops(gm_env* env, int32_t* out, void* stream) {
+    if (!env || !out) return gm_fail(GM_ERR_INVALID_ARG, "gm_env_first_hops: null argument");
+    hipLaunchKernelGGL(k_env_first_hops, dim3(env->d.n_env), dim3(64), 0, (hipStream_t)stream, env->d, out);
     return check_launch();
 }
 

@@ -123,6 +123,9 @@ int gm_env_topology(gm_env* env, int32_t* nbr, int8_t* node_adj, float* node_aux
  * neighbour id) of the first hop of networkx's weighted shortest path now -> target
  * (Dijkstra with networkx's tie-breaking, src/env/network.py:279), 0 at the target. */
 int gm_policy_shortest_path(gm_env* env, int32_t* actions, void* stream);
+/* first-hop table int32 [n_env, N, N]: out[s][t] = next node on the s -> t path (t on the
+ * diagonal) — network.shortest_paths[s][t][1] (src/env/network.py:279) */
+int gm_env_first_hops(gm_env* env, int32_t* out, void* stream);
 /* Switch the topology source between resets (the reference's evaluation sets
  * network.seeds = EVAL_SEEDS and sequential_topology_seeds = True, src/main.py:553-560,
  * 1049-1053). The sequential index restarts at 0 (network.py:87); with interleave, env b

@@ -625,6 +625,78 @@ def gen_cli_flags(out, ref):
     print("cli flags:", len(flags))
 
 
+# ---------------------------------------------------------------------------
+# Supervised shortest-path task (src/sl.py): samples and one NetMonSL update
+# ---------------------------------------------------------------------------
+def gen_sl(out, Network, Routing, EVAL_SEEDS, NetMon):
+    import torch
+    import torch.nn as nn
+    import torch.nn.functional as F
+
+    d = {}
+    # get_sl_sample (src/sl.py:174-218) on graphs from fixed seeds
+    seeds = list(EVAL_SEEDS[100:108])
+    net = Network(20, random_topology=True, sequential_topology_seeds=True, provided_seeds=seeds)
+    env = Routing(net, 20, 1)
+    np.random.seed(5)
+    env.reset()
+    obs, adj, labels, targets_all = [], [], [], []
+    for s in range(len(seeds)):
+        if s > 0:
+            env.reset()
+        n = env.get_num_nodes()
+        lab = np.zeros(n, np.int64)
+        ta = np.zeros((n, n), np.float32)
+        for v in range(n):
+            for w in range(n):
+                ta[v, w] = env.network.shortest_paths_weights[v][w]
+            p0 = env.network.shortest_paths[v][0]
+            if len(p0) > 1:
+                for e_idx, e in enumerate(env.network.nodes[v].edges):
+                    if env.network.edges[e].get_other_node(v) == p0[1]:
+                        lab[v] = e_idx + 1
+                        break
+        obs.append(env.get_node_observation())
+        adj.append(env.get_nodes_adjacency().astype(np.float32))
+        labels.append(lab)
+        targets_all.append(ta)
+    d["seeds"] = np.array(seeds, np.int64)
+    d["node_obs"] = np.stack(obs)
+    d["node_adj"] = np.stack(adj)
+    d["labels"] = np.stack(labels)
+    d["targets_all"] = np.stack(targets_all)
+    # NetMonSL (src/sl.py:132-168) = reference NetMon + 3 nn.Linear heads; one train
+    # iteration (src/sl.py:360-424) with seq_len 2, regression-all loss
+    torch.manual_seed(3)
+    netmon = NetMon(88, 32, [64, 48], 1, activation_fn=F.leaky_relu, rnn_type="lstm", rnn_carryover=True,
+                    agg_type="sum", output_neighbor_hidden=True, output_global_hidden=False)
+    heads = [nn.Linear(netmon.get_out_features(), k) for k in (4, 1, 20)]
+    params = list(netmon.parameters()) + [p for h in heads for p in h.parameters()]
+    names = [f"netmon.{k}" for k, _ in netmon.named_parameters()] + \
+        [f"{hn}.{k}" for hn, h in zip(("linear", "linear_reg", "linear_reg_all"), heads) for k, _ in h.named_parameters()]
+    for nme, p in zip(names, params):
+        d["w_" + nme] = p.detach().numpy().copy()
+    x = torch.tensor(d["node_obs"])
+    a = torch.tensor(d["node_adj"])
+    eye = torch.eye(20).repeat(x.shape[0], 1, 1)
+    tgt = torch.tensor(d["targets_all"])
+    netmon.state = None
+    seq = []
+    for t in range(2):
+        feats = netmon(x, a, eye)
+        pred_all = heads[2](feats)
+        d[f"pred_all_{t}"] = pred_all.detach().numpy().copy()
+        seq.append(F.mse_loss(pred_all, tgt))
+    total = torch.mean(torch.stack(seq))
+    total.backward()
+    d["loss"] = np.float64(total.item())
+    for nme, p in zip(names, params):
+        d["g_" + nme] = (p.grad.numpy().copy() if p.grad is not None else np.zeros(p.shape, np.float32))
+    d["param_names"] = np.array(names)
+    np.savez_compressed(out, **d)
+    print("sl:", out)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--ref", default="/root/reference/src")
@@ -662,6 +734,8 @@ def main():
         gen_eval(os.path.join(HERE, "eval.npz"), Network, Routing, EVAL_SEEDS, ShortestPath, evaluate)
     if only is None or "cli" in only:
         gen_cli_flags(os.path.join(HERE, "cli_flags.json"), args.ref)
+    if only is None or "sl" in only:
+        gen_sl(os.path.join(HERE, "sl.npz"), Network, Routing, EVAL_SEEDS, NetMon)
     if only is None or "simple" in only:
         gen_simple(os.path.join(HERE, "simple.npz"), SimpleEnvironment)
 
