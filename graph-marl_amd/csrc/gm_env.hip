@@ -78,19 +78,23 @@ namespace {
 // ---------------------------------------------------------------------------
 // Shared per-block LDS image of one env
 // ---------------------------------------------------------------------------
+// NC = node capacity of the kernel instance (64 or 128, picked from N at launch so
+// that N <= 64 keeps the small LDS footprint and occupancy)
+template <int NC>
 struct EnvLds {
     int32_t now[MAX_AGENTS], target[MAX_AGENTS], edge[MAX_AGENTS], time[MAX_AGENTS];
     double size[MAX_AGENTS];
-    double load[MAX_EDGES];
-    uint8_t nbr[MAX_NODES * 3], nbr_edge[MAX_NODES * 3];
-    uint8_t ea[MAX_EDGES], eb[MAX_EDGES], elen[MAX_EDGES];
-    uint64_t nbrmask[MAX_NODES][2];
-    float node_cnt[MAX_NODES], node_load[MAX_NODES];
+    double load[NC * 3 / 2];
+    uint8_t nbr[NC * 3], nbr_edge[NC * 3];
+    uint8_t ea[NC * 3 / 2], eb[NC * 3 / 2], elen[NC * 3 / 2];
+    uint64_t nbrmask[NC][2];
+    float node_cnt[NC], node_load[NC];
     uint32_t rbuf[RNG_BUF];
     uint32_t rtmp[MT_N];
 };
 
-__device__ void load_topology_lds(const EnvDev& d, int env, EnvLds& s) {
+template <class ES>
+__device__ void load_topology_lds(const EnvDev& d, int env, ES& s) {
     const int l = lane_id();
     const int N = d.N, E = d.E;
     for (int i = l; i < N * 3; i += WAVE) {
@@ -112,7 +116,8 @@ __device__ void load_topology_lds(const EnvDev& d, int env, EnvLds& s) {
     __syncthreads();
 }
 
-__device__ __forceinline__ MainRng open_rng(const EnvDev& d, int env, EnvLds& s) {
+template <class ES>
+__device__ __forceinline__ MainRng open_rng(const EnvDev& d, int env, ES& s) {
     MainRng r;
     r.g = d.mt + (size_t)env * 2 * MT_N;
     r.buf = s.rbuf;
@@ -137,7 +142,8 @@ __device__ __forceinline__ void close_rng(const EnvDev& d, int env, MainRng& r) 
 // ---------------------------------------------------------------------------
 // Observation emission (routing.py:187-358, 522-539), packet state in LDS.
 // ---------------------------------------------------------------------------
-__device__ void emit_obs(const EnvDev& d, int env, EnvLds& s, const gm_obs_buffers& o) {
+template <class ES>
+__device__ void emit_obs(const EnvDev& d, int env, ES& s, const gm_obs_buffers& o) {
     const int l = lane_id();
     const int N = d.N, A = d.A;
     if (o.node_obs) {
@@ -209,7 +215,8 @@ __device__ void emit_obs(const EnvDev& d, int env, EnvLds& s, const gm_obs_buffe
     }
 }
 
-__device__ void load_packets_lds(const EnvDev& d, int env, EnvLds& s) {
+template <class ES>
+__device__ void load_packets_lds(const EnvDev& d, int env, ES& s) {
     const int l = lane_id();
     if (l < d.A) {
         size_t p = (size_t)env * d.A + l;
@@ -226,16 +233,17 @@ __device__ void load_packets_lds(const EnvDev& d, int env, EnvLds& s) {
 // ---------------------------------------------------------------------------
 // Topology generation (network.py:122-272), one wave per env, state in LDS.
 // ---------------------------------------------------------------------------
+template <int NC>
 struct TopoLds {
-    double x[MAX_NODES], y[MAX_NODES], d2[MAX_NODES];
+    double x[NC], y[NC], d2[NC];
     uint32_t tkey[MT_N];
-    int32_t deg[MAX_NODES];
-    uint64_t adj[MAX_NODES][2];
-    int32_t node_edges[MAX_NODES * 3];
-    int32_t ea[MAX_EDGES], eb[MAX_EDGES], elen[MAX_EDGES];
+    int32_t deg[NC];
+    uint64_t adj[NC][2];
+    int32_t node_edges[NC * 3];
+    int32_t ea[NC * 3 / 2], eb[NC * 3 / 2], elen[NC * 3 / 2];
     int32_t n_edges;
-    int32_t cand_at_rank[MAX_NODES];
-    uint8_t ok_at_rank[MAX_NODES];
+    int32_t cand_at_rank[NC];
+    uint8_t ok_at_rank[NC];
 };
 
 __device__ __forceinline__ bool is_excluded(const EnvDev& d, int64_t sd) {
@@ -259,7 +267,8 @@ __device__ int64_t draw_topology_seed(const EnvDev& d, R& r) {  // network.py:23
 
 // One _create_random_topology attempt from the LDS stream t.tkey (fresh after seeding).
 // Node-indexed work runs in lanes v = l and v = l + 64 (N <= 128).
-__device__ bool topology_attempt(const EnvDev& d, TopoLds& t, LocalRng& tr) {
+template <class TS>
+__device__ bool topology_attempt(const EnvDev& d, TS& t, LocalRng& tr) {
     const int l = lane_id();
     const int N = d.N;
     // positions: node i draws x then y (network.py:134-138) = tempered words 4i..4i+3
@@ -375,7 +384,8 @@ __device__ bool topology_attempt(const EnvDev& d, TopoLds& t, LocalRng& tr) {
     return reach[0] == full0 && reach[1] == full1;
 }
 
-__device__ void topology_finish(const EnvDev& d, int env, TopoLds& t, int16_t* dist, int64_t seed, int reps) {
+template <class TS>
+__device__ void topology_finish(const EnvDev& d, int env, TS& t, int16_t* dist, int64_t seed, int reps) {
     const int l = lane_id();
     const int N = d.N, E = d.E;
     // per-node edges sorted by neighbour id (network.py:191-195)
@@ -427,7 +437,8 @@ __device__ void topology_finish(const EnvDev& d, int env, TopoLds& t, int16_t* d
 }
 
 // network.py:242-258: fresh stream per topology seed, reseed on invalid topology
-__device__ void generate_topology(const EnvDev& d, int env, TopoLds& t, int16_t* dist, int64_t seed,
+template <class TS>
+__device__ void generate_topology(const EnvDev& d, int env, TS& t, int16_t* dist, int64_t seed,
                                   bool allow_retry) {
     LocalRng tr;
     tr.key = t.tkey;
@@ -449,20 +460,22 @@ __device__ void generate_topology(const EnvDev& d, int env, TopoLds& t, int16_t*
     __syncthreads();
 }
 
+template <int NC>
 struct ResetLds {
-    EnvLds env;
-    TopoLds topo;
-    int16_t dist[MAX_NODES * MAX_NODES];  // Floyd-Warshall APSP
+    EnvLds<NC> env;
+    TopoLds<NC> topo;
+    int16_t dist[NC * NC];  // Floyd-Warshall APSP
 };
 
 // src/env/routing.py:160-178 (+ network.py:366-371): new topology (per mode), zero
 // loads, respawn every packet in id order (reset_packet, routing.py:119-144).
+template <int NC>
 __global__ __launch_bounds__(64) void k_env_reset(EnvDev d, const uint8_t* mask, gm_obs_buffers o) {
     const int env = blockIdx.x;
     if (mask && !mask[env]) return;
     const int l = lane_id();
-    __shared__ ResetLds S;
-    EnvLds& s = S.env;
+    __shared__ ResetLds<NC> S;
+    EnvLds<NC>& s = S.env;
     MainRng r = open_rng(d, env, s);
     const int N = d.N, A = d.A;
 
@@ -541,11 +554,12 @@ struct StepOut {
 };
 
 // src/env/routing.py:360-520
+template <int NC>
 __global__ __launch_bounds__(64) void k_env_step(EnvDev d, const int32_t* act, StepOut out, gm_obs_buffers o) {
     const int env = blockIdx.x;
     const int l = lane_id();
     const int N = d.N, A = d.A, E = d.E;
-    __shared__ EnvLds s;
+    __shared__ EnvLds<NC> s;
     load_topology_lds(d, env, s);
 
     // packet a in lane a (registers)
@@ -757,9 +771,10 @@ __global__ __launch_bounds__(64) void k_env_step(EnvDev d, const int32_t* act, S
     if (o.obs || o.node_obs || o.agent_node || o.agent_adj) emit_obs(d, env, s, o);
 }
 
+template <int NC>
 __global__ __launch_bounds__(64) void k_env_observe(EnvDev d, gm_obs_buffers o) {
     const int env = blockIdx.x;
-    __shared__ EnvLds s;
+    __shared__ EnvLds<NC> s;
     load_topology_lds(d, env, s);
     load_packets_lds(d, env, s);
     emit_obs(d, env, s, o);
@@ -818,17 +833,19 @@ __global__ __launch_bounds__(64) void k_policy_egreedy(EnvDev d, const float* q,
 // Only the latest push of a node can be live, so the heap is the per-node
 // (seen, counter) pair. first[s][t] = first hop on the s -> t path.
 // LDS: first 16 KB + seen/cnt 32 KB + the topology image.
+template <int NC>
 struct FirstHopLds {
-    EnvLds s;
-    uint8_t first[MAX_NODES * MAX_NODES];
-    int16_t seen[MAX_NODES * WAVE];
-    int16_t cnt[MAX_NODES * WAVE];
+    EnvLds<NC> s;
+    uint8_t first[NC * NC];
+    int16_t seen[NC * WAVE];
+    int16_t cnt[NC * WAVE];
 };
 
-__device__ void first_hops_lds(const EnvDev& d, int env, FirstHopLds& F) {
+template <class FS>
+__device__ void first_hops_lds(const EnvDev& d, int env, FS& F) {
     const int l = lane_id();
     const int N = d.N;
-    EnvLds& s = F.s;
+    auto& s = F.s;
     uint8_t* first = F.first;
     int16_t* seen = F.seen;
     int16_t* cnt = F.cnt;
@@ -880,13 +897,14 @@ __device__ void first_hops_lds(const EnvDev& d, int env, FirstHopLds& F) {
     __syncthreads();
 }
 
+template <int NC>
 __global__ __launch_bounds__(64) void k_policy_shortest_path(EnvDev d, int32_t* actions) {
     const int env = blockIdx.x;
     const int l = lane_id();
     const int N = d.N, A = d.A;
-    __shared__ FirstHopLds F;
+    __shared__ FirstHopLds<NC> F;
     first_hops_lds(d, env, F);
-    EnvLds& s = F.s;
+    auto& s = F.s;
     const uint8_t* first = F.first;
     if (l < A) {
         const size_t p = (size_t)env * A + l;
@@ -904,9 +922,10 @@ __global__ __launch_bounds__(64) void k_policy_shortest_path(EnvDev d, int32_t* 
     }
 }
 
+template <int NC>
 __global__ __launch_bounds__(64) void k_env_first_hops(EnvDev d, int32_t* out) {
     const int env = blockIdx.x;
-    __shared__ FirstHopLds F;
+    __shared__ FirstHopLds<NC> F;
     first_hops_lds(d, env, F);
     const int N = d.N;
     for (int i = lane_id(); i < N * N; i += WAVE) out[(size_t)env * N * N + i] = F.first[i];
@@ -968,13 +987,15 @@ __global__ void k_final_info(EnvDev d, double* out) {
 // (reseeding on invalid graphs) gives the final seed; unique seeds in order.
 constexpr int MAX_SEED_LIST = 4096;
 
+template <int NC>
 struct SeedListLds {
-    EnvLds env;
-    TopoLds topo;
+    EnvLds<NC> env;
+    TopoLds<NC> topo;
 };
 
+template <int NC>
 __global__ __launch_bounds__(64) void k_build_seed_list(EnvDev d, int count, int64_t* out) {
-    __shared__ SeedListLds S;
+    __shared__ SeedListLds<NC> S;
     __shared__ int64_t found[MAX_SEED_LIST];
     MainRng r = open_rng(d, 0, S.env);
     int have = 0;
@@ -1011,6 +1032,8 @@ __global__ __launch_bounds__(64) void k_build_seed_list(EnvDev d, int count, int
     for (int i = lane_id(); i < have; i += WAVE) out[i] = found[i];
     close_rng(d, 0, r);
 }
+
+inline int ncap(int n) { return n <= 64 ? 64 : 128; }
 
 bool has_obs(const gm_obs_buffers* o) {
     return o && (o->obs || o->node_obs || o->agent_node || o->agent_adj);
@@ -1162,7 +1185,8 @@ extern "C" int gm_env_reset(gm_env* env, const uint8_t* reset_mask, const gm_obs
     int rc = check_obs(env, obs);
     if (rc) return rc;
     gm_obs_buffers o = obs ? *obs : gm_obs_buffers{};
-    hipLaunchKernelGGL(k_env_reset, dim3(env->d.n_env), dim3(64), 0, (hipStream_t)stream, env->d, reset_mask, o);
+    if (ncap(env->d.N) == 64) hipLaunchKernelGGL(k_env_reset<64>, dim3(env->d.n_env), dim3(64), 0, (hipStream_t)stream, env->d, reset_mask, o);
+    else hipLaunchKernelGGL(k_env_reset<128>, dim3(env->d.n_env), dim3(64), 0, (hipStream_t)stream, env->d, reset_mask, o);
     return check_launch();
 }
 
@@ -1177,7 +1201,8 @@ extern "C" int gm_env_step(gm_env* env, const int32_t* actions, float* reward, u
     so.info = info;
     so.det = detail ? *detail : gm_step_detail{};
     gm_obs_buffers o = obs ? *obs : gm_obs_buffers{};
-    hipLaunchKernelGGL(k_env_step, dim3(env->d.n_env), dim3(64), 0, (hipStream_t)stream, env->d, actions, so, o);
+    if (ncap(env->d.N) == 64) hipLaunchKernelGGL(k_env_step<64>, dim3(env->d.n_env), dim3(64), 0, (hipStream_t)stream, env->d, actions, so, o);
+    else hipLaunchKernelGGL(k_env_step<128>, dim3(env->d.n_env), dim3(64), 0, (hipStream_t)stream, env->d, actions, so, o);
     return check_launch();
 }
 
@@ -1190,13 +1215,15 @@ __global__ void k_topology_rewind(EnvDev d, int interleave) {
 
 extern "C" int gm_policy_shortest_path(gm_env* env, int32_t* actions, void* stream) {
     if (!env || !actions) return gm_fail(GM_ERR_INVALID_ARG, "gm_policy_shortest_path: null argument");
-    hipLaunchKernelGGL(k_policy_shortest_path, dim3(env->d.n_env), dim3(64), 0, (hipStream_t)stream, env->d, actions);
+    if (ncap(env->d.N) == 64) hipLaunchKernelGGL(k_policy_shortest_path<64>, dim3(env->d.n_env), dim3(64), 0, (hipStream_t)stream, env->d, actions);
+    else hipLaunchKernelGGL(k_policy_shortest_path<128>, dim3(env->d.n_env), dim3(64), 0, (hipStream_t)stream, env->d, actions);
     return check_launch();
 }
 
 extern "C" int gm_env_first_hops(gm_env* env, int32_t* out, void* stream) {
     if (!env || !out) return gm_fail(GM_ERR_INVALID_ARG, "gm_env_first_hops: null argument");
-    hipLaunchKernelGGL(k_env_first_hops, dim3(env->d.n_env), dim3(64), 0, (hipStream_t)stream, env->d, out);
+    if (ncap(env->d.N) == 64) hipLaunchKernelGGL(k_env_first_hops<64>, dim3(env->d.n_env), dim3(64), 0, (hipStream_t)stream, env->d, out);
+    else hipLaunchKernelGGL(k_env_first_hops<128>, dim3(env->d.n_env), dim3(64), 0, (hipStream_t)stream, env->d, out);
     return check_launch();
 }
 
@@ -1235,7 +1262,8 @@ extern "C" int gm_env_observe(gm_env* env, const gm_obs_buffers* obs, void* stre
     if (!has_obs(obs)) return GM_OK;
     int rc = check_obs(env, obs);
     if (rc) return rc;
-    hipLaunchKernelGGL(k_env_observe, dim3(env->d.n_env), dim3(64), 0, (hipStream_t)stream, env->d, *obs);
+    if (ncap(env->d.N) == 64) hipLaunchKernelGGL(k_env_observe<64>, dim3(env->d.n_env), dim3(64), 0, (hipStream_t)stream, env->d, *obs);
+    else hipLaunchKernelGGL(k_env_observe<128>, dim3(env->d.n_env), dim3(64), 0, (hipStream_t)stream, env->d, *obs);
     return check_launch();
 }
 
@@ -1284,7 +1312,8 @@ extern "C" int gm_build_seed_list(int32_t n_nodes, int64_t init_seed, int32_t co
         gm_env_destroy(env);
         return rc;
     }
-    hipLaunchKernelGGL(k_build_seed_list, dim3(1), dim3(64), 0, 0, env->d, count, dout);
+    if (ncap(env->d.N) == 64) hipLaunchKernelGGL(k_build_seed_list<64>, dim3(1), dim3(64), 0, 0, env->d, count, dout);
+    else hipLaunchKernelGGL(k_build_seed_list<128>, dim3(1), dim3(64), 0, 0, env->d, count, dout);
     rc = check_launch();
     if (rc == GM_OK) {
         hipError_t e = hipMemcpy(out, dout, (size_t)count * sizeof(int64_t), hipMemcpyDeviceToHost);

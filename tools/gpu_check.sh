@@ -21,6 +21,10 @@ for s in "$@"; do
         tests) step gpu_tests 900 python -m pytest tests -m gpu -x -q --tb=short --timeout=300 -p no:cacheprovider || exit $? ;;
         envtests) step env_tests 600 python -m pytest tests/test_env_gpu.py -x -q --tb=short --timeout=300 -p no:cacheprovider || exit $? ;;
         nettests) step net_tests 600 python -m pytest tests/test_netmon_gpu.py tests/test_train_gpu.py -x -q --tb=short --timeout=300 -p no:cacheprovider || exit $? ;;
+        sl) step sl_bench 600 python graph-marl_amd/sl.py --bench --n-nodes 100 --batch-size 8192 --sequence-length 8 \
+                --netmon-iterations 1 --iterations 5 --warmup 2 || exit $? ;;
+        sl20) step sl20_bench 600 python graph-marl_amd/sl.py --bench --n-nodes 20 --batch-size 1024 --sequence-length 4 \
+                --netmon-iterations 3 --iterations 20 --warmup 3 || exit $? ;;
         gemm) step gemm 300 python tools/gemm_bench.py || exit $? ;;
         bench) step bench 600 python bench.py || exit $? ;;
         benchq) step bench 300 python bench.py --no-cpu-baseline --steps 100 || exit $? ;;
