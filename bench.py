@@ -80,9 +80,15 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # GM_BENCH_SHARE_GPU=1 rehearses the N-rank path on one GPU (all ranks on cuda:0, gloo)
+    share = os.environ.get("GM_BENCH_SHARE_GPU") == "1"
     if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        gpu = 0 if share else local
+        torch.cuda.set_device(gpu)
+        if share:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", gpu))
     else:
         torch.cuda.set_device(0)
     dev = torch.device("cuda", torch.cuda.current_device())
@@ -133,7 +139,7 @@ def main():
             dist.barrier()
         elapsed = time.perf_counter() - t0
         prof, L.PROF = L.PROF, None
-    el = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    el = torch.tensor([elapsed], dtype=torch.float64, device="cpu" if share else dev)
     if world > 1:
         dist.all_reduce(el, op=dist.ReduceOp.MAX)
     elapsed = float(el.item())

@@ -25,6 +25,9 @@ for s in "$@"; do
                 --netmon-iterations 1 --iterations 5 --warmup 2 || exit $? ;;
         sl20) step sl20_bench 600 python graph-marl_amd/sl.py --bench --n-nodes 20 --batch-size 1024 --sequence-length 4 \
                 --netmon-iterations 3 --iterations 20 --warmup 3 || exit $? ;;
+        dist2) GM_BENCH_SHARE_GPU=1 step dist2 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
+                --master-addr 127.0.0.1 --master-port 29511 bench.py --gpus 2 --steps 20 --warmup 5 \
+                --no-cpu-baseline || exit $? ;;
         gemm) step gemm 300 python tools/gemm_bench.py || exit $? ;;
         bench) step bench 600 python bench.py || exit $? ;;
         benchq) step bench 300 python bench.py --no-cpu-baseline --steps 100 || exit $? ;;
