@@ -56,6 +56,9 @@ def kernel_cost(tag, n_env, N, A, E):
     if kind in ("linear", "lstm", "lstm_agg"):
         m, n, k = (int(v) for v in tag.split(":")[2].split("x"))
         return "mfma", 2.0 * m * n * k
+    if kind == "routing_enc":
+        rows, n = (int(v) for v in tag.split(":")[2].split("x"))
+        return "hbm", rows * n * 4 + rows * 11 * 4  # write y, read the 11 nonzero features per row
     if kind == "mp_aggregate":
         rows, H = (int(v) for v in tag.split(":")[1].split("x"))
         return "hbm", rows * H * 4 * 2 + rows * 3 * 4  # read h, write M, read nbr

@@ -209,6 +209,91 @@ __global__ __launch_bounds__(256) void k_lstm_pw_bwd(const float* __restrict__ d
     dc[gid] = dct * f;
 }
 
+
+// First NetMon encoder layer on routing node observations (src/model.py:272-276 on the
+// node obs of src/env/routing.py:187-235). Row n of graph g is
+//   [onehot(n) | cnt | load | 3 x (onehot(nbr_k) | len_k | load_k)]
+// so W x touches 12 of the 4N+8 weight columns: the dense GEMM's K = 4N+8 collapses to a
+// 12-term gather over W^T staged in LDS (BN output columns per block, 64 lanes x BN/64
+// columns). HBM-bound on the output rows (n floats per node).
+template <int CPL>  // output columns per lane (BN = 64 * CPL)
+__global__ __launch_bounds__(256) void k_routing_enc(const float* __restrict__ x, long long ldx,
+                                                     const int32_t* __restrict__ nbr, int G, int N,
+                                                     const float* __restrict__ wt, const float* __restrict__ b,
+                                                     int n, int act, float* __restrict__ y, long long ldy,
+                                                     int rows_per_block) {
+    constexpr int BN = 64 * CPL;
+    extern __shared__ float sw[];  // [K][BN]
+    const int K = 4 * N + 8;
+    const int c0 = blockIdx.y * BN;
+    for (int i = threadIdx.x; i < K * (BN / 4); i += blockDim.x) {
+        const int r = i / (BN / 4), c4 = i - r * (BN / 4);
+        reinterpret_cast<float4*>(sw)[i] = *reinterpret_cast<const float4*>(wt + (size_t)r * n + c0 + 4 * c4);
+    }
+    __syncthreads();
+    const int lane = threadIdx.x & 63;
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int col = CPL * lane;
+    float bias[CPL];
+#pragma unroll
+    for (int j = 0; j < CPL; j++) bias[j] = b ? b[c0 + col + j] : 0.f;
+    const long long M = (long long)G * N;
+    // each wave owns 64 consecutive rows: lane l gathers the 11 nonzero features of row
+    // base + l up front (coalesced, one latency), the row loop broadcasts them by readlane
+    const long long base = (long long)blockIdx.x * rows_per_block + (long long)wv * 64;
+    if (base >= M) return;
+    const int nrows = M - base < 64 ? (int)(M - base) : 64;
+    int fv = 0, f_nb[3] = {0, 0, 0};
+    float f_cnt = 0.f, f_tl = 0.f, f_len[3] = {0.f, 0.f, 0.f}, f_ld[3] = {0.f, 0.f, 0.f};
+    if (lane < nrows) {
+        const long long r = base + lane;
+        const int g = (int)(r / N);
+        fv = (int)(r - (long long)g * N);
+        const float* xr = x + r * ldx;
+        f_cnt = xr[N];
+        f_tl = xr[N + 1];
+#pragma unroll
+        for (int k = 0; k < 3; k++) {
+            const int off = N + 2 + k * (N + 2);
+            f_len[k] = xr[off + N];
+            f_ld[k] = xr[off + N + 1];
+            f_nb[k] = nbr[((size_t)g * N + fv) * 3 + k];
+        }
+    }
+    for (int i = 0; i < nrows; i++) {
+        const int v = __builtin_amdgcn_readlane(fv, i);
+        const float cnt = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(f_cnt), i));
+        const float tl = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(f_tl), i));
+        float acc[CPL];
+#pragma unroll
+        for (int j = 0; j < CPL; j++)
+            acc[j] = bias[j] + sw[v * BN + col + j] + cnt * sw[N * BN + col + j] + tl * sw[(N + 1) * BN + col + j];
+#pragma unroll
+        for (int k = 0; k < 3; k++) {
+            const int off = N + 2 + k * (N + 2);
+            const int u = __builtin_amdgcn_readlane(f_nb[k], i);
+            const float ln = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(f_len[k]), i));
+            const float ld = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(f_ld[k]), i));
+#pragma unroll
+            for (int j = 0; j < CPL; j++)
+                acc[j] += sw[(off + u) * BN + col + j] + ln * sw[(off + N) * BN + col + j] +
+                          ld * sw[(off + N + 1) * BN + col + j];
+        }
+        float* yr = y + (base + i) * ldy + c0 + col;
+        if (CPL == 2) {
+            float a0 = acc[0], a1 = acc[CPL - 1];
+            if (act) {
+                a0 = a0 >= 0.f ? a0 : 0.01f * a0;
+                a1 = a1 >= 0.f ? a1 : 0.01f * a1;
+            }
+            *reinterpret_cast<float2*>(yr) = make_float2(a0, a1);
+        } else {
+#pragma unroll
+            for (int j = 0; j < CPL; j++) yr[j] = act ? (acc[j] >= 0.f ? acc[j] : 0.01f * acc[j]) : acc[j];
+        }
+    }
+}
+
 inline unsigned nblocks(long long total, int bs) { return (unsigned)((total + bs - 1) / bs); }
 
 int launched() {
@@ -307,5 +392,27 @@ extern "C" int gm_lstm_pointwise_bwd(const float* dh1, const float* dc1, const f
     long long total = (long long)m * H;
     hipLaunchKernelGGL(k_lstm_pw_bwd, dim3(nblocks(total, 256)), dim3(256), 0, (hipStream_t)stream, dh1, dc1, act, c,
                        c1, m, H, dgates, dc);
+    return launched();
+}
+
+extern "C" int gm_routing_node_encoder(const float* x, int64_t ldx, const int32_t* nbr, int32_t G, int32_t N,
+                                       const float* wt, const float* b, int32_t n, int32_t act, float* y, int64_t ldy,
+                                       void* stream) {
+    if (!x || !nbr || !wt || !y || G <= 0 || N < 4 || n <= 0 || (n % 64) || act < 0 || act > 1 ||
+        ldx < 4 * N + 8 || ldy < n || (ldy % 2) || (reinterpret_cast<uintptr_t>(wt) & 15))
+        return gm_fail(GM_ERR_INVALID_ARG, "gm_routing_node_encoder: bad arguments (n % 64 == 0, 16-byte W^T)");
+    const int K = 4 * N + 8;
+    const int cpl = (n % 128 == 0 && (size_t)K * 128 * 4 <= 65536) ? 2 : 1;
+    const size_t lds = (size_t)K * 64 * cpl * 4;
+    if (lds > 65536) return gm_fail(GM_ERR_UNSUPPORTED, "gm_routing_node_encoder: 4N+8 too large for the LDS slice");
+    const long long M = (long long)G * N;
+    const int rows = 256;
+    dim3 grid((unsigned)((M + rows - 1) / rows), (unsigned)(n / (64 * cpl)));
+    if (cpl == 2)
+        hipLaunchKernelGGL(k_routing_enc<2>, grid, dim3(256), lds, (hipStream_t)stream, x, (long long)ldx, nbr, G, N,
+                           wt, b, n, act, y, (long long)ldy, rows);
+    else
+        hipLaunchKernelGGL(k_routing_enc<1>, grid, dim3(256), lds, (hipStream_t)stream, x, (long long)ldx, nbr, G, N,
+                           wt, b, n, act, y, (long long)ldy, rows);
     return launched();
 }

@@ -1,7 +1,7 @@
 """Fused no-grad rollout path over gm_gemm_f32 (include/graph_marl_amd.h).
 
 NetMon step (reference src/model.py:476-580):
-  x  = MLP encoder(node_obs)                                   gm_linear_f32 x3
+  x  = MLP encoder(node_obs)              gm_routing_node_encoder (layer 0) + gm_linear_f32 x2
   S1 = LSTM_obs([x | h_state], c_state)                        one GEMM, gate math in epilogue
   S2 = LSTM_upd([Σ_{I+A} h(S1) | h(S1)], c(S1))  (K times)     aggregate folded into the A load
 state = S_K ([h | c] per node, the reference's (B, N, 2H) layout), h_prev = h before the
@@ -138,6 +138,25 @@ def _linear(x, ldx, k, lin, out):
     return out
 
 
+def routing_encoder_ok(lin, N, Fd, nbr):
+    """The routing node-obs layout (4N+8 columns, degree-3 neighbour table) lets the first
+    encoder layer run as a 12-column gather (gm_routing_node_encoder)."""
+    return (Fd == 4 * N + 8 and nbr.shape[-1] == 3 and lin.out_features % 64 == 0 and
+            (4 * N + 8) * 64 * (2 if lin.out_features % 128 == 0 and (4 * N + 8) <= 128 else 1) * 4 <= 65536)
+
+
+def routing_encoder(lin, x, nbr, G, N, out):
+    """y = act(W x + b) on routing node observations from their nonzero entries."""
+    if not hasattr(lin, "_packed_t"):
+        lin._packed_t = Packed()
+    wt = lin._packed_t.get(_key(lin.weight), lambda: lin.weight.detach().t().contiguous())
+    with L.timed(lin.tag and f"routing_enc:{lin.tag}:{G * N}x{lin.out_features}"):
+        L.check(L.lib().gm_routing_node_encoder(L.ptr(x), x.stride(0), L.ptr(nbr), G, N, L.ptr(wt), L.ptr(lin.bias),
+                                                lin.out_features, lin.act, L.ptr(out), out.stride(0),
+                                                L.stream_ptr()))
+    return out
+
+
 @torch.no_grad()
 def netmon_step(netmon, node_obs, nbr, state):
     """One NetMon step for B graphs. node_obs [B, N, F]; nbr int32 [B, N, deg]; state
@@ -150,7 +169,11 @@ def netmon_step(netmon, node_obs, nbr, state):
     M = B * N
     dev = node_obs.device
     x = node_obs.reshape(M, Fd)
-    for lin in netmon.encode.linear_layers:
+    layers = list(netmon.encode.linear_layers)
+    if routing_encoder_ok(layers[0], N, Fd, nbr):
+        x = routing_encoder(layers[0], x, nbr, B, N, torch.empty(M, layers[0].out_features, device=dev))
+        layers = layers[1:]
+    for lin in layers:
         x = _linear(x, x.stride(0), x.shape[1], lin, torch.empty(M, lin.out_features, device=dev))
     if state is None:
         state = torch.zeros(B, N, 2 * H, device=dev)

@@ -218,6 +218,15 @@ typedef struct {
 int gm_gemm_f32(const gm_a_src* src0, const gm_a_src* src1, const float* w, int64_t ldw, const float* b, int32_t m,
                 int32_t n, int32_t epilogue, float* y, int64_t ldy, float* y2, int64_t ldy2, const float* c_in,
                 int64_t ldc, float* act_out, void* stream);
+/* First NetMon encoder layer on routing node observations (src/model.py:272-276 applied
+ * to src/env/routing.py:187-235): y = act(W x + b) from the 12 nonzero entries of each node
+ * row (own one-hot, packet count and load, per neighbour one-hot, edge length, edge load)
+ * instead of the dense K = 4N+8 product. x: node obs rows [G*N][ldx]; nbr int32 [G][N][3]
+ * ascending; wt = W^T [4N+8][n] row-major (16-byte aligned); b [n] or NULL; y [G*N][ldy].
+ * n % 64 == 0; act 0 none, 1 leaky_relu(0.01). */
+int gm_routing_node_encoder(const float* x, int64_t ldx, const int32_t* nbr, int32_t G, int32_t N,
+                            const float* wt, const float* b, int32_t n, int32_t act, float* y, int64_t ldy,
+                            void* stream);
 /* Tuning knob: tile configuration of gm_gemm_f32 (-1 = per-shape default; 0 = 128x128x32;
  * 1 = 128x256x16; 2 = 256x128x16 (LSTM: 256x128x16); 3 = 128x128x16). Process-wide. */
 int gm_gemm_set_tile(int32_t tile);

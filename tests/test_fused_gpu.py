@@ -111,3 +111,26 @@ def test_fused_netmon_vs_reference_golden(vi):
         Hh = int(H)
         out = M.netmon_readout(state.reshape(B * N, -1)[:, :Hh].contiguous(), hprev[:, :Hh].contiguous(), nbr, an)
         np.testing.assert_allclose(out.view(B, -1, 4 * Hh).cpu().numpy(), g[f"v{vi}_mapped_{t}"], atol=1e-5, rtol=0)
+
+
+@pytest.mark.parametrize("n,out", [(20, 512), (50, 512), (10, 64), (20, 192)])
+def test_routing_node_encoder_vs_torch(n, out):
+    """Sparse first encoder layer on real routing node observations vs the dense fp32 product."""
+    gm = importlib.import_module("graph-marl_amd")
+    M = importlib.import_module("graph-marl_amd.model")
+    FU = importlib.import_module("graph-marl_amd.fused")
+    B, A = 64, 20
+    env = gm.Routing(gm.Network(n, random_topology=True, excluded_seeds=gm.EVAL_SEEDS), A, n_env=B, seed=5)
+    env.reset()
+    rng = np.random.RandomState(0)
+    for _ in range(5):
+        env.step_(torch.as_tensor(rng.randint(0, 4, (B, A)), dtype=torch.int32, device="cuda"))
+    x = env.node_obs.reshape(-1, 4 * n + 8)
+    torch.manual_seed(1)
+    lin = M.Linear(4 * n + 8, out, act=1).cuda()
+    assert FU.routing_encoder_ok(lin, n, 4 * n + 8, env.nbr)
+    y = FU.routing_encoder(lin, x, env.nbr, B, n, torch.empty(B * n, out, device="cuda"))
+    ref = torch.nn.functional.leaky_relu(torch.nn.functional.linear(x.double(), lin.weight.double(),
+                                                                    lin.bias.double()), 0.01)
+    err = (y.double() - ref).abs().max().item()
+    assert err < 1e-5, err
