@@ -87,8 +87,8 @@ struct Cfg {
     static constexpr int RSTEP = THREADS / (BK / 4);   // rows between a thread's A rows
 };
 
-template <int WGM, int WGN, int TM, int TN, int BK_, int AMODE, int EPI>
-__global__ __launch_bounds__(WGM* WGN * 64, 2) void k_gemm(ASrc a0, ASrc a1, const float* __restrict__ w,
+template <int WGM, int WGN, int TM, int TN, int BK_, int AMODE, int EPI, int OCC>
+__global__ __launch_bounds__(WGM* WGN * 64, OCC) void k_gemm(ASrc a0, ASrc a1, const float* __restrict__ w,
                                                             long long ldw, unsigned wbytes, int M, int N, int K,
                                                             Epi ep) {
     using C = Cfg<WGM, WGN, TM, TN, BK_>;
@@ -112,6 +112,9 @@ __global__ __launch_bounds__(WGM* WGN * 64, 2) void k_gemm(ASrc a0, ASrc a1, con
     const int rbase = tid / (BK / 4);
     int rowoff0[C::AQ], rowoff1[C::AQ];
     int src[C::AQ][4];  // AGGREGATE: member rows; READOUT: segment source rows (-1 = none)
+    // READOUT: byte offsets of the 4 segment rows in separate register arrays (one array
+    // indexed by the runtime segment would be demoted to scratch)
+    int ro0[C::AQ], ro1[C::AQ], ro2[C::AQ], ro3[C::AQ];
     float scale[C::AQ];
 #pragma unroll
     for (int q = 0; q < C::AQ; q++) {
@@ -143,6 +146,10 @@ __global__ __launch_bounds__(WGM* WGN * 64, 2) void k_gemm(ASrc a0, ASrc a1, con
                 int m = j - 1 < a0.deg ? nb[j - 1] : -1;
                 src[q][j] = m >= 0 ? g * a0.n_nodes + m : -1;
             }
+            ro0[q] = (int)(src[q][0] * a0.ld0) * 4;
+            ro1[q] = src[q][1] >= 0 ? (int)(src[q][1] * a0.ld1) * 4 : OOB;
+            ro2[q] = src[q][2] >= 0 ? (int)(src[q][2] * a0.ld1) * 4 : OOB;
+            ro3[q] = src[q][3] >= 0 ? (int)(src[q][3] * a0.ld1) * 4 : OOB;
         }
     }
     int woff[C::BQ];
@@ -172,16 +179,19 @@ __global__ __launch_bounds__(WGM* WGN * 64, 2) void k_gemm(ASrc a0, ASrc a1, con
                     ra[q] = make_float4(v.x * scale[q], v.y * scale[q], v.z * scale[q], v.w * scale[q]);
                 }
             } else {  // READOUT: the K tile lies inside one H-wide segment
-                const int seg = k0 / a0.hidden, ko = kl - seg * a0.hidden;
+                const int seg = k0 / a0.hidden, ko4 = (kl - seg * a0.hidden) * 4;
                 if (seg == 0) {
 #pragma unroll
-                    for (int q = 0; q < C::AQ; q++) ra[q] = bload(r0a, (int)(src[q][0] * a0.ld0 + ko) * 4);
+                    for (int q = 0; q < C::AQ; q++) ra[q] = bload(r0a, ro0[q] + ko4);
+                } else if (seg == 1) {
+#pragma unroll
+                    for (int q = 0; q < C::AQ; q++) ra[q] = bload(r0b, ro1[q] == OOB ? OOB : ro1[q] + ko4);
+                } else if (seg == 2) {
+#pragma unroll
+                    for (int q = 0; q < C::AQ; q++) ra[q] = bload(r0b, ro2[q] == OOB ? OOB : ro2[q] + ko4);
                 } else {
 #pragma unroll
-                    for (int q = 0; q < C::AQ; q++) {
-                        int s = seg == 1 ? src[q][1] : seg == 2 ? src[q][2] : src[q][3];
-                        ra[q] = bload(r0b, s >= 0 ? (int)(s * a0.ld1 + ko) * 4 : OOB);
-                    }
+                    for (int q = 0; q < C::AQ; q++) ra[q] = bload(r0b, ro3[q] == OOB ? OOB : ro3[q] + ko4);
                 }
             }
         } else {
@@ -313,12 +323,12 @@ __global__ __launch_bounds__(WGM* WGN * 64, 2) void k_gemm(ASrc a0, ASrc a1, con
     }
 }
 
-template <int WGM, int WGN, int TM, int TN, int BK_, int AMODE, int EPI>
+template <int WGM, int WGN, int TM, int TN, int BK_, int AMODE, int EPI, int OCC = 2>
 int launch(const ASrc& a0, const ASrc& a1, const float* w, long long ldw, unsigned wbytes, int M, int N, int K,
            const Epi& ep, hipStream_t st) {
     using C = Cfg<WGM, WGN, TM, TN, BK_>;
     const int T = ((M + C::BM - 1) / C::BM) * ((N + C::BN - 1) / C::BN);
-    hipLaunchKernelGGL((k_gemm<WGM, WGN, TM, TN, BK_, AMODE, EPI>), dim3(T), dim3(C::THREADS), 0, st, a0, a1, w,
+    hipLaunchKernelGGL((k_gemm<WGM, WGN, TM, TN, BK_, AMODE, EPI, OCC>), dim3(T), dim3(C::THREADS), 0, st, a0, a1, w,
                        ldw, wbytes, M, N, K, ep);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return gm_fail(GM_ERR_HIP, std::string("gm_gemm launch: ") + hipGetErrorString(e));
@@ -407,16 +417,21 @@ extern "C" int gm_gemm_f32(const gm_a_src* a0, const gm_a_src* a1, const float* 
     const int tile = g_tile;
 #define GM_L(WGM, WGN, TM, TN, BK_, AM, EP) \
     launch<WGM, WGN, TM, TN, BK_, AM, EP>(s0, s1, w, ldw, (unsigned)wb, m, n, K, ep, st)
+#define GM_L4(WGM, WGN, TM, TN, BK_, AM, EP) \
+    launch<WGM, WGN, TM, TN, BK_, AM, EP, 4>(s0, s1, w, ldw, (unsigned)wb, m, n, K, ep, st)
     if (epilogue == GM_EPI_LSTM) {
         if (n % 128 || !y2 || !c_in) return gm_fail(GM_ERR_INVALID_ARG, "gm_gemm_f32: LSTM epilogue needs 4H % 128 == 0");
         ep.hidden = n / 4;
+        // default: 128x128x16 at 4 blocks/CU (<= 128 VGPRs, 40 KB LDS): +20 % over 2 blocks/CU
         if (s0.mode == GM_A_DENSE) {
+            if (tile == 0) return GM_L(4, 1, 1, 4, 32, GM_A_DENSE, EPI_LSTM);
             if (tile == 2) return GM_L(4, 1, 2, 4, 16, GM_A_DENSE, EPI_LSTM);
-            return GM_L(4, 1, 1, 4, 32, GM_A_DENSE, EPI_LSTM);
+            return GM_L4(4, 1, 1, 4, 16, GM_A_DENSE, EPI_LSTM);
         }
         if (s0.mode == GM_A_AGGREGATE) {
+            if (tile == 0) return GM_L(4, 1, 1, 4, 32, GM_A_AGGREGATE, EPI_LSTM);
             if (tile == 2) return GM_L(4, 1, 2, 4, 16, GM_A_AGGREGATE, EPI_LSTM);
-            return GM_L(4, 1, 1, 4, 32, GM_A_AGGREGATE, EPI_LSTM);
+            return GM_L4(4, 1, 1, 4, 16, GM_A_AGGREGATE, EPI_LSTM);
         }
         return gm_fail(GM_ERR_UNSUPPORTED, "gm_gemm_f32: LSTM epilogue with readout source");
     }
@@ -431,6 +446,7 @@ extern "C" int gm_gemm_f32(const gm_a_src* a0, const gm_a_src* a1, const float* 
         if (t == 1) return GM_L(2, 2, 2, 4, 16, GM_A_READOUT, EPI_BIAS);
         if (t == 2) return GM_L(2, 2, 4, 2, 16, GM_A_READOUT, EPI_BIAS);
         if (t == 3) return GM_L(2, 2, 2, 2, 16, GM_A_READOUT, EPI_BIAS);
+        if (t == 4) return GM_L4(2, 2, 2, 2, 16, GM_A_READOUT, EPI_BIAS);
         return GM_L(2, 2, 2, 2, 32, GM_A_READOUT, EPI_BIAS);
     }
     if (s0.mode == GM_A_AGGREGATE) return GM_L(2, 2, 2, 2, 32, GM_A_AGGREGATE, EPI_BIAS);
@@ -438,12 +454,14 @@ extern "C" int gm_gemm_f32(const gm_a_src* a0, const gm_a_src* a1, const float* 
     if (t == 1) return GM_L(2, 2, 2, 4, 16, GM_A_DENSE, EPI_BIAS);
     if (t == 2) return GM_L(2, 2, 4, 2, 16, GM_A_DENSE, EPI_BIAS);
     if (t == 3) return GM_L(2, 2, 2, 2, 16, GM_A_DENSE, EPI_BIAS);
+    if (t == 4) return GM_L4(2, 2, 2, 2, 16, GM_A_DENSE, EPI_BIAS);
     return GM_L(2, 2, 2, 2, 32, GM_A_DENSE, EPI_BIAS);
 #undef GM_L
+#undef GM_L4
 }
 
 extern "C" int gm_gemm_set_tile(int32_t tile) {
-    if (tile < -1 || tile > 3) return gm_fail(GM_ERR_INVALID_ARG, "gm_gemm_set_tile: tile in [-1, 3]");
+    if (tile < -1 || tile > 4) return gm_fail(GM_ERR_INVALID_ARG, "gm_gemm_set_tile: tile in [-1, 4]");
     g_tile = tile;
     return GM_OK;
 }

@@ -228,7 +228,8 @@ int gm_routing_node_encoder(const float* x, int64_t ldx, const int32_t* nbr, int
                             const float* wt, const float* b, int32_t n, int32_t act, float* y, int64_t ldy,
                             void* stream);
 /* Tuning knob: tile configuration of gm_gemm_f32 (-1 = per-shape default; 0 = 128x128x32;
- * 1 = 128x256x16; 2 = 256x128x16 (LSTM: 256x128x16); 3 = 128x128x16). Process-wide. */
+ * 1 = 128x256x16; 2 = 256x128x16 (LSTM: 256x128x16); 3 = 128x128x16; 4 = 128x128x16 at 4
+ * blocks/CU). Process-wide. */
 int gm_gemm_set_tile(int32_t tile);
 
 /* ---------------------------------------------------------------------------

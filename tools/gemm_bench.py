@@ -18,7 +18,7 @@ SHAPES = [  # name, M, N, K
 ]
 
 
-TILES = [int(t) for t in os.environ.get("TILES", "-1,0,1,2,3").split(",")]
+TILES = [int(t) for t in os.environ.get("TILES", "-1,0,3,4").split(",")]
 
 
 def timeit(fn, reps=20):
@@ -64,6 +64,33 @@ def main():
         fl = 2.0 * m * n * k
         out[name] = {k2: {"us": round(min(v), 1), "tflops": round(fl / (min(v) * 1e-6) / 1e12, 1)} for k2, v in r.items()}
         print(name, json.dumps(out[name]), flush=True)
+    # DQN first layer as run in the rollout: A = [NetMon readout gathered per agent | env obs]
+    B_, N_, A_, H_ = 4096, 20, 20, 128
+    m = B_ * A_
+    state = torch.randn(B_ * N_, 2 * H_, device="cuda")
+    hprev = torch.randn(B_ * N_, 2 * H_, device="cuda")
+    nbr = torch.randint(0, N_, (B_, N_, 3), device="cuda", dtype=torch.int32)
+    agent_node = torch.randint(0, N_, (B_, A_), device="cuda", dtype=torch.int32)
+    obs = torch.randn(B_, A_, 644, device="cuda")
+    w = torch.randn(512, 642, device="cuda") / 642 ** 0.5
+    b = torch.randn(512, device="cuda")
+    wp, ldw = FU._pad_cols(w)
+    y = torch.empty(m, 512, device="cuda")
+
+    def ro():
+        a0 = FU.readout(state.data_ptr(), 2 * H_, hprev.data_ptr(), 2 * H_, nbr, agent_node, N_, H_)
+        FU.gemm(a0, FU.dense(obs.data_ptr(), 644, 130), wp.data_ptr(), ldw, b.data_ptr(), m, 512, 1, y.data_ptr(), 512)
+
+    lib = FU._setup()
+    r = {t: [] for t in TILES}
+    for _ in range(3):
+        for t in TILES:
+            lib.gm_gemm_set_tile(t)
+            r[t].append(timeit(ro))
+    lib.gm_gemm_set_tile(-1)
+    fl = 2.0 * m * 512 * 642
+    print("dqn.l1.readout", json.dumps({f"tile{t}": {"us": round(min(v), 1), "tflops": round(fl / (min(v) * 1e-6) / 1e12, 1)}
+                                        for t, v in r.items()}), flush=True)
     # fused LSTM cell GEMM (dense [x|h] source, gate epilogue)
     M_ = importlib.import_module("graph-marl_amd.model")
     H, m = 128, 81920
@@ -85,7 +112,7 @@ def main():
 
     lib = FU._setup()
     for name, fn in (("lstm_fused", lstm_dense), ("lstm_agg_fused", lstm_agg)):
-        r = {0: [], 2: []}
+        r = {0: [], 2: [], 4: []}
         for _ in range(3):
             for t in r:
                 lib.gm_gemm_set_tile(t)
