@@ -27,15 +27,21 @@ NETMON = ["netmon.enc0(K=88)", "netmon.enc1(K=512)", "netmon.enc2(K=256)", "netm
 DQN = ["dqn.enc0(K=642)", "dqn.enc1(K=512)", "dqn.q(K=256)"]
 
 
-def linear_labels(n_dispatch, episode_steps, netmon_iters=1):
-    """Call-site names of the k_linear_f32 dispatches of one bench.py process, in
-    launch order: reset (NetMon start-up step), then per step 3 DQN + 1 NetMon step,
+# k_gemm (gm_gemm_f32, fused path): encoder layer 0 runs in k_routing_enc, the LSTM
+# cells carry their gate epilogue, the DQN's first layer gathers the NetMon readout
+NETMON_G = ["netmon.enc1(K=512)", "netmon.enc2(K=256)", "netmon.rnn_obs(K=128+128)", "netmon.rnn_update(K=agg128+128)"]
+DQN_G = ["dqn.enc0(K=512 readout+130)", "dqn.enc1(K=512)", "dqn.q(K=256)"]
+
+
+def linear_labels(n_dispatch, episode_steps, netmon_iters=1, netmon=NETMON, dqn=DQN):
+    """Call-site names of the GEMM dispatches of one bench.py process, in launch
+    order: reset (NetMon start-up step), then per step the DQN layers + 1 NetMon step,
     and a reset after every `episode_steps` steps."""
-    nm = NETMON[:4] + [NETMON[4]] * netmon_iters
+    nm = netmon[:-1] + [netmon[-1]] * netmon_iters
     out = list(nm)
     step = 0
     while len(out) < n_dispatch:
-        out += DQN + nm
+        out += dqn + nm
         step += 1
         if step % episode_steps == 0:
             out += nm
@@ -43,9 +49,10 @@ def linear_labels(n_dispatch, episode_steps, netmon_iters=1):
 
 
 def relabel(rows, episode_steps):
-    lin = [r for r in rows if r["Kernel_Name"].startswith("k_linear_f32")]
-    for r, lab in zip(lin, linear_labels(len(lin), episode_steps)):
-        r["Kernel_Name"] = f"k_linear_f32[{lab}]"
+    for name, nm, dq in (("k_linear_f32", NETMON, DQN), ("k_gemm", NETMON_G, DQN_G)):
+        lin = [r for r in rows if r["Kernel_Name"].startswith(name)]
+        for r, lab in zip(lin, linear_labels(len(lin), episode_steps, netmon=nm, dqn=dq)):
+            r["Kernel_Name"] = f"{name}[{lab}]"
     return rows
 
 
