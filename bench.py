@@ -28,6 +28,7 @@ sys.path.insert(0, ROOT)
 METRIC = "env-steps/sec (routing, --netmon, 20-node graphs) at 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8 TB/s spec
 F32_MFMA_PEAK_TFS = 157.3  # MI355X_MICROARCH.md: f32-input MFMA dense peak
+F16_MFMA_PEAK_TFS = 16 * 157.3  # MI355X_MICROARCH.md: BF16/F16 dense = 16x the f32-input MFMA rate
 
 
 def parse():
@@ -45,17 +46,20 @@ def parse():
     p.add_argument("--no-kernel-timers", action="store_true")
     p.add_argument("--unfused", action="store_true", help="materialise the joint obs; separate LSTM/aggregate kernels")
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--no-f32-compare", action="store_true",
+                   help="skip the second timed pass with the exact-fp32 GEMM form (GM_GEMM=f32)")
     p.add_argument("--cpu-envs", type=int, default=256)
     p.add_argument("--cpu-steps", type=int, default=20)
     return p.parse_args()
 
 
-def kernel_cost(tag, n_env, N, A, E):
-    """(bound, algorithmic units per launch) for a timer tag — DESIGN.md §4."""
+def kernel_cost(tag, n_env, N, A, E, x3=False):
+    """(bound, algorithmic units per launch) for a timer tag — DESIGN.md §4. GEMMs in the
+    split-f16 form count the MFMA work they issue: 3 f16 products per fp32 multiply-add."""
     kind = tag.split(":")[0]
     if kind in ("linear", "lstm", "lstm_agg"):
         m, n, k = (int(v) for v in tag.split(":")[2].split("x"))
-        return "mfma", 2.0 * m * n * k
+        return ("mfma16" if x3 and n > 32 else "mfma"), (3.0 if x3 and n > 32 else 1.0) * 2.0 * m * n * k
     if kind == "routing_enc":
         rows, n = (int(v) for v in tag.split(":")[2].split("x"))
         return "hbm", rows * n * 4 + rows * 11 * 4  # write y, read the 11 nonzero features per row
@@ -124,30 +128,42 @@ def main():
             wenv.reset()
             state["ep"] = 0
 
-    with torch.no_grad():
-        wenv.reset()
-        for _ in range(args.warmup):
-            step()
-        torch.cuda.synchronize()
+    def timed_region(warmup, steps, timers):
+        with torch.no_grad():
+            wenv.reset()
+            state["ep"] = 0
+            for _ in range(warmup):
+                step()
+            torch.cuda.synchronize()
+            if world > 1:
+                dist.barrier()
+            if timers:
+                L.PROF = {}
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for _ in range(steps):
+                step()
+            torch.cuda.synchronize()
+            if world > 1:
+                dist.barrier()
+            elapsed = time.perf_counter() - t0
+            prof, L.PROF = L.PROF, None
+        el = torch.tensor([elapsed], dtype=torch.float64, device="cpu" if share else dev)
         if world > 1:
-            dist.barrier()
-        if not args.no_kernel_timers:
-            L.PROF = {}
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        for _ in range(args.steps):
-            step()
-        torch.cuda.synchronize()
-        if world > 1:
-            dist.barrier()
-        elapsed = time.perf_counter() - t0
-        prof, L.PROF = L.PROF, None
-    el = torch.tensor([elapsed], dtype=torch.float64, device="cpu" if share else dev)
-    if world > 1:
-        dist.all_reduce(el, op=dist.ReduceOp.MAX)
-    elapsed = float(el.item())
+            dist.all_reduce(el, op=dist.ReduceOp.MAX)
+        return float(el.item()), prof
+
+    x3 = L.GEMM_MODE == "x3"
+    elapsed, prof = timed_region(args.warmup, args.steps, not args.no_kernel_timers)
     total = B * world * args.steps
     value = total / elapsed
+    f32cmp = None
+    if x3 and world == 1 and not args.no_f32_compare:
+        # the same rollout with every GEMM in the exact-fp32 form, for reference
+        L.GEMM_MODE = "f32"
+        el32, _ = timed_region(5, args.steps, False)
+        L.GEMM_MODE = "x3"
+        f32cmp = {"value": round(B * args.steps / el32, 1), "ms_per_step": round(1e3 * el32 / args.steps, 4)}
 
     kernels = {}
     if prof:
@@ -157,22 +173,24 @@ def main():
     roof = None
     if kernels:
         dom = max(kernels, key=lambda k: kernels[k]["total_ms"])
-        bound, units = kernel_cost(dom, B, N, A, E)
+        bound, units = kernel_cost(dom, B, N, A, E, x3)
         sec = kernels[dom]["avg_us"] * 1e-6
-        if bound == "mfma":
+        if bound in ("mfma", "mfma16"):
             ach = units / sec / 1e12
-            roof = {"kernel": dom, "bound": "mfma", "achieved": round(ach, 2), "peak": F32_MFMA_PEAK_TFS,
-                    "unit": "TFLOP/s", "frac": round(ach / F32_MFMA_PEAK_TFS, 4), "traffic": None}
+            peak = F16_MFMA_PEAK_TFS if bound == "mfma16" else F32_MFMA_PEAK_TFS
+            roof = {"kernel": dom, "bound": "mfma", "achieved": round(ach, 2), "peak": peak,
+                    "unit": "TFLOP/s" + (" (f16 MFMA, 3 per fp32 multiply-add)" if bound == "mfma16" else " (f32 MFMA)"),
+                    "frac": round(ach / peak, 4), "traffic": None}
         else:
             ach = units / sec / 1e9
             roof = {"kernel": dom, "bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                     "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None}
         for tag, kv in kernels.items():
-            bound, units = kernel_cost(tag, B, N, A, E)
+            bound, units = kernel_cost(tag, B, N, A, E, x3)
             if bound:
                 s = kv["avg_us"] * 1e-6
-                kv["achieved"] = round(units / s / (1e12 if bound == "mfma" else 1e9), 2)
-                kv["unit"] = "TFLOP/s" if bound == "mfma" else "GB/s"
+                kv["achieved"] = round(units / s / (1e9 if bound == "hbm" else 1e12), 2)
+                kv["unit"] = {"hbm": "GB/s", "mfma": "TFLOP/s f32", "mfma16": "TFLOP/s f16"}[bound]
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -193,14 +211,16 @@ def main():
         line = {
             "metric": METRIC, "value": round(value, 1), "unit": "env-steps/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(1e3 * elapsed / args.steps, 4),
-            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+            "dtype": "f32 (GEMMs: 3xf16-split MFMA, f32 accumulate)" if x3 else "f32",
             "data": "synthetic: random-init NetMon+DQN weights, on-device random topologies and packets",
             "config": {"workload": f"routing rollout --netmon (NetMon K={K}, H=128, enc 512,256, lstm, sum) + "
                                    f"DQN 512,256 eps-greedy, {'random' if args.random_topology else 'fixed'} "
                                    f"{N}-node topologies, episode {args.episode_steps} steps",
                        "n_env_per_gpu": B, "n_nodes": N, "n_data": A, "netmon_iterations": K,
+                       "gemm_form": L.GEMM_MODE,
                        "parallelism": f"dp{world} (env shards, no rollout collective)"},
-            "roofline": roof, "cpu_baseline": cpu, "kernels": kernels,
+            "roofline": roof, "cpu_baseline": cpu, "f32_exact_gemms": f32cmp, "kernels": kernels,
         }
         print(json.dumps(line))
     if world > 1:

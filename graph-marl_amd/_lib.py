@@ -29,8 +29,16 @@ EXPORTS = [
     "gm_netmon_readout_bwd", "gm_lstm_pointwise", "gm_lstm_pointwise_bwd", "gm_linear_f32", "gm_gemm_f32",
     "gm_gemm_set_tile", "gm_simple_create", "gm_simple_destroy", "gm_simple_reset", "gm_simple_step",
     "gm_simple_observe", "gm_simple_policy_egreedy", "gm_simple_get_state", "gm_env_set_topology",
-    "gm_policy_shortest_path", "gm_env_first_hops", "gm_routing_node_encoder",
+    "gm_policy_shortest_path", "gm_env_first_hops", "gm_routing_node_encoder", "gm_gemm_x3",
+    "gm_gemm_pack_x3", "gm_gemm_pack_x3_bytes",
 ]
+
+# Arithmetic form of the fused rollout GEMMs (graph-marl_amd/fused.py): "x3" = split-f16
+# MFMA with fp32 accumulation (default), "f32" = exact fp32 MFMA. GM_GEMM=f32 selects the
+# exact form process-wide.
+GEMM_MODE = os.environ.get("GM_GEMM", "x3")
+if GEMM_MODE not in ("x3", "f32"):
+    raise ValueError(f"GM_GEMM must be 'x3' or 'f32', not {GEMM_MODE!r}")
 
 
 class EnvConfig(C.Structure):
@@ -96,6 +104,9 @@ def lib():
     L.gm_env_set_topology.argtypes = [vp, i32, i64, vp, i32, i32]
     L.gm_policy_shortest_path.argtypes = [vp, vp, vp]
     L.gm_env_first_hops.argtypes = [vp, vp, vp]
+    L.gm_gemm_pack_x3_bytes.argtypes = [i32, i32]
+    L.gm_gemm_pack_x3_bytes.restype = i64
+    L.gm_gemm_pack_x3.argtypes = [vp, i64, i32, i32, vp, vp, vp]
     L.gm_routing_node_encoder.argtypes = [vp, i64, vp, i32, i32, vp, vp, i32, i32, vp, i64, vp]
     _lib = L
     return L

@@ -13,7 +13,18 @@
 // Epilogues: bias (+ leaky_relu), or LSTM gates (weights packed so one 128-wide tile holds
 // i,f,g,o of 32 hidden units): c' = σ(f)c + σ(i)tanh(g), h' = σ(o)tanh(c').
 //
-// Exact fp32 (v_mfma_f32_32x32x2_f32 = fmaf chain per k). All operand loads are
+// Two arithmetic forms of the same kernel:
+//   F32  exact fp32 (v_mfma_f32_32x32x2_f32 = fmaf chain per k), W as given (fp32 rows);
+//   X3   split-f16 (v_mfma_f32_32x32x16_f16, 1/5.3 of the f32 MFMA cycles per k): every
+//        operand is a sum of two f16 pieces, a = a_hi + a_lo (a_hi = f16(a), 22 significant
+//        bits together), and a·w = a_hi·w_hi + a_hi·w_lo + a_lo·w_hi accumulated in fp32
+//        (the dropped a_lo·w_lo term is ~2^-22 |a·w|). W is split once (gm_gemm_pack_x3)
+//        after a power-of-two scale S keeps its pieces normal; A (fp32 in HBM) is split
+//        while its tile is stored to LDS, its low piece scaled by 2^12 (a_lo' = f16((a -
+//        a_hi)·2^12), normal down to |a| ~ 2^-15) and paired with a third weight plane
+//        w_hi·2^-12, so all three products share one accumulator; the epilogue
+//        multiplies by 1/S (exact).
+// All operand loads are
 // unconditional buffer_load_dwordx4 (hardware bounds check returns 0: missing
 // neighbours use an out-of-range offset, rows are clamped), so the load stream has
 // no per-lane branches; the ragged K tail is zeroed in the LDS store of the last tile
@@ -33,6 +44,9 @@ namespace {
 
 typedef float floatx16 __attribute__((ext_vector_type(16)));
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef _Float16 half4 __attribute__((ext_vector_type(4)));
+typedef _Float16 half8 __attribute__((ext_vector_type(8)));
+typedef float floatx4 __attribute__((ext_vector_type(4)));
 
 constexpr int BKMAX = 32;            // largest K tile of any configuration (host-side checks)
 constexpr int OOB = 0x7ff00000;       // byte offset beyond any buffer: load returns 0
@@ -73,6 +87,12 @@ __device__ __forceinline__ float4 f4add(float4 a, float4 b) {
     return make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w);
 }
 __device__ __forceinline__ float sigm(float x) { return 1.0f / (1.0f + expf(-x)); }
+// a = hi + 2^-12 lo with hi = f16(a) (RNE), lo = f16((a - hi) * 2^12): 2 x 8 bytes to LDS
+__device__ __forceinline__ void split4(float4 v, half4& hi, half4& lo) {
+    const floatx4 a = {v.x, v.y, v.z, v.w};
+    hi = __builtin_convertvector(a, half4);
+    lo = __builtin_convertvector((a - __builtin_convertvector(hi, floatx4)) * 4096.0f, half4);
+}
 
 template <int WGM, int WGN, int TM, int TN, int BK_>
 struct Cfg {
@@ -87,14 +107,23 @@ struct Cfg {
     static constexpr int RSTEP = THREADS / (BK / 4);   // rows between a thread's A rows
 };
 
-template <int WGM, int WGN, int TM, int TN, int BK_, int AMODE, int EPI, int OCC>
+// X3 LDS row images. A (same 4*BK + 16 bytes as the F32 row): per 16-deep k block s,
+// bytes [64s, 64s+32) = 16 hi halves, [64s+32, 64s+64) = 16 lo' halves. B (6*BK + 16
+// bytes): per block s, [96s, 96s+96) = 16 hi | 16 lo | 16 hi*2^-12 halves — the packed
+// weights (gm_gemm_pack_x3) have this block layout in HBM, so B tiles are plain copies.
+template <int WGM, int WGN, int TM, int TN, int BK_, int AMODE, int EPI, int OCC, bool X3>
 __global__ __launch_bounds__(WGM* WGN * 64, OCC) void k_gemm(ASrc a0, ASrc a1, const float* __restrict__ w,
                                                             long long ldw, unsigned wbytes, int M, int N, int K,
-                                                            Epi ep) {
+                                                            Epi ep, const float* __restrict__ wscale_inv) {
     using C = Cfg<WGM, WGN, TM, TN, BK_>;
     constexpr int BK = C::BK, LDP = C::LDP, KH = C::KH;
+    constexpr int ROWB = LDP * 4;                        // bytes per A LDS row (both forms)
+    constexpr int ROWBB = X3 ? 6 * BK + 16 : ROWB;       // bytes per B LDS row
+    constexpr int CB = 6 * BK / 16;                      // X3: 16-byte chunks per B tile row
+    constexpr int BQ3 = (C::BN * CB + C::THREADS - 1) / C::THREADS;
+    static_assert(!X3 || BK % 16 == 0, "X3 tiles hold whole 16-deep k blocks");
     __shared__ __attribute__((aligned(16))) float As[2][C::BM * LDP];
-    __shared__ __attribute__((aligned(16))) float Bs[2][C::BN * LDP];
+    __shared__ __attribute__((aligned(16))) float Bs[2][C::BN * ROWBB / 4];
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int wr = wave / WGN, wc = wave % WGN;
@@ -152,16 +181,29 @@ __global__ __launch_bounds__(WGM* WGN * 64, OCC) void k_gemm(ASrc a0, ASrc a1, c
             ro3[q] = src[q][3] >= 0 ? (int)(src[q][3] * a0.ld1) * 4 : OOB;
         }
     }
-    int woff[C::BQ];
+    // F32: element offset of the thread's W rows. X3: chunk q of the thread is chunk
+    // tid + q*THREADS of the tile (row id / CB, 16-byte column id % CB): byte offset of
+    // its packed row + column (ldw = packed row bytes), and its LDS byte offset
+    constexpr int NW = X3 ? BQ3 : C::BQ;
+    int woff[NW], bdst[NW];
 #pragma unroll
-    for (int q = 0; q < C::BQ; q++) woff[q] = (int)(min(n0 + rbase + q * C::RSTEP, N - 1) * ldw);
+    for (int q = 0; q < NW; q++) {
+        if (X3) {
+            const int id = min(tid + q * C::THREADS, C::BN * CB - 1), r = id / CB, c = id - r * CB;
+            woff[q] = (int)(min(n0 + r, N - 1) * ldw) + 16 * c;
+            bdst[q] = r * ROWBB + 16 * c;
+        } else {
+            woff[q] = (int)(min(n0 + rbase + q * C::RSTEP, N - 1) * ldw);
+            bdst[q] = 0;
+        }
+    }
 
     const __amdgpu_buffer_rsrc_t r0a = rsrc(a0.p0, a0.bytes0);
     const __amdgpu_buffer_rsrc_t r0b = rsrc(a0.p1 ? a0.p1 : a0.p0, a0.p1 ? a0.bytes1 : a0.bytes0);
     const __amdgpu_buffer_rsrc_t r1 = rsrc(a1.p0 ? a1.p0 : a0.p0, a1.p0 ? a1.bytes0 : 0u);
     const __amdgpu_buffer_rsrc_t rw = rsrc(w, wbytes);
 
-    float4 ra[C::AQ], rb[C::BQ];
+    float4 ra[C::AQ], rb[NW];
     auto gload = [&](int k0) {
         if (k0 < a0.k) {
             const int kl = k0 + 4 * c4;
@@ -199,8 +241,13 @@ __global__ __launch_bounds__(WGM* WGN * 64, OCC) void k_gemm(ASrc a0, ASrc a1, c
 #pragma unroll
             for (int q = 0; q < C::AQ; q++) ra[q] = bload(r1, (rowoff1[q] + kl) * 4);
         }
+        if (X3) {
 #pragma unroll
-        for (int q = 0; q < C::BQ; q++) rb[q] = bload(rw, (woff[q] + k0 + 4 * c4) * 4);
+            for (int q = 0; q < NW; q++) rb[q] = bload(rw, woff[q] + k0 * 6);
+        } else {
+#pragma unroll
+            for (int q = 0; q < C::BQ; q++) rb[q] = bload(rw, (woff[q] + k0 + 4 * c4) * 4);
+        }
     };
     auto lstore = [&](int buf, int k0) {
         // zero the columns past the end of the current source on its last (ragged) tile
@@ -214,20 +261,43 @@ __global__ __launch_bounds__(WGM* WGN * 64, OCC) void k_gemm(ASrc a0, ASrc a1, c
                 if (kk + 2 >= kend) ra[q].z = 0.f;
                 if (kk + 3 >= kend) ra[q].w = 0.f;
             }
+            if (!X3) {  // packed X3 weights are zero past K
 #pragma unroll
-            for (int q = 0; q < C::BQ; q++) {
-                if (kk + 0 >= K) rb[q].x = 0.f;
-                if (kk + 1 >= K) rb[q].y = 0.f;
-                if (kk + 2 >= K) rb[q].z = 0.f;
-                if (kk + 3 >= K) rb[q].w = 0.f;
+                for (int q = 0; q < C::BQ; q++) {
+                    if (kk + 0 >= K) rb[q].x = 0.f;
+                    if (kk + 1 >= K) rb[q].y = 0.f;
+                    if (kk + 2 >= K) rb[q].z = 0.f;
+                    if (kk + 3 >= K) rb[q].w = 0.f;
+                }
             }
         }
+        if (X3) {
+            char* as = reinterpret_cast<char*>(As[buf]);
+            const int hb = (c4 >> 2) * 64 + (c4 & 3) * 8;  // hi bytes of k = 4*c4 .. 4*c4+3
 #pragma unroll
-        for (int q = 0; q < C::AQ; q++)
-            *reinterpret_cast<float4*>(&As[buf][(rbase + q * C::RSTEP) * LDP + 4 * c4]) = ra[q];
+            for (int q = 0; q < C::AQ; q++) {
+                half4 hi, lo;
+                split4(ra[q], hi, lo);
+                char* row = as + (rbase + q * C::RSTEP) * ROWB + hb;
+                *reinterpret_cast<half4*>(row) = hi;
+                *reinterpret_cast<half4*>(row + 32) = lo;
+            }
+        } else {
 #pragma unroll
-        for (int q = 0; q < C::BQ; q++)
-            *reinterpret_cast<float4*>(&Bs[buf][(rbase + q * C::RSTEP) * LDP + 4 * c4]) = rb[q];
+            for (int q = 0; q < C::AQ; q++)
+                *reinterpret_cast<float4*>(&As[buf][(rbase + q * C::RSTEP) * LDP + 4 * c4]) = ra[q];
+        }
+        if (X3) {
+            char* bsm = reinterpret_cast<char*>(Bs[buf]);
+#pragma unroll
+            for (int q = 0; q < NW; q++)
+                if ((C::BN * CB) % C::THREADS == 0 || tid + q * C::THREADS < C::BN * CB)
+                    *reinterpret_cast<float4*>(bsm + bdst[q]) = rb[q];
+        } else {
+#pragma unroll
+            for (int q = 0; q < C::BQ; q++)
+                *reinterpret_cast<float4*>(&Bs[buf][(rbase + q * C::RSTEP) * LDP + 4 * c4]) = rb[q];
+        }
     };
 
     floatx16 acc[TM][TN];
@@ -248,6 +318,35 @@ __global__ __launch_bounds__(WGM* WGN * 64, OCC) void k_gemm(ASrc a0, ASrc a1, c
         if (kt + 1 < nk) gload((kt + 1) * BK);
         const float* as = As[cur];
         const float* bs = Bs[cur];
+        if (X3) {
+            const char* ac = reinterpret_cast<const char*>(as);
+            const char* bc = reinterpret_cast<const char*>(bs);
+#pragma unroll
+            for (int sb = 0; sb < BK / 16; sb++) {
+                half8 ah[TM], al[TM], bh[TN], bl[TN], bs3[TN];
+#pragma unroll
+                for (int i = 0; i < TM; i++) {
+                    const char* p = ac + (wr * TM * 32 + i * 32 + l32) * ROWB + sb * 64 + 16 * h;
+                    ah[i] = *reinterpret_cast<const half8*>(p);
+                    al[i] = *reinterpret_cast<const half8*>(p + 32);
+                }
+#pragma unroll
+                for (int j = 0; j < TN; j++) {
+                    const char* p = bc + (wc * TN * 32 + j * 32 + l32) * ROWBB + sb * 96 + 16 * h;
+                    bh[j] = *reinterpret_cast<const half8*>(p);
+                    bl[j] = *reinterpret_cast<const half8*>(p + 32);
+                    bs3[j] = *reinterpret_cast<const half8*>(p + 64);
+                }
+#pragma unroll
+                for (int i = 0; i < TM; i++)
+#pragma unroll
+                    for (int j = 0; j < TN; j++) {
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[i], bs3[j], acc[i][j], 0, 0, 0);
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[i], bl[j], acc[i][j], 0, 0, 0);
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[i], bh[j], acc[i][j], 0, 0, 0);
+                    }
+            }
+        } else {
 #pragma unroll
         for (int s4 = 0; s4 < KH / 4; s4++) {
             float4 af[TM], bf[TN];
@@ -268,11 +367,21 @@ __global__ __launch_bounds__(WGM* WGN * 64, OCC) void k_gemm(ASrc a0, ASrc a1, c
                         acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, acc[i][j], 0, 0, 0);
                     }
         }
+        }
         if (kt + 1 < nk) lstore(cur ^ 1, (kt + 1) * BK);
         __syncthreads();
     }
 
     // ---- epilogue: C/D map col = lane & 31, row = (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5) ----
+    if (X3) {  // undo the weight scale (a power of two: exact)
+        const float si = *wscale_inv;
+#pragma unroll
+        for (int i = 0; i < TM; i++)
+#pragma unroll
+            for (int j = 0; j < TN; j++)
+#pragma unroll
+                for (int r = 0; r < 16; r++) acc[i][j][r] *= si;
+    }
     if (EPI == EPI_BIAS) {
 #pragma unroll
         for (int j = 0; j < TN; j++) {
@@ -323,13 +432,13 @@ __global__ __launch_bounds__(WGM* WGN * 64, OCC) void k_gemm(ASrc a0, ASrc a1, c
     }
 }
 
-template <int WGM, int WGN, int TM, int TN, int BK_, int AMODE, int EPI, int OCC = 2>
+template <int WGM, int WGN, int TM, int TN, int BK_, int AMODE, int EPI, int OCC = 2, bool X3 = false>
 int launch(const ASrc& a0, const ASrc& a1, const float* w, long long ldw, unsigned wbytes, int M, int N, int K,
-           const Epi& ep, hipStream_t st) {
+           const Epi& ep, hipStream_t st, const float* wscale_inv = nullptr) {
     using C = Cfg<WGM, WGN, TM, TN, BK_>;
     const int T = ((M + C::BM - 1) / C::BM) * ((N + C::BN - 1) / C::BN);
-    hipLaunchKernelGGL((k_gemm<WGM, WGN, TM, TN, BK_, AMODE, EPI, OCC>), dim3(T), dim3(C::THREADS), 0, st, a0, a1, w,
-                       ldw, wbytes, M, N, K, ep);
+    hipLaunchKernelGGL((k_gemm<WGM, WGN, TM, TN, BK_, AMODE, EPI, OCC, X3>), dim3(T), dim3(C::THREADS), 0, st, a0, a1,
+                       w, ldw, wbytes, M, N, K, ep, wscale_inv);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return gm_fail(GM_ERR_HIP, std::string("gm_gemm launch: ") + hipGetErrorString(e));
     return GM_OK;
@@ -385,62 +494,58 @@ int to_asrc(const gm_a_src* s, int M, ASrc& o) {
     return GM_OK;
 }
 
-}  // namespace
-
-extern "C" int gm_gemm_f32(const gm_a_src* a0, const gm_a_src* a1, const float* w, int64_t ldw, const float* b,
-                           int32_t m, int32_t n, int32_t epilogue, float* y, int64_t ldy, float* y2, int64_t ldy2,
-                           const float* c_in, int64_t ldc, float* act_out, void* stream) {
-    if (!a0 || !w || !y || m <= 0 || n <= 0 || (ldw & 3) || (reinterpret_cast<uintptr_t>(w) & 15))
-        return gm_fail(GM_ERR_INVALID_ARG, "gm_gemm_f32: bad arguments");
-    ASrc s0, s1;
-    int rc = to_asrc(a0, m, s0);
-    if (rc) return rc;
-    rc = to_asrc(a1, m, s1);
-    if (rc) return rc;
-    if (a1 && (a1->mode != GM_A_DENSE || (s0.k % BKMAX)))
-        return gm_fail(GM_ERR_INVALID_ARG, "gm_gemm_f32: second A source must be dense and the first k % 32 == 0");
-    const int K = s0.k + (a1 ? s1.k : 0);
-    if (ldw < K) return gm_fail(GM_ERR_INVALID_ARG, "gm_gemm_f32: ldw < K");
-    long long wb = ((long long)(n - 1) * ldw + ((K + 3) & ~3)) * 4;
-    if (!fits(wb)) return gm_fail(GM_ERR_UNSUPPORTED, "gm_gemm_f32: weights larger than 2 GB");
-    Epi ep;
-    memset(&ep, 0, sizeof(ep));
-    ep.bias = b;
-    ep.y = y;
-    ep.ldy = ldy;
-    ep.y2 = y2;
-    ep.ldy2 = ldy2;
-    ep.c_in = c_in;
-    ep.ldc = ldc;
-    ep.act_out = act_out;
-    hipStream_t st = (hipStream_t)stream;
+// Tile tables. F32: per-shape default from tools/gemm_bench.py on MI355X (BK=16 for short
+// K, narrow N and the readout layer; BK=32 for K=512, N>=256). X3: 128x128x16 tiles
+// (49 KB of LDS: 3 blocks/CU), LSTM 128 rows x 4 gate tiles.
+template <bool X3>
+int dispatch(const ASrc& s0, const ASrc& s1, const float* w, long long ldw, unsigned wb, int m, int n, int K,
+             int epilogue, Epi& ep, hipStream_t st, const float* wsi) {
     const int tile = g_tile;
 #define GM_L(WGM, WGN, TM, TN, BK_, AM, EP) \
-    launch<WGM, WGN, TM, TN, BK_, AM, EP>(s0, s1, w, ldw, (unsigned)wb, m, n, K, ep, st)
+    launch<WGM, WGN, TM, TN, BK_, AM, EP, 2, X3>(s0, s1, w, ldw, wb, m, n, K, ep, st, wsi)
 #define GM_L4(WGM, WGN, TM, TN, BK_, AM, EP) \
-    launch<WGM, WGN, TM, TN, BK_, AM, EP, 4>(s0, s1, w, ldw, (unsigned)wb, m, n, K, ep, st)
+    launch<WGM, WGN, TM, TN, BK_, AM, EP, 4, X3>(s0, s1, w, ldw, wb, m, n, K, ep, st, wsi)
     if (epilogue == GM_EPI_LSTM) {
-        if (n % 128 || !y2 || !c_in) return gm_fail(GM_ERR_INVALID_ARG, "gm_gemm_f32: LSTM epilogue needs 4H % 128 == 0");
         ep.hidden = n / 4;
-        // default: 128x128x16 at 4 blocks/CU (<= 128 VGPRs, 40 KB LDS): +20 % over 2 blocks/CU
-        if (s0.mode == GM_A_DENSE) {
-            if (tile == 0) return GM_L(4, 1, 1, 4, 32, GM_A_DENSE, EPI_LSTM);
-            if (tile == 2) return GM_L(4, 1, 2, 4, 16, GM_A_DENSE, EPI_LSTM);
-            return GM_L4(4, 1, 1, 4, 16, GM_A_DENSE, EPI_LSTM);
+        if constexpr (X3) {
+            if (s0.mode == GM_A_DENSE) {
+                if (tile == 1) return GM_L(4, 1, 1, 4, 32, GM_A_DENSE, EPI_LSTM);
+                if (tile == 2) return GM_L(4, 1, 2, 4, 16, GM_A_DENSE, EPI_LSTM);
+                return GM_L(4, 1, 1, 4, 16, GM_A_DENSE, EPI_LSTM);
+            }
+            if (s0.mode == GM_A_AGGREGATE) {
+                if (tile == 1) return GM_L(4, 1, 1, 4, 32, GM_A_AGGREGATE, EPI_LSTM);
+                if (tile == 2) return GM_L(4, 1, 2, 4, 16, GM_A_AGGREGATE, EPI_LSTM);
+                return GM_L(4, 1, 1, 4, 16, GM_A_AGGREGATE, EPI_LSTM);
+            }
+        } else {
+            // default: 128x128x16 at 4 blocks/CU (<= 128 VGPRs, 40 KB LDS): +20 % over 2 blocks/CU
+            if (s0.mode == GM_A_DENSE) {
+                if (tile == 0) return GM_L(4, 1, 1, 4, 32, GM_A_DENSE, EPI_LSTM);
+                if (tile == 2) return GM_L(4, 1, 2, 4, 16, GM_A_DENSE, EPI_LSTM);
+                return GM_L4(4, 1, 1, 4, 16, GM_A_DENSE, EPI_LSTM);
+            }
+            if (s0.mode == GM_A_AGGREGATE) {
+                if (tile == 0) return GM_L(4, 1, 1, 4, 32, GM_A_AGGREGATE, EPI_LSTM);
+                if (tile == 2) return GM_L(4, 1, 2, 4, 16, GM_A_AGGREGATE, EPI_LSTM);
+                return GM_L4(4, 1, 1, 4, 16, GM_A_AGGREGATE, EPI_LSTM);
+            }
         }
-        if (s0.mode == GM_A_AGGREGATE) {
-            if (tile == 0) return GM_L(4, 1, 1, 4, 32, GM_A_AGGREGATE, EPI_LSTM);
-            if (tile == 2) return GM_L(4, 1, 2, 4, 16, GM_A_AGGREGATE, EPI_LSTM);
-            return GM_L4(4, 1, 1, 4, 16, GM_A_AGGREGATE, EPI_LSTM);
-        }
-        return gm_fail(GM_ERR_UNSUPPORTED, "gm_gemm_f32: LSTM epilogue with readout source");
+        return gm_fail(GM_ERR_UNSUPPORTED, "gm_gemm: LSTM epilogue with readout source");
     }
-    if (epilogue != GM_EPI_BIAS && epilogue != GM_EPI_BIAS_LEAKY)
-        return gm_fail(GM_ERR_INVALID_ARG, "gm_gemm_f32: unknown epilogue");
-    if (ldy < n) return gm_fail(GM_ERR_INVALID_ARG, "gm_gemm_f32: ldy < n");
     ep.act = epilogue == GM_EPI_BIAS_LEAKY ? 1 : 0;
-    // per-shape default (tools/gemm_bench.py on MI355X): BK=16 wins for short K (enc.l0),
-    // narrow N (enc.l2) and the K=642 readout layer; BK=32 for K=512, N>=256
+    if constexpr (X3) {
+        if (s0.mode == GM_A_READOUT) {
+            if (tile == 1) return GM_L(2, 2, 2, 4, 16, GM_A_READOUT, EPI_BIAS);
+            if (tile == 2) return GM_L(2, 2, 2, 2, 32, GM_A_READOUT, EPI_BIAS);
+            return GM_L(2, 2, 2, 2, 16, GM_A_READOUT, EPI_BIAS);
+        }
+        if (s0.mode == GM_A_AGGREGATE) return GM_L(2, 2, 2, 2, 16, GM_A_AGGREGATE, EPI_BIAS);
+        if (n <= 32) return GM_L(4, 1, 1, 1, 16, GM_A_DENSE, EPI_BIAS);
+        if (tile == 1) return GM_L(2, 2, 2, 4, 16, GM_A_DENSE, EPI_BIAS);
+        if (tile == 2) return GM_L(2, 2, 2, 2, 32, GM_A_DENSE, EPI_BIAS);
+        return GM_L(2, 2, 2, 2, 16, GM_A_DENSE, EPI_BIAS);
+    } else {
     const int t = tile >= 0 ? tile : ((s0.mode == GM_A_READOUT || K <= 128 || n <= 128) ? 3 : 0);
     if (s0.mode == GM_A_READOUT) {
         if (t == 1) return GM_L(2, 2, 2, 4, 16, GM_A_READOUT, EPI_BIAS);
@@ -456,8 +561,135 @@ extern "C" int gm_gemm_f32(const gm_a_src* a0, const gm_a_src* a1, const float* 
     if (t == 3) return GM_L(2, 2, 2, 2, 16, GM_A_DENSE, EPI_BIAS);
     if (t == 4) return GM_L4(2, 2, 2, 2, 16, GM_A_DENSE, EPI_BIAS);
     return GM_L(2, 2, 2, 2, 32, GM_A_DENSE, EPI_BIAS);
+    }
 #undef GM_L
 #undef GM_L4
+}
+
+// shared argument checks of gm_gemm_f32 / gm_gemm_x3; x3: w = packed weights
+int gemm_entry(bool x3, const gm_a_src* a0, const gm_a_src* a1, const void* w, int64_t ldw, const float* wsi,
+               const float* b, int32_t m, int32_t n, int32_t epilogue, float* y, int64_t ldy, float* y2,
+               int64_t ldy2, const float* c_in, int64_t ldc, float* act_out, void* stream) {
+    const char* fn = x3 ? "gm_gemm_x3" : "gm_gemm_f32";
+    if (!a0 || !w || !y || m <= 0 || n <= 0 || (reinterpret_cast<uintptr_t>(w) & 15) || (!x3 && (ldw & 3)) ||
+        (x3 && !wsi))
+        return gm_fail(GM_ERR_INVALID_ARG, std::string(fn) + ": bad arguments");
+    ASrc s0, s1;
+    int rc = to_asrc(a0, m, s0);
+    if (rc) return rc;
+    rc = to_asrc(a1, m, s1);
+    if (rc) return rc;
+    if (a1 && (a1->mode != GM_A_DENSE || (s0.k % BKMAX)))
+        return gm_fail(GM_ERR_INVALID_ARG, std::string(fn) + ": second A source must be dense and the first k % 32 == 0");
+    const int K = s0.k + (a1 ? s1.k : 0);
+    long long wb;
+    if (x3) {
+        ldw = (long long)((K + BKMAX - 1) / BKMAX * BKMAX) / 16 * 96;  // packed row bytes
+        wb = (long long)n * ldw;
+    } else {
+        if (ldw < K) return gm_fail(GM_ERR_INVALID_ARG, "gm_gemm_f32: ldw < K");
+        wb = ((long long)(n - 1) * ldw + ((K + 3) & ~3)) * 4;
+    }
+    if (!fits(wb)) return gm_fail(GM_ERR_UNSUPPORTED, std::string(fn) + ": weights larger than 2 GB");
+    Epi ep;
+    memset(&ep, 0, sizeof(ep));
+    ep.bias = b;
+    ep.y = y;
+    ep.ldy = ldy;
+    ep.y2 = y2;
+    ep.ldy2 = ldy2;
+    ep.c_in = c_in;
+    ep.ldc = ldc;
+    ep.act_out = act_out;
+    if (epilogue == GM_EPI_LSTM) {
+        if (n % 128 || !y2 || !c_in) return gm_fail(GM_ERR_INVALID_ARG, std::string(fn) + ": LSTM epilogue needs 4H % 128 == 0");
+    } else if (epilogue != GM_EPI_BIAS && epilogue != GM_EPI_BIAS_LEAKY) {
+        return gm_fail(GM_ERR_INVALID_ARG, std::string(fn) + ": unknown epilogue");
+    } else if (ldy < n) {
+        return gm_fail(GM_ERR_INVALID_ARG, std::string(fn) + ": ldy < n");
+    }
+    const float* wf = static_cast<const float*>(w);
+    hipStream_t st = (hipStream_t)stream;
+    return x3 ? dispatch<true>(s0, s1, wf, ldw, (unsigned)wb, m, n, K, epilogue, ep, st, wsi)
+              : dispatch<false>(s0, s1, wf, ldw, (unsigned)wb, m, n, K, epilogue, ep, st, nullptr);
+}
+
+// ---- weight split for X3: S = 2^(15 - e) with max|w| = f * 2^e (f in [0.5, 1)), so
+// S*max|w| in [2^14, 2^15) (< f16 max 65504) and both pieces of every weight stay normal
+// down to ~2^-24 of the largest ----
+__global__ void k_absmax(const float* __restrict__ w, long long ldw, int n, int k, float* __restrict__ wsi) {
+    __shared__ float red[16];
+    float m = 0.f;
+    const long long tot = (long long)n * k;
+    for (long long i = threadIdx.x; i < tot; i += blockDim.x) {
+        const long long r = i / k, c = i - r * k;
+        m = fmaxf(m, fabsf(w[r * ldw + c]));
+    }
+    for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int i = 1; i < (int)(blockDim.x >> 6); i++) m = fmaxf(m, red[i]);
+        m = fmaxf(m, red[0]);
+        int e = 0;
+        if (m > 0.f && isfinite(m)) frexpf(m, &e);
+        e = max(-100, min(100, e));
+        wsi[0] = ldexpf(1.0f, e - 15);  // 1/S
+    }
+}
+
+// one thread per (row, 16-deep k block, element): packed[row][blk] = hi[16] | lo[16] | hi*2^-12 [16]
+__global__ void k_split_w(const float* __restrict__ w, long long ldw, int n, int k, int nblk,
+                          _Float16* __restrict__ wp, const float* __restrict__ wsi) {
+    const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= (long long)n * nblk * 16) return;
+    const int e = (int)(i & 15);
+    const long long rb = i >> 4;
+    const int r = (int)(rb / nblk), blk = (int)(rb - (long long)r * nblk);
+    const int c = blk * 16 + e;
+    const float S = 1.0f / wsi[0];
+    const float v = c < k ? w[(long long)r * ldw + c] * S : 0.f;
+    const _Float16 hi = (_Float16)v;
+    const _Float16 lo = (_Float16)(v - (float)hi);
+    _Float16* o = wp + rb * 48;
+    o[e] = hi;
+    o[16 + e] = lo;
+    o[32 + e] = (_Float16)((float)hi * (1.0f / 4096.0f));
+}
+
+}  // namespace
+
+extern "C" int gm_gemm_f32(const gm_a_src* a0, const gm_a_src* a1, const float* w, int64_t ldw, const float* b,
+                           int32_t m, int32_t n, int32_t epilogue, float* y, int64_t ldy, float* y2, int64_t ldy2,
+                           const float* c_in, int64_t ldc, float* act_out, void* stream) {
+    return gemm_entry(false, a0, a1, w, ldw, nullptr, b, m, n, epilogue, y, ldy, y2, ldy2, c_in, ldc, act_out, stream);
+}
+
+extern "C" int gm_gemm_x3(const gm_a_src* a0, const gm_a_src* a1, const void* wp, const float* wscale_inv,
+                          const float* b, int32_t m, int32_t n, int32_t epilogue, float* y, int64_t ldy, float* y2,
+                          int64_t ldy2, const float* c_in, int64_t ldc, float* act_out, void* stream) {
+    return gemm_entry(true, a0, a1, wp, 0, wscale_inv, b, m, n, epilogue, y, ldy, y2, ldy2, c_in, ldc, act_out,
+                      stream);
+}
+
+extern "C" int64_t gm_gemm_pack_x3_bytes(int32_t n, int32_t k) {
+    if (n <= 0 || k <= 0) return 0;
+    return (int64_t)n * ((k + BKMAX - 1) / BKMAX * BKMAX / 16) * 96;
+}
+
+extern "C" int gm_gemm_pack_x3(const float* w, int64_t ldw, int32_t n, int32_t k, void* wp, float* wscale_inv,
+                               void* stream) {
+    if (!w || !wp || !wscale_inv || n <= 0 || k <= 0 || ldw < k || (reinterpret_cast<uintptr_t>(wp) & 15))
+        return gm_fail(GM_ERR_INVALID_ARG, "gm_gemm_pack_x3: bad arguments");
+    hipStream_t st = (hipStream_t)stream;
+    const int nblk = (k + BKMAX - 1) / BKMAX * BKMAX / 16;
+    hipLaunchKernelGGL(k_absmax, dim3(1), dim3(1024), 0, st, w, (long long)ldw, n, k, wscale_inv);
+    const long long tot = (long long)n * nblk * 16;
+    hipLaunchKernelGGL(k_split_w, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, st, w, (long long)ldw, n, k, nblk,
+                       static_cast<_Float16*>(wp), wscale_inv);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return gm_fail(GM_ERR_HIP, std::string("gm_gemm_pack_x3: ") + hipGetErrorString(e));
+    return GM_OK;
 }
 
 extern "C" int gm_gemm_set_tile(int32_t tile) {

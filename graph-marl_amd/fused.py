@@ -10,7 +10,8 @@ last update (readout's neighbour features, src/model.py:510-519).
 DQN Q (src/model.py:187-203) on the joint observation without materialising it:
   h1 = leaky(W1 @ [readout(h_final, h_prev, nbr, agent_node) | env_obs] + b1)
 so the NetMon readout + agent gather (src/model.py:582-631) happen in the GEMM's A load.
-Weights are packed once per parameter version (LSTM gate interleave, W1 column order).
+Weights are packed once per parameter version (LSTM gate interleave, W1 column order,
+and for the split-f16 form (L.GEMM_MODE == "x3", gm_gemm_x3) the hi/lo f16 split).
 """
 import ctypes as C
 
@@ -37,8 +38,29 @@ def _setup():
         vp = C.c_void_p
         lib.gm_gemm_f32.argtypes = [C.POINTER(ASrc), C.POINTER(ASrc), vp, C.c_int64, vp, C.c_int32, C.c_int32,
                                     C.c_int32, vp, C.c_int64, vp, C.c_int64, vp, C.c_int64, vp, vp]
+        lib.gm_gemm_x3.argtypes = [C.POINTER(ASrc), C.POINTER(ASrc), vp, vp, vp, C.c_int32, C.c_int32,
+                                   C.c_int32, vp, C.c_int64, vp, C.c_int64, vp, C.c_int64, vp, vp]
         lib._gemm_ready = True
     return lib
+
+
+class X3:
+    """Weights split for gm_gemm_x3: packed hi/lo f16 blocks + the device scalar 1/S."""
+    __slots__ = ("wp", "sinv", "n", "k")
+
+    def __init__(self, w, ldw, n, k):
+        lib = _setup()
+        nb = lib.gm_gemm_pack_x3_bytes(n, k)
+        self.wp = torch.empty(nb, dtype=torch.uint8, device=w.device)
+        self.sinv = torch.empty(1, dtype=torch.float32, device=w.device)
+        self.n, self.k = n, k
+        L.check(lib.gm_gemm_pack_x3(w.data_ptr(), ldw, n, k, self.wp.data_ptr(), self.sinv.data_ptr(),
+                                    L.stream_ptr()))
+
+
+def use_x3(n):
+    """The split-f16 form runs every GEMM wider than the 32-column tail (the Q head stays f32)."""
+    return L.GEMM_MODE == "x3" and n > 32
 
 
 def dense(p, ld, k):
@@ -62,11 +84,18 @@ def readout(h_final, ld_f, h_prev, ld_p, nbr, agent_node, n_nodes, hidden):
     return s
 
 
-def gemm(a0, a1, w, ldw, b, m, n, epi, y, ldy, y2=None, ldy2=0, c_in=None, ldc=0, act_out=None, tag=None):
+def gemm(a0, a1, w, ldw, b, m, n, epi, y, ldy, y2=None, ldy2=0, c_in=None, ldc=0, act_out=None, tag=None, x3=None):
+    """y = epi(A @ W^T + b); with x3 (an X3 of the same W) the split-f16 form runs."""
     lib = _setup()
+    a1p = None if a1 is None else C.byref(a1)
     with L.timed(tag):
-        L.check(lib.gm_gemm_f32(C.byref(a0), None if a1 is None else C.byref(a1), w, ldw, b, m, n, epi, y, ldy,
-                                y2, ldy2, c_in, ldc, act_out, L.stream_ptr()))
+        if x3 is not None:
+            assert x3.n == n and x3.k == a0.k + (0 if a1 is None else a1.k), "packed weights do not match the GEMM"
+            L.check(lib.gm_gemm_x3(C.byref(a0), a1p, x3.wp.data_ptr(), x3.sinv.data_ptr(), b, m, n, epi, y, ldy,
+                                   y2, ldy2, c_in, ldc, act_out, L.stream_ptr()))
+        else:
+            L.check(lib.gm_gemm_f32(C.byref(a0), a1p, w, ldw, b, m, n, epi, y, ldy, y2, ldy2, c_in, ldc, act_out,
+                                    L.stream_ptr()))
 
 
 def _key(*ts):
@@ -110,9 +139,10 @@ def pack_lstm(cell):
             u = torch.arange(32, device=w.device)
             orig = (g[None, :, None] * H + 32 * t[:, None, None] + u[None, None, :]).reshape(-1)
             wp, ldw = _pad_cols(w[orig])
-            return wp, ldw, b[orig].contiguous()
+            x3 = X3(wp, ldw, 4 * H, 2 * H) if use_x3(4 * H) else None
+            return wp, ldw, b[orig].contiguous(), x3
 
-    return cell._packed.get(_key(cell.weight_ih, cell.weight_hh, cell.bias_ih, cell.bias_hh), build)
+    return cell._packed.get(_key(cell.weight_ih, cell.weight_hh, cell.bias_ih, cell.bias_hh) + (L.GEMM_MODE,), build)
 
 
 def pack_dqn_first(lin, obs_dim):
@@ -124,9 +154,21 @@ def pack_dqn_first(lin, obs_dim):
         with torch.no_grad():
             w = torch.cat([lin.weight[:, obs_dim:], lin.weight[:, :obs_dim]], 1)
             wp, ldw = _pad_cols(w)
-            return wp, ldw, lin.bias.contiguous()
+            n = lin.out_features
+            x3 = X3(wp, ldw, n, lin.in_features) if use_x3(n) else None
+            return wp, ldw, lin.bias.contiguous(), x3
 
-    return lin._packed_first.get(_key(lin.weight, lin.bias) + (obs_dim,), build)
+    return lin._packed_first.get(_key(lin.weight, lin.bias) + (obs_dim, L.GEMM_MODE), build)
+
+
+def pack_x3(lin):
+    """Split-f16 weights of a Linear (None when the f32 form runs it)."""
+    if not use_x3(lin.out_features):
+        return None
+    if not hasattr(lin, "_packed_x3"):
+        lin._packed_x3 = Packed()
+    return lin._packed_x3.get(_key(lin.weight), lambda: X3(lin.weight, lin.weight.stride(0), lin.out_features,
+                                                           lin.in_features))
 
 
 def _linear(x, ldx, k, lin, out):
@@ -134,7 +176,7 @@ def _linear(x, ldx, k, lin, out):
     a = dense(x.data_ptr(), ldx, k)
     gemm(a, None, wp.data_ptr(), ldw, lin.bias.data_ptr(), x.shape[0], lin.out_features,
          GM_EPI_BIAS_LEAKY if lin.act == 1 else GM_EPI_BIAS, out.data_ptr(), out.stride(0),
-         tag=lin.tag and f"linear:{lin.tag}:{x.shape[0]}x{lin.out_features}x{k}")
+         tag=lin.tag and f"linear:{lin.tag}:{x.shape[0]}x{lin.out_features}x{k}", x3=pack_x3(lin))
     return out
 
 
@@ -178,12 +220,12 @@ def netmon_step(netmon, node_obs, nbr, state):
     if state is None:
         state = torch.zeros(B, N, 2 * H, device=dev)
     st = state.reshape(M, 2 * H)
-    wp, ldw, bp = pack_lstm(netmon.rnn_obs)
+    wp, ldw, bp, x3 = pack_lstm(netmon.rnn_obs)
     S = torch.empty(M, 2 * H, device=dev)
     gemm(dense(x.data_ptr(), x.stride(0), H), dense(st.data_ptr(), 2 * H, H), wp.data_ptr(), ldw, bp.data_ptr(),
          M, 4 * H, GM_EPI_LSTM, S.data_ptr(), 2 * H, S[:, H:].data_ptr(), 2 * H, st[:, H:].data_ptr(), 2 * H,
-         tag=netmon.rnn_obs.tag and f"lstm:{netmon.rnn_obs.tag}:{M}x{4 * H}x{2 * H}")
-    wu, ldu, bu = pack_lstm(netmon.rnn_update)
+         tag=netmon.rnn_obs.tag and f"lstm:{netmon.rnn_obs.tag}:{M}x{4 * H}x{2 * H}", x3=x3)
+    wu, ldu, bu, xu = pack_lstm(netmon.rnn_update)
     last = S
     mean = netmon.agg_mode == 1
     for it in range(netmon.iterations):
@@ -192,7 +234,7 @@ def netmon_step(netmon, node_obs, nbr, state):
         gemm(aggregate(S.data_ptr(), 2 * H, H, nbr, N, mean), dense(S.data_ptr(), 2 * H, H), wu.data_ptr(), ldu,
              bu.data_ptr(), M, 4 * H, GM_EPI_LSTM, S2.data_ptr(), 2 * H, S2[:, H:].data_ptr(), 2 * H,
              S[:, H:].data_ptr(), 2 * H,
-             tag=netmon.rnn_update.tag and f"lstm_agg:{netmon.rnn_update.tag}:{M}x{4 * H}x{2 * H}")
+             tag=netmon.rnn_update.tag and f"lstm_agg:{netmon.rnn_update.tag}:{M}x{4 * H}x{2 * H}", x3=xu)
         S = S2
     if netmon.iterations <= 0:
         last = torch.zeros_like(S)
@@ -209,12 +251,12 @@ def dqn_q(dqn, env_obs, obs_dim, state, h_prev, nbr, agent_node, scratch):
     H = state.shape[-1] // 2
     M = B * A
     lin0 = dqn.encoder.linear_layers[0]
-    wp, ldw, b = pack_dqn_first(lin0, obs_dim)
+    wp, ldw, b, x3 = pack_dqn_first(lin0, obs_dim)
     h1 = scratch(0, M, lin0.out_features)
     a0 = readout(state.data_ptr(), 2 * H, h_prev.data_ptr(), h_prev.stride(0), nbr, agent_node, N, H)
     gemm(a0, dense(env_obs.data_ptr(), stride, obs_dim), wp.data_ptr(), ldw, b.data_ptr(), M, lin0.out_features,
          GM_EPI_BIAS_LEAKY if lin0.act == 1 else GM_EPI_BIAS, h1.data_ptr(), h1.stride(0),
-         tag=lin0.tag and f"linear:{lin0.tag}:{M}x{lin0.out_features}x{a0.k + obs_dim}")
+         tag=lin0.tag and f"linear:{lin0.tag}:{M}x{lin0.out_features}x{a0.k + obs_dim}", x3=x3)
     h = h1
     for i, lin in enumerate(list(dqn.encoder.linear_layers[1:]) + [dqn.q_net.fc]):
         h = _linear(h, h.stride(0), h.shape[1], lin, scratch(i + 1, M, lin.out_features))

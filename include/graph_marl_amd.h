@@ -21,6 +21,7 @@
  *   gm_lstm_pointwise(_bwd)          nn.LSTMCell gate math / LayerNorm-free part    src/model.py:379-382, 491, 543
  *   gm_linear_f32                    nn.Linear (+ leaky_relu of MLP)        src/model.py:13-42, 119-125
  *   gm_gemm_f32                      Linear / LSTMCell GEMMs with aggregate, readout and gate math fused
+ *   gm_gemm_x3 / gm_gemm_pack_x3     the same GEMMs in split-f16 form (f16 MFMA, fp32 accumulate)
  */
 #ifndef GRAPH_MARL_AMD_H
 #define GRAPH_MARL_AMD_H
@@ -218,6 +219,23 @@ typedef struct {
 int gm_gemm_f32(const gm_a_src* src0, const gm_a_src* src1, const float* w, int64_t ldw, const float* b, int32_t m,
                 int32_t n, int32_t epilogue, float* y, int64_t ldy, float* y2, int64_t ldy2, const float* c_in,
                 int64_t ldc, float* act_out, void* stream);
+/* Same GEMM in split-f16 form (the rollout's default): every operand a = a_hi + a_lo with
+ * f16 pieces (22 significant bits), a·w = a_hi·w_hi + a_hi·w_lo + a_lo·w_hi on
+ * v_mfma_f32_32x32x16_f16 with fp32 accumulation — 5.3x fewer MFMA cycles than the f32
+ * form; error vs fp64 the order of an fp32 GEMM's (tests/test_fused_gpu.py). A stays fp32
+ * in HBM (split while staged to LDS); wp = weights packed by gm_gemm_pack_x3 for the same
+ * (n, K = src0->k + src1->k), wscale_inv its device scalar. Arguments otherwise as
+ * gm_gemm_f32. |A| must stay below the f16 range (65504). */
+int gm_gemm_x3(const gm_a_src* src0, const gm_a_src* src1, const void* wp, const float* wscale_inv, const float* b,
+               int32_t m, int32_t n, int32_t epilogue, float* y, int64_t ldy, float* y2, int64_t ldy2,
+               const float* c_in, int64_t ldc, float* act_out, void* stream);
+/* Packed size in bytes of an [n][k] weight for gm_gemm_x3: n * ceil(k/32)*2 blocks * 96 B. */
+int64_t gm_gemm_pack_x3_bytes(int32_t n, int32_t k);
+/* Split W [n][ldw] (first k columns) into wp (16-byte aligned, gm_gemm_pack_x3_bytes):
+ * per row and 16-deep k block, 16 f16 hi, 16 f16 lo, 16 f16 hi*2^-12 of S*W, zero past k, with S = a
+ * power of two that puts S*max|W| in [2^14, 2^15); writes 1/S to *wscale_inv (device).
+ * Stream-ordered, no host sync. */
+int gm_gemm_pack_x3(const float* w, int64_t ldw, int32_t n, int32_t k, void* wp, float* wscale_inv, void* stream);
 /* First NetMon encoder layer on routing node observations (src/model.py:272-276 applied
  * to src/env/routing.py:187-235): y = act(W x + b) from the 12 nonzero entries of each node
  * row (own one-hot, packet count and load, per neighbour one-hot, edge length, edge load)
@@ -229,7 +247,8 @@ int gm_routing_node_encoder(const float* x, int64_t ldx, const int32_t* nbr, int
                             void* stream);
 /* Tuning knob: tile configuration of gm_gemm_f32 (-1 = per-shape default; 0 = 128x128x32;
  * 1 = 128x256x16; 2 = 256x128x16 (LSTM: 256x128x16); 3 = 128x128x16; 4 = 128x128x16 at 4
- * blocks/CU). Process-wide. */
+ * blocks/CU); of gm_gemm_x3 (-1/0 = 128x128x16; 1 = 128x256x16 (LSTM: 128x128x32);
+ * 2 = 128x128x32 (LSTM: 256x128x16)). Process-wide. */
 int gm_gemm_set_tile(int32_t tile);
 
 /* ---------------------------------------------------------------------------

@@ -19,9 +19,11 @@ def mods():
 
 
 @pytest.mark.parametrize("m,n,k,ldx", [(81920, 512, 642, 644), (1000, 256, 512, 512), (777, 130, 90, 92),
-                                       (5, 3, 7, 8), (4097, 33, 129, 132), (64, 4, 256, 256)])
+                                       (5, 3, 7, 8), (4097, 33, 129, 132), (64, 4, 256, 256), (300, 64, 16, 16)])
 @pytest.mark.parametrize("epi", [0, 1])
-def test_gemm_dense_vs_torch(m, n, k, ldx, epi):
+@pytest.mark.parametrize("form", ["f32", "x3"])
+def test_gemm_dense_vs_torch(m, n, k, ldx, epi, form):
+    """Both arithmetic forms within the rollout tolerance (1e-5, scaled for K > 64) of fp64."""
     gm, M, FU, W = mods()
     torch.manual_seed(m + n + k)
     buf = torch.randn(m, ldx, device="cuda")
@@ -29,26 +31,54 @@ def test_gemm_dense_vs_torch(m, n, k, ldx, epi):
     w = torch.randn(n, k, device="cuda") / k ** 0.5
     b = torch.randn(n, device="cuda")
     wp, ldw = FU._pad_cols(w)
+    x3 = FU.X3(wp, ldw, n, k) if form == "x3" else None
     y = torch.empty(m, n, device="cuda")
-    FU.gemm(FU.dense(buf.data_ptr(), ldx, k), None, wp.data_ptr(), ldw, b.data_ptr(), m, n, epi, y.data_ptr(), n)
+    FU.gemm(FU.dense(buf.data_ptr(), ldx, k), None, wp.data_ptr(), ldw, b.data_ptr(), m, n, epi, y.data_ptr(), n,
+            x3=x3)
     ref = F.linear(x.double(), w.double(), b.double())
     if epi == 1:
         ref = F.leaky_relu(ref)
     assert (y.double() - ref).abs().max().item() < 1e-5 * max(1.0, k ** 0.5 / 8)
 
 
-def test_gemm_two_sources_and_lstm_epilogue():
+def test_gemm_x3_error_is_fp32_order():
+    """Split-f16 error vs fp64 stays within a small factor of the exact-fp32 GEMM's own
+    error, on activations spanning 2^-9..2^3 (rows of very different scale) and weights
+    spanning 2^-12..2^0 — i.e. x3 is an fp32-accuracy GEMM, not a reduced-precision one."""
     gm, M, FU, W = mods()
+    torch.manual_seed(7)
+    m, n, k = 8192, 256, 512
+    x = torch.randn(m, k, device="cuda") * torch.exp2(torch.randint(-9, 4, (m, 1), device="cuda").float())
+    w = torch.randn(n, k, device="cuda") * torch.exp2(torch.randint(-12, 1, (n, 1), device="cuda").float())
+    b = torch.zeros(n, device="cuda")
+    wp, ldw = FU._pad_cols(w)
+    ref = F.linear(x.double(), w.double())
+    mag = F.linear(x.abs().double(), w.abs().double())  # sum |a*w| per output
+    errs = {}
+    for form in ("f32", "x3"):
+        y = torch.empty(m, n, device="cuda")
+        FU.gemm(FU.dense(x.data_ptr(), k, k), None, wp.data_ptr(), ldw, b.data_ptr(), m, n, 0, y.data_ptr(), n,
+                x3=FU.X3(wp, ldw, n, k) if form == "x3" else None)
+        errs[form] = ((y.double() - ref).abs() / mag.clamp_min(1e-30)).max().item()
+    assert errs["f32"] < 1e-6
+    assert errs["x3"] < 4e-6, errs
+
+
+@pytest.mark.parametrize("form", ["f32", "x3"])
+def test_gemm_two_sources_and_lstm_epilogue(form, monkeypatch):
+    gm, M, FU, W = mods()
+    monkeypatch.setattr(FU.L, "GEMM_MODE", form)
     torch.manual_seed(0)
     Mr, H = 5000, 128
     cell = M.LSTMCell(H, H).cuda()
     x = torch.randn(Mr, H, device="cuda")
     st = torch.randn(Mr, 2 * H, device="cuda")
     h, c = st[:, :H], st[:, H:]
-    wp, ldw, bp = FU.pack_lstm(cell)
+    wp, ldw, bp, x3 = FU.pack_lstm(cell)
+    assert (x3 is not None) == (form == "x3")
     S = torch.empty(Mr, 2 * H, device="cuda")
     FU.gemm(FU.dense(x.data_ptr(), H, H), FU.dense(st.data_ptr(), 2 * H, H), wp.data_ptr(), ldw, bp.data_ptr(), Mr,
-            4 * H, FU.GM_EPI_LSTM, S.data_ptr(), 2 * H, S[:, H:].data_ptr(), 2 * H, c.data_ptr(), 2 * H)
+            4 * H, FU.GM_EPI_LSTM, S.data_ptr(), 2 * H, S[:, H:].data_ptr(), 2 * H, c.data_ptr(), 2 * H, x3=x3)
     ref = torch.nn.LSTMCell(H, H).cuda()
     ref.load_state_dict(cell.state_dict())
     rh, rc = ref(x, (h.contiguous(), c.contiguous()))

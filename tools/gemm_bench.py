@@ -18,7 +18,8 @@ SHAPES = [  # name, M, N, K
 ]
 
 
-TILES = [int(t) for t in os.environ.get("TILES", "-1,0,3,4").split(",")]
+TILES = [int(t) for t in os.environ.get("TILES", "-1").split(",")]
+X3_TILES = [int(t) for t in os.environ.get("X3_TILES", "-1,1,2").split(",")]
 
 
 def timeit(fn, reps=20):
@@ -46,19 +47,29 @@ def main():
         y = torch.empty(m, n, device="cuda")
         xc = x.contiguous()
 
+        x3 = FU.X3(wp, ldw, n, k)
+
         def mine():
             FU.gemm(FU.dense(buf.data_ptr(), ldx, k), None, wp.data_ptr(), ldw, b.data_ptr(), m, n, 1, y.data_ptr(), n)
+
+        def mine3():
+            FU.gemm(FU.dense(buf.data_ptr(), ldx, k), None, wp.data_ptr(), ldw, b.data_ptr(), m, n, 1, y.data_ptr(), n,
+                    x3=x3)
 
         def blas():
             F.linear(xc, w, b)
 
         lib = FU._setup()
         r = {f"tile{t}": [] for t in TILES}
+        r.update({f"x3tile{t}": [] for t in X3_TILES})
         r["hipblaslt"] = []
         for _ in range(3):
             for t in TILES:
                 lib.gm_gemm_set_tile(t)
                 r[f"tile{t}"].append(timeit(mine))
+            for t in X3_TILES:
+                lib.gm_gemm_set_tile(t)
+                r[f"x3tile{t}"].append(timeit(mine3))
             r["hipblaslt"].append(timeit(blas))
         lib.gm_gemm_set_tile(-1)
         fl = 2.0 * m * n * k
@@ -77,19 +88,26 @@ def main():
     wp, ldw = FU._pad_cols(w)
     y = torch.empty(m, 512, device="cuda")
 
-    def ro():
+    x3r = FU.X3(wp, ldw, 512, 642)
+
+    def ro(x3=None):
         a0 = FU.readout(state.data_ptr(), 2 * H_, hprev.data_ptr(), 2 * H_, nbr, agent_node, N_, H_)
-        FU.gemm(a0, FU.dense(obs.data_ptr(), 644, 130), wp.data_ptr(), ldw, b.data_ptr(), m, 512, 1, y.data_ptr(), 512)
+        FU.gemm(a0, FU.dense(obs.data_ptr(), 644, 130), wp.data_ptr(), ldw, b.data_ptr(), m, 512, 1, y.data_ptr(), 512,
+                x3=x3)
 
     lib = FU._setup()
-    r = {t: [] for t in TILES}
+    r = {f"tile{t}": [] for t in TILES}
+    r.update({f"x3tile{t}": [] for t in X3_TILES})
     for _ in range(3):
         for t in TILES:
             lib.gm_gemm_set_tile(t)
-            r[t].append(timeit(ro))
+            r[f"tile{t}"].append(timeit(ro))
+        for t in X3_TILES:
+            lib.gm_gemm_set_tile(t)
+            r[f"x3tile{t}"].append(timeit(lambda: ro(x3r)))
     lib.gm_gemm_set_tile(-1)
     fl = 2.0 * m * 512 * 642
-    print("dqn.l1.readout", json.dumps({f"tile{t}": {"us": round(min(v), 1), "tflops": round(fl / (min(v) * 1e-6) / 1e12, 1)}
+    print("dqn.l1.readout", json.dumps({t: {"us": round(min(v), 1), "tflops": round(fl / (min(v) * 1e-6) / 1e12, 1)}
                                         for t, v in r.items()}), flush=True)
     # fused LSTM cell GEMM (dense [x|h] source, gate epilogue)
     M_ = importlib.import_module("graph-marl_amd.model")
@@ -97,29 +115,35 @@ def main():
     cell = M_.LSTMCell(H, H).cuda()
     x = torch.randn(m, H, device="cuda")
     st = torch.randn(m, 2 * H, device="cuda")
-    wp, ldw, bp = FU.pack_lstm(cell)
+    wp, ldw, bp, _ = FU.pack_lstm(cell)
+    x3l = FU.X3(wp, ldw, 4 * H, 2 * H)
     S = torch.empty(m, 2 * H, device="cuda")
     nbr = torch.randint(0, 20, (m // 20, 20, 3), device="cuda", dtype=torch.int32)
 
-    def lstm_dense():
+    def lstm_dense(x3=None):
         FU.gemm(FU.dense(x.data_ptr(), H, H), FU.dense(st.data_ptr(), 2 * H, H), wp.data_ptr(), ldw, bp.data_ptr(),
-                m, 4 * H, FU.GM_EPI_LSTM, S.data_ptr(), 2 * H, S[:, H:].data_ptr(), 2 * H, st[:, H:].data_ptr(), 2 * H)
+                m, 4 * H, FU.GM_EPI_LSTM, S.data_ptr(), 2 * H, S[:, H:].data_ptr(), 2 * H, st[:, H:].data_ptr(), 2 * H,
+                x3=x3)
 
-    def lstm_agg():
+    def lstm_agg(x3=None):
         FU.gemm(FU.aggregate(st.data_ptr(), 2 * H, H, nbr, 20), FU.dense(st.data_ptr(), 2 * H, H), wp.data_ptr(),
                 ldw, bp.data_ptr(), m, 4 * H, FU.GM_EPI_LSTM, S.data_ptr(), 2 * H, S[:, H:].data_ptr(), 2 * H,
-                st[:, H:].data_ptr(), 2 * H)
+                st[:, H:].data_ptr(), 2 * H, x3=x3)
 
     lib = FU._setup()
     for name, fn in (("lstm_fused", lstm_dense), ("lstm_agg_fused", lstm_agg)):
-        r = {0: [], 2: [], 4: []}
+        r = {f"tile{t}": [] for t in TILES}
+        r.update({f"x3tile{t}": [] for t in X3_TILES})
         for _ in range(3):
-            for t in r:
+            for t in TILES:
                 lib.gm_gemm_set_tile(t)
-                r[t].append(timeit(fn))
+                r[f"tile{t}"].append(timeit(fn))
+            for t in X3_TILES:
+                lib.gm_gemm_set_tile(t)
+                r[f"x3tile{t}"].append(timeit(lambda: fn(x3l)))
         lib.gm_gemm_set_tile(-1)
         fl = 2.0 * m * 4 * H * 2 * H
-        print(name, json.dumps({f"tile{t}": {"us": round(min(v), 1), "tflops": round(fl / (min(v) * 1e-6) / 1e12, 1)}
+        print(name, json.dumps({t: {"us": round(min(v), 1), "tflops": round(fl / (min(v) * 1e-6) / 1e12, 1)}
                                 for t, v in r.items()}), flush=True)
 
 

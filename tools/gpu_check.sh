@@ -29,6 +29,8 @@ for s in "$@"; do
                 --master-addr 127.0.0.1 --master-port 29511 bench.py --gpus 2 --steps 20 --warmup 5 \
                 --no-cpu-baseline || exit $? ;;
         gemm) step gemm 300 python tools/gemm_bench.py || exit $? ;;
+        fused) step fused_tests 600 python -m pytest tests/test_fused_gpu.py -x -q --tb=short --timeout=300 -p no:cacheprovider || exit $? ;;
+        benchf32) GM_GEMM=f32 step bench_f32 300 python bench.py --no-cpu-baseline --steps 100 || exit $? ;;
         bench) step bench 600 python bench.py || exit $? ;;
         benchq) step bench 300 python bench.py --no-cpu-baseline --steps 100 || exit $? ;;
         prof) step prof 600 rocprofv3 --kernel-trace --stats -T --output-format csv -d gpurun_out/prof -o bench \
