@@ -21,9 +21,9 @@
 //        (the dropped a_lo·w_lo term is ~2^-22 |a·w|). W is split once (gm_gemm_pack_x3)
 //        after a power-of-two scale S keeps its pieces normal; A (fp32 in HBM) is split
 //        while its tile is stored to LDS, its low piece scaled by 2^12 (a_lo' = f16((a -
-//        a_hi)·2^12), normal down to |a| ~ 2^-15) and paired with a third weight plane
-//        w_hi·2^-12, so all three products share one accumulator; the epilogue
-//        multiplies by 1/S (exact).
+//        a_hi)·2^12), normal down to |a| ~ 2^-15) and paired with w_hi·2^-12 (formed in
+//        registers, exact), so all three products share one accumulator; the epilogue
+//        multiplies by 1/S (exact). Operand tiles are prefetched two k steps ahead.
 // All operand loads are
 // unconditional buffer_load_dwordx4 (hardware bounds check returns 0: missing
 // neighbours use an out-of-range offset, rows are clamped), so the load stream has
@@ -34,6 +34,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstring>
+#include <type_traits>
 #include <string>
 
 #include "../../include/graph_marl_amd.h"
@@ -87,11 +88,73 @@ __device__ __forceinline__ float4 f4add(float4 a, float4 b) {
     return make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w);
 }
 __device__ __forceinline__ float sigm(float x) { return 1.0f / (1.0f + expf(-x)); }
-// a = hi + 2^-12 lo with hi = f16(a) (RNE), lo = f16((a - hi) * 2^12): 2 x 8 bytes to LDS
+// a = hi + 2^-12 lo with hi = f16(a) (RNE), lo = f16((a - hi) * 2^12)
 __device__ __forceinline__ void split4(float4 v, half4& hi, half4& lo) {
     const floatx4 a = {v.x, v.y, v.z, v.w};
     hi = __builtin_convertvector(a, half4);
     lo = __builtin_convertvector((a - __builtin_convertvector(hi, floatx4)) * 4096.0f, half4);
+}
+
+// Epilogue of both forms. C/D map of the 32x32 MFMA tiles: col = lane & 31, row =
+// (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5); wave tile origin (wm0, wn0).
+template <int TM, int TN, int EPI>
+__device__ __forceinline__ void epilogue(floatx16 (&acc)[TM][TN], const Epi& ep, int wm0, int wn0, int M, int N,
+                                         int lane) {
+    const int h = lane >> 5, l32 = lane & 31;
+    if constexpr (EPI == EPI_BIAS) {
+#pragma unroll
+        for (int j = 0; j < TN; j++) {
+            const int col = wn0 + j * 32 + l32;
+            const float bv = (ep.bias && col < N) ? ep.bias[col] : 0.f;
+#pragma unroll
+            for (int i = 0; i < TM; i++) {
+                const int rb0 = wm0 + i * 32 + 4 * h;
+#pragma unroll
+                for (int r = 0; r < 16; r++) {
+                    const int row = rb0 + (r & 3) + 8 * (r >> 2);
+                    float v = acc[i][j][r] + bv;
+                    if (ep.act == 1) v = v >= 0.f ? v : 0.01f * v;
+                    if (row < M && col < N) ep.y[(long long)row * ep.ldy + col] = v;
+                }
+            }
+        }
+    } else {  // EPI_LSTM: TN == 4 gate tiles (i, f, g, o) of 32 hidden units
+        const int H = ep.hidden;
+        const int unit = (wn0 >> 2) + l32;
+        float bgate[4];
+#pragma unroll
+        for (int g = 0; g < 4; g++) bgate[g] = ep.bias ? ep.bias[wn0 + g * 32 + l32] : 0.f;
+#pragma unroll
+        for (int i = 0; i < TM; i++) {
+            const int rb0 = wm0 + i * 32 + 4 * h;
+#pragma unroll
+            for (int r = 0; r < 16; r++) {
+                const int row = rb0 + (r & 3) + 8 * (r >> 2);
+                if (row >= M || unit >= H) continue;
+                float gi = sigm(acc[i][0][r] + bgate[0]);
+                float gf = sigm(acc[i][1][r] + bgate[1]);
+                float gg = tanhf(acc[i][2][r] + bgate[2]);
+                float go = sigm(acc[i][3][r] + bgate[3]);
+                float cn = gf * ep.c_in[(long long)row * ep.ldc + unit] + gi * gg;
+                float hn = go * tanhf(cn);
+                ep.y[(long long)row * ep.ldy + unit] = hn;
+                ep.y2[(long long)row * ep.ldy2 + unit] = cn;
+                if (ep.act_out) {
+                    float* ao = ep.act_out + (long long)row * 4 * H;
+                    ao[unit] = gi;
+                    ao[H + unit] = gf;
+                    ao[2 * H + unit] = gg;
+                    ao[3 * H + unit] = go;
+                }
+            }
+        }
+    }
+}
+
+// XCD-aware tile order: consecutive tiles (sharing A rows) land on one XCD
+__device__ __forceinline__ int xcd_remap(int bid, int T) {
+    const int q = T / 8, r = T % 8, xcd = bid % 8, loc = bid / 8;
+    return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + loc;
 }
 
 template <int WGM, int WGN, int TM, int TN, int BK_>
@@ -107,33 +170,20 @@ struct Cfg {
     static constexpr int RSTEP = THREADS / (BK / 4);   // rows between a thread's A rows
 };
 
-// X3 LDS row images. A (same 4*BK + 16 bytes as the F32 row): per 16-deep k block s,
-// bytes [64s, 64s+32) = 16 hi halves, [64s+32, 64s+64) = 16 lo' halves. B (6*BK + 16
-// bytes): per block s, [96s, 96s+96) = 16 hi | 16 lo | 16 hi*2^-12 halves — the packed
-// weights (gm_gemm_pack_x3) have this block layout in HBM, so B tiles are plain copies.
-template <int WGM, int WGN, int TM, int TN, int BK_, int AMODE, int EPI, int OCC, bool X3>
+template <int WGM, int WGN, int TM, int TN, int BK_, int AMODE, int EPI, int OCC>
 __global__ __launch_bounds__(WGM* WGN * 64, OCC) void k_gemm(ASrc a0, ASrc a1, const float* __restrict__ w,
                                                             long long ldw, unsigned wbytes, int M, int N, int K,
-                                                            Epi ep, const float* __restrict__ wscale_inv) {
+                                                            Epi ep) {
     using C = Cfg<WGM, WGN, TM, TN, BK_>;
     constexpr int BK = C::BK, LDP = C::LDP, KH = C::KH;
-    constexpr int ROWB = LDP * 4;                        // bytes per A LDS row (both forms)
-    constexpr int ROWBB = X3 ? 6 * BK + 16 : ROWB;       // bytes per B LDS row
-    constexpr int CB = 6 * BK / 16;                      // X3: 16-byte chunks per B tile row
-    constexpr int BQ3 = (C::BN * CB + C::THREADS - 1) / C::THREADS;
-    static_assert(!X3 || BK % 16 == 0, "X3 tiles hold whole 16-deep k blocks");
     __shared__ __attribute__((aligned(16))) float As[2][C::BM * LDP];
-    __shared__ __attribute__((aligned(16))) float Bs[2][C::BN * ROWBB / 4];
+    __shared__ __attribute__((aligned(16))) float Bs[2][C::BN * LDP];
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int wr = wave / WGN, wc = wave % WGN;
     const int nM = (M + C::BM - 1) / C::BM, nN = (N + C::BN - 1) / C::BN;
     const int T = nM * nN;
-    int bid = blockIdx.x;
-    {
-        const int q = T / 8, r = T % 8, xcd = bid % 8, loc = bid / 8;
-        bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + loc;
-    }
+    const int bid = xcd_remap(blockIdx.x, T);
     const int m0 = (bid / nN) * C::BM, n0 = (bid % nN) * C::BN;
 
     // ---- per-thread A rows (fixed over K) and their source rows ----
@@ -181,29 +231,16 @@ __global__ __launch_bounds__(WGM* WGN * 64, OCC) void k_gemm(ASrc a0, ASrc a1, c
             ro3[q] = src[q][3] >= 0 ? (int)(src[q][3] * a0.ld1) * 4 : OOB;
         }
     }
-    // F32: element offset of the thread's W rows. X3: chunk q of the thread is chunk
-    // tid + q*THREADS of the tile (row id / CB, 16-byte column id % CB): byte offset of
-    // its packed row + column (ldw = packed row bytes), and its LDS byte offset
-    constexpr int NW = X3 ? BQ3 : C::BQ;
-    int woff[NW], bdst[NW];
+    int woff[C::BQ];
 #pragma unroll
-    for (int q = 0; q < NW; q++) {
-        if (X3) {
-            const int id = min(tid + q * C::THREADS, C::BN * CB - 1), r = id / CB, c = id - r * CB;
-            woff[q] = (int)(min(n0 + r, N - 1) * ldw) + 16 * c;
-            bdst[q] = r * ROWBB + 16 * c;
-        } else {
-            woff[q] = (int)(min(n0 + rbase + q * C::RSTEP, N - 1) * ldw);
-            bdst[q] = 0;
-        }
-    }
+    for (int q = 0; q < C::BQ; q++) woff[q] = (int)(min(n0 + rbase + q * C::RSTEP, N - 1) * ldw);
 
     const __amdgpu_buffer_rsrc_t r0a = rsrc(a0.p0, a0.bytes0);
     const __amdgpu_buffer_rsrc_t r0b = rsrc(a0.p1 ? a0.p1 : a0.p0, a0.p1 ? a0.bytes1 : a0.bytes0);
     const __amdgpu_buffer_rsrc_t r1 = rsrc(a1.p0 ? a1.p0 : a0.p0, a1.p0 ? a1.bytes0 : 0u);
     const __amdgpu_buffer_rsrc_t rw = rsrc(w, wbytes);
 
-    float4 ra[C::AQ], rb[NW];
+    float4 ra[C::AQ], rb[C::BQ];
     auto gload = [&](int k0) {
         if (k0 < a0.k) {
             const int kl = k0 + 4 * c4;
@@ -241,13 +278,8 @@ __global__ __launch_bounds__(WGM* WGN * 64, OCC) void k_gemm(ASrc a0, ASrc a1, c
 #pragma unroll
             for (int q = 0; q < C::AQ; q++) ra[q] = bload(r1, (rowoff1[q] + kl) * 4);
         }
-        if (X3) {
 #pragma unroll
-            for (int q = 0; q < NW; q++) rb[q] = bload(rw, woff[q] + k0 * 6);
-        } else {
-#pragma unroll
-            for (int q = 0; q < C::BQ; q++) rb[q] = bload(rw, (woff[q] + k0 + 4 * c4) * 4);
-        }
+        for (int q = 0; q < C::BQ; q++) rb[q] = bload(rw, (woff[q] + k0 + 4 * c4) * 4);
     };
     auto lstore = [&](int buf, int k0) {
         // zero the columns past the end of the current source on its last (ragged) tile
@@ -261,43 +293,20 @@ __global__ __launch_bounds__(WGM* WGN * 64, OCC) void k_gemm(ASrc a0, ASrc a1, c
                 if (kk + 2 >= kend) ra[q].z = 0.f;
                 if (kk + 3 >= kend) ra[q].w = 0.f;
             }
-            if (!X3) {  // packed X3 weights are zero past K
 #pragma unroll
-                for (int q = 0; q < C::BQ; q++) {
-                    if (kk + 0 >= K) rb[q].x = 0.f;
-                    if (kk + 1 >= K) rb[q].y = 0.f;
-                    if (kk + 2 >= K) rb[q].z = 0.f;
-                    if (kk + 3 >= K) rb[q].w = 0.f;
-                }
+            for (int q = 0; q < C::BQ; q++) {
+                if (kk + 0 >= K) rb[q].x = 0.f;
+                if (kk + 1 >= K) rb[q].y = 0.f;
+                if (kk + 2 >= K) rb[q].z = 0.f;
+                if (kk + 3 >= K) rb[q].w = 0.f;
             }
         }
-        if (X3) {
-            char* as = reinterpret_cast<char*>(As[buf]);
-            const int hb = (c4 >> 2) * 64 + (c4 & 3) * 8;  // hi bytes of k = 4*c4 .. 4*c4+3
 #pragma unroll
-            for (int q = 0; q < C::AQ; q++) {
-                half4 hi, lo;
-                split4(ra[q], hi, lo);
-                char* row = as + (rbase + q * C::RSTEP) * ROWB + hb;
-                *reinterpret_cast<half4*>(row) = hi;
-                *reinterpret_cast<half4*>(row + 32) = lo;
-            }
-        } else {
+        for (int q = 0; q < C::AQ; q++)
+            *reinterpret_cast<float4*>(&As[buf][(rbase + q * C::RSTEP) * LDP + 4 * c4]) = ra[q];
 #pragma unroll
-            for (int q = 0; q < C::AQ; q++)
-                *reinterpret_cast<float4*>(&As[buf][(rbase + q * C::RSTEP) * LDP + 4 * c4]) = ra[q];
-        }
-        if (X3) {
-            char* bsm = reinterpret_cast<char*>(Bs[buf]);
-#pragma unroll
-            for (int q = 0; q < NW; q++)
-                if ((C::BN * CB) % C::THREADS == 0 || tid + q * C::THREADS < C::BN * CB)
-                    *reinterpret_cast<float4*>(bsm + bdst[q]) = rb[q];
-        } else {
-#pragma unroll
-            for (int q = 0; q < C::BQ; q++)
-                *reinterpret_cast<float4*>(&Bs[buf][(rbase + q * C::RSTEP) * LDP + 4 * c4]) = rb[q];
-        }
+        for (int q = 0; q < C::BQ; q++)
+            *reinterpret_cast<float4*>(&Bs[buf][(rbase + q * C::RSTEP) * LDP + 4 * c4]) = rb[q];
     };
 
     floatx16 acc[TM][TN];
@@ -318,35 +327,6 @@ __global__ __launch_bounds__(WGM* WGN * 64, OCC) void k_gemm(ASrc a0, ASrc a1, c
         if (kt + 1 < nk) gload((kt + 1) * BK);
         const float* as = As[cur];
         const float* bs = Bs[cur];
-        if (X3) {
-            const char* ac = reinterpret_cast<const char*>(as);
-            const char* bc = reinterpret_cast<const char*>(bs);
-#pragma unroll
-            for (int sb = 0; sb < BK / 16; sb++) {
-                half8 ah[TM], al[TM], bh[TN], bl[TN], bs3[TN];
-#pragma unroll
-                for (int i = 0; i < TM; i++) {
-                    const char* p = ac + (wr * TM * 32 + i * 32 + l32) * ROWB + sb * 64 + 16 * h;
-                    ah[i] = *reinterpret_cast<const half8*>(p);
-                    al[i] = *reinterpret_cast<const half8*>(p + 32);
-                }
-#pragma unroll
-                for (int j = 0; j < TN; j++) {
-                    const char* p = bc + (wc * TN * 32 + j * 32 + l32) * ROWBB + sb * 96 + 16 * h;
-                    bh[j] = *reinterpret_cast<const half8*>(p);
-                    bl[j] = *reinterpret_cast<const half8*>(p + 32);
-                    bs3[j] = *reinterpret_cast<const half8*>(p + 64);
-                }
-#pragma unroll
-                for (int i = 0; i < TM; i++)
-#pragma unroll
-                    for (int j = 0; j < TN; j++) {
-                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[i], bs3[j], acc[i][j], 0, 0, 0);
-                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[i], bl[j], acc[i][j], 0, 0, 0);
-                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[i], bh[j], acc[i][j], 0, 0, 0);
-                    }
-            }
-        } else {
 #pragma unroll
         for (int s4 = 0; s4 < KH / 4; s4++) {
             float4 af[TM], bf[TN];
@@ -367,69 +347,227 @@ __global__ __launch_bounds__(WGM* WGN * 64, OCC) void k_gemm(ASrc a0, ASrc a1, c
                         acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, acc[i][j], 0, 0, 0);
                     }
         }
-        }
         if (kt + 1 < nk) lstore(cur ^ 1, (kt + 1) * BK);
         __syncthreads();
     }
 
-    // ---- epilogue: C/D map col = lane & 31, row = (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5) ----
-    if (X3) {  // undo the weight scale (a power of two: exact)
-        const float si = *wscale_inv;
+    epilogue<TM, TN, EPI>(acc, ep, m0 + wr * TM * 32, n0 + wc * TN * 32, M, N, lane);
+}
+
+// ---------------------------------------------------------------------------------------
+// X3 (split-f16) kernel. LDS row image of A and B tiles (4*BK + 16 bytes, conflict-free
+// ds_read_b128 on the 32 rows of an MFMA operand): per 16-deep k block s, bytes
+// [64s, 64s+32) = 16 hi halves, [64s+32, 64s+64) = 16 lo halves. Packed weights
+// (gm_gemm_pack_x3) have this block layout in HBM, so B tiles are plain copies; A tiles
+// are split while stored. Operand tiles are loaded two k steps ahead into two register
+// sets (the loop is unrolled by two so each set has fixed registers and the waits stay
+// counted); AGGREGATE keeps its 4 member rows raw until the store, so no load result is
+// consumed before the step that stores it.
+template <int WGM, int WGN, int TM, int TN, int BK, int AMODE, int EPI, int OCC>
+__global__ __launch_bounds__(WGM* WGN * 64, OCC) void k_gemm3(ASrc a0, ASrc a1, const _Float16* __restrict__ w,
+                                                             long long ldw, unsigned wbytes, int M, int N, int K,
+                                                             Epi ep, const float* __restrict__ wscale_inv) {
+    constexpr int BM = WGM * TM * 32, BN = WGN * TN * 32, THREADS = WGM * WGN * 64;
+    constexpr int ROWB = 4 * BK + 16;          // LDS row bytes (A and B)
+    constexpr int CPR = BK / 4;                // 16-byte chunks per tile row (A: float4; B: 8 halves)
+    constexpr int RSTEP = THREADS / CPR;       // rows between a thread's rows
+    constexpr int AQ = BM / RSTEP, BQ = BN / RSTEP;
+    constexpr int NR = AMODE == GM_A_AGGREGATE ? 4 : 1;  // raw float4 per A chunk
+    static_assert(BK % 16 == 0 && BM % RSTEP == 0 && BN % RSTEP == 0, "tile shape");
+    __shared__ __attribute__((aligned(16))) char As[2][BM * ROWB];
+    __shared__ __attribute__((aligned(16))) char Bs[2][BN * ROWB];
+
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wr = wave / WGN, wc = wave % WGN;
+    const int nM = (M + BM - 1) / BM, nN = (N + BN - 1) / BN;
+    const int bid = xcd_remap(blockIdx.x, nM * nN);
+    const int m0 = (bid / nN) * BM, n0 = (bid % nN) * BN;
+
+    // ---- per-thread source byte offsets (fixed over K) ----
+    const int c4 = tid % CPR, rbase = tid / CPR;
+    int off1[AQ];       // src1 row
+    int so[AQ][4];      // DENSE: so[q][0] row; AGGREGATE: member rows; READOUT: segment rows (OOB = none)
+    float scale[AQ];
 #pragma unroll
-        for (int i = 0; i < TM; i++)
+    for (int q = 0; q < AQ; q++) {
+        const int row = min(m0 + rbase + q * RSTEP, M - 1);
+        off1[q] = (int)(row * a1.ld0) * 4;
+        scale[q] = 1.0f;
 #pragma unroll
-            for (int j = 0; j < TN; j++)
+        for (int j = 0; j < 4; j++) so[q][j] = OOB;
+        if (AMODE == GM_A_DENSE) {
+            so[q][0] = (int)(row * a0.ld0) * 4;
+        } else if (AMODE == GM_A_AGGREGATE) {
+            // members of (I + A) row n in ascending node id (SimpleAggregation's bmm order)
+            const int g = row / a0.n_nodes, n = row - g * a0.n_nodes;
+            const int* nb = a0.nbr + (size_t)row * a0.deg;
+            int mem[4] = {-1, -1, -1, -1};
+            int cnt = 0, self_done = 0;
+            for (int j = 0; j < a0.deg; j++) {
+                const int v = nb[j];
+                if (v < 0) continue;
+                if (!self_done && n < v) { mem[cnt++] = n; self_done = 1; }
+                mem[cnt++] = v;
+            }
+            if (!self_done) mem[cnt++] = n;
 #pragma unroll
-                for (int r = 0; r < 16; r++) acc[i][j][r] *= si;
+            for (int j = 0; j < 4; j++) so[q][j] = mem[j] >= 0 ? (int)((g * a0.n_nodes + mem[j]) * a0.ld0) * 4 : OOB;
+            if (a0.mean) scale[q] = 1.0f / (float)cnt;
+        } else {  // READOUT: [h_final[v] | h_prev[nbr(v, 0..2)]], v = agent_node[row]
+            const int g = row / a0.rows_per_graph;
+            const int v = a0.agent_node[row];
+            const int* nb = a0.nbr + ((size_t)g * a0.n_nodes + v) * a0.deg;
+            so[q][0] = (int)((g * a0.n_nodes + v) * a0.ld0) * 4;
+#pragma unroll
+            for (int j = 1; j < 4; j++) {
+                const int m = j - 1 < a0.deg ? nb[j - 1] : -1;
+                so[q][j] = m >= 0 ? (int)((g * a0.n_nodes + m) * a0.ld1) * 4 : OOB;
+            }
+        }
     }
-    if (EPI == EPI_BIAS) {
+    int woff[BQ];
 #pragma unroll
-        for (int j = 0; j < TN; j++) {
-            const int col = n0 + wc * TN * 32 + j * 32 + l32;
-            const float bv = (ep.bias && col < N) ? ep.bias[col] : 0.f;
+    for (int q = 0; q < BQ; q++) woff[q] = (int)(min(n0 + rbase + q * RSTEP, N - 1) * ldw) + 16 * c4;
+
+    const __amdgpu_buffer_rsrc_t r0a = rsrc(a0.p0, a0.bytes0);
+    const __amdgpu_buffer_rsrc_t r0b = rsrc(a0.p1 ? a0.p1 : a0.p0, a0.p1 ? a0.bytes1 : a0.bytes0);
+    const __amdgpu_buffer_rsrc_t r1 = rsrc(a1.p0 ? a1.p0 : a0.p0, a1.p0 ? a1.bytes0 : 0u);
+    const __amdgpu_buffer_rsrc_t rw = rsrc(reinterpret_cast<const float*>(w), wbytes);
+
+    float4 ra[2][AQ][NR], rb[2][BQ];
+    auto gload = [&](auto SET, int k0) {
+        constexpr int S = decltype(SET)::value;
+        if (k0 < a0.k) {
+            const int kb = (k0 + 4 * c4) * 4;
+            if (AMODE == GM_A_DENSE) {
+#pragma unroll
+                for (int q = 0; q < AQ; q++) ra[S][q][0] = bload(r0a, so[q][0] + kb);
+            } else if (AMODE == GM_A_AGGREGATE) {
+#pragma unroll
+                for (int q = 0; q < AQ; q++)
+#pragma unroll
+                    for (int j = 0; j < NR; j++) ra[S][q][j] = bload(r0a, so[q][j] == OOB ? OOB : so[q][j] + kb);
+            } else {  // READOUT: the k tile lies inside one H-wide segment
+                const int seg = k0 / a0.hidden, ko = kb - seg * a0.hidden * 4;
+                if (seg == 0) {
+#pragma unroll
+                    for (int q = 0; q < AQ; q++) ra[S][q][0] = bload(r0a, so[q][0] + ko);
+                } else if (seg == 1) {
+#pragma unroll
+                    for (int q = 0; q < AQ; q++) ra[S][q][0] = bload(r0b, so[q][1] == OOB ? OOB : so[q][1] + ko);
+                } else if (seg == 2) {
+#pragma unroll
+                    for (int q = 0; q < AQ; q++) ra[S][q][0] = bload(r0b, so[q][2] == OOB ? OOB : so[q][2] + ko);
+                } else {
+#pragma unroll
+                    for (int q = 0; q < AQ; q++) ra[S][q][0] = bload(r0b, so[q][3] == OOB ? OOB : so[q][3] + ko);
+                }
+            }
+        } else {
+            const int kb = (k0 - a0.k + 4 * c4) * 4;
+#pragma unroll
+            for (int q = 0; q < AQ; q++) ra[S][q][0] = bload(r1, off1[q] + kb);
+        }
+#pragma unroll
+        for (int q = 0; q < BQ; q++) rb[S][q] = bload(rw, woff[q] + k0 * 4);
+    };
+    auto lstore = [&](auto SET, int buf, int k0) {
+        constexpr int S = decltype(SET)::value;
+        const bool agg = AMODE == GM_A_AGGREGATE && k0 < a0.k;
+        const int kend = k0 < a0.k ? a0.k : K;  // zero the columns past the current source
+        const int kk = k0 + 4 * c4;
+        char* as = As[buf] + (c4 >> 2) * 64 + (c4 & 3) * 8;
+#pragma unroll
+        for (int q = 0; q < AQ; q++) {
+            float4 v = ra[S][q][0];
+            if (agg) {
+#pragma unroll
+                for (int j = 1; j < NR; j++) v = f4add(v, ra[S][q][j]);
+                v = make_float4(v.x * scale[q], v.y * scale[q], v.z * scale[q], v.w * scale[q]);
+            }
+            if (k0 + BK > kend) {
+                if (kk + 0 >= kend) v.x = 0.f;
+                if (kk + 1 >= kend) v.y = 0.f;
+                if (kk + 2 >= kend) v.z = 0.f;
+                if (kk + 3 >= kend) v.w = 0.f;
+            }
+            half4 hi, lo;
+            split4(v, hi, lo);
+            char* row = as + (rbase + q * RSTEP) * ROWB;
+            *reinterpret_cast<half4*>(row) = hi;
+            *reinterpret_cast<half4*>(row + 32) = lo;
+        }
+#pragma unroll
+        for (int q = 0; q < BQ; q++) *reinterpret_cast<float4*>(Bs[buf] + (rbase + q * RSTEP) * ROWB + 16 * c4) = rb[S][q];
+    };
+
+    floatx16 acc[TM][TN];
+#pragma unroll
+    for (int i = 0; i < TM; i++)
+#pragma unroll
+        for (int j = 0; j < TN; j++)
+#pragma unroll
+            for (int r = 0; r < 16; r++) acc[i][j][r] = 0.f;
+
+    const int h = lane >> 5, l32 = lane & 31;
+    const _Float16 s12 = (_Float16)(1.0f / 4096.0f);
+    auto compute = [&](int buf) {
+        const char* ac = As[buf] + (wr * TM * 32 + l32) * ROWB + 16 * h;
+        const char* bc = Bs[buf] + (wc * TN * 32 + l32) * ROWB + 16 * h;
+#pragma unroll
+        for (int sb = 0; sb < BK / 16; sb++) {
+            half8 ah[TM], al[TM], bh[TN], bl[TN];
 #pragma unroll
             for (int i = 0; i < TM; i++) {
-                const int rb0 = m0 + wr * TM * 32 + i * 32 + 4 * h;
-#pragma unroll
-                for (int r = 0; r < 16; r++) {
-                    const int row = rb0 + (r & 3) + 8 * (r >> 2);
-                    float v = acc[i][j][r] + bv;
-                    if (ep.act == 1) v = v >= 0.f ? v : 0.01f * v;
-                    if (row < M && col < N) ep.y[(long long)row * ep.ldy + col] = v;
-                }
+                ah[i] = *reinterpret_cast<const half8*>(ac + i * 32 * ROWB + sb * 64);
+                al[i] = *reinterpret_cast<const half8*>(ac + i * 32 * ROWB + sb * 64 + 32);
             }
-        }
-    } else {  // EPI_LSTM: TN == 4 gate tiles (i, f, g, o) of 32 hidden units
-        const int H = ep.hidden;
-        const int unit = (n0 >> 2) + l32;
-        float bgate[4];
 #pragma unroll
-        for (int g = 0; g < 4; g++) bgate[g] = ep.bias ? ep.bias[n0 + g * 32 + l32] : 0.f;
-#pragma unroll
-        for (int i = 0; i < TM; i++) {
-            const int rb0 = m0 + wr * TM * 32 + i * 32 + 4 * h;
-#pragma unroll
-            for (int r = 0; r < 16; r++) {
-                const int row = rb0 + (r & 3) + 8 * (r >> 2);
-                if (row >= M || unit >= H) continue;
-                float gi = sigm(acc[i][0][r] + bgate[0]);
-                float gf = sigm(acc[i][1][r] + bgate[1]);
-                float gg = tanhf(acc[i][2][r] + bgate[2]);
-                float go = sigm(acc[i][3][r] + bgate[3]);
-                float cn = gf * ep.c_in[(long long)row * ep.ldc + unit] + gi * gg;
-                float hn = go * tanhf(cn);
-                ep.y[(long long)row * ep.ldy + unit] = hn;
-                ep.y2[(long long)row * ep.ldy2 + unit] = cn;
-                if (ep.act_out) {
-                    float* ao = ep.act_out + (long long)row * 4 * H;
-                    ao[unit] = gi;
-                    ao[H + unit] = gf;
-                    ao[2 * H + unit] = gg;
-                    ao[3 * H + unit] = go;
-                }
+            for (int j = 0; j < TN; j++) {
+                bh[j] = *reinterpret_cast<const half8*>(bc + j * 32 * ROWB + sb * 64);
+                bl[j] = *reinterpret_cast<const half8*>(bc + j * 32 * ROWB + sb * 64 + 32);
             }
+#pragma unroll
+            for (int i = 0; i < TM; i++)
+#pragma unroll
+                for (int j = 0; j < TN; j++) {
+                    const half8 bs = bh[j] * s12;  // w_hi * 2^-12, exact
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[i], bs, acc[i][j], 0, 0, 0);
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[i], bl[j], acc[i][j], 0, 0, 0);
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[i], bh[j], acc[i][j], 0, 0, 0);
+                }
         }
+    };
+
+    using S0 = std::integral_constant<int, 0>;
+    using S1 = std::integral_constant<int, 1>;
+    const int nk = (K + BK - 1) / BK;
+    gload(S0{}, 0);
+    if (nk > 1) gload(S1{}, BK);
+    lstore(S0{}, 0, 0);
+    __syncthreads();
+    // step kt computes LDS buffer kt&1, loads tile kt+2 into register set kt&1 (its tile kt
+    // is already in LDS) and stores tile kt+1 (set (kt+1)&1) into the other buffer
+    auto step = [&](auto SET, int kt) {
+        constexpr int S = decltype(SET)::value;
+        if (kt + 2 < nk) gload(SET, (kt + 2) * BK);
+        compute(S);
+        if (kt + 1 < nk) lstore(std::integral_constant<int, S ^ 1>{}, S ^ 1, (kt + 1) * BK);
+        __syncthreads();
+    };
+    for (int kt = 0; kt < nk; kt += 2) {
+        step(S0{}, kt);
+        if (kt + 1 < nk) step(S1{}, kt + 1);
     }
+
+    const float si = *wscale_inv;  // undo the weight scale (a power of two: exact)
+#pragma unroll
+    for (int i = 0; i < TM; i++)
+#pragma unroll
+        for (int j = 0; j < TN; j++)
+#pragma unroll
+            for (int r = 0; r < 16; r++) acc[i][j][r] *= si;
+    epilogue<TM, TN, EPI>(acc, ep, m0 + wr * TM * 32, n0 + wc * TN * 32, M, N, lane);
 }
 
 template <int WGM, int WGN, int TM, int TN, int BK_, int AMODE, int EPI, int OCC = 2, bool X3 = false>
@@ -437,8 +575,12 @@ int launch(const ASrc& a0, const ASrc& a1, const float* w, long long ldw, unsign
            const Epi& ep, hipStream_t st, const float* wscale_inv = nullptr) {
     using C = Cfg<WGM, WGN, TM, TN, BK_>;
     const int T = ((M + C::BM - 1) / C::BM) * ((N + C::BN - 1) / C::BN);
-    hipLaunchKernelGGL((k_gemm<WGM, WGN, TM, TN, BK_, AMODE, EPI, OCC, X3>), dim3(T), dim3(C::THREADS), 0, st, a0, a1,
-                       w, ldw, wbytes, M, N, K, ep, wscale_inv);
+    if constexpr (X3)
+        hipLaunchKernelGGL((k_gemm3<WGM, WGN, TM, TN, BK_, AMODE, EPI, OCC>), dim3(T), dim3(C::THREADS), 0, st, a0, a1,
+                           reinterpret_cast<const _Float16*>(w), ldw, wbytes, M, N, K, ep, wscale_inv);
+    else
+        hipLaunchKernelGGL((k_gemm<WGM, WGN, TM, TN, BK_, AMODE, EPI, OCC>), dim3(T), dim3(C::THREADS), 0, st, a0, a1, w,
+                           ldw, wbytes, M, N, K, ep);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return gm_fail(GM_ERR_HIP, std::string("gm_gemm launch: ") + hipGetErrorString(e));
     return GM_OK;
@@ -541,7 +683,7 @@ int dispatch(const ASrc& s0, const ASrc& s1, const float* w, long long ldw, unsi
             return GM_L(2, 2, 2, 2, 16, GM_A_READOUT, EPI_BIAS);
         }
         if (s0.mode == GM_A_AGGREGATE) return GM_L(2, 2, 2, 2, 16, GM_A_AGGREGATE, EPI_BIAS);
-        if (n <= 32) return GM_L(4, 1, 1, 1, 16, GM_A_DENSE, EPI_BIAS);
+        if (n <= 32) return GM_L(1, 1, 1, 1, 16, GM_A_DENSE, EPI_BIAS);
         if (tile == 1) return GM_L(2, 2, 2, 4, 16, GM_A_DENSE, EPI_BIAS);
         if (tile == 2) return GM_L(2, 2, 2, 2, 32, GM_A_DENSE, EPI_BIAS);
         return GM_L(2, 2, 2, 2, 16, GM_A_DENSE, EPI_BIAS);
@@ -584,7 +726,7 @@ int gemm_entry(bool x3, const gm_a_src* a0, const gm_a_src* a1, const void* w, i
     const int K = s0.k + (a1 ? s1.k : 0);
     long long wb;
     if (x3) {
-        ldw = (long long)((K + BKMAX - 1) / BKMAX * BKMAX) / 16 * 96;  // packed row bytes
+        ldw = (long long)((K + BKMAX - 1) / BKMAX * BKMAX) / 16 * 64;  // packed row bytes
         wb = (long long)n * ldw;
     } else {
         if (ldw < K) return gm_fail(GM_ERR_INVALID_ARG, "gm_gemm_f32: ldw < K");
@@ -638,7 +780,7 @@ __global__ void k_absmax(const float* __restrict__ w, long long ldw, int n, int 
     }
 }
 
-// one thread per (row, 16-deep k block, element): packed[row][blk] = hi[16] | lo[16] | hi*2^-12 [16]
+// one thread per (row, 16-deep k block, element): packed[row][blk] = hi[16] | lo[16]
 __global__ void k_split_w(const float* __restrict__ w, long long ldw, int n, int k, int nblk,
                           _Float16* __restrict__ wp, const float* __restrict__ wsi) {
     const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -651,10 +793,9 @@ __global__ void k_split_w(const float* __restrict__ w, long long ldw, int n, int
     const float v = c < k ? w[(long long)r * ldw + c] * S : 0.f;
     const _Float16 hi = (_Float16)v;
     const _Float16 lo = (_Float16)(v - (float)hi);
-    _Float16* o = wp + rb * 48;
+    _Float16* o = wp + rb * 32;
     o[e] = hi;
     o[16 + e] = lo;
-    o[32 + e] = (_Float16)((float)hi * (1.0f / 4096.0f));
 }
 
 }  // namespace
@@ -674,7 +815,7 @@ extern "C" int gm_gemm_x3(const gm_a_src* a0, const gm_a_src* a1, const void* wp
 
 extern "C" int64_t gm_gemm_pack_x3_bytes(int32_t n, int32_t k) {
     if (n <= 0 || k <= 0) return 0;
-    return (int64_t)n * ((k + BKMAX - 1) / BKMAX * BKMAX / 16) * 96;
+    return (int64_t)n * ((k + BKMAX - 1) / BKMAX * BKMAX / 16) * 64;
 }
 
 extern "C" int gm_gemm_pack_x3(const float* w, int64_t ldw, int32_t n, int32_t k, void* wp, float* wscale_inv,

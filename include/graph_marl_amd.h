@@ -229,10 +229,10 @@ int gm_gemm_f32(const gm_a_src* src0, const gm_a_src* src1, const float* w, int6
 int gm_gemm_x3(const gm_a_src* src0, const gm_a_src* src1, const void* wp, const float* wscale_inv, const float* b,
                int32_t m, int32_t n, int32_t epilogue, float* y, int64_t ldy, float* y2, int64_t ldy2,
                const float* c_in, int64_t ldc, float* act_out, void* stream);
-/* Packed size in bytes of an [n][k] weight for gm_gemm_x3: n * ceil(k/32)*2 blocks * 96 B. */
+/* Packed size in bytes of an [n][k] weight for gm_gemm_x3: n * ceil(k/32)*2 blocks * 64 B. */
 int64_t gm_gemm_pack_x3_bytes(int32_t n, int32_t k);
 /* Split W [n][ldw] (first k columns) into wp (16-byte aligned, gm_gemm_pack_x3_bytes):
- * per row and 16-deep k block, 16 f16 hi, 16 f16 lo, 16 f16 hi*2^-12 of S*W, zero past k, with S = a
+ * per row and 16-deep k block, 16 f16 hi then 16 f16 lo of S*W, zero past k, with S = a
  * power of two that puts S*max|W| in [2^14, 2^15); writes 1/S to *wscale_inv (device).
  * Stream-ordered, no host sync. */
 int gm_gemm_pack_x3(const float* w, int64_t ldw, int32_t n, int32_t k, void* wp, float* wscale_inv, void* stream);
