@@ -48,6 +48,11 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-f32-compare", action="store_true",
                    help="skip the second timed pass with the exact-fp32 GEMM form (GM_GEMM=f32)")
+    p.add_argument("--no-train", action="store_true", help="skip the rollout + training measurement")
+    p.add_argument("--train-steps", type=int, default=5, help="timed vector steps of rollout + update")
+    p.add_argument("--train-batch", type=int, default=0,
+                   help="sequences per update (0: 32 * n_env / 10 = the reference replay ratio, SURVEY 8d)")
+    p.add_argument("--train-seq", type=int, default=8, help="sequence length of an update")
     p.add_argument("--cpu-envs", type=int, default=256)
     p.add_argument("--cpu-steps", type=int, default=20)
     return p.parse_args()
@@ -80,6 +85,75 @@ def kernel_cost(tag, n_env, N, A, E, x3=False):
     if kind == "egreedy":
         return "hbm", float(n_env * A * (16 + 4 + 12))
     return None, None
+
+
+def measure_train(args, gm, M, W, P, env, wenv, netmon, dqn, policy, dev, world):
+    """Rollout + DQN/NetMon training at the reference's replay ratio: every
+    vector step stores its n_env transitions in the device replay and runs one update of
+    B sequences x L steps (B = 32 n_env / 10: the paper's B=32, L=8 update every 10
+    env-steps, per env), with the gradient all-reduce across ranks (src/main.py:667-1026;
+    graph-marl_amd/train.py). Value = env-steps/s of the whole loop (all ranks)."""
+    import copy
+
+    import importlib as il
+
+    T = il.import_module("graph-marl_amd.train")
+    RB = il.import_module("graph-marl_amd.replaybuffer")
+    B = env.n_env
+    bsz = args.train_batch or max(1, (32 * B + 9) // 10)
+    L_ = args.train_seq
+    model_tar = copy.deepcopy(dqn)
+    params = list(dqn.parameters()) + list(netmon.parameters())
+    opt = torch.optim.AdamW(params, lr=1e-4)
+    T.broadcast_parameters([dqn, netmon])
+    slots = L_ + 8
+    buff = RB.ReplayBuffer(0, slots * B, B, env.n_data, env.obs_dim, env.n_nodes, env.node_obs_dim,
+                           netmon.get_state_size(), dev, nbr_width=env.nbr.shape[-1])
+    ep = {"n": 0}
+
+    def vstep(update):
+        if ep["n"] == 0:
+            wenv.reset()
+        buff.add_pre(env.obs, wenv.last_netmon_state, env.node_obs, env.nbr, env.agent_node)
+        with torch.no_grad():
+            act = policy.act(wenv)
+        wenv.step_(act)
+        ep["n"] += 1
+        done_ep = ep["n"] >= args.episode_steps
+        buff.add_post(act, env.reward, env.obs, env.done.bool(), done_ep, env.node_obs, env.agent_node)
+        if done_ep:
+            ep["n"] = 0
+        if update:
+            dqn.train()
+            netmon.train()
+            batches = list(buff.get_batch(bsz, sequence_length=L_))
+            T.dqn_update(netmon, dqn, model_tar, opt, params, batches, 0.98, 0.01)
+            dqn.eval()
+            netmon.eval()
+            netmon.state = None
+
+    for _ in range(L_ + 2):  # fill the replay past one sequence
+        vstep(False)
+    vstep(True)  # warm-up update
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.train_steps):
+        vstep(True)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    share = os.environ.get("GM_BENCH_SHARE_GPU") == "1"
+    t = torch.tensor([el], dtype=torch.float64, device="cpu" if share else dev)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    el = float(t.item())
+    return {"value": round(B * world * args.train_steps / el, 1), "unit": "env-steps/s",
+            "ms_per_step": round(1e3 * el / args.train_steps, 3), "steps": args.train_steps,
+            "update": {"sequences": bsz, "seq_len": L_, "graph_steps": bsz * L_,
+                       "per": "vector step of n_env envs (replay ratio 25.6 = reference B=32, L=8 every 10 steps)"}}
 
 
 def main():
@@ -192,6 +266,13 @@ def main():
                 kv["achieved"] = round(units / s / (1e9 if bound == "hbm" else 1e12), 2)
                 kv["unit"] = {"hbm": "GB/s", "mfma": "TFLOP/s f32", "mfma16": "TFLOP/s f16"}[bound]
 
+    train = None
+    if not args.no_train:
+        try:
+            train = measure_train(args, gm, M, W, P, env, wenv, netmon, dqn, policy, dev, world)
+        except Exception as ex:  # the training figure must never break the rollout line
+            train = {"value": None, "error": repr(ex)[:300]}
+
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         try:
@@ -220,7 +301,8 @@ def main():
                        "n_env_per_gpu": B, "n_nodes": N, "n_data": A, "netmon_iterations": K,
                        "gemm_form": L.GEMM_MODE,
                        "parallelism": f"dp{world} (env shards, no rollout collective)"},
-            "roofline": roof, "cpu_baseline": cpu, "f32_exact_gemms": f32cmp, "kernels": kernels,
+            "roofline": roof, "cpu_baseline": cpu, "f32_exact_gemms": f32cmp, "rollout_train": train,
+            "kernels": kernels,
         }
         print(json.dumps(line))
     if world > 1:

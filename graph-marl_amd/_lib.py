@@ -11,7 +11,7 @@ import os
 import torch  # noqa: F401  (must precede the HIP library load)
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "lib", "libgraphmarl_amd.so")
+LIB_PATH = os.environ.get("GM_LIB") or os.path.join(HERE, "lib", "libgraphmarl_amd.so")
 
 GM_OK = 0
 GM_INFO_FIELDS = 9
@@ -47,6 +47,7 @@ class EnvConfig(C.Structure):
         ("congestion", C.c_int32), ("action_mask", C.c_int32), ("ttl", C.c_int32), ("topo_mode", C.c_int32),
         ("topo_seed", C.c_int64), ("seed_list", C.POINTER(C.c_int64)), ("n_seed_list", C.c_int32),
         ("excluded", C.POINTER(C.c_int64)), ("n_excluded", C.c_int32), ("device", C.c_int32),
+        ("k", C.c_int32),
     ]
 
 

@@ -15,6 +15,7 @@ constexpr int MT_N = 624;
 constexpr int MT_M = 397;
 constexpr int MAX_NODES = 128;  // node-indexed work runs in lanes v = l, l + 64
 constexpr int MAX_AGENTS = 64;
+constexpr int MAX_KNBR = 8;     // neighbour slots of variant-2 observations
 constexpr int MAX_EDGES = MAX_NODES * 3 / 2;
 constexpr int RNG_BUF = 256;
 

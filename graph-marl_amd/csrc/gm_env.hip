@@ -47,6 +47,7 @@ int gm_fail(int code, const std::string& msg) {
 
 struct EnvDev {
     int n_env, N, A, E;
+    int env_var, k;  // observation variant (routing.py:268-358) and variant-2 neighbour count
     int cong, amask_on, ttl, topo_mode, n_list, n_excl, seq_stride;
     int64_t fixed_seed;
     const int64_t* list;
@@ -88,6 +89,7 @@ struct EnvLds {
     uint8_t nbr[NC * 3], nbr_edge[NC * 3];
     uint8_t ea[NC * 3 / 2], eb[NC * 3 / 2], elen[NC * 3 / 2];
     uint64_t nbrmask[NC][2];
+    int8_t kn[MAX_AGENTS][MAX_KNBR];  // variant 2: the first k packets on the same / an adjacent node
     float node_cnt[NC], node_load[NC];
     uint32_t rbuf[RNG_BUF];
     uint32_t rtmp[MT_N];
@@ -142,11 +144,27 @@ __device__ __forceinline__ void close_rng(const EnvDev& d, int env, MainRng& r) 
 // ---------------------------------------------------------------------------
 // Observation emission (routing.py:187-358, 522-539), packet state in LDS.
 // ---------------------------------------------------------------------------
+__host__ __device__ __forceinline__ int obs_dim_of(int N, int env_var, int k) {
+    return 6 * N + 10 + (env_var == 2 ? 5 * k : 0) + (env_var == 3 ? N * N + N * (4 * N + 8) : 0);
+}
+
+// node observation entry (routing.py:187-235) from the per-node packet count / size sums
+template <class ES>
+__device__ __forceinline__ float node_obs_value(const ES& s, int N, int j, int c) {
+    if (c < N) return (float)(c == j);
+    if (c == N) return s.node_cnt[j];
+    if (c == N + 1) return s.node_load[j];
+    int r = c - (N + 2), k = r / (N + 2), q = r - k * (N + 2);
+    if (q < N) return (float)(s.nbr[j * 3 + k] == q);
+    if (q == N) return (float)s.elen[s.nbr_edge[j * 3 + k]];
+    return (float)s.load[s.nbr_edge[j * 3 + k]];
+}
+
 template <class ES>
 __device__ void emit_obs(const EnvDev& d, int env, ES& s, const gm_obs_buffers& o) {
     const int l = lane_id();
     const int N = d.N, A = d.A;
-    if (o.node_obs) {
+    if (o.node_obs || (o.obs && d.env_var == 3)) {
         // packets waiting at node j (not on an edge) and the sum of their sizes in id order
         for (int v = l; v < N; v += WAVE) {
             int cnt = 0;
@@ -161,33 +179,53 @@ __device__ void emit_obs(const EnvDev& d, int env, ES& s, const gm_obs_buffers& 
             s.node_load[v] = (float)tl;
         }
         __syncthreads();
-        const int ND = 4 * N + 8;
-        float* base = o.node_obs + (size_t)env * N * ND;
-        for (int j = 0; j < N; j++) {
-            for (int c = l; c < ND; c += WAVE) {
-                float v;
-                if (c < N) v = (float)(c == j);
-                else if (c == N) v = s.node_cnt[j];
-                else if (c == N + 1) v = s.node_load[j];
-                else {
-                    int r = c - (N + 2), k = r / (N + 2), q = r - k * (N + 2);
-                    if (q < N) v = (float)(s.nbr[j * 3 + k] == q);
-                    else if (q == N) v = (float)s.elen[s.nbr_edge[j * 3 + k]];
-                    else v = (float)s.load[s.nbr_edge[j * 3 + k]];
-                }
-                base[(size_t)j * ND + c] = v;
-            }
+        if (o.node_obs) {
+            const int ND = 4 * N + 8;
+            float* base = o.node_obs + (size_t)env * N * ND;
+            for (int j = 0; j < N; j++)
+                for (int c = l; c < ND; c += WAVE) base[(size_t)j * ND + c] = node_obs_value(s, N, j, c);
         }
     }
+    if (o.obs && d.env_var == 2) {
+        // routing.py:317-342: packets j != a in id order on a's node or a neighbour; the
+        // first k contribute (now, target, edge, size, a) — the reference appends its own id
+        if (l < A) {
+            const int now = s.now[l];
+            int cnt = 0;
+            for (int j = 0; j < A && cnt < d.k; j++) {
+                if (j == l) continue;
+                const int nj = s.now[j];
+                if (nj == now || bit128(s.nbrmask[now], nj)) s.kn[l][cnt++] = (int8_t)j;
+            }
+            for (int q = cnt; q < d.k; q++) s.kn[l][q] = -1;
+        }
+        __syncthreads();
+    }
     if (o.obs) {
-        const int D = 6 * N + 10;
+        const int D1 = 6 * N + 10, D = obs_dim_of(N, d.env_var, d.k);
         float* base = o.obs + (size_t)env * A * o.obs_row_stride;
         for (int a = 0; a < A; a++) {
             const int now = s.now[a], e = s.edge[a];
             const int other = e >= 0 ? (s.ea[e] ^ s.eb[e] ^ now) : -1;
             for (int c = l; c < D; c += WAVE) {
                 float v;
-                if (c < N) v = (float)(c == now);
+                if (c >= D1) {
+                    const int g = c - D1;
+                    if (d.env_var == 2) {  // k neighbour slots of 5, -1 placeholders
+                        const int slot = g / 5, f = g - slot * 5, j = s.kn[a][slot];
+                        v = j < 0 ? -1.0f
+                                  : f == 0 ? (float)s.now[j]
+                                  : f == 1 ? (float)s.target[j]
+                                  : f == 2 ? (float)s.edge[j]
+                                  : f == 3 ? (float)s.size[j] : (float)a;
+                    } else if (g < N * N) {  // variant 3: I + A flattened, then node obs
+                        const int r = g / N, q = g - r * N;
+                        v = (float)(r == q || bit128(s.nbrmask[r], q));
+                    } else {
+                        const int ND = 4 * N + 8, h = g - N * N, j = h / ND;
+                        v = node_obs_value(s, N, j, h - j * ND);
+                    }
+                } else if (c < N) v = (float)(c == now);
                 else if (c < 2 * N) v = (float)(c - N == s.target[a]);
                 else if (c == 2 * N) v = (float)(e != -1);
                 else if (c < 3 * N + 1) v = (float)(c - (2 * N + 1) == other);
@@ -1077,7 +1115,9 @@ extern "C" int gm_env_create(const gm_env_config* cfg, const uint32_t* env_seeds
     if (N < 4 || N > MAX_NODES || (N % 2) != 0)
         return gm_fail(GM_ERR_INVALID_ARG, "n_nodes must be even and in [4, 128] (3-regular topology generator)");
     if (A < 1 || A > MAX_AGENTS) return gm_fail(GM_ERR_INVALID_ARG, "n_data must be in [1, 64]");
-    if (cfg->env_var != 1) return gm_fail(GM_ERR_UNSUPPORTED, "only env_var=1 (INDEPENDENT) is implemented");
+    if (cfg->env_var < 1 || cfg->env_var > 3) return gm_fail(GM_ERR_INVALID_ARG, "env_var must be 1, 2 or 3");
+    if (cfg->env_var == 2 && (cfg->k < 0 || cfg->k > MAX_KNBR))
+        return gm_fail(GM_ERR_INVALID_ARG, "k (variant-2 neighbours) must be in [0, 8]");
     if ((cfg->topo_mode == GM_TOPO_LIST || cfg->topo_mode == GM_TOPO_SEQUENTIAL) &&
         (cfg->n_seed_list <= 0 || !cfg->seed_list))
         return gm_fail(GM_ERR_INVALID_ARG, "seed list required for LIST/SEQUENTIAL topology mode");
@@ -1100,6 +1140,8 @@ extern "C" int gm_env_create(const gm_env_config* cfg, const uint32_t* env_seeds
     d.N = N;
     d.A = A;
     d.E = 3 * N / 2;
+    d.env_var = cfg->env_var;
+    d.k = cfg->env_var == 2 ? cfg->k : 0;
     d.cong = cfg->congestion != 0;
     d.amask_on = cfg->action_mask != 0;
     d.ttl = cfg->ttl;
@@ -1169,13 +1211,13 @@ extern "C" int gm_env_dims(const gm_env* env, int32_t* n_env, int32_t* n_nodes, 
     if (n_env) *n_env = env->d.n_env;
     if (n_nodes) *n_nodes = env->d.N;
     if (n_data) *n_data = env->d.A;
-    if (obs_dim) *obs_dim = 6 * env->d.N + 10;
+    if (obs_dim) *obs_dim = obs_dim_of(env->d.N, env->d.env_var, env->d.k);
     if (node_obs_dim) *node_obs_dim = 4 * env->d.N + 8;
     return GM_OK;
 }
 
 static int check_obs(const gm_env* env, const gm_obs_buffers* o) {
-    if (o && o->obs && o->obs_row_stride < 6 * env->d.N + 10)
+    if (o && o->obs && o->obs_row_stride < obs_dim_of(env->d.N, env->d.env_var, env->d.k))
         return gm_fail(GM_ERR_INVALID_ARG, "obs_row_stride smaller than the observation size");
     return GM_OK;
 }

@@ -35,6 +35,10 @@
 
 #include <cstring>
 #include <type_traits>
+
+#ifndef GM_DIAG
+#define GM_DIAG 0  // 1: no A split, 2: no loads/stores in the k loop, 3: as 2 without barriers
+#endif
 #include <string>
 
 #include "../../include/graph_marl_amd.h"
@@ -492,7 +496,12 @@ __global__ __launch_bounds__(WGM* WGN * 64, OCC) void k_gemm3(ASrc a0, ASrc a1, 
                 if (kk + 3 >= kend) v.w = 0.f;
             }
             half4 hi, lo;
+#if GM_DIAG == 1  // diagnostic build: raw bits instead of the split
+            hi = __builtin_bit_cast(half4, make_float2(v.x, v.y));
+            lo = __builtin_bit_cast(half4, make_float2(v.z, v.w));
+#else
             split4(v, hi, lo);
+#endif
             char* row = as + (rbase + q * RSTEP) * ROWB;
             *reinterpret_cast<half4*>(row) = hi;
             *reinterpret_cast<half4*>(row + 32) = lo;
@@ -550,10 +559,17 @@ __global__ __launch_bounds__(WGM* WGN * 64, OCC) void k_gemm3(ASrc a0, ASrc a1, 
     // is already in LDS) and stores tile kt+1 (set (kt+1)&1) into the other buffer
     auto step = [&](auto SET, int kt) {
         constexpr int S = decltype(SET)::value;
+#if GM_DIAG >= 2  // diagnostic builds only: no operand traffic inside the loop
+        compute(S);
+#if GM_DIAG == 2
+        __syncthreads();
+#endif
+#else
         if (kt + 2 < nk) gload(SET, (kt + 2) * BK);
         compute(S);
         if (kt + 1 < nk) lstore(std::integral_constant<int, S ^ 1>{}, S ^ 1, (kt + 1) * BK);
         __syncthreads();
+#endif
     };
     for (int kt = 0; kt < nk; kt += 2) {
         step(S0{}, kt);
@@ -650,16 +666,16 @@ int dispatch(const ASrc& s0, const ASrc& s1, const float* w, long long ldw, unsi
     if (epilogue == GM_EPI_LSTM) {
         ep.hidden = n / 4;
         if constexpr (X3) {
-            if (s0.mode == GM_A_DENSE) {
-                if (tile == 1) return GM_L(4, 1, 1, 4, 32, GM_A_DENSE, EPI_LSTM);
-                if (tile == 2) return GM_L(4, 1, 2, 4, 16, GM_A_DENSE, EPI_LSTM);
-                return GM_L(4, 1, 1, 4, 16, GM_A_DENSE, EPI_LSTM);
-            }
-            if (s0.mode == GM_A_AGGREGATE) {
-                if (tile == 1) return GM_L(4, 1, 1, 4, 32, GM_A_AGGREGATE, EPI_LSTM);
-                if (tile == 2) return GM_L(4, 1, 2, 4, 16, GM_A_AGGREGATE, EPI_LSTM);
-                return GM_L(4, 1, 1, 4, 16, GM_A_AGGREGATE, EPI_LSTM);
-            }
+            // 0: 128 rows x 4 gate tiles (4 waves of 32 rows); 1: 256 rows, 8 waves; 2: BK = 32
+#define GM_LSTM3(AM)                                          \
+    switch (tile) {                                           \
+        case 1: return GM_L(8, 1, 1, 4, 16, AM, EPI_LSTM);    \
+        case 2: return GM_L(4, 1, 1, 4, 32, AM, EPI_LSTM);    \
+        default: return GM_L(4, 1, 1, 4, 16, AM, EPI_LSTM);   \
+    }
+            if (s0.mode == GM_A_DENSE) GM_LSTM3(GM_A_DENSE)
+            if (s0.mode == GM_A_AGGREGATE) GM_LSTM3(GM_A_AGGREGATE)
+#undef GM_LSTM3
         } else {
             // default: 128x128x16 at 4 blocks/CU (<= 128 VGPRs, 40 KB LDS): +20 % over 2 blocks/CU
             if (s0.mode == GM_A_DENSE) {
@@ -677,16 +693,19 @@ int dispatch(const ASrc& s0, const ASrc& s1, const float* w, long long ldw, unsi
     }
     ep.act = epilogue == GM_EPI_BIAS_LEAKY ? 1 : 0;
     if constexpr (X3) {
-        if (s0.mode == GM_A_READOUT) {
-            if (tile == 1) return GM_L(2, 2, 2, 4, 16, GM_A_READOUT, EPI_BIAS);
-            if (tile == 2) return GM_L(2, 2, 2, 2, 32, GM_A_READOUT, EPI_BIAS);
-            return GM_L(2, 2, 2, 2, 16, GM_A_READOUT, EPI_BIAS);
-        }
-        if (s0.mode == GM_A_AGGREGATE) return GM_L(2, 2, 2, 2, 16, GM_A_AGGREGATE, EPI_BIAS);
+        // 0: 128x128 (4 waves of 64x64); 1: 128x256, 8 waves; 2: 256x128, 8 waves; 3: BK = 32
+#define GM_BIAS3(AM)                                          \
+    switch (tile) {                                           \
+        case 1: return GM_L(2, 4, 2, 2, 16, AM, EPI_BIAS);    \
+        case 2: return GM_L(4, 2, 2, 2, 16, AM, EPI_BIAS);    \
+        case 3: return GM_L(2, 2, 2, 2, 32, AM, EPI_BIAS);    \
+        default: return GM_L(2, 2, 2, 2, 16, AM, EPI_BIAS);   \
+    }
+        if (s0.mode == GM_A_READOUT) GM_BIAS3(GM_A_READOUT)
+        if (s0.mode == GM_A_AGGREGATE) GM_BIAS3(GM_A_AGGREGATE)
         if (n <= 32) return GM_L(1, 1, 1, 1, 16, GM_A_DENSE, EPI_BIAS);
-        if (tile == 1) return GM_L(2, 2, 2, 4, 16, GM_A_DENSE, EPI_BIAS);
-        if (tile == 2) return GM_L(2, 2, 2, 2, 32, GM_A_DENSE, EPI_BIAS);
-        return GM_L(2, 2, 2, 2, 16, GM_A_DENSE, EPI_BIAS);
+        GM_BIAS3(GM_A_DENSE)
+#undef GM_BIAS3
     } else {
     const int t = tile >= 0 ? tile : ((s0.mode == GM_A_READOUT || K <= 128 || n <= 128) ? 3 : 0);
     if (s0.mode == GM_A_READOUT) {

@@ -85,7 +85,9 @@ class Routing:
 
     :param network: topology configuration (`Network`)
     :param n_data: packets (agents) per env
-    :param env_var: environment variant; 1 (INDEPENDENT) is implemented
+    :param env_var: environment variant: 1 INDEPENDENT, 2 WITH_K_NEIGHBORS (+5k columns),
+        3 GLOBAL (+ flattened I+A and node observations)
+    :param k: neighbour slots of variant 2 (reference default 3)
     :param n_env: number of parallel graph instances
     :param seeds: per-env numpy-legacy seeds (default: seed + env index)
     :param obs_extra: extra zero columns reserved after each agent observation (the
@@ -112,7 +114,8 @@ class Routing:
         self.eval_info_enabled = False
         mode, tseed, lst = network.mode()
         cfg = L.EnvConfig()
-        cfg.n_env, cfg.n_nodes, cfg.n_data, cfg.env_var = n_env, network.n_nodes, n_data, env_var
+        cfg.n_env, cfg.n_nodes, cfg.n_data, cfg.env_var = n_env, network.n_nodes, n_data, int(env_var)
+        cfg.k = int(k)
         cfg.congestion, cfg.action_mask, cfg.ttl = int(enable_congestion), int(enable_action_mask), int(ttl)
         cfg.topo_mode, cfg.topo_seed = mode, int(tseed)
         self._keep = []
@@ -135,7 +138,9 @@ class Routing:
         self._h = h
         N, A = network.n_nodes, n_data
         self.n_nodes = N
-        self.obs_dim = 6 * N + 10
+        dims = [C.c_int32() for _ in range(5)]
+        L.check(L.lib().gm_env_dims(h, *[C.byref(x) for x in dims]))
+        self.obs_dim = dims[3].value  # 6N+10 (+5k variant 2, +N^2+N(4N+8) variant 3)
         self.node_obs_dim = 4 * N + 8
         self.obs_stride = ((self.obs_dim + obs_extra + 3) // 4) * 4
         dev = self.device

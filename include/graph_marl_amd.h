@@ -53,7 +53,7 @@ typedef struct {
     int32_t n_env;
     int32_t n_nodes;        /* --n-router, even, <= 64          */
     int32_t n_data;         /* --n-data (agents), <= 64          */
-    int32_t env_var;        /* --env-var; only 1 (INDEPENDENT)   */
+    int32_t env_var;        /* --env-var: 1 INDEPENDENT, 2 WITH_K_NEIGHBORS, 3 GLOBAL (routing.py:268-358) */
     int32_t congestion;     /* !--no-congestion                  */
     int32_t action_mask;    /* --action-mask                     */
     int32_t ttl;            /* --ttl (0 disables)                */
@@ -64,12 +64,14 @@ typedef struct {
     const int64_t* excluded;   /* host, seeds never used (EVAL_SEEDS); may be NULL */
     int32_t n_excluded;
     int32_t device;         /* HIP device ordinal                */
+    int32_t k;              /* env_var 2: neighbour slots per observation, 0..8 (reference default 3) */
 } gm_env_config;
 
 /* Optional observation outputs (any pointer may be NULL). */
 typedef struct {
-    float* obs;             /* [n_env, A, obs_row_stride]; columns [0, 6N+10) written     */
-    int64_t obs_row_stride; /* floats between agent rows (>= 6N+10; 6N+10+512 with NetMon) */
+    float* obs;             /* [n_env, A, obs_row_stride]; columns [0, obs_dim) written: 6N+10,
+                               +5k (env_var 2), +N^2+N(4N+8) (env_var 3) — gm_env_dims     */
+    int64_t obs_row_stride; /* floats between agent rows (>= obs_dim; obs_dim+512 with NetMon) */
     float* node_obs;        /* [n_env, N, 4N+8]                                           */
     int32_t* agent_node;    /* [n_env, A] node index of every agent (node-agent matrix)   */
     int8_t* agent_adj;      /* [n_env, A, A] agent adjacency                              */

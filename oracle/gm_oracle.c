@@ -274,6 +274,14 @@ static inline int vis_has(const uint64_t* v, int i) { return (int)((v[i >> 6] >>
 static inline void vis_add(uint64_t* v, int i) { v[i >> 6] |= 1ull << (i & 63); }
 
 int32_t gmo_obs_dim(int32_t n) { return 6 * n + 10; }
+/* routing.py:268-358: variant 2 appends k x (now, target, edge, size, own id) of the first k
+ * packets on the same or an adjacent node, variant 3 the flattened I+A and node observations */
+int32_t gmo_obs_dim_cfg(const gmo_config* c) {
+    int32_t n = c->n_nodes, d = 6 * n + 10;
+    if (c->env_var == 2) d += 5 * (c->k > 0 ? c->k : 0);
+    if (c->env_var == 3) d += n * n + n * (4 * n + 8);
+    return d;
+}
 int32_t gmo_node_obs_dim(int32_t n) { return 4 * n + 8; }
 size_t gmo_env_sizeof(void) { return sizeof(gmo_env); }
 
@@ -418,10 +426,49 @@ void gmo_env_final_delays(const gmo_env* e, double* out, int32_t* n_out) {
  *   node-agent  src/env/routing.py:256-267
  *   node aux    src/env/routing.py:237-254
  * Any output pointer may be NULL. */
+/* node observation rows (routing.py:187-235): one-hot id, packets waiting (not on an edge)
+ * and the sum of their sizes in id order, then per neighbour (ascending id) one-hot, length,
+ * load */
+static void node_obs_rows(const gmo_env* e, float* node_obs) {
+    const gmo_topo* t = &e->topo;
+    int n = t->n, A = e->cfg.n_data, ND = gmo_node_obs_dim(n);
+    for (int j = 0; j < n; j++) {
+        float* o = node_obs + (size_t)j * ND;
+        memset(o, 0, sizeof(float) * ND);
+        o[j] = 1.0f;
+        int np = 0;
+        double tl = 0.0;
+        for (int i = 0; i < A; i++)
+            if (e->now[i] == j && e->edge[i] == -1) {
+                np++;
+                tl += e->size[i];
+            }
+        o[n] = (float)np;
+        o[n + 1] = (float)tl;
+        for (int k = 0; k < 3; k++) {
+            int ed = t->node_edges[j][k];
+            float* ok = o + n + 2 + k * (n + 2);
+            ok[other_node(t, ed, j)] = 1.0f;
+            ok[n] = (float)t->edge_len[ed];
+            ok[n + 1] = (float)e->load[ed];
+        }
+    }
+}
+
 void gmo_env_observe(gmo_env* e, float* obs, float* node_obs, int8_t* adj, int8_t* node_agent, float* aux) {
     gmo_topo* t = &e->topo;
     int n = t->n, A = e->cfg.n_data;
-    int D = gmo_obs_dim(n), ND = gmo_node_obs_dim(n);
+    int D = gmo_obs_dim_cfg(&e->cfg), D1 = gmo_obs_dim(n), ND = gmo_node_obs_dim(n);
+    int var = e->cfg.env_var, K = e->cfg.k;
+    float* glob = NULL; /* variant 3: [I+A flattened | node obs flattened] (routing.py:271-274) */
+    if (obs && var == 3) {
+        glob = (float*)calloc((size_t)n * n + (size_t)n * ND, sizeof(float));
+        for (int j = 0; j < n; j++) {
+            glob[(size_t)j * n + j] = 1.0f;
+            for (int k = 0; k < t->deg[j]; k++) glob[(size_t)j * n + t->neighbors[j][k]] = 1.0f;
+        }
+        node_obs_rows(e, glob + (size_t)n * n);
+    }
     for (int i = 0; i < A; i++) {
         int now = e->now[i];
         if (obs) {
@@ -443,17 +490,32 @@ void gmo_env_observe(gmo_env* e, float* obs, float* node_obs, int8_t* adj, int8_
             }
         }
         /* neighbour list: self, then packets on the same or an adjacent node (routing.py:317-327) */
-        int cnt = 0;
+        int cnt = 0, kn = 0;
         e->neigh[i][cnt++] = (int16_t)i;
         for (int j = 0; j < A; j++) {
             if (j == i) continue;
             int nj = e->now[j];
             int adjacent = nj == now;
             for (int k = 0; k < t->deg[now]; k++) adjacent |= t->neighbors[now][k] == nj;
-            if (adjacent) e->neigh[i][cnt++] = (int16_t)j;
+            if (adjacent) {
+                e->neigh[i][cnt++] = (int16_t)j;
+                if (obs && var == 2 && kn < K) { /* routing.py:329-338 (appends its own id) */
+                    float* ok = obs + (size_t)i * D + D1 + 5 * kn;
+                    ok[0] = (float)e->now[j];
+                    ok[1] = (float)e->target[j];
+                    ok[2] = (float)e->edge[j];
+                    ok[3] = (float)e->size[j];
+                    ok[4] = (float)i;
+                    kn++;
+                }
+            }
         }
+        if (obs && var == 2)
+            for (int q = 5 * kn; q < 5 * K; q++) obs[(size_t)i * D + D1 + q] = -1.0f; /* placeholders (340-342) */
+        if (obs && var == 3) memcpy(obs + (size_t)i * D + D1, glob, sizeof(float) * (size_t)(D - D1));
         e->neigh_cnt[i] = cnt;
     }
+    free(glob);
     if (adj) {
         memset(adj, 0, (size_t)A * A);
         for (int i = 0; i < A; i++) {
@@ -461,29 +523,7 @@ void gmo_env_observe(gmo_env* e, float* obs, float* node_obs, int8_t* adj, int8_
             for (int q = 0; q < e->neigh_cnt[i]; q++) adj[(size_t)i * A + e->neigh[i][q]] = 1;
         }
     }
-    if (node_obs) {
-        for (int j = 0; j < n; j++) {
-            float* o = node_obs + (size_t)j * ND;
-            memset(o, 0, sizeof(float) * ND);
-            o[j] = 1.0f;
-            int np = 0;
-            double tl = 0.0;
-            for (int i = 0; i < A; i++)
-                if (e->now[i] == j && e->edge[i] == -1) {
-                    np++;
-                    tl += e->size[i];
-                }
-            o[n] = (float)np;
-            o[n + 1] = (float)tl;
-            for (int k = 0; k < 3; k++) {
-                int ed = t->node_edges[j][k];
-                float* ok = o + n + 2 + k * (n + 2);
-                ok[other_node(t, ed, j)] = 1.0f;
-                ok[n] = (float)t->edge_len[ed];
-                ok[n + 1] = (float)e->load[ed];
-            }
-        }
-    }
+    if (node_obs) node_obs_rows(e, node_obs);
     if (node_agent) {
         memset(node_agent, 0, (size_t)n * A);
         for (int a = 0; a < A; a++) node_agent[(size_t)e->now[a] * A + a] = 1;

@@ -52,6 +52,8 @@ typedef struct {
     int32_t n_seed_list;
     const int64_t* excluded;       /* sorted ascending, may be NULL */
     int32_t n_excluded;
+    int32_t env_var;               /* 1 INDEPENDENT, 2 WITH_K_NEIGHBORS, 3 GLOBAL (0 = 1) */
+    int32_t k;                     /* neighbours in variant-2 observations (routing.py:59, default 3) */
 } gmo_config;
 
 typedef struct {
@@ -90,6 +92,8 @@ void gmo_env_step(gmo_env* e, const int32_t* act, float* reward, uint8_t* done, 
 void gmo_env_observe(gmo_env* e, float* obs, float* node_obs, int8_t* adj, int8_t* node_agent, float* aux);
 void gmo_env_final_delays(const gmo_env* e, double* out, int32_t* n_out);
 int32_t gmo_obs_dim(int32_t n);
+/* agent observation width of a configuration: 6N+10 (+5k for variant 2, +N^2+N(4N+8) for 3) */
+int32_t gmo_obs_dim_cfg(const gmo_config* c);
 int32_t gmo_node_obs_dim(int32_t n);
 size_t gmo_env_sizeof(void);
 

@@ -60,6 +60,7 @@ class Config(C.Structure):
         ("topo_mode", C.c_int32), ("topo_seed", C.c_int64),
         ("seed_list", C.POINTER(C.c_int64)), ("n_seed_list", C.c_int32),
         ("excluded", C.POINTER(C.c_int64)), ("n_excluded", C.c_int32),
+        ("env_var", C.c_int32), ("k", C.c_int32),
     ]
 
 
@@ -99,6 +100,7 @@ def lib():
         L.gmo_mt_random.restype = C.c_double
         L.gmo_mt_randint.argtypes = [C.POINTER(MT), C.c_int64]
         L.gmo_mt_randint.restype = C.c_int64
+        L.gmo_obs_dim_cfg.argtypes = [C.POINTER(Config)]
         L.gmo_create_valid.argtypes = [C.POINTER(Topo), C.POINTER(Config), C.POINTER(MT), C.c_int32]
         L.gmo_create_valid.restype = C.c_int64
         L.gmo_build_seed_list.argtypes = [C.c_int32, C.c_int64, C.c_int32, C.POINTER(C.c_int64), C.c_int32,
@@ -140,9 +142,10 @@ class MTStream:
 
 
 def make_config(n_nodes, n_data, congestion=True, action_mask=False, ttl=0, topo_mode=TOPO_FIXED,
-                topo_seed=476, seed_list=None, excluded=None):
+                topo_seed=476, seed_list=None, excluded=None, env_var=1, k=3):
     cfg = Config()
     cfg.n_nodes, cfg.n_data = n_nodes, n_data
+    cfg.env_var, cfg.k = int(env_var), int(k)
     cfg.congestion, cfg.action_mask, cfg.ttl = int(congestion), int(action_mask), int(ttl)
     cfg.topo_mode, cfg.topo_seed = topo_mode, topo_seed
     keep = []
@@ -218,9 +221,12 @@ class OracleEnv:
         )
         return rew, done.astype(bool), inf
 
+    def obs_dim(self):
+        return lib().gmo_obs_dim_cfg(C.byref(self.cfg))
+
     def observe(self):
         n, A = self.n, self.A
-        obs = np.zeros((A, 6 * n + 10), np.float32)
+        obs = np.zeros((A, self.obs_dim()), np.float32)
         nobs = np.zeros((n, 4 * n + 8), np.float32)
         adj = np.zeros((A, A), np.int8)
         na = np.zeros((n, A), np.int8)

@@ -176,15 +176,20 @@ ENV_CONFIGS = [
     dict(name="evalseq", n=20, a=20, mode="sequential", topo=476, cong=True, mask=False, ttl=0, seed=4, T=100, ep=20, eps=None),
     dict(name="egreedy_rand20", n=20, a=20, mode="random", topo=476, cong=True, mask=False, ttl=0, seed=11, T=150, ep=50, eps=0.3),
     dict(name="fixed476_a1", n=20, a=1, mode="fixed", topo=476, cong=True, mask=False, ttl=0, seed=13, T=60, ep=60, eps=None),
+    # observation variants 2 (k neighbours) and 3 (global), src/env/routing.py:268-358
+    dict(name="fixed476_var2", n=20, a=20, mode="fixed", topo=476, cong=True, mask=False, ttl=0, seed=17, T=80, ep=40, eps=None, var=2),
+    dict(name="rand10_var3", n=10, a=12, mode="random", topo=476, cong=True, mask=False, ttl=0, seed=19, T=60, ep=20, eps=None, var=3),
 ]
 FULL_STEPS = (0, 1, 2, 3, 26, 52)  # snapshot indices with full arrays
 
 
-def gen_env(out_dir, Network, Routing, EVAL_SEEDS):
+def gen_env(out_dir, Network, Routing, EVAL_SEEDS, names=None):
     """Per config: a snapshot stream. Snapshot 0 is the initial reset; then every
     env.step(t) appends a snapshot, and an episode reset (episode_steps reached)
     appends another snapshot with kind=1 right after the step's snapshot."""
     for cfg in ENV_CONFIGS:
+        if names and cfg["name"] not in names:
+            continue
         n, a = cfg["n"], cfg["a"]
         if cfg["mode"] == "fixed":
             net = Network(n_nodes=n, random_topology=False, topology_init_seed=cfg["topo"])
@@ -196,7 +201,8 @@ def gen_env(out_dir, Network, Routing, EVAL_SEEDS):
             net = Network(n_nodes=n, random_topology=True, provided_seeds=list(EVAL_SEEDS[:8]), sequential_topology_seeds=True)
         else:
             raise ValueError(cfg["mode"])
-        env = Routing(net, a, 1, enable_congestion=cfg["cong"], enable_action_mask=cfg["mask"], ttl=cfg["ttl"])
+        env = Routing(net, a, cfg.get("var", 1), enable_congestion=cfg["cong"], enable_action_mask=cfg["mask"],
+                      ttl=cfg["ttl"])
         tape_rng = np.random.RandomState(1000 + cfg["seed"])
         np.random.seed(cfg["seed"])
         snap_keys = ["kind", "step", "now", "target", "edge", "time", "ttl", "size", "start", "spw", "visited",
@@ -724,6 +730,8 @@ def main():
         gen_topology(os.path.join(HERE, "topology.npz"), Network, EVAL_SEEDS)
     if only is None or "env" in only:
         gen_env(HERE, Network, Routing, EVAL_SEEDS)
+    elif any(o.startswith("env:") for o in only):  # --only env:name1,env:name2
+        gen_env(HERE, Network, Routing, EVAL_SEEDS, {o[4:] for o in only if o.startswith("env:")})
     if only is None or "netmon" in only:
         gen_netmon(os.path.join(HERE, "netmon.npz"), Network, Routing, EVAL_SEEDS, NetMon, DQN)
     if only is None or "train" in only:

@@ -27,7 +27,8 @@ class DeviceAdapter:
         else:
             net = gm.Network(n, random_topology=True, provided_seeds=[int(s) for s in lst],
                              sequential_topology_seeds=True)
-        self.env = gm.Routing(net, a, 1, enable_congestion=bool(cfg["cong"]), enable_action_mask=bool(cfg["mask"]),
+        self.env = gm.Routing(net, a, int(cfg.get("var", 1)), enable_congestion=bool(cfg["cong"]),
+                              enable_action_mask=bool(cfg["mask"]),
                               ttl=int(cfg["ttl"]), n_env=n_env, seed=int(cfg["seed"]))
         self.gm = gm
         self.A = a
@@ -97,11 +98,11 @@ def test_build_seed_list_reproduces_eval_seeds(gm):
     np.testing.assert_array_equal(np.array(got), np.load(f"{R.GOLDEN}/eval_seeds.npy"))
 
 
-def _oracle_env(oracle_mod, n, a, mode, topo_seed, seed, cong=True, mask=False, ttl=0, lst=None):
+def _oracle_env(oracle_mod, n, a, mode, topo_seed, seed, cong=True, mask=False, ttl=0, lst=None, var=1, k=3):
     O = oracle_mod
     m = {"fixed": O.TOPO_FIXED, "random": O.TOPO_RANDOM, "list": O.TOPO_LIST, "sequential": O.TOPO_SEQUENTIAL}[mode]
     c = O.make_config(n, a, cong, mask, ttl, m, topo_seed, seed_list=lst,
-                      excluded=R.EVAL_SEEDS if mode in ("random", "list") else None)
+                      excluded=R.EVAL_SEEDS if mode in ("random", "list") else None, env_var=var, k=k)
     e = O.OracleEnv(c, seed)
     e._cfg_keep = c
     return e
@@ -117,19 +118,28 @@ BATCH_CASES = [
     (4, 1, "random", True, False, 0, 16, 40, 20),
     (100, 20, "random", True, False, 0, 8, 60, 30),
     (128, 64, "random", True, True, 16, 4, 40, 20),
+    # observation variants: (env_var, k) as an optional 10th element
+    (20, 20, "random", True, False, 0, 16, 60, 30, (2, 3)),
+    (12, 40, "random", True, False, 0, 8, 40, 20, (2, 8)),
+    (20, 20, "fixed", True, False, 0, 8, 40, 20, (2, 0)),
+    (10, 12, "random", True, False, 0, 8, 40, 20, (3, 3)),
+    (64, 8, "random", True, False, 0, 4, 20, 10, (3, 3)),
 ]
 
 
-@pytest.mark.parametrize("case", BATCH_CASES, ids=lambda c: f"n{c[0]}a{c[1]}{c[2]}e{c[6]}")
+@pytest.mark.parametrize("case", BATCH_CASES,
+                         ids=lambda c: f"n{c[0]}a{c[1]}{c[2]}e{c[6]}" + (f"v{c[9][0]}k{c[9][1]}" if len(c) > 9 else ""))
 def test_batch_vs_oracle(gm, oracle_mod, case):
-    n, a, mode, cong, mask, ttl, B, T, ep = case
+    n, a, mode, cong, mask, ttl, B, T, ep = case[:9]
+    var, k = case[9] if len(case) > 9 else (1, 3)
     if mode == "fixed":
         net = gm.Network(n, random_topology=False, topology_init_seed=476)
     else:
         net = gm.Network(n, random_topology=True, excluded_seeds=gm.EVAL_SEEDS)
     seeds = [(7919 * b + 17) & 0xFFFFFFFF for b in range(B)]
-    env = gm.Routing(net, a, 1, enable_congestion=cong, enable_action_mask=mask, ttl=ttl, n_env=B, seeds=seeds)
-    orc = [_oracle_env(oracle_mod, n, a, mode, 476, s, cong, mask, ttl) for s in seeds]
+    env = gm.Routing(net, a, var, k=k, enable_congestion=cong, enable_action_mask=mask, ttl=ttl, n_env=B, seeds=seeds)
+    orc = [_oracle_env(oracle_mod, n, a, mode, 476, s, cong, mask, ttl, var=var, k=k) for s in seeds]
+    assert env.obs_dim == orc[0].obs_dim()
     rng = np.random.RandomState(123)
     env.reset_()
     for o in orc:

@@ -87,7 +87,8 @@ class OracleAdapter:
              "sequential": O.TOPO_SEQUENTIAL}[mode]
         self.c = O.make_config(int(cfg["n"]), int(cfg["a"]), bool(cfg["cong"]), bool(cfg["mask"]), int(cfg["ttl"]),
                                m, seed, seed_list=lst,
-                               excluded=R.EVAL_SEEDS if mode in ("random", "list") else None)
+                               excluded=R.EVAL_SEEDS if mode in ("random", "list") else None,
+                               env_var=int(cfg.get("var", 1)))
         self.env = O.OracleEnv(self.c, int(cfg["seed"]))
 
     def reset(self):

@@ -28,7 +28,7 @@ for s in "$@"; do
         dist2) GM_BENCH_SHARE_GPU=1 step dist2 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
                 --master-addr 127.0.0.1 --master-port 29511 bench.py --gpus 2 --steps 20 --warmup 5 \
                 --no-cpu-baseline || exit $? ;;
-        gemm) step gemm 300 python tools/gemm_bench.py || exit $? ;;
+        gemm) X3_TILES=${X3_TILES:--1,1,2,3,4,5} step gemm 300 python tools/gemm_bench.py || exit $? ;;
         fused) step fused_tests 600 python -m pytest tests/test_fused_gpu.py -x -q --tb=short --timeout=300 -p no:cacheprovider || exit $? ;;
         benchf32) GM_GEMM=f32 step bench_f32 300 python bench.py --no-cpu-baseline --steps 100 || exit $? ;;
         bench) step bench 600 python bench.py || exit $? ;;
