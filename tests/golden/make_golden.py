@@ -396,6 +396,66 @@ def gen_netmon(out, Network, Routing, EVAL_SEEDS, NetMon, DQN):
     np.savez_compressed(out, **d)
 
 
+def gen_models(out, Network, Routing, EVAL_SEEDS, DGN, DQNR, CommNet):
+    """DGN / DQNR / CommNet forwards (src/model.py:45-184, 653-794) on real routing agent
+    observations and agent adjacency: Q, attention weights, recurrent agent states over a
+    3-step sequence (state carried, done agents reset like src/main.py:712-716)."""
+    import torch
+    import torch.nn.functional as F
+
+    d = {}
+    n, a, B, steps = 20, 20, 4, 3
+    obs_l, adj_l, done_l = [], [], []
+    envs = []
+    for b in range(B):
+        net = Network(n_nodes=n, random_topology=True, topology_init_seed=476, excluded_seeds=EVAL_SEEDS)
+        env = Routing(net, a, 1)
+        np.random.seed(300 + b)
+        envs.append((env, env.reset()))
+    rs = np.random.RandomState(5)
+    for t in range(steps):
+        ob, ad, dn = [], [], []
+        for b, (env, (o, g)) in enumerate(envs):
+            ob.append(o.astype(np.float32))
+            ad.append(g.astype(np.float32))
+            o2, g2, r, done, _ = env.step(rs.randint(4, size=a))
+            dn.append(done)
+            envs[b] = (env, (o2, g2))
+        obs_l.append(np.stack(ob))
+        adj_l.append(np.stack(ad))
+        done_l.append(np.stack(dn))
+    d["obs"], d["adj"], d["done"] = np.stack(obs_l), np.stack(adj_l), np.stack(done_l).astype(np.int8)
+    D = d["obs"].shape[-1]
+    models = [
+        ("dgn", lambda: DGN(D, [512, 256], 4, 8, 2, F.leaky_relu)),
+        ("dgn_small", lambda: DGN(D, [64], 4, 3, 1, F.leaky_relu)),
+        ("dqnr", lambda: DQNR(D, [128, 64], 4, F.leaky_relu)),
+        ("commnet", lambda: CommNet(D, [128, 64], 4, 2, F.leaky_relu)),
+    ]
+    for mi, (name, make) in enumerate(models):
+        torch.manual_seed(70 + mi)
+        m = make()
+        m.eval()
+        sd_to_npz(f"{name}_w_", m.state_dict(), d)
+        last_state = None
+        with torch.no_grad():
+            for t in range(steps):
+                if hasattr(m, "state"):
+                    m.state = last_state
+                    if last_state is not None:
+                        d[f"{name}_statein_{t}"] = last_state.numpy().copy()
+                q = m(torch.tensor(d["obs"][t]), torch.tensor(d["adj"][t]))
+                d[f"{name}_q_{t}"] = q.numpy()
+                if hasattr(m, "att_weights"):
+                    for li, w in enumerate(m.att_weights):
+                        d[f"{name}_att{li}_{t}"] = w.numpy()
+                if hasattr(m, "state"):
+                    d[f"{name}_state_{t}"] = m.state.numpy().copy()
+                    last_state = m.state * ~torch.tensor(d["done"][t], dtype=torch.bool).view(B, -1, 1)
+    np.savez_compressed(out, **d)
+    print("models done", flush=True)
+
+
 def gen_train(out, Network, Routing, EVAL_SEEDS, NetMon, DQN, interpolate_model):
     """One DQN+NetMon update exactly as src/main.py:832-1022 performs it (sequence replay)."""
     import torch
@@ -715,7 +775,7 @@ def main():
     from env.network import Network  # noqa: E402
     from env.routing import Routing  # noqa: E402
     from env.constants import EVAL_SEEDS  # noqa: E402
-    from model import NetMon, DQN  # noqa: E402
+    from model import NetMon, DQN, DGN, DQNR, CommNet  # noqa: E402
     from util import interpolate_model  # noqa: E402
     from env.simple_environment import SimpleEnvironment  # noqa: E402
     from policy import ShortestPath  # noqa: E402
@@ -734,6 +794,8 @@ def main():
         gen_env(HERE, Network, Routing, EVAL_SEEDS, {o[4:] for o in only if o.startswith("env:")})
     if only is None or "netmon" in only:
         gen_netmon(os.path.join(HERE, "netmon.npz"), Network, Routing, EVAL_SEEDS, NetMon, DQN)
+    if only is None or "models" in only:
+        gen_models(os.path.join(HERE, "models.npz"), Network, Routing, EVAL_SEEDS, DGN, DQNR, CommNet)
     if only is None or "train" in only:
         gen_train(os.path.join(HERE, "train.npz"), Network, Routing, EVAL_SEEDS, NetMon, DQN, interpolate_model)
     if only is None or "shortest" in only:

@@ -5,6 +5,8 @@ The golden files were produced by importing the reference (tests/golden/make_gol
 import numpy as np
 import pytest
 
+import os
+
 import golden_replay as R
 import netmon_ref
 
@@ -164,3 +166,28 @@ def test_train_golden_forward_matches_restatement():
         tot += ((q - qt) ** 2).mean() / L
         state = ns * (1 - g["episode_done"][t])[:, None, None]
     np.testing.assert_allclose(tot, g["loss"].item(), rtol=1e-6)
+
+
+@pytest.mark.parametrize("name", ["dgn", "dgn_small", "dqnr", "commnet"])
+def test_agent_model_restatement_matches_reference(name):
+    """oracle/models_ref.py (fp64) vs the reference's DGN / DQNR / CommNet forwards."""
+    import models_ref as MR
+
+    g = np.load(os.path.join(R.GOLDEN, "models.npz"))
+    W = {k[len(name) + 3:]: g[k].astype(np.float64) for k in g.files if k.startswith(name + "_w_")}
+    state = None
+    for t in range(3):
+        x, adj = g["obs"][t].astype(np.float64), g["adj"][t].astype(np.float64)
+        if name.startswith("dgn"):
+            heads = g[f"{name}_att0_{t}"].shape[1]
+            q, atts = MR.dgn(W, x, adj, heads)
+            for li, w in enumerate(atts):
+                np.testing.assert_allclose(w, g[f"{name}_att{li}_{t}"], atol=5e-6, rtol=0)
+        else:
+            if t > 0:
+                np.testing.assert_allclose(state, g[f"{name}_statein_{t}"], atol=5e-6, rtol=0)
+            f = MR.dqnr if name == "dqnr" else (lambda W, x, s: MR.commnet(W, x, adj, s))
+            q, st = f(W, x, state)
+            np.testing.assert_allclose(st, g[f"{name}_state_{t}"], atol=5e-6, rtol=0)
+            state = st * (1 - g["done"][t][..., None])
+        np.testing.assert_allclose(q, g[f"{name}_q_{t}"], atol=5e-6, rtol=0)
