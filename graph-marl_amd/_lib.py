@@ -30,7 +30,7 @@ EXPORTS = [
     "gm_gemm_set_tile", "gm_simple_create", "gm_simple_destroy", "gm_simple_reset", "gm_simple_step",
     "gm_simple_observe", "gm_simple_policy_egreedy", "gm_simple_get_state", "gm_env_set_topology",
     "gm_policy_shortest_path", "gm_env_first_hops", "gm_routing_node_encoder", "gm_gemm_x3",
-    "gm_gemm_pack_x3", "gm_gemm_pack_x3_bytes",
+    "gm_gemm_pack_x3", "gm_gemm_pack_x3_bytes", "gm_agent_attention", "gm_agent_comm",
 ]
 
 # Arithmetic form of the fused rollout GEMMs (graph-marl_amd/fused.py): "x3" = split-f16
@@ -105,6 +105,8 @@ def lib():
     L.gm_env_set_topology.argtypes = [vp, i32, i64, vp, i32, i32]
     L.gm_policy_shortest_path.argtypes = [vp, vp, vp]
     L.gm_env_first_hops.argtypes = [vp, vp, vp]
+    L.gm_agent_attention.argtypes = [vp, vp, vp, i64, vp, i32, i32, i32, i32, i32, vp, i64, vp, vp]
+    L.gm_agent_comm.argtypes = [vp, i64, vp, i32, i32, i32, vp, i64, vp]
     L.gm_gemm_pack_x3_bytes.argtypes = [i32, i32]
     L.gm_gemm_pack_x3_bytes.restype = i64
     L.gm_gemm_pack_x3.argtypes = [vp, i64, i32, i32, vp, vp, vp]

@@ -39,6 +39,8 @@ def evaluate(env, policy, episodes, steps_per_episode, disable_progressbar=True,
         active = torch.arange(n_env, device=dev) < (episodes - r * n_env)
         w = active.to(torch.float64)
         env.reset()
+        if hasattr(policy, "reset"):  # recurrent agent models start every episode from zeros
+            policy.reset(True)
         if hasattr(policy, "reset_episode"):
             policy.reset_episode()
         for step in range(steps_per_episode):
@@ -55,6 +57,8 @@ def evaluate(env, policy, episodes, steps_per_episode, disable_progressbar=True,
                     for k in L.EVAL_KEYS:
                         add(k, (info[k] * w).sum())
             add("steps", w.sum())
+            if hasattr(policy, "reset"):  # reset done agents (src/eval.py:111-113)
+                policy.reset(done)
     if hasattr(env, "set_eval_info"):
         env.set_eval_info(False)
     h = {k: float(v.item()) for k, v in acc.items()}

@@ -180,6 +180,61 @@ def _linear(x, ldx, k, lin, out):
     return out
 
 
+def linear_rows(lin, x, ldx, M, out, ldo, k=None):
+    """out rows (stride ldo) = act(x rows (stride ldx, first k = in_features columns) @ W^T + b)."""
+    k = lin.in_features if k is None else k
+    wp, ldw = lin._wc.get(lin.weight)
+    gemm(dense(x.data_ptr(), ldx, k), None, wp.data_ptr(), ldw, lin.bias.data_ptr(), M, lin.out_features,
+         GM_EPI_BIAS_LEAKY if lin.act == 1 else GM_EPI_BIAS, out.data_ptr(), ldo,
+         tag=lin.tag and f"linear:{lin.tag}:{M}x{lin.out_features}x{k}", x3=pack_x3(lin))
+    return out
+
+
+def mlp_rows(mlp, x, ldx, k, M, scratch, out=None, ldo=None):
+    """MLP over strided rows; the last layer writes into `out` (stride ldo) when given.
+    Rows whose stride or base is not 16-byte aligned are first copied into a padded buffer."""
+    if ldx % 4 or x.data_ptr() % 16:
+        xp = scratch(("mlp_in", id(mlp)), M, (k + 3) // 4 * 4)
+        xp[:, :k].copy_(torch.as_strided(x, (M, k), (ldx, 1)))
+        x, ldx = xp, xp.stride(0)
+    h, ld, kk = x, ldx, k
+    layers = list(mlp.linear_layers)
+    for i, lin in enumerate(layers):
+        if i == len(layers) - 1 and out is not None:
+            dst, ldd = out, ldo
+        else:
+            dst = scratch(("mlp", id(mlp), i), M, lin.out_features)
+            ldd = dst.stride(0)
+        linear_rows(lin, h, ld, M, dst, ldd, k=kk)
+        h, ld, kk = dst, ldd, lin.out_features
+    return h
+
+
+class _CatLinear:
+    """Row-concatenation of Linears with the same input and activation (one GEMM)."""
+
+    def __init__(self, linears):
+        from .model import _WeightCache
+
+        with torch.no_grad():
+            self.weight = torch.cat([l.weight for l in linears], 0).contiguous()
+            self.bias = torch.cat([l.bias for l in linears], 0).contiguous()
+        self.act = linears[0].act
+        assert all(l.act == self.act for l in linears)
+        self.in_features = linears[0].in_features
+        self.out_features = self.weight.shape[0]
+        self._wc = _WeightCache()
+        self.tag = linears[0].tag and linears[0].tag.rsplit(".", 1)[0] + ".fc_vkq"
+
+
+def concat_linears(owner, linears):
+    """Cached _CatLinear of `linears` (rebuilt when a parameter changes)."""
+    if not hasattr(owner, "_packed_cat"):
+        owner._packed_cat = Packed()
+    key = tuple(x for l in linears for x in _key(l.weight, l.bias)) + (L.GEMM_MODE,)
+    return owner._packed_cat.get(key, lambda: _CatLinear(linears))
+
+
 def routing_encoder_ok(lin, N, Fd, nbr):
     """The routing node-obs layout (4N+8 columns, degree-3 neighbour table) lets the first
     encoder layer run as a 12-column gather (gm_routing_node_encoder)."""

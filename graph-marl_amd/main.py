@@ -19,7 +19,7 @@ Differences from the reference, by design:
     consumes exactly the reference's numpy stream); one update per vector step;
   * no tensorboard: the log lines go to stdout and checkpoints / eval metrics to
     --log-dir (default runs/<date>_<host><comment>, like SummaryWriter's logdir);
-  * models: dqn (DGN / DQNR / CommNet are not built); activation: leaky_relu only;
+  * models: dqn, dgn, dqnr, commnet (comm_rounds 2); activation: leaky_relu only;
     NetMon: sum/mean aggregation, lstm/lnlstm/gru cells, carry-over on, no --netmon-global.
 """
 import argparse
@@ -234,6 +234,20 @@ class Logger:
         return float(h.get("reward", 0.0)) / max(self.steps, 1), out
 
 
+def build_model(args, agent_obs_size, n_actions):
+    """src/main.py:486-523"""
+    hidden = dim_str_to_list(args.hidden_dim)
+    if args.model == "dgn":
+        return M.DGN(agent_obs_size, hidden, n_actions, args.num_heads, args.num_attention_layers)
+    if args.model == "dqnr":
+        return M.DQNR(agent_obs_size, hidden, n_actions)
+    if args.model == "commnet":
+        return M.CommNet(agent_obs_size, hidden, n_actions, comm_rounds=2)
+    if args.model == "dqn":
+        return M.DQN(agent_obs_size, hidden, n_actions)
+    raise ValueError(f"Unknown model type {args.model}")
+
+
 def make_env(args, dev, obs_extra):
     if args.env_type == "routing":
         network = gm.Network(n_nodes=args.n_router, random_topology=bool(args.random_topology),
@@ -243,7 +257,7 @@ def make_env(args, dev, obs_extra):
         return gm.Routing(network, args.n_data, args.env_var, enable_congestion=not args.no_congestion,
                           enable_action_mask=args.enable_action_mask, ttl=args.ttl, n_env=args.n_env,
                           seeds=[(args.seed + b) & 0xFFFFFFFF for b in range(args.n_env)], obs_extra=obs_extra,
-                          agent_adjacency=False, device=dev.index)
+                          agent_adjacency=args.model in ("dgn", "commnet"), device=dev.index)
     if args.env_type == "simple":
         return S.SimpleEnvironment(args.env_var, bool(args.random_topology), n_env=args.n_env,
                                    seeds=[(args.seed + b) & 0xFFFFFFFF for b in range(args.n_env)],
@@ -268,8 +282,6 @@ def main(argv=None):
     set_seed(args.seed)
     if args.sequence_length <= 0:
         raise ValueError(f"Invalid sequence length {args.sequence_length}. Must be greater 0.")
-    if args.model != "dqn" and args.policy == "trained":
-        raise NotImplementedError(f"--model={args.model}: only dqn is built (DGN/DQNR/CommNet are not)")
     if args.activation_function != "leaky_relu":
         raise NotImplementedError("only --activation-function=leaky_relu is built")
 
@@ -292,8 +304,8 @@ def main(argv=None):
         agent_obs_size = env.obs_dim
     base = env.get()
     model = model_tar = None
-    if args.model == "dqn":
-        model = M.DQN(agent_obs_size, dim_str_to_list(args.hidden_dim), base.action_space.n).to(dev)
+    if args.policy == "trained" or args.model_load_path:
+        model = build_model(args, agent_obs_size, base.action_space.n).to(dev)
         if args.model_load_path:
             load_state_dict(load_checkpoint(args.model_load_path), model, netmon)
         model_tar = copy.deepcopy(model)
@@ -324,10 +336,15 @@ def main(argv=None):
     assert args.policy == "trained", f"Given policy {args.policy} cannot be used for training."
     params = list(model.parameters()) + ([] if netmon is None else list(netmon.parameters()))
     optimizer = torch.optim.AdamW(params, lr=args.lr)
+    has_state = hasattr(model, "state")
+    needs_adj = args.model in ("dgn", "commnet")
     buff = RB.ReplayBuffer(args.seed, int(args.capacity), base.n_env, n_agents, base.obs_dim, n_nodes,
                            node_obs_size, node_state_size, dev, half_precision=args.replay_half_precision,
-                           nbr_width=base.nbr.shape[-1])
-    comment = "_" + (f"R{args.env_var}" if args.env_type == "routing" else "Simple") + "_DQN"
+                           nbr_width=base.nbr.shape[-1] if hasattr(base, "nbr") else 3,
+                           agent_state_size=model.get_state_len() if has_state else 0, store_adj=needs_adj)
+    last_state = None
+    comment = "_" + (f"R{args.env_var}" if args.env_type == "routing" else "Simple") + "_" + \
+        {"dqn": "DQN", "dgn": "DGN", "dqnr": "DQNR", "commnet": "CommNet"}[args.model]
     if netmon is not None:
         comment += "_netmon"
     if args.comment:
@@ -354,18 +371,26 @@ def main(argv=None):
                 episode_step = 0
                 env.reset()
                 current_episode += 1
+                last_state = None  # src/main.py:683-686
+            if has_state:
+                model.state = last_state
+            adj = base.agent_adj if needs_adj else None
             if netmon is not None:
-                buff.add_pre(base.obs, env.last_netmon_state, base.node_obs, base.nbr, base.agent_node)
+                buff.add_pre(base.obs, env.last_netmon_state, base.node_obs, base.nbr, base.agent_node, adj=adj,
+                             agent_state=last_state)
             else:
-                buff.add_pre(base.obs)
+                buff.add_pre(base.obs, adj=adj, agent_state=last_state)
             with torch.no_grad():
                 actions = policy.act(env)
             env.step_(actions)
+            if has_state:  # done agents restart from a zero state (src/main.py:710-716)
+                last_state = model.state * ~base.done.bool().unsqueeze(-1)
             episode_step += 1
             episode_done = episode_step >= args.episode_steps
             buff.add_post(actions, base.reward, base.obs, base.done.bool(), episode_done,
                           base.node_obs if netmon is not None else None,
-                          base.agent_node if netmon is not None else None)
+                          base.agent_node if netmon is not None else None,
+                          next_adj=base.agent_adj if needs_adj else None)
             info_sum = None
             if isinstance(base, gm.Routing):
                 info_sum = base.info.sum(0)
@@ -396,7 +421,8 @@ def main(argv=None):
                 netmon.train()
             batches = list(buff.get_batch(args.mini_batch_size, sequence_length=args.sequence_length))
             loss, qs, qts = T.dqn_update(netmon, model, model_tar, optimizer, params, batches, args.gamma, args.tau,
-                                         args.target_update_steps, iteration)
+                                         args.target_update_steps, iteration,
+                                         att_coeff=args.att_regularization_coeff if args.model == "dgn" else 0.0)
             model.eval()
             if netmon is not None:
                 netmon.eval()

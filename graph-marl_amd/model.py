@@ -453,7 +453,7 @@ class DQN(nn.Module):
     def forward(self, x, mask=None):
         return self.q_net(self.encoder(x))
 
-    def forward_rows(self, x2d, ldx, k, scratch):
+    def forward_rows(self, x2d, ldx, k, scratch, **unused):
         """no-grad fast path: q [rows, actions] from a strided observation buffer."""
         h = self.encoder.forward_into(x2d, ldx, k, scratch)
         out = scratch(len(self.encoder.linear_layers), x2d.shape[0], self.q_net.fc.out_features)
@@ -466,3 +466,230 @@ def tag_modules(root, prefix=""):
     for name, m in root.named_modules():
         if isinstance(m, (Linear, LSTMCell)):
             m.tag = prefix + name
+
+
+# ---------------------------------------------------------------------------
+# Agent models of the reference besides DQN: DGN (agent attention), DQNR (recurrent
+# DQN), CommNet (recurrent + masked mean communication), src/model.py:45-184, 653-794.
+# forward(x, mask) is the reference signature (autograd; the GEMMs on the MFMA kernels,
+# the small A x A attention / communication in torch). forward_rows() is the no-grad
+# rollout path: fused GEMMs + gm_agent_attention / gm_agent_comm, no A x A tensors in torch.
+# ---------------------------------------------------------------------------
+def _adj_i8(mask):
+    return mask.contiguous() if mask.dtype == torch.int8 else (mask != 0).to(torch.int8).contiguous()
+
+
+class AttModel(nn.Module):
+    """src/model.py:45-117: v/k/q = act(linear(x)) per head, softmax(q k^T / sqrt(dk))
+    masked by the agent adjacency (-1e9), att v + v, heads concatenated, act(fc_out).
+    forward returns (out, att_weights) with the weights before masking, like the reference."""
+
+    def __init__(self, in_features, k_features, v_features, out_features, num_heads):
+        super().__init__()
+        self.k_features, self.v_features, self.num_heads = k_features, v_features, num_heads
+        self.fc_v = Linear(in_features, v_features * num_heads, act=1)
+        self.fc_k = Linear(in_features, k_features * num_heads, act=1)
+        self.fc_q = Linear(in_features, k_features * num_heads, act=1)
+        self.fc_out = Linear(v_features * num_heads, out_features, act=1)
+        self.attention_scale = 1 / (k_features ** 0.5)
+
+    def forward(self, x, mask):
+        B, A = x.shape[0], x.shape[1]
+        nh = self.num_heads
+        v = self.fc_v(x).view(B, A, nh, self.v_features).transpose(1, 2)
+        q = self.fc_q(x).view(B, A, nh, self.k_features).transpose(1, 2)
+        k = self.fc_k(x).view(B, A, nh, self.k_features).transpose(1, 2)
+        att_weights = torch.matmul(q, k.transpose(2, 3)) * self.attention_scale
+        att = F.softmax(att_weights.masked_fill(mask.unsqueeze(1) == 0, -1e9), dim=-1)
+        out = (torch.matmul(att, v) + v).transpose(1, 2).contiguous().view(B, A, -1)
+        return self.fc_out(out), att_weights
+
+    def forward_rows(self, x2d, ldx, adj, B, A, out, ldo, scratch, att_weights=None):
+        """no-grad: rows [B*A] of x (stride ldx) -> out rows (stride ldo) via one q/k/v GEMM,
+        gm_agent_attention and the fc_out GEMM."""
+        from . import fused as FU
+
+        M = B * A
+        nh, dk, dv = self.num_heads, self.k_features, self.v_features
+        qkv = scratch(("qkv", id(self)), M, nh * (dv + 2 * dk))
+        FU.linear_rows(FU.concat_linears(self, (self.fc_v, self.fc_k, self.fc_q)), x2d, ldx, M, qkv, qkv.stride(0))
+        core = scratch(("att", id(self)), M, nh * dv)
+        vo, ko, qo = 0, nh * dv, nh * (dv + dk)
+        L.check(L.lib().gm_agent_attention(
+            qkv.data_ptr() + 4 * qo, qkv.data_ptr() + 4 * ko, qkv.data_ptr() + 4 * vo, qkv.stride(0), L.ptr(adj), B, A,
+            nh, dk, dv, L.ptr(core), core.stride(0), L.ptr(att_weights), _s()))
+        FU.linear_rows(self.fc_out, core, core.stride(0), M, out, ldo)
+        return out
+
+
+class DGN(nn.Module):
+    """src/model.py:120-176 "Graph Convolutional Reinforcement Learning": MLP encoder,
+    num_attention_layers AttModel layers (dk = dv = 16), Q head on the concatenation of
+    the encoder output and every attention layer's output. att_weights holds the
+    per-layer weights of the last forward (attention regularisation, src/main.py:924-954)."""
+
+    def __init__(self, in_features, mlp_units, num_actions, num_heads=8, num_attention_layers=2):
+        super().__init__()
+        self.encoder = MLP(in_features, mlp_units)
+        hidden = self.encoder.out_features
+        self.att_layers = nn.ModuleList(
+            [AttModel(hidden, 16, 16, hidden, num_heads) for _ in range(num_attention_layers)])
+        self.q_net = Q_Net(hidden * (num_attention_layers + 1), num_actions)
+        self.att_weights = []
+
+    def forward(self, x, mask):
+        h = self.encoder(x)
+        q_input = h
+        self.att_weights.clear()
+        for layer in self.att_layers:
+            if torch.is_grad_enabled() or x.shape[1] > 64:
+                h, w = layer(h, mask)
+            else:  # no-grad: the HIP attention core (weights recorded for the regulariser)
+                B, A, Hd = h.shape
+                w = torch.empty(B, layer.num_heads, A, A, device=x.device)
+                o = torch.empty(B * A, layer.fc_out.out_features, device=x.device)
+                hr = h.reshape(B * A, Hd).contiguous()
+                layer.forward_rows(hr, hr.stride(0), _adj_i8(mask), B, A, o, o.stride(0), _scratch_dict({}), w)
+                h = o.view(B, A, -1)
+            self.att_weights.append(w)
+            q_input = torch.cat((q_input, h), dim=-1)
+        return self.q_net(q_input)
+
+    def forward_rows(self, x2d, ldx, k, scratch, adj=None, B=None, A=None):
+        """no-grad rollout path: encoder, attention layers and Q head over a strided
+        observation buffer; [h_enc | h_1 | ...] are written side by side (no concat)."""
+        from . import fused as FU
+
+        M = x2d.shape[0]
+        hid = self.encoder.out_features
+        nl = len(self.att_layers)
+        qin = scratch(("dgn_qin", id(self)), M, hid * (nl + 1))
+        FU.mlp_rows(self.encoder, x2d, ldx, k, M, scratch, out=qin, ldo=qin.stride(0))
+        for li, layer in enumerate(self.att_layers):
+            layer.forward_rows(qin[:, li * hid:], qin.stride(0), adj, B, A, qin[:, (li + 1) * hid:], qin.stride(0),
+                               scratch)
+        out = scratch(("dgn_q", id(self)), M, self.q_net.fc.out_features)
+        FU.linear_rows(self.q_net.fc, qin, qin.stride(0), M, out, out.stride(0))
+        return out
+
+
+def _scratch_dict(d):
+    def get(key, m, n):
+        b = d.get((key, m, n))
+        if b is None:
+            b = torch.empty(m, n, device="cuda")
+            d[(key, m, n)] = b
+        return b
+    return get
+
+
+class DQNR(nn.Module):
+    """src/model.py:653-744: MLP encoder, LSTMCell over the encoding with a carried agent
+    state, Q head. `state` is [B, A, 2H] ([h | c] per agent) or None (= zeros) between
+    calls, like the reference's external layout (_state_reshape_out)."""
+
+    def __init__(self, in_features, mlp_units, num_actions):
+        super().__init__()
+        self.encoder = MLP(in_features, mlp_units)
+        H = self.encoder.out_features
+        self.lstm = LSTMCell(H, H)
+        self.state = None
+        self.q_net = Q_Net(H, num_actions)
+
+    def get_state_len(self):
+        return 2 * self.lstm.hidden_size
+
+    def _split(self, B, A):
+        H = self.lstm.hidden_size
+        if self.state is None:
+            z = torch.zeros(B * A, H, device=self.lstm.weight_ih.device)
+            return z, z
+        st = self.state.reshape(B * A, 2, H)
+        return st[:, 0], st[:, 1]
+
+    def _step(self, x, h, c, B, A):
+        h1, c1 = self.lstm(x, (h.contiguous(), c.contiguous()))
+        return h1, c1
+
+    def forward(self, x, mask=None):
+        B, A, _ = x.shape
+        h = self.encoder(x).reshape(B * A, -1)
+        hs, cs = self._split(B, A)
+        h1, c1 = self._step(h, hs, cs, B, A)
+        self.state = torch.stack((h1, c1), 1).reshape(B, A, -1)
+        return self.q_net(h1.view(B, A, -1))
+
+    def _lstm_rows(self, x, ldx, S_in, S_out, M):
+        """fused LSTM GEMM: S_out = [h' | c'] rows from x rows and S_in = [h | c] rows."""
+        from . import fused as FU
+
+        H = self.lstm.hidden_size
+        wp, ldw, bp, x3 = FU.pack_lstm(self.lstm)
+        FU.gemm(FU.dense(x.data_ptr(), ldx, H), FU.dense(S_in.data_ptr(), S_in.stride(0), H), wp.data_ptr(), ldw,
+                bp.data_ptr(), M, 4 * H, FU.GM_EPI_LSTM, S_out.data_ptr(), S_out.stride(0),
+                S_out.data_ptr() + 4 * H, S_out.stride(0), S_in.data_ptr() + 4 * H, S_in.stride(0),
+                tag=self.lstm.tag and f"lstm:{self.lstm.tag}:{M}x{4 * H}x{2 * H}", x3=x3)
+
+    def _state_rows(self, B, A, M):
+        if self.state is None:
+            return torch.zeros(M, 2 * self.lstm.hidden_size, device=self.lstm.weight_ih.device)
+        return self.state.reshape(M, -1).contiguous()
+
+    def forward_rows(self, x2d, ldx, k, scratch, adj=None, B=None, A=None):
+        from . import fused as FU
+
+        M = x2d.shape[0]
+        h = FU.mlp_rows(self.encoder, x2d, ldx, k, M, scratch)
+        S = torch.empty(M, 2 * self.lstm.hidden_size, device=x2d.device)
+        self._lstm_rows(h, h.stride(0), self._state_rows(B, A, M), S, M)
+        self.state = S.view(B, A, -1)
+        out = scratch(("q", id(self)), M, self.q_net.fc.out_features)
+        FU.linear_rows(self.q_net.fc, S, S.stride(0), M, out, out.stride(0), k=self.lstm.hidden_size)
+        return out
+
+
+class CommNet(DQNR):
+    """src/model.py:747-794: DQNR whose hidden state is, for comm_rounds rounds, added to
+    the mean of the other adjacent agents' hidden states (self excluded, count clamped to
+    1) and fed through the LSTM again as both input and hidden state (cell states are not
+    communicated, as in IC3Net)."""
+
+    def __init__(self, in_features, mlp_units, num_actions, comm_rounds=2):
+        super().__init__(in_features, mlp_units, num_actions)
+        assert comm_rounds >= 0
+        self.comm_rounds = comm_rounds
+
+    def forward(self, x, mask):
+        B, A, _ = x.shape
+        h = self.encoder(x).reshape(B * A, -1)
+        hs, cs = self._split(B, A)
+        h, c = self._step(h, hs, cs, B, A)
+        m = (mask != 0).float() * ~torch.eye(A, dtype=torch.bool, device=x.device).unsqueeze(0)
+        cnt = torch.clamp(m.sum(dim=-1).unsqueeze(-1), min=1)
+        for _ in range(self.comm_rounds):
+            hv = h.view(B, A, -1)
+            hv = hv + torch.bmm(m, hv) / cnt
+            h = hv.reshape(B * A, -1)
+            h, c = self._step(h, h, c, B, A)
+        self.state = torch.stack((h, c), 1).reshape(B, A, -1)
+        return self.q_net(h.view(B, A, -1))
+
+    def forward_rows(self, x2d, ldx, k, scratch, adj=None, B=None, A=None):
+        from . import fused as FU
+
+        M = x2d.shape[0]
+        H = self.lstm.hidden_size
+        h = FU.mlp_rows(self.encoder, x2d, ldx, k, M, scratch)
+        S = torch.empty(M, 2 * H, device=x2d.device)
+        self._lstm_rows(h, h.stride(0), self._state_rows(B, A, M), S, M)
+        for _ in range(self.comm_rounds):
+            hc = torch.empty(M, 2 * H, device=x2d.device)  # [h + comm | c]
+            L.check(L.lib().gm_agent_comm(L.ptr(S), S.stride(0), L.ptr(adj), B, A, H, L.ptr(hc), hc.stride(0), _s()))
+            hc[:, H:].copy_(S[:, H:])
+            S2 = torch.empty(M, 2 * H, device=x2d.device)
+            self._lstm_rows(hc, hc.stride(0), hc, S2, M)
+            S = S2
+        self.state = S.view(B, A, -1)
+        out = scratch(("q", id(self)), M, self.q_net.fc.out_features)
+        FU.linear_rows(self.q_net.fc, S, S.stride(0), M, out, out.stride(0), k=H)
+        return out

@@ -1,6 +1,6 @@
 """ε-greedy action selection on the device (reference src/policy.py:7-87 EpsilonGreedy).
 
-Q-values come from the DQN on the HIP linear kernels; the random draws
+Q-values come from the agent model (DQN, DGN, DQNR, CommNet) on the HIP kernels; the random draws
 (randint(n_actions, size=A) then rand(A), every call, from each env's numpy-legacy
 stream) and the argmax/mix run in the env's egreedy kernel (gm_policy_egreedy /
 gm_simple_policy_egreedy).
@@ -35,13 +35,19 @@ class EpsilonGreedy:
             self._scratch[key] = b
         return b
 
-    def q_values(self, obs):
-        """q [n_env, A, 4] for a joint observation view [n_env, A, D] (strided rows ok)."""
+    def q_values(self, obs, adj=None):
+        """q [n_env, A, 4] for a joint observation view [n_env, A, D] (strided rows ok); adj:
+        agent adjacency [n_env, A, A] for DGN / CommNet (default: the env's)."""
         e = self._env
         with torch.no_grad():
             x2 = obs.reshape(-1, obs.shape[-1])
+            if adj is None:
+                adj = getattr(e, "agent_adj", None)
+            if adj is not None and adj.dtype != torch.int8:
+                adj = (adj != 0).to(torch.int8)
             # rows are spaced by the agent-dim stride (reshape may renormalise size-1 dims)
-            q = self._model.forward_rows(x2, obs.stride(-2), obs.shape[-1], self._buf)
+            q = self._model.forward_rows(x2, obs.stride(-2), obs.shape[-1], self._buf, adj=adj, B=e.n_env,
+                                         A=e.n_data)
         return q.view(e.n_env, e.n_data, -1)
 
     def select(self, q):
@@ -54,7 +60,7 @@ class EpsilonGreedy:
             self._epsilon = max(self._epsilon * self._decay, 0.01)
 
     def __call__(self, obs, adj=None):
-        actions = self.select(self.q_values(obs))
+        actions = self.select(self.q_values(obs, adj))
         self._decay_step()
         return actions
 
@@ -62,8 +68,9 @@ class EpsilonGreedy:
         """Fast path for a fused NetMonWrapper: the DQN's first GEMM gathers the NetMon
         readout from the node state tables instead of reading a materialised joint obs."""
         from . import fused as FU
+        from .model import DQN
 
-        if not getattr(wenv, "fused", False):
+        if not getattr(wenv, "fused", False) or not isinstance(self._model, DQN):
             return self(wenv.obs)
         e = wenv.env
         q = FU.dqn_q(self._model, e.obs_buf, e.obs_dim, wenv.current_netmon_state, wenv.h_prev, e.nbr,
@@ -71,6 +78,14 @@ class EpsilonGreedy:
         actions = self.select(q.view(e.n_env, e.n_data, -1))
         self._decay_step()
         return actions
+
+    def reset(self, agents_to_reset):
+        """src/policy.py:72-82: zero the recurrent agent state of the given agents
+        ([n_env, A] bool, or True for all)."""
+        st = getattr(self._model, "state", None)
+        if st is not None:
+            m = torch.as_tensor(agents_to_reset, device=st.device).bool()
+            self._model.state = st * ~(m.unsqueeze(-1) if m.dim() else m)
 
     def eval(self):
         self._eps_tmp = self._epsilon

@@ -20,15 +20,18 @@ import torch
 TransitionBatch = namedtuple(
     "TransitionBatch",
     ["idx", "obs", "action", "reward", "next_obs", "done", "episode_done", "node_obs", "nbr", "node_state",
-     "agent_node", "next_node_obs", "next_agent_node"],
+     "agent_node", "next_node_obs", "next_agent_node", "adj", "next_adj", "agent_state"],
+    defaults=(None, None, None),
 )
 
 
 class ReplayBuffer:
     def __init__(self, seed, capacity, n_env, n_agents, obs_dim, n_nodes, node_obs_dim, node_state_size,
-                 device, half_precision=False, nbr_width=3):
+                 device, half_precision=False, nbr_width=3, agent_state_size=0, store_adj=False):
         """capacity: transitions (env-steps) like the reference; the ring holds
-        ceil(capacity / n_env) vector steps."""
+        ceil(capacity / n_env) vector steps. agent_state_size > 0 stores the recurrent
+        models' agent state (DQNR / CommNet), store_adj the agent adjacency (DGN / CommNet),
+        src/replaybuffer.py:64-99."""
         self.n_env, self.A, self.N = n_env, n_agents, n_nodes
         self.slots = max(1, -(-int(capacity) // n_env))
         self.capacity = self.slots * n_env
@@ -55,17 +58,28 @@ class ReplayBuffer:
             self.agent_node = z(S, B, A, dtype=torch.int8)
             self.next_agent_node = z(S, B, A, dtype=torch.int8)
             self.node_state = z(S, B, N, node_state_size)
+        self.agent_state = z(S, B, A, agent_state_size) if agent_state_size > 0 else None
+        self.adj = z(S, B, A, A, dtype=torch.bool) if store_adj else None
+        self.next_adj = z(S, B, A, A, dtype=torch.bool) if store_adj else None
         self.gen = torch.Generator(device=device)
         self.gen.manual_seed(seed)
 
     def nbytes(self):
         return sum(t.numel() * t.element_size() for t in self.__dict__.values() if torch.is_tensor(t))
 
-    def add_pre(self, obs, node_state=None, node_obs=None, nbr=None, agent_node=None):
+    def add_pre(self, obs, node_state=None, node_obs=None, nbr=None, agent_node=None, adj=None, agent_state=None):
         """First half of a transition, recorded before the env step: the observation and the
-        NetMon inputs that produced it (node_state = the NetMon state before that call)."""
+        NetMon inputs that produced it (node_state = the NetMon state before that call), the
+        agent adjacency and the agent state the model starts the step from (None = zeros)."""
         i = self.index
         self.obs[i].copy_(obs)
+        if self.adj is not None:
+            self.adj[i].copy_(adj != 0)
+        if self.agent_state is not None:
+            if agent_state is None:
+                self.agent_state[i].zero_()
+            else:
+                self.agent_state[i].copy_(agent_state)
         if self.graph:
             if node_state is None:
                 self.node_state[i].zero_()
@@ -75,9 +89,12 @@ class ReplayBuffer:
             self.nbr[i].copy_(nbr)
             self.agent_node[i].copy_(agent_node)
 
-    def add_post(self, action, reward, next_obs, done, episode_done, next_node_obs=None, next_agent_node=None):
+    def add_post(self, action, reward, next_obs, done, episode_done, next_node_obs=None, next_agent_node=None,
+                 next_adj=None):
         """Second half, after the step; commits the slot."""
         i = self.index
+        if self.next_adj is not None:
+            self.next_adj[i].copy_(next_adj != 0)
         self.action[i].copy_(action)
         self.reward[i].copy_(reward)
         self.next_obs[i].copy_(next_obs)
@@ -107,6 +124,9 @@ class ReplayBuffer:
             self.agent_node[slot, env].int().contiguous() if g else None,
             self.next_node_obs[slot, env].to(f) if g else None,
             self.next_agent_node[slot, env].int().contiguous() if g else None,
+            self.adj[slot, env].to(f) if self.adj is not None else None,
+            self.next_adj[slot, env].to(f) if self.next_adj is not None else None,
+            self.agent_state[slot, env].to(f) if self.agent_state is not None else None,
         )
 
     def get_batch(self, batch_size, sequence_length=1):

@@ -1,7 +1,8 @@
 """DQN + NetMon update on the device (reference src/main.py:819-1026) and the
 data-parallel gradient exchange across GPUs.
 
-Per update: for each step of the sampled sequence, NetMon re-runs with gradient
+Models: DQN, DGN (+ attention regularisation), DQNR, CommNet (agent state carried over
+the sequence). Per update: for each step of the sampled sequence, NetMon re-runs with gradient
 from the stored input state (reset on episode boundaries), its readout replaces
 the graph part of the observation, the online DQN gives Q, the target DQN (online
 NetMon, no grad) gives max Q of the next observation, the TD target is written
@@ -13,6 +14,7 @@ clips and steps on the global gradient and the replicas stay identical.
 """
 import torch
 import torch.distributed as dist
+import torch.nn.functional as F
 
 
 def allreduce_gradients(params, group=None):
@@ -57,45 +59,72 @@ def joint_obs(env_obs, network_obs):
     return torch.cat([env_obs, network_obs], -1)
 
 
-def dqn_loss(netmon, model, model_tar, batches, gamma):
-    """Sequence loss of src/main.py:840-954 (no DGN attention / aux terms); netmon may be None.
-    Returns (loss, list of q, list of q_target)."""
+def attention_kl(att_weights, tar_att_weights, done):
+    """DGN attention regularisation (src/main.py:924-954): KL(softmax(target weights) ||
+    softmax(online weights)) per source agent, summed over layers, heads and destination
+    agents, averaged over the agents that are not done."""
+    attention = F.log_softmax(torch.stack(att_weights), dim=-1)
+    target_attention = F.softmax(torch.stack(tar_att_weights), dim=-1)
+    shape = attention.shape  # (layers, batch, heads, agents, agents)
+    n = shape[-1]
+    kl = F.kl_div(attention.reshape(-1, n), target_attention.reshape(-1, n), reduction="none").view(shape)
+    kl = kl.transpose(0, -2).transpose(0, 1).sum(dim=(-1, -2, -3))
+    return (kl * ~done).sum() / torch.clamp((~done).sum(), min=1)
+
+
+def dqn_loss(netmon, model, model_tar, batches, gamma, att_coeff=0.0):
+    """Sequence loss of src/main.py:840-960 for DQN / DGN / DQNR / CommNet (no aux term);
+    netmon may be None. Recurrent models start from the stored agent state, the target
+    model runs from the online model's next state, and the state is reset for done agents
+    and at episode ends. Returns (loss, list of q, list of q_target)."""
     L = len(batches)
-    loss_q = None
+    has_state = hasattr(model, "state")
+    loss_q = loss_att = None
     qs, qts = [], []
     last_state = last_ep_done = None
     for t, batch in enumerate(batches):
+        if has_state and t == 0:
+            model.state = batch.agent_state
         if netmon is None:
-            q = model(batch.obs)
-            with torch.no_grad():
-                next_q_max = model_tar(batch.next_obs).max(dim=2)[0]
+            obs, next_obs = batch.obs, batch.next_obs
         else:
             if t == 0:
                 netmon.state = batch.node_state
             else:
                 netmon.state = last_state * (~last_ep_done).view(-1, 1, 1)
-            network_obs = netmon.forward_graph(batch.node_obs, batch.nbr, batch.agent_node)
-            obs = joint_obs(batch.obs, network_obs)
+            obs = joint_obs(batch.obs, netmon.forward_graph(batch.node_obs, batch.nbr, batch.agent_node))
             last_state = netmon.state
             last_ep_done = batch.episode_done.expand(batch.obs.shape[0]) if batch.episode_done.dim() == 0 \
                 else batch.episode_done
-            q = model(obs)
-            with torch.no_grad():
+            next_obs = None
+        q = model(obs, batch.adj)
+        with torch.no_grad():
+            if has_state:
+                model_tar.state = model.state.detach()
+            if netmon is not None:
                 nno = netmon.forward_graph(batch.next_node_obs, batch.nbr, batch.next_agent_node)
-                next_q = model_tar(joint_obs(batch.next_obs, nno))
-                next_q_max = next_q.max(dim=2)[0]
+                next_obs = joint_obs(batch.next_obs, nno)
+            next_q_max = model_tar(next_obs, batch.next_adj).max(dim=2)[0]
+        if has_state:
+            ep = batch.episode_done.expand(batch.obs.shape[0]) if batch.episode_done.dim() == 0 \
+                else batch.episode_done
+            model.state = model.state * (~batch.done * (~ep).view(-1, 1)).unsqueeze(-1)
         target = batch.reward + (~batch.done) * gamma * next_q_max
         q_target = torch.scatter(q.detach(), -1, batch.action.unsqueeze(-1), target.unsqueeze(-1))
         term = torch.mean((q - q_target).pow(2)) / L
         loss_q = term if loss_q is None else loss_q + term
+        if att_coeff > 0 and hasattr(model, "att_weights"):
+            kl = attention_kl(model.att_weights, model_tar.att_weights, batch.done) / L
+            loss_att = kl if loss_att is None else loss_att + kl
         qs.append(q)
         qts.append(q_target)
-    return loss_q, qs, qts
+    loss = loss_q if loss_att is None else loss_q + att_coeff * loss_att
+    return loss, qs, qts
 
 
 def dqn_update(netmon, model, model_tar, optimizer, params, batches, gamma, tau, target_update_steps=0,
-               iteration=1, group=None):
-    loss, qs, qts = dqn_loss(netmon, model, model_tar, batches, gamma)
+               iteration=1, group=None, att_coeff=0.0):
+    loss, qs, qts = dqn_loss(netmon, model, model_tar, batches, gamma, att_coeff)
     optimizer.zero_grad(set_to_none=False)
     loss.backward()
     allreduce_gradients(params, group)

@@ -22,6 +22,8 @@
  *   gm_linear_f32                    nn.Linear (+ leaky_relu of MLP)        src/model.py:13-42, 119-125
  *   gm_gemm_f32                      Linear / LSTMCell GEMMs with aggregate, readout and gate math fused
  *   gm_gemm_x3 / gm_gemm_pack_x3     the same GEMMs in split-f16 form (f16 MFMA, fp32 accumulate)
+ *   gm_agent_attention               AttModel attention core (DGN)          src/model.py:86-117
+ *   gm_agent_comm                    CommNet communication step             src/model.py:780-787
  */
 #ifndef GRAPH_MARL_AMD_H
 #define GRAPH_MARL_AMD_H
@@ -247,6 +249,20 @@ int gm_gemm_pack_x3(const float* w, int64_t ldw, int32_t n, int32_t k, void* wp,
 int gm_routing_node_encoder(const float* x, int64_t ldx, const int32_t* nbr, int32_t G, int32_t N,
                             const float* wt, const float* b, int32_t n, int32_t act, float* y, int64_t ldy,
                             void* stream);
+/* ---- Agent models (DGN, CommNet): per-env A x A agent communication ----
+ * gm_agent_attention (AttModel.forward, src/model.py:86-117): for every env b, agent i and
+ * head h: w_ij = <q_i, k_j> / sqrt(dk); p = softmax_j(adj_ij ? w_ij : -1e9); out_i =
+ * sum_j p_ij v_j + v_i. q, k, v: rows [B*A][ld] (head h at columns [h*d, (h+1)*d)), already
+ * activated; adj int8 [B][A][A]; out rows [B*A][ldo] (heads concatenated); att_weights
+ * (nullable) [B][heads][A][A] receives w (unmasked, like the reference). A <= 64, dk, dv <= 64. */
+int gm_agent_attention(const float* q, const float* k, const float* v, int64_t ld, const int8_t* adj, int32_t B,
+                       int32_t A, int32_t heads, int32_t dk, int32_t dv, float* out, int64_t ldo,
+                       float* att_weights, void* stream);
+/* gm_agent_comm (CommNet.forward, src/model.py:780-787): out_i = h_i + sum_{j != i, adj_ij}
+ * h_j / max(count, 1) per env; h, out rows [B*A][ldh / ldo] (out must not alias h). */
+int gm_agent_comm(const float* h, int64_t ldh, const int8_t* adj, int32_t B, int32_t A, int32_t H, float* out,
+                  int64_t ldo, void* stream);
+
 /* Tuning knob: tile configuration of gm_gemm_f32 (-1 = per-shape default; 0 = 128x128x32;
  * 1 = 128x256x16; 2 = 256x128x16 (LSTM: 256x128x16); 3 = 128x128x16; 4 = 128x128x16 at 4
  * blocks/CU); of gm_gemm_x3 (-1/0 = 128x128x16; 1 = 128x256x16 (LSTM: 128x128x32);

@@ -20,6 +20,7 @@ for s in "$@"; do
         smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" || exit $? ;;
         tests) step gpu_tests 900 python -m pytest tests -m gpu -x -q --tb=short --timeout=300 -p no:cacheprovider || exit $? ;;
         envtests) step env_tests 600 python -m pytest tests/test_env_gpu.py -x -q --tb=short --timeout=300 -p no:cacheprovider || exit $? ;;
+        clitests) step cli_tests 900 python -m pytest tests/test_cli_train_gpu.py -x -q --tb=short --timeout=600 -p no:cacheprovider || exit $? ;;
         nettests) step net_tests 600 python -m pytest tests/test_netmon_gpu.py tests/test_train_gpu.py -x -q --tb=short --timeout=300 -p no:cacheprovider || exit $? ;;
         sl) step sl_bench 600 python graph-marl_amd/sl.py --bench --n-nodes 100 --batch-size 8192 --sequence-length 8 \
                 --netmon-iterations 1 --iterations 5 --warmup 2 || exit $? ;;
@@ -29,6 +30,7 @@ for s in "$@"; do
                 --master-addr 127.0.0.1 --master-port 29511 bench.py --gpus 2 --steps 20 --warmup 5 \
                 --no-cpu-baseline || exit $? ;;
         gemm) X3_TILES=${X3_TILES:--1,1,2,3,4,5} step gemm 300 python tools/gemm_bench.py || exit $? ;;
+        models) step models_tests 600 python -m pytest tests/test_models_gpu.py -x -q --tb=short --timeout=300 -p no:cacheprovider || exit $? ;;
         fused) step fused_tests 600 python -m pytest tests/test_fused_gpu.py -x -q --tb=short --timeout=300 -p no:cacheprovider || exit $? ;;
         benchf32) GM_GEMM=f32 step bench_f32 300 python bench.py --no-cpu-baseline --steps 100 || exit $? ;;
         bench) step bench 600 python bench.py || exit $? ;;
