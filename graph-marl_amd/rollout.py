@@ -1,0 +1,76 @@
+"""Vectorised rollout driver: the reference's act -> step -> NetMon loop
+(src/main.py:667-748 with src/env/wrapper.py:66-109) over many envs per GPU, split into
+`groups` independent env groups that run on their own HIP streams.
+
+Each group owns a Routing env batch (its own seeds, topology, packets and NetMon state)
+and an ε-greedy policy; the NetMon and DQN modules (and their packed weights) are shared.
+One call to step() enqueues every group's step on that group's stream, so the GPU
+overlaps one group's latency-bound kernels (env step, ε-greedy draws, routing encoder)
+and GEMM tails with another group's GEMMs. Results are identical to running the groups
+one after another: the groups share no mutable state.
+"""
+import torch
+
+from . import fused as FU  # noqa: F401  (packed-weight caches shared by the groups)
+from .policy import EpsilonGreedy
+from .routing import Routing
+from .wrapper import NetMonWrapper
+
+
+class StreamedRollout:
+    def __init__(self, network, n_data, n_env, netmon, model, groups=1, seed=0, epsilon=0.5, episode_steps=50,
+                 obs_extra=None, device=None, **env_kw):
+        assert n_env % groups == 0, "n_env must be divisible by groups"
+        self.groups = groups
+        self.n_env = n_env
+        self.episode_steps = episode_steps
+        per = n_env // groups
+        dev = torch.device("cuda", torch.cuda.current_device() if device is None else device)
+        extra = netmon.get_out_features() if obs_extra is None else obs_extra
+        self.envs, self.wenvs, self.policies, self.streams = [], [], [], []
+        for g in range(groups):
+            env = Routing(network, n_data, n_env=per, seed=seed + g * per, obs_extra=extra, agent_adjacency=False,
+                          device=dev.index, **env_kw)
+            wenv = NetMonWrapper(env, netmon, 1)
+            pol = EpsilonGreedy(wenv, model, epsilon=epsilon, epsilon_decay=1.0, epsilon_update_freq=100,
+                                step_before_train=0)
+            self.envs.append(env)
+            self.wenvs.append(wenv)
+            self.policies.append(pol)
+            self.streams.append(torch.cuda.Stream(dev) if groups > 1 else torch.cuda.current_stream(dev))
+        self.ep = 0
+
+    def _on(self, g):
+        return torch.cuda.stream(self.streams[g])
+
+    @torch.no_grad()
+    def reset(self):
+        """Reset every group (new topologies + NetMon start-up step). The first call also
+        builds the packed weights on the caller's stream before the group streams use them."""
+        cur = torch.cuda.current_stream()
+        for g in range(self.groups):
+            self.streams[g].wait_stream(cur)
+            with self._on(g):
+                self.wenvs[g].reset()
+        self.ep = 0
+
+    @torch.no_grad()
+    def step(self):
+        """One vector step of every env (act, env step, NetMon step), a reset of every group
+        after episode_steps steps like the reference's fixed-length episodes."""
+        for g in range(self.groups):
+            with self._on(g):
+                act = self.policies[g].act(self.wenvs[g])
+                self.wenvs[g].step_(act)
+        self.ep += 1
+        if self.ep >= self.episode_steps:
+            for g in range(self.groups):
+                with self._on(g):
+                    self.wenvs[g].reset()
+            self.ep = 0
+
+    def join(self):
+        """Make the caller's stream wait for every group's work."""
+        cur = torch.cuda.current_stream()
+        for s in self.streams:
+            cur.wait_stream(s)

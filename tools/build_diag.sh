@@ -1,0 +1,11 @@
+#!/bin/bash
+# Diagnostic builds of the GEMM (csrc GM_DIAG=1: no A split, 2: no operand traffic in the
+# k loop, 3: as 2 without barriers) into graph-marl_amd/lib/diagN/ (timing only, wrong results).
+cd "$(dirname "$0")/../graph-marl_amd/csrc" || exit 1
+make -s || exit 1
+for d in 1 2 3; do
+  mkdir -p ../lib/diag$d
+  /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -I../../include -DGM_DIAG=$d -c gm_gemm.hip -o ../lib/diag$d/gm_gemm.o || exit 1
+  /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o ../lib/diag$d/libgraphmarl_amd.so ../lib/obj/gm_env.o \
+      ../lib/obj/gm_netmon.o ../lib/obj/gm_simple.o ../lib/obj/gm_agents.o ../lib/diag$d/gm_gemm.o || exit 1
+done
