@@ -44,7 +44,7 @@ def parse():
     p.add_argument("--random-topology", type=int, default=1)
     p.add_argument("--epsilon", type=float, default=0.5)
     p.add_argument("--no-kernel-timers", action="store_true")
-    p.add_argument("--groups", type=int, default=1,
+    p.add_argument("--groups", type=int, default=2,
                    help="env groups on separate HIP streams (graph-marl_amd/rollout.py StreamedRollout)")
     p.add_argument("--unfused", action="store_true", help="materialise the joint obs; separate LSTM/aggregate kernels")
     p.add_argument("--no-cpu-baseline", action="store_true")
@@ -58,6 +58,22 @@ def parse():
     p.add_argument("--cpu-envs", type=int, default=256)
     p.add_argument("--cpu-steps", type=int, default=20)
     return p.parse_args()
+
+
+def pmc_traffic(tag):
+    """HBM bytes per launch of a kernel (FETCH_SIZE x2 + WRITE_SIZE) from the latest committed
+    rocprofv3 PMC passes (profiles/*/pmc_traffic.json); None when not profiled."""
+    import glob
+
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "*", "pmc_traffic.json")), reverse=True):
+        try:
+            with open(path) as f:
+                k = json.load(f)["kernels"].get(tag)
+        except (OSError, ValueError, KeyError):
+            continue
+        if k:
+            return k["fetch_bytes"] + k["write_bytes"], os.path.relpath(path, ROOT)
+    return None, None
 
 
 def kernel_cost(tag, n_env, N, A, E, x3=False):
@@ -198,14 +214,11 @@ def main():
             w.fused = False
     env, wenv, policy = ro.envs[0], ro.wenvs[0], ro.policies[0]
 
-    def step():
-        ro.step()
-
-    def timed_region(warmup, steps, timers):
+    def timed_region(warmup, steps, timers, ro=ro):
         with torch.no_grad():
             ro.reset()
             for _ in range(warmup):
-                step()
+                ro.step()
             torch.cuda.synchronize()
             if world > 1:
                 dist.barrier()
@@ -214,7 +227,7 @@ def main():
             torch.cuda.synchronize()
             t0 = time.perf_counter()
             for _ in range(steps):
-                step()
+                ro.step()
             torch.cuda.synchronize()
             if world > 1:
                 dist.barrier()
@@ -227,7 +240,16 @@ def main():
 
     x3 = L.GEMM_MODE == "x3"
     G = args.groups
-    elapsed, prof = timed_region(args.warmup, args.steps, not args.no_kernel_timers)
+    # headline: the groups run concurrently, no per-kernel events in the timed region
+    timers = not args.no_kernel_timers
+    elapsed, prof = timed_region(args.warmup, args.steps, timers and G == 1)
+    if timers and G > 1:
+        # per-kernel durations from the same rollout as ONE group (kernels not overlapped), for
+        # the roofline fields and the rocprofv3 cross-check (tools/gpu_check.sh prof: --groups 1)
+        ro1 = RO.StreamedRollout(net, A, B, netmon, dqn, groups=1, seed=rank * B, epsilon=args.epsilon,
+                                 episode_steps=args.episode_steps, device=dev.index)
+        _, prof = timed_region(5, min(args.steps, 100), True, ro=ro1)
+        del ro1
     total = B * world * args.steps
     value = total / elapsed
     f32cmp = None
@@ -244,26 +266,24 @@ def main():
             ts = [s.elapsed_time(e) for s, e in evs]
             kernels[tag] = {"launches": len(ts), "avg_us": 1e3 * sum(ts) / len(ts), "total_ms": sum(ts)}
     roof = None
-    if kernels and G > 1:
-        # concurrent groups: per-kernel event pairs on a shared GPU measure overlapped time
-        for kv in kernels.values():
-            kv["note"] = "groups run concurrently: durations include overlap with other groups' kernels"
     if kernels:
         dom = max(kernels, key=lambda k: kernels[k]["total_ms"])
-        bound, units = kernel_cost(dom, B // G, N, A, E, x3)
+        bound, units = kernel_cost(dom, B, N, A, E, x3)
         sec = kernels[dom]["avg_us"] * 1e-6
         if bound in ("mfma", "mfma16"):
             ach = units / sec / 1e12
             peak = F16_MFMA_PEAK_TFS if bound == "mfma16" else F32_MFMA_PEAK_TFS
+            tb, src = pmc_traffic(dom)
             roof = {"kernel": dom, "bound": "mfma", "achieved": round(ach, 2), "peak": peak,
                     "unit": "TFLOP/s" + (" (f16 MFMA, 3 per fp32 multiply-add)" if bound == "mfma16" else " (f32 MFMA)"),
-                    "frac": round(ach / peak, 4), "traffic": None}
+                    "frac": round(ach / peak, 4), "traffic": tb,
+                    "traffic_note": None if tb is None else f"HBM bytes per launch (rocprofv3 PMC, {src})"}
         else:
             ach = units / sec / 1e9
             roof = {"kernel": dom, "bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                     "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None}
         for tag, kv in kernels.items():
-            bound, units = kernel_cost(tag, B // G, N, A, E, x3)
+            bound, units = kernel_cost(tag, B, N, A, E, x3)
             if bound:
                 s = kv["avg_us"] * 1e-6
                 kv["achieved"] = round(units / s / (1e9 if bound == "hbm" else 1e12), 2)

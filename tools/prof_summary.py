@@ -49,6 +49,9 @@ def linear_labels(n_dispatch, episode_steps, netmon_iters=1, netmon=NETMON, dqn=
 
 
 def relabel(rows, episode_steps):
+    for r in rows:  # k_gemm3<...> (split-f16 form) and k_gemm<...> (f32) are one call-site sequence
+        if "k_gemm3" in r["Kernel_Name"] or r["Kernel_Name"].startswith("k_gemm") or "k_gemmI" in r["Kernel_Name"]:
+            r["Kernel_Name"] = "k_gemm"
     for name, nm, dq in (("k_linear_f32", NETMON, DQN), ("k_gemm", NETMON_G, DQN_G)):
         lin = [r for r in rows if r["Kernel_Name"].startswith(name)]
         for r, lab in zip(lin, linear_labels(len(lin), episode_steps, netmon=nm, dqn=dq)):
