@@ -20,7 +20,7 @@ Differences from the reference, by design:
   * no tensorboard: the log lines go to stdout and checkpoints / eval metrics to
     --log-dir (default runs/<date>_<host><comment>, like SummaryWriter's logdir);
   * models: dqn, dgn, dqnr, commnet (comm_rounds 2); activation: leaky_relu only;
-    NetMon: sum/mean aggregation, lstm/lnlstm/gru cells, carry-over on, no --netmon-global.
+    NetMon: sum/mean aggregation, lstm/lnlstm/gru cells, carry-over on, --netmon-global.
 """
 import argparse
 import copy
@@ -286,7 +286,7 @@ def main(argv=None):
         raise NotImplementedError("only --activation-function=leaky_relu is built")
 
     H = args.netmon_dim
-    env = make_env(args, dev, obs_extra=4 * H if args.netmon else 0)
+    env = make_env(args, dev, obs_extra=(5 if args.netmon_global else 4) * H if args.netmon else 0)
     env.reset()  # reset_and_get_sizes (src/main.py:443): the reference's first reset
     n_agents, n_nodes, node_obs_size = env.n_data, env.n_nodes, env.node_obs_dim
     netmon = None

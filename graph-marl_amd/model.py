@@ -355,8 +355,6 @@ class NetMon(nn.Module):
                                       "are out of scope)")
         if not rnn_carryover:
             raise NotImplementedError("rnn_carryover=False is not built")
-        if output_global_hidden:
-            raise NotImplementedError("--netmon-global readout is not built")
         self.encode = MLP(in_features, (*encoder_units, hidden_features))
         self.state = None
         self.iterations = iterations
@@ -384,7 +382,9 @@ class NetMon(nn.Module):
         self.state_size = hidden_features * self.num_states
 
     def get_out_features(self):
-        return self.hidden_features * (4 if self.output_neighbor_hidden else 1)
+        """src/model.py:403-415 for routing graphs (max degree 3): h, [global mean], [3 neighbours]."""
+        return self.hidden_features * (1 + (1 if self.output_global_hidden else 0) +
+                                       (3 if self.output_neighbor_hidden else 0))
 
     def get_state_size(self):
         return self.state_size
@@ -412,6 +412,19 @@ class NetMon(nn.Module):
             M = mp_aggregate(h, nbr, self.agg_mode)
             h, c = self._cell(self.rnn_update, M, h, c)
         self.state = (torch.stack((h, c), 1) if c is not None else h.unsqueeze(1)).reshape(B, N, self.state_size)
+        if self.output_global_hidden:
+            # [h | mean over the graph's nodes of h | neighbour h] (src/model.py:458-469, 624-627)
+            hv = h.reshape(B, N, H)
+            parts = [hv, hv.mean(dim=1, keepdim=True).expand(B, N, H)]
+            if self.output_neighbor_hidden:
+                parts.append(netmon_readout(h, last_nbr, nbr, None).reshape(B, N, -1)[..., H:])
+            full = torch.cat(parts, -1)
+            if agent_node is not None:
+                full = torch.gather(full, 1, agent_node.long().unsqueeze(-1).expand(-1, -1, full.shape[-1]))
+            if out is not None:
+                out[..., out_col:out_col + full.shape[-1]] = full
+                return out
+            return full
         if not self.output_neighbor_hidden:
             hv = h.reshape(B, N, H)
             if agent_node is None:

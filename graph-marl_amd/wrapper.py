@@ -22,7 +22,8 @@ class NetMonWrapper:
         # the readout is [h, h_prev of deg neighbours] with deg = the graph's max degree
         # (src/model.py:582-589), so the graph part is (deg + 1) H wide (4H on routing graphs)
         H = netmon.hidden_features
-        self.graph_features = (env.nbr.shape[-1] + 1) * H if netmon.output_neighbor_hidden else H
+        self.graph_features = H * (1 + (env.nbr.shape[-1] if netmon.output_neighbor_hidden else 0) +
+                                   (1 if netmon.output_global_hidden else 0))
         need = env.obs_dim + self.graph_features
         if env.obs_stride < need:
             raise ValueError(f"env obs buffer too narrow: create the env with obs_extra={self.graph_features}")
@@ -34,7 +35,8 @@ class NetMonWrapper:
         self.h_prev = None
         self.obs_dim = need
         if fused is None:
-            fused = netmon.rnn_type == "lstm" and netmon.output_neighbor_hidden and H % 32 == 0
+            fused = (netmon.rnn_type == "lstm" and netmon.output_neighbor_hidden and not netmon.output_global_hidden
+                     and H % 32 == 0)
         self.fused = fused
         self._dirty = False
 

@@ -66,12 +66,13 @@ def gru_cell(x, h, W, p):
     return (1 - z) * n + z * h
 
 
-def netmon_forward(W, x, adj, state, rnn="lstm", agg="sum", K=1, n_enc_layers=3):
+def netmon_forward(W, x, adj, state, rnn="lstm", agg="sum", K=1, n_enc_layers=3, global_h=False):
     """src/model.py:451-622 NetMon.forward with output_neighbor_hidden=True,
-    rnn_carryover=True, no global readout, no_agent_mapping=True.
+    rnn_carryover=True, no_agent_mapping=True; global_h adds the --netmon-global readout
+    (mean of h over the graph's nodes after h, src/model.py:461-462, 624-627).
 
     x [B,N,F], adj [B,N,N] (I+A), state [B,N,S] or None.
-    Returns (out [B,N,4H], new_state [B,N,S])."""
+    Returns (out [B,N,4H] ([B,N,5H] with global_h), new_state [B,N,S])."""
     x = np.asarray(x, np.float64)
     adj = np.asarray(adj, np.float64)
     B, N, _ = x.shape
@@ -113,7 +114,10 @@ def netmon_forward(W, x, adj, state, rnn="lstm", agg="sum", K=1, n_enc_layers=3)
             js = np.nonzero(mask[b, i])[0]
             for k, j in enumerate(js):
                 out_n[b, i, k] = nb[b, j]
-    out = np.concatenate([h.reshape(B, N, H), out_n.reshape(B, N, deg * H)], -1)
+    parts = [h.reshape(B, N, H)]
+    if global_h:
+        parts.append(np.repeat(h.reshape(B, N, H).mean(1, keepdims=True), N, 1))
+    out = np.concatenate(parts + [out_n.reshape(B, N, deg * H)], -1)
     return out, new_state
 
 

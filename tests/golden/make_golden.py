@@ -396,6 +396,33 @@ def gen_netmon(out, Network, Routing, EVAL_SEEDS, NetMon, DQN):
     np.savez_compressed(out, **d)
 
 
+def gen_netmon_global(out, Network, Routing, EVAL_SEEDS, NetMon):
+    """NetMon with --netmon-global (src/model.py:451-474, 624-627): readout [h | mean_nodes(h) |
+    neighbour h], mapped to agents; 3 steps with carried state, K = 1 and 2."""
+    import torch
+    import torch.nn.functional as F
+
+    d = {}
+    n, a, B, steps = 20, 20, 4, 3
+    node_obs, node_adj, node_agent, _ = collect_graph_inputs(Network, Routing, EVAL_SEEDS, n, a, B, steps, 200)
+    d["node_obs"], d["node_adj"], d["node_agent"] = node_obs, node_adj, node_agent
+    for vi, K in enumerate((1, 2)):
+        torch.manual_seed(50 + vi)
+        nm = NetMon(node_obs.shape[-1], 32, [64, 48], K, F.leaky_relu, rnn_type="lstm", rnn_carryover=True,
+                    agg_type="sum", output_neighbor_hidden=True, output_global_hidden=True)
+        nm.eval()
+        sd_to_npz(f"v{vi}_w_", nm.state_dict(), d)
+        d[f"v{vi}_out_features"] = np.int64(nm.get_out_features())
+        nm.state = None
+        with torch.no_grad():
+            for t in range(steps):
+                mapped = nm(torch.tensor(node_obs[t]), torch.tensor(node_adj[t]), torch.tensor(node_agent[t]))
+                d[f"v{vi}_mapped_{t}"] = mapped.numpy()
+                d[f"v{vi}_state_{t}"] = nm.state.numpy()
+    np.savez_compressed(out, **d)
+    print("netmon_global done", flush=True)
+
+
 def gen_models(out, Network, Routing, EVAL_SEEDS, DGN, DQNR, CommNet):
     """DGN / DQNR / CommNet forwards (src/model.py:45-184, 653-794) on real routing agent
     observations and agent adjacency: Q, attention weights, recurrent agent states over a
@@ -794,6 +821,8 @@ def main():
         gen_env(HERE, Network, Routing, EVAL_SEEDS, {o[4:] for o in only if o.startswith("env:")})
     if only is None or "netmon" in only:
         gen_netmon(os.path.join(HERE, "netmon.npz"), Network, Routing, EVAL_SEEDS, NetMon, DQN)
+    if only is None or "netmon_global" in only:
+        gen_netmon_global(os.path.join(HERE, "netmon_global.npz"), Network, Routing, EVAL_SEEDS, NetMon)
     if only is None or "models" in only:
         gen_models(os.path.join(HERE, "models.npz"), Network, Routing, EVAL_SEEDS, DGN, DQNR, CommNet)
     if only is None or "train" in only:

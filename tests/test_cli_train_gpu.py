@@ -64,3 +64,12 @@ def test_routing_agent_models_train_and_eval(tmp_path, model, netmon):
     assert ck.exists()
     m2 = main.main(common + ["--eval", f"--model-load-path={ck}", "--policy=trained"])
     assert np.isfinite(m2["reward_mean"])
+
+
+def test_routing_netmon_global_train(tmp_path):
+    main = importlib.import_module("graph-marl_amd.main")
+    m = main.main(["--env-type=routing", "--model=dqn", "--netmon", "--netmon-global", "--netmon-iterations=1",
+                   "--netmon-dim=32", "--netmon-encoder-dim=64", "--n-env=16", "--total-steps=80",
+                   "--step-before-train=30", "--mini-batch-size=16", "--sequence-length=2", "--episode-steps=30",
+                   "--eval-episodes=16", "--eval-episode-steps=10", "--disable-progressbar", f"--log-dir={tmp_path}"])
+    assert np.isfinite(m["reward_mean"])

@@ -2,6 +2,7 @@
 of the same op, and full NetMon / DQN forward vs the reference's golden outputs.
 Tolerance (north star): 1e-5 absolute on GNN/LSTM float outputs."""
 import importlib
+import os
 
 import numpy as np
 import pytest
@@ -203,3 +204,27 @@ def test_dqn_forward_vs_reference_golden():
     with torch.no_grad():
         q = dqn(obs)
     np.testing.assert_allclose(q.cpu().numpy(), g["dqn_q"], atol=ATOL, rtol=0)
+
+
+def test_netmon_global_readout_vs_reference_golden():
+    """--netmon-global (src/model.py:458-469, 624-627): [h | node mean of h | neighbour h]
+    mapped to agents, over 3 steps with carried state, vs the reference."""
+    import importlib
+
+    import numpy as np
+    import torch
+
+    M = importlib.import_module("graph-marl_amd.model")
+    g = np.load(os.path.join(R.GOLDEN, "netmon_global.npz"))
+    for vi, K in enumerate((1, 2)):
+        nm = M.NetMon(g["node_obs"].shape[-1], 32, [64, 48], K, output_global_hidden=True).cuda()
+        nm.load_state_dict({k[len(f"v{vi}_w_"):]: torch.as_tensor(g[k]) for k in g.files if k.startswith(f"v{vi}_w_")})
+        assert nm.get_out_features() == int(g[f"v{vi}_out_features"])
+        nm.state = None
+        for t in range(3):
+            with torch.no_grad():
+                mapped = nm(torch.as_tensor(g["node_obs"][t], device="cuda"),
+                            torch.as_tensor(g["node_adj"][t], device="cuda"),
+                            torch.as_tensor(g["node_agent"][t], device="cuda"))
+            np.testing.assert_allclose(mapped.cpu().numpy(), g[f"v{vi}_mapped_{t}"], atol=1e-5, rtol=0)
+            np.testing.assert_allclose(nm.state.cpu().numpy(), g[f"v{vi}_state_{t}"], atol=1e-5, rtol=0)

@@ -191,3 +191,17 @@ def test_agent_model_restatement_matches_reference(name):
             np.testing.assert_allclose(st, g[f"{name}_state_{t}"], atol=5e-6, rtol=0)
             state = st * (1 - g["done"][t][..., None])
         np.testing.assert_allclose(q, g[f"{name}_q_{t}"], atol=5e-6, rtol=0)
+
+
+def test_netmon_global_restatement_matches_reference():
+    """--netmon-global readout of the fp64 restatement vs the reference (netmon_global.npz)."""
+    g = np.load(os.path.join(R.GOLDEN, "netmon_global.npz"))
+    for vi, K in enumerate((1, 2)):
+        W = {k[len(f"v{vi}_w_"):]: g[k].astype(np.float64) for k in g.files if k.startswith(f"v{vi}_w_")}
+        state = None
+        for t in range(3):
+            out, state = netmon_ref.netmon_forward(W, g["node_obs"][t], g["node_adj"][t], state, "lstm", "sum", K,
+                                                   global_h=True)
+            mapped = netmon_ref.to_network_obs(out, g["node_agent"][t])
+            np.testing.assert_allclose(mapped, g[f"v{vi}_mapped_{t}"], atol=5e-6, rtol=0)
+            np.testing.assert_allclose(state, g[f"v{vi}_state_{t}"], atol=5e-6, rtol=0)
