@@ -214,6 +214,8 @@ def main():
             w.fused = False
     env, wenv, policy = ro.envs[0], ro.wenvs[0], ro.policies[0]
 
+    state = {}
+
     def timed_region(warmup, steps, timers, ro=ro):
         with torch.no_grad():
             ro.reset()
@@ -228,11 +230,13 @@ def main():
             t0 = time.perf_counter()
             for _ in range(steps):
                 ro.step()
+            t_issue = time.perf_counter() - t0  # host time to enqueue the steps
             torch.cuda.synchronize()
             if world > 1:
                 dist.barrier()
             elapsed = time.perf_counter() - t0
             prof, L.PROF = L.PROF, None
+            state["host_ms_per_step"] = 1e3 * t_issue / steps
         el = torch.tensor([elapsed], dtype=torch.float64, device="cpu" if share else dev)
         if world > 1:
             dist.all_reduce(el, op=dist.ReduceOp.MAX)
@@ -243,6 +247,7 @@ def main():
     # headline: the groups run concurrently, no per-kernel events in the timed region
     timers = not args.no_kernel_timers
     elapsed, prof = timed_region(args.warmup, args.steps, timers and G == 1)
+    host_ms = state["host_ms_per_step"]
     if timers and G > 1:
         # per-kernel durations from the same rollout as ONE group (kernels not overlapped), for
         # the roofline fields and the rocprofv3 cross-check (tools/gpu_check.sh prof: --groups 1)
@@ -325,6 +330,7 @@ def main():
                        "gemm_form": L.GEMM_MODE,
                        "parallelism": f"dp{world} (env shards, no rollout collective)",
                        "stream_groups": G},
+            "host_enqueue_ms_per_step": round(host_ms, 4),
             "roofline": roof, "cpu_baseline": cpu, "f32_exact_gemms": f32cmp, "rollout_train": train,
             "kernels": kernels,
         }
