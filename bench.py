@@ -44,6 +44,8 @@ def parse():
     p.add_argument("--random-topology", type=int, default=1)
     p.add_argument("--epsilon", type=float, default=0.5)
     p.add_argument("--no-kernel-timers", action="store_true")
+    p.add_argument("--graph", type=int, default=0,
+                   help="replay the rollout as a HIP graph of this many (even) vector steps (0: eager launches)")
     p.add_argument("--groups", type=int, default=2,
                    help="env groups on separate HIP streams (graph-marl_amd/rollout.py StreamedRollout)")
     p.add_argument("--unfused", action="store_true", help="materialise the joint obs; separate LSTM/aggregate kernels")
@@ -216,11 +218,17 @@ def main():
 
     state = {}
 
-    def timed_region(warmup, steps, timers, ro=ro):
+    def timed_region(warmup, steps, timers, ro=ro, graph=0):
         with torch.no_grad():
             ro.reset()
-            for _ in range(warmup):
+            for _ in range(warmup + (warmup % 2 if graph else 0)):
                 ro.step()
+            if graph:
+                # capture after the eager warmup (packed weights, scratch buffers exist), then
+                # one untimed replay; the timed loop replays steps/graph graphs
+                assert steps % graph == 0, "--steps must be a multiple of --graph"
+                ro.capture(graph)
+                ro.run(graph)
             torch.cuda.synchronize()
             if world > 1:
                 dist.barrier()
@@ -228,8 +236,11 @@ def main():
                 L.PROF = {}
             torch.cuda.synchronize()
             t0 = time.perf_counter()
-            for _ in range(steps):
-                ro.step()
+            if graph:
+                ro.run(steps)
+            else:
+                for _ in range(steps):
+                    ro.step()
             t_issue = time.perf_counter() - t0  # host time to enqueue the steps
             torch.cuda.synchronize()
             if world > 1:
@@ -246,9 +257,9 @@ def main():
     G = args.groups
     # headline: the groups run concurrently, no per-kernel events in the timed region
     timers = not args.no_kernel_timers
-    elapsed, prof = timed_region(args.warmup, args.steps, timers and G == 1)
+    elapsed, prof = timed_region(args.warmup, args.steps, timers and G == 1 and not args.graph, graph=args.graph)
     host_ms = state["host_ms_per_step"]
-    if timers and G > 1:
+    if timers and (G > 1 or args.graph):
         # per-kernel durations from the same rollout as ONE group (kernels not overlapped), for
         # the roofline fields and the rocprofv3 cross-check (tools/gpu_check.sh prof: --groups 1)
         ro1 = RO.StreamedRollout(net, A, B, netmon, dqn, groups=1, seed=rank * B, epsilon=args.epsilon,
@@ -329,7 +340,7 @@ def main():
                        "n_env_per_gpu": B, "n_nodes": N, "n_data": A, "netmon_iterations": K,
                        "gemm_form": L.GEMM_MODE,
                        "parallelism": f"dp{world} (env shards, no rollout collective)",
-                       "stream_groups": G},
+                       "stream_groups": G, "graph_steps": args.graph},
             "host_enqueue_ms_per_step": round(host_ms, 4),
             "roofline": roof, "cpu_baseline": cpu, "f32_exact_gemms": f32cmp, "rollout_train": train,
             "kernels": kernels,

@@ -255,10 +255,11 @@ def routing_encoder(lin, x, nbr, G, N, out):
 
 
 @torch.no_grad()
-def netmon_step(netmon, node_obs, nbr, state):
+def netmon_step(netmon, node_obs, nbr, state, out=None, last_out=None):
     """One NetMon step for B graphs. node_obs [B, N, F]; nbr int32 [B, N, deg]; state
     [B, N, 2H] or None. Returns (new state [B, N, 2H], h_prev rows [B*N, 2H] whose first
-    H columns are the last pre-aggregation h)."""
+    H columns are the last pre-aggregation h). out / last_out ([B*N, 2H], optional) receive
+    the new state and h_prev, so a caller can keep them in fixed buffers (graph replay)."""
     if netmon.rnn_type != "lstm":
         raise NotImplementedError("fused NetMon step: lstm only (lnlstm/gru use NetMon.forward_graph)")
     B, N, Fd = node_obs.shape
@@ -276,7 +277,16 @@ def netmon_step(netmon, node_obs, nbr, state):
         state = torch.zeros(B, N, 2 * H, device=dev)
     st = state.reshape(M, 2 * H)
     wp, ldw, bp, x3 = pack_lstm(netmon.rnn_obs)
-    S = torch.empty(M, 2 * H, device=dev)
+    K = netmon.iterations
+
+    def buf(i):  # storage of S_i (S_0 = obs cell output, S_K = new state, S_{K-1} = h_prev)
+        if i == K and out is not None:
+            return out.reshape(M, 2 * H)
+        if i == K - 1 and last_out is not None:
+            return last_out.reshape(M, 2 * H)
+        return torch.empty(M, 2 * H, device=dev)
+
+    S = buf(0)
     gemm(dense(x.data_ptr(), x.stride(0), H), dense(st.data_ptr(), 2 * H, H), wp.data_ptr(), ldw, bp.data_ptr(),
          M, 4 * H, GM_EPI_LSTM, S.data_ptr(), 2 * H, S[:, H:].data_ptr(), 2 * H, st[:, H:].data_ptr(), 2 * H,
          tag=netmon.rnn_obs.tag and f"lstm:{netmon.rnn_obs.tag}:{M}x{4 * H}x{2 * H}", x3=x3)
@@ -285,7 +295,7 @@ def netmon_step(netmon, node_obs, nbr, state):
     mean = netmon.agg_mode == 1
     for it in range(netmon.iterations):
         last = S
-        S2 = torch.empty(M, 2 * H, device=dev)
+        S2 = buf(it + 1)
         gemm(aggregate(S.data_ptr(), 2 * H, H, nbr, N, mean), dense(S.data_ptr(), 2 * H, H), wu.data_ptr(), ldu,
              bu.data_ptr(), M, 4 * H, GM_EPI_LSTM, S2.data_ptr(), 2 * H, S2[:, H:].data_ptr(), 2 * H,
              S[:, H:].data_ptr(), 2 * H,

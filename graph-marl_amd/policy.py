@@ -79,6 +79,10 @@ class EpsilonGreedy:
         self._decay_step()
         return actions
 
+    def _eps_changes(self):
+        """True when ε still decays (its value is a kernel argument)."""
+        return self._epsilon > 0.01 and self._decay != 1.0
+
     def reset(self, agents_to_reset):
         """src/policy.py:72-82: zero the recurrent agent state of the given agents
         ([n_env, A] bool, or True for all)."""

@@ -8,6 +8,13 @@ One call to step() enqueues every group's step on that group's stream, so the GP
 overlaps one group's latency-bound kernels (env step, ε-greedy draws, routing encoder)
 and GEMM tails with another group's GEMMs. Results are identical to running the groups
 one after another: the groups share no mutable state.
+
+capture() records an even number of vector steps of all groups as ONE HIP graph (the
+NetMon state and h_prev alternate between two fixed buffer pairs, so the graph reads and
+writes the same addresses on every replay); run() then replays it, which removes the
+per-kernel launch gaps and the host launch cost. Graph replay bakes the kernel arguments
+in: it is for fixed-ε rollouts (ε decay 1.0: benchmarks, evaluation); episode resets stay
+eager between replays.
 """
 import torch
 
@@ -37,8 +44,10 @@ class StreamedRollout:
             self.envs.append(env)
             self.wenvs.append(wenv)
             self.policies.append(pol)
-            self.streams.append(torch.cuda.Stream(dev) if groups > 1 else torch.cuda.current_stream(dev))
+            self.streams.append(torch.cuda.Stream(dev))
         self.ep = 0
+        self._graph = None
+        self._gsteps = 0
 
     def _on(self, g):
         return torch.cuda.stream(self.streams[g])
@@ -54,20 +63,67 @@ class StreamedRollout:
                 self.wenvs[g].reset()
         self.ep = 0
 
-    @torch.no_grad()
-    def step(self):
-        """One vector step of every env (act, env step, NetMon step), a reset of every group
-        after episode_steps steps like the reference's fixed-length episodes."""
+    def _enqueue_step(self):
         for g in range(self.groups):
             with self._on(g):
                 act = self.policies[g].act(self.wenvs[g])
                 self.wenvs[g].step_(act)
+
+    @torch.no_grad()
+    def step(self):
+        """One vector step of every env (act, env step, NetMon step), a reset of every group
+        after episode_steps steps like the reference's fixed-length episodes."""
+        self._enqueue_step()
         self.ep += 1
         if self.ep >= self.episode_steps:
             for g in range(self.groups):
                 with self._on(g):
                     self.wenvs[g].reset()
             self.ep = 0
+
+    @torch.no_grad()
+    def capture(self, steps=2):
+        """Record `steps` (even, dividing episode_steps) vector steps of every group as one
+        graph. Call after reset() and a few eager steps (packed weights and scratch exist)."""
+        assert steps % 2 == 0 and self.episode_steps % steps == 0, "steps must be even and divide episode_steps"
+        if any(w._eps_changes() for w in self.policies):
+            raise ValueError("graph replay needs a fixed epsilon (epsilon_decay = 1.0)")
+        torch.cuda.synchronize()
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            cap = torch.cuda.current_stream()
+            for s in self.streams:
+                s.wait_stream(cap)
+            for _ in range(steps):
+                self._enqueue_step()
+            for s in self.streams:
+                cap.wait_stream(s)
+        self._graph, self._gsteps = graph, steps
+        # the capture only recorded: the env / NetMon state is where it was before it; the
+        # ping-pong buffer parity advanced by `steps` (even): unchanged
+
+    @torch.no_grad()
+    def run(self, n):
+        """n vector steps (graph replays of capture()'s length when captured, else eager)."""
+        if self._graph is None:
+            for _ in range(n):
+                self.step()
+            return
+        assert n % self._gsteps == 0
+        for _ in range(n // self._gsteps):
+            if self.ep % self._gsteps:
+                raise RuntimeError("graph replay must start at a multiple of the captured length")
+            self._graph.replay()
+            self.ep += self._gsteps
+            if self.ep >= self.episode_steps:
+                cur = torch.cuda.current_stream()  # the replay's stream
+                for g in range(self.groups):
+                    self.streams[g].wait_stream(cur)
+                    with self._on(g):
+                        self.wenvs[g].reset()
+                for s in self.streams:
+                    cur.wait_stream(s)
+                self.ep = 0
 
     def join(self):
         """Make the caller's stream wait for every group's work."""

@@ -39,6 +39,11 @@ class NetMonWrapper:
                      and H % 32 == 0)
         self.fused = fused
         self._dirty = False
+        # fused mode: the state and h_prev alternate between two fixed buffer pairs, so a
+        # captured 2-step HIP graph (rollout.StreamedRollout.capture) reads and writes the
+        # same addresses on every replay
+        self._bufs = None
+        self._cur = 0
 
     def __getattr__(self, name):
         return getattr(self.env, name)
@@ -67,7 +72,15 @@ class NetMonWrapper:
         with torch.no_grad():
             self.last_netmon_state = self.current_netmon_state
             if self.fused:
-                state, self.h_prev = FU.netmon_step(self.netmon, e.node_obs, e.nbr, self.current_netmon_state)
+                B, N, H2 = e.n_env, e.n_nodes, 2 * self.netmon.hidden_features
+                if self._bufs is None:
+                    self._bufs = [(torch.empty(B, N, H2, device=e.device), torch.empty(B * N, H2, device=e.device))
+                                  for _ in range(2)]
+                nxt = 1 - self._cur
+                st, hp = self._bufs[nxt]
+                state, self.h_prev = FU.netmon_step(self.netmon, e.node_obs, e.nbr, self.current_netmon_state,
+                                                    out=st, last_out=hp)
+                self._cur = nxt
                 self.current_netmon_state = state
                 self._dirty = True
             else:
@@ -78,6 +91,7 @@ class NetMonWrapper:
     def reset(self):
         self.current_netmon_state = None
         self.last_netmon_state = None
+        self._cur = 1  # the start-up step writes buffer pair 0
         self.env.reset_()
         for _ in range(self.startup_iterations):
             self._netmon_step()

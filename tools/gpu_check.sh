@@ -32,6 +32,9 @@ for s in "$@"; do
         gemm) X3_TILES=${X3_TILES:--1,1,2,3,4,5} step gemm 300 python tools/gemm_bench.py || exit $? ;;
         models) step models_tests 600 python -m pytest tests/test_models_gpu.py -x -q --tb=short --timeout=300 -p no:cacheprovider || exit $? ;;
         fused) step fused_tests 600 python -m pytest tests/test_fused_gpu.py -x -q --tb=short --timeout=300 -p no:cacheprovider || exit $? ;;
+        rollout) step rollout_tests 600 python -m pytest tests/test_rollout_gpu.py -x -q --tb=short --timeout=300 -p no:cacheprovider || exit $? ;;
+        benchg) step bench_graph 300 python bench.py --no-cpu-baseline --steps 100 --graph ${GRAPH:-2} --no-train || exit $? ;;
+        benchg0) step bench_eager 300 python bench.py --no-cpu-baseline --steps 100 --no-train || exit $? ;;
         benchf32) GM_GEMM=f32 step bench_f32 300 python bench.py --no-cpu-baseline --steps 100 || exit $? ;;
         bench) step bench 600 python bench.py || exit $? ;;
         benchq) step bench 300 python bench.py --no-cpu-baseline --steps 100 || exit $? ;;
