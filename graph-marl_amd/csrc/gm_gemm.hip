@@ -88,6 +88,11 @@ __device__ __forceinline__ float4 bload(__amdgpu_buffer_rsrc_t r, int byte_off) 
     u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(r, byte_off, 0, 0);
     return make_float4(__uint_as_float(v.x), __uint_as_float(v.y), __uint_as_float(v.z), __uint_as_float(v.w));
 }
+// 16 B per lane from a buffer straight into LDS (lane-linear from the wave-uniform base)
+__device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, char* lds_base, int byte_off) {
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)lds_base, 16, byte_off, 0, 0,
+                                             0);
+}
 __device__ __forceinline__ float4 f4add(float4 a, float4 b) {
     return make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w);
 }
@@ -586,6 +591,218 @@ __global__ __launch_bounds__(WGM* WGN * 64, OCC) void k_gemm3(ASrc a0, ASrc a1, 
     epilogue<TM, TN, EPI>(acc, ep, m0 + wr * TM * 32, n0 + wc * TN * 32, M, N, lane);
 }
 
+// ---------------------------------------------------------------------------------------
+// X3 kernel with LDS-DMA staging (buffer_load ... lds): both operands go HBM/L2 -> LDS with
+// no VGPR round trip and no ds_write pass. A stays fp32 in LDS (32-deep k tiles = one 128-B
+// line per row) and is split into its f16 hi / 2^12-scaled lo pieces per MFMA fragment, in
+// registers, between the MFMAs; B tiles are the packed weight rows (same 128-B line per row).
+// LDS image per stage: [BM rows of A | BN rows of B] x 128 B, 16-B chunks XOR-swizzled by
+// row (pos = chunk ^ ((row >> 1) & 7): conflict-free ds_read_b128 on the 32-row fragments);
+// the DMA writes lane-linear (8 rows per wave-instruction), so the swizzle is applied to the
+// per-lane SOURCE address. STAGES-deep ring: tile kt+STAGES-1 is issued at the top of step
+// kt, and a counted vmcnt + raw s_barrier at the bottom retires tile kt+1 only, so the
+// younger tiles stay in flight across the barrier. A sources: DENSE, READOUT (the 32-deep
+// tile lies inside one H-wide segment: per-lane segment row offsets; missing neighbours
+// read an out-of-range offset = zeros), then the optional dense second source.
+template <int WGM, int WGN, int TM, int TN, int STAGES, int AMODE, int EPI, int OCC>
+__global__ __launch_bounds__(WGM* WGN * 64, OCC) void k_gemm3g(ASrc a0, ASrc a1, const _Float16* __restrict__ w,
+                                                              long long ldw, unsigned wbytes, int M, int N, int K,
+                                                              Epi ep, const float* __restrict__ wscale_inv) {
+    constexpr int BK = 32, NW = WGM * WGN;
+    constexpr int BM = WGM * TM * 32, BN = WGN * TN * 32;
+    constexpr int NA = BM / 8 / NW, NB = BN / 8 / NW;  // DMA instructions per wave per tile
+    constexpr int NL = NA + NB;
+    constexpr int STAGE_B = (BM + BN) * 128;
+    static_assert(BM % (8 * NW) == 0 && BN % (8 * NW) == 0, "tile rows per wave");
+    static_assert(AMODE != GM_A_AGGREGATE, "aggregate source uses k_gemm3");
+    __shared__ __attribute__((aligned(16))) char lds[STAGES * STAGE_B];
+
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wr = wave / WGN, wc = wave % WGN;
+    const int nM = (M + BM - 1) / BM, nN = (N + BN - 1) / BN;
+    const int bid = xcd_remap(blockIdx.x, nM * nN);
+    const int m0 = (bid / nN) * BM, n0 = (bid % nN) * BN;
+
+    // ---- per-lane DMA source offsets (fixed over K): row (lane >> 3) of each 8-row piece,
+    // logical chunk c = (lane & 7) ^ swizzle(row) ----
+    const int sub = lane >> 3;
+    int so[NA][4];  // DENSE: [0]; READOUT: segment rows (OOB = none)
+    int o1[NA];     // second (dense) source
+    int cc[NA];     // logical chunk of this lane's 16 B (k offset 4 cc)
+#pragma unroll
+    for (int j = 0; j < NA; j++) {
+        const int R = (wave * NA + j) * 8 + sub;
+        const int c = (lane & 7) ^ ((R >> 1) & 7);
+        cc[j] = c;
+        const int row = min(m0 + R, M - 1);
+        o1[j] = (int)(row * a1.ld0) * 4 + 16 * c;
+#pragma unroll
+        for (int s = 0; s < 4; s++) so[j][s] = OOB;
+        if (AMODE == GM_A_DENSE) {
+            so[j][0] = (int)(row * a0.ld0) * 4 + 16 * c;
+        } else {  // READOUT: [h_final[v] | h_prev[nbr(v, 0..2)]], v = agent_node[row]
+            const int g = row / a0.rows_per_graph;
+            const int v = a0.agent_node[row];
+            const int* nb = a0.nbr + ((size_t)g * a0.n_nodes + v) * a0.deg;
+            so[j][0] = (int)((g * a0.n_nodes + v) * a0.ld0) * 4 + 16 * c;
+#pragma unroll
+            for (int s = 1; s < 4; s++) {
+                const int mm = s - 1 < a0.deg ? nb[s - 1] : -1;
+                so[j][s] = mm >= 0 ? (int)((g * a0.n_nodes + mm) * a0.ld1) * 4 + 16 * c : OOB;
+            }
+        }
+    }
+    int wo[NB];
+#pragma unroll
+    for (int j = 0; j < NB; j++) {
+        const int R = (wave * NB + j) * 8 + sub;
+        const int c = (lane & 7) ^ ((R >> 1) & 7);
+        wo[j] = (int)(min(n0 + R, N - 1) * ldw) + 16 * c;
+    }
+
+    const __amdgpu_buffer_rsrc_t r0a = rsrc(a0.p0, a0.bytes0);
+    const __amdgpu_buffer_rsrc_t r0b = rsrc(a0.p1 ? a0.p1 : a0.p0, a0.p1 ? a0.bytes1 : a0.bytes0);
+    const __amdgpu_buffer_rsrc_t r1 = rsrc(a1.p0 ? a1.p0 : a0.p0, a1.p0 ? a1.bytes0 : 0u);
+    const __amdgpu_buffer_rsrc_t rw = rsrc(reinterpret_cast<const float*>(w), wbytes);
+
+    // issue the DMA of k tile kt into stage st (wave-uniform LDS bases)
+    auto issue = [&](int kt, int st) {
+        char* base = lds + st * STAGE_B;
+        const int k0 = kt * BK;
+        if (k0 < a0.k) {
+            const int kend = a0.k;
+            if (AMODE == GM_A_DENSE) {
+#pragma unroll
+                for (int j = 0; j < NA; j++) {
+                    const int off = k0 + 4 * cc[j] < kend ? so[j][0] + k0 * 4 : OOB;
+                    dma16(r0a, base + (wave * NA + j) * 1024, off);
+                }
+            } else {
+                const int seg = k0 / a0.hidden, ko = (k0 - seg * a0.hidden) * 4;
+#pragma unroll
+                for (int j = 0; j < NA; j++) {
+                    const int s = so[j][seg];
+                    dma16(seg == 0 ? r0a : r0b, base + (wave * NA + j) * 1024, s == OOB ? OOB : s + ko);
+                }
+            }
+        } else {
+            const int kk = k0 - a0.k;
+#pragma unroll
+            for (int j = 0; j < NA; j++) {
+                const int off = kk + 4 * cc[j] < a1.k ? o1[j] + kk * 4 : OOB;
+                dma16(r1, base + (wave * NA + j) * 1024, off);
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < NB; j++)
+            dma16(rw, base + BM * 128 + (wave * NB + j) * 1024, wo[j] + k0 * 4);
+    };
+
+    floatx16 acc[TM][TN];
+#pragma unroll
+    for (int i = 0; i < TM; i++)
+#pragma unroll
+        for (int j = 0; j < TN; j++)
+#pragma unroll
+            for (int r = 0; r < 16; r++) acc[i][j][r] = 0.f;
+
+    const int h = lane >> 5, l32 = lane & 31;
+    const int gsw = (l32 >> 1) & 7;  // swizzle of every fragment row this lane reads
+    const _Float16 s12 = (_Float16)(1.0f / 4096.0f);
+    // kend_t: columns >= kend_t of this tile are zero (ragged tail inside a 4-column chunk)
+    auto compute = [&](int st, int k0, bool tail, int kend) {
+        const char* ab = lds + st * STAGE_B + (wr * TM * 32 + l32) * 128;
+        const char* bb = lds + st * STAGE_B + BM * 128 + (wc * TN * 32 + l32) * 128;
+#pragma unroll
+        for (int sb = 0; sb < 2; sb++) {
+            half8 ah[TM], al[TM], bh[TN], bl[TN];
+#pragma unroll
+            for (int j = 0; j < TN; j++) {
+                bh[j] = *reinterpret_cast<const half8*>(bb + j * 32 * 128 + (((4 * sb + h) ^ gsw) << 4));
+                bl[j] = *reinterpret_cast<const half8*>(bb + j * 32 * 128 + (((4 * sb + 2 + h) ^ gsw) << 4));
+            }
+#pragma unroll
+            for (int i = 0; i < TM; i++) {
+                floatx4 x0 = *reinterpret_cast<const floatx4*>(ab + i * 32 * 128 + (((4 * sb + 2 * h) ^ gsw) << 4));
+                floatx4 x1 = *reinterpret_cast<const floatx4*>(ab + i * 32 * 128 + (((4 * sb + 2 * h + 1) ^ gsw) << 4));
+                if (tail) {  // last tile only (wave-uniform): zero the columns past the source end
+                    const int kc = k0 + 16 * sb + 8 * h;
+#pragma unroll
+                    for (int e = 0; e < 4; e++) {
+                        if (kc + e >= kend) x0[e] = 0.f;
+                        if (kc + 4 + e >= kend) x1[e] = 0.f;
+                    }
+                }
+                const half4 h0 = __builtin_convertvector(x0, half4), h1 = __builtin_convertvector(x1, half4);
+                const half4 l0 = __builtin_convertvector((x0 - __builtin_convertvector(h0, floatx4)) * 4096.0f, half4);
+                const half4 l1 = __builtin_convertvector((x1 - __builtin_convertvector(h1, floatx4)) * 4096.0f, half4);
+                ah[i] = __builtin_shufflevector(h0, h1, 0, 1, 2, 3, 4, 5, 6, 7);
+                al[i] = __builtin_shufflevector(l0, l1, 0, 1, 2, 3, 4, 5, 6, 7);
+            }
+#pragma unroll
+            for (int j = 0; j < TN; j++) {
+                const half8 bs = bh[j] * s12;  // w_hi * 2^-12, exact
+#pragma unroll
+                for (int i = 0; i < TM; i++) {
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[i], bs, acc[i][j], 0, 0, 0);
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[i], bl[j], acc[i][j], 0, 0, 0);
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[i], bh[j], acc[i][j], 0, 0, 0);
+                }
+            }
+        }
+    };
+
+    const int nk = (K + BK - 1) / BK;
+    // the source a k tile belongs to ends at a0.k (first source) or K (second)
+#pragma unroll
+    for (int p = 0; p < STAGES - 1; p++)
+        if (p < nk) issue(p, p);
+    // retire tile 0: the younger prologue tiles stay in flight
+    if (STAGES == 3 && nk > 1)
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NL) : "memory");
+    else
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    int st = 0;
+    for (int kt = 0; kt < nk; kt++) {
+        if (kt + STAGES - 1 < nk) issue(kt + STAGES - 1, (st + STAGES - 1) % STAGES);
+        const int k0 = kt * BK;
+        const int kend = k0 < a0.k ? a0.k : K;
+        compute(st, k0, k0 + BK > kend, kend);
+        if (kt + 1 < nk) {
+            // retire tile kt+1; tiles issued after it (kt+2 .. kt+STAGES-1) may stay in flight
+            if (STAGES == 3 && kt + 2 < nk)
+                asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NL) : "memory");
+            else
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_s_barrier();
+        }
+        st = st + 1 == STAGES ? 0 : st + 1;
+    }
+
+    const float si = *wscale_inv;  // undo the weight scale (a power of two: exact)
+#pragma unroll
+    for (int i = 0; i < TM; i++)
+#pragma unroll
+        for (int j = 0; j < TN; j++)
+#pragma unroll
+            for (int r = 0; r < 16; r++) acc[i][j][r] *= si;
+    epilogue<TM, TN, EPI>(acc, ep, m0 + wr * TM * 32, n0 + wc * TN * 32, M, N, lane);
+}
+
+template <int WGM, int WGN, int TM, int TN, int STAGES, int AMODE, int EPI, int OCC>
+int launch_g(const ASrc& a0, const ASrc& a1, const float* w, long long ldw, unsigned wbytes, int M, int N, int K,
+             const Epi& ep, hipStream_t st, const float* wscale_inv) {
+    constexpr int BM = WGM * TM * 32, BN = WGN * TN * 32;
+    const int T = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
+    hipLaunchKernelGGL((k_gemm3g<WGM, WGN, TM, TN, STAGES, AMODE, EPI, OCC>), dim3(T), dim3(WGM * WGN * 64), 0, st, a0,
+                       a1, reinterpret_cast<const _Float16*>(w), ldw, wbytes, M, N, K, ep, wscale_inv);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return gm_fail(GM_ERR_HIP, std::string("gm_gemm launch: ") + hipGetErrorString(e));
+    return GM_OK;
+}
+
 template <int WGM, int WGN, int TM, int TN, int BK_, int AMODE, int EPI, int OCC = 2, bool X3 = false>
 int launch(const ASrc& a0, const ASrc& a1, const float* w, long long ldw, unsigned wbytes, int M, int N, int K,
            const Epi& ep, hipStream_t st, const float* wscale_inv = nullptr) {
@@ -663,6 +880,37 @@ int dispatch(const ASrc& s0, const ASrc& s1, const float* w, long long ldw, unsi
     launch<WGM, WGN, TM, TN, BK_, AM, EP, 2, X3>(s0, s1, w, ldw, wb, m, n, K, ep, st, wsi)
 #define GM_L4(WGM, WGN, TM, TN, BK_, AM, EP) \
     launch<WGM, WGN, TM, TN, BK_, AM, EP, 4, X3>(s0, s1, w, ldw, wb, m, n, K, ep, st, wsi)
+    if constexpr (X3) {
+        // LDS-DMA kernel (tiles 8..11) for dense / readout sources
+#define GM_G(WGM, WGN, TM, TN, S, AM, EP, OC) \
+    launch_g<WGM, WGN, TM, TN, S, AM, EP, OC>(s0, s1, w, ldw, wb, m, n, K, ep, st, wsi)
+        if (tile >= 8 && s0.mode != GM_A_AGGREGATE) {
+            if (epilogue == GM_EPI_LSTM) {
+                ep.hidden = n / 4;
+                if (s0.mode != GM_A_DENSE) return gm_fail(GM_ERR_UNSUPPORTED, "gm_gemm: LSTM epilogue with readout source");
+                switch (tile) {
+                    case 8: return GM_G(4, 1, 1, 4, 3, GM_A_DENSE, EPI_LSTM, 1);
+                    case 9: return GM_G(4, 1, 1, 4, 2, GM_A_DENSE, EPI_LSTM, 2);
+                    case 10: return GM_G(4, 2, 1, 4, 2, GM_A_DENSE, EPI_LSTM, 1);
+                    default: return GM_G(2, 2, 2, 4, 2, GM_A_DENSE, EPI_LSTM, 1);
+                }
+            }
+            ep.act = epilogue == GM_EPI_BIAS_LEAKY ? 1 : 0;
+#define GM_GB(AM)                                                \
+    switch (tile) {                                              \
+        case 8: return GM_G(2, 2, 2, 2, 3, AM, EPI_BIAS, 1);     \
+        case 9: return GM_G(2, 2, 2, 2, 2, AM, EPI_BIAS, 2);     \
+        case 10: return GM_G(2, 4, 2, 2, 2, AM, EPI_BIAS, 1);    \
+        default: return GM_G(4, 2, 2, 2, 2, AM, EPI_BIAS, 1);    \
+    }
+            if (n > 32) {
+                if (s0.mode == GM_A_READOUT) GM_GB(GM_A_READOUT)
+                GM_GB(GM_A_DENSE)
+            }
+#undef GM_GB
+        }
+#undef GM_G
+    }
     if (epilogue == GM_EPI_LSTM) {
         ep.hidden = n / 4;
         if constexpr (X3) {
@@ -853,7 +1101,7 @@ extern "C" int gm_gemm_pack_x3(const float* w, int64_t ldw, int32_t n, int32_t k
 }
 
 extern "C" int gm_gemm_set_tile(int32_t tile) {
-    if (tile < -1 || tile > 4) return gm_fail(GM_ERR_INVALID_ARG, "gm_gemm_set_tile: tile in [-1, 4]");
+    if (tile < -1 || tile > 11) return gm_fail(GM_ERR_INVALID_ARG, "gm_gemm_set_tile: tile in [-1, 11]");
     g_tile = tile;
     return GM_OK;
 }

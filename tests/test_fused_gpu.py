@@ -164,3 +164,31 @@ def test_routing_node_encoder_vs_torch(n, out):
                                                                     lin.bias.double()), 0.01)
     err = (y.double() - ref).abs().max().item()
     assert err < 1e-5, err
+
+
+@pytest.mark.parametrize("tile", [8, 9, 10, 11])
+def test_gemm_lds_dma_tiles(tile):
+    """The LDS-DMA x3 kernel (tiles 8..11): dense (ragged M/N/K, padded rows), two sources
+    with the LSTM epilogue, and the DQN readout gather of the fused rollout, vs fp64 / torch."""
+    gm, M, FU, W = mods()
+    lib = FU._setup()
+    lib.gm_gemm_set_tile(tile)
+    try:
+        for (m, n, k, ldx) in [(81920, 512, 642, 644), (1000, 256, 512, 512), (777, 130, 90, 92),
+                               (4097, 33, 129, 132), (300, 64, 16, 16)]:
+            for epi in (0, 1):
+                test_gemm_dense_vs_torch(m, n, k, ldx, epi, "x3")
+        test_gemm_x3_error_is_fp32_order()
+
+        class MP:
+            def setattr(self, obj, name, val):
+                setattr(obj, name, val)
+        old = FU.L.GEMM_MODE
+        try:
+            test_gemm_two_sources_and_lstm_epilogue("x3", MP())
+            FU.L.GEMM_MODE = "x3"
+            test_fused_rollout_matches_unfused_path()
+        finally:
+            FU.L.GEMM_MODE = old
+    finally:
+        lib.gm_gemm_set_tile(-1)

@@ -17,6 +17,7 @@ def main():
     form = sys.argv[2] if len(sys.argv) > 2 else "x3"
     reps = int(sys.argv[3]) if len(sys.argv) > 3 else 10
     torch.manual_seed(0)
+    FU._setup().gm_gemm_set_tile(int(os.environ.get("GM_TILE", "-1")))
     m = 81920
     if name == "lstm_agg":
         H = 128
