@@ -88,9 +88,12 @@ __device__ __forceinline__ float4 bload(__amdgpu_buffer_rsrc_t r, int byte_off) 
     u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(r, byte_off, 0, 0);
     return make_float4(__uint_as_float(v.x), __uint_as_float(v.y), __uint_as_float(v.z), __uint_as_float(v.w));
 }
-// 16 B per lane from a buffer straight into LDS (lane-linear from the wave-uniform base)
-__device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, char* lds_base, int byte_off) {
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)lds_base, 16, byte_off, 0, 0,
+// 16 B per lane from a buffer straight into LDS (lane-linear from the wave-uniform base);
+// voff per lane, soff wave-uniform
+// (kept out of the kernel bodies: with the builtin inside a __global__ template, hipcc's host
+// pass silently drops the kernel's launch stub)
+__device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, char* lds_base, int voff, int soff) {
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)lds_base, 16, voff, soff, 0,
                                              0);
 }
 __device__ __forceinline__ float4 f4add(float4 a, float4 b) {
@@ -102,6 +105,32 @@ __device__ __forceinline__ void split4(float4 v, half4& hi, half4& lo) {
     const floatx4 a = {v.x, v.y, v.z, v.w};
     hi = __builtin_convertvector(a, half4);
     lo = __builtin_convertvector((a - __builtin_convertvector(hi, floatx4)) * 4096.0f, half4);
+}
+
+// The same split for 8 floats with 4 vector instructions per pair: hi = cvt_pk (RNE), X =
+// 4096 x (packed multiply, exact), lo = f16(fma(hi, -4096, X)) = f16(4096 (x - hi)) by
+// v_fma_mix{lo,hi}_f16 (the f16 hi read as f32 by the mixed fma; one rounding, RNE), the
+// same bits as split4.
+__device__ __forceinline__ void split8(floatx4 x0, floatx4 x1, half8& hi, half8& lo) {
+    typedef float floatx2 __attribute__((ext_vector_type(2)));
+    typedef _Float16 half2_t __attribute__((ext_vector_type(2)));
+    const float m4096 = -4096.0f;
+    unsigned hp[4], lp[4];
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+        const floatx2 x = q < 2 ? floatx2{x0[2 * q], x0[2 * q + 1]} : floatx2{x1[2 * q - 4], x1[2 * q - 3]};
+        hp[q] = __builtin_bit_cast(unsigned, __builtin_convertvector(x, half2_t));
+        const floatx2 X = x * 4096.0f;
+        unsigned l;
+        asm("v_fma_mixlo_f16 %0, %1, %2, %3 op_sel_hi:[1,0,0]" : "=&v"(l) : "v"(hp[q]), "s"(m4096), "v"(X[0]));
+        asm("v_fma_mixhi_f16 %0, %1, %2, %3 op_sel:[1,0,0] op_sel_hi:[1,0,0]"
+            : "+v"(l)
+            : "v"(hp[q]), "s"(m4096), "v"(X[1]));
+        lp[q] = l;
+    }
+    typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
+    hi = __builtin_bit_cast(half8, u32x4_t{hp[0], hp[1], hp[2], hp[3]});
+    lo = __builtin_bit_cast(half8, u32x4_t{lp[0], lp[1], lp[2], lp[3]});
 }
 
 // Epilogue of both forms. C/D map of the 32x32 MFMA tiles: col = lane & 31, row =
@@ -599,11 +628,13 @@ __global__ __launch_bounds__(WGM* WGN * 64, OCC) void k_gemm3(ASrc a0, ASrc a1, 
 // LDS image per stage: [BM rows of A | BN rows of B] x 128 B, 16-B chunks XOR-swizzled by
 // row (pos = chunk ^ ((row >> 1) & 7): conflict-free ds_read_b128 on the 32-row fragments);
 // the DMA writes lane-linear (8 rows per wave-instruction), so the swizzle is applied to the
-// per-lane SOURCE address. STAGES-deep ring: tile kt+STAGES-1 is issued at the top of step
-// kt, and a counted vmcnt + raw s_barrier at the bottom retires tile kt+1 only, so the
-// younger tiles stay in flight across the barrier. A sources: DENSE, READOUT (the 32-deep
-// tile lies inside one H-wide segment: per-lane segment row offsets; missing neighbours
-// read an out-of-range offset = zeros), then the optional dense second source.
+// per-lane SOURCE address. The k loop is unrolled by STAGES so every LDS stage offset is a
+// compile-time immediate; the per-lane DMA offsets are fixed over K (the k position goes in
+// the scalar offset) and the fragment addresses are fixed per lane, so the loop's vector ALU
+// work is the A split and the w_hi * 2^-12 scaling only. Tile kt+STAGES-1 is issued at the
+// top of step kt, and a counted vmcnt + raw s_barrier at the bottom retires tile kt+1 only.
+// A sources: DENSE, READOUT (the 32-deep tile lies inside one H-wide segment; missing
+// neighbours read an out-of-range offset = zeros), then the optional dense second source.
 template <int WGM, int WGN, int TM, int TN, int STAGES, int AMODE, int EPI, int OCC>
 __global__ __launch_bounds__(WGM* WGN * 64, OCC) void k_gemm3g(ASrc a0, ASrc a1, const _Float16* __restrict__ w,
                                                               long long ldw, unsigned wbytes, int M, int N, int K,
@@ -615,9 +646,11 @@ __global__ __launch_bounds__(WGM* WGN * 64, OCC) void k_gemm3g(ASrc a0, ASrc a1,
     constexpr int STAGE_B = (BM + BN) * 128;
     static_assert(BM % (8 * NW) == 0 && BN % (8 * NW) == 0, "tile rows per wave");
     static_assert(AMODE != GM_A_AGGREGATE, "aggregate source uses k_gemm3");
+    static_assert(STAGES == 2 || STAGES == 3, "stages");
     __shared__ __attribute__((aligned(16))) char lds[STAGES * STAGE_B];
 
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: LDS bases in SGPRs
     const int wr = wave / WGN, wc = wave % WGN;
     const int nM = (M + BM - 1) / BM, nN = (N + BN - 1) / BN;
     const int bid = xcd_remap(blockIdx.x, nM * nN);
@@ -628,12 +661,10 @@ __global__ __launch_bounds__(WGM* WGN * 64, OCC) void k_gemm3g(ASrc a0, ASrc a1,
     const int sub = lane >> 3;
     int so[NA][4];  // DENSE: [0]; READOUT: segment rows (OOB = none)
     int o1[NA];     // second (dense) source
-    int cc[NA];     // logical chunk of this lane's 16 B (k offset 4 cc)
 #pragma unroll
     for (int j = 0; j < NA; j++) {
         const int R = (wave * NA + j) * 8 + sub;
         const int c = (lane & 7) ^ ((R >> 1) & 7);
-        cc[j] = c;
         const int row = min(m0 + R, M - 1);
         o1[j] = (int)(row * a1.ld0) * 4 + 16 * c;
 #pragma unroll
@@ -665,37 +696,44 @@ __global__ __launch_bounds__(WGM* WGN * 64, OCC) void k_gemm3g(ASrc a0, ASrc a1,
     const __amdgpu_buffer_rsrc_t r1 = rsrc(a1.p0 ? a1.p0 : a0.p0, a1.p0 ? a1.bytes0 : 0u);
     const __amdgpu_buffer_rsrc_t rw = rsrc(reinterpret_cast<const float*>(w), wbytes);
 
-    // issue the DMA of k tile kt into stage st (wave-uniform LDS bases)
-    auto issue = [&](int kt, int st) {
-        char* base = lds + st * STAGE_B;
+    // DMA of k tile kt into stage ST (all LDS bases wave-uniform)
+    auto issue = [&](auto ST, int kt) {
+        char* base = lds + decltype(ST)::value * STAGE_B + wave * NA * 1024;
         const int k0 = kt * BK;
         if (k0 < a0.k) {
-            const int kend = a0.k;
             if (AMODE == GM_A_DENSE) {
 #pragma unroll
-                for (int j = 0; j < NA; j++) {
-                    const int off = k0 + 4 * cc[j] < kend ? so[j][0] + k0 * 4 : OOB;
-                    dma16(r0a, base + (wave * NA + j) * 1024, off);
-                }
+                for (int j = 0; j < NA; j++) dma16(r0a, base + j * 1024, so[j][0], k0 * 4);
             } else {
                 const int seg = k0 / a0.hidden, ko = (k0 - seg * a0.hidden) * 4;
+                // OOB + ko stays out of range, so missing neighbours need no select
+                switch (seg) {
+                    case 0:
 #pragma unroll
-                for (int j = 0; j < NA; j++) {
-                    const int s = so[j][seg];
-                    dma16(seg == 0 ? r0a : r0b, base + (wave * NA + j) * 1024, s == OOB ? OOB : s + ko);
+                        for (int j = 0; j < NA; j++) dma16(r0a, base + j * 1024, so[j][0], ko);
+                        break;
+                    case 1:
+#pragma unroll
+                        for (int j = 0; j < NA; j++) dma16(r0b, base + j * 1024, so[j][1], ko);
+                        break;
+                    case 2:
+#pragma unroll
+                        for (int j = 0; j < NA; j++) dma16(r0b, base + j * 1024, so[j][2], ko);
+                        break;
+                    default:
+#pragma unroll
+                        for (int j = 0; j < NA; j++) dma16(r0b, base + j * 1024, so[j][3], ko);
+                        break;
                 }
             }
         } else {
             const int kk = k0 - a0.k;
 #pragma unroll
-            for (int j = 0; j < NA; j++) {
-                const int off = kk + 4 * cc[j] < a1.k ? o1[j] + kk * 4 : OOB;
-                dma16(r1, base + (wave * NA + j) * 1024, off);
-            }
+            for (int j = 0; j < NA; j++) dma16(r1, base + j * 1024, o1[j], kk * 4);
         }
+        char* bbase = lds + decltype(ST)::value * STAGE_B + BM * 128 + wave * NB * 1024;
 #pragma unroll
-        for (int j = 0; j < NB; j++)
-            dma16(rw, base + BM * 128 + (wave * NB + j) * 1024, wo[j] + k0 * 4);
+        for (int j = 0; j < NB; j++) dma16(rw, bbase + j * 1024, wo[j], k0 * 4);
     };
 
     floatx16 acc[TM][TN];
@@ -708,36 +746,37 @@ __global__ __launch_bounds__(WGM* WGN * 64, OCC) void k_gemm3g(ASrc a0, ASrc a1,
 
     const int h = lane >> 5, l32 = lane & 31;
     const int gsw = (l32 >> 1) & 7;  // swizzle of every fragment row this lane reads
+    // per-lane fragment byte offsets inside a stage: A chunks (4 sb + 2 h + p), B hi/lo chunks
+    // (4 sb + 2 p + h); the stage and fragment-row offsets are immediates
+    int aoff[2][2], boff[2][2];
+#pragma unroll
+    for (int sb = 0; sb < 2; sb++)
+#pragma unroll
+        for (int p = 0; p < 2; p++) {
+            aoff[sb][p] = (wr * TM * 32 + l32) * 128 + (((4 * sb + 2 * h + p) ^ gsw) << 4);
+            boff[sb][p] = BM * 128 + (wc * TN * 32 + l32) * 128 + (((4 * sb + 2 * p + h) ^ gsw) << 4);
+        }
     const _Float16 s12 = (_Float16)(1.0f / 4096.0f);
-    // kend_t: columns >= kend_t of this tile are zero (ragged tail inside a 4-column chunk)
-    auto compute = [&](int st, int k0, bool tail, int kend) {
-        const char* ab = lds + st * STAGE_B + (wr * TM * 32 + l32) * 128;
-        const char* bb = lds + st * STAGE_B + BM * 128 + (wc * TN * 32 + l32) * 128;
+    auto compute = [&](auto ST) {
+        const char* sbase = lds + decltype(ST)::value * STAGE_B;
 #pragma unroll
         for (int sb = 0; sb < 2; sb++) {
             half8 ah[TM], al[TM], bh[TN], bl[TN];
 #pragma unroll
             for (int j = 0; j < TN; j++) {
-                bh[j] = *reinterpret_cast<const half8*>(bb + j * 32 * 128 + (((4 * sb + h) ^ gsw) << 4));
-                bl[j] = *reinterpret_cast<const half8*>(bb + j * 32 * 128 + (((4 * sb + 2 + h) ^ gsw) << 4));
+                bh[j] = *reinterpret_cast<const half8*>(sbase + boff[sb][0] + j * 32 * 128);
+                bl[j] = *reinterpret_cast<const half8*>(sbase + boff[sb][1] + j * 32 * 128);
             }
 #pragma unroll
             for (int i = 0; i < TM; i++) {
-                floatx4 x0 = *reinterpret_cast<const floatx4*>(ab + i * 32 * 128 + (((4 * sb + 2 * h) ^ gsw) << 4));
-                floatx4 x1 = *reinterpret_cast<const floatx4*>(ab + i * 32 * 128 + (((4 * sb + 2 * h + 1) ^ gsw) << 4));
-                if (tail) {  // last tile only (wave-uniform): zero the columns past the source end
-                    const int kc = k0 + 16 * sb + 8 * h;
-#pragma unroll
-                    for (int e = 0; e < 4; e++) {
-                        if (kc + e >= kend) x0[e] = 0.f;
-                        if (kc + 4 + e >= kend) x1[e] = 0.f;
-                    }
-                }
-                const half4 h0 = __builtin_convertvector(x0, half4), h1 = __builtin_convertvector(x1, half4);
-                const half4 l0 = __builtin_convertvector((x0 - __builtin_convertvector(h0, floatx4)) * 4096.0f, half4);
-                const half4 l1 = __builtin_convertvector((x1 - __builtin_convertvector(h1, floatx4)) * 4096.0f, half4);
-                ah[i] = __builtin_shufflevector(h0, h1, 0, 1, 2, 3, 4, 5, 6, 7);
-                al[i] = __builtin_shufflevector(l0, l1, 0, 1, 2, 3, 4, 5, 6, 7);
+                floatx4 x0 = *reinterpret_cast<const floatx4*>(sbase + aoff[sb][0] + i * 32 * 128);
+                floatx4 x1 = *reinterpret_cast<const floatx4*>(sbase + aoff[sb][1] + i * 32 * 128);
+#if GM_DIAG == 4  // diagnostic build: raw bits instead of the split (timing only)
+                ah[i] = __builtin_bit_cast(half8, x0);
+                al[i] = __builtin_bit_cast(half8, x1);
+#else
+                split8(x0, x1, ah[i], al[i]);
+#endif
             }
 #pragma unroll
             for (int j = 0; j < TN; j++) {
@@ -753,32 +792,56 @@ __global__ __launch_bounds__(WGM* WGN * 64, OCC) void k_gemm3g(ASrc a0, ASrc a1,
     };
 
     const int nk = (K + BK - 1) / BK;
-    // the source a k tile belongs to ends at a0.k (first source) or K (second)
-#pragma unroll
-    for (int p = 0; p < STAGES - 1; p++)
-        if (p < nk) issue(p, p);
-    // retire tile 0: the younger prologue tiles stay in flight
+    using I0 = std::integral_constant<int, 0>;
+    using I1 = std::integral_constant<int, 1>;
+    using I2 = std::integral_constant<int, 2>;
+    issue(I0{}, 0);
+    if (STAGES == 3 && nk > 1) issue(I1{}, 1);
     if (STAGES == 3 && nk > 1)
         asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NL) : "memory");
     else
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
-    int st = 0;
-    for (int kt = 0; kt < nk; kt++) {
-        if (kt + STAGES - 1 < nk) issue(kt + STAGES - 1, (st + STAGES - 1) % STAGES);
-        const int k0 = kt * BK;
-        const int kend = k0 < a0.k ? a0.k : K;
-        compute(st, k0, k0 + BK > kend, kend);
+    asm volatile("" ::: "memory");
+    // step kt on stage ST: issue tile kt+STAGES-1 into stage (ST+STAGES-1)%STAGES, compute,
+    // retire tile kt+1 (tiles issued after it stay in flight), barrier
+    // the DMA reads whatever lies past a ragged source end (in-buffer data, or zeros out of
+    // range); on the last tile those A columns are zeroed in LDS before the fragment reads
+    const int kend_last = (nk - 1) * BK < a0.k ? a0.k : K;
+    const bool ragged = kend_last < nk * BK;
+    auto step = [&](auto ST, int kt) {
+        constexpr int S = decltype(ST)::value;
+#if GM_DIAG != 5  // diagnostic build 5: no operand traffic in the k loop (timing only)
+        if (kt + STAGES - 1 < nk) issue(std::integral_constant<int, (S + STAGES - 1) % STAGES>{}, kt + STAGES - 1);
+#endif
+        if (ragged && kt == nk - 1) {  // wave-uniform; nothing is in flight any more
+            char* sa = lds + S * STAGE_B;
+            for (int e = tid; e < BM * BK; e += NW * 64) {
+                const int r = e / BK, c = e % BK;
+                if (kt * BK + c >= kend_last)
+                    *reinterpret_cast<float*>(sa + r * 128 + ((((c >> 2) ^ ((r >> 1) & 7))) << 4) + (c & 3) * 4) = 0.f;
+            }
+            __syncthreads();
+        }
+#if GM_DIAG != 6  // diagnostic build 6: operand traffic only, no fragment reads / MFMAs
+        compute(ST);
+#endif
         if (kt + 1 < nk) {
-            // retire tile kt+1; tiles issued after it (kt+2 .. kt+STAGES-1) may stay in flight
             if (STAGES == 3 && kt + 2 < nk)
                 asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NL) : "memory");
             else
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            // this step's fragment reads are retired before any wave can restage their buffer
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
             __builtin_amdgcn_s_barrier();
+            asm volatile("" ::: "memory");  // no LDS read is hoisted above the barrier
         }
-        st = st + 1 == STAGES ? 0 : st + 1;
+    };
+    for (int kt = 0; kt < nk; kt += STAGES) {
+        step(I0{}, kt);
+        if (kt + 1 < nk) step(I1{}, kt + 1);
+        if constexpr (STAGES == 3)
+            if (kt + 2 < nk) step(I2{}, kt + 2);
     }
 
     const float si = *wscale_inv;  // undo the weight scale (a power of two: exact)
@@ -888,20 +951,20 @@ int dispatch(const ASrc& s0, const ASrc& s1, const float* w, long long ldw, unsi
             if (epilogue == GM_EPI_LSTM) {
                 ep.hidden = n / 4;
                 if (s0.mode != GM_A_DENSE) return gm_fail(GM_ERR_UNSUPPORTED, "gm_gemm: LSTM epilogue with readout source");
-                switch (tile) {
-                    case 8: return GM_G(4, 1, 1, 4, 3, GM_A_DENSE, EPI_LSTM, 1);
-                    case 9: return GM_G(4, 1, 1, 4, 2, GM_A_DENSE, EPI_LSTM, 2);
-                    case 10: return GM_G(4, 2, 1, 4, 2, GM_A_DENSE, EPI_LSTM, 1);
-                    default: return GM_G(2, 2, 2, 4, 2, GM_A_DENSE, EPI_LSTM, 1);
+                switch (tile) {  // 8 waves each
+                    case 8: return GM_G(4, 2, 2, 4, 2, GM_A_DENSE, EPI_LSTM, 1);   // 256x256
+                    case 9: return GM_G(4, 2, 1, 4, 3, GM_A_DENSE, EPI_LSTM, 1);   // 128x256, 3 stages
+                    case 10: return GM_G(4, 2, 1, 4, 2, GM_A_DENSE, EPI_LSTM, 1);  // 128x256, 2 stages
+                    default: return GM_G(8, 1, 1, 4, 2, GM_A_DENSE, EPI_LSTM, 1);  // 256x128
                 }
             }
             ep.act = epilogue == GM_EPI_BIAS_LEAKY ? 1 : 0;
 #define GM_GB(AM)                                                \
     switch (tile) {                                              \
-        case 8: return GM_G(2, 2, 2, 2, 3, AM, EPI_BIAS, 1);     \
-        case 9: return GM_G(2, 2, 2, 2, 2, AM, EPI_BIAS, 2);     \
-        case 10: return GM_G(2, 4, 2, 2, 2, AM, EPI_BIAS, 1);    \
-        default: return GM_G(4, 2, 2, 2, 2, AM, EPI_BIAS, 1);    \
+        case 8: return GM_G(4, 2, 2, 4, 2, AM, EPI_BIAS, 1);     \
+        case 9: return GM_G(4, 2, 1, 4, 3, AM, EPI_BIAS, 1);     \
+        case 10: return GM_G(4, 2, 1, 4, 2, AM, EPI_BIAS, 1);    \
+        default: return GM_G(8, 1, 1, 4, 2, AM, EPI_BIAS, 1);    \
     }
             if (n > 32) {
                 if (s0.mode == GM_A_READOUT) GM_GB(GM_A_READOUT)

@@ -3,7 +3,7 @@
 # k loop, 3: as 2 without barriers) into graph-marl_amd/lib/diagN/ (timing only, wrong results).
 cd "$(dirname "$0")/../graph-marl_amd/csrc" || exit 1
 make -s || exit 1
-for d in 1 2 3; do
+for d in ${DIAGS:-1 2 3}; do
   mkdir -p ../lib/diag$d
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -I../../include -DGM_DIAG=$d -c gm_gemm.hip -o ../lib/diag$d/gm_gemm.o || exit 1
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o ../lib/diag$d/libgraphmarl_amd.so ../lib/obj/gm_env.o \
