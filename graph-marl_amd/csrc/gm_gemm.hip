@@ -99,7 +99,13 @@ __device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, char* lds_base, 
 __device__ __forceinline__ float4 f4add(float4 a, float4 b) {
     return make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w);
 }
-__device__ __forceinline__ float sigm(float x) { return 1.0f / (1.0f + expf(-x)); }
+// LSTM gate nonlinearities on the hardware transcendentals (v_exp_f32 / v_rcp_f32, ~1 ulp
+// each): sigma(x) = 1 / (1 + 2^(-x log2 e)), tanh(x) = 2 sigma(2x) - 1; absolute error
+// < 1e-6, against the 1e-5 tolerance of the NetMon outputs (expf/divide/tanhf cost ~4x)
+__device__ __forceinline__ float sigm(float x) {
+    return __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(-1.44269504088896341f * x));
+}
+__device__ __forceinline__ float tanh_fast(float x) { return 2.0f * sigm(2.0f * x) - 1.0f; }
 // a = hi + 2^-12 lo with hi = f16(a) (RNE), lo = f16((a - hi) * 2^12)
 __device__ __forceinline__ void split4(float4 v, half4& hi, half4& lo) {
     const floatx4 a = {v.x, v.y, v.z, v.w};
@@ -171,10 +177,10 @@ __device__ __forceinline__ void epilogue(floatx16 (&acc)[TM][TN], const Epi& ep,
                 if (row >= M || unit >= H) continue;
                 float gi = sigm(acc[i][0][r] + bgate[0]);
                 float gf = sigm(acc[i][1][r] + bgate[1]);
-                float gg = tanhf(acc[i][2][r] + bgate[2]);
+                float gg = tanh_fast(acc[i][2][r] + bgate[2]);
                 float go = sigm(acc[i][3][r] + bgate[3]);
                 float cn = gf * ep.c_in[(long long)row * ep.ldc + unit] + gi * gg;
-                float hn = go * tanhf(cn);
+                float hn = go * tanh_fast(cn);
                 ep.y[(long long)row * ep.ldy + unit] = hn;
                 ep.y2[(long long)row * ep.ldy2 + unit] = cn;
                 if (ep.act_out) {
@@ -757,35 +763,46 @@ __global__ __launch_bounds__(WGM* WGN * 64, OCC) void k_gemm3g(ASrc a0, ASrc a1,
             boff[sb][p] = BM * 128 + (wc * TN * 32 + l32) * 128 + (((4 * sb + 2 * p + h) ^ gsw) << 4);
         }
     const _Float16 s12 = (_Float16)(1.0f / 4096.0f);
+    // all fragment reads of the step (both 16-deep halves) are issued first and pinned there,
+    // so the second half's LDS latency hides behind the first half's MFMAs
     auto compute = [&](auto ST) {
         const char* sbase = lds + decltype(ST)::value * STAGE_B;
+        floatx4 xa[2][TM][2];
+        half8 bh[2][TN], bl[2][TN];
 #pragma unroll
         for (int sb = 0; sb < 2; sb++) {
-            half8 ah[TM], al[TM], bh[TN], bl[TN];
-#pragma unroll
-            for (int j = 0; j < TN; j++) {
-                bh[j] = *reinterpret_cast<const half8*>(sbase + boff[sb][0] + j * 32 * 128);
-                bl[j] = *reinterpret_cast<const half8*>(sbase + boff[sb][1] + j * 32 * 128);
-            }
 #pragma unroll
             for (int i = 0; i < TM; i++) {
-                floatx4 x0 = *reinterpret_cast<const floatx4*>(sbase + aoff[sb][0] + i * 32 * 128);
-                floatx4 x1 = *reinterpret_cast<const floatx4*>(sbase + aoff[sb][1] + i * 32 * 128);
+                xa[sb][i][0] = *reinterpret_cast<const floatx4*>(sbase + aoff[sb][0] + i * 32 * 128);
+                xa[sb][i][1] = *reinterpret_cast<const floatx4*>(sbase + aoff[sb][1] + i * 32 * 128);
+            }
+#pragma unroll
+            for (int j = 0; j < TN; j++) {
+                bh[sb][j] = *reinterpret_cast<const half8*>(sbase + boff[sb][0] + j * 32 * 128);
+                bl[sb][j] = *reinterpret_cast<const half8*>(sbase + boff[sb][1] + j * 32 * 128);
+            }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int sb = 0; sb < 2; sb++) {
+            half8 ah[TM], al[TM];
+#pragma unroll
+            for (int i = 0; i < TM; i++) {
 #if GM_DIAG == 4  // diagnostic build: raw bits instead of the split (timing only)
-                ah[i] = __builtin_bit_cast(half8, x0);
-                al[i] = __builtin_bit_cast(half8, x1);
+                ah[i] = __builtin_bit_cast(half8, xa[sb][i][0]);
+                al[i] = __builtin_bit_cast(half8, xa[sb][i][1]);
 #else
-                split8(x0, x1, ah[i], al[i]);
+                split8(xa[sb][i][0], xa[sb][i][1], ah[i], al[i]);
 #endif
             }
 #pragma unroll
             for (int j = 0; j < TN; j++) {
-                const half8 bs = bh[j] * s12;  // w_hi * 2^-12, exact
+                const half8 bs = bh[sb][j] * s12;  // w_hi * 2^-12, exact
 #pragma unroll
                 for (int i = 0; i < TM; i++) {
                     acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[i], bs, acc[i][j], 0, 0, 0);
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[i], bl[j], acc[i][j], 0, 0, 0);
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[i], bh[j], acc[i][j], 0, 0, 0);
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[i], bl[sb][j], acc[i][j], 0, 0, 0);
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[i], bh[sb][j], acc[i][j], 0, 0, 0);
                 }
             }
         }
@@ -837,6 +854,9 @@ __global__ __launch_bounds__(WGM* WGN * 64, OCC) void k_gemm3g(ASrc a0, ASrc a1,
             asm volatile("" ::: "memory");  // no LDS read is hoisted above the barrier
         }
     };
+#if GM_DIAG == 7  // diagnostic build 7: prologue + epilogue only (timing only)
+    if (nk < 0)
+#endif
     for (int kt = 0; kt < nk; kt += STAGES) {
         step(I0{}, kt);
         if (kt + 1 < nk) step(I1{}, kt + 1);
@@ -947,11 +967,13 @@ int dispatch(const ASrc& s0, const ASrc& s1, const float* w, long long ldw, unsi
         // LDS-DMA kernel (tiles 8..11) for dense / readout sources
 #define GM_G(WGM, WGN, TM, TN, S, AM, EP, OC) \
     launch_g<WGM, WGN, TM, TN, S, AM, EP, OC>(s0, s1, w, ldw, wb, m, n, K, ep, st, wsi)
-        if (tile >= 8 && s0.mode != GM_A_AGGREGATE) {
+        // default: the readout-sourced DQN layer (the rollout's largest GEMM) on tile 10
+        const int gt = tile >= 8 ? tile : (tile == -1 && s0.mode == GM_A_READOUT && n > 128 ? 10 : 0);
+        if (gt >= 8 && s0.mode != GM_A_AGGREGATE) {
             if (epilogue == GM_EPI_LSTM) {
                 ep.hidden = n / 4;
                 if (s0.mode != GM_A_DENSE) return gm_fail(GM_ERR_UNSUPPORTED, "gm_gemm: LSTM epilogue with readout source");
-                switch (tile) {  // 8 waves each
+                switch (gt) {  // 8 waves each
                     case 8: return GM_G(4, 2, 2, 4, 2, GM_A_DENSE, EPI_LSTM, 1);   // 256x256
                     case 9: return GM_G(4, 2, 1, 4, 3, GM_A_DENSE, EPI_LSTM, 1);   // 128x256, 3 stages
                     case 10: return GM_G(4, 2, 1, 4, 2, GM_A_DENSE, EPI_LSTM, 1);  // 128x256, 2 stages
@@ -960,7 +982,7 @@ int dispatch(const ASrc& s0, const ASrc& s1, const float* w, long long ldw, unsi
             }
             ep.act = epilogue == GM_EPI_BIAS_LEAKY ? 1 : 0;
 #define GM_GB(AM)                                                \
-    switch (tile) {                                              \
+    switch (gt) {                                              \
         case 8: return GM_G(4, 2, 2, 4, 2, AM, EPI_BIAS, 1);     \
         case 9: return GM_G(4, 2, 1, 4, 3, AM, EPI_BIAS, 1);     \
         case 10: return GM_G(4, 2, 1, 4, 2, AM, EPI_BIAS, 1);    \
