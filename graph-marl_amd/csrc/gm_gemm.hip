@@ -139,11 +139,33 @@ __device__ __forceinline__ void split8(floatx4 x0, floatx4 x1, half8& hi, half8&
     lo = __builtin_bit_cast(half8, u32x4_t{lp[0], lp[1], lp[2], lp[3]});
 }
 
+// LSTM epilogue input c, loaded into registers before the k loop (the loads retire behind
+// the MFMAs instead of one dependent HBM round trip per output row in the epilogue)
+template <int TM, int EPI>
+struct CIn {
+    float v[TM][16];
+};
+template <int TM>
+struct CIn<TM, EPI_BIAS> {};
+template <int TM, int EPI>
+__device__ __forceinline__ void cin_load(CIn<TM, EPI>& c, const Epi& ep, int wm0, int wn0, int M, int lane) {
+    if constexpr (EPI == EPI_LSTM) {
+        const int h = lane >> 5, unit = (wn0 >> 2) + (lane & 31);
+#pragma unroll
+        for (int i = 0; i < TM; i++)
+#pragma unroll
+            for (int r = 0; r < 16; r++) {
+                const int row = wm0 + i * 32 + 4 * h + (r & 3) + 8 * (r >> 2);
+                c.v[i][r] = (row < M && unit < ep.hidden) ? ep.c_in[(long long)row * ep.ldc + unit] : 0.f;
+            }
+    }
+}
+
 // Epilogue of both forms. C/D map of the 32x32 MFMA tiles: col = lane & 31, row =
 // (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5); wave tile origin (wm0, wn0).
 template <int TM, int TN, int EPI>
 __device__ __forceinline__ void epilogue(floatx16 (&acc)[TM][TN], const Epi& ep, int wm0, int wn0, int M, int N,
-                                         int lane) {
+                                         int lane, const CIn<TM, EPI>& cin) {
     const int h = lane >> 5, l32 = lane & 31;
     if constexpr (EPI == EPI_BIAS) {
 #pragma unroll
@@ -179,7 +201,7 @@ __device__ __forceinline__ void epilogue(floatx16 (&acc)[TM][TN], const Epi& ep,
                 float gf = sigm(acc[i][1][r] + bgate[1]);
                 float gg = tanh_fast(acc[i][2][r] + bgate[2]);
                 float go = sigm(acc[i][3][r] + bgate[3]);
-                float cn = gf * ep.c_in[(long long)row * ep.ldc + unit] + gi * gg;
+                float cn = gf * cin.v[i][r] + gi * gg;
                 float hn = go * tanh_fast(cn);
                 ep.y[(long long)row * ep.ldy + unit] = hn;
                 ep.y2[(long long)row * ep.ldy2 + unit] = cn;
@@ -395,7 +417,9 @@ __global__ __launch_bounds__(WGM* WGN * 64, OCC) void k_gemm(ASrc a0, ASrc a1, c
         __syncthreads();
     }
 
-    epilogue<TM, TN, EPI>(acc, ep, m0 + wr * TM * 32, n0 + wc * TN * 32, M, N, lane);
+    CIn<TM, EPI> cin;
+    cin_load<TM, EPI>(cin, ep, m0 + wr * TM * 32, n0 + wc * TN * 32, M, lane);
+    epilogue<TM, TN, EPI>(acc, ep, m0 + wr * TM * 32, n0 + wc * TN * 32, M, N, lane, cin);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -623,7 +647,9 @@ __global__ __launch_bounds__(WGM* WGN * 64, OCC) void k_gemm3(ASrc a0, ASrc a1, 
         for (int j = 0; j < TN; j++)
 #pragma unroll
             for (int r = 0; r < 16; r++) acc[i][j][r] *= si;
-    epilogue<TM, TN, EPI>(acc, ep, m0 + wr * TM * 32, n0 + wc * TN * 32, M, N, lane);
+    CIn<TM, EPI> cin;
+    cin_load<TM, EPI>(cin, ep, m0 + wr * TM * 32, n0 + wc * TN * 32, M, lane);
+    epilogue<TM, TN, EPI>(acc, ep, m0 + wr * TM * 32, n0 + wc * TN * 32, M, N, lane, cin);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -742,6 +768,8 @@ __global__ __launch_bounds__(WGM* WGN * 64, OCC) void k_gemm3g(ASrc a0, ASrc a1,
         for (int j = 0; j < NB; j++) dma16(rw, bbase + j * 1024, wo[j], k0 * 4);
     };
 
+    CIn<TM, EPI> cin;
+    cin_load<TM, EPI>(cin, ep, m0 + wr * TM * 32, n0 + wc * TN * 32, M, lane);
     floatx16 acc[TM][TN];
 #pragma unroll
     for (int i = 0; i < TM; i++)
@@ -763,96 +791,125 @@ __global__ __launch_bounds__(WGM* WGN * 64, OCC) void k_gemm3g(ASrc a0, ASrc a1,
             boff[sb][p] = BM * 128 + (wc * TN * 32 + l32) * 128 + (((4 * sb + 2 * p + h) ^ gsw) << 4);
         }
     const _Float16 s12 = (_Float16)(1.0f / 4096.0f);
-    // all fragment reads of the step (both 16-deep halves) are issued first and pinned there,
-    // so the second half's LDS latency hides behind the first half's MFMAs
-    auto compute = [&](auto ST) {
+    // fragments of one 16-deep half (SB) of a k tile: A raw fp32 (split at use), B hi / lo
+    struct Frag {
+        floatx4 xa[TM][2];
+        half8 bh[TN], bl[TN];
+    };
+    auto read = [&](auto ST, auto SB, Frag& f) {
+        constexpr int sb = decltype(SB)::value;
         const char* sbase = lds + decltype(ST)::value * STAGE_B;
-        floatx4 xa[2][TM][2];
-        half8 bh[2][TN], bl[2][TN];
 #pragma unroll
-        for (int sb = 0; sb < 2; sb++) {
-#pragma unroll
-            for (int i = 0; i < TM; i++) {
-                xa[sb][i][0] = *reinterpret_cast<const floatx4*>(sbase + aoff[sb][0] + i * 32 * 128);
-                xa[sb][i][1] = *reinterpret_cast<const floatx4*>(sbase + aoff[sb][1] + i * 32 * 128);
-            }
-#pragma unroll
-            for (int j = 0; j < TN; j++) {
-                bh[sb][j] = *reinterpret_cast<const half8*>(sbase + boff[sb][0] + j * 32 * 128);
-                bl[sb][j] = *reinterpret_cast<const half8*>(sbase + boff[sb][1] + j * 32 * 128);
-            }
+        for (int i = 0; i < TM; i++) {
+            f.xa[i][0] = *reinterpret_cast<const floatx4*>(sbase + aoff[sb][0] + i * 32 * 128);
+            f.xa[i][1] = *reinterpret_cast<const floatx4*>(sbase + aoff[sb][1] + i * 32 * 128);
         }
-        __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-        for (int sb = 0; sb < 2; sb++) {
-            half8 ah[TM], al[TM];
+        for (int j = 0; j < TN; j++) {
+            f.bh[j] = *reinterpret_cast<const half8*>(sbase + boff[sb][0] + j * 32 * 128);
+            f.bl[j] = *reinterpret_cast<const half8*>(sbase + boff[sb][1] + j * 32 * 128);
+        }
+    };
+    auto mfma = [&](const Frag& f) {
+        half8 ah[TM], al[TM];
+#pragma unroll
+        for (int i = 0; i < TM; i++) {
+#if GM_DIAG == 10
+            ah[i] = __builtin_bit_cast(half8, f.xa[i][0]);
+            al[i] = __builtin_bit_cast(half8, f.xa[i][1]);
+#else
+            split8(f.xa[i][0], f.xa[i][1], ah[i], al[i]);
+#endif
+        }
+#pragma unroll
+        for (int j = 0; j < TN; j++) {
+#if GM_DIAG == 10
+            const half8 bs = f.bh[j];
+#else
+            const half8 bs = f.bh[j] * s12;  // w_hi * 2^-12, exact
+#endif
 #pragma unroll
             for (int i = 0; i < TM; i++) {
-#if GM_DIAG == 4  // diagnostic build: raw bits instead of the split (timing only)
-                ah[i] = __builtin_bit_cast(half8, xa[sb][i][0]);
-                al[i] = __builtin_bit_cast(half8, xa[sb][i][1]);
-#else
-                split8(xa[sb][i][0], xa[sb][i][1], ah[i], al[i]);
-#endif
-            }
-#pragma unroll
-            for (int j = 0; j < TN; j++) {
-                const half8 bs = bh[sb][j] * s12;  // w_hi * 2^-12, exact
-#pragma unroll
-                for (int i = 0; i < TM; i++) {
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[i], bs, acc[i][j], 0, 0, 0);
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[i], bl[sb][j], acc[i][j], 0, 0, 0);
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[i], bh[sb][j], acc[i][j], 0, 0, 0);
-                }
+                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[i], bs, acc[i][j], 0, 0, 0);
+                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[i], f.bl[j], acc[i][j], 0, 0, 0);
+                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[i], f.bh[j], acc[i][j], 0, 0, 0);
             }
         }
     };
 
     const int nk = (K + BK - 1) / BK;
+    // the DMA reads whatever lies past a ragged source end (in-buffer data, or zeros out of
+    // range); once the last tile has landed, those A columns are zeroed in LDS (all waves,
+    // then a barrier) before its first fragment read
+    const int kend_last = (nk - 1) * BK < a0.k ? a0.k : K;
+    const bool ragged = kend_last < nk * BK;
+    auto zero_tail = [&](auto ST) {
+        char* sa = lds + decltype(ST)::value * STAGE_B;
+        for (int e = tid; e < BM * BK; e += NW * 64) {
+            const int r = e / BK, c = e % BK;
+            if ((nk - 1) * BK + c >= kend_last)
+                *reinterpret_cast<float*>(sa + r * 128 + ((((c >> 2) ^ ((r >> 1) & 7))) << 4) + (c & 3) * 4) = 0.f;
+        }
+        __syncthreads();
+    };
     using I0 = std::integral_constant<int, 0>;
     using I1 = std::integral_constant<int, 1>;
     using I2 = std::integral_constant<int, 2>;
+    // Pipeline, one barrier per k tile placed MID-step: tile t lives in stage t % STAGES.
+    //   step k: read half 1 of tile k | MFMAs half 0 of tile k | wait own DMA of tile k+1,
+    //   lgkmcnt(0), barrier B_k | DMA tile k+STAGES into stage k (every wave is past its reads
+    //   of tile k) | read half 0 of tile k+1 | MFMAs half 1 of tile k
+    // so every fragment read overlaps the MFMAs of the other half, and a DMA has STAGES-1
+    // steps to land.
     issue(I0{}, 0);
-    if (STAGES == 3 && nk > 1) issue(I1{}, 1);
-    if (STAGES == 3 && nk > 1)
-        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NL) : "memory");
-    else
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (nk > 1) issue(I1{}, 1);
+    if constexpr (STAGES == 3)
+        if (nk > 2) issue(I2{}, 2);
+    {
+        const int out = min(STAGES - 1, nk - 1);  // tiles issued after tile 0
+        if (out >= 2)
+            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * NL) : "memory");
+        else if (out == 1)
+            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NL) : "memory");
+        else
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
-    // step kt on stage ST: issue tile kt+STAGES-1 into stage (ST+STAGES-1)%STAGES, compute,
-    // retire tile kt+1 (tiles issued after it stay in flight), barrier
-    // the DMA reads whatever lies past a ragged source end (in-buffer data, or zeros out of
-    // range); on the last tile those A columns are zeroed in LDS before the fragment reads
-    const int kend_last = (nk - 1) * BK < a0.k ? a0.k : K;
-    const bool ragged = kend_last < nk * BK;
+    if (ragged && nk == 1) zero_tail(I0{});
+    Frag f0, f1;
+    read(I0{}, I0{}, f0);
+#if GM_DIAG == 10
+    read(I0{}, I1{}, f1);
+#endif
     auto step = [&](auto ST, int kt) {
         constexpr int S = decltype(ST)::value;
-#if GM_DIAG != 5  // diagnostic build 5: no operand traffic in the k loop (timing only)
-        if (kt + STAGES - 1 < nk) issue(std::integral_constant<int, (S + STAGES - 1) % STAGES>{}, kt + STAGES - 1);
-#endif
-        if (ragged && kt == nk - 1) {  // wave-uniform; nothing is in flight any more
-            char* sa = lds + S * STAGE_B;
-            for (int e = tid; e < BM * BK; e += NW * 64) {
-                const int r = e / BK, c = e % BK;
-                if (kt * BK + c >= kend_last)
-                    *reinterpret_cast<float*>(sa + r * 128 + ((((c >> 2) ^ ((r >> 1) & 7))) << 4) + (c & 3) * 4) = 0.f;
-            }
-            __syncthreads();
-        }
-#if GM_DIAG != 6  // diagnostic build 6: operand traffic only, no fragment reads / MFMAs
-        compute(ST);
-#endif
+        using SN = std::integral_constant<int, (S + 1) % STAGES>;
+#if GM_DIAG == 10  // diagnostic build 10: MFMAs only in the k loop (timing only)
+        mfma(f0);
+        mfma(f1);
+        if (kt < 0) {
+#else
+        read(ST, I1{}, f1);
+        __builtin_amdgcn_sched_barrier(0);
+        mfma(f0);
+        __builtin_amdgcn_sched_barrier(0);
         if (kt + 1 < nk) {
+#endif
+            // own DMA of tile kt+1 landed (tiles kt+2 .. kt+STAGES-1 may stay in flight)
             if (STAGES == 3 && kt + 2 < nk)
                 asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NL) : "memory");
             else
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            // this step's fragment reads are retired before any wave can restage their buffer
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's reads of tile kt done
             __builtin_amdgcn_s_barrier();
-            asm volatile("" ::: "memory");  // no LDS read is hoisted above the barrier
+            asm volatile("" ::: "memory");  // no LDS access moves across the barrier
+            if (kt + STAGES < nk) issue(ST, kt + STAGES);
+            if (ragged && kt + 1 == nk - 1) zero_tail(SN{});
+            read(SN{}, I0{}, f0);
         }
+        __builtin_amdgcn_sched_barrier(0);
+        mfma(f1);
     };
 #if GM_DIAG == 7  // diagnostic build 7: prologue + epilogue only (timing only)
     if (nk < 0)
@@ -871,7 +928,7 @@ __global__ __launch_bounds__(WGM* WGN * 64, OCC) void k_gemm3g(ASrc a0, ASrc a1,
         for (int j = 0; j < TN; j++)
 #pragma unroll
             for (int r = 0; r < 16; r++) acc[i][j][r] *= si;
-    epilogue<TM, TN, EPI>(acc, ep, m0 + wr * TM * 32, n0 + wc * TN * 32, M, N, lane);
+    epilogue<TM, TN, EPI>(acc, ep, m0 + wr * TM * 32, n0 + wc * TN * 32, M, N, lane, cin);
 }
 
 template <int WGM, int WGN, int TM, int TN, int STAGES, int AMODE, int EPI, int OCC>
@@ -964,7 +1021,7 @@ int dispatch(const ASrc& s0, const ASrc& s1, const float* w, long long ldw, unsi
 #define GM_L4(WGM, WGN, TM, TN, BK_, AM, EP) \
     launch<WGM, WGN, TM, TN, BK_, AM, EP, 4, X3>(s0, s1, w, ldw, wb, m, n, K, ep, st, wsi)
     if constexpr (X3) {
-        // LDS-DMA kernel (tiles 8..11) for dense / readout sources
+        // LDS-DMA kernel (tiles 8..14) for dense / readout sources
 #define GM_G(WGM, WGN, TM, TN, S, AM, EP, OC) \
     launch_g<WGM, WGN, TM, TN, S, AM, EP, OC>(s0, s1, w, ldw, wb, m, n, K, ep, st, wsi)
         // default: the readout-sourced DQN layer (the rollout's largest GEMM) on tile 10
@@ -977,6 +1034,9 @@ int dispatch(const ASrc& s0, const ASrc& s1, const float* w, long long ldw, unsi
                     case 8: return GM_G(4, 2, 2, 4, 2, GM_A_DENSE, EPI_LSTM, 1);   // 256x256
                     case 9: return GM_G(4, 2, 1, 4, 3, GM_A_DENSE, EPI_LSTM, 1);   // 128x256, 3 stages
                     case 10: return GM_G(4, 2, 1, 4, 2, GM_A_DENSE, EPI_LSTM, 1);  // 128x256, 2 stages
+                    case 12:  // 128x128, 4 waves, 2 blocks/CU (tile 13's 64x64 waves cannot hold a gate group)
+                    case 13: return GM_G(4, 1, 1, 4, 2, GM_A_DENSE, EPI_LSTM, 2);
+                    case 14: return GM_G(2, 2, 2, 4, 2, GM_A_DENSE, EPI_LSTM, 1);  // 128x256, 64x128 waves
                     default: return GM_G(8, 1, 1, 4, 2, GM_A_DENSE, EPI_LSTM, 1);  // 256x128
                 }
             }
@@ -986,6 +1046,9 @@ int dispatch(const ASrc& s0, const ASrc& s1, const float* w, long long ldw, unsi
         case 8: return GM_G(4, 2, 2, 4, 2, AM, EPI_BIAS, 1);     \
         case 9: return GM_G(4, 2, 1, 4, 3, AM, EPI_BIAS, 1);     \
         case 10: return GM_G(4, 2, 1, 4, 2, AM, EPI_BIAS, 1);    \
+        case 12: return GM_G(4, 1, 1, 4, 2, AM, EPI_BIAS, 2);    \
+        case 13: return GM_G(2, 2, 2, 2, 2, AM, EPI_BIAS, 2);    \
+        case 14: return GM_G(2, 2, 2, 4, 2, AM, EPI_BIAS, 1);    \
         default: return GM_G(8, 1, 1, 4, 2, AM, EPI_BIAS, 1);    \
     }
             if (n > 32) {

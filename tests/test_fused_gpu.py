@@ -166,9 +166,9 @@ def test_routing_node_encoder_vs_torch(n, out):
     assert err < 1e-5, err
 
 
-@pytest.mark.parametrize("tile", [8, 9, 10, 11])
+@pytest.mark.parametrize("tile", [8, 9, 10, 11, 12, 13, 14])
 def test_gemm_lds_dma_tiles(tile):
-    """The LDS-DMA x3 kernel (tiles 8..11): dense (ragged M/N/K, padded rows), two sources
+    """The LDS-DMA x3 kernel (tiles 8..14): dense (ragged M/N/K, padded rows), two sources
     with the LSTM epilogue, and the DQN readout gather of the fused rollout, vs fp64 / torch."""
     gm, M, FU, W = mods()
     lib = FU._setup()
