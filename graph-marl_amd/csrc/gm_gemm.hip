@@ -55,7 +55,7 @@ typedef float floatx4 __attribute__((ext_vector_type(4)));
 
 constexpr int BKMAX = 32;            // largest K tile of any configuration (host-side checks)
 constexpr int OOB = 0x7ff00000;       // byte offset beyond any buffer: load returns 0
-enum { EPI_BIAS = 0, EPI_LSTM = 1 };
+enum { EPI_BIAS = 0, EPI_LSTM = 1, EPI_HEAD = 2 };
 
 struct ASrc {
     int mode;                 // GM_A_DENSE / GM_A_AGGREGATE / GM_A_READOUT
@@ -79,6 +79,12 @@ struct Epi {
     long long ldc;
     float* act_out;           // EPI_LSTM: [M][4H] activations i,f,g,o (optional)
     int hidden;
+    const float* wq;          // EPI_HEAD: head weights [nq][ldwq], bias bq, out q [M][ldq]
+    long long ldwq;
+    const float* bq;
+    int nq;
+    float* q;
+    long long ldq;
 };
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const float* p, unsigned bytes) {
@@ -142,11 +148,11 @@ __device__ __forceinline__ void split8(floatx4 x0, floatx4 x1, half8& hi, half8&
 // LSTM epilogue input c, loaded into registers before the k loop (the loads retire behind
 // the MFMAs instead of one dependent HBM round trip per output row in the epilogue)
 template <int TM, int EPI>
-struct CIn {
+struct CIn {};
+template <int TM>
+struct CIn<TM, EPI_LSTM> {
     float v[TM][16];
 };
-template <int TM>
-struct CIn<TM, EPI_BIAS> {};
 template <int TM, int EPI>
 __device__ __forceinline__ void cin_load(CIn<TM, EPI>& c, const Epi& ep, int wm0, int wn0, int M, int lane) {
     if constexpr (EPI == EPI_LSTM) {
@@ -214,6 +220,78 @@ __device__ __forceinline__ void epilogue(floatx16 (&acc)[TM][TN], const Epi& ep,
                 }
             }
         }
+    }
+}
+
+// EPI_HEAD (block spans all N columns, n0 = 0): y = act(acc + b) stays in registers and
+// q[row][a] = bq[a] + sum_col y[row][col] wq[a][col] (a < nq <= 4). Per lane, the partial
+// dot products of its TN columns for its 16 rows x 4 heads (64 values) are reduce-scattered
+// over the 32 lanes of its half (xor 16..1: 62 shuffles, lane l ends with entries 2l, 2l+1
+// of row r = l >> 1, heads 2 (l & 1) + t); the WGN column waves are summed through LDS.
+template <int TM, int TN, int WGN, int BM>
+__device__ __forceinline__ void head_epilogue(floatx16 (&acc)[TM][TN], const Epi& ep, char* lds, int m0, int wr,
+                                              int wc, int M, int N, int lane, int tid) {
+    const int h = lane >> 5, l32 = lane & 31;
+    float bv[TN], wqv[TN][4];
+#pragma unroll
+    for (int j = 0; j < TN; j++) {
+        const int col = wc * TN * 32 + j * 32 + l32;
+        bv[j] = (ep.bias && col < N) ? ep.bias[col] : 0.f;
+#pragma unroll
+        for (int a = 0; a < 4; a++) wqv[j][a] = (col < N && a < ep.nq) ? ep.wq[a * ep.ldwq + col] : 0.f;
+    }
+    float* qp = reinterpret_cast<float*>(lds);  // [WGN][BM][4]
+    float red[TM][2];
+#pragma unroll
+    for (int i = 0; i < TM; i++) {
+        float x[64];
+#pragma unroll
+        for (int e = 0; e < 64; e++) x[e] = 0.f;
+#pragma unroll
+        for (int j = 0; j < TN; j++) {
+            const int col = wc * TN * 32 + j * 32 + l32;
+#pragma unroll
+            for (int r = 0; r < 16; r++) {
+                float y = acc[i][j][r] + bv[j];
+                if (ep.act == 1) y = y >= 0.f ? y : 0.01f * y;
+                if (ep.y) {
+                    const int row = m0 + wr * TM * 32 + i * 32 + 4 * h + (r & 3) + 8 * (r >> 2);
+                    if (row < M && col < N) ep.y[(long long)row * ep.ldy + col] = y;
+                }
+#pragma unroll
+                for (int a = 0; a < 4; a++) x[r * 4 + a] = fmaf(y, wqv[j][a], x[r * 4 + a]);
+            }
+        }
+#pragma unroll
+        for (int mask = 16, n = 32; mask >= 1; mask >>= 1, n >>= 1) {
+            const bool up = (l32 & mask) != 0;
+#pragma unroll
+            for (int k = 0; k < n; k++) {
+                const float mine = up ? x[n + k] : x[k];
+                const float other = up ? x[k] : x[n + k];
+                x[k] = mine + __shfl_xor(other, mask);
+            }
+        }
+        red[i][0] = x[0];
+        red[i][1] = x[1];
+    }
+    __syncthreads();  // every wave is done with the operand stages
+#pragma unroll
+    for (int i = 0; i < TM; i++) {
+        const int r = l32 >> 1;
+        const int rl = wr * TM * 32 + i * 32 + 4 * h + (r & 3) + 8 * (r >> 2);
+        const int a = 2 * (l32 & 1);
+        qp[(wc * BM + rl) * 4 + a] = red[i][0];
+        qp[(wc * BM + rl) * 4 + a + 1] = red[i][1];
+    }
+    __syncthreads();
+    for (int e = tid; e < BM * 4; e += WGN * (BM / TM / 32) * 64) {
+        const int rl = e >> 2, a = e & 3, row = m0 + rl;
+        if (a >= ep.nq || row >= M) continue;
+        float v = ep.bq ? ep.bq[a] : 0.f;
+#pragma unroll
+        for (int w = 0; w < WGN; w++) v += qp[(w * BM + rl) * 4 + a];
+        ep.q[(long long)row * ep.ldq + a] = v;
     }
 }
 
@@ -928,7 +1006,10 @@ __global__ __launch_bounds__(WGM* WGN * 64, OCC) void k_gemm3g(ASrc a0, ASrc a1,
         for (int j = 0; j < TN; j++)
 #pragma unroll
             for (int r = 0; r < 16; r++) acc[i][j][r] *= si;
-    epilogue<TM, TN, EPI>(acc, ep, m0 + wr * TM * 32, n0 + wc * TN * 32, M, N, lane, cin);
+    if constexpr (EPI == EPI_HEAD)
+        head_epilogue<TM, TN, WGN, BM>(acc, ep, lds, m0, wr, wc, M, N, lane, tid);
+    else
+        epilogue<TM, TN, EPI>(acc, ep, m0 + wr * TM * 32, n0 + wc * TN * 32, M, N, lane, cin);
 }
 
 template <int WGM, int WGN, int TM, int TN, int STAGES, int AMODE, int EPI, int OCC>
@@ -1226,6 +1307,36 @@ extern "C" int gm_gemm_x3(const gm_a_src* a0, const gm_a_src* a1, const void* wp
                           int64_t ldy2, const float* c_in, int64_t ldc, float* act_out, void* stream) {
     return gemm_entry(true, a0, a1, wp, 0, wscale_inv, b, m, n, epilogue, y, ldy, y2, ldy2, c_in, ldc, act_out,
                       stream);
+}
+
+extern "C" int gm_gemm_x3_head(const gm_a_src* a0, const void* wp, const float* wscale_inv, const float* b,
+                               int32_t m, int32_t n, int32_t act, const float* wq, int64_t ldwq, const float* bq,
+                               int32_t nq, float* q, int64_t ldq, float* y, int64_t ldy, void* stream) {
+    if (!a0 || a0->mode != GM_A_DENSE || !wp || !wscale_inv || !wq || !q || m <= 0 || n <= 0 || n > 256 ||
+        nq <= 0 || nq > 4 || ldwq < n || ldq < nq || (y && ldy < n) || (act != 0 && act != 1) ||
+        (reinterpret_cast<uintptr_t>(wp) & 15))
+        return gm_fail(GM_ERR_INVALID_ARG, "gm_gemm_x3_head: bad arguments (dense source, n <= 256, nq <= 4)");
+    ASrc s0, s1;
+    int rc = to_asrc(a0, m, s0);
+    if (rc) return rc;
+    memset(&s1, 0, sizeof(s1));
+    const int K = s0.k;
+    const long long ldw = (long long)((K + BKMAX - 1) / BKMAX * BKMAX) / 16 * 64, wb = (long long)n * ldw;
+    if (!fits(wb)) return gm_fail(GM_ERR_UNSUPPORTED, "gm_gemm_x3_head: weights larger than 2 GB");
+    Epi ep;
+    memset(&ep, 0, sizeof(ep));
+    ep.bias = b;
+    ep.act = act;
+    ep.y = y;
+    ep.ldy = ldy;
+    ep.wq = wq;
+    ep.ldwq = ldwq;
+    ep.bq = bq;
+    ep.nq = nq;
+    ep.q = q;
+    ep.ldq = ldq;
+    return launch_g<4, 2, 1, 4, 2, GM_A_DENSE, EPI_HEAD, 1>(s0, s1, static_cast<const float*>(wp), ldw, (unsigned)wb, m,
+                                                          n, K, ep, (hipStream_t)stream, wscale_inv);
 }
 
 extern "C" int64_t gm_gemm_pack_x3_bytes(int32_t n, int32_t k) {

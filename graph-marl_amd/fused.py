@@ -40,6 +40,8 @@ def _setup():
                                     C.c_int32, vp, C.c_int64, vp, C.c_int64, vp, C.c_int64, vp, vp]
         lib.gm_gemm_x3.argtypes = [C.POINTER(ASrc), C.POINTER(ASrc), vp, vp, vp, C.c_int32, C.c_int32,
                                    C.c_int32, vp, C.c_int64, vp, C.c_int64, vp, C.c_int64, vp, vp]
+        lib.gm_gemm_x3_head.argtypes = [C.POINTER(ASrc), vp, vp, vp, C.c_int32, C.c_int32, C.c_int32, vp, C.c_int64,
+                                        vp, C.c_int32, vp, C.c_int64, vp, C.c_int64, vp]
         lib._gemm_ready = True
     return lib
 
@@ -169,6 +171,29 @@ def pack_x3(lin):
         lin._packed_x3 = Packed()
     return lin._packed_x3.get(_key(lin.weight), lambda: X3(lin.weight, lin.weight.stride(0), lin.out_features,
                                                            lin.in_features))
+
+
+def head_ok(lin, fc):
+    """The last hidden layer and the Q head run as one kernel (gm_gemm_x3_head) in the split
+    form when the layer is at most 256 wide and the head at most 4 outputs, both with bias."""
+    return (use_x3(lin.out_features) and lin.out_features <= 256 and fc.out_features <= 4 and fc.act == 0
+            and fc.in_features == lin.out_features and lin.bias is not None and fc.bias is not None)
+
+
+def linear_head(lin, fc, x, ldx, k, q, y=None):
+    """q = fc(act(x @ W^T + b)) without writing the hidden activation (written to y if given)."""
+    lib = _setup()
+    x3 = pack_x3(lin)
+    M = q.shape[0]
+    wq = fc.weight if fc.weight.is_contiguous() else fc.weight.contiguous()
+    tag = lin.tag and f"linear:{lin.tag}+head:{M}x{lin.out_features}x{k}"
+    with L.timed(tag):
+        L.check(lib.gm_gemm_x3_head(C.byref(dense(x.data_ptr(), ldx, k)), x3.wp.data_ptr(), x3.sinv.data_ptr(),
+                                    lin.bias.data_ptr(), M, lin.out_features, int(lin.act == 1), wq.data_ptr(),
+                                    wq.stride(0), fc.bias.data_ptr(), fc.out_features, q.data_ptr(), q.stride(0),
+                                    None if y is None else y.data_ptr(), 0 if y is None else y.stride(0),
+                                    L.stream_ptr()))
+    return q
 
 
 def _linear(x, ldx, k, lin, out):
@@ -323,6 +348,11 @@ def dqn_q(dqn, env_obs, obs_dim, state, h_prev, nbr, agent_node, scratch):
          GM_EPI_BIAS_LEAKY if lin0.act == 1 else GM_EPI_BIAS, h1.data_ptr(), h1.stride(0),
          tag=lin0.tag and f"linear:{lin0.tag}:{M}x{lin0.out_features}x{a0.k + obs_dim}", x3=x3)
     h = h1
-    for i, lin in enumerate(list(dqn.encoder.linear_layers[1:]) + [dqn.q_net.fc]):
+    hidden = list(dqn.encoder.linear_layers[1:])
+    fc = dqn.q_net.fc
+    fuse = len(hidden) > 0 and head_ok(hidden[-1], fc)
+    for i, lin in enumerate(hidden[:-1] if fuse else hidden + [fc]):
         h = _linear(h, h.stride(0), h.shape[1], lin, scratch(i + 1, M, lin.out_features))
+    if fuse:  # last hidden layer + Q head in one kernel
+        h = linear_head(hidden[-1], fc, h, h.stride(0), h.shape[1], scratch(len(hidden) + 1, M, fc.out_features))
     return h

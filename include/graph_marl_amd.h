@@ -22,6 +22,7 @@
  *   gm_linear_f32                    nn.Linear (+ leaky_relu of MLP)        src/model.py:13-42, 119-125
  *   gm_gemm_f32                      Linear / LSTMCell GEMMs with aggregate, readout and gate math fused
  *   gm_gemm_x3 / gm_gemm_pack_x3     the same GEMMs in split-f16 form (f16 MFMA, fp32 accumulate)
+ *   gm_gemm_x3_head                  last DQN layer + Q head in one kernel
  *   gm_agent_attention               AttModel attention core (DGN)          src/model.py:86-117
  *   gm_agent_comm                    CommNet communication step             src/model.py:780-787
  */
@@ -233,6 +234,14 @@ int gm_gemm_f32(const gm_a_src* src0, const gm_a_src* src1, const float* w, int6
 int gm_gemm_x3(const gm_a_src* src0, const gm_a_src* src1, const void* wp, const float* wscale_inv, const float* b,
                int32_t m, int32_t n, int32_t epilogue, float* y, int64_t ldy, float* y2, int64_t ldy2,
                const float* c_in, int64_t ldc, float* act_out, void* stream);
+/* Last DQN encoder layer + Q head in one kernel (split-f16 form for the layer, fp32 head):
+ * q[m][nq] = Wq · act(src0 · W^T + b) + bq, act 0 none / 1 leaky_relu(0.01); the hidden
+ * activation stays in registers (also written to y when y != NULL). src0 DENSE, n <= 256,
+ * nq <= 4, wq [nq][ldwq] fp32. Replaces encoder.linear_layers[-1] + Q_Net.fc of the
+ * reference DQN (src/model.py:119-125, 187-203). */
+int gm_gemm_x3_head(const gm_a_src* src0, const void* wp, const float* wscale_inv, const float* b, int32_t m,
+                    int32_t n, int32_t act, const float* wq, int64_t ldwq, const float* bq, int32_t nq, float* q,
+                    int64_t ldq, float* y, int64_t ldy, void* stream);
 /* Packed size in bytes of an [n][k] weight for gm_gemm_x3: n * ceil(k/32)*2 blocks * 64 B. */
 int64_t gm_gemm_pack_x3_bytes(int32_t n, int32_t k);
 /* Split W [n][ldw] (first k columns) into wp (16-byte aligned, gm_gemm_pack_x3_bytes):

@@ -192,3 +192,33 @@ def test_gemm_lds_dma_tiles(tile):
             FU.L.GEMM_MODE = old
     finally:
         lib.gm_gemm_set_tile(-1)
+
+
+@pytest.mark.parametrize("m,n,k,ldx,nq", [(81920, 256, 512, 512, 4), (1000, 256, 512, 516, 4), (777, 100, 90, 92, 2),
+                                          (33, 256, 256, 256, 3), (5, 64, 16, 16, 1)])
+@pytest.mark.parametrize("act", [0, 1])
+def test_gemm_x3_head_vs_torch(m, n, k, ldx, nq, act):
+    """gm_gemm_x3_head (last DQN layer + Q head in one kernel) vs fp64: q within the rollout
+    tolerance, and the optional hidden output equal to the plain split-f16 GEMM's."""
+    gm, M, FU, W = mods()
+    torch.manual_seed(m + n + k + nq)
+    buf = torch.randn(m, ldx, device="cuda")
+    x = buf[:, :k]
+    lin = M.Linear(k, n, act=act).cuda()
+    fc = M.Linear(n, nq, act=0).cuda()
+    assert FU.head_ok(lin, fc) == (FU.L.GEMM_MODE == "x3")
+    if FU.L.GEMM_MODE != "x3":
+        pytest.skip("split-f16 form disabled (GM_GEMM=f32)")
+    q = torch.full((m, nq), float("nan"), device="cuda")
+    y = torch.empty(m, n, device="cuda")
+    FU.linear_head(lin, fc, buf, ldx, k, q, y=y)
+    hid = F.linear(x.double(), lin.weight.double(), lin.bias.double())
+    if act == 1:
+        hid = F.leaky_relu(hid)
+    ref = F.linear(hid, fc.weight.double(), fc.bias.double())
+    tol = 1e-5 * max(1.0, k ** 0.5 / 8)
+    assert (y.double() - hid).abs().max().item() < tol
+    assert (q.double() - ref).abs().max().item() < tol * max(1.0, n ** 0.5 / 8)
+    q2 = torch.full((m, nq), float("nan"), device="cuda")
+    FU.linear_head(lin, fc, buf, ldx, k, q2)  # without the hidden output: same q
+    assert torch.equal(q, q2)
