@@ -30,7 +30,8 @@ DQN = ["dqn.enc0(K=642)", "dqn.enc1(K=512)", "dqn.q(K=256)"]
 # k_gemm (gm_gemm_f32, fused path): encoder layer 0 runs in k_routing_enc, the LSTM
 # cells carry their gate epilogue, the DQN's first layer gathers the NetMon readout
 NETMON_G = ["netmon.enc1(K=512)", "netmon.enc2(K=256)", "netmon.rnn_obs(K=128+128)", "netmon.rnn_update(K=agg128+128)"]
-DQN_G = ["dqn.enc0(K=512 readout+130)", "dqn.enc1(K=512)", "dqn.q(K=256)"]
+DQN_G = ["dqn.enc0(K=512 readout+130)", "dqn.enc1+q(K=512, Q head fused)"]
+DQN_G3 = ["dqn.enc0(K=512 readout+130)", "dqn.enc1(K=512)", "dqn.q(K=256)"]  # before gm_gemm_x3_head
 
 
 def linear_labels(n_dispatch, episode_steps, netmon_iters=1, netmon=NETMON, dqn=DQN):
@@ -48,11 +49,11 @@ def linear_labels(n_dispatch, episode_steps, netmon_iters=1, netmon=NETMON, dqn=
     return out[:n_dispatch]
 
 
-def relabel(rows, episode_steps):
+def relabel(rows, episode_steps, dqn_g=DQN_G):
     for r in rows:  # k_gemm3<...> (split-f16 form) and k_gemm<...> (f32) are one call-site sequence
         if "k_gemm3" in r["Kernel_Name"] or r["Kernel_Name"].startswith("k_gemm") or "k_gemmI" in r["Kernel_Name"]:
             r["Kernel_Name"] = "k_gemm"
-    for name, nm, dq in (("k_linear_f32", NETMON, DQN), ("k_gemm", NETMON_G, DQN_G)):
+    for name, nm, dq in (("k_linear_f32", NETMON, DQN), ("k_gemm", NETMON_G, dqn_g)):
         lin = [r for r in rows if r["Kernel_Name"].startswith(name)]
         for r, lab in zip(lin, linear_labels(len(lin), episode_steps, netmon=nm, dqn=dq)):
             r["Kernel_Name"] = f"{name}[{lab}]"
@@ -66,11 +67,13 @@ def main():
     ap.add_argument("--write")
     ap.add_argument("--top", type=int, default=20)
     ap.add_argument("--episode-steps", type=int, default=50)
+    ap.add_argument("--unfused-head", action="store_true", help="profiles taken before gm_gemm_x3_head")
     a = ap.parse_args()
+    dqn_g = DQN_G3 if a.unfused_head else DQN_G
     dur = defaultdict(list)
     trace = load(a.trace)
     trace.sort(key=lambda r: int(r["Start_Timestamp"]))
-    for r in relabel(trace, a.episode_steps):
+    for r in relabel(trace, a.episode_steps, dqn_g):
         dur[key(r)].append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
     pmc = defaultdict(dict)
     for name, path in (("FETCH_SIZE", a.fetch), ("WRITE_SIZE", a.write)):
@@ -79,7 +82,7 @@ def main():
         acc = defaultdict(list)
         rows = [r for r in load(path) if r["Counter_Name"] == name]
         rows.sort(key=lambda r: int(r["Dispatch_Id"]))
-        for r in relabel(rows, a.episode_steps):
+        for r in relabel(rows, a.episode_steps, dqn_g):
             if r["Counter_Name"] == name:
                 acc[key(r)].append(float(r["Counter_Value"]))
         for k, v in acc.items():
