@@ -1258,11 +1258,9 @@ int gemm_entry(bool x3, const gm_a_src* a0, const gm_a_src* a1, const void* w, i
 __global__ void k_absmax(const float* __restrict__ w, long long ldw, int n, int k, float* __restrict__ wsi) {
     __shared__ float red[16];
     float m = 0.f;
-    const long long tot = (long long)n * k;
-    for (long long i = threadIdx.x; i < tot; i += blockDim.x) {
-        const long long r = i / k, c = i - r * k;
-        m = fmaxf(m, fabsf(w[r * ldw + c]));
-    }
+    const int wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    for (int r = wave; r < n; r += nw)  // one row per wave at a time, lanes over columns (coalesced)
+        for (int c = threadIdx.x & 63; c < k; c += 64) m = fmaxf(m, fabsf(w[(long long)r * ldw + c]));
     for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
     if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
     __syncthreads();

@@ -238,11 +238,13 @@ __global__ __launch_bounds__(256) void k_routing_enc(const float* __restrict__ x
 #pragma unroll
     for (int j = 0; j < CPL; j++) bias[j] = b ? b[c0 + col + j] : 0.f;
     const long long M = (long long)G * N;
-    // each wave owns 64 consecutive rows: lane l gathers the 11 nonzero features of row
-    // base + l up front (coalesced, one latency), the row loop broadcasts them by readlane
-    const long long base = (long long)blockIdx.x * rows_per_block + (long long)wv * 64;
-    if (base >= M) return;
-    const int nrows = M - base < 64 ? (int)(M - base) : 64;
+    // each wave owns groups of 64 consecutive rows: lane l gathers the 11 nonzero features of
+    // row base + l up front (coalesced, one latency), the row loop broadcasts them by readlane;
+    // the block's W^T slice is staged once for rows_per_block rows
+    const long long bend = min(M, (long long)(blockIdx.x + 1) * rows_per_block);
+    for (long long base = (long long)blockIdx.x * rows_per_block + (long long)wv * 64; base < bend;
+         base += (blockDim.x >> 6) * 64) {
+    const int nrows = bend - base < 64 ? (int)(bend - base) : 64;
     int fv = 0, f_nb[3] = {0, 0, 0};
     float f_cnt = 0.f, f_tl = 0.f, f_len[3] = {0.f, 0.f, 0.f}, f_ld[3] = {0.f, 0.f, 0.f};
     if (lane < nrows) {
@@ -291,6 +293,7 @@ __global__ __launch_bounds__(256) void k_routing_enc(const float* __restrict__ x
 #pragma unroll
             for (int j = 0; j < CPL; j++) yr[j] = act ? (acc[j] >= 0.f ? acc[j] : 0.01f * acc[j]) : acc[j];
         }
+    }
     }
 }
 
@@ -406,7 +409,7 @@ extern "C" int gm_routing_node_encoder(const float* x, int64_t ldx, const int32_
     const size_t lds = (size_t)K * 64 * cpl * 4;
     if (lds > 65536) return gm_fail(GM_ERR_UNSUPPORTED, "gm_routing_node_encoder: 4N+8 too large for the LDS slice");
     const long long M = (long long)G * N;
-    const int rows = 256;
+    const int rows = 256;  // 64 rows per wave (512 / 1024 / 2048: +/-0 / +17 / +52 % time)
     dim3 grid((unsigned)((M + rows - 1) / rows), (unsigned)(n / (64 * cpl)));
     if (cpl == 2)
         hipLaunchKernelGGL(k_routing_enc<2>, grid, dim3(256), lds, (hipStream_t)stream, x, (long long)ldx, nbr, G, N,

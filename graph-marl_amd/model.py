@@ -3,7 +3,9 @@
 Parameter names match the reference's state_dicts (MLP.linear_layers.*,
 nn.LSTMCell weight_ih/weight_hh/bias_ih/bias_hh, q_net.fc.*), so reference
 checkpoints load unchanged. The forward arithmetic runs in libgraphmarl_amd:
-  * gm_linear_f32          every nn.Linear (+ MLP leaky_relu), fp32 MFMA
+  * gm_gemm_x3             every nn.Linear wider than 32 outputs (+ MLP leaky_relu): the
+                           split-f16 MFMA form with fp32-order error (GM_GEMM=f32 or narrow
+                           layers: gm_linear_f32, exact fp32 MFMA)
   * gm_lstm_pointwise      nn.LSTMCell gate math
   * gm_mp_aggregate        SimpleAggregation (sum / mean over I + A)
   * gm_netmon_readout      [h, last neighbour h] readout fused with the agent gather
@@ -30,11 +32,24 @@ def _pad_stride(k):
 
 
 class _WeightCache:
-    """fp32 weight with its row stride padded to a multiple of 4 (16-byte rows)."""
+    """fp32 weight with its row stride padded to a multiple of 4 (16-byte rows), and its
+    split-f16 packing for gm_gemm_x3 (both refreshed when the parameter changes)."""
 
     def __init__(self):
         self.key = None
         self.val = None
+        self.key3 = None
+        self.val3 = None
+
+    def x3(self, w):
+        from . import fused as FU
+
+        key = (w.data_ptr(), w._version)
+        if self.key3 != key:
+            wp, ldw = self.get(w)
+            self.val3 = FU.X3(wp, ldw, w.shape[0], w.shape[1])
+            self.key3 = key
+        return self.val3
 
     def get(self, w):
         n, k = w.shape
@@ -56,6 +71,14 @@ def linear_raw(x2d, ldx, k, w, b, act, out=None, ldy=None, wcache=None, tag=None
     if out is None:
         out = torch.empty(m, n, device=x2d.device, dtype=torch.float32)
         ldy = n
+    from . import fused as FU
+
+    if FU.use_x3(n) and ldx % 4 == 0 and x2d.data_ptr() % 16 == 0:
+        # split-f16 form (fp32-order error, tests/test_fused_gpu.py), as in the rollout
+        x3 = (wcache if wcache is not None else _WeightCache()).x3(w)
+        FU.gemm(FU.dense(x2d.data_ptr(), ldx, k), None, wp.data_ptr(), ldw, L.ptr(b), m, n, act, out.data_ptr(), ldy,
+                tag=tag and f"linear:{tag}:{m}x{n}x{k}", x3=x3)
+        return out
     with L.timed(tag and f"linear:{tag}:{m}x{n}x{k}"):
         L.check(L.lib().gm_linear_f32(L.ptr(x2d), ldx, L.ptr(wp), ldw, L.ptr(b), m, n, k, act, L.ptr(out), ldy,
                                       _s()))
@@ -87,6 +110,8 @@ class LinearFn(torch.autograd.Function):
         gy = gy.reshape(-1, w.shape[0])
         if ctx.act == 1:
             gy = torch.where(y >= 0, gy, 0.01 * gy)
+        # input/weight gradients stay on the library fp32 GEMMs: gradients are far below the
+        # f16 range the split form needs (|a| >= 2^-15 for a normal low piece)
         gx = gy @ w if ctx.needs_input_grad[0] else None
         gw = gy.t() @ x2 if ctx.needs_input_grad[1] else None
         gb = gy.sum(0) if ctx.needs_input_grad[2] else None
