@@ -54,7 +54,7 @@ typedef enum {
 
 typedef struct {
     int32_t n_env;
-    int32_t n_nodes;        /* --n-router, even, <= 64          */
+    int32_t n_nodes;        /* --n-router, even, 4..128          */
     int32_t n_data;         /* --n-data (agents), <= 64          */
     int32_t env_var;        /* --env-var: 1 INDEPENDENT, 2 WITH_K_NEIGHBORS, 3 GLOBAL (routing.py:268-358) */
     int32_t congestion;     /* !--no-congestion                  */
