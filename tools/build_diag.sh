@@ -1,8 +1,8 @@
 #!/bin/bash
 # Diagnostic builds of the GEMM into graph-marl_amd/lib/diagN/ (timing only, wrong results).
 # k_gemm3 (GM_DIAG 1: no A split, 2: no operand traffic in the k loop, 3: as 2 without barriers);
-# k_gemm3g (4: no split, 5: no DMA in the loop, 6: no fragment reads / MFMAs, 7: prologue +
-# epilogue only, 8: no barrier in the k loop, 9: no fragment reads in the k loop).
+# k_gemm3g (7: prologue + epilogue only, 10: MFMAs only in the k loop). Results of the removed
+# variants (no split / no DMA / no fragment reads / no barrier, 16x16x32 MFMAs): DESIGN.md 4a.
 cd "$(dirname "$0")/../graph-marl_amd/csrc" || exit 1
 make -s || exit 1
 for d in ${DIAGS:-1 2 3}; do
