@@ -149,16 +149,32 @@ __host__ __device__ __forceinline__ int obs_dim_of(int N, int env_var, int k) {
 }
 
 // node observation entry (routing.py:187-235) from the per-node packet count / size sums
+// (block k, offset q) of column r of the 3 neighbour blocks of N+2 columns (no division)
+__device__ __forceinline__ void nbr_block(int r, int N, int& k, int& q) {
+    k = (r >= N + 2) + (r >= 2 * (N + 2));
+    q = r - k * (N + 2);
+}
+
+// value of neighbour-block column (k, q) of node v: onehot(nbr) | edge length | edge load
+template <class ES>
+__device__ __forceinline__ float nbr_block_value(const ES& s, int N, int v, int k, int q) {
+    const int nb = s.nbr[v * 3 + k], ne = s.nbr_edge[v * 3 + k];
+    return q < N ? (float)(nb == q) : (q == N ? (float)s.elen[ne] : (float)s.load[ne]);
+}
+
 template <class ES>
 __device__ __forceinline__ float node_obs_value(const ES& s, int N, int j, int c) {
     if (c < N) return (float)(c == j);
     if (c == N) return s.node_cnt[j];
     if (c == N + 1) return s.node_load[j];
-    int r = c - (N + 2), k = r / (N + 2), q = r - k * (N + 2);
-    if (q < N) return (float)(s.nbr[j * 3 + k] == q);
-    if (q == N) return (float)s.elen[s.nbr_edge[j * 3 + k]];
-    return (float)s.load[s.nbr_edge[j * 3 + k]];
+    int k, q;
+    nbr_block(c - (N + 2), N, k, q);
+    return nbr_block_value(s, N, j, k, q);
 }
+
+
+// Observation rows are one-hot blocks plus a few scalars: zero-fill (one flat lane-strided
+// pass), then each lane writes the entries of its own row (no per-column branch chains).
 
 template <class ES>
 __device__ void emit_obs(const EnvDev& d, int env, ES& s, const gm_obs_buffers& o) {
@@ -180,10 +196,31 @@ __device__ void emit_obs(const EnvDev& d, int env, ES& s, const gm_obs_buffers& 
         }
         __syncthreads();
         if (o.node_obs) {
+            // routing.py:187-235. Rows are mostly zeros: zero-fill the env's N x (4N+8) block
+            // (contiguous), then each lane writes the 12 nonzero-capable entries of node v
             const int ND = 4 * N + 8;
             float* base = o.node_obs + (size_t)env * N * ND;
-            for (int j = 0; j < N; j++)
-                for (int c = l; c < ND; c += WAVE) base[(size_t)j * ND + c] = node_obs_value(s, N, j, c);
+            if ((reinterpret_cast<uintptr_t>(base) & 15) == 0) {  // N*ND is a multiple of 4
+                for (int idx = l; idx < N * ND / 4; idx += WAVE)
+                    reinterpret_cast<float4*>(base)[idx] = make_float4(0.f, 0.f, 0.f, 0.f);
+            } else {
+                for (int idx = l; idx < N * ND; idx += WAVE) base[idx] = 0.f;
+            }
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // zeros land before the entries
+            for (int v = l; v < N; v += WAVE) {
+                float* row = base + (size_t)v * ND;
+                row[v] = 1.f;
+                row[N] = s.node_cnt[v];
+                row[N + 1] = s.node_load[v];
+#pragma unroll
+                for (int k = 0; k < 3; k++) {
+                    float* blk = row + N + 2 + k * (N + 2);
+                    const int ne = s.nbr_edge[v * 3 + k];
+                    blk[s.nbr[v * 3 + k]] = 1.f;
+                    blk[N] = (float)s.elen[ne];
+                    blk[N + 1] = (float)s.load[ne];
+                }
+            }
         }
     }
     if (o.obs && d.env_var == 2) {
@@ -202,15 +239,54 @@ __device__ void emit_obs(const EnvDev& d, int env, ES& s, const gm_obs_buffers& 
         __syncthreads();
     }
     if (o.obs) {
+        // routing.py:269-315. The INDEPENDENT part of a row has at most 16 nonzero entries:
+        // zero-fill columns [0, 6N+10) of all A rows, then lane a writes packet a's entries
         const int D1 = 6 * N + 10, D = obs_dim_of(N, d.env_var, d.k);
-        float* base = o.obs + (size_t)env * A * o.obs_row_stride;
-        for (int a = 0; a < A; a++) {
-            const int now = s.now[a], e = s.edge[a];
-            const int other = e >= 0 ? (s.ea[e] ^ s.eb[e] ^ now) : -1;
-            for (int c = l; c < D; c += WAVE) {
-                float v;
-                if (c >= D1) {
+        const size_t ld = o.obs_row_stride;
+        float* base = o.obs + (size_t)env * A * ld;
+        {
+            // 16-B stores over the first 4*floor(D1/4) columns when rows are 16-B aligned
+            const int Q = ((ld & 3) == 0 && (reinterpret_cast<uintptr_t>(base) & 15) == 0) ? D1 / 4 : 0;
+            if (Q) {
+                int a = l / Q, q = l - a * Q;
+                for (int idx = l; idx < A * Q; idx += WAVE) {
+                    *reinterpret_cast<float4*>(base + (size_t)a * ld + 4 * q) = make_float4(0.f, 0.f, 0.f, 0.f);
+                    for (q += WAVE; q >= Q; q -= Q) a++;
+                }
+            }
+            const int T = D1 - 4 * Q;  // remaining columns [4Q, D1) of every row
+            int a = l / T, c = l - a * T;
+            for (int idx = l; idx < A * T; idx += WAVE) {
+                base[(size_t)a * ld + 4 * Q + c] = 0.f;
+                for (c += WAVE; c >= T; c -= T) a++;
+            }
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // zeros land before the entries
+        if (l < A) {
+            float* row = base + (size_t)l * ld;
+            const int now = s.now[l], e = s.edge[l];
+            row[now] = 1.f;
+            row[N + s.target[l]] = 1.f;
+            row[2 * N] = (float)(e != -1);
+            if (e >= 0) row[2 * N + 1 + (s.ea[e] ^ s.eb[e] ^ now)] = 1.f;
+            row[3 * N + 1] = (float)s.time[l];
+            row[3 * N + 2] = (float)s.size[l];
+            row[3 * N + 3] = (float)l;
+#pragma unroll
+            for (int k = 0; k < 3; k++) {
+                float* blk = row + 3 * N + 4 + k * (N + 2);
+                const int ne = s.nbr_edge[now * 3 + k];
+                blk[s.nbr[now * 3 + k]] = 1.f;
+                blk[N] = (float)s.elen[ne];
+                blk[N + 1] = (float)s.load[ne];
+            }
+        }
+        if (D > D1) {  // variant columns (2: k neighbour slots, 3: global), lane-strided per row
+            for (int a = 0; a < A; a++) {
+                float* row = base + (size_t)a * ld;
+                for (int c = D1 + l; c < D; c += WAVE) {
                     const int g = c - D1;
+                    float v;
                     if (d.env_var == 2) {  // k neighbour slots of 5, -1 placeholders
                         const int slot = g / 5, f = g - slot * 5, j = s.kn[a][slot];
                         v = j < 0 ? -1.0f
@@ -225,20 +301,8 @@ __device__ void emit_obs(const EnvDev& d, int env, ES& s, const gm_obs_buffers& 
                         const int ND = 4 * N + 8, h = g - N * N, j = h / ND;
                         v = node_obs_value(s, N, j, h - j * ND);
                     }
-                } else if (c < N) v = (float)(c == now);
-                else if (c < 2 * N) v = (float)(c - N == s.target[a]);
-                else if (c == 2 * N) v = (float)(e != -1);
-                else if (c < 3 * N + 1) v = (float)(c - (2 * N + 1) == other);
-                else if (c == 3 * N + 1) v = (float)s.time[a];
-                else if (c == 3 * N + 2) v = (float)s.size[a];
-                else if (c == 3 * N + 3) v = (float)a;
-                else {
-                    int r = c - (3 * N + 4), k = r / (N + 2), q = r - k * (N + 2);
-                    if (q < N) v = (float)(s.nbr[now * 3 + k] == q);
-                    else if (q == N) v = (float)s.elen[s.nbr_edge[now * 3 + k]];
-                    else v = (float)s.load[s.nbr_edge[now * 3 + k]];
+                    row[c] = v;
                 }
-                base[(size_t)a * o.obs_row_stride + c] = v;
             }
         }
     }
