@@ -262,14 +262,25 @@ __global__ __launch_bounds__(256) void k_routing_enc(const float* __restrict__ x
             f_nb[k] = nbr[((size_t)g * N + fv) * 3 + k];
         }
     }
+    // weight columns of the 8 scalar features (cnt, load, 3 x (len, load)) stay in registers;
+    // only the 4 one-hot columns (node, 3 neighbours) are looked up in LDS per row
+    float wc[4][2][CPL];
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const int off = k == 0 ? N : N + 2 + (k - 1) * (N + 2) + N;
+#pragma unroll
+        for (int j = 0; j < CPL; j++) {
+            wc[k][0][j] = sw[off * BN + col + j];
+            wc[k][1][j] = sw[(off + 1) * BN + col + j];
+        }
+    }
     for (int i = 0; i < nrows; i++) {
         const int v = __builtin_amdgcn_readlane(fv, i);
         const float cnt = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(f_cnt), i));
         const float tl = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(f_tl), i));
         float acc[CPL];
 #pragma unroll
-        for (int j = 0; j < CPL; j++)
-            acc[j] = bias[j] + sw[v * BN + col + j] + cnt * sw[N * BN + col + j] + tl * sw[(N + 1) * BN + col + j];
+        for (int j = 0; j < CPL; j++) acc[j] = bias[j] + sw[v * BN + col + j] + cnt * wc[0][0][j] + tl * wc[0][1][j];
 #pragma unroll
         for (int k = 0; k < 3; k++) {
             const int off = N + 2 + k * (N + 2);
@@ -278,8 +289,7 @@ __global__ __launch_bounds__(256) void k_routing_enc(const float* __restrict__ x
             const float ld = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(f_ld[k]), i));
 #pragma unroll
             for (int j = 0; j < CPL; j++)
-                acc[j] += sw[(off + u) * BN + col + j] + ln * sw[(off + N) * BN + col + j] +
-                          ld * sw[(off + N + 1) * BN + col + j];
+                acc[j] += sw[(off + u) * BN + col + j] + ln * wc[k + 1][0][j] + ld * wc[k + 1][1][j];
         }
         float* yr = y + (base + i) * ldy + c0 + col;
         if (CPL == 2) {
