@@ -378,8 +378,9 @@ class NetMon(nn.Module):
         if agg_type not in ("sum", "mean"):
             raise NotImplementedError(f"agg_type {agg_type!r}: only sum/mean are built (torch_geometric variants "
                                       "are out of scope)")
-        if not rnn_carryover:
-            raise NotImplementedError("rnn_carryover=False is not built")
+        if not rnn_carryover and iterations < 1:
+            raise ValueError("rnn_carryover=False needs netmon iterations >= 1 (the reference's update "
+                             "cell output is the stored state)")
         self.encode = MLP(in_features, (*encoder_units, hidden_features))
         self.state = None
         self.iterations = iterations
@@ -403,6 +404,10 @@ class NetMon(nn.Module):
             self.num_states = 1
         else:
             raise NotImplementedError(f"rnn_type {rnn_type!r}")
+        # without carry-over the state also keeps the update cell's output (src/model.py:380-391)
+        self.cell_states = self.num_states
+        if not rnn_carryover:
+            self.num_states *= 2
         self.hidden_features = hidden_features
         self.state_size = hidden_features * self.num_states
 
@@ -426,17 +431,31 @@ class NetMon(nn.Module):
         H = self.hidden_features
         if self.state is None:
             self.state = torch.zeros(B, N, self.state_size, device=x.device)
+        nc = self.cell_states
         st = self.state.reshape(B * N, self.num_states, H)
         h = self.encode(x.reshape(B * N, Fdim))
-        hs, cs = st[:, 0], (st[:, 1] if self.num_states == 2 else None)
+        hs, cs = st[:, 0], (st[:, 1] if nc == 2 else None)
         h, c = self._cell(self.rnn_obs, h, hs.contiguous(), None if cs is None else cs.contiguous())
+        h0, c0 = h, c
         last_nbr = torch.zeros_like(h) if self.iterations <= 0 else None
         for it in range(self.iterations):
             if it == self.iterations - 1:
                 last_nbr = h
             M = mp_aggregate(h, nbr, self.agg_mode)
-            h, c = self._cell(self.rnn_update, M, h, c)
-        self.state = (torch.stack((h, c), 1) if c is not None else h.unsqueeze(1)).reshape(B, N, self.state_size)
+            hin, cin = h, c
+            if not self.rnn_carryover and it == 0:  # src/model.py:538-549
+                hin = st[:, nc].contiguous()
+                cin = st[:, nc + 1].contiguous() if nc == 2 else None
+            h, c = self._cell(self.rnn_update, M, hin, cin)
+        if self.rnn_carryover:
+            self.state = (torch.stack((h, c), 1) if c is not None else h.unsqueeze(1)).reshape(B, N, self.state_size)
+        elif nc == 2:
+            self.state = torch.stack((h0, c0, h, c), 1).reshape(B, N, self.state_size)
+        else:
+            # the reference stacks (h0[None], h1[None]) and its transpose(0, 1) + reshape keeps
+            # the component-major order: rows hold [h0 of all nodes | h1 of all nodes]
+            # (src/model.py:566-567, 447-449)
+            self.state = torch.cat((h0.reshape(-1), h.reshape(-1))).reshape(B, N, self.state_size)
         if self.output_global_hidden:
             # [h | mean over the graph's nodes of h | neighbour h] (src/model.py:458-469, 624-627)
             hv = h.reshape(B, N, H)

@@ -35,8 +35,8 @@ class NetMonWrapper:
         self.h_prev = None
         self.obs_dim = need
         if fused is None:
-            fused = (netmon.rnn_type == "lstm" and netmon.output_neighbor_hidden and not netmon.output_global_hidden
-                     and H % 32 == 0)
+            fused = (netmon.rnn_type == "lstm" and netmon.rnn_carryover and netmon.output_neighbor_hidden
+                     and not netmon.output_global_hidden and H % 32 == 0)
         self.fused = fused
         self._dirty = False
         # fused mode: the state and h_prev alternate between two fixed buffer pairs, so a

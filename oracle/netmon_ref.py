@@ -66,10 +66,13 @@ def gru_cell(x, h, W, p):
     return (1 - z) * n + z * h
 
 
-def netmon_forward(W, x, adj, state, rnn="lstm", agg="sum", K=1, n_enc_layers=3, global_h=False):
+def netmon_forward(W, x, adj, state, rnn="lstm", agg="sum", K=1, n_enc_layers=3, global_h=False, carryover=True):
     """src/model.py:451-622 NetMon.forward with output_neighbor_hidden=True,
-    rnn_carryover=True, no_agent_mapping=True; global_h adds the --netmon-global readout
-    (mean of h over the graph's nodes after h, src/model.py:461-462, 624-627).
+    no_agent_mapping=True; global_h adds the --netmon-global readout (mean of h over the
+    graph's nodes after h, src/model.py:461-462, 624-627). carryover=False
+    (--netmon-rnn-carryover 0, src/model.py:380-391, 536-570): the state is [obs-cell state |
+    update-cell state] and the first update iteration continues from the stored update-cell
+    state instead of the obs cell's output.
 
     x [B,N,F], adj [B,N,N] (I+A), state [B,N,S] or None.
     Returns (out [B,N,4H] ([B,N,5H] with global_h), new_state [B,N,S])."""
@@ -77,17 +80,20 @@ def netmon_forward(W, x, adj, state, rnn="lstm", agg="sum", K=1, n_enc_layers=3,
     adj = np.asarray(adj, np.float64)
     B, N, _ = x.shape
     H = W["rnn_obs.weight_hh"].shape[-1]
-    ns = 1 if rnn == "gru" else 2
+    nc = 1 if rnn == "gru" else 2  # tensors per cell state
+    ns = nc * (1 if carryover else 2)
     if state is None:
         state = np.zeros((B, N, ns * H))
     st = np.asarray(state, np.float64).reshape(B * N, ns, H)
     h = mlp(x.reshape(B * N, -1), W, "encode", n_enc_layers)
+    c = None
     if rnn == "lstm":
         h, c = lstm_cell(h, st[:, 0], st[:, 1], W, "rnn_obs")
     elif rnn == "lnlstm":
         h, c = lnlstm_cell(h, st[:, 0], st[:, 1], W, "rnn_obs")
     else:
         h = gru_cell(h, st[:, 0], W, "rnn_obs")
+    h0, c0 = h, c
     last_nbr = None
     for it in range(K):
         if it == K - 1:
@@ -96,13 +102,24 @@ def netmon_forward(W, x, adj, state, rnn="lstm", agg="sum", K=1, n_enc_layers=3,
         if agg == "mean":
             M = M / np.maximum(adj.sum(-1), 1)[..., None]
         M = M.reshape(B * N, H)
+        hin, cin = h, c
+        if not carryover and it == 0:
+            hin, cin = st[:, nc], (st[:, nc + 1] if nc == 2 else None)
         if rnn == "lstm":
-            h, c = lstm_cell(M, h, c, W, "rnn_update")
+            h, c = lstm_cell(M, hin, cin, W, "rnn_update")
         elif rnn == "lnlstm":
-            h, c = lnlstm_cell(M, h, c, W, "rnn_update")
+            h, c = lnlstm_cell(M, hin, cin, W, "rnn_update")
         else:
-            h = gru_cell(M, h, W, "rnn_update")
-    new_state = np.stack([h, c], 1).reshape(B, N, -1) if rnn != "gru" else h.reshape(B, N, -1)
+            h = gru_cell(M, hin, W, "rnn_update")
+    if carryover:
+        new_state = (np.stack([h, c], 1) if nc == 2 else h).reshape(B, N, -1)
+    elif nc == 2:
+        new_state = np.stack([h0, c0, h, c], 1).reshape(B, N, -1)
+    else:
+        # gru without carry-over: the reference stacks (h0[None], h1[None]) into (2, 1, BN, H),
+        # and transpose(0, 1) + reshape(B, N, 2H) keeps that component-major order
+        # (src/model.py:566-567, 447-449): rows hold [h0 of all nodes | h1 of all nodes]
+        new_state = np.concatenate([h0.reshape(-1), h.reshape(-1)]).reshape(B, N, 2 * H)
     # neighbour readout (src/model.py:582-622): neighbours in ascending node id order
     nb = last_nbr.reshape(B, N, H)
     eye = np.eye(N, dtype=bool)[None]

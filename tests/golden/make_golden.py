@@ -423,6 +423,36 @@ def gen_netmon_global(out, Network, Routing, EVAL_SEEDS, NetMon):
     print("netmon_global done", flush=True)
 
 
+def gen_netmon_nocarry(out, Network, Routing, EVAL_SEEDS, NetMon):
+    """NetMon with --netmon-rnn-carryover 0 (src/model.py:380-391, 536-570): the state holds the
+    obs cell's and the update cell's outputs, the first update iteration continues from the
+    previous step's update-cell state; 3 steps with carried state, lstm / lnlstm / gru, K = 1, 2."""
+    import torch
+    import torch.nn.functional as F
+
+    d = {}
+    n, a, B, steps = 20, 20, 4, 3
+    node_obs, node_adj, node_agent, _ = collect_graph_inputs(Network, Routing, EVAL_SEEDS, n, a, B, steps, 300)
+    d["node_obs"], d["node_adj"], d["node_agent"] = node_obs, node_adj, node_agent
+    variants = [("lstm", 1), ("lstm", 2), ("lnlstm", 1), ("gru", 2)]
+    d["variants"] = np.array([f"{r}:{k}" for r, k in variants])
+    for vi, (rnn, K) in enumerate(variants):
+        torch.manual_seed(70 + vi)
+        nm = NetMon(node_obs.shape[-1], 32, [64, 48], K, F.leaky_relu, rnn_type=rnn, rnn_carryover=False,
+                    agg_type="sum", output_neighbor_hidden=True, output_global_hidden=False)
+        nm.eval()
+        sd_to_npz(f"v{vi}_w_", nm.state_dict(), d)
+        d[f"v{vi}_state_size"] = np.int64(nm.get_state_size())
+        nm.state = None
+        with torch.no_grad():
+            for t in range(steps):
+                mapped = nm(torch.tensor(node_obs[t]), torch.tensor(node_adj[t]), torch.tensor(node_agent[t]))
+                d[f"v{vi}_mapped_{t}"] = mapped.numpy()
+                d[f"v{vi}_state_{t}"] = nm.state.numpy()
+    np.savez_compressed(out, **d)
+    print("netmon_nocarry done", flush=True)
+
+
 def gen_models(out, Network, Routing, EVAL_SEEDS, DGN, DQNR, CommNet):
     """DGN / DQNR / CommNet forwards (src/model.py:45-184, 653-794) on real routing agent
     observations and agent adjacency: Q, attention weights, recurrent agent states over a
@@ -823,6 +853,8 @@ def main():
         gen_netmon(os.path.join(HERE, "netmon.npz"), Network, Routing, EVAL_SEEDS, NetMon, DQN)
     if only is None or "netmon_global" in only:
         gen_netmon_global(os.path.join(HERE, "netmon_global.npz"), Network, Routing, EVAL_SEEDS, NetMon)
+    if only is None or "netmon_nocarry" in only:
+        gen_netmon_nocarry(os.path.join(HERE, "netmon_nocarry.npz"), Network, Routing, EVAL_SEEDS, NetMon)
     if only is None or "models" in only:
         gen_models(os.path.join(HERE, "models.npz"), Network, Routing, EVAL_SEEDS, DGN, DQNR, CommNet)
     if only is None or "train" in only:

@@ -73,3 +73,16 @@ def test_routing_netmon_global_train(tmp_path):
                    "--step-before-train=30", "--mini-batch-size=16", "--sequence-length=2", "--episode-steps=30",
                    "--eval-episodes=16", "--eval-episode-steps=10", "--disable-progressbar", f"--log-dir={tmp_path}"])
     assert np.isfinite(m["reward_mean"])
+
+
+@pytest.mark.parametrize("rnn", ["lstm", "gru"])
+def test_routing_netmon_no_carryover_train(tmp_path, rnn):
+    """--netmon-rnn-carryover 0: the doubled NetMon state goes through rollout, replay and the
+    sequence update (unfused NetMon path)."""
+    main = importlib.import_module("graph-marl_amd.main")
+    m = main.main(["--env-type=routing", "--model=dqn", "--netmon", "--netmon-rnn-carryover=0",
+                   f"--netmon-rnn-type={rnn}", "--netmon-iterations=1", "--netmon-dim=32",
+                   "--netmon-encoder-dim=64", "--n-env=16", "--total-steps=80", "--step-before-train=30",
+                   "--mini-batch-size=16", "--sequence-length=2", "--episode-steps=30", "--eval-episodes=16",
+                   "--eval-episode-steps=10", "--disable-progressbar", f"--log-dir={tmp_path}"])
+    assert np.isfinite(m["reward_mean"])

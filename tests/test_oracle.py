@@ -205,3 +205,20 @@ def test_netmon_global_restatement_matches_reference():
             mapped = netmon_ref.to_network_obs(out, g["node_agent"][t])
             np.testing.assert_allclose(mapped, g[f"v{vi}_mapped_{t}"], atol=5e-6, rtol=0)
             np.testing.assert_allclose(state, g[f"v{vi}_state_{t}"], atol=5e-6, rtol=0)
+
+
+def test_netmon_nocarry_restatement_matches_reference():
+    """--netmon-rnn-carryover 0 (lstm / lnlstm / gru) of the fp64 restatement vs the reference
+    (netmon_nocarry.npz): agent-mapped readout and the 2x state over 3 carried steps."""
+    g = np.load(os.path.join(R.GOLDEN, "netmon_nocarry.npz"))
+    for vi, v in enumerate(g["variants"]):
+        rnn, K = str(v).split(":")
+        W = {k[len(f"v{vi}_w_"):]: g[k].astype(np.float64) for k in g.files if k.startswith(f"v{vi}_w_")}
+        state = None
+        for t in range(3):
+            out, state = netmon_ref.netmon_forward(W, g["node_obs"][t], g["node_adj"][t], state, rnn, "sum", int(K),
+                                                   carryover=False)
+            assert state.shape[-1] == int(g[f"v{vi}_state_size"])
+            mapped = netmon_ref.to_network_obs(out, g["node_agent"][t])
+            np.testing.assert_allclose(mapped, g[f"v{vi}_mapped_{t}"], atol=5e-6, rtol=0)
+            np.testing.assert_allclose(state, g[f"v{vi}_state_{t}"], atol=5e-6, rtol=0)
