@@ -40,6 +40,8 @@ def parse():
     p.add_argument("--n-router", type=int, default=20)
     p.add_argument("--n-data", type=int, default=20)
     p.add_argument("--netmon-iterations", type=int, default=1)
+    p.add_argument("--no-netmon", action="store_true",
+                   help="DQN on the env observation alone (BASELINE config 2: the reference without --netmon)")
     p.add_argument("--episode-steps", type=int, default=50)
     p.add_argument("--random-topology", type=int, default=1)
     p.add_argument("--epsilon", type=float, default=0.5)
@@ -204,9 +206,10 @@ def main():
     net = gm.Network(N, random_topology=bool(args.random_topology), excluded_seeds=gm.EVAL_SEEDS,
                      device=dev.index)
     torch.manual_seed(0)
-    netmon = M.NetMon(4 * N + 8, 128, [512, 256], K).to(dev)
-    dqn = M.DQN(6 * N + 10 + netmon.get_out_features(), [512, 256], 4).to(dev)
-    M.tag_modules(netmon, "netmon.")
+    netmon = None if args.no_netmon else M.NetMon(4 * N + 8, 128, [512, 256], K).to(dev)
+    dqn = M.DQN(6 * N + 10 + (0 if netmon is None else netmon.get_out_features()), [512, 256], 4).to(dev)
+    if netmon is not None:
+        M.tag_modules(netmon, "netmon.")
     M.tag_modules(dqn, "dqn.")
     RO = importlib.import_module("graph-marl_amd.rollout")
     ro = RO.StreamedRollout(net, A, B, netmon, dqn, groups=args.groups, seed=rank * B, epsilon=args.epsilon,
@@ -306,7 +309,7 @@ def main():
                 kv["unit"] = {"hbm": "GB/s", "mfma": "TFLOP/s f32", "mfma16": "TFLOP/s f16"}[bound]
 
     train = None
-    if not args.no_train:
+    if not args.no_train and netmon is not None:
         try:
             train = measure_train(args, gm, M, W, P, env, wenv, netmon, dqn, policy, dev, world)
         except Exception as ex:  # the training figure must never break the rollout line
@@ -334,7 +337,8 @@ def main():
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
             "dtype": "f32 (GEMMs: 3xf16-split MFMA, f32 accumulate)" if x3 else "f32",
             "data": "synthetic: random-init NetMon+DQN weights, on-device random topologies and packets",
-            "config": {"workload": f"routing rollout --netmon (NetMon K={K}, H=128, enc 512,256, lstm, sum) + "
+            "config": {"workload": ("routing rollout (no NetMon) + " if netmon is None else
+                                    f"routing rollout --netmon (NetMon K={K}, H=128, enc 512,256, lstm, sum) + ") +
                                    f"DQN 512,256 eps-greedy, {'random' if args.random_topology else 'fixed'} "
                                    f"{N}-node topologies, episode {args.episode_steps} steps",
                        "n_env_per_gpu": B, "n_nodes": N, "n_data": A, "netmon_iterations": K,

@@ -157,10 +157,11 @@ class MLP(nn.Module):
             x = lin(x)
         return x
 
-    def forward_into(self, x2d, ldx, k, scratch):
-        """no-grad fast path over a strided row buffer (e.g. the joint observation)."""
+    def forward_into(self, x2d, ldx, k, scratch, n_layers=None):
+        """no-grad fast path over a strided row buffer (e.g. the joint observation); the first
+        n_layers layers (default all)."""
         h, ld, kk = x2d, ldx, k
-        for i, lin in enumerate(self.linear_layers):
+        for i, lin in enumerate(self.linear_layers[:n_layers]):
             out = scratch(i, x2d.shape[0], lin.out_features)
             linear_raw(h, ld, kk, lin.weight, lin.bias, lin.act, out=out, ldy=out.stride(0), wcache=lin._wc,
                        tag=lin.tag)
@@ -511,9 +512,16 @@ class DQN(nn.Module):
         return self.q_net(self.encoder(x))
 
     def forward_rows(self, x2d, ldx, k, scratch, **unused):
-        """no-grad fast path: q [rows, actions] from a strided observation buffer."""
+        """no-grad fast path: q [rows, actions] from a strided observation buffer; the last
+        hidden layer and the Q head run as one kernel (gm_gemm_x3_head) when they fit it."""
+        from . import fused as FU
+
+        layers = self.encoder.linear_layers
+        out = scratch(len(layers), x2d.shape[0], self.q_net.fc.out_features)
+        if len(layers) > 1 and FU.head_ok(layers[-1], self.q_net.fc):
+            h = self.encoder.forward_into(x2d, ldx, k, scratch, n_layers=len(layers) - 1)
+            return FU.linear_head(layers[-1], self.q_net.fc, h, h.stride(0), h.shape[1], out)
         h = self.encoder.forward_into(x2d, ldx, k, scratch)
-        out = scratch(len(self.encoder.linear_layers), x2d.shape[0], self.q_net.fc.out_features)
         return linear_raw(h, h.stride(0), h.shape[1], self.q_net.fc.weight, self.q_net.fc.bias, 0, out=out,
                           ldy=out.stride(0), wcache=self.q_net.fc._wc, tag=self.q_net.fc.tag)
 

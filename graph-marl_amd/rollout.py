@@ -24,21 +24,46 @@ from .routing import Routing
 from .wrapper import NetMonWrapper
 
 
+class _PlainEnv:
+    """The no-NetMon counterpart of NetMonWrapper (reference: the env used directly,
+    src/main.py without --netmon): same reset / step_ / obs surface."""
+
+    def __init__(self, env):
+        self.env = env
+
+    def __getattr__(self, name):
+        return getattr(self.env, name)
+
+    def get(self):
+        return self.env
+
+    @property
+    def obs(self):
+        return self.env.obs_buf[..., : self.env.obs_dim]
+
+    def reset(self):
+        self.env.reset_()
+
+    def step_(self, actions, detail=None):
+        self.env.step_(actions, detail)
+
+
 class StreamedRollout:
     def __init__(self, network, n_data, n_env, netmon, model, groups=1, seed=0, epsilon=0.5, episode_steps=50,
                  obs_extra=None, device=None, **env_kw):
+        """netmon None: DQN on the env observation alone (the reference without --netmon)."""
         assert n_env % groups == 0, "n_env must be divisible by groups"
         self.groups = groups
         self.n_env = n_env
         self.episode_steps = episode_steps
         per = n_env // groups
         dev = torch.device("cuda", torch.cuda.current_device() if device is None else device)
-        extra = netmon.get_out_features() if obs_extra is None else obs_extra
+        extra = (netmon.get_out_features() if netmon is not None else 0) if obs_extra is None else obs_extra
         self.envs, self.wenvs, self.policies, self.streams = [], [], [], []
         for g in range(groups):
             env = Routing(network, n_data, n_env=per, seed=seed + g * per, obs_extra=extra, agent_adjacency=False,
                           device=dev.index, **env_kw)
-            wenv = NetMonWrapper(env, netmon, 1)
+            wenv = NetMonWrapper(env, netmon, 1) if netmon is not None else _PlainEnv(env)
             pol = EpsilonGreedy(wenv, model, epsilon=epsilon, epsilon_decay=1.0, epsilon_update_freq=100,
                                 step_before_train=0)
             self.envs.append(env)
