@@ -66,6 +66,7 @@ struct ASrc {
     const int* agent_node;    // READOUT: [G*R]
     int n_nodes, deg, mean, rows_per_graph, k, hidden;
     unsigned bytes0, bytes1;  // buffer extents for the bounds check
+    const float* scale;       // k_gemm3 DENSE source: power-of-two A scale (nullable)
 };
 
 struct Epi {
@@ -617,6 +618,8 @@ __global__ __launch_bounds__(WGM* WGN * 64, OCC) void k_gemm3(ASrc a0, ASrc a1, 
 #pragma unroll
         for (int q = 0; q < BQ; q++) rb[S][q] = bload(rw, woff[q] + k0 * 4);
     };
+    const bool ascaled = a0.scale != nullptr;  // uniform
+    const float ascale = ascaled ? *a0.scale : 1.0f;
     auto lstore = [&](auto SET, int buf, int k0) {
         constexpr int S = decltype(SET)::value;
         const bool agg = AMODE == GM_A_AGGREGATE && k0 < a0.k;
@@ -637,6 +640,7 @@ __global__ __launch_bounds__(WGM* WGN * 64, OCC) void k_gemm3(ASrc a0, ASrc a1, 
                 if (kk + 2 >= kend) v.z = 0.f;
                 if (kk + 3 >= kend) v.w = 0.f;
             }
+            if (ascaled) v = make_float4(v.x * ascale, v.y * ascale, v.z * ascale, v.w * ascale);
             half4 hi, lo;
 #if GM_DIAG == 1  // diagnostic build: raw bits instead of the split
             hi = __builtin_bit_cast(half4, make_float2(v.x, v.y));
@@ -718,7 +722,7 @@ __global__ __launch_bounds__(WGM* WGN * 64, OCC) void k_gemm3(ASrc a0, ASrc a1, 
         if (kt + 1 < nk) step(S1{}, kt + 1);
     }
 
-    const float si = *wscale_inv;  // undo the weight scale (a power of two: exact)
+    const float si = *wscale_inv / ascale;  // undo the weight and A scales (powers of two: exact)
 #pragma unroll
     for (int i = 0; i < TM; i++)
 #pragma unroll
@@ -1060,6 +1064,9 @@ int to_asrc(const gm_a_src* s, int M, ASrc& o) {
     o.rows_per_graph = s->rows_per_graph;
     o.k = s->k;
     o.hidden = s->hidden;
+    o.scale = s->scale;
+    if (s->scale && s->mode != GM_A_DENSE)
+        return gm_fail(GM_ERR_INVALID_ARG, "gm_gemm: an A scale needs a DENSE source");
     if (!s->p0 || s->k <= 0 || (s->ld0 & 3) || (reinterpret_cast<uintptr_t>(s->p0) & 15))
         return gm_fail(GM_ERR_INVALID_ARG, "gm_gemm_f32: A source needs p0, k > 0, ld0 % 4 == 0, 16-byte base");
     long long rows0 = M;
@@ -1106,7 +1113,7 @@ int dispatch(const ASrc& s0, const ASrc& s1, const float* w, long long ldw, unsi
 #define GM_G(WGM, WGN, TM, TN, S, AM, EP, OC) \
     launch_g<WGM, WGN, TM, TN, S, AM, EP, OC>(s0, s1, w, ldw, wb, m, n, K, ep, st, wsi)
         // default: the readout-sourced DQN layer (the rollout's largest GEMM) on tile 10
-        const int gt = tile >= 8 ? tile : (tile == -1 && s0.mode == GM_A_READOUT && n > 128 ? 10 : 0);
+        const int gt = s0.scale ? 0 : (tile >= 8 ? tile : (tile == -1 && s0.mode == GM_A_READOUT && n > 128 ? 10 : 0));
         if (gt >= 8 && s0.mode != GM_A_AGGREGATE) {
             if (epilogue == GM_EPI_LSTM) {
                 ep.hidden = n / 4;
@@ -1217,6 +1224,8 @@ int gemm_entry(bool x3, const gm_a_src* a0, const gm_a_src* a1, const void* w, i
     if (rc) return rc;
     rc = to_asrc(a1, m, s1);
     if (rc) return rc;
+    if (s0.scale && (!x3 || a1 || s1.scale))
+        return gm_fail(GM_ERR_INVALID_ARG, std::string(fn) + ": an A scale needs the x3 form and a single source");
     if (a1 && (a1->mode != GM_A_DENSE || (s0.k % BKMAX)))
         return gm_fail(GM_ERR_INVALID_ARG, std::string(fn) + ": second A source must be dense and the first k % 32 == 0");
     const int K = s0.k + (a1 ? s1.k : 0);
@@ -1317,6 +1326,7 @@ extern "C" int gm_gemm_x3_head(const gm_a_src* a0, const void* wp, const float* 
     ASrc s0, s1;
     int rc = to_asrc(a0, m, s0);
     if (rc) return rc;
+    if (s0.scale) return gm_fail(GM_ERR_INVALID_ARG, "gm_gemm_x3_head: no A scale");
     memset(&s1, 0, sizeof(s1));
     const int K = s0.k;
     const long long ldw = (long long)((K + BKMAX - 1) / BKMAX * BKMAX) / 16 * 64, wb = (long long)n * ldw;
@@ -1335,6 +1345,44 @@ extern "C" int gm_gemm_x3_head(const gm_a_src* a0, const void* wp, const float* 
     ep.ldq = ldq;
     return launch_g<4, 2, 1, 4, 2, GM_A_DENSE, EPI_HEAD, 1>(s0, s1, static_cast<const float*>(wp), ldw, (unsigned)wb, m,
                                                           n, K, ep, (hipStream_t)stream, wscale_inv);
+}
+
+// max |x| as float bits (non-negative floats order as unsigned ints) into *acc (zeroed first)
+__global__ void k_absmax_atomic(const float* __restrict__ x, long long n, unsigned* __restrict__ acc) {
+    __shared__ float red[4];
+    float m = 0.f;
+    for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x)
+        m = fmaxf(m, fabsf(x[i]));
+    for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int i = 1; i < (int)(blockDim.x >> 6); i++) m = fmaxf(m, red[i]);
+        m = fmaxf(m, red[0]);
+        atomicMax(acc, __float_as_uint(m));
+    }
+}
+
+__global__ void k_scale_from_max(float* __restrict__ scale) {
+    const float m = __uint_as_float(*reinterpret_cast<const unsigned*>(scale));
+    int e = 0;
+    if (m > 0.f && isfinite(m)) frexpf(m, &e);  // m in [2^(e-1), 2^e)
+    e = max(-100, min(100, e));
+    scale[0] = (m > 0.f && isfinite(m)) ? ldexpf(1.0f, 14 - e) : 1.0f;  // s * max in [2^13, 2^14)
+}
+
+extern "C" int gm_absmax_scale(const float* x, int64_t n, float* scale, void* stream) {
+    if (!x || !scale || n <= 0) return gm_fail(GM_ERR_INVALID_ARG, "gm_absmax_scale: bad arguments");
+    hipStream_t st = (hipStream_t)stream;
+    hipError_t e = hipMemsetAsync(scale, 0, sizeof(float), st);
+    if (e != hipSuccess) return gm_fail(GM_ERR_HIP, std::string("gm_absmax_scale: ") + hipGetErrorString(e));
+    const long long blocks = std::min<long long>(1024, (n + 255) / 256);
+    hipLaunchKernelGGL(k_absmax_atomic, dim3((unsigned)blocks), dim3(256), 0, st, x, (long long)n,
+                       reinterpret_cast<unsigned*>(scale));
+    hipLaunchKernelGGL(k_scale_from_max, dim3(1), dim3(1), 0, st, scale);
+    e = hipGetLastError();
+    if (e != hipSuccess) return gm_fail(GM_ERR_HIP, std::string("gm_absmax_scale: ") + hipGetErrorString(e));
+    return GM_OK;
 }
 
 extern "C" int64_t gm_gemm_pack_x3_bytes(int32_t n, int32_t k) {

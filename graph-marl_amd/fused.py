@@ -29,6 +29,7 @@ class ASrc(C.Structure):
         ("mode", C.c_int32), ("p0", C.c_void_p), ("p1", C.c_void_p), ("ld0", C.c_int64), ("ld1", C.c_int64),
         ("nbr", C.c_void_p), ("agent_node", C.c_void_p), ("n_nodes", C.c_int32), ("deg", C.c_int32),
         ("mean", C.c_int32), ("rows_per_graph", C.c_int32), ("k", C.c_int32), ("hidden", C.c_int32),
+        ("scale", C.c_void_p),
     ]
 
 
@@ -40,6 +41,7 @@ def _setup():
                                     C.c_int32, vp, C.c_int64, vp, C.c_int64, vp, C.c_int64, vp, vp]
         lib.gm_gemm_x3.argtypes = [C.POINTER(ASrc), C.POINTER(ASrc), vp, vp, vp, C.c_int32, C.c_int32,
                                    C.c_int32, vp, C.c_int64, vp, C.c_int64, vp, C.c_int64, vp, vp]
+        lib.gm_absmax_scale.argtypes = [vp, C.c_int64, vp, vp]
         lib.gm_gemm_x3_head.argtypes = [C.POINTER(ASrc), vp, vp, vp, C.c_int32, C.c_int32, C.c_int32, vp, C.c_int64,
                                         vp, C.c_int32, vp, C.c_int64, vp, C.c_int64, vp]
         lib._gemm_ready = True
@@ -65,9 +67,11 @@ def use_x3(n):
     return L.GEMM_MODE == "x3" and n > 32
 
 
-def dense(p, ld, k):
+def dense(p, ld, k, scale=None):
+    """DENSE A source; scale: device float from gm_absmax_scale (split-f16 form only)."""
     s = ASrc()
     s.mode, s.p0, s.ld0, s.k = GM_A_DENSE, p, ld, k
+    s.scale = scale
     return s
 
 

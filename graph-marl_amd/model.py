@@ -51,6 +51,17 @@ class _WeightCache:
             self.key3 = key
         return self.val3
 
+    def x3t(self, w):
+        """split-f16 packing of w^T ([in][out]) for the input-gradient GEMM gx = gy @ w."""
+        from . import fused as FU
+
+        key = (w.data_ptr(), w._version)
+        if getattr(self, "key3t", None) != key:
+            wt, ldt = FU._pad_cols(w.detach().t())
+            self.val3t = FU.X3(wt, ldt, w.shape[1], w.shape[0])
+            self.key3t = key
+        return self.val3t
+
     def get(self, w):
         n, k = w.shape
         kp = _pad_stride(k)
@@ -95,12 +106,34 @@ def _as_rows(x):
     return x2, x2.stride(0), k
 
 
+def _dgrad(gy, w, wcache=None):
+    """gx = gy @ w. Split-f16 form over the packed w^T with gy scaled by a device power of two
+    (gm_absmax_scale: gradients sit far below the range where both f16 pieces are normal);
+    library fp32 GEMM when the shapes do not fit the kernel."""
+    from . import fused as FU
+
+    n, k = w.shape
+    if FU.use_x3(k) and n % 4 == 0:
+        gy = gy.contiguous()
+        if gy.data_ptr() % 16 == 0:
+            lib = FU._setup()
+            x3 = (wcache if wcache is not None else _WeightCache()).x3t(w)
+            sc = torch.empty(1, device=gy.device)
+            L.check(lib.gm_absmax_scale(gy.data_ptr(), gy.numel(), sc.data_ptr(), L.stream_ptr()))
+            gx = torch.empty(gy.shape[0], k, device=gy.device)
+            FU.gemm(FU.dense(gy.data_ptr(), n, n, scale=sc.data_ptr()), None, None, 0, None, gy.shape[0], k, 0,
+                    gx.data_ptr(), k, x3=x3)
+            return gx
+    return gy @ w
+
+
 class LinearFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w, b, act, wcache, tag=None):
         x2, ldx, k = _as_rows(x)
         y = linear_raw(x2, ldx, k, w, b, act, wcache=wcache, tag=tag)
         ctx.act = act
+        ctx.wcache = wcache
         ctx.save_for_backward(x2[:, :k] if x2.shape[1] != k else x2, w, y)
         return y.reshape(*x.shape[:-1], w.shape[0])
 
@@ -110,9 +143,7 @@ class LinearFn(torch.autograd.Function):
         gy = gy.reshape(-1, w.shape[0])
         if ctx.act == 1:
             gy = torch.where(y >= 0, gy, 0.01 * gy)
-        # input/weight gradients stay on the library fp32 GEMMs: gradients are far below the
-        # f16 range the split form needs (|a| >= 2^-15 for a normal low piece)
-        gx = gy @ w if ctx.needs_input_grad[0] else None
+        gx = _dgrad(gy, w, ctx.wcache) if ctx.needs_input_grad[0] else None
         gw = gy.t() @ x2 if ctx.needs_input_grad[1] else None
         gb = gy.sum(0) if ctx.needs_input_grad[2] else None
         if gx is not None:

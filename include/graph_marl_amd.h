@@ -23,6 +23,7 @@
  *   gm_gemm_f32                      Linear / LSTMCell GEMMs with aggregate, readout and gate math fused
  *   gm_gemm_x3 / gm_gemm_pack_x3     the same GEMMs in split-f16 form (f16 MFMA, fp32 accumulate)
  *   gm_gemm_x3_head                  last DQN layer + Q head in one kernel
+ *   gm_absmax_scale                  power-of-two operand scale for gm_gemm_x3 (input gradients)
  *   gm_agent_attention               AttModel attention core (DGN)          src/model.py:86-117
  *   gm_agent_comm                    CommNet communication step             src/model.py:780-787
  */
@@ -216,6 +217,8 @@ typedef struct {
     int32_t n_nodes, deg, mean, rows_per_graph;
     int32_t k;                 /* columns this source contributes (READOUT: (deg + 1) * hidden)    */
     int32_t hidden;            /* READOUT: H (multiple of 32)                                      */
+    const float* scale;        /* gm_gemm_x3, DENSE src0 without src1 (nullable): device power of  */
+                               /* two s from gm_absmax_scale; A is split as s*A, the result / s    */
 } gm_a_src;
 /* src1 (nullable) must be DENSE and src0->k a multiple of 32. W: [n][ldw] (ldw >= K, zero
  * padded to a multiple of 4). GM_EPI_LSTM: W rows packed so that rows [128t, 128t+128) are
@@ -242,6 +245,10 @@ int gm_gemm_x3(const gm_a_src* src0, const gm_a_src* src1, const void* wp, const
 int gm_gemm_x3_head(const gm_a_src* src0, const void* wp, const float* wscale_inv, const float* b, int32_t m,
                     int32_t n, int32_t act, const float* wq, int64_t ldwq, const float* bq, int32_t nq, float* q,
                     int64_t ldq, float* y, int64_t ldy, void* stream);
+/* s = 2^(14 - e) with max|x| in [2^(e-1), 2^e) (1 when x is all zero): the power-of-two scale
+ * that brings a gm_gemm_x3 A operand of small magnitude (e.g. gradients) into the range where
+ * both f16 pieces of the split are normal. x: n floats; scale: one device float. */
+int gm_absmax_scale(const float* x, int64_t n, float* scale, void* stream);
 /* Packed size in bytes of an [n][k] weight for gm_gemm_x3: n * ceil(k/32)*2 blocks * 64 B. */
 int64_t gm_gemm_pack_x3_bytes(int32_t n, int32_t k);
 /* Split W [n][ldw] (first k columns) into wp (16-byte aligned, gm_gemm_pack_x3_bytes):

@@ -222,3 +222,25 @@ def test_gemm_x3_head_vs_torch(m, n, k, ldx, nq, act):
     q2 = torch.full((m, nq), float("nan"), device="cuda")
     FU.linear_head(lin, fc, buf, ldx, k, q2)  # without the hidden output: same q
     assert torch.equal(q, q2)
+
+
+@pytest.mark.parametrize("mag", [1e-9, 1e-6, 1.0, 3e3])
+def test_input_gradient_x3_scaled(mag):
+    """gx = gy @ w in the split-f16 form with the device power-of-two A scale
+    (gm_absmax_scale): fp32-order error relative to sum |gy*w| at any gradient magnitude,
+    including far below the f16 normal range, where the unscaled split would lose precision."""
+    gm, M, FU, W = mods()
+    if FU.L.GEMM_MODE != "x3":
+        pytest.skip("split-f16 form disabled (GM_GEMM=f32)")
+    torch.manual_seed(11)
+    m, n, k = 4096, 512, 642
+    gy = torch.randn(m, n, device="cuda") * mag * torch.exp2(torch.randint(-6, 1, (m, 1), device="cuda").float())
+    w = torch.randn(n, k, device="cuda") / n ** 0.5
+    gx = M._dgrad(gy, w)
+    ref = gy.double() @ w.double()
+    mag_ref = gy.abs().double() @ w.abs().double()
+    rel = ((gx.double() - ref).abs() / mag_ref.clamp_min(1e-300)).max().item()
+    assert rel < 4e-6, rel
+    f32 = gy @ w
+    rel32 = ((f32.double() - ref).abs() / mag_ref.clamp_min(1e-300)).max().item()
+    assert rel < 8 * max(rel32, 5e-7), (rel, rel32)
