@@ -1264,23 +1264,31 @@ int gemm_entry(bool x3, const gm_a_src* a0, const gm_a_src* a1, const void* w, i
 // ---- weight split for X3: S = 2^(15 - e) with max|w| = f * 2^e (f in [0.5, 1)), so
 // S*max|w| in [2^14, 2^15) (< f16 max 65504) and both pieces of every weight stay normal
 // down to ~2^-24 of the largest ----
-__global__ void k_absmax(const float* __restrict__ w, long long ldw, int n, int k, float* __restrict__ wsi) {
+// max |W| over the [n][k] block (row stride ldw) as float bits into *acc (zeroed first): one
+// row per wave at a time, lanes over columns (coalesced), rows spread over the grid
+__global__ void k_absmax(const float* __restrict__ w, long long ldw, int n, int k, unsigned* __restrict__ acc) {
     __shared__ float red[16];
     float m = 0.f;
     const int wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
-    for (int r = wave; r < n; r += nw)  // one row per wave at a time, lanes over columns (coalesced)
+    for (int r = blockIdx.x * nw + wave; r < n; r += gridDim.x * nw)
         for (int c = threadIdx.x & 63; c < k; c += 64) m = fmaxf(m, fabsf(w[(long long)r * ldw + c]));
     for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
     if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
     __syncthreads();
     if (threadIdx.x == 0) {
-        for (int i = 1; i < (int)(blockDim.x >> 6); i++) m = fmaxf(m, red[i]);
+        for (int i = 1; i < nw; i++) m = fmaxf(m, red[i]);
         m = fmaxf(m, red[0]);
-        int e = 0;
-        if (m > 0.f && isfinite(m)) frexpf(m, &e);
-        e = max(-100, min(100, e));
-        wsi[0] = ldexpf(1.0f, e - 15);  // 1/S
+        atomicMax(acc, __float_as_uint(m));
     }
+}
+
+// 1/S from the max: S * max|W| in [2^14, 2^15)
+__global__ void k_wscale_from_max(float* __restrict__ wsi) {
+    const float m = __uint_as_float(*reinterpret_cast<const unsigned*>(wsi));
+    int e = 0;
+    if (m > 0.f && isfinite(m)) frexpf(m, &e);
+    e = max(-100, min(100, e));
+    wsi[0] = ldexpf(1.0f, e - 15);
 }
 
 // one thread per (row, 16-deep k block, element): packed[row][blk] = hi[16] | lo[16]
@@ -1396,7 +1404,11 @@ extern "C" int gm_gemm_pack_x3(const float* w, int64_t ldw, int32_t n, int32_t k
         return gm_fail(GM_ERR_INVALID_ARG, "gm_gemm_pack_x3: bad arguments");
     hipStream_t st = (hipStream_t)stream;
     const int nblk = (k + BKMAX - 1) / BKMAX * BKMAX / 16;
-    hipLaunchKernelGGL(k_absmax, dim3(1), dim3(1024), 0, st, w, (long long)ldw, n, k, wscale_inv);
+    hipError_t e0 = hipMemsetAsync(wscale_inv, 0, sizeof(float), st);
+    if (e0 != hipSuccess) return gm_fail(GM_ERR_HIP, std::string("gm_gemm_pack_x3: ") + hipGetErrorString(e0));
+    hipLaunchKernelGGL(k_absmax, dim3((unsigned)std::min(64, (n + 3) / 4)), dim3(256), 0, st, w, (long long)ldw, n, k,
+                       reinterpret_cast<unsigned*>(wscale_inv));
+    hipLaunchKernelGGL(k_wscale_from_max, dim3(1), dim3(1), 0, st, wscale_inv);
     const long long tot = (long long)n * nblk * 16;
     hipLaunchKernelGGL(k_split_w, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, st, w, (long long)ldw, n, k, nblk,
                        static_cast<_Float16*>(wp), wscale_inv);
