@@ -68,7 +68,8 @@ __device__ __forceinline__ int members(const int32_t* nb, int deg, int n, int* o
 // backward (symmetric adjacency): dh[j] = Σ_{n ∈ {j} ∪ nbr(j)} dout[n] * scale(n)
 template <bool BWD, int V>
 __global__ __launch_bounds__(256) void k_mp_aggregate(const float* __restrict__ h, const int32_t* __restrict__ nbr,
-                                                      int G, int N, int deg, int H, int mode, float* __restrict__ out) {
+                                                      int G, int N, int deg, int H, int mode, float* __restrict__ out,
+                                                      long long ldh, long long ldo) {
     const int HV = H / V;
     const long long gid = (long long)blockIdx.x * blockDim.x + threadIdx.x;
     const long long total = (long long)G * N * HV;
@@ -79,10 +80,10 @@ __global__ __launch_bounds__(256) void k_mp_aggregate(const float* __restrict__ 
     const int32_t* nb = nbr + ((size_t)g * N + n) * deg;
     int mem[MAXDEG + 1];
     const int cnt = members(nb, deg, n, mem);
-    const float* src = h + (size_t)g * N * H + (size_t)cv * V;
+    const float* src = h + (size_t)g * N * ldh + (size_t)cv * V;
     Vec<V> acc = zerov<V>();
     for (int q = 0; q < cnt; q++) {
-        Vec<V> x = ldv<V>(src + (size_t)mem[q] * H);
+        Vec<V> x = ldv<V>(src + (size_t)mem[q] * ldh);
         if (BWD && mode == 1) {
             const int32_t* nbm = nbr + ((size_t)g * N + mem[q]) * deg;
             int cm = 1;
@@ -97,7 +98,7 @@ __global__ __launch_bounds__(256) void k_mp_aggregate(const float* __restrict__ 
 #pragma unroll
         for (int i = 0; i < V; i++) acc.v[i] = acc.v[i] / cnt;
     }
-    stv<V>(out + row * H + (size_t)cv * V, acc);
+    stv<V>(out + row * ldo + (size_t)cv * V, acc);
 }
 
 // readout: out row r of graph g = [h_final[v], h_prev[nbr(v,0..deg-1)]], v = agent_node or r.
@@ -334,13 +335,15 @@ static int vec_width(int H, long long stride, const void* p) {
 
 template <bool BWD>
 static int launch_agg(const float* h, const int32_t* nbr, int32_t G, int32_t N, int32_t deg, int32_t H, int32_t mode,
-                      float* out, void* stream) {
-    const int V = vec_width(H, H, h) < vec_width(H, H, out) ? vec_width(H, H, h) : vec_width(H, H, out);
+                      float* out, void* stream, long long ldh = 0, long long ldo = 0) {
+    if (!ldh) ldh = H;
+    if (!ldo) ldo = H;
+    const int V = vec_width(H, ldh, h) < vec_width(H, ldo, out) ? vec_width(H, ldh, h) : vec_width(H, ldo, out);
     long long total = (long long)G * N * (H / V);
     dim3 grid(nblocks(total, 256));
-    if (V == 4) hipLaunchKernelGGL((k_mp_aggregate<BWD, 4>), grid, dim3(256), 0, (hipStream_t)stream, h, nbr, G, N, deg, H, mode, out);
-    else if (V == 2) hipLaunchKernelGGL((k_mp_aggregate<BWD, 2>), grid, dim3(256), 0, (hipStream_t)stream, h, nbr, G, N, deg, H, mode, out);
-    else hipLaunchKernelGGL((k_mp_aggregate<BWD, 1>), grid, dim3(256), 0, (hipStream_t)stream, h, nbr, G, N, deg, H, mode, out);
+    if (V == 4) hipLaunchKernelGGL((k_mp_aggregate<BWD, 4>), grid, dim3(256), 0, (hipStream_t)stream, h, nbr, G, N, deg, H, mode, out, ldh, ldo);
+    else if (V == 2) hipLaunchKernelGGL((k_mp_aggregate<BWD, 2>), grid, dim3(256), 0, (hipStream_t)stream, h, nbr, G, N, deg, H, mode, out, ldh, ldo);
+    else hipLaunchKernelGGL((k_mp_aggregate<BWD, 1>), grid, dim3(256), 0, (hipStream_t)stream, h, nbr, G, N, deg, H, mode, out, ldh, ldo);
     return launched();
 }
 
@@ -349,6 +352,14 @@ extern "C" int gm_mp_aggregate(const float* h, const int32_t* nbr, int32_t G, in
     if (!h || !nbr || !out || G <= 0 || N <= 0 || deg < 0 || deg > MAXDEG || H <= 0 || mode < 0 || mode > 1)
         return gm_fail(GM_ERR_INVALID_ARG, "gm_mp_aggregate: bad arguments (deg <= 8)");
     return launch_agg<false>(h, nbr, G, N, deg, H, mode, out, stream);
+}
+
+extern "C" int gm_mp_aggregate_rows(const float* h, int64_t ldh, const int32_t* nbr, int32_t G, int32_t N, int32_t deg,
+                                    int32_t H, int32_t mode, float* out, int64_t ldo, void* stream) {
+    if (!h || !nbr || !out || G <= 0 || N <= 0 || deg < 0 || deg > MAXDEG || H <= 0 || mode < 0 || mode > 1 ||
+        ldh < H || ldo < H)
+        return gm_fail(GM_ERR_INVALID_ARG, "gm_mp_aggregate_rows: bad arguments (deg <= 8, ld >= H)");
+    return launch_agg<false>(h, nbr, G, N, deg, H, mode, out, stream, ldh, ldo);
 }
 
 extern "C" int gm_mp_aggregate_bwd(const float* dout, const int32_t* nbr, int32_t G, int32_t N, int32_t deg,

@@ -21,6 +21,9 @@ import torch.nn.functional as F
 from . import _lib as L
 
 GM_A_DENSE, GM_A_AGGREGATE, GM_A_READOUT = 0, 1, 2
+# LSTM update cell: a strided aggregate pass (gm_mp_aggregate_rows, 29 us at 81920 nodes) + the
+# cell on dense [Σ h | h] (111 us) instead of the AGGREGATE A source inside the GEMM (159 us)
+PRE_AGG = True
 GM_EPI_BIAS, GM_EPI_BIAS_LEAKY, GM_EPI_LSTM = 0, 1, 2
 
 
@@ -322,10 +325,18 @@ def netmon_step(netmon, node_obs, nbr, state, out=None, last_out=None):
     wu, ldu, bu, xu = pack_lstm(netmon.rnn_update)
     last = S
     mean = netmon.agg_mode == 1
+    agg = torch.empty(M, H, device=dev) if PRE_AGG else None
     for it in range(netmon.iterations):
         last = S
         S2 = buf(it + 1)
-        gemm(aggregate(S.data_ptr(), 2 * H, H, nbr, N, mean), dense(S.data_ptr(), 2 * H, H), wu.data_ptr(), ldu,
+        if PRE_AGG:  # aggregate pass, then the update cell on dense [Σ h | h]
+            with L.timed(f"mp_aggregate:{M}x{H}"):
+                L.check(L.lib().gm_mp_aggregate_rows(S.data_ptr(), 2 * H, nbr.data_ptr(), B, N, nbr.shape[-1], H,
+                                                     int(mean), agg.data_ptr(), H, L.stream_ptr()))
+            a_src = dense(agg.data_ptr(), H, H)
+        else:
+            a_src = aggregate(S.data_ptr(), 2 * H, H, nbr, N, mean)
+        gemm(a_src, dense(S.data_ptr(), 2 * H, H), wu.data_ptr(), ldu,
              bu.data_ptr(), M, 4 * H, GM_EPI_LSTM, S2.data_ptr(), 2 * H, S2[:, H:].data_ptr(), 2 * H,
              S[:, H:].data_ptr(), 2 * H,
              tag=netmon.rnn_update.tag and f"lstm_agg:{netmon.rnn_update.tag}:{M}x{4 * H}x{2 * H}", x3=xu)

@@ -175,6 +175,10 @@ int gm_env_get_state(gm_env* env, gm_env_state* st);
  * out[n] = Σ over {n} ∪ nbr(n) in ascending node order (mode 0 = sum, 1 = mean). */
 int gm_mp_aggregate(const float* h, const int32_t* nbr, int32_t n_graphs, int32_t n_nodes, int32_t deg,
                     int32_t hidden, int32_t mode, float* out, void* stream);
+/* gm_mp_aggregate over strided rows (row strides ldh / ldo in floats): aggregates the h part of
+ * [h | c] state rows in place of the GEMM's AGGREGATE A source. */
+int gm_mp_aggregate_rows(const float* h, int64_t ldh, const int32_t* nbr, int32_t n_graphs, int32_t n_nodes,
+                         int32_t deg, int32_t hidden, int32_t mode, float* out, int64_t ldo, void* stream);
 /* Backward of gm_mp_aggregate for symmetric adjacency: dh[j] = Σ_{n ∈ {j} ∪ nbr(j)} dout[n] / cnt(n). */
 int gm_mp_aggregate_bwd(const float* dout, const int32_t* nbr, int32_t n_graphs, int32_t n_nodes, int32_t deg,
                         int32_t hidden, int32_t mode, float* dh, void* stream);
