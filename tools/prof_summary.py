@@ -29,7 +29,7 @@ DQN = ["dqn.enc0(K=642)", "dqn.enc1(K=512)", "dqn.q(K=256)"]
 
 # k_gemm (gm_gemm_f32, fused path): encoder layer 0 runs in k_routing_enc, the LSTM
 # cells carry their gate epilogue, the DQN's first layer gathers the NetMon readout
-NETMON_G = ["netmon.enc1(K=512)", "netmon.enc2(K=256)", "netmon.rnn_obs(K=128+128)", "netmon.rnn_update(K=agg128+128)"]
+NETMON_G = ["netmon.enc1(K=512)", "netmon.enc2(K=256)", "netmon.rnn_obs(K=128+128)", "netmon.rnn_update(K=sum128+128)"]
 DQN_G = ["dqn.enc0(K=512 readout+130)", "dqn.enc1+q(K=512, Q head fused)"]
 DQN_G3 = ["dqn.enc0(K=512 readout+130)", "dqn.enc1(K=512)", "dqn.q(K=256)"]  # before gm_gemm_x3_head
 
