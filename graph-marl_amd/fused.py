@@ -21,10 +21,12 @@ import torch.nn.functional as F
 from . import _lib as L
 
 GM_A_DENSE, GM_A_AGGREGATE, GM_A_READOUT = 0, 1, 2
-# LSTM update cell: a strided aggregate pass (gm_mp_aggregate_rows, 29 us at 81920 nodes) + the
-# cell on dense [Σ h | h] (111 us) instead of the AGGREGATE A source inside the GEMM (159 us)
-PRE_AGG = True
 GM_EPI_BIAS, GM_EPI_BIAS_LEAKY, GM_EPI_LSTM = 0, 1, 2
+
+# LSTM update cell: a strided aggregate pass (gm_mp_aggregate_rows, 26-29 us at 81920 nodes) +
+# the cell on dense [Σ h | h] (103-111 us) instead of the AGGREGATE A source inside the GEMM
+# (159 us); False selects the in-GEMM aggregate
+PRE_AGG = True
 
 
 class ASrc(C.Structure):

@@ -40,6 +40,23 @@ def dense_adj(nbr, N):
 
 
 @pytest.mark.parametrize("mode", [0, 1])
+def test_mp_aggregate_rows_strided(mode):
+    """gm_mp_aggregate_rows on the h half of [h | c] state rows into a strided output equals the
+    contiguous gm_mp_aggregate bit for bit (same member order)."""
+    M = model_mod()
+    L = M.L
+    G, N, H = 64, 20, 128
+    nbr, _ = random_graphs(G, N)
+    st = torch.randn(G * N, 2 * H, device="cuda")
+    out = torch.full((G * N, H + 4), float("nan"), device="cuda")
+    L.check(L.lib().gm_mp_aggregate_rows(st.data_ptr(), 2 * H, nbr.data_ptr(), G, N, nbr.shape[-1], H, mode,
+                                         out.data_ptr(), H + 4, L.stream_ptr()))
+    ref = M.mp_aggregate(st[:, :H].contiguous(), nbr, mode)
+    assert torch.equal(out[:, :H], ref)
+    assert torch.isnan(out[:, H:]).all()  # nothing written past the row's H columns
+
+
+@pytest.mark.parametrize("mode", [0, 1])
 def test_mp_aggregate_fwd_bwd(mode):
     M = model_mod()
     G, N, H = 64, 20, 128
