@@ -1393,6 +1393,132 @@ extern "C" int gm_absmax_scale(const float* x, int64_t n, float* scale, void* st
     return GM_OK;
 }
 
+// ---------------------------------------------------------------------------------------
+// Weight-gradient GEMM (training): C_z[m][n] = sum over k of split z of A[k][m] * B[k][n],
+// A = dY [K][lda], B = X [K][ldb], both K-major fp32 (K = batch rows) — the transposes are done
+// on the way into LDS. Both operands are scaled by device powers of two (sa, sb) and split as
+// a = a_hi + 2^-12 a_lo' (both pieces normal f16), a*b ~ a_hi b_hi + 2^-12 (a_lo' b_hi + a_hi b_lo')
+// with the 2^-12 terms in a second accumulator. 128x128x16 tiles, 4 waves of 64x64; each
+// thread moves one 4(k) x 4(m|n) sub-block per k step (4 row-contiguous float4 loads, a
+// register transpose, 2 x 8-B LDS stores per column). Split-K over blockIdx.y, partial sums
+// written to C + z * cz (the caller reduces them).
+__global__ __launch_bounds__(256, 2) void k_gemm3_kmajor(const float* __restrict__ A, long long lda,
+                                                        const float* __restrict__ B, long long ldb, int M, int N,
+                                                        int K, int kchunk, const float* __restrict__ sa,
+                                                        const float* __restrict__ sb, float* __restrict__ C,
+                                                        long long ldc, long long cz) {
+    constexpr int BM = 128, BN = 128, BK = 16, ROWB = 80, TM = 2, TN = 2;
+    __shared__ __attribute__((aligned(16))) char As[2][BM * ROWB];
+    __shared__ __attribute__((aligned(16))) char Bs[2][BN * ROWB];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wr = wave >> 1, wc = wave & 1;
+    const int nN = (N + BN - 1) / BN;
+    const int m0 = (blockIdx.x / nN) * BM, n0 = (blockIdx.x % nN) * BN;
+    const int kb = blockIdx.y * kchunk, ke = min(K, kb + kchunk);
+    const int nk = (ke - kb + BK - 1) / BK;
+    // this thread's sub-block: operand (A for tid < 128), 4-deep k group k4, 4-wide column group c4
+    const bool isA = tid < 128;
+    const int t = tid & 127, k4 = t >> 5, c4 = t & 31;
+    const float* src = isA ? A : B;
+    const long long ld = isA ? lda : ldb;
+    const int col = (isA ? m0 : n0) + 4 * c4;
+    const bool colok = col < (isA ? M : N);  // M, N multiples of 4
+    const float s = isA ? *sa : *sb;
+    char* dstb[2] = {(isA ? As[0] : Bs[0]) + (4 * c4) * ROWB + 8 * k4, (isA ? As[1] : Bs[1]) + (4 * c4) * ROWB + 8 * k4};
+    float4 rv[4];
+    auto load = [&](int kt) {
+        const int k = kb + kt * BK + 4 * k4;
+#pragma unroll
+        for (int r = 0; r < 4; r++)
+            rv[r] = (colok && k + r < ke) ? *reinterpret_cast<const float4*>(src + (long long)(k + r) * ld + col)
+                                          : make_float4(0.f, 0.f, 0.f, 0.f);
+    };
+    auto store = [&](int buf) {
+        // column c of the sub-block = LDS row 4*c4 + c: its 4 k values (rows r) as f16 hi / lo'
+        const float cv[4][4] = {{rv[0].x, rv[1].x, rv[2].x, rv[3].x}, {rv[0].y, rv[1].y, rv[2].y, rv[3].y},
+                                {rv[0].z, rv[1].z, rv[2].z, rv[3].z}, {rv[0].w, rv[1].w, rv[2].w, rv[3].w}};
+#pragma unroll
+        for (int c = 0; c < 4; c++) {
+            half4 hi, lo;
+            split4(make_float4(cv[c][0] * s, cv[c][1] * s, cv[c][2] * s, cv[c][3] * s), hi, lo);
+            char* row = dstb[buf] + c * ROWB;
+            *reinterpret_cast<half4*>(row) = hi;
+            *reinterpret_cast<half4*>(row + 32) = lo;
+        }
+    };
+    floatx16 acc[TM][TN], acc2[TM][TN];
+#pragma unroll
+    for (int i = 0; i < TM; i++)
+#pragma unroll
+        for (int j = 0; j < TN; j++)
+#pragma unroll
+            for (int r = 0; r < 16; r++) acc[i][j][r] = acc2[i][j][r] = 0.f;
+    const int h = lane >> 5, l32 = lane & 31;
+    auto compute = [&](int buf) {
+        const char* ac = As[buf] + (wr * TM * 32 + l32) * ROWB + 16 * h;
+        const char* bc = Bs[buf] + (wc * TN * 32 + l32) * ROWB + 16 * h;
+        half8 ah[TM], al[TM], bh[TN], bl[TN];
+#pragma unroll
+        for (int i = 0; i < TM; i++) {
+            ah[i] = *reinterpret_cast<const half8*>(ac + i * 32 * ROWB);
+            al[i] = *reinterpret_cast<const half8*>(ac + i * 32 * ROWB + 32);
+        }
+#pragma unroll
+        for (int j = 0; j < TN; j++) {
+            bh[j] = *reinterpret_cast<const half8*>(bc + j * 32 * ROWB);
+            bl[j] = *reinterpret_cast<const half8*>(bc + j * 32 * ROWB + 32);
+        }
+#pragma unroll
+        for (int i = 0; i < TM; i++)
+#pragma unroll
+            for (int j = 0; j < TN; j++) {
+                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[i], bh[j], acc[i][j], 0, 0, 0);
+                acc2[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[i], bh[j], acc2[i][j], 0, 0, 0);
+                acc2[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[i], bl[j], acc2[i][j], 0, 0, 0);
+            }
+    };
+    if (nk > 0) {
+        load(0);
+        store(0);
+    }
+    __syncthreads();
+    for (int kt = 0; kt < nk; kt++) {
+        if (kt + 1 < nk) load(kt + 1);
+        compute(kt & 1);
+        if (kt + 1 < nk) store((kt + 1) & 1);
+        __syncthreads();
+    }
+    const float inv = 1.0f / (*sa * *sb);  // powers of two: exact
+    float* Cz = C + (size_t)blockIdx.y * cz;
+#pragma unroll
+    for (int i = 0; i < TM; i++)
+#pragma unroll
+        for (int j = 0; j < TN; j++) {
+            const int n = n0 + wc * TN * 32 + j * 32 + l32;
+#pragma unroll
+            for (int r = 0; r < 16; r++) {
+                const int m = m0 + wr * TM * 32 + i * 32 + 4 * h + (r & 3) + 8 * (r >> 2);
+                if (m < M && n < N) Cz[(long long)m * ldc + n] = (acc[i][j][r] + acc2[i][j][r] * (1.0f / 4096.0f)) * inv;
+            }
+        }
+}
+
+extern "C" int gm_gemm_x3_wgrad(const float* a, int64_t lda, const float* b, int64_t ldb, int32_t m, int32_t n, int32_t k,
+                                int32_t kchunk, const float* sa, const float* sb, float* c, int64_t ldc, void* stream) {
+    if (!a || !b || !sa || !sb || !c || m <= 0 || n <= 0 || k <= 0 || kchunk <= 0 || (kchunk % 16) || (m % 4) ||
+        (n % 4) || lda < m || ldb < n || (lda % 4) || (ldb % 4) || ldc < n || (reinterpret_cast<uintptr_t>(a) & 15) ||
+        (reinterpret_cast<uintptr_t>(b) & 15))
+        return gm_fail(GM_ERR_INVALID_ARG, "gm_gemm_x3_wgrad: bad arguments (m, n, ld multiples of 4, 16-B bases, "
+                                           "kchunk % 16 == 0)");
+    const int T = ((m + 127) / 128) * ((n + 127) / 128);
+    const int S = (k + kchunk - 1) / kchunk;
+    hipLaunchKernelGGL(k_gemm3_kmajor, dim3(T, S), dim3(256), 0, (hipStream_t)stream, a, (long long)lda, b,
+                       (long long)ldb, m, n, k, kchunk, sa, sb, c, (long long)ldc, (long long)m * ldc);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return gm_fail(GM_ERR_HIP, std::string("gm_gemm_x3_wgrad: ") + hipGetErrorString(e));
+    return GM_OK;
+}
+
 extern "C" int64_t gm_gemm_pack_x3_bytes(int32_t n, int32_t k) {
     if (n <= 0 || k <= 0) return 0;
     return (int64_t)n * ((k + BKMAX - 1) / BKMAX * BKMAX / 16) * 64;

@@ -106,7 +106,17 @@ def _as_rows(x):
     return x2, x2.stride(0), k
 
 
-def _dgrad(gy, w, wcache=None):
+def _gy_scale(gy):
+    """Device power-of-two scale of a gradient operand (gm_absmax_scale), shared by its dgrad /
+    wgrad GEMMs."""
+    from . import fused as FU
+
+    sc = torch.empty(1, device=gy.device)
+    L.check(FU._setup().gm_absmax_scale(gy.data_ptr(), gy.numel(), sc.data_ptr(), L.stream_ptr()))
+    return sc
+
+
+def _dgrad(gy, w, wcache=None, sc=None):
     """gx = gy @ w. Split-f16 form over the packed w^T with gy scaled by a device power of two
     (gm_absmax_scale: gradients sit far below the range where both f16 pieces are normal);
     library fp32 GEMM when the shapes do not fit the kernel."""
@@ -118,13 +128,43 @@ def _dgrad(gy, w, wcache=None):
         if gy.data_ptr() % 16 == 0:
             lib = FU._setup()
             x3 = (wcache if wcache is not None else _WeightCache()).x3t(w)
-            sc = torch.empty(1, device=gy.device)
-            L.check(lib.gm_absmax_scale(gy.data_ptr(), gy.numel(), sc.data_ptr(), L.stream_ptr()))
+            sc = _gy_scale(gy) if sc is None else sc
             gx = torch.empty(gy.shape[0], k, device=gy.device)
             FU.gemm(FU.dense(gy.data_ptr(), n, n, scale=sc.data_ptr()), None, None, 0, None, gy.shape[0], k, 0,
                     gx.data_ptr(), k, x3=x3)
             return gx
     return gy @ w
+
+
+def _wgrad(gy, x, k, sa=None):
+    """gW = gy^T @ x[:, :k], a reduction over the batch rows: split-K split-f16 GEMM on the
+    K-major operands (gm_gemm_x3_wgrad; both scaled by device powers of two), partials summed
+    here; library fp32 GEMM when the shapes do not fit the kernel."""
+    from . import fused as FU
+
+    Mb, o = gy.shape
+    N = (k + 3) // 4 * 4
+    ldx = x.stride(0)
+    if not (FU.use_x3(k) and Mb >= 4096 and o % 4 == 0 and N <= ldx and ldx % 4 == 0 and x.stride(1) == 1
+            and x.data_ptr() % 16 == 0):
+        return gy.t() @ x[:, :k]
+    gy = gy.contiguous()
+    if gy.data_ptr() % 16:
+        return gy.t() @ x[:, :k]
+    lib = FU._setup()
+    dev = gy.device
+    sa = _gy_scale(gy) if sa is None else sa
+    # scale from the k real columns; the up to 3 padding columns only reach output columns >= k
+    _, e = torch.frexp(x[:, :k].abs().amax().reshape(1))
+    sb = torch.ldexp(torch.ones(1, device=dev), (14 - e).float())
+    tiles = ((o + 127) // 128) * ((N + 127) // 128)
+    splits = max(1, min(Mb // 2048, (1024 + tiles - 1) // tiles))
+    kchunk = ((Mb + splits - 1) // splits + 15) // 16 * 16
+    splits = (Mb + kchunk - 1) // kchunk
+    part = torch.empty(splits, o, N, device=dev)
+    L.check(lib.gm_gemm_x3_wgrad(gy.data_ptr(), o, x.data_ptr(), ldx, o, N, Mb, kchunk, sa.data_ptr(), sb.data_ptr(),
+                                 part.data_ptr(), N, L.stream_ptr()))
+    return part.sum(0)[:, :k]
 
 
 class LinearFn(torch.autograd.Function):
@@ -143,8 +183,11 @@ class LinearFn(torch.autograd.Function):
         gy = gy.reshape(-1, w.shape[0])
         if ctx.act == 1:
             gy = torch.where(y >= 0, gy, 0.01 * gy)
-        gx = _dgrad(gy, w, ctx.wcache) if ctx.needs_input_grad[0] else None
-        gw = gy.t() @ x2 if ctx.needs_input_grad[1] else None
+        sc = None
+        if ctx.needs_input_grad[0] and ctx.needs_input_grad[1] and gy.is_contiguous() and gy.shape[0] >= 4096:
+            sc = _gy_scale(gy)  # one scale for both gradient GEMMs
+        gx = _dgrad(gy, w, ctx.wcache, sc) if ctx.needs_input_grad[0] else None
+        gw = _wgrad(gy, x2, w.shape[1], sc) if ctx.needs_input_grad[1] else None
         gb = gy.sum(0) if ctx.needs_input_grad[2] else None
         if gx is not None:
             gx = gx.reshape(*ctx.saved_tensors[0].shape[:-1], w.shape[1])

@@ -24,6 +24,7 @@
  *   gm_gemm_x3 / gm_gemm_pack_x3     the same GEMMs in split-f16 form (f16 MFMA, fp32 accumulate)
  *   gm_gemm_x3_head                  last DQN layer + Q head in one kernel
  *   gm_absmax_scale                  power-of-two operand scale for gm_gemm_x3 (input gradients)
+ *   gm_gemm_x3_wgrad                 split-K weight-gradient GEMM over K-major operands
  *   gm_agent_attention               AttModel attention core (DGN)          src/model.py:86-117
  *   gm_agent_comm                    CommNet communication step             src/model.py:780-787
  */
@@ -249,6 +250,14 @@ int gm_gemm_x3(const gm_a_src* src0, const gm_a_src* src1, const void* wp, const
 int gm_gemm_x3_head(const gm_a_src* src0, const void* wp, const float* wscale_inv, const float* b, int32_t m,
                     int32_t n, int32_t act, const float* wq, int64_t ldwq, const float* bq, int32_t nq, float* q,
                     int64_t ldq, float* y, int64_t ldy, void* stream);
+/* Weight-gradient GEMM of the training path: C_z = A_z^T B_z for k-splits z of kchunk rows
+ * (K = batch rows): A = dY [k][lda], B = X [k][ldb], both K-major fp32, scaled by the device
+ * powers of two sa, sb (gm_absmax_scale) and split into f16 pieces on the way into LDS;
+ * partial C_z [m][ldc] at c + z*m*ldc (the caller sums the ceil(k / kchunk) partials). m, n,
+ * lda, ldb multiples of 4, 16-byte bases, kchunk a multiple of 16. Replaces the weight
+ * gradients of the reference's Linear / LSTMCell layers (torch autograd, src/main.py:840-1026). */
+int gm_gemm_x3_wgrad(const float* a, int64_t lda, const float* b, int64_t ldb, int32_t m, int32_t n, int32_t k,
+                     int32_t kchunk, const float* sa, const float* sb, float* c, int64_t ldc, void* stream);
 /* s = 2^(14 - e) with max|x| in [2^(e-1), 2^e) (1 when x is all zero): the power-of-two scale
  * that brings a gm_gemm_x3 A operand of small magnitude (e.g. gradients) into the range where
  * both f16 pieces of the split are normal. x: n floats; scale: one device float. */

@@ -244,3 +244,24 @@ def test_input_gradient_x3_scaled(mag):
     f32 = gy @ w
     rel32 = ((f32.double() - ref).abs() / mag_ref.clamp_min(1e-300)).max().item()
     assert rel < 8 * max(rel32, 5e-7), (rel, rel32)
+
+
+@pytest.mark.parametrize("Mb,o,k,ldx,mag", [(20001, 512, 642, 644, 1e-7), (65536, 256, 512, 512, 1.0),
+                                            (9000, 4, 256, 256, 1e-4), (131072, 512, 130, 132, 1e-6)])
+def test_weight_gradient_kmajor(Mb, o, k, ldx, mag):
+    """gW = gy^T x by the split-K split-f16 GEMM on K-major operands (gm_gemm_x3_wgrad; ragged
+    batch, ragged k with padded rows, 4-wide heads, tiny gradients): fp32-order error relative
+    to sum |gy*x|."""
+    gm, M_, FU, W = mods()
+    if FU.L.GEMM_MODE != "x3":
+        pytest.skip("split-f16 form disabled (GM_GEMM=f32)")
+    torch.manual_seed(Mb + o)
+    gy = torch.randn(Mb, o, device="cuda") * mag
+    xb = torch.randn(Mb, ldx, device="cuda")
+    x = xb[:, :k]
+    gw = M_._wgrad(gy, x, k)
+    assert gw.shape == (o, k)
+    ref = gy.double().t() @ x.double()
+    mag_ref = gy.abs().double().t() @ x.abs().double()
+    rel = ((gw.double() - ref).abs() / mag_ref.clamp_min(1e-300)).max().item()
+    assert rel < 4e-6, rel
