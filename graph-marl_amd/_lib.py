@@ -29,7 +29,7 @@ EXPORTS = [
     "gm_netmon_readout_bwd", "gm_lstm_pointwise", "gm_lstm_pointwise_bwd", "gm_linear_f32", "gm_gemm_f32",
     "gm_gemm_set_tile", "gm_simple_create", "gm_simple_destroy", "gm_simple_reset", "gm_simple_step",
     "gm_simple_observe", "gm_simple_policy_egreedy", "gm_simple_get_state", "gm_env_set_topology",
-    "gm_policy_shortest_path", "gm_env_first_hops", "gm_routing_node_encoder", "gm_gemm_x3", "gm_gemm_x3_head", "gm_absmax_scale", "gm_gemm_x3_wgrad",
+    "gm_policy_shortest_path", "gm_env_first_hops", "gm_routing_node_encoder", "gm_gemm_x3", "gm_gemm_x3_head", "gm_absmax_scale", "gm_absmax_scale_rows", "gm_gemm_x3_wgrad",
     "gm_gemm_pack_x3", "gm_gemm_pack_x3_bytes", "gm_agent_attention", "gm_agent_comm",
 ]
 

@@ -1379,6 +1379,41 @@ __global__ void k_scale_from_max(float* __restrict__ scale) {
     scale[0] = (m > 0.f && isfinite(m)) ? ldexpf(1.0f, 14 - e) : 1.0f;  // s * max in [2^13, 2^14)
 }
 
+// max |x| over a [rows][cols] block with row stride ld: one row per wave at a time, lanes over
+// columns, rows spread over the grid; float bits into *acc (zeroed first)
+__global__ void k_absmax_rows(const float* __restrict__ x, long long rows, int cols, long long ld,
+                              unsigned* __restrict__ acc) {
+    __shared__ float red[4];
+    float m = 0.f;
+    const int wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    for (long long r = (long long)blockIdx.x * nw + wave; r < rows; r += (long long)gridDim.x * nw)
+        for (int c = threadIdx.x & 63; c < cols; c += 64) m = fmaxf(m, fabsf(x[r * ld + c]));
+    for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int i = 1; i < nw; i++) m = fmaxf(m, red[i]);
+        m = fmaxf(m, red[0]);
+        atomicMax(acc, __float_as_uint(m));
+    }
+}
+
+extern "C" int gm_absmax_scale_rows(const float* x, int64_t rows, int32_t cols, int64_t ld, float* scale,
+                                    void* stream) {
+    if (!x || !scale || rows <= 0 || cols <= 0 || ld < cols)
+        return gm_fail(GM_ERR_INVALID_ARG, "gm_absmax_scale_rows: bad arguments");
+    hipStream_t st = (hipStream_t)stream;
+    hipError_t e = hipMemsetAsync(scale, 0, sizeof(float), st);
+    if (e != hipSuccess) return gm_fail(GM_ERR_HIP, std::string("gm_absmax_scale_rows: ") + hipGetErrorString(e));
+    const long long blocks = std::min<long long>(1024, (rows + 3) / 4);
+    hipLaunchKernelGGL(k_absmax_rows, dim3((unsigned)blocks), dim3(256), 0, st, x, (long long)rows, (int)cols,
+                       (long long)ld, reinterpret_cast<unsigned*>(scale));
+    hipLaunchKernelGGL(k_scale_from_max, dim3(1), dim3(1), 0, st, scale);
+    e = hipGetLastError();
+    if (e != hipSuccess) return gm_fail(GM_ERR_HIP, std::string("gm_absmax_scale_rows: ") + hipGetErrorString(e));
+    return GM_OK;
+}
+
 extern "C" int gm_absmax_scale(const float* x, int64_t n, float* scale, void* stream) {
     if (!x || !scale || n <= 0) return gm_fail(GM_ERR_INVALID_ARG, "gm_absmax_scale: bad arguments");
     hipStream_t st = (hipStream_t)stream;

@@ -155,8 +155,8 @@ def _wgrad(gy, x, k, sa=None):
     dev = gy.device
     sa = _gy_scale(gy) if sa is None else sa
     # scale from the k real columns; the up to 3 padding columns only reach output columns >= k
-    _, e = torch.frexp(x[:, :k].abs().amax().reshape(1))
-    sb = torch.ldexp(torch.ones(1, device=dev), (14 - e).float())
+    sb = torch.empty(1, device=dev)
+    L.check(lib.gm_absmax_scale_rows(x.data_ptr(), Mb, k, ldx, sb.data_ptr(), L.stream_ptr()))
     tiles = ((o + 127) // 128) * ((N + 127) // 128)
     splits = max(1, min(Mb // 2048, (1024 + tiles - 1) // tiles))
     kchunk = ((Mb + splits - 1) // splits + 15) // 16 * 16

@@ -262,6 +262,8 @@ int gm_gemm_x3_wgrad(const float* a, int64_t lda, const float* b, int64_t ldb, i
  * that brings a gm_gemm_x3 A operand of small magnitude (e.g. gradients) into the range where
  * both f16 pieces of the split are normal. x: n floats; scale: one device float. */
 int gm_absmax_scale(const float* x, int64_t n, float* scale, void* stream);
+/* The same scale for a [rows][cols] block with row stride ld (floats). */
+int gm_absmax_scale_rows(const float* x, int64_t rows, int32_t cols, int64_t ld, float* scale, void* stream);
 /* Packed size in bytes of an [n][k] weight for gm_gemm_x3: n * ceil(k/32)*2 blocks * 64 B. */
 int64_t gm_gemm_pack_x3_bytes(int32_t n, int32_t k);
 /* Split W [n][ldw] (first k columns) into wp (16-byte aligned, gm_gemm_pack_x3_bytes):
