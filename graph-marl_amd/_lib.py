@@ -25,7 +25,7 @@ EVAL_KEYS = ["total_edge_load", "occupied_edges", "packets_on_edges", "total_pac
 EXPORTS = [
     "gm_last_error", "gm_version", "gm_env_create", "gm_env_destroy", "gm_env_dims", "gm_env_reset",
     "gm_env_step", "gm_env_observe", "gm_env_topology", "gm_env_final_info", "gm_policy_egreedy",
-    "gm_env_get_state", "gm_build_seed_list", "gm_mp_aggregate", "gm_mp_aggregate_rows", "gm_mp_aggregate_bwd", "gm_netmon_readout",
+    "gm_env_get_state", "gm_build_seed_list", "gm_mp_aggregate", "gm_mp_aggregate_rows", "gm_mp_aggregate_bwd", "gm_leaky_bwd", "gm_netmon_readout",
     "gm_netmon_readout_bwd", "gm_lstm_pointwise", "gm_lstm_pointwise_bwd", "gm_linear_f32", "gm_gemm_f32",
     "gm_gemm_set_tile", "gm_simple_create", "gm_simple_destroy", "gm_simple_reset", "gm_simple_step",
     "gm_simple_observe", "gm_simple_policy_egreedy", "gm_simple_get_state", "gm_env_set_topology",
@@ -96,6 +96,7 @@ def lib():
     L.gm_build_seed_list.argtypes = [i32, i64, i32, vp, i32, i32, vp]
     L.gm_mp_aggregate.argtypes = [vp, vp, i32, i32, i32, i32, i32, vp, vp]
     L.gm_mp_aggregate_rows.argtypes = [vp, C.c_int64, vp, i32, i32, i32, i32, i32, vp, C.c_int64, vp]
+    L.gm_leaky_bwd.argtypes = [vp, vp, C.c_int64, i32, C.c_float, vp, vp, i32, vp]
     L.gm_mp_aggregate_bwd.argtypes = [vp, vp, i32, i32, i32, i32, i32, vp, vp]
     L.gm_netmon_readout.argtypes = [vp, vp, vp, vp, i32, i32, i32, i32, i32, vp, i64, vp]
     L.gm_netmon_readout_bwd.argtypes = [vp, i64, vp, vp, i32, i32, i32, i32, i32, vp, vp, vp]

@@ -347,6 +347,37 @@ static int launch_agg(const float* h, const int32_t* nbr, int32_t G, int32_t N, 
     return launched();
 }
 
+// Backward of act(x W^T + b) with leaky_relu(0.01) after the Linear (reference MLP,
+// src/model.py:13-42): g = dY * (Y >= 0 ? 1 : slope), and per-block column sums of g for the
+// bias gradient (partial[block][col]; the caller sums the blocks: a fixed summation order).
+// Threads own columns, blocks own row chunks; loads and stores are row-contiguous.
+__global__ __launch_bounds__(256) void k_leaky_bwd(const float* __restrict__ gy, const float* __restrict__ y,
+                                                   long long rows, int cols, int rows_per_block, float slope,
+                                                   float* __restrict__ g, float* __restrict__ part) {
+    const long long r0 = (long long)blockIdx.x * rows_per_block;
+    const long long r1 = min(rows, r0 + rows_per_block);
+    for (int c = threadIdx.x; c < cols; c += blockDim.x) {
+        float acc = 0.f;
+        for (long long r = r0; r < r1; r++) {
+            const long long i = r * cols + c;
+            const float v = y[i] >= 0.f ? gy[i] : slope * gy[i];
+            g[i] = v;
+            acc += v;
+        }
+        part[(long long)blockIdx.x * cols + c] = acc;
+    }
+}
+
+extern "C" int gm_leaky_bwd(const float* gy, const float* y, int64_t rows, int32_t cols, float slope, float* g,
+                            float* part, int32_t rows_per_block, void* stream) {
+    if (!gy || !y || !g || !part || rows <= 0 || cols <= 0 || rows_per_block <= 0)
+        return gm_fail(GM_ERR_INVALID_ARG, "gm_leaky_bwd: bad arguments");
+    const long long nb = (rows + rows_per_block - 1) / rows_per_block;
+    hipLaunchKernelGGL(k_leaky_bwd, dim3((unsigned)nb), dim3(256), 0, (hipStream_t)stream, gy, y, (long long)rows,
+                       (int)cols, (int)rows_per_block, slope, g, part);
+    return launched();
+}
+
 extern "C" int gm_mp_aggregate(const float* h, const int32_t* nbr, int32_t G, int32_t N, int32_t deg, int32_t H,
                                int32_t mode, float* out, void* stream) {
     if (!h || !nbr || !out || G <= 0 || N <= 0 || deg < 0 || deg > MAXDEG || H <= 0 || mode < 0 || mode > 1)

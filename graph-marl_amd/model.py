@@ -181,14 +181,28 @@ class LinearFn(torch.autograd.Function):
     def backward(ctx, gy):
         x2, w, y = ctx.saved_tensors
         gy = gy.reshape(-1, w.shape[0])
+        gb = None
         if ctx.act == 1:
-            gy = torch.where(y >= 0, gy, 0.01 * gy)
+            if gy.is_contiguous() and y.is_contiguous() and gy.shape[0] >= 4096:
+                # leaky_relu backward + per-block bias-gradient partial sums in one pass
+                rows, cols = gy.shape
+                rpb = 64
+                g2 = torch.empty_like(gy)
+                part = torch.empty((rows + rpb - 1) // rpb, cols, device=gy.device)
+                L.check(L.lib().gm_leaky_bwd(gy.data_ptr(), y.data_ptr(), rows, cols, 0.01, g2.data_ptr(),
+                                             part.data_ptr(), rpb, _s()))
+                gy = g2
+                if ctx.needs_input_grad[2]:
+                    gb = part.sum(0)
+            else:
+                gy = torch.where(y >= 0, gy, 0.01 * gy)
         sc = None
         if ctx.needs_input_grad[0] and ctx.needs_input_grad[1] and gy.is_contiguous() and gy.shape[0] >= 4096:
             sc = _gy_scale(gy)  # one scale for both gradient GEMMs
         gx = _dgrad(gy, w, ctx.wcache, sc) if ctx.needs_input_grad[0] else None
         gw = _wgrad(gy, x2, w.shape[1], sc) if ctx.needs_input_grad[1] else None
-        gb = gy.sum(0) if ctx.needs_input_grad[2] else None
+        if gb is None and ctx.needs_input_grad[2]:
+            gb = gy.sum(0)
         if gx is not None:
             gx = gx.reshape(*ctx.saved_tensors[0].shape[:-1], w.shape[1])
         return gx, gw, gb, None, None, None

@@ -180,6 +180,11 @@ int gm_mp_aggregate(const float* h, const int32_t* nbr, int32_t n_graphs, int32_
  * [h | c] state rows in place of the GEMM's AGGREGATE A source. */
 int gm_mp_aggregate_rows(const float* h, int64_t ldh, const int32_t* nbr, int32_t n_graphs, int32_t n_nodes,
                          int32_t deg, int32_t hidden, int32_t mode, float* out, int64_t ldo, void* stream);
+/* Backward of a Linear followed by leaky_relu (MLP layers, src/model.py:13-42): g = dY where
+ * Y >= 0 else slope * dY ([rows][cols] contiguous), and per-block column sums of g for the bias
+ * gradient: part[ceil(rows / rows_per_block)][cols] (the caller sums the blocks). */
+int gm_leaky_bwd(const float* dy, const float* y, int64_t rows, int32_t cols, float slope, float* g, float* part,
+                 int32_t rows_per_block, void* stream);
 /* Backward of gm_mp_aggregate for symmetric adjacency: dh[j] = Σ_{n ∈ {j} ∪ nbr(j)} dout[n] / cnt(n). */
 int gm_mp_aggregate_bwd(const float* dout, const int32_t* nbr, int32_t n_graphs, int32_t n_nodes, int32_t deg,
                         int32_t hidden, int32_t mode, float* dh, void* stream);

@@ -265,3 +265,31 @@ def test_weight_gradient_kmajor(Mb, o, k, ldx, mag):
     mag_ref = gy.abs().double().t() @ x.abs().double()
     rel = ((gw.double() - ref).abs() / mag_ref.clamp_min(1e-300)).max().item()
     assert rel < 4e-6, rel
+
+
+@pytest.mark.parametrize("rows,k,n,act", [(8192, 642, 512, 1), (5000, 256, 128, 1), (4096, 512, 4, 0)])
+def test_linear_backward_large_batch(rows, k, n, act):
+    """LinearFn backward at training batch sizes — fused leaky-ReLU backward + bias partials
+    (gm_leaky_bwd), scaled split-f16 input and weight gradients — vs fp64 autograd, relative to
+    the magnitude of each gradient's terms."""
+    gm, M, FU, W = mods()
+    torch.manual_seed(rows + n)
+    lin = M.Linear(k, n, act=act).cuda()
+    x = torch.randn(rows, k, device="cuda", requires_grad=True)
+    y = lin(x)
+    g = torch.randn_like(y) * 1e-5
+    y.backward(g)
+    xd = x.detach().double().requires_grad_(True)
+    wd = lin.weight.detach().double().requires_grad_(True)
+    bd = lin.bias.detach().double().requires_grad_(True)
+    yd = torch.nn.functional.linear(xd, wd, bd)
+    if act == 1:
+        yd = torch.nn.functional.leaky_relu(yd, 0.01)
+    yd.backward(g.double())
+    gyd = g.double() * torch.where(yd.detach() >= 0, 1.0, 0.01 if act == 1 else 1.0)
+    mag_x = gyd.abs() @ wd.detach().abs()
+    mag_w = gyd.abs().t() @ xd.detach().abs()
+    mag_b = gyd.abs().sum(0)
+    for got, ref, mag in ((x.grad, xd.grad, mag_x), (lin.weight.grad, wd.grad, mag_w), (lin.bias.grad, bd.grad, mag_b)):
+        rel = ((got.double() - ref).abs() / mag.clamp_min(1e-300)).max().item()
+        assert rel < 1e-5, rel
