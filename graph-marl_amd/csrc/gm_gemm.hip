@@ -1434,8 +1434,8 @@ extern "C" int gm_absmax_scale(const float* x, int64_t n, float* scale, void* st
 // on the way into LDS. Both operands are scaled by device powers of two (sa, sb) and split as
 // a = a_hi + 2^-12 a_lo' (both pieces normal f16), a*b ~ a_hi b_hi + 2^-12 (a_lo' b_hi + a_hi b_lo')
 // with the 2^-12 terms in a second accumulator. 128x128x16 tiles, 4 waves of 64x64; each
-// thread moves one 4(k) x 4(m|n) sub-block per k step (4 row-contiguous float4 loads, a
-// register transpose, 2 x 8-B LDS stores per column). Split-K over blockIdx.y, partial sums
+// thread moves one 4(k) x 4(m|n) sub-block per k step (16 coalesced dword loads, a register
+// transpose, 2 x 8-B LDS stores per column). Split-K over blockIdx.y, partial sums
 // written to C + z * cz (the caller reduces them).
 __global__ __launch_bounds__(256, 2) void k_gemm3_kmajor(const float* __restrict__ A, long long lda,
                                                         const float* __restrict__ B, long long ldb, int M, int N,
@@ -1452,31 +1452,33 @@ __global__ __launch_bounds__(256, 2) void k_gemm3_kmajor(const float* __restrict
     const int kb = blockIdx.y * kchunk, ke = min(K, kb + kchunk);
     const int nk = (ke - kb + BK - 1) / BK;
     // this thread's sub-block: operand (A for tid < 128), 4-deep k group k4, 4-wide column group c4
+    // this thread: operand (A for tid < 128), 4-deep k group k4, columns c4 + 32 c (c = 0..3):
+    // dword loads (coalesced over c4) and LDS rows c4 + 32 c (consecutive rows per store
+    // instruction: conflict-free 8-B stores on the 80-B row pitch)
     const bool isA = tid < 128;
     const int t = tid & 127, k4 = t >> 5, c4 = t & 31;
     const float* src = isA ? A : B;
     const long long ld = isA ? lda : ldb;
-    const int col = (isA ? m0 : n0) + 4 * c4;
-    const bool colok = col < (isA ? M : N);  // M, N multiples of 4
+    const int col0 = (isA ? m0 : n0) + c4, lim = isA ? M : N;
     const float s = isA ? *sa : *sb;
-    char* dstb[2] = {(isA ? As[0] : Bs[0]) + (4 * c4) * ROWB + 8 * k4, (isA ? As[1] : Bs[1]) + (4 * c4) * ROWB + 8 * k4};
-    float4 rv[4];
+    char* dstb[2] = {(isA ? As[0] : Bs[0]) + c4 * ROWB + 8 * k4, (isA ? As[1] : Bs[1]) + c4 * ROWB + 8 * k4};
+    float rv[4][4];  // [column c][k row r]
     auto load = [&](int kt) {
         const int k = kb + kt * BK + 4 * k4;
 #pragma unroll
-        for (int r = 0; r < 4; r++)
-            rv[r] = (colok && k + r < ke) ? *reinterpret_cast<const float4*>(src + (long long)(k + r) * ld + col)
-                                          : make_float4(0.f, 0.f, 0.f, 0.f);
+        for (int r = 0; r < 4; r++) {
+            const float* rowp = src + (long long)(k + r) * ld + col0;
+            const bool kok = k + r < ke;
+#pragma unroll
+            for (int c = 0; c < 4; c++) rv[c][r] = (kok && col0 + 32 * c < lim) ? rowp[32 * c] : 0.f;
+        }
     };
     auto store = [&](int buf) {
-        // column c of the sub-block = LDS row 4*c4 + c: its 4 k values (rows r) as f16 hi / lo'
-        const float cv[4][4] = {{rv[0].x, rv[1].x, rv[2].x, rv[3].x}, {rv[0].y, rv[1].y, rv[2].y, rv[3].y},
-                                {rv[0].z, rv[1].z, rv[2].z, rv[3].z}, {rv[0].w, rv[1].w, rv[2].w, rv[3].w}};
 #pragma unroll
         for (int c = 0; c < 4; c++) {
             half4 hi, lo;
-            split4(make_float4(cv[c][0] * s, cv[c][1] * s, cv[c][2] * s, cv[c][3] * s), hi, lo);
-            char* row = dstb[buf] + c * ROWB;
+            split4(make_float4(rv[c][0] * s, rv[c][1] * s, rv[c][2] * s, rv[c][3] * s), hi, lo);
+            char* row = dstb[buf] + 32 * c * ROWB;
             *reinterpret_cast<half4*>(row) = hi;
             *reinterpret_cast<half4*>(row + 32) = lo;
         }

@@ -1,0 +1,40 @@
+#!/usr/bin/env python3
+"""Weight-gradient GEMM timing on the training shapes (131072 batch rows): split-f16 K-major
+kernel (model._wgrad) vs the library fp32 GEMM. python tools/wgrad_bench.py"""
+import importlib
+import json
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+M = importlib.import_module("graph-marl_amd.model")
+
+
+def timeit(fn, reps=10):
+    fn()
+    torch.cuda.synchronize()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(reps):
+        fn()
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) / reps * 1e3
+
+
+def main():
+    torch.manual_seed(0)
+    Mb = 131072
+    out = {}
+    for o, k, ldx in ((512, 642, 644), (256, 512, 512), (512, 256, 256), (128, 256, 256)):
+        gy = torch.randn(Mb, o, device="cuda") * 1e-6
+        x = torch.randn(Mb, ldx, device="cuda")[:, :k]
+        out[f"{o}x{k}"] = {"x3_kmajor_us": round(timeit(lambda: M._wgrad(gy, x, k)), 1),
+                           "fp32_lib_us": round(timeit(lambda: gy.t() @ x), 1)}
+    print(json.dumps(out))
+
+
+if __name__ == "__main__":
+    main()
