@@ -1291,7 +1291,9 @@ extern "C" int gm_env_reset(gm_env* env, const uint8_t* reset_mask, const gm_obs
     int rc = check_obs(env, obs);
     if (rc) return rc;
     gm_obs_buffers o = obs ? *obs : gm_obs_buffers{};
-    if (ncap(env->d.N) == 64) hipLaunchKernelGGL(k_env_reset<64>, dim3(env->d.n_env), dim3(64), 0, (hipStream_t)stream, env->d, reset_mask, o);
+    // N <= 32: the 32-node LDS image (14 KB instead of 24 KB per env) doubles the envs per CU
+    if (env->d.N <= 32) hipLaunchKernelGGL(k_env_reset<32>, dim3(env->d.n_env), dim3(64), 0, (hipStream_t)stream, env->d, reset_mask, o);
+    else if (ncap(env->d.N) == 64) hipLaunchKernelGGL(k_env_reset<64>, dim3(env->d.n_env), dim3(64), 0, (hipStream_t)stream, env->d, reset_mask, o);
     else hipLaunchKernelGGL(k_env_reset<128>, dim3(env->d.n_env), dim3(64), 0, (hipStream_t)stream, env->d, reset_mask, o);
     return check_launch();
 }
