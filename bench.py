@@ -48,6 +48,9 @@ def parse():
     p.add_argument("--no-kernel-timers", action="store_true")
     p.add_argument("--graph", type=int, default=0,
                    help="replay the rollout as a HIP graph of this many (even) vector steps (0: eager launches)")
+    p.add_argument("--stagger", action="store_true",
+                   help="stagger the stream groups' episodes so their resets overlap the other group's GEMMs "
+                        "(measured neutral at 4096 envs: the reset is ~2%% of a 50-step episode)")
     p.add_argument("--groups", type=int, default=2,
                    help="env groups on separate HIP streams (graph-marl_amd/rollout.py StreamedRollout)")
     p.add_argument("--unfused", action="store_true", help="materialise the joint obs; separate LSTM/aggregate kernels")
@@ -213,7 +216,8 @@ def main():
     M.tag_modules(dqn, "dqn.")
     RO = importlib.import_module("graph-marl_amd.rollout")
     ro = RO.StreamedRollout(net, A, B, netmon, dqn, groups=args.groups, seed=rank * B, epsilon=args.epsilon,
-                            episode_steps=args.episode_steps, device=dev.index)
+                            episode_steps=args.episode_steps, device=dev.index,
+                            stagger=args.stagger and not args.graph)
     if args.unfused:
         for w in ro.wenvs:
             w.fused = False

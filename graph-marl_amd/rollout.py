@@ -50,8 +50,12 @@ class _PlainEnv:
 
 class StreamedRollout:
     def __init__(self, network, n_data, n_env, netmon, model, groups=1, seed=0, epsilon=0.5, episode_steps=50,
-                 obs_extra=None, device=None, **env_kw):
-        """netmon None: DQN on the env observation alone (the reference without --netmon)."""
+                 obs_extra=None, device=None, stagger=False, **env_kw):
+        """netmon None: DQN on the env observation alone (the reference without --netmon).
+        stagger: group g's episodes start g * episode_steps / groups steps into the first one, so
+        the groups' resets (latency-bound, low occupancy) overlap another group's GEMMs instead
+        of all groups resetting on the same step; every env still runs fixed-length episodes
+        (eager stepping only: graph capture needs aligned resets)."""
         assert n_env % groups == 0, "n_env must be divisible by groups"
         self.groups = groups
         self.n_env = n_env
@@ -71,6 +75,8 @@ class StreamedRollout:
             self.policies.append(pol)
             self.streams.append(torch.cuda.Stream(dev))
         self.ep = 0
+        self.stagger = stagger and groups > 1
+        self._offs = [(g * episode_steps) // groups if self.stagger else 0 for g in range(groups)]
         self._graph = None
         self._gsteps = 0
 
@@ -97,13 +103,15 @@ class StreamedRollout:
     @torch.no_grad()
     def step(self):
         """One vector step of every env (act, env step, NetMon step), a reset of every group
-        after episode_steps steps like the reference's fixed-length episodes."""
+        after episode_steps steps like the reference's fixed-length episodes (per group when
+        staggered)."""
         self._enqueue_step()
         self.ep += 1
-        if self.ep >= self.episode_steps:
-            for g in range(self.groups):
+        for g in range(self.groups):
+            if (self.ep + self._offs[g]) % self.episode_steps == 0:
                 with self._on(g):
                     self.wenvs[g].reset()
+        if self.ep >= self.episode_steps:
             self.ep = 0
 
     @torch.no_grad()
@@ -111,6 +119,8 @@ class StreamedRollout:
         """Record `steps` (even, dividing episode_steps) vector steps of every group as one
         graph. Call after reset() and a few eager steps (packed weights and scratch exist)."""
         assert steps % 2 == 0 and self.episode_steps % steps == 0, "steps must be even and divide episode_steps"
+        if self.stagger:
+            raise ValueError("graph replay needs aligned group resets (stagger=False)")
         if any(w._eps_changes() for w in self.policies):
             raise ValueError("graph replay needs a fixed epsilon (epsilon_decay = 1.0)")
         torch.cuda.synchronize()

@@ -66,6 +66,43 @@ def test_groups_match_serial():
     assert_same(got, cat(parts))
 
 
+def test_staggered_groups_match_serial():
+    """stagger=True: group g resets g * episode_steps / groups steps out of phase; each group ==
+    a single-group rollout that resets on the same steps."""
+    gm = importlib.import_module("graph-marl_amd")
+    RO = importlib.import_module("graph-marl_amd.rollout")
+    base = build(2)
+    net = gm.Network(N, random_topology=True, excluded_seeds=gm.EVAL_SEEDS, device=0)
+    ro = RO.StreamedRollout(net, A, B, base.wenvs[0].netmon, base.policies[0]._model, groups=2, seed=0,
+                            epsilon=0.3, episode_steps=10, device=0, stagger=True)
+    assert ro._offs == [0, 5]
+    ro.reset()
+    ro.run(27)
+    got = cat(snapshot(ro))
+    parts = []
+    for g, off in enumerate(ro._offs):
+        r1 = RO.StreamedRollout(net, A, B // 2, ro.wenvs[0].netmon, ro.policies[0]._model, groups=1,
+                                seed=g * (B // 2), epsilon=0.3, episode_steps=10, device=0)
+        r1.reset()
+        for t in range(1, 28):
+            r1._enqueue_step()
+            if (t + off) % 10 == 0:
+                with r1._on(0):
+                    r1.wenvs[0].reset()
+        parts.append(cat(snapshot(r1)))
+    assert_same(got, cat(parts))
+
+
+def test_stagger_refuses_graph():
+    ro = build(2)
+    ro.stagger = True
+    ro.reset()
+    ro.step()
+    ro.step()
+    with pytest.raises(ValueError):
+        ro.capture(2)
+
+
 @pytest.mark.parametrize("groups,gsteps,warm", [(1, 2, 4), (2, 2, 4), (2, 10, 10)])
 def test_graph_replay_matches_eager(groups, gsteps, warm):
     """Replays cross episode resets (episode 10 steps), which run eagerly in between."""

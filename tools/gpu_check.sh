@@ -37,6 +37,7 @@ for s in "$@"; do
         benchg0) step bench_eager 300 python bench.py --no-cpu-baseline --steps 100 --no-train || exit $? ;;
         benchf32) GM_GEMM=f32 step bench_f32 300 python bench.py --no-cpu-baseline --steps 100 || exit $? ;;
         bench) step bench 600 python bench.py || exit $? ;;
+        benchst) step bench_stagger 300 python bench.py --no-cpu-baseline --steps 100 --stagger || exit $? ;;
         benchq) step bench 300 python bench.py --no-cpu-baseline --steps 100 || exit $? ;;
         prof) step prof 600 rocprofv3 --kernel-trace --stats -T --output-format csv -d gpurun_out/prof -o bench \
                   -- python bench.py --steps 100 --groups 1 --no-cpu-baseline --no-train --no-f32-compare || exit $? ;;
