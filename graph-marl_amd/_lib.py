@@ -29,7 +29,7 @@ EXPORTS = [
     "gm_netmon_readout_bwd", "gm_lstm_pointwise", "gm_lstm_pointwise_bwd", "gm_linear_f32", "gm_gemm_f32",
     "gm_gemm_set_tile", "gm_simple_create", "gm_simple_destroy", "gm_simple_reset", "gm_simple_step",
     "gm_simple_observe", "gm_simple_policy_egreedy", "gm_simple_get_state", "gm_env_set_topology",
-    "gm_policy_shortest_path", "gm_env_first_hops", "gm_routing_node_encoder", "gm_gemm_x3", "gm_gemm_x3_head", "gm_absmax_scale", "gm_absmax_scale_rows", "gm_gemm_x3_wgrad",
+    "gm_policy_shortest_path", "gm_env_first_hops", "gm_routing_node_encoder", "gm_gemm_x3", "gm_gemm_x3_head", "gm_absmax_scale", "gm_absmax_scale_rows", "gm_gemm_x3_wgrad", "gm_absmax_finish",
     "gm_gemm_pack_x3", "gm_gemm_pack_x3_bytes", "gm_agent_attention", "gm_agent_comm",
 ]
 
@@ -96,12 +96,12 @@ def lib():
     L.gm_build_seed_list.argtypes = [i32, i64, i32, vp, i32, i32, vp]
     L.gm_mp_aggregate.argtypes = [vp, vp, i32, i32, i32, i32, i32, vp, vp]
     L.gm_mp_aggregate_rows.argtypes = [vp, C.c_int64, vp, i32, i32, i32, i32, i32, vp, C.c_int64, vp]
-    L.gm_leaky_bwd.argtypes = [vp, vp, C.c_int64, i32, C.c_float, vp, vp, i32, vp]
+    L.gm_leaky_bwd.argtypes = [vp, vp, C.c_int64, i32, C.c_float, vp, vp, i32, vp, vp]
     L.gm_mp_aggregate_bwd.argtypes = [vp, vp, i32, i32, i32, i32, i32, vp, vp]
     L.gm_netmon_readout.argtypes = [vp, vp, vp, vp, i32, i32, i32, i32, i32, vp, i64, vp]
     L.gm_netmon_readout_bwd.argtypes = [vp, i64, vp, vp, i32, i32, i32, i32, i32, vp, vp, vp]
     L.gm_lstm_pointwise.argtypes = [vp, vp, i32, i32, vp, vp, vp, vp]
-    L.gm_lstm_pointwise_bwd.argtypes = [vp, vp, vp, vp, vp, i32, i32, vp, vp, vp]
+    L.gm_lstm_pointwise_bwd.argtypes = [vp, vp, vp, vp, vp, i32, i32, vp, vp, vp, vp]
     L.gm_linear_f32.argtypes = [vp, i64, vp, i64, vp, i32, i32, i32, i32, vp, i64, vp]
     L.gm_gemm_set_tile.argtypes = [i32]
     L.gm_env_set_topology.argtypes = [vp, i32, i64, vp, i32, i32]

@@ -42,6 +42,7 @@
 #include <string>
 
 #include "../../include/graph_marl_amd.h"
+#include "gm_amax.hpp"
 
 int gm_fail(int code, const std::string& msg);
 
@@ -67,6 +68,7 @@ struct ASrc {
     int n_nodes, deg, mean, rows_per_graph, k, hidden;
     unsigned bytes0, bytes1;  // buffer extents for the bounds check
     const float* scale;       // k_gemm3 DENSE source: power-of-two A scale (nullable)
+    unsigned* amax;           // k_gemm3: max |A| float bits published here (nullable)
 };
 
 struct Epi {
@@ -620,6 +622,8 @@ __global__ __launch_bounds__(WGM* WGN * 64, OCC) void k_gemm3(ASrc a0, ASrc a1, 
     };
     const bool ascaled = a0.scale != nullptr;  // uniform
     const float ascale = ascaled ? *a0.scale : 1.0f;
+    unsigned* const amax = a0.amax;  // uniform
+    float amx = 0.f;
     auto lstore = [&](auto SET, int buf, int k0) {
         constexpr int S = decltype(SET)::value;
         const bool agg = AMODE == GM_A_AGGREGATE && k0 < a0.k;
@@ -640,6 +644,7 @@ __global__ __launch_bounds__(WGM* WGN * 64, OCC) void k_gemm3(ASrc a0, ASrc a1, 
                 if (kk + 2 >= kend) v.z = 0.f;
                 if (kk + 3 >= kend) v.w = 0.f;
             }
+            if (amax) amx = fmaxf(amx, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
             if (ascaled) v = make_float4(v.x * ascale, v.y * ascale, v.z * ascale, v.w * ascale);
             half4 hi, lo;
 #if GM_DIAG == 1  // diagnostic build: raw bits instead of the split
@@ -722,6 +727,10 @@ __global__ __launch_bounds__(WGM* WGN * 64, OCC) void k_gemm3(ASrc a0, ASrc a1, 
         if (kt + 1 < nk) step(S1{}, kt + 1);
     }
 
+    if (amax) {
+        amx = gm_wave_max(amx);
+        if (lane == 0) gm_amax_publish(amax, amx);
+    }
     const float si = *wscale_inv / ascale;  // undo the weight and A scales (powers of two: exact)
 #pragma unroll
     for (int i = 0; i < TM; i++)
@@ -1065,6 +1074,7 @@ int to_asrc(const gm_a_src* s, int M, ASrc& o) {
     o.k = s->k;
     o.hidden = s->hidden;
     o.scale = s->scale;
+    o.amax = reinterpret_cast<unsigned*>(s->amax);
     if (s->scale && s->mode != GM_A_DENSE)
         return gm_fail(GM_ERR_INVALID_ARG, "gm_gemm: an A scale needs a DENSE source");
     if (!s->p0 || s->k <= 0 || (s->ld0 & 3) || (reinterpret_cast<uintptr_t>(s->p0) & 15))
@@ -1113,7 +1123,7 @@ int dispatch(const ASrc& s0, const ASrc& s1, const float* w, long long ldw, unsi
 #define GM_G(WGM, WGN, TM, TN, S, AM, EP, OC) \
     launch_g<WGM, WGN, TM, TN, S, AM, EP, OC>(s0, s1, w, ldw, wb, m, n, K, ep, st, wsi)
         // default: the readout-sourced DQN layer (the rollout's largest GEMM) on tile 10
-        const int gt = s0.scale ? 0 : (tile >= 8 ? tile : (tile == -1 && s0.mode == GM_A_READOUT && n > 128 ? 10 : 0));
+        const int gt = (s0.scale || s0.amax) ? 0 : (tile >= 8 ? tile : (tile == -1 && s0.mode == GM_A_READOUT && n > 128 ? 10 : 0));
         if (gt >= 8 && s0.mode != GM_A_AGGREGATE) {
             if (epilogue == GM_EPI_LSTM) {
                 ep.hidden = n / 4;
@@ -1226,6 +1236,8 @@ int gemm_entry(bool x3, const gm_a_src* a0, const gm_a_src* a1, const void* w, i
     if (rc) return rc;
     if (s0.scale && (!x3 || a1 || s1.scale))
         return gm_fail(GM_ERR_INVALID_ARG, std::string(fn) + ": an A scale needs the x3 form and a single source");
+    if ((s0.amax && !x3) || s1.amax)
+        return gm_fail(GM_ERR_INVALID_ARG, std::string(fn) + ": amax needs the x3 form and goes on src0");
     if (a1 && (a1->mode != GM_A_DENSE || (s0.k % BKMAX)))
         return gm_fail(GM_ERR_INVALID_ARG, std::string(fn) + ": second A source must be dense and the first k % 32 == 0");
     const int K = s0.k + (a1 ? s1.k : 0);
@@ -1334,7 +1346,7 @@ extern "C" int gm_gemm_x3_head(const gm_a_src* a0, const void* wp, const float* 
     ASrc s0, s1;
     int rc = to_asrc(a0, m, s0);
     if (rc) return rc;
-    if (s0.scale) return gm_fail(GM_ERR_INVALID_ARG, "gm_gemm_x3_head: no A scale");
+    if (s0.scale || s0.amax) return gm_fail(GM_ERR_INVALID_ARG, "gm_gemm_x3_head: no A scale / amax");
     memset(&s1, 0, sizeof(s1));
     const int K = s0.k;
     const long long ldw = (long long)((K + BKMAX - 1) / BKMAX * BKMAX) / 16 * 64, wb = (long long)n * ldw;
@@ -1411,6 +1423,14 @@ extern "C" int gm_absmax_scale_rows(const float* x, int64_t rows, int32_t cols, 
     hipLaunchKernelGGL(k_scale_from_max, dim3(1), dim3(1), 0, st, scale);
     e = hipGetLastError();
     if (e != hipSuccess) return gm_fail(GM_ERR_HIP, std::string("gm_absmax_scale_rows: ") + hipGetErrorString(e));
+    return GM_OK;
+}
+
+extern "C" int gm_absmax_finish(float* scale, void* stream) {
+    if (!scale) return gm_fail(GM_ERR_INVALID_ARG, "gm_absmax_finish: bad arguments");
+    hipLaunchKernelGGL(k_scale_from_max, dim3(1), dim3(1), 0, (hipStream_t)stream, scale);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return gm_fail(GM_ERR_HIP, std::string("gm_absmax_finish: ") + hipGetErrorString(e));
     return GM_OK;
 }
 

@@ -9,9 +9,11 @@
 // graph's 10 KB working set in L2.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <string>
 
 #include "../../include/graph_marl_amd.h"
+#include "gm_amax.hpp"
 
 int gm_fail(int code, const std::string& msg);
 
@@ -192,22 +194,30 @@ __global__ __launch_bounds__(256) void k_lstm_pw(const float* __restrict__ gates
 __global__ __launch_bounds__(256) void k_lstm_pw_bwd(const float* __restrict__ dh1, const float* __restrict__ dc1,
                                                      const float* __restrict__ act, const float* __restrict__ c,
                                                      const float* __restrict__ c1, int M, int H,
-                                                     float* __restrict__ dgates, float* __restrict__ dc) {
-    const long long gid = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-    if (gid >= (long long)M * H) return;
-    const long long m = gid / H;
-    const int j = (int)(gid % H);
-    const float* a = act + m * 4 * H;
-    float i = a[j], f = a[H + j], gg = a[2 * H + j], o = a[3 * H + j];
-    float tc = tanhf(c1[gid]);
-    float dh = dh1 ? dh1[gid] : 0.f;
-    float dct = (dc1 ? dc1[gid] : 0.f) + dh * o * (1.f - tc * tc);
-    float* dg = dgates + m * 4 * H;
-    dg[j] = dct * gg * i * (1.f - i);
-    dg[H + j] = dct * c[gid] * f * (1.f - f);
-    dg[2 * H + j] = dct * i * (1.f - gg * gg);
-    dg[3 * H + j] = dh * tc * o * (1.f - o);
-    dc[gid] = dct * f;
+                                                     float* __restrict__ dgates, float* __restrict__ dc,
+                                                     unsigned* __restrict__ amax) {
+    float mx = 0.f;
+    const long long total = (long long)M * H;
+    for (long long gid = (long long)blockIdx.x * blockDim.x + threadIdx.x; gid < total;
+         gid += (long long)gridDim.x * blockDim.x) {
+        const long long m = gid / H;
+        const int j = (int)(gid % H);
+        const float* a = act + m * 4 * H;
+        float i = a[j], f = a[H + j], gg = a[2 * H + j], o = a[3 * H + j];
+        float tc = tanhf(c1[gid]);
+        float dh = dh1 ? dh1[gid] : 0.f;
+        float dct = (dc1 ? dc1[gid] : 0.f) + dh * o * (1.f - tc * tc);
+        float* dg = dgates + m * 4 * H;
+        const float d0 = dct * gg * i * (1.f - i), d1 = dct * c[gid] * f * (1.f - f);
+        const float d2 = dct * i * (1.f - gg * gg), d3 = dh * tc * o * (1.f - o);
+        dg[j] = d0;
+        dg[H + j] = d1;
+        dg[2 * H + j] = d2;
+        dg[3 * H + j] = d3;
+        dc[gid] = dct * f;
+        mx = fmaxf(mx, fmaxf(fmaxf(fabsf(d0), fabsf(d1)), fmaxf(fabsf(d2), fabsf(d3))));
+    }
+    if (amax) gm_block_amax(amax, mx);
 }
 
 
@@ -353,9 +363,11 @@ static int launch_agg(const float* h, const int32_t* nbr, int32_t G, int32_t N, 
 // Threads own columns, blocks own row chunks; loads and stores are row-contiguous.
 __global__ __launch_bounds__(256) void k_leaky_bwd(const float* __restrict__ gy, const float* __restrict__ y,
                                                    long long rows, int cols, int rows_per_block, float slope,
-                                                   float* __restrict__ g, float* __restrict__ part) {
+                                                   float* __restrict__ g, float* __restrict__ part,
+                                                   unsigned* __restrict__ amax) {
     const long long r0 = (long long)blockIdx.x * rows_per_block;
     const long long r1 = min(rows, r0 + rows_per_block);
+    float m = 0.f;
     for (int c = threadIdx.x; c < cols; c += blockDim.x) {
         float acc = 0.f;
         for (long long r = r0; r < r1; r++) {
@@ -363,19 +375,26 @@ __global__ __launch_bounds__(256) void k_leaky_bwd(const float* __restrict__ gy,
             const float v = y[i] >= 0.f ? gy[i] : slope * gy[i];
             g[i] = v;
             acc += v;
+            m = fmaxf(m, fabsf(v));
         }
         part[(long long)blockIdx.x * cols + c] = acc;
     }
+    if (amax) gm_block_amax(amax, m);
 }
 
 extern "C" int gm_leaky_bwd(const float* gy, const float* y, int64_t rows, int32_t cols, float slope, float* g,
-                            float* part, int32_t rows_per_block, void* stream) {
+                            float* part, int32_t rows_per_block, float* g_scale, void* stream) {
     if (!gy || !y || !g || !part || rows <= 0 || cols <= 0 || rows_per_block <= 0)
         return gm_fail(GM_ERR_INVALID_ARG, "gm_leaky_bwd: bad arguments");
+    hipStream_t st = (hipStream_t)stream;
+    if (g_scale && hipMemsetAsync(g_scale, 0, sizeof(float), st) != hipSuccess)
+        return gm_fail(GM_ERR_HIP, "gm_leaky_bwd: memset");
     const long long nb = (rows + rows_per_block - 1) / rows_per_block;
-    hipLaunchKernelGGL(k_leaky_bwd, dim3((unsigned)nb), dim3(256), 0, (hipStream_t)stream, gy, y, (long long)rows,
-                       (int)cols, (int)rows_per_block, slope, g, part);
-    return launched();
+    hipLaunchKernelGGL(k_leaky_bwd, dim3((unsigned)nb), dim3(256), 0, st, gy, y, (long long)rows, (int)cols,
+                       (int)rows_per_block, slope, g, part, reinterpret_cast<unsigned*>(g_scale));
+    int rc = launched();
+    if (rc == GM_OK && g_scale) rc = gm_absmax_finish(g_scale, stream);
+    return rc;
 }
 
 extern "C" int gm_mp_aggregate(const float* h, const int32_t* nbr, int32_t G, int32_t N, int32_t deg, int32_t H,
@@ -441,13 +460,21 @@ extern "C" int gm_lstm_pointwise(const float* gates, const float* c, int32_t m, 
 }
 
 extern "C" int gm_lstm_pointwise_bwd(const float* dh1, const float* dc1, const float* act, const float* c,
-                                     const float* c1, int32_t m, int32_t H, float* dgates, float* dc, void* stream) {
+                                     const float* c1, int32_t m, int32_t H, float* dgates, float* dc,
+                                     float* dgates_scale, void* stream) {
     if (!act || !c || !c1 || !dgates || !dc || m <= 0 || H <= 0)
         return gm_fail(GM_ERR_INVALID_ARG, "gm_lstm_pointwise_bwd: bad args");
+    hipStream_t st = (hipStream_t)stream;
+    if (dgates_scale && hipMemsetAsync(dgates_scale, 0, sizeof(float), st) != hipSuccess)
+        return gm_fail(GM_ERR_HIP, "gm_lstm_pointwise_bwd: memset");
     long long total = (long long)m * H;
-    hipLaunchKernelGGL(k_lstm_pw_bwd, dim3(nblocks(total, 256)), dim3(256), 0, (hipStream_t)stream, dh1, dc1, act, c,
-                       c1, m, H, dgates, dc);
-    return launched();
+    // grid-stride over at most 4096 blocks: one published max per block
+    const long long nb = std::min<long long>(nblocks(total, 256), 4096);
+    hipLaunchKernelGGL(k_lstm_pw_bwd, dim3((unsigned)nb), dim3(256), 0, st, dh1, dc1, act, c, c1, m, H, dgates, dc,
+                       reinterpret_cast<unsigned*>(dgates_scale));
+    int rc = launched();
+    if (rc == GM_OK && dgates_scale) rc = gm_absmax_finish(dgates_scale, stream);
+    return rc;
 }
 
 extern "C" int gm_routing_node_encoder(const float* x, int64_t ldx, const int32_t* nbr, int32_t G, int32_t N,

@@ -34,7 +34,7 @@ class ASrc(C.Structure):
         ("mode", C.c_int32), ("p0", C.c_void_p), ("p1", C.c_void_p), ("ld0", C.c_int64), ("ld1", C.c_int64),
         ("nbr", C.c_void_p), ("agent_node", C.c_void_p), ("n_nodes", C.c_int32), ("deg", C.c_int32),
         ("mean", C.c_int32), ("rows_per_graph", C.c_int32), ("k", C.c_int32), ("hidden", C.c_int32),
-        ("scale", C.c_void_p),
+        ("scale", C.c_void_p), ("amax", C.c_void_p),
     ]
 
 
@@ -47,6 +47,7 @@ def _setup():
         lib.gm_gemm_x3.argtypes = [C.POINTER(ASrc), C.POINTER(ASrc), vp, vp, vp, C.c_int32, C.c_int32,
                                    C.c_int32, vp, C.c_int64, vp, C.c_int64, vp, C.c_int64, vp, vp]
         lib.gm_absmax_scale.argtypes = [vp, C.c_int64, vp, vp]
+        lib.gm_absmax_finish.argtypes = [vp, vp]
         lib.gm_absmax_scale_rows.argtypes = [vp, C.c_int64, C.c_int32, C.c_int64, vp, vp]
         lib.gm_gemm_x3_wgrad.argtypes = [vp, C.c_int64, vp, C.c_int64, C.c_int32, C.c_int32, C.c_int32, C.c_int32,
                                          vp, vp, vp, C.c_int64, vp]
@@ -75,11 +76,13 @@ def use_x3(n):
     return L.GEMM_MODE == "x3" and n > 32
 
 
-def dense(p, ld, k, scale=None):
-    """DENSE A source; scale: device float from gm_absmax_scale (split-f16 form only)."""
+def dense(p, ld, k, scale=None, amax=None):
+    """DENSE A source; scale: device float from gm_absmax_scale; amax: zeroed device float that
+    receives max|A| as float bits (gm_absmax_finish turns it into the scale); split-f16 only."""
     s = ASrc()
     s.mode, s.p0, s.ld0, s.k = GM_A_DENSE, p, ld, k
     s.scale = scale
+    s.amax = amax
     return s
 
 

@@ -74,8 +74,30 @@ class _WeightCache:
         return self.val, kp
 
 
-def linear_raw(x2d, ldx, k, w, b, act, out=None, ldy=None, wcache=None, tag=None):
-    """y = act(x @ w^T + b) on the MFMA kernel. x2d: row-major rows with stride ldx."""
+def _x3_rows_ok(x2d, ldx, n):
+    from . import fused as FU
+
+    return FU.use_x3(n) and ldx % 4 == 0 and x2d.data_ptr() % 16 == 0
+
+
+def _amax_slot(x2d, ldx, n, wanted):
+    """Zeroed device slot for the forward GEMM to publish max|x| into (the weight gradient's
+    operand scale, so backward needs no extra pass over x), or None."""
+    if wanted and x2d.shape[0] >= 4096 and _x3_rows_ok(x2d, ldx, n):
+        return torch.zeros(1, device=x2d.device)
+    return None
+
+
+def _finish_scale(slot):
+    from . import fused as FU
+
+    L.check(FU._setup().gm_absmax_finish(slot.data_ptr(), L.stream_ptr()))
+    return slot
+
+
+def linear_raw(x2d, ldx, k, w, b, act, out=None, ldy=None, wcache=None, tag=None, amax=None):
+    """y = act(x @ w^T + b) on the MFMA kernel. x2d: row-major rows with stride ldx.
+    amax: slot from _amax_slot (split-f16 form only; the kernel publishes max|x| into it)."""
     m = x2d.shape[0]
     n = w.shape[0]
     wp, ldw = (wcache.get(w) if wcache is not None else _WeightCache().get(w))
@@ -84,12 +106,14 @@ def linear_raw(x2d, ldx, k, w, b, act, out=None, ldy=None, wcache=None, tag=None
         ldy = n
     from . import fused as FU
 
-    if FU.use_x3(n) and ldx % 4 == 0 and x2d.data_ptr() % 16 == 0:
+    if _x3_rows_ok(x2d, ldx, n):
         # split-f16 form (fp32-order error, tests/test_fused_gpu.py), as in the rollout
         x3 = (wcache if wcache is not None else _WeightCache()).x3(w)
-        FU.gemm(FU.dense(x2d.data_ptr(), ldx, k), None, wp.data_ptr(), ldw, L.ptr(b), m, n, act, out.data_ptr(), ldy,
+        FU.gemm(FU.dense(x2d.data_ptr(), ldx, k, amax=None if amax is None else amax.data_ptr()), None,
+                wp.data_ptr(), ldw, L.ptr(b), m, n, act, out.data_ptr(), ldy,
                 tag=tag and f"linear:{tag}:{m}x{n}x{k}", x3=x3)
         return out
+    assert amax is None, "amax needs the split-f16 form"
     with L.timed(tag and f"linear:{tag}:{m}x{n}x{k}"):
         L.check(L.lib().gm_linear_f32(L.ptr(x2d), ldx, L.ptr(wp), ldw, L.ptr(b), m, n, k, act, L.ptr(out), ldy,
                                       _s()))
@@ -136,7 +160,7 @@ def _dgrad(gy, w, wcache=None, sc=None):
     return gy @ w
 
 
-def _wgrad(gy, x, k, sa=None):
+def _wgrad(gy, x, k, sa=None, sb=None):
     """gW = gy^T @ x[:, :k], a reduction over the batch rows: split-K split-f16 GEMM on the
     K-major operands (gm_gemm_x3_wgrad; both scaled by device powers of two), partials summed
     here; library fp32 GEMM when the shapes do not fit the kernel."""
@@ -154,9 +178,10 @@ def _wgrad(gy, x, k, sa=None):
     lib = FU._setup()
     dev = gy.device
     sa = _gy_scale(gy) if sa is None else sa
-    # scale from the k real columns; the up to 3 padding columns only reach output columns >= k
-    sb = torch.empty(1, device=dev)
-    L.check(lib.gm_absmax_scale_rows(x.data_ptr(), Mb, k, ldx, sb.data_ptr(), L.stream_ptr()))
+    if sb is None:
+        # scale from the k real columns; the up to 3 padding columns only reach output columns >= k
+        sb = torch.empty(1, device=dev)
+        L.check(lib.gm_absmax_scale_rows(x.data_ptr(), Mb, k, ldx, sb.data_ptr(), L.stream_ptr()))
     tiles = ((o + 127) // 128) * ((N + 127) // 128)
     splits = max(1, min(Mb // 2048, (1024 + tiles - 1) // tiles))
     kchunk = ((Mb + splits - 1) // splits + 15) // 16 * 16
@@ -171,7 +196,9 @@ class LinearFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w, b, act, wcache, tag=None):
         x2, ldx, k = _as_rows(x)
-        y = linear_raw(x2, ldx, k, w, b, act, wcache=wcache, tag=tag)
+        xs = _amax_slot(x2, ldx, w.shape[0], ctx.needs_input_grad[1])
+        y = linear_raw(x2, ldx, k, w, b, act, wcache=wcache, tag=tag, amax=xs)
+        ctx.xs = None if xs is None else _finish_scale(xs)
         ctx.act = act
         ctx.wcache = wcache
         ctx.save_for_backward(x2[:, :k] if x2.shape[1] != k else x2, w, y)
@@ -182,25 +209,28 @@ class LinearFn(torch.autograd.Function):
         x2, w, y = ctx.saved_tensors
         gy = gy.reshape(-1, w.shape[0])
         gb = None
+        sc = None
         if ctx.act == 1:
             if gy.is_contiguous() and y.is_contiguous() and gy.shape[0] >= 4096:
-                # leaky_relu backward + per-block bias-gradient partial sums in one pass
+                # leaky_relu backward + per-block bias-gradient partial sums + max|g| (the
+                # gradient GEMMs' operand scale) in one pass
                 rows, cols = gy.shape
                 rpb = 64
                 g2 = torch.empty_like(gy)
                 part = torch.empty((rows + rpb - 1) // rpb, cols, device=gy.device)
+                sc = torch.empty(1, device=gy.device)
                 L.check(L.lib().gm_leaky_bwd(gy.data_ptr(), y.data_ptr(), rows, cols, 0.01, g2.data_ptr(),
-                                             part.data_ptr(), rpb, _s()))
+                                             part.data_ptr(), rpb, sc.data_ptr(), _s()))
                 gy = g2
                 if ctx.needs_input_grad[2]:
                     gb = part.sum(0)
             else:
                 gy = torch.where(y >= 0, gy, 0.01 * gy)
-        sc = None
-        if ctx.needs_input_grad[0] and ctx.needs_input_grad[1] and gy.is_contiguous() and gy.shape[0] >= 4096:
+        if sc is None and ctx.needs_input_grad[0] and ctx.needs_input_grad[1] and gy.is_contiguous() \
+                and gy.shape[0] >= 4096:
             sc = _gy_scale(gy)  # one scale for both gradient GEMMs
         gx = _dgrad(gy, w, ctx.wcache, sc) if ctx.needs_input_grad[0] else None
-        gw = _wgrad(gy, x2, w.shape[1], sc) if ctx.needs_input_grad[1] else None
+        gw = _wgrad(gy, x2, w.shape[1], sc, ctx.xs) if ctx.needs_input_grad[1] else None
         if gb is None and ctx.needs_input_grad[2]:
             gb = gy.sum(0)
         if gx is not None:
@@ -350,8 +380,48 @@ class _LSTMPointwise(torch.autograd.Function):
         dh1 = None if dh1 is None else dh1.contiguous()
         dc1 = None if dc1 is None else dc1.contiguous()
         L.check(L.lib().gm_lstm_pointwise_bwd(L.ptr(dh1), L.ptr(dc1), L.ptr(act), L.ptr(c), L.ptr(c1), M, H,
-                                              L.ptr(dg), L.ptr(dc), _s()))
+                                              L.ptr(dg), L.ptr(dc), None, _s()))
         return dg, dc
+
+
+class _LSTMCellFn(torch.autograd.Function):
+    """One LSTMCell step as one autograd node: gates = [x|h] W^T + b (split-f16 GEMM that
+    publishes max|[x|h]| for the weight gradient) and the gate math; backward runs the gate-math
+    backward (publishing max|dgates|) straight into the two gradient GEMMs, so neither operand
+    scale costs a pass of its own."""
+
+    @staticmethod
+    def forward(ctx, xh, w, b, c, wcache, tag):
+        x2, ldx, k = _as_rows(xh)
+        xs = _amax_slot(x2, ldx, w.shape[0], ctx.needs_input_grad[1])
+        gates = linear_raw(x2, ldx, k, w, b, 0, wcache=wcache, tag=tag, amax=xs)
+        ctx.xs = None if xs is None else _finish_scale(xs)
+        M, H4 = gates.shape
+        H = H4 // 4
+        h1 = torch.empty(M, H, device=gates.device)
+        c1 = torch.empty(M, H, device=gates.device)
+        act = torch.empty_like(gates)
+        L.check(L.lib().gm_lstm_pointwise(L.ptr(gates), L.ptr(c), M, H, L.ptr(h1), L.ptr(c1), L.ptr(act), _s()))
+        ctx.wcache = wcache
+        ctx.save_for_backward(x2[:, :k] if x2.shape[1] != k else x2, w, act, c, c1)
+        return h1, c1
+
+    @staticmethod
+    def backward(ctx, dh1, dc1):
+        x2, w, act, c, c1 = ctx.saved_tensors
+        M, H = c.shape
+        dg = torch.empty(M, 4 * H, device=c.device)
+        dc = torch.empty(M, H, device=c.device)
+        sc = torch.empty(1, device=c.device)
+        dh1 = None if dh1 is None else dh1.contiguous()
+        dc1 = None if dc1 is None else dc1.contiguous()
+        L.check(L.lib().gm_lstm_pointwise_bwd(L.ptr(dh1), L.ptr(dc1), L.ptr(act), L.ptr(c), L.ptr(c1), M, H,
+                                              L.ptr(dg), L.ptr(dc), L.ptr(sc), _s()))
+        n = ctx.needs_input_grad
+        gx = _dgrad(dg, w, ctx.wcache, sc) if n[0] else None
+        gw = _wgrad(dg, x2, w.shape[1], sc, ctx.xs) if n[1] else None
+        gb = dg.sum(0) if n[2] else None
+        return gx, gw, gb, dc if n[3] else None, None, None
 
 
 class LSTMCell(nn.Module):
@@ -377,6 +447,8 @@ class LSTMCell(nn.Module):
         w = torch.cat([self.weight_ih, self.weight_hh], 1)
         b = self.bias_ih + self.bias_hh
         if torch.is_grad_enabled() and (w.requires_grad or xh.requires_grad):
+            if xh.shape[0] >= 4096 and _x3_rows_ok(xh, xh.stride(0), w.shape[0]):
+                return _LSTMCellFn.apply(xh, w, b, c.contiguous(), None, self.tag)
             gates = LinearFn.apply(xh, w, b, 0, None, self.tag)
         else:
             gates = linear_raw(xh, xh.stride(0), xh.shape[1], w, b, 0, tag=self.tag)

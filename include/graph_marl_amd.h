@@ -23,7 +23,7 @@
  *   gm_gemm_f32                      Linear / LSTMCell GEMMs with aggregate, readout and gate math fused
  *   gm_gemm_x3 / gm_gemm_pack_x3     the same GEMMs in split-f16 form (f16 MFMA, fp32 accumulate)
  *   gm_gemm_x3_head                  last DQN layer + Q head in one kernel
- *   gm_absmax_scale                  power-of-two operand scale for gm_gemm_x3 (input gradients)
+ *   gm_absmax_scale(_rows/_finish)   power-of-two operand scale for gm_gemm_x3 (input gradients)
  *   gm_gemm_x3_wgrad                 split-K weight-gradient GEMM over K-major operands
  *   gm_agent_attention               AttModel attention core (DGN)          src/model.py:86-117
  *   gm_agent_comm                    CommNet communication step             src/model.py:780-787
@@ -182,9 +182,10 @@ int gm_mp_aggregate_rows(const float* h, int64_t ldh, const int32_t* nbr, int32_
                          int32_t deg, int32_t hidden, int32_t mode, float* out, int64_t ldo, void* stream);
 /* Backward of a Linear followed by leaky_relu (MLP layers, src/model.py:13-42): g = dY where
  * Y >= 0 else slope * dY ([rows][cols] contiguous), and per-block column sums of g for the bias
- * gradient: part[ceil(rows / rows_per_block)][cols] (the caller sums the blocks). */
+ * gradient: part[ceil(rows / rows_per_block)][cols] (the caller sums the blocks); g_scale
+ * (nullable) receives the power-of-two scale of g (as gm_absmax_scale, without a second pass). */
 int gm_leaky_bwd(const float* dy, const float* y, int64_t rows, int32_t cols, float slope, float* g, float* part,
-                 int32_t rows_per_block, void* stream);
+                 int32_t rows_per_block, float* g_scale, void* stream);
 /* Backward of gm_mp_aggregate for symmetric adjacency: dh[j] = Σ_{n ∈ {j} ∪ nbr(j)} dout[n] / cnt(n). */
 int gm_mp_aggregate_bwd(const float* dout, const int32_t* nbr, int32_t n_graphs, int32_t n_nodes, int32_t deg,
                         int32_t hidden, int32_t mode, float* dh, void* stream);
@@ -202,9 +203,11 @@ int gm_netmon_readout_bwd(const float* dout, int64_t dout_stride, const int32_t*
  * -> h_new, c_new [M, H]; saves sigmoid/tanh activations in act [M, 4H] if non-NULL. */
 int gm_lstm_pointwise(const float* gates, const float* c, int32_t m, int32_t hidden, float* h_new, float* c_new,
                       float* act, void* stream);
-/* Backward: given dh_new, dc_new (nullable = 0), act, c, c_new -> dgates [M,4H], dc [M,H]. */
+/* Backward: given dh_new, dc_new (nullable = 0), act, c, c_new -> dgates [M,4H], dc [M,H];
+ * dgates_scale (nullable) receives the power-of-two scale of dgates (as gm_absmax_scale). */
 int gm_lstm_pointwise_bwd(const float* dh_new, const float* dc_new, const float* act, const float* c,
-                          const float* c_new, int32_t m, int32_t hidden, float* dgates, float* dc, void* stream);
+                          const float* c_new, int32_t m, int32_t hidden, float* dgates, float* dc,
+                          float* dgates_scale, void* stream);
 /* Fused f32 MFMA linear layer: y[M,N] = act(x[M,K] @ w[N,K]^T + b[N]); row strides ldx, ldw
  * (multiples of 4 floats, 16-byte aligned bases), ldy; K may be ragged; b nullable;
  * act 0 = none, 1 = leaky_relu(0.01). */
@@ -229,6 +232,8 @@ typedef struct {
     int32_t hidden;            /* READOUT: H (multiple of 32)                                      */
     const float* scale;        /* gm_gemm_x3, DENSE src0 without src1 (nullable): device power of  */
                                /* two s from gm_absmax_scale; A is split as s*A, the result / s    */
+    uint32_t* amax;            /* gm_gemm_x3, src0 (nullable): max |A| over [src0 | src1] published */
+                               /* as float bits by atomicMax (zero it first; gm_absmax_finish)      */
 } gm_a_src;
 /* src1 (nullable) must be DENSE and src0->k a multiple of 32. W: [n][ldw] (ldw >= K, zero
  * padded to a multiple of 4). GM_EPI_LSTM: W rows packed so that rows [128t, 128t+128) are
@@ -269,6 +274,10 @@ int gm_gemm_x3_wgrad(const float* a, int64_t lda, const float* b, int64_t ldb, i
 int gm_absmax_scale(const float* x, int64_t n, float* scale, void* stream);
 /* The same scale for a [rows][cols] block with row stride ld (floats). */
 int gm_absmax_scale_rows(const float* x, int64_t rows, int32_t cols, int64_t ld, float* scale, void* stream);
+/* The same scale from a max already published by a producer (gm_gemm_x3's src0 amax,
+ * gm_leaky_bwd, gm_lstm_pointwise_bwd): *scale holds max|x| as float bits on entry, the scale
+ * on exit. */
+int gm_absmax_finish(float* scale, void* stream);
 /* Packed size in bytes of an [n][k] weight for gm_gemm_x3: n * ceil(k/32)*2 blocks * 64 B. */
 int64_t gm_gemm_pack_x3_bytes(int32_t n, int32_t k);
 /* Split W [n][ldw] (first k columns) into wp (16-byte aligned, gm_gemm_pack_x3_bytes):

@@ -293,3 +293,93 @@ def test_linear_backward_large_batch(rows, k, n, act):
     for got, ref, mag in ((x.grad, xd.grad, mag_x), (lin.weight.grad, wd.grad, mag_w), (lin.bias.grad, bd.grad, mag_b)):
         rel = ((got.double() - ref).abs() / mag.clamp_min(1e-300)).max().item()
         assert rel < 1e-5, rel
+
+
+@pytest.mark.parametrize("rows,k,n", [(8192, 642, 512), (4096, 256, 512)])
+def test_forward_amax_publishes_max(rows, k, n):
+    """gm_gemm_x3's src0 amax: the forward GEMM publishes max|x| (exact float bits) and
+    gm_absmax_finish turns it into the same scale gm_absmax_scale_rows computes."""
+    gm, M, FU, W = mods()
+    if FU.L.GEMM_MODE != "x3":
+        pytest.skip("split-f16 form disabled (GM_GEMM=f32)")
+    torch.manual_seed(rows + k)
+    ld = (k + 3) // 4 * 4 + 4
+    xb = torch.randn(rows, ld, device="cuda") * 3.0
+    xb[:, k:] = 1e6  # padding columns past k must not count
+    x = xb[:, :k]
+    w = torch.randn(n, k, device="cuda") * 0.05
+    slot = M._amax_slot(xb, ld, n, True)
+    assert slot is not None
+    y = M.linear_raw(xb, ld, k, w, None, 0, amax=slot)
+    torch.cuda.synchronize()
+    assert slot.view(torch.int32).item() == x.abs().max().view(torch.int32).item()
+    M._finish_scale(slot)
+    ref = torch.empty(1, device="cuda")
+    FU.L.check(FU._setup().gm_absmax_scale_rows(xb.data_ptr(), rows, k, ld, ref.data_ptr(), FU.L.stream_ptr()))
+    assert slot.item() == ref.item()
+    torch.testing.assert_close(y, x @ w.t(), rtol=1e-5, atol=1e-4)
+
+
+def test_backward_kernels_publish_scale():
+    """gm_leaky_bwd / gm_lstm_pointwise_bwd g_scale == gm_absmax_scale of their output."""
+    gm, M, FU, W = mods()
+    lib = FU._setup()
+    torch.manual_seed(11)
+    rows, cols = 5000, 256
+    gy = torch.randn(rows, cols, device="cuda") * 1e-4
+    y = torch.randn(rows, cols, device="cuda")
+    g = torch.empty_like(gy)
+    part = torch.empty((rows + 63) // 64, cols, device="cuda")
+    sc = torch.empty(1, device="cuda")
+    FU.L.check(lib.gm_leaky_bwd(gy.data_ptr(), y.data_ptr(), rows, cols, 0.01, g.data_ptr(), part.data_ptr(), 64,
+                                sc.data_ptr(), FU.L.stream_ptr()))
+    ref = M._gy_scale(g)
+    assert sc.item() == ref.item()
+    torch.testing.assert_close(g, torch.where(y >= 0, gy, 0.01 * gy), rtol=0, atol=0)
+    Mr, H = 9000, 128
+    act = torch.rand(Mr, 4 * H, device="cuda")
+    c = torch.randn(Mr, H, device="cuda")
+    c1 = torch.randn(Mr, H, device="cuda")
+    dh = torch.randn(Mr, H, device="cuda") * 1e-3
+    dg = torch.empty(Mr, 4 * H, device="cuda")
+    dc = torch.empty(Mr, H, device="cuda")
+    sc2 = torch.empty(1, device="cuda")
+    FU.L.check(lib.gm_lstm_pointwise_bwd(dh.data_ptr(), None, act.data_ptr(), c.data_ptr(), c1.data_ptr(), Mr, H,
+                                         dg.data_ptr(), dc.data_ptr(), sc2.data_ptr(), FU.L.stream_ptr()))
+    dg0 = torch.empty_like(dg)
+    dc0 = torch.empty_like(dc)
+    FU.L.check(lib.gm_lstm_pointwise_bwd(dh.data_ptr(), None, act.data_ptr(), c.data_ptr(), c1.data_ptr(), Mr, H,
+                                         dg0.data_ptr(), dc0.data_ptr(), None, FU.L.stream_ptr()))
+    assert torch.equal(dg, dg0) and torch.equal(dc, dc0)
+    assert sc2.item() == M._gy_scale(dg).item()
+
+
+@pytest.mark.parametrize("rows", [8192, 1000])
+def test_lstm_cell_backward_large_batch(rows):
+    """LSTMCell step at training batch sizes (one autograd node: gates GEMM + gate math, scales
+    published by the producers) vs fp64 autograd of nn.LSTMCell semantics."""
+    gm, M, FU, W = mods()
+    torch.manual_seed(rows)
+    H = 128
+    cell = M.LSTMCell(H, H).cuda()
+    x = torch.randn(rows, H, device="cuda", requires_grad=True)
+    h = torch.randn(rows, H, device="cuda", requires_grad=True)
+    c = torch.randn(rows, H, device="cuda", requires_grad=True)
+    h1, c1 = cell(x, (h, c))
+    gh = torch.randn_like(h1) * 1e-4
+    gc = torch.randn_like(c1) * 1e-4
+    torch.autograd.backward((h1, c1), (gh, gc))
+    ref = torch.nn.LSTMCell(H, H).double().cuda()
+    with torch.no_grad():
+        for name in ("weight_ih", "weight_hh", "bias_ih", "bias_hh"):
+            getattr(ref, name).copy_(getattr(cell, name).double())
+    xd, hd, cd = (t.detach().double().requires_grad_(True) for t in (x, h, c))
+    h1d, c1d = ref(xd, (hd, cd))
+    torch.testing.assert_close(h1.double(), h1d, rtol=0, atol=2e-5)
+    torch.testing.assert_close(c1.double(), c1d, rtol=0, atol=2e-5)
+    torch.autograd.backward((h1d, c1d), (gh.double(), gc.double()))
+    for got, want in ((x.grad, xd.grad), (h.grad, hd.grad), (c.grad, cd.grad), (cell.weight_ih.grad, ref.weight_ih.grad),
+                      (cell.weight_hh.grad, ref.weight_hh.grad), (cell.bias_ih.grad, ref.bias_ih.grad)):
+        scale = want.abs().max().item()
+        err = (got.double() - want).abs().max().item()
+        assert err <= 1e-5 * scale + 1e-12, (err, scale)
