@@ -1122,8 +1122,19 @@ int dispatch(const ASrc& s0, const ASrc& s1, const float* w, long long ldw, unsi
         // LDS-DMA kernel (tiles 8..14) for dense / readout sources
 #define GM_G(WGM, WGN, TM, TN, S, AM, EP, OC) \
     launch_g<WGM, WGN, TM, TN, S, AM, EP, OC>(s0, s1, w, ldw, wb, m, n, K, ep, st, wsi)
-        // default: the readout-sourced DQN layer (the rollout's largest GEMM) on tile 10
-        const int gt = (s0.scale || s0.amax) ? 0 : (tile >= 8 ? tile : (tile == -1 && s0.mode == GM_A_READOUT && n > 128 ? 10 : 0));
+        // defaults (tools/gemm_bench.py on MI355X): the readout-sourced DQN layer (the rollout's
+        // largest GEMM) on tile 10; wide dense layers with K >= 256 at rollout batch sizes (incl.
+        // the LSTM gate GEMMs on [x | h]) on tile 12 (128x128, 2 blocks/CU: 7-11 % faster than
+        // k_gemm3 at 81920 rows); narrow or short-K layers on k_gemm3
+        int gt = 0;
+        if (s0.scale || s0.amax)
+            gt = 0;
+        else if (tile >= 8)
+            gt = tile;
+        else if (tile == -1 && s0.mode == GM_A_READOUT && n > 128)
+            gt = 10;
+        else if (tile == -1 && s0.mode == GM_A_DENSE && n >= 256 && K >= 256 && m >= 32768)
+            gt = 12;
         if (gt >= 8 && s0.mode != GM_A_AGGREGATE) {
             if (epilogue == GM_EPI_LSTM) {
                 ep.hidden = n / 4;
@@ -1601,7 +1612,7 @@ extern "C" int gm_gemm_pack_x3(const float* w, int64_t ldw, int32_t n, int32_t k
 }
 
 extern "C" int gm_gemm_set_tile(int32_t tile) {
-    if (tile < -1 || tile > 11) return gm_fail(GM_ERR_INVALID_ARG, "gm_gemm_set_tile: tile in [-1, 11]");
+    if (tile < -1 || tile > 14) return gm_fail(GM_ERR_INVALID_ARG, "gm_gemm_set_tile: tile in [-1, 14]");
     g_tile = tile;
     return GM_OK;
 }

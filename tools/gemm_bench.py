@@ -18,6 +18,10 @@ SHAPES = [  # name, M, N, K
 ]
 
 
+if os.environ.get("SHAPES") == "train":  # the update's dense layers at 131072 rows (8 x 819 sequences x 20)
+    SHAPES = [("dqn.l1", 131072, 512, 642), ("dqn.l2", 131072, 256, 512), ("enc.l1", 131072, 256, 512),
+              ("enc.l2", 131072, 128, 256), ("lstm", 131072, 512, 256)]
+
 TILES = [int(t) for t in os.environ.get("TILES", "-1").split(",")]
 X3_TILES = [int(t) for t in os.environ.get("X3_TILES", "-1,1,2").split(",")]
 
