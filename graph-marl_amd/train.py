@@ -55,6 +55,10 @@ def interpolate_model(a, b, a_weight, target):
         st[k].copy_(a_weight * sa[k] + (1 - a_weight) * sb[k])
 
 
+# the no-grad target pass on the fused rollout kernels (False: NetMon.forward_graph + joint obs)
+FUSED_TARGET = True
+
+
 def joint_obs(env_obs, network_obs):
     return torch.cat([env_obs, network_obs], -1)
 
@@ -72,6 +76,34 @@ def attention_kl(att_weights, tar_att_weights, done):
     return (kl * ~done).sum() / torch.clamp((~done).sum(), min=1)
 
 
+def _fused_target_ok(netmon, model_tar):
+    """The no-grad target pass can run the rollout's fused kernels (fused.netmon_step +
+    fused.dqn_q) under the same conditions as a fused NetMonWrapper with a DQN."""
+    from .model import DQN
+
+    return (netmon is not None and isinstance(model_tar, DQN) and netmon.rnn_type == "lstm"
+            and netmon.rnn_carryover and netmon.output_neighbor_hidden and not netmon.output_global_hidden
+            and netmon.hidden_features % 32 == 0)
+
+
+@torch.no_grad()
+def _fused_next_q(netmon, model_tar, batch):
+    """Q_target(next obs) [B, A, actions] without materialising the joint next observation:
+    the NetMon step on the next node observations (continuing from netmon.state) and the
+    target DQN with the readout gathered inside its first GEMM (the rollout's path)."""
+    from . import fused as FU
+
+    B, A, od = batch.next_obs.shape
+    odp = (od + 3) // 4 * 4  # 16-byte rows for the GEMM's dense source
+    env_obs = batch.next_obs.contiguous() if odp == od else F.pad(batch.next_obs, (0, odp - od))
+    state, h_prev = FU.netmon_step(netmon, batch.next_node_obs, batch.nbr.contiguous(),
+                                   netmon.state.detach().contiguous())
+    dev = env_obs.device
+    q = FU.dqn_q(model_tar, env_obs, od, state, h_prev, batch.nbr.contiguous(), batch.next_agent_node.contiguous(),
+                 lambda i, m, n: torch.empty(m, n, device=dev))
+    return q.view(B, A, -1)
+
+
 def dqn_loss(netmon, model, model_tar, batches, gamma, att_coeff=0.0):
     """Sequence loss of src/main.py:840-960 for DQN / DGN / DQNR / CommNet (no aux term);
     netmon may be None. Recurrent models start from the stored agent state, the target
@@ -82,6 +114,7 @@ def dqn_loss(netmon, model, model_tar, batches, gamma, att_coeff=0.0):
     loss_q = loss_att = None
     qs, qts = [], []
     last_state = last_ep_done = None
+    fused_tar = not has_state and _fused_target_ok(netmon, model_tar) and FUSED_TARGET
     for t, batch in enumerate(batches):
         if has_state and t == 0:
             model.state = batch.agent_state
@@ -101,10 +134,13 @@ def dqn_loss(netmon, model, model_tar, batches, gamma, att_coeff=0.0):
         with torch.no_grad():
             if has_state:
                 model_tar.state = model.state.detach()
-            if netmon is not None:
-                nno = netmon.forward_graph(batch.next_node_obs, batch.nbr, batch.next_agent_node)
-                next_obs = joint_obs(batch.next_obs, nno)
-            next_q_max = model_tar(next_obs, batch.next_adj).max(dim=2)[0]
+            if fused_tar:
+                next_q_max = _fused_next_q(netmon, model_tar, batch).max(dim=2)[0]
+            else:
+                if netmon is not None:
+                    nno = netmon.forward_graph(batch.next_node_obs, batch.nbr, batch.next_agent_node)
+                    next_obs = joint_obs(batch.next_obs, nno)
+                next_q_max = model_tar(next_obs, batch.next_adj).max(dim=2)[0]
         if has_state:
             ep = batch.episode_done.expand(batch.obs.shape[0]) if batch.episode_done.dim() == 0 \
                 else batch.episode_done

@@ -109,6 +109,19 @@ def test_replay_sequences_and_full_update_on_env_data():
     envs = torch.stack([s.idx[1] for s in seqs])
     assert (envs == envs[0]).all()
     assert ((slots[1:] - slots[:-1]) % rb.count == 1).all()
+    # the fused no-grad target pass (fused.netmon_step + fused.dqn_q) == NetMon.forward_graph +
+    # joint obs + target DQN
+    assert T._fused_target_ok(netmon, target)
+    with torch.no_grad():
+        l1, q1, t1 = T.dqn_loss(netmon, model, target, seqs, 0.9)
+        T.FUSED_TARGET = False
+        try:
+            l0, q0, t0 = T.dqn_loss(netmon, model, target, seqs, 0.9)
+        finally:
+            T.FUSED_TARGET = True
+    for a, b in zip(t1, t0):
+        torch.testing.assert_close(a, b, rtol=0, atol=1e-5)
+    torch.testing.assert_close(l1, l0, rtol=1e-5, atol=1e-7)
     params = list(model.parameters()) + list(netmon.parameters())
     before = [p.detach().clone() for p in params]
     opt = torch.optim.AdamW(params, lr=1e-3)
