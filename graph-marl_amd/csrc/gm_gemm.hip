@@ -1464,16 +1464,18 @@ extern "C" int gm_absmax_scale(const float* x, int64_t n, float* scale, void* st
 // A = dY [K][lda], B = X [K][ldb], both K-major fp32 (K = batch rows) — the transposes are done
 // on the way into LDS. Both operands are scaled by device powers of two (sa, sb) and split as
 // a = a_hi + 2^-12 a_lo' (both pieces normal f16), a*b ~ a_hi b_hi + 2^-12 (a_lo' b_hi + a_hi b_lo')
-// with the 2^-12 terms in a second accumulator. 128x128x16 tiles, 4 waves of 64x64; each
-// thread moves one 4(k) x 4(m|n) sub-block per k step (16 coalesced dword loads, a register
-// transpose, 2 x 8-B LDS stores per column). Split-K over blockIdx.y, partial sums
+// with the 2^-12 terms in a second accumulator. 128x128x32 tiles, 4 waves of 64x64; each
+// thread moves two 4(k) x 4(m|n) sub-blocks per k step (32 coalesced dword loads, a register
+// transpose, 2 x 8-B LDS stores per column and block). Split-K over blockIdx.y, partial sums
 // written to C + z * cz (the caller reduces them).
 __global__ __launch_bounds__(256, 2) void k_gemm3_kmajor(const float* __restrict__ A, long long lda,
                                                         const float* __restrict__ B, long long ldb, int M, int N,
                                                         int K, int kchunk, const float* __restrict__ sa,
                                                         const float* __restrict__ sb, float* __restrict__ C,
                                                         long long ldc, long long cz) {
-    constexpr int BM = 128, BN = 128, BK = 16, ROWB = 80, TM = 2, TN = 2;
+    // 32-deep k tiles: per LDS row two 16-deep blocks of [16 hi | 16 lo] halves (64 B each) + 16 B
+    // pad (conflict-free ds_read_b128 over the 32 rows of a fragment, as k_gemm3's BK=32 tiles)
+    constexpr int BM = 128, BN = 128, BK = 32, ROWB = 4 * BK + 16, TM = 2, TN = 2;
     __shared__ __attribute__((aligned(16))) char As[2][BM * ROWB];
     __shared__ __attribute__((aligned(16))) char Bs[2][BN * ROWB];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -1482,10 +1484,9 @@ __global__ __launch_bounds__(256, 2) void k_gemm3_kmajor(const float* __restrict
     const int m0 = (blockIdx.x / nN) * BM, n0 = (blockIdx.x % nN) * BN;
     const int kb = blockIdx.y * kchunk, ke = min(K, kb + kchunk);
     const int nk = (ke - kb + BK - 1) / BK;
-    // this thread's sub-block: operand (A for tid < 128), 4-deep k group k4, 4-wide column group c4
-    // this thread: operand (A for tid < 128), 4-deep k group k4, columns c4 + 32 c (c = 0..3):
-    // dword loads (coalesced over c4) and LDS rows c4 + 32 c (consecutive rows per store
-    // instruction: conflict-free 8-B stores on the 80-B row pitch)
+    // this thread: operand (A for tid < 128), 4-deep k groups k4 and k4 + 4 (one per 16-deep
+    // block), columns c4 + 32 c (c = 0..3): dword loads (coalesced over c4) and LDS rows
+    // c4 + 32 c (consecutive rows per store instruction: conflict-free 8-B stores)
     const bool isA = tid < 128;
     const int t = tid & 127, k4 = t >> 5, c4 = t & 31;
     const float* src = isA ? A : B;
@@ -1493,26 +1494,31 @@ __global__ __launch_bounds__(256, 2) void k_gemm3_kmajor(const float* __restrict
     const int col0 = (isA ? m0 : n0) + c4, lim = isA ? M : N;
     const float s = isA ? *sa : *sb;
     char* dstb[2] = {(isA ? As[0] : Bs[0]) + c4 * ROWB + 8 * k4, (isA ? As[1] : Bs[1]) + c4 * ROWB + 8 * k4};
-    float rv[4][4];  // [column c][k row r]
+    float rv[2][4][4];  // [16-deep block g][column c][k row r]
     auto load = [&](int kt) {
-        const int k = kb + kt * BK + 4 * k4;
 #pragma unroll
-        for (int r = 0; r < 4; r++) {
-            const float* rowp = src + (long long)(k + r) * ld + col0;
-            const bool kok = k + r < ke;
+        for (int g = 0; g < 2; g++) {
+            const int k = kb + kt * BK + 16 * g + 4 * k4;
 #pragma unroll
-            for (int c = 0; c < 4; c++) rv[c][r] = (kok && col0 + 32 * c < lim) ? rowp[32 * c] : 0.f;
+            for (int r = 0; r < 4; r++) {
+                const float* rowp = src + (long long)(k + r) * ld + col0;
+                const bool kok = k + r < ke;
+#pragma unroll
+                for (int c = 0; c < 4; c++) rv[g][c][r] = (kok && col0 + 32 * c < lim) ? rowp[32 * c] : 0.f;
+            }
         }
     };
     auto store = [&](int buf) {
 #pragma unroll
-        for (int c = 0; c < 4; c++) {
-            half4 hi, lo;
-            split4(make_float4(rv[c][0] * s, rv[c][1] * s, rv[c][2] * s, rv[c][3] * s), hi, lo);
-            char* row = dstb[buf] + 32 * c * ROWB;
-            *reinterpret_cast<half4*>(row) = hi;
-            *reinterpret_cast<half4*>(row + 32) = lo;
-        }
+        for (int g = 0; g < 2; g++)
+#pragma unroll
+            for (int c = 0; c < 4; c++) {
+                half4 hi, lo;
+                split4(make_float4(rv[g][c][0] * s, rv[g][c][1] * s, rv[g][c][2] * s, rv[g][c][3] * s), hi, lo);
+                char* row = dstb[buf] + 32 * c * ROWB + 64 * g;
+                *reinterpret_cast<half4*>(row) = hi;
+                *reinterpret_cast<half4*>(row + 32) = lo;
+            }
     };
     floatx16 acc[TM][TN], acc2[TM][TN];
 #pragma unroll
@@ -1525,26 +1531,30 @@ __global__ __launch_bounds__(256, 2) void k_gemm3_kmajor(const float* __restrict
     auto compute = [&](int buf) {
         const char* ac = As[buf] + (wr * TM * 32 + l32) * ROWB + 16 * h;
         const char* bc = Bs[buf] + (wc * TN * 32 + l32) * ROWB + 16 * h;
-        half8 ah[TM], al[TM], bh[TN], bl[TN];
 #pragma unroll
-        for (int i = 0; i < TM; i++) {
-            ah[i] = *reinterpret_cast<const half8*>(ac + i * 32 * ROWB);
-            al[i] = *reinterpret_cast<const half8*>(ac + i * 32 * ROWB + 32);
-        }
+        for (int sb = 0; sb < BK / 16; sb++) {
+            half8 ah[TM], al[TM], bh[TN], bl[TN];
 #pragma unroll
-        for (int j = 0; j < TN; j++) {
-            bh[j] = *reinterpret_cast<const half8*>(bc + j * 32 * ROWB);
-            bl[j] = *reinterpret_cast<const half8*>(bc + j * 32 * ROWB + 32);
-        }
-#pragma unroll
-        for (int i = 0; i < TM; i++)
+            for (int i = 0; i < TM; i++) {
+                ah[i] = *reinterpret_cast<const half8*>(ac + i * 32 * ROWB + 64 * sb);
+                al[i] = *reinterpret_cast<const half8*>(ac + i * 32 * ROWB + 64 * sb + 32);
+            }
 #pragma unroll
             for (int j = 0; j < TN; j++) {
-                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[i], bh[j], acc[i][j], 0, 0, 0);
-                acc2[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[i], bh[j], acc2[i][j], 0, 0, 0);
-                acc2[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[i], bl[j], acc2[i][j], 0, 0, 0);
+                bh[j] = *reinterpret_cast<const half8*>(bc + j * 32 * ROWB + 64 * sb);
+                bl[j] = *reinterpret_cast<const half8*>(bc + j * 32 * ROWB + 64 * sb + 32);
             }
+#pragma unroll
+            for (int i = 0; i < TM; i++)
+#pragma unroll
+                for (int j = 0; j < TN; j++) {
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[i], bh[j], acc[i][j], 0, 0, 0);
+                    acc2[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[i], bh[j], acc2[i][j], 0, 0, 0);
+                    acc2[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[i], bl[j], acc2[i][j], 0, 0, 0);
+                }
+        }
     };
+    // (loading two steps ahead into alternating register sets measured no faster)
     if (nk > 0) {
         load(0);
         store(0);

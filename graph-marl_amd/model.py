@@ -184,7 +184,7 @@ def _wgrad(gy, x, k, sa=None, sb=None):
         L.check(lib.gm_absmax_scale_rows(x.data_ptr(), Mb, k, ldx, sb.data_ptr(), L.stream_ptr()))
     tiles = ((o + 127) // 128) * ((N + 127) // 128)
     splits = max(1, min(Mb // 2048, (1024 + tiles - 1) // tiles))
-    kchunk = ((Mb + splits - 1) // splits + 15) // 16 * 16
+    kchunk = ((Mb + splits - 1) // splits + 31) // 32 * 32  # the kernel's k tile is 32 deep
     splits = (Mb + kchunk - 1) // kchunk
     part = torch.empty(splits, o, N, device=dev)
     L.check(lib.gm_gemm_x3_wgrad(gy.data_ptr(), o, x.data_ptr(), ldx, o, N, Mb, kchunk, sa.data_ptr(), sb.data_ptr(),
