@@ -267,11 +267,14 @@ def test_weight_gradient_kmajor(Mb, o, k, ldx, mag):
     assert rel < 4e-6, rel
 
 
-@pytest.mark.parametrize("rows,k,n,act", [(8192, 642, 512, 1), (5000, 256, 128, 1), (4096, 512, 4, 0)])
+@pytest.mark.parametrize("rows,k,n,act", [(8192, 642, 512, 1), (5000, 256, 128, 1), (4096, 512, 4, 0),
+                                          (100000, 512, 640, 1), (131072, 256, 512, 0)])
 def test_linear_backward_large_batch(rows, k, n, act):
     """LinearFn backward at training batch sizes — fused leaky-ReLU backward + bias partials
-    (gm_leaky_bwd), scaled split-f16 input and weight gradients — vs fp64 autograd, relative to
-    the magnitude of each gradient's terms."""
+    (gm_leaky_bwd), scaled split-f16 input and weight gradients — vs fp64, relative to the
+    magnitude of each gradient's terms. The reference takes the leaky-ReLU mask from the
+    kernel's own forward output: at 1e5 rows a few pre-activations within the forward's 5e-6
+    error of zero flip sign, which is a forward property, not a backward one."""
     gm, M, FU, W = mods()
     torch.manual_seed(rows + n)
     lin = M.Linear(k, n, act=act).cuda()
@@ -279,23 +282,16 @@ def test_linear_backward_large_batch(rows, k, n, act):
     y = lin(x)
     g = torch.randn_like(y) * 1e-5
     y.backward(g)
-    xd = x.detach().double().requires_grad_(True)
-    wd = lin.weight.detach().double().requires_grad_(True)
-    bd = lin.bias.detach().double().requires_grad_(True)
-    yd = torch.nn.functional.linear(xd, wd, bd)
-    if act == 1:
-        yd = torch.nn.functional.leaky_relu(yd, 0.01)
-    yd.backward(g.double())
-    gyd = g.double() * torch.where(yd.detach() >= 0, 1.0, 0.01 if act == 1 else 1.0)
-    mag_x = gyd.abs() @ wd.detach().abs()
-    mag_w = gyd.abs().t() @ xd.detach().abs()
-    mag_b = gyd.abs().sum(0)
-    for got, ref, mag in ((x.grad, xd.grad, mag_x), (lin.weight.grad, wd.grad, mag_w), (lin.bias.grad, bd.grad, mag_b)):
+    xd, wd = x.detach().double(), lin.weight.detach().double()
+    gyd = g.double() * torch.where(y.detach() >= 0, 1.0, 0.01 if act == 1 else 1.0)
+    refs = ((x.grad, gyd @ wd, gyd.abs() @ wd.abs()), (lin.weight.grad, gyd.t() @ xd, gyd.abs().t() @ xd.abs()),
+            (lin.bias.grad, gyd.sum(0), gyd.abs().sum(0)))
+    for got, ref, mag in refs:
         rel = ((got.double() - ref).abs() / mag.clamp_min(1e-300)).max().item()
         assert rel < 1e-5, rel
 
 
-@pytest.mark.parametrize("rows,k,n", [(8192, 642, 512), (4096, 256, 512)])
+@pytest.mark.parametrize("rows,k,n", [(8192, 642, 512), (4096, 256, 512), (100000, 642, 512), (131072, 256, 512)])
 def test_forward_amax_publishes_max(rows, k, n):
     """gm_gemm_x3's src0 amax: the forward GEMM publishes max|x| (exact float bits) and
     gm_absmax_finish turns it into the same scale gm_absmax_scale_rows computes."""
