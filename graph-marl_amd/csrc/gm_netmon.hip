@@ -436,6 +436,49 @@ extern "C" int gm_netmon_readout(const float* hf, const float* hp, const int32_t
     return launched();
 }
 
+// Same gather, one block per graph: the graph's agent nodes and their neighbour lists are
+// staged in LDS once (the per-thread version re-read them from L1/L2 for every node and column
+// chunk), then every (node, column chunk) thread sums its contributions in the same (agent,
+// segment) order as k_readout_bwd, so the results are identical.
+template <int V>
+__global__ __launch_bounds__(1024) void k_readout_bwd_g(const float* __restrict__ dout, long long stride,
+                                                        const int32_t* __restrict__ nbr,
+                                                        const int32_t* __restrict__ agent_node, int N, int R, int deg,
+                                                        int H, float* __restrict__ dhf, float* __restrict__ dhp) {
+    __shared__ int su[64];
+    __shared__ int snb[64 * MAXDEG];
+    const long long g = blockIdx.x;
+    for (int i = threadIdx.x; i < R; i += blockDim.x) su[i] = agent_node ? agent_node[g * R + i] : i;
+    __syncthreads();
+    for (int i = threadIdx.x; i < R * deg; i += blockDim.x) {
+        const int r = i / deg, k = i - r * deg;
+        snb[i] = nbr[(g * N + su[r]) * deg + k];
+    }
+    __syncthreads();
+    const int HV = H / V;
+    if ((int)threadIdx.x >= N * HV) return;
+    const int v = threadIdx.x / HV, off = (threadIdx.x % HV) * V;
+    Vec<V> af = zerov<V>(), ap = zerov<V>();
+    for (int r = 0; r < R; r++) {
+        const float* drow = dout + (g * R + r) * stride;
+        if (su[r] == v) {
+            Vec<V> x = ldv<V>(drow + off);
+#pragma unroll
+            for (int i = 0; i < V; i++) af.v[i] += x.v[i];
+        }
+        for (int k = 0; k < deg; k++) {
+            if (snb[r * deg + k] == v) {
+                Vec<V> x = ldv<V>(drow + (size_t)(k + 1) * H + off);
+#pragma unroll
+                for (int i = 0; i < V; i++) ap.v[i] += x.v[i];
+            }
+        }
+    }
+    const long long node = g * N + v;
+    if (dhf) stv<V>(dhf + node * H + off, af);
+    if (dhp) stv<V>(dhp + node * H + off, ap);
+}
+
 extern "C" int gm_netmon_readout_bwd(const float* dout, int64_t stride, const int32_t* nbr, const int32_t* agent_node,
                                      int32_t G, int32_t N, int32_t R, int32_t deg, int32_t H, float* dhf, float* dhp,
                                      void* stream) {
@@ -444,6 +487,20 @@ extern "C" int gm_netmon_readout_bwd(const float* dout, int64_t stride, const in
     int V = vec_width(H, stride, dout);
     if (dhf) { int v = vec_width(H, H, dhf); V = V < v ? V : v; }
     if (dhp) { int v = vec_width(H, H, dhp); V = V < v ? V : v; }
+    if (R <= 64 && deg <= MAXDEG && N * (H / V) <= 1024) {
+        const int threads = (N * (H / V) + 63) / 64 * 64;
+        hipStream_t st = (hipStream_t)stream;
+        if (V == 4)
+            hipLaunchKernelGGL(k_readout_bwd_g<4>, dim3(G), dim3(threads), 0, st, dout, (long long)stride, nbr,
+                               agent_node, N, R, deg, H, dhf, dhp);
+        else if (V == 2)
+            hipLaunchKernelGGL(k_readout_bwd_g<2>, dim3(G), dim3(threads), 0, st, dout, (long long)stride, nbr,
+                               agent_node, N, R, deg, H, dhf, dhp);
+        else
+            hipLaunchKernelGGL(k_readout_bwd_g<1>, dim3(G), dim3(threads), 0, st, dout, (long long)stride, nbr,
+                               agent_node, N, R, deg, H, dhf, dhp);
+        return launched();
+    }
     long long total = (long long)G * N * (H / V);
     GM_VLAUNCH(k_readout_bwd, V, dim3(nblocks(total, 256)), dout, (long long)stride, nbr, agent_node, G, N, R, deg, H,
                dhf, dhp);
