@@ -30,7 +30,7 @@ EXPORTS = [
     "gm_gemm_set_tile", "gm_simple_create", "gm_simple_destroy", "gm_simple_reset", "gm_simple_step",
     "gm_simple_observe", "gm_simple_policy_egreedy", "gm_simple_get_state", "gm_env_set_topology",
     "gm_policy_shortest_path", "gm_env_first_hops", "gm_routing_node_encoder", "gm_gemm_x3", "gm_gemm_x3_head", "gm_absmax_scale", "gm_absmax_scale_rows", "gm_gemm_x3_wgrad", "gm_absmax_finish",
-    "gm_gemm_pack_x3", "gm_gemm_pack_x3_bytes", "gm_agent_attention", "gm_agent_comm",
+    "gm_gemm_pack_x3", "gm_gemm_pack_x3_bytes", "gm_gemm_range_status", "gm_agent_attention", "gm_agent_comm",
 ]
 
 # Arithmetic form of the fused rollout GEMMs (graph-marl_amd/fused.py): "x3" = split-f16
@@ -113,6 +113,7 @@ def lib():
     L.gm_gemm_pack_x3_bytes.restype = i64
     L.gm_gemm_pack_x3.argtypes = [vp, i64, i32, i32, vp, vp, vp]
     L.gm_routing_node_encoder.argtypes = [vp, i64, vp, i32, i32, vp, vp, i32, i32, vp, i64, vp]
+    L.gm_gemm_range_status.argtypes = [C.POINTER(i32), i32]
     _lib = L
     return L
 
@@ -120,6 +121,23 @@ def lib():
 def check(rc):
     if rc != GM_OK:
         raise GMError(f"graph_marl_amd error {rc}: {lib().gm_last_error().decode()}")
+
+
+def range_status(clear=False):
+    """1 when a finished split-f16 GEMM saw an operand outside the f16 range since the last
+    clear (gm_gemm_range_status: a host-mapped word, no stream synchronisation)."""
+    v = C.c_int32(0)
+    check(lib().gm_gemm_range_status(C.byref(v), int(clear)))
+    return v.value
+
+
+def check_range():
+    """Raise GMError when a finished split-f16 GEMM went out of the f16 range: its outputs
+    (and everything computed from them) are invalid. Called at the rollout's episode ends
+    and after every update; the next gm_gemm_x3 call fails the same way."""
+    if GEMM_MODE == "x3" and range_status():
+        raise GMError("split-f16 GEMM operand outside the f16 range (|a| >= 2^15 possible): results since the "
+                      "last check are invalid; rerun with GM_GEMM=f32")
 
 
 def ptr(t):

@@ -88,6 +88,7 @@ struct Epi {
     int nq;
     float* q;
     long long ldq;
+    unsigned* range_flag;     // X3: set to 1 when an accumulator is not finite (host-mapped; nullable)
 };
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const float* p, unsigned bytes) {
@@ -115,6 +116,24 @@ __device__ __forceinline__ float sigm(float x) {
     return __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(-1.44269504088896341f * x));
 }
 __device__ __forceinline__ float tanh_fast(float x) { return 2.0f * sigm(2.0f * x) - 1.0f; }
+
+// Range guard of the split-f16 form: an A element whose pieces leave the f16 range (|a| >=
+// 65520, or a low piece (a - a_hi) * 2^12 >= 65520, possible from |a| >= 2^15) makes every
+// accumulator of its row inf or NaN, whatever the epilogue does with it afterwards (the LSTM
+// gates would squash inf to a finite h). One wave-wide vote per tile; lane 0 of a wave that saw
+// a non-finite accumulator stores 1 into the host-mapped status word (gm_gemm_range_status).
+template <int TM, int TN>
+__device__ __forceinline__ void range_guard(const floatx16 (&acc)[TM][TN], unsigned* flag, int lane) {
+    if (!flag) return;
+    bool bad = false;
+#pragma unroll
+    for (int i = 0; i < TM; i++)
+#pragma unroll
+        for (int j = 0; j < TN; j++)
+#pragma unroll
+            for (int r = 0; r < 16; r++) bad |= !__builtin_isfinite(acc[i][j][r]);
+    if (__ballot(bad) != 0ull && lane == 0) *reinterpret_cast<volatile unsigned*>(flag) = 1u;
+}
 // a = hi + 2^-12 lo with hi = f16(a) (RNE), lo = f16((a - hi) * 2^12)
 __device__ __forceinline__ void split4(float4 v, half4& hi, half4& lo) {
     const floatx4 a = {v.x, v.y, v.z, v.w};
@@ -738,6 +757,7 @@ __global__ __launch_bounds__(WGM* WGN * 64, OCC) void k_gemm3(ASrc a0, ASrc a1, 
         for (int j = 0; j < TN; j++)
 #pragma unroll
             for (int r = 0; r < 16; r++) acc[i][j][r] *= si;
+    range_guard<TM, TN>(acc, ep.range_flag, lane);
     CIn<TM, EPI> cin;
     cin_load<TM, EPI>(cin, ep, m0 + wr * TM * 32, n0 + wc * TN * 32, M, lane);
     epilogue<TM, TN, EPI>(acc, ep, m0 + wr * TM * 32, n0 + wc * TN * 32, M, N, lane, cin);
@@ -1019,6 +1039,7 @@ __global__ __launch_bounds__(WGM* WGN * 64, OCC) void k_gemm3g(ASrc a0, ASrc a1,
         for (int j = 0; j < TN; j++)
 #pragma unroll
             for (int r = 0; r < 16; r++) acc[i][j][r] *= si;
+    range_guard<TM, TN>(acc, ep.range_flag, lane);
     if constexpr (EPI == EPI_HEAD)
         head_epilogue<TM, TN, WGN, BM>(acc, ep, lds, m0, wr, wc, M, N, lane, tid);
     else
@@ -1232,6 +1253,33 @@ int dispatch(const ASrc& s0, const ASrc& s1, const float* w, long long ldw, unsi
 #undef GM_L4
 }
 
+// Status word of the split-f16 range guard: host memory mapped into the device address space
+// (fine-grained, coherent), so the host reads what a finished kernel stored without a copy or a
+// stream synchronisation. Allocated on the first x3 call.
+unsigned* g_range_host = nullptr;
+unsigned* g_range_dev = nullptr;
+
+int range_flag(unsigned** dev) {
+    if (!g_range_host) {
+        void* p = nullptr;
+        if (hipHostMalloc(&p, 64, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess)
+            return gm_fail(GM_ERR_HIP, "gm_gemm_x3: hipHostMalloc of the range status word failed");
+        memset(p, 0, 64);
+        void* d = nullptr;
+        if (hipHostGetDevicePointer(&d, p, 0) != hipSuccess)
+            return gm_fail(GM_ERR_HIP, "gm_gemm_x3: hipHostGetDevicePointer of the range status word failed");
+        g_range_host = static_cast<unsigned*>(p);
+        g_range_dev = static_cast<unsigned*>(d);
+    }
+    if (*reinterpret_cast<volatile unsigned*>(g_range_host))
+        return gm_fail(GM_ERR_RANGE,
+                       "gm_gemm_x3: an earlier split-f16 GEMM produced a non-finite accumulator (an A operand "
+                       "outside the f16 range, |a| >= 2^15 possible); its outputs are invalid: rerun with the exact "
+                       "form (GM_GEMM=f32) or clear with gm_gemm_range_status(.., 1)");
+    *dev = g_range_dev;
+    return GM_OK;
+}
+
 // shared argument checks of gm_gemm_f32 / gm_gemm_x3; x3: w = packed weights
 int gemm_entry(bool x3, const gm_a_src* a0, const gm_a_src* a1, const void* w, int64_t ldw, const float* wsi,
                const float* b, int32_t m, int32_t n, int32_t epilogue, float* y, int64_t ldy, float* y2,
@@ -1271,6 +1319,7 @@ int gemm_entry(bool x3, const gm_a_src* a0, const gm_a_src* a1, const void* w, i
     ep.c_in = c_in;
     ep.ldc = ldc;
     ep.act_out = act_out;
+    if (x3 && (rc = range_flag(&ep.range_flag))) return rc;
     if (epilogue == GM_EPI_LSTM) {
         if (n % 128 || !y2 || !c_in) return gm_fail(GM_ERR_INVALID_ARG, std::string(fn) + ": LSTM epilogue needs 4H % 128 == 0");
     } else if (epilogue != GM_EPI_BIAS && epilogue != GM_EPI_BIAS_LEAKY) {
@@ -1347,6 +1396,13 @@ extern "C" int gm_gemm_x3(const gm_a_src* a0, const gm_a_src* a1, const void* wp
                       stream);
 }
 
+extern "C" int gm_gemm_range_status(int32_t* status, int32_t clear) {
+    if (!status) return gm_fail(GM_ERR_INVALID_ARG, "gm_gemm_range_status: null status");
+    *status = g_range_host ? (int32_t)*reinterpret_cast<volatile unsigned*>(g_range_host) : 0;
+    if (clear && g_range_host) *reinterpret_cast<volatile unsigned*>(g_range_host) = 0u;
+    return GM_OK;
+}
+
 extern "C" int gm_gemm_x3_head(const gm_a_src* a0, const void* wp, const float* wscale_inv, const float* b,
                                int32_t m, int32_t n, int32_t act, const float* wq, int64_t ldwq, const float* bq,
                                int32_t nq, float* q, int64_t ldq, float* y, int64_t ldy, void* stream) {
@@ -1374,6 +1430,7 @@ extern "C" int gm_gemm_x3_head(const gm_a_src* a0, const void* wp, const float* 
     ep.nq = nq;
     ep.q = q;
     ep.ldq = ldq;
+    if ((rc = range_flag(&ep.range_flag))) return rc;
     return launch_g<4, 2, 1, 4, 2, GM_A_DENSE, EPI_HEAD, 1>(s0, s1, static_cast<const float*>(wp), ldw, (unsigned)wb, m,
                                                           n, K, ep, (hipStream_t)stream, wscale_inv);
 }

@@ -368,6 +368,8 @@ def main(argv=None):
     try:
         for step in range(1, int(args.total_steps) + 1):
             if episode_step is None or episode_done:
+                if episode_step is not None:
+                    L.check_range()  # split-f16 range guard (graph_marl_amd.h gm_gemm_range_status)
                 episode_step = 0
                 env.reset()
                 current_episode += 1

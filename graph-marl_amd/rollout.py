@@ -18,6 +18,7 @@ eager between replays.
 """
 import torch
 
+from . import _lib as L
 from . import fused as FU  # noqa: F401  (packed-weight caches shared by the groups)
 from .policy import EpsilonGreedy
 from .routing import Routing
@@ -107,6 +108,8 @@ class StreamedRollout:
         staggered)."""
         self._enqueue_step()
         self.ep += 1
+        if self.ep >= self.episode_steps:
+            L.check_range()  # split-f16 range guard of the finished launches (no sync)
         for g in range(self.groups):
             if (self.ep + self._offs[g]) % self.episode_steps == 0:
                 with self._on(g):
@@ -151,6 +154,7 @@ class StreamedRollout:
             self._graph.replay()
             self.ep += self._gsteps
             if self.ep >= self.episode_steps:
+                L.check_range()
                 cur = torch.cuda.current_stream()  # the replay's stream
                 for g in range(self.groups):
                     self.streams[g].wait_stream(cur)

@@ -16,6 +16,8 @@ import torch
 import torch.distributed as dist
 import torch.nn.functional as F
 
+from . import _lib as GL
+
 
 def allreduce_gradients(params, group=None):
     """Average .grad over the process group with one bucketed all-reduce."""
@@ -171,4 +173,5 @@ def dqn_update(netmon, model, model_tar, optimizer, params, batches, gamma, tau,
         interpolate_model(model, model_tar, tau, model_tar)
     elif iteration % target_update_steps == 0:
         model_tar.load_state_dict(model.state_dict())
+    GL.check_range()  # split-f16 range guard of the launches that have finished (no sync)
     return loss.detach(), qs, qts

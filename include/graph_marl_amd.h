@@ -43,7 +43,8 @@ typedef enum {
     GM_ERR_OOM = -2,
     GM_ERR_HIP = -3,
     GM_ERR_TOPOLOGY = -4, /* a provided topology seed is invalid / generator retry limit hit */
-    GM_ERR_UNSUPPORTED = -5
+    GM_ERR_UNSUPPORTED = -5,
+    GM_ERR_RANGE = -6 /* a split-f16 GEMM saw an operand outside the f16 range (gm_gemm_range_status) */
 } gm_status;
 
 /* topology modes: Network seed handling, src/env/network.py:215-272, 356-371 */
@@ -248,10 +249,18 @@ int gm_gemm_f32(const gm_a_src* src0, const gm_a_src* src1, const float* w, int6
  * form; error vs fp64 the order of an fp32 GEMM's (tests/test_fused_gpu.py). A stays fp32
  * in HBM (split while staged to LDS); wp = weights packed by gm_gemm_pack_x3 for the same
  * (n, K = src0->k + src1->k), wscale_inv its device scalar. Arguments otherwise as
- * gm_gemm_f32. |A| must stay below the f16 range (65504). */
+ * gm_gemm_f32. Range: an A element whose split leaves the f16 range (|a| >= 65520, or a low
+ * piece (a - a_hi) * 2^12 >= 65520, possible from |a| >= 2^15) turns its row's accumulators
+ * inf/NaN; the kernel then sets a host-mapped status word, and every later gm_gemm_x3 /
+ * gm_gemm_x3_head call fails with GM_ERR_RANGE until gm_gemm_range_status clears it. */
 int gm_gemm_x3(const gm_a_src* src0, const gm_a_src* src1, const void* wp, const float* wscale_inv, const float* b,
                int32_t m, int32_t n, int32_t epilogue, float* y, int64_t ldy, float* y2, int64_t ldy2,
                const float* c_in, int64_t ldc, float* act_out, void* stream);
+/* Status of the split-f16 range guard (no stream synchronisation: the word is host memory the
+ * kernels write): *status = 1 when a gm_gemm_x3 / gm_gemm_x3_head launch that has finished
+ * produced a non-finite accumulator since the last clear; clear != 0 resets it. Callers check
+ * it at their synchronisation points (episode ends, after an update). */
+int gm_gemm_range_status(int32_t* status, int32_t clear);
 /* Last DQN encoder layer + Q head in one kernel (split-f16 form for the layer, fp32 head):
  * q[m][nq] = Wq · act(src0 · W^T + b) + bq, act 0 none / 1 leaky_relu(0.01); the hidden
  * activation stays in registers (also written to y when y != NULL). src0 DENSE, n <= 256,

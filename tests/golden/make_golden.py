@@ -751,15 +751,17 @@ def gen_cli_flags(out, ref):
 # ---------------------------------------------------------------------------
 # Supervised shortest-path task (src/sl.py): samples and one NetMonSL update
 # ---------------------------------------------------------------------------
-def gen_sl(out, Network, Routing, EVAL_SEEDS, NetMon):
+def gen_sl(out, Network, Routing, EVAL_SEEDS, NetMon, n=20, seeds=None, H=32, enc=(64, 48)):
+    """n = 20: small NetMon (H 32, encoder 64,48) on 8 EVAL_SEEDS graphs; n = 100 (BASELINE
+    config 5): the CLI-default NetMon (H 128, encoder 512,256) on 4 valid 100-node seeds."""
     import torch
     import torch.nn as nn
     import torch.nn.functional as F
 
     d = {}
     # get_sl_sample (src/sl.py:174-218) on graphs from fixed seeds
-    seeds = list(EVAL_SEEDS[100:108])
-    net = Network(20, random_topology=True, sequential_topology_seeds=True, provided_seeds=seeds)
+    seeds = list(EVAL_SEEDS[100:108]) if seeds is None else [int(x) for x in seeds]
+    net = Network(n, random_topology=True, sequential_topology_seeds=True, provided_seeds=seeds)
     env = Routing(net, 20, 1)
     np.random.seed(5)
     env.reset()
@@ -791,9 +793,9 @@ def gen_sl(out, Network, Routing, EVAL_SEEDS, NetMon):
     # NetMonSL (src/sl.py:132-168) = reference NetMon + 3 nn.Linear heads; one train
     # iteration (src/sl.py:360-424) with seq_len 2, regression-all loss
     torch.manual_seed(3)
-    netmon = NetMon(88, 32, [64, 48], 1, activation_fn=F.leaky_relu, rnn_type="lstm", rnn_carryover=True,
+    netmon = NetMon(4 * n + 8, H, list(enc), 1, activation_fn=F.leaky_relu, rnn_type="lstm", rnn_carryover=True,
                     agg_type="sum", output_neighbor_hidden=True, output_global_hidden=False)
-    heads = [nn.Linear(netmon.get_out_features(), k) for k in (4, 1, 20)]
+    heads = [nn.Linear(netmon.get_out_features(), k) for k in (4, 1, n)]
     params = list(netmon.parameters()) + [p for h in heads for p in h.parameters()]
     names = [f"netmon.{k}" for k, _ in netmon.named_parameters()] + \
         [f"{hn}.{k}" for hn, h in zip(("linear", "linear_reg", "linear_reg_all"), heads) for k, _ in h.named_parameters()]
@@ -801,7 +803,7 @@ def gen_sl(out, Network, Routing, EVAL_SEEDS, NetMon):
         d["w_" + nme] = p.detach().numpy().copy()
     x = torch.tensor(d["node_obs"])
     a = torch.tensor(d["node_adj"])
-    eye = torch.eye(20).repeat(x.shape[0], 1, 1)
+    eye = torch.eye(n).repeat(x.shape[0], 1, 1)
     tgt = torch.tensor(d["targets_all"])
     netmon.state = None
     seq = []
@@ -816,6 +818,7 @@ def gen_sl(out, Network, Routing, EVAL_SEEDS, NetMon):
     for nme, p in zip(names, params):
         d["g_" + nme] = (p.grad.numpy().copy() if p.grad is not None else np.zeros(p.shape, np.float32))
     d["param_names"] = np.array(names)
+    d["config"] = np.array([n, H, enc[0], enc[1]], np.int64)
     np.savez_compressed(out, **d)
     print("sl:", out)
 
@@ -867,6 +870,10 @@ def main():
         gen_cli_flags(os.path.join(HERE, "cli_flags.json"), args.ref)
     if only is None or "sl" in only:
         gen_sl(os.path.join(HERE, "sl.npz"), Network, Routing, EVAL_SEEDS, NetMon)
+    if only is None or "sl100" in only:
+        seeds100 = np.load(os.path.join(HERE, "topology.npz"))["rand_n100_seed"][:4]
+        gen_sl(os.path.join(HERE, "sl_n100.npz"), Network, Routing, EVAL_SEEDS, NetMon, n=100, seeds=seeds100,
+               H=128, enc=(512, 256))
     if only is None or "simple" in only:
         gen_simple(os.path.join(HERE, "simple.npz"), SimpleEnvironment)
 

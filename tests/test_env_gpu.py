@@ -116,6 +116,11 @@ BATCH_CASES = [
     (64, 64, "random", True, False, 0, 8, 60, 30),
     (50, 20, "random", True, True, 12, 16, 90, 45),
     (4, 1, "random", True, False, 0, 16, 40, 20),
+    # config-4 node counts around the 32-node LDS image of the reset (k_env_reset<32>)
+    (30, 20, "random", True, False, 0, 24, 110, 50),
+    (32, 20, "random", True, False, 0, 16, 80, 40),
+    (34, 20, "random", True, False, 0, 8, 60, 30),
+    (40, 20, "random", True, False, 0, 16, 110, 50),
     (100, 20, "random", True, False, 0, 8, 60, 30),
     (128, 64, "random", True, True, 16, 4, 40, 20),
     # observation variants: (env_var, k) as an optional 10th element
@@ -261,11 +266,12 @@ def test_large_batch_invariants(gm, oracle_mod):
                 np.testing.assert_array_equal(obs[b], o.observe()["obs"])
 
 
-@pytest.mark.parametrize("n", [10, 20, 50, 100])
+@pytest.mark.parametrize("n", [10, 20, 30, 40, 50, 100])
 def test_topology_from_seed_matches_reference_golden(gm, n):
     """Topologies generated on the device from the reference's recorded (valid) seeds:
-    edges in creation order, lengths and APSP equal the reference's networkx output
-    (tests/golden/topology.npz, rand_n*), up to N = 100 (BASELINE config 5)."""
+    edges in creation order, lengths, APSP and the I+A adjacency (get_nodes_adjacency,
+    src/env/network.py:385-389) equal the reference's networkx output
+    (tests/golden/topology.npz, rand_n*), N = 10..50 (BASELINE config 4) and 100 (config 5)."""
     g = np.load(f"{R.GOLDEN}/topology.npz")
     seeds = g[f"rand_n{n}_seed"]
     B = len(seeds)
@@ -281,3 +287,5 @@ def test_topology_from_seed_matches_reference_golden(gm, n):
         np.testing.assert_array_equal(st["edge_len"][b, :E], ge[:, 2])
         np.testing.assert_array_equal(st["apsp"][b], g[f"rand_n{n}_apsp"][b])
         assert st["topo_seed"][b] == seeds[b]
+    adj = env.get_nodes_adjacency().cpu().numpy()
+    np.testing.assert_array_equal(adj, g[f"rand_n{n}_adj"].astype(np.int8))

@@ -379,3 +379,56 @@ def test_lstm_cell_backward_large_batch(rows):
         scale = want.abs().max().item()
         err = (got.double() - want).abs().max().item()
         assert err <= 1e-5 * scale + 1e-12, (err, scale)
+
+
+@pytest.mark.parametrize("m,n,k,epi", [(4096, 128, 128, 0), (32768, 256, 256, 1), (4096, 512, 256, 2)])
+def test_gemm_x3_range_guard(m, n, k, epi):
+    """Split-f16 operands in [2^15, 65504): values whose low piece stays in the f16 range give
+    fp32-order results and leave the guard clear; one value whose low piece overflows
+    (32784 = f16 32768 + 16: 16 * 2^12 = 65536 -> inf) sets the host-mapped status word, the
+    next x3 call raises GMError, and clearing the word re-enables the form. Covers the
+    register-staged kernel (n = 128), the LDS-DMA kernel (n >= 256, K >= 256, m >= 32768) and
+    the LSTM epilogue (which would squash the inf to a finite h)."""
+    gm, M, FU, W = mods()
+    L = gm._lib
+    L.range_status(clear=True)
+    torch.manual_seed(11)
+    x = torch.empty(m, k, device="cuda").uniform_(32768.0, 60000.0) * torch.where(
+        torch.rand(m, k, device="cuda") < 0.5, -1.0, 1.0)
+    r = (x - x.half().float()).abs()
+    x = torch.where(r < 15.9, x, x.half().float())  # keep every low piece inside the f16 range
+    w = torch.randn(n, k, device="cuda") * 0.05
+    b = torch.zeros(n, device="cuda")
+    wp, ldw = FU._pad_cols(w)
+    xp = FU.X3(wp, ldw, n, k)
+    y = torch.empty(m, n if epi != 2 else n // 4, device="cuda")
+
+    def run(xx):
+        if epi == 2:  # LSTM epilogue on [x | h] halves of K
+            c_in = torch.zeros(m, n // 4, device="cuda")
+            y2 = torch.empty(m, n // 4, device="cuda")
+            FU.gemm(FU.dense(xx.data_ptr(), k, k // 2), FU.dense(xx[:, k // 2:].data_ptr(), k, k // 2), wp.data_ptr(),
+                    ldw, b.data_ptr(), m, n, FU.GM_EPI_LSTM, y.data_ptr(), n // 4, y2.data_ptr(), n // 4,
+                    c_in.data_ptr(), n // 4, x3=xp)
+        else:
+            FU.gemm(FU.dense(xx.data_ptr(), k, k), None, wp.data_ptr(), ldw, b.data_ptr(), m, n, epi, y.data_ptr(), n,
+                    x3=xp)
+        torch.cuda.synchronize()
+
+    run(x)
+    assert L.range_status() == 0
+    if epi == 0:
+        ref = F.linear(x.double(), w.double())
+        mag = F.linear(x.abs().double(), w.abs().double())
+        assert ((y.double() - ref).abs() / mag).max().item() < 4e-6
+    bad = x.clone()
+    bad[m // 3, 5] = 32784.0
+    run(bad)
+    assert L.range_status() == 1
+    with pytest.raises(gm._lib.GMError):
+        L.check_range()
+    with pytest.raises(gm._lib.GMError):
+        run(x)  # every later x3 call fails until the word is cleared
+    assert L.range_status(clear=True) == 1
+    run(x)
+    assert L.range_status() == 0

@@ -1,0 +1,127 @@
+"""Full-size, long-horizon parity of the benched rollout (bench.py's default workload).
+
+StreamedRollout exactly as bench.py runs it: 4096 envs in 2 stream groups, N = 20 random
+topologies (EVAL_SEEDS excluded), A = 20 packets, NetMon K = 1 (lstm, sum) + DQN 512,256,
+ε = 0.5, 50-step episodes, 120 vector steps (two topology resets + NetMon start-ups inside).
+Eight envs spread over both groups are shadowed every step by
+  * the C oracle env (oracle/gm_oracle.c) fed the GPU's Q-values, which must take the same
+    ε-greedy actions and give bit-identical rewards, done flags, agent and node observations
+    and I+A adjacency (reference src/env/routing.py:160-539, src/policy.py:20-64);
+  * the NumPy fp64 restatement of NetMon (oracle/netmon_ref.py, reference src/model.py:451-631)
+    carried over the whole horizon from its own fp64 state (reset to the start-up step at each
+    episode), against which the GPU NetMon state, the readout part of the joint observation and
+    the Q-values must stay within 1e-5 (BASELINE.json north_star tolerance) at every step.
+Run once per GEMM form: the split-f16 form the headline is measured with, and GM_GEMM=f32.
+"""
+import importlib
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+N, A, B, G, EP, STEPS, EPS = 20, 20, 4096, 2, 50, 120, 0.5
+SAMPLE = [0, 1, 777, 2047, 2048, 2049, 3333, 4095]
+TOL = 1e-5
+
+
+def adjacency(topo):
+    m = np.eye(N, dtype=np.int8)
+    for i, row in enumerate(topo["nbr"]):
+        for j in row:
+            if j >= 0:
+                m[i, j] = 1
+    return m
+
+
+@pytest.mark.parametrize("form", ["x3", "f32"])
+def test_benched_rollout_long_horizon(form, monkeypatch, oracle_mod):
+    import netmon_ref
+
+    gm = importlib.import_module("graph-marl_amd")
+    M = importlib.import_module("graph-marl_amd.model")
+    RO = importlib.import_module("graph-marl_amd.rollout")
+    monkeypatch.setattr(gm._lib, "GEMM_MODE", form)
+    gm._lib.range_status(clear=True)
+    net = gm.Network(N, random_topology=True, excluded_seeds=gm.EVAL_SEEDS, device=0)
+    torch.manual_seed(0)
+    netmon = M.NetMon(4 * N + 8, 128, [512, 256], 1).cuda()
+    dqn = M.DQN(6 * N + 10 + netmon.get_out_features(), [512, 256], 4).cuda()
+    ro = RO.StreamedRollout(net, A, B, netmon, dqn, groups=G, seed=0, epsilon=EPS, episode_steps=EP, device=0)
+    per = B // G
+    Wn = {k: v.detach().double().cpu().numpy() for k, v in netmon.state_dict().items()}
+    Wd = {k: v.detach().double().cpu().numpy() for k, v in dqn.state_dict().items()}
+    od = 6 * N + 10
+
+    qrec = {}
+    for g, pol in enumerate(ro.policies):
+        orig = pol.select
+
+        def select(q, g=g, orig=orig):
+            qrec[g] = q
+            return orig(q)
+
+        pol.select = select
+
+    cfg = oracle_mod.make_config(N, A, topo_mode=oracle_mod.TOPO_RANDOM, excluded=gm.EVAL_SEEDS)
+    orc = {e: oracle_mod.OracleEnv(cfg, e) for e in SAMPLE}
+    loc = {e: (e // per, e % per) for e in SAMPLE}
+
+    def gpu_view():
+        torch.cuda.synchronize()
+        out = {}
+        for e, (g, i) in loc.items():
+            env, wenv = ro.envs[g], ro.wenvs[g]
+            out[e] = dict(obs=env.obs_buf[i, :, :od].cpu().numpy(), node_obs=env.node_obs[i].cpu().numpy(),
+                          state=wenv.current_netmon_state[i].cpu().numpy(),
+                          readout=wenv.obs[i, :, od:].cpu().numpy(), reward=env.reward[i].cpu().numpy(),
+                          done=env.done[i].cpu().numpy().astype(bool),
+                          adj=env.get_nodes_adjacency()[i].cpu().numpy())
+        return out
+
+    state64, worst = {}, {"state": 0.0, "readout": 0.0, "q": 0.0}
+
+    def netmon_check(e, o, v, t):
+        ob = o.observe()
+        assert (v["obs"] == ob["obs"]).all(), f"step {t} env {e}: agent obs"
+        assert (v["node_obs"] == ob["node_obs"]).all(), f"step {t} env {e}: node obs"
+        adj = adjacency(o.topology())
+        assert (v["adj"] == adj).all(), f"step {t} env {e}: I+A adjacency"
+        out, st = netmon_ref.netmon_forward(Wn, ob["node_obs"][None], adj[None], state64.get(e), "lstm", "sum", 1)
+        state64[e] = st
+        ro_ = netmon_ref.to_network_obs(out, ob["node_agent"][None])[0]
+        es = np.abs(v["state"] - st[0]).max()
+        er = np.abs(v["readout"] - ro_).max()
+        worst["state"], worst["readout"] = max(worst["state"], es), max(worst["readout"], er)
+        assert es < TOL and er < TOL, f"step {t} env {e}: NetMon state err {es}, readout err {er}"
+        return np.concatenate([ob["obs"].astype(np.float64), ro_], -1)
+
+    ro.reset()
+    for o in orc.values():
+        o.reset()
+    joint = {e: netmon_check(e, orc[e], v, 0) for e, v in gpu_view().items()}
+    resets = 0
+    for t in range(1, STEPS + 1):
+        ro.step()
+        v = gpu_view()
+        acts = {g: ro.policies[g].actions.cpu().numpy() for g in range(G)}
+        for e, o in orc.items():
+            g, i = loc[e]
+            q = qrec[g][i].cpu().numpy()
+            q64 = netmon_ref.dqn_forward(Wd, joint[e])
+            eq = np.abs(q - q64).max()
+            worst["q"] = max(worst["q"], eq)
+            assert eq < TOL, f"step {t} env {e}: Q err {eq}"
+            exp = o.draw_egreedy(q, EPS)
+            assert (exp == acts[g][i]).all(), f"step {t} env {e}: ε-greedy actions"
+            rew, done, _ = o.step(acts[g][i])
+            assert (rew == v[e]["reward"]).all() and (done == v[e]["done"]).all(), f"step {t} env {e}: reward/done"
+            if t % EP == 0:  # the rollout reset the episode after this step: new topology, NetMon start-up
+                o.reset()
+                state64.pop(e)
+            joint[e] = netmon_check(e, o, v[e], t)
+        resets += t % EP == 0
+    assert resets == STEPS // EP >= 2
+    gm._lib.check_range()
+    print(f"form {form}: worst |err| over {STEPS} steps x {len(SAMPLE)} envs: {worst}")

@@ -9,29 +9,40 @@ import pytest
 import torch
 
 pytestmark = pytest.mark.gpu
-GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "sl.npz")
+HERE = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+# sl.npz: N = 20, small NetMon (H 32); sl_n100.npz: BASELINE config 5's N = 100 graphs with the
+# CLI-default NetMon (H 128, encoder 512,256)
+GOLDENS = ["sl.npz", "sl_n100.npz"]
 
 
-def test_sl_samples_match_reference():
+def _golden(name):
+    g = np.load(os.path.join(HERE, name))
+    n, H, e0, e1 = (int(v) for v in g["config"]) if "config" in g.files else (20, 32, 64, 48)
+    return g, n, H, f"{e0},{e1}"
+
+
+@pytest.mark.parametrize("name", GOLDENS)
+def test_sl_samples_match_reference(name):
     SL = importlib.import_module("graph-marl_amd.sl")
     M = importlib.import_module("graph-marl_amd.model")
-    g = np.load(GOLDEN)
+    g, n, _, _ = _golden(name)
     seeds = [int(s) for s in g["seeds"]]
-    data = SL.build_dataset(20, 20, len(seeds), 0, seeds=seeds)
+    data = SL.build_dataset(n, 20, len(seeds), 0, seeds=seeds)
     np.testing.assert_array_equal(data.targets_all.cpu().numpy(), g["targets_all"])
     np.testing.assert_array_equal(data.labels.cpu().numpy(), g["labels"])
     nbr_ref = M.dense_to_nbr(torch.as_tensor(g["node_adj"], device="cuda"))
     np.testing.assert_array_equal(data.nbr.cpu().numpy(), nbr_ref.cpu().numpy())
 
 
-def test_sl_iteration_matches_reference():
+@pytest.mark.parametrize("name", GOLDENS)
+def test_sl_iteration_matches_reference(name):
     SL = importlib.import_module("graph-marl_amd.sl")
     M = importlib.import_module("graph-marl_amd.model")
-    g = np.load(GOLDEN)
-    args = argparse.Namespace(netmon_dim=32, netmon_encoder_dim="64,48", netmon_iterations=1, netmon_rnn_type="lstm",
+    g, n, H, enc = _golden(name)
+    args = argparse.Namespace(netmon_dim=H, netmon_encoder_dim=enc, netmon_iterations=1, netmon_rnn_type="lstm",
                               netmon_rnn_carryover=1, netmon_agg_type="sum", netmon_last_neighbors=1,
-                              netmon_global=False, num_targets=20)
-    model = SL.NetMonSL(args, 88, 4, 20).cuda()
+                              netmon_global=False, num_targets=n)
+    model = SL.NetMonSL(args, 4 * n + 8, 4, n).cuda()
     names = [str(n) for n in g["param_names"]]
     sd = {n: torch.as_tensor(g["w_" + n]) for n in names}
     model.load_state_dict(sd)
