@@ -62,8 +62,8 @@ def parse():
     p.add_argument("--train-batch", type=int, default=0,
                    help="sequences per update (0: 32 * n_env / 10 = the reference replay ratio, SURVEY 8d)")
     p.add_argument("--train-seq", type=int, default=8, help="sequence length of an update")
-    p.add_argument("--cpu-envs", type=int, default=256)
-    p.add_argument("--cpu-steps", type=int, default=20)
+    p.add_argument("--cpu-envs", type=int, default=1024)
+    p.add_argument("--cpu-steps", type=int, default=50, help="one full episode (includes its reset)")
     return p.parse_args()
 
 
@@ -81,6 +81,17 @@ def pmc_traffic(tag):
         if k:
             return k["fetch_bytes"] + k["write_bytes"], os.path.relpath(path, ROOT)
     return None, None
+
+
+def cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return None
 
 
 def kernel_cost(tag, n_env, N, A, E, x3=False):
@@ -112,19 +123,25 @@ def kernel_cost(tag, n_env, N, A, E, x3=False):
     return None, None
 
 
-def measure_train(args, gm, M, W, P, env, wenv, netmon, dqn, policy, dev, world):
+def measure_train(args, gm, M, W, P, net, netmon, dqn, dev, world, rank):
     """Rollout + DQN/NetMon training at the reference's replay ratio: every
-    vector step stores its n_env transitions in the device replay and runs one update of
-    B sequences x L steps (B = 32 n_env / 10: the paper's B=32, L=8 update every 10
-    env-steps, per env), with the gradient all-reduce across ranks (src/main.py:667-1026;
-    graph-marl_amd/train.py). Value = env-steps/s of the whole loop (all ranks)."""
+    vector step of ALL n_env envs of the GPU (one env batch, one stream) stores its n_env
+    transitions in the device replay and runs one update of B sequences x L steps
+    (B = 32 n_env / 10: the paper's B=32, L=8 update every 10 env-steps, per env), with the
+    gradient all-reduce across ranks (src/main.py:667-1026; graph-marl_amd/train.py).
+    Value = env-steps/s of the whole loop (all ranks)."""
     import copy
 
     import importlib as il
 
     T = il.import_module("graph-marl_amd.train")
     RB = il.import_module("graph-marl_amd.replaybuffer")
-    B = env.n_env
+    B = args.n_env
+    env = gm.Routing(net, args.n_data, n_env=B, seed=rank * B, obs_extra=netmon.get_out_features(),
+                     agent_adjacency=False, device=dev.index)
+    wenv = W.NetMonWrapper(env, netmon, 1)
+    policy = P.EpsilonGreedy(wenv, dqn, epsilon=args.epsilon, epsilon_decay=1.0, epsilon_update_freq=100,
+                             step_before_train=0)
     bsz = args.train_batch or max(1, (32 * B + 9) // 10)
     L_ = args.train_seq
     model_tar = copy.deepcopy(dqn)
@@ -175,7 +192,7 @@ def measure_train(args, gm, M, W, P, env, wenv, netmon, dqn, policy, dev, world)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     el = float(t.item())
-    return {"value": round(B * world * args.train_steps / el, 1), "unit": "env-steps/s",
+    return {"value": round(B * world * args.train_steps / el, 1), "unit": "env-steps/s", "n_env_per_gpu": B,
             "ms_per_step": round(1e3 * el / args.train_steps, 3), "steps": args.train_steps,
             "update": {"sequences": bsz, "seq_len": L_, "graph_steps": bsz * L_,
                        "per": "vector step of n_env envs (replay ratio 25.6 = reference B=32, L=8 every 10 steps)"}}
@@ -221,11 +238,15 @@ def main():
     if args.unfused:
         for w in ro.wenvs:
             w.fused = False
-    env, wenv, policy = ro.envs[0], ro.wenvs[0], ro.policies[0]
 
     state = {}
 
     def timed_region(warmup, steps, timers, ro=ro, graph=0):
+        """W warmup steps, then untimed steps up to the episode phase where the FIRST timed step
+        (graph: replay) ends an episode, so the K timed steps always contain ceil(K / episode)
+        topology resets + NetMon start-ups (at the reference's rate or above, whatever K is)."""
+        EP = args.episode_steps
+        g = graph or 1
         with torch.no_grad():
             ro.reset()
             for _ in range(warmup + (warmup % 2 if graph else 0)):
@@ -236,6 +257,8 @@ def main():
                 assert steps % graph == 0, "--steps must be a multiple of --graph"
                 ro.capture(graph)
                 ro.run(graph)
+            while ro.ep != EP - g:  # position: the first timed step (replay) triggers a reset
+                ro.run(g) if graph else ro.step()
             torch.cuda.synchronize()
             if world > 1:
                 dist.barrier()
@@ -255,6 +278,7 @@ def main():
             elapsed = time.perf_counter() - t0
             prof, L.PROF = L.PROF, None
             state["host_ms_per_step"] = 1e3 * t_issue / steps
+            state["resets"] = -(-steps // EP)
         el = torch.tensor([elapsed], dtype=torch.float64, device="cpu" if share else dev)
         if world > 1:
             dist.all_reduce(el, op=dist.ReduceOp.MAX)
@@ -266,6 +290,7 @@ def main():
     timers = not args.no_kernel_timers
     elapsed, prof = timed_region(args.warmup, args.steps, timers and G == 1 and not args.graph, graph=args.graph)
     host_ms = state["host_ms_per_step"]
+    resets = state["resets"]
     if timers and (G > 1 or args.graph):
         # per-kernel durations from the same rollout as ONE group (kernels not overlapped), for
         # the roofline fields and the rocprofv3 cross-check (tools/gpu_check.sh prof: --groups 1)
@@ -289,6 +314,7 @@ def main():
             ts = [s.elapsed_time(e) for s, e in evs]
             kernels[tag] = {"launches": len(ts), "avg_us": 1e3 * sum(ts) / len(ts), "total_ms": sum(ts)}
     roof = None
+    roof_hbm = {}
     if kernels:
         dom = max(kernels, key=lambda k: kernels[k]["total_ms"])
         bound, units = kernel_cost(dom, B, N, A, E, x3)
@@ -311,11 +337,23 @@ def main():
                 s = kv["avg_us"] * 1e-6
                 kv["achieved"] = round(units / s / (1e9 if bound == "hbm" else 1e12), 2)
                 kv["unit"] = {"hbm": "GB/s", "mfma": "TFLOP/s f32", "mfma16": "TFLOP/s f16"}[bound]
+        # the two HBM-bound kernels the north star names: env step (+ obs emission) and the
+        # message-passing aggregate; algorithmic bytes per launch / HIP-event time
+        for tag, kv in kernels.items():
+            if tag.split(":")[0] not in ("env_step", "mp_aggregate"):
+                continue
+            bound, units = kernel_cost(tag, B, N, A, E, x3)
+            ach = units / (kv["avg_us"] * 1e-6) / 1e9
+            tb, src = pmc_traffic(tag)
+            roof_hbm[tag] = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                             "frac": round(ach / HBM_PEAK_GBS, 4), "algorithmic_bytes": units, "traffic": tb,
+                             "traffic_note": None if tb is None else f"HBM bytes per launch (rocprofv3 PMC, {src})",
+                             "avg_us": round(kv["avg_us"], 2)}
 
     train = None
     if not args.no_train and netmon is not None:
         try:
-            train = measure_train(args, gm, M, W, P, env, wenv, netmon, dqn, policy, dev, world)
+            train = measure_train(args, gm, M, W, P, net, netmon, dqn, dev, world, rank)
         except Exception as ex:  # the training figure must never break the rollout line
             train = {"value": None, "error": repr(ex)[:300]}
 
@@ -325,10 +363,13 @@ def main():
             sys.path.insert(0, os.path.join(ROOT, "oracle"))
             import cpu_baseline
 
-            threads = int(os.environ.get("OMP_NUM_THREADS", str(min(16, os.cpu_count() or 1))))
+            # the GPU box's CPU share of one GPU (its harness exports OMP_NUM_THREADS=16; nproc shows the
+            # whole machine); in a plain environment every core
+            threads = int(os.environ.get("OMP_NUM_THREADS") or (os.cpu_count() or 1))
             v, dt = cpu_baseline.measure(args.cpu_envs, args.cpu_steps, threads, K=K,
                                          episode_steps=args.episode_steps)
             cpu = {"value": round(v, 1), "unit": "env-steps/s", "cores": threads, "kind": "port",
+                   "cpu_model": cpu_model(), "host_cpus": os.cpu_count(),
                    "sample": f"{args.cpu_envs} envs x {args.cpu_steps} steps ({dt:.1f} s): C oracle env (OpenMP) "
                              f"+ NumPy fp32 NetMon(K={K}) + DQN eps-greedy, same shapes"}
         except Exception as ex:  # the baseline must never break the GPU line
@@ -348,9 +389,10 @@ def main():
                        "n_env_per_gpu": B, "n_nodes": N, "n_data": A, "netmon_iterations": K,
                        "gemm_form": L.GEMM_MODE,
                        "parallelism": f"dp{world} (env shards, no rollout collective)",
-                       "stream_groups": G, "graph_steps": args.graph},
+                       "stream_groups": G, "graph_steps": args.graph,
+                       "resets_in_window": resets},
             "host_enqueue_ms_per_step": round(host_ms, 4),
-            "roofline": roof, "cpu_baseline": cpu, "f32_exact_gemms": f32cmp, "rollout_train": train,
+            "roofline": roof, "roofline_hbm": roof_hbm or None, "cpu_baseline": cpu, "f32_exact_gemms": f32cmp, "rollout_train": train,
             "kernels": kernels,
         }
         print(json.dumps(line))

@@ -60,6 +60,30 @@ def relabel(rows, episode_steps, dqn_g=DQN_G):
     return rows
 
 
+def bench_tag(name, grid, rows):
+    """bench.py timer tag of a relabelled kernel (default rollout: N=20, H=128, M = rows)."""
+    M = rows
+    gemm = {
+        "dqn.enc0(K=512 readout+130)": f"linear:dqn.encoder.linear_layers.0:{M}x512x642",
+        "dqn.enc1+q(K=512, Q head fused)": f"linear:dqn.encoder.linear_layers.1+head:{M}x256x512",
+        "netmon.enc1(K=512)": f"linear:netmon.encode.linear_layers.1:{M}x256x512",
+        "netmon.enc2(K=256)": f"linear:netmon.encode.linear_layers.2:{M}x128x256",
+        "netmon.rnn_obs(K=128+128)": f"lstm:netmon.rnn_obs:{M}x512x256",
+        "netmon.rnn_update(K=sum128+128)": f"lstm_agg:netmon.rnn_update:{M}x512x256",
+    }
+    if name.startswith("k_gemm[") and name.endswith("]"):
+        return gemm.get(name[7:-1])
+    if name.startswith("k_env_step"):
+        return "env_step"
+    if name.startswith("k_mp_aggregate"):
+        return f"mp_aggregate:{M}x128"
+    if name.startswith("k_routing_enc"):
+        return f"routing_enc:netmon.encode.linear_layers.0:{M}x512"
+    if name.startswith("k_policy_egreedy"):
+        return "egreedy"
+    return None
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--trace", required=True)
@@ -68,6 +92,8 @@ def main():
     ap.add_argument("--top", type=int, default=20)
     ap.add_argument("--episode-steps", type=int, default=50)
     ap.add_argument("--unfused-head", action="store_true", help="profiles taken before gm_gemm_x3_head")
+    ap.add_argument("--json", help="write per-launch HBM bytes keyed by bench.py timer tags (pmc_traffic.json)")
+    ap.add_argument("--rows", type=int, default=81920, help="GEMM rows of the profiled rollout (n_env * N)")
     a = ap.parse_args()
     dqn_g = DQN_G3 if a.unfused_head else DQN_G
     dur = defaultdict(list)
@@ -98,6 +124,18 @@ def main():
         fes = "" if fe is None else f"{fe:.0f} ({2 * fe:.0f})"
         wrs = "" if wr is None else f"{wr:.0f}"
         print(f"| {n} | {g} | {w} | {len(v)} | {sum(v) / len(v) / 1e3:.1f} | {100 * sum(v) / total:.1f} | {fes} | {wrs} |")
+    if a.json:
+        import json
+
+        out = {}
+        for (n, g, w), p in pmc.items():
+            tag = bench_tag(n, g, a.rows)
+            if tag and "FETCH_SIZE" in p and "WRITE_SIZE" in p and tag not in out:
+                # KiB per launch; FETCH_SIZE doubled (gfx950 counts half of a 16-B/lane stream)
+                out[tag] = {"fetch_bytes": int(2 * p["FETCH_SIZE"] * 1024), "write_bytes": int(p["WRITE_SIZE"] * 1024),
+                            "kernel": n, "grid": g}
+        with open(a.json, "w") as f:
+            json.dump({"source": {"trace": a.trace, "fetch": a.fetch, "write": a.write}, "kernels": out}, f, indent=1)
 
 
 if __name__ == "__main__":
