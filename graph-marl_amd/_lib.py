@@ -25,12 +25,13 @@ EVAL_KEYS = ["total_edge_load", "occupied_edges", "packets_on_edges", "total_pac
 EXPORTS = [
     "gm_last_error", "gm_version", "gm_env_create", "gm_env_destroy", "gm_env_dims", "gm_env_reset",
     "gm_env_step", "gm_env_observe", "gm_env_topology", "gm_env_final_info", "gm_policy_egreedy",
-    "gm_env_get_state", "gm_build_seed_list", "gm_mp_aggregate", "gm_mp_aggregate_rows", "gm_mp_aggregate_bwd", "gm_leaky_bwd", "gm_netmon_readout",
+    "gm_env_get_state", "gm_env_set_state", "gm_build_seed_list", "gm_mp_aggregate", "gm_mp_aggregate_rows", "gm_mp_aggregate_bwd", "gm_leaky_bwd", "gm_netmon_readout",
     "gm_netmon_readout_bwd", "gm_lstm_pointwise", "gm_lstm_pointwise_bwd", "gm_linear_f32", "gm_gemm_f32",
     "gm_gemm_set_tile", "gm_simple_create", "gm_simple_destroy", "gm_simple_reset", "gm_simple_step",
     "gm_simple_observe", "gm_simple_policy_egreedy", "gm_simple_get_state", "gm_env_set_topology",
     "gm_policy_shortest_path", "gm_env_first_hops", "gm_routing_node_encoder", "gm_gemm_x3", "gm_gemm_x3_head", "gm_absmax_scale", "gm_absmax_scale_rows", "gm_gemm_x3_wgrad", "gm_absmax_finish",
-    "gm_gemm_pack_x3", "gm_gemm_pack_x3_bytes", "gm_gemm_range_status", "gm_agent_attention", "gm_agent_comm",
+    "gm_gemm_pack_x3", "gm_gemm_pack_x3_bytes", "gm_gemm_range_status",
+    "gm_pcg64_seed", "gm_pcg64_choice", "gm_agent_attention", "gm_agent_comm",
 ]
 
 # Arithmetic form of the fused rollout GEMMs (graph-marl_amd/fused.py): "x3" = split-f16
@@ -67,6 +68,12 @@ class EnvState(C.Structure):
         "rng_pos"]]
 
 
+class PCG64(C.Structure):
+    """gm_pcg64: numpy Generator(PCG64) state (bit_generator.state)."""
+    _fields_ = [("state_hi", C.c_uint64), ("state_lo", C.c_uint64), ("inc_hi", C.c_uint64), ("inc_lo", C.c_uint64),
+                ("has_uint32", C.c_uint32), ("uinteger", C.c_uint32)]
+
+
 class GMError(RuntimeError):
     pass
 
@@ -93,6 +100,7 @@ def lib():
     L.gm_env_final_info.argtypes = [vp, vp, vp]
     L.gm_policy_egreedy.argtypes = [vp, vp, C.c_double, vp, vp]
     L.gm_env_get_state.argtypes = [vp, C.POINTER(EnvState)]
+    L.gm_env_set_state.argtypes = [vp, C.POINTER(EnvState)]
     L.gm_build_seed_list.argtypes = [i32, i64, i32, vp, i32, i32, vp]
     L.gm_mp_aggregate.argtypes = [vp, vp, i32, i32, i32, i32, i32, vp, vp]
     L.gm_mp_aggregate_rows.argtypes = [vp, C.c_int64, vp, i32, i32, i32, i32, i32, vp, C.c_int64, vp]
@@ -114,6 +122,8 @@ def lib():
     L.gm_gemm_pack_x3.argtypes = [vp, i64, i32, i32, vp, vp, vp]
     L.gm_routing_node_encoder.argtypes = [vp, i64, vp, i32, i32, vp, vp, i32, i32, vp, i64, vp]
     L.gm_gemm_range_status.argtypes = [C.POINTER(i32), i32]
+    L.gm_pcg64_seed.argtypes = [C.c_uint64, C.POINTER(PCG64)]
+    L.gm_pcg64_choice.argtypes = [vp, i64, i64, vp, vp]
     _lib = L
     return L
 

@@ -1480,3 +1480,71 @@ extern "C" int gm_env_get_state(gm_env* env, gm_env_state* st) {
     }
     return GM_OK;
 }
+
+template <typename T>
+static int h2d(T* dev, const T* host, size_t n) {
+    if (!host) return GM_OK;
+    GM_HIP(hipMemcpy(dev, host, n * sizeof(T), hipMemcpyHostToDevice));
+    return GM_OK;
+}
+
+// Inverse of gm_env_get_state (parity dumps / restores): every non-NULL field is written back;
+// the neighbour table is rebuilt from the edge arrays, the numpy stream is restored as block 0
+// at rng_pos with no pre-twisted next block (pos 624 = twist before the next draw, as numpy).
+// Observation buffers are not touched: call gm_env_observe afterwards.
+extern "C" int gm_env_set_state(gm_env* env, const gm_env_state* st) {
+    if (!env || !st) return gm_fail(GM_ERR_INVALID_ARG, "null argument");
+    GM_HIP(hipSetDevice(env->device));
+    GM_HIP(hipDeviceSynchronize());
+    EnvDev& d = env->d;
+    const size_t B = d.n_env, A = d.A, N = d.N, E = d.E;
+    if (st->rng_pos)
+        for (size_t b = 0; b < B; b++)
+            if (st->rng_pos[b] < 0 || st->rng_pos[b] > (int32_t)MT_N)
+                return gm_fail(GM_ERR_INVALID_ARG, "gm_env_set_state: rng_pos outside [0, 624]");
+    if (st->nbr_edge && (!st->edge_a || !st->edge_b))
+        return gm_fail(GM_ERR_INVALID_ARG, "gm_env_set_state: nbr_edge needs edge_a and edge_b");
+    if (st->nbr_edge)
+        for (size_t i = 0; i < B * N * 3; i++)
+            if (st->nbr_edge[i] < -1 || st->nbr_edge[i] >= (int32_t)E)
+                return gm_fail(GM_ERR_INVALID_ARG, "gm_env_set_state: nbr_edge entry outside [-1, E)");
+    int rc = 0;
+    if ((rc = h2d(d.now, st->now, B * A)) || (rc = h2d(d.target, st->target, B * A)) ||
+        (rc = h2d(d.edge, st->edge, B * A)) || (rc = h2d(d.time, st->time, B * A)) ||
+        (rc = h2d(d.ttl_, st->ttl, B * A)) || (rc = h2d(d.start, st->start, B * A)) ||
+        (rc = h2d(d.spw, st->spw, B * A)) || (rc = h2d(d.steps, st->agent_steps, B * A)) ||
+        (rc = h2d(d.size, st->size, B * A)) || (rc = h2d(d.visited, st->visited, B * A * 2)) ||
+        (rc = h2d(d.amask, st->amask, B * A * 4)) || (rc = h2d(d.load, st->loads, B * E)) ||
+        (rc = h2d(d.topo_seed, st->topo_seed, B)) || (rc = h2d(d.topo_reps, st->topo_reps, B)) ||
+        (rc = h2d(d.edge_a, st->edge_a, B * E)) || (rc = h2d(d.edge_b, st->edge_b, B * E)) ||
+        (rc = h2d(d.edge_len, st->edge_len, B * E)) || (rc = h2d(d.nbr_edge, st->nbr_edge, B * N * 3)))
+        return rc;
+    if (st->nbr_edge) {  // neighbour ids in the per-node edge order (ascending neighbour id)
+        std::vector<int32_t> nbr(B * N * 3);
+        for (size_t b = 0; b < B; b++)
+            for (size_t v = 0; v < N; v++)
+                for (int k = 0; k < 3; k++) {
+                    const int32_t e = st->nbr_edge[(b * N + v) * 3 + k];
+                    nbr[(b * N + v) * 3 + k] =
+                        e < 0 ? -1 : (st->edge_a[b * E + e] == (int32_t)v ? st->edge_b[b * E + e] : st->edge_a[b * E + e]);
+                }
+        GM_HIP(hipMemcpy(d.nbr, nbr.data(), nbr.size() * sizeof(int32_t), hipMemcpyHostToDevice));
+    }
+    if (st->apsp) {
+        std::vector<int16_t> tmp(B * N * N);
+        for (size_t i = 0; i < tmp.size(); i++) tmp[i] = (int16_t)st->apsp[i];
+        GM_HIP(hipMemcpy(d.apsp, tmp.data(), tmp.size() * sizeof(int16_t), hipMemcpyHostToDevice));
+    }
+    if (st->rng_key && st->rng_pos) {
+        std::vector<uint32_t> mt(B * 2 * MT_N, 0u);
+        for (size_t b = 0; b < B; b++) memcpy(mt.data() + b * 2 * MT_N, st->rng_key + b * MT_N, MT_N * 4);
+        std::vector<int32_t> zero(B, 0);
+        GM_HIP(hipMemcpy(d.mt, mt.data(), mt.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
+        GM_HIP(hipMemcpy(d.mt_cur, zero.data(), B * sizeof(int32_t), hipMemcpyHostToDevice));
+        GM_HIP(hipMemcpy(d.mt_has_next, zero.data(), B * sizeof(int32_t), hipMemcpyHostToDevice));
+        GM_HIP(hipMemcpy(d.mt_pos, st->rng_pos, B * sizeof(int32_t), hipMemcpyHostToDevice));
+    } else if (st->rng_key || st->rng_pos) {
+        return gm_fail(GM_ERR_INVALID_ARG, "gm_env_set_state: rng_key and rng_pos go together");
+    }
+    return GM_OK;
+}

@@ -335,13 +335,20 @@ def main(argv=None):
 
     assert args.policy == "trained", f"Given policy {args.policy} cannot be used for training."
     params = list(model.parameters()) + ([] if netmon is None else list(netmon.parameters()))
+    aux_model = None
+    node_aux_size = n_nodes if (netmon is not None and isinstance(base, gm.Routing)) else 0
+    if netmon is not None and node_aux_size > 0 and args.aux_loss_coeff > 0:
+        # NetMon aux head (src/main.py:586-594): MLP(state, (state, aux), activation_on_output=False)
+        aux_model = M.MLP(node_state_size, [node_state_size, node_aux_size], activation_on_output=False).to(dev)
+        params = params + list(aux_model.parameters())
     optimizer = torch.optim.AdamW(params, lr=args.lr)
     has_state = hasattr(model, "state")
     needs_adj = args.model in ("dgn", "commnet")
     buff = RB.ReplayBuffer(args.seed, int(args.capacity), base.n_env, n_agents, base.obs_dim, n_nodes,
                            node_obs_size, node_state_size, dev, half_precision=args.replay_half_precision,
                            nbr_width=base.nbr.shape[-1] if hasattr(base, "nbr") else 3,
-                           agent_state_size=model.get_state_len() if has_state else 0, store_adj=needs_adj)
+                           agent_state_size=model.get_state_len() if has_state else 0, store_adj=needs_adj,
+                           node_aux_size=node_aux_size if aux_model is not None else 0)
     last_state = None
     comment = "_" + (f"R{args.env_var}" if args.env_type == "routing" else "Simple") + "_" + \
         {"dqn": "DQN", "dgn": "DGN", "dqnr": "DQNR", "commnet": "CommNet"}[args.model]
@@ -379,7 +386,8 @@ def main(argv=None):
             adj = base.agent_adj if needs_adj else None
             if netmon is not None:
                 buff.add_pre(base.obs, env.last_netmon_state, base.node_obs, base.nbr, base.agent_node, adj=adj,
-                             agent_state=last_state)
+                             agent_state=last_state,
+                             node_aux=base.get_node_aux() if aux_model is not None else None)
             else:
                 buff.add_pre(base.obs, adj=adj, agent_state=last_state)
             with torch.no_grad():
@@ -422,9 +430,11 @@ def main(argv=None):
             if netmon is not None:
                 netmon.train()
             batches = list(buff.get_batch(args.mini_batch_size, sequence_length=args.sequence_length))
+            parts = {}
             loss, qs, qts = T.dqn_update(netmon, model, model_tar, optimizer, params, batches, args.gamma, args.tau,
                                          args.target_update_steps, iteration,
-                                         att_coeff=args.att_regularization_coeff if args.model == "dgn" else 0.0)
+                                         att_coeff=args.att_regularization_coeff if args.model == "dgn" else 0.0,
+                                         aux_model=aux_model, aux_coeff=args.aux_loss_coeff, parts=parts)
             model.eval()
             if netmon is not None:
                 netmon.eval()
@@ -433,6 +443,8 @@ def main(argv=None):
                 log.add_host("q_values", float(torch.stack([q.detach().mean() for q in qs]).mean().item()))
                 log.add_host("q_target", float(torch.stack([q.mean() for q in qts]).mean().item()))
                 log.add_host("loss", float(loss.item()))
+                if aux_model is not None:
+                    log.add_host("loss_aux", float(parts["loss_aux"].item()))
             if args.target_update_steps > 0 and iteration % args.target_update_steps == 0:
                 print(f"Update network, train iteration {iteration}")
             if step % int(args.model_checkpoint_steps) == 0:

@@ -9,29 +9,37 @@ Differences from the reference, by design:
     909-915); the graph is stored as its neighbour table and the node-agent matrix
     as the agent -> node index, the NetMon input state as in the reference
     (the state *before* the NetMon call that produced obs, wrapper.py:99-104);
-  * sampling draws from a torch device generator seeded with `seed` — uniform like
-    the reference's np.random.default_rng(seed).choice, but a different stream
-    (sampling indices are not part of the parity contract).
+  * sampling: the reference's stream itself, np.random.default_rng(seed).choice(n, size,
+    replace=True), generated on the device (gm_pcg64_choice: numpy's PCG64 + Lemire bounded
+    draws, state kept in HBM). The ring is (slot, env): a uniform batch draws
+    f = choice(count * n_env) -> (slot f // n_env, env f % n_env); a sequence batch draws
+    f = choice(n_env * (count - L)) -> env f // (count - L), start = (index % count +
+    f % (count - L)) % count. With n_env = 1 both are the reference's indices exactly
+    (src/replaybuffer.py:107-130; tests/test_replay_rng.py against its golden).
 """
+import ctypes as C
 from collections import namedtuple
 
 import torch
 
+from . import _lib as L
+
 TransitionBatch = namedtuple(
     "TransitionBatch",
     ["idx", "obs", "action", "reward", "next_obs", "done", "episode_done", "node_obs", "nbr", "node_state",
-     "agent_node", "next_node_obs", "next_agent_node", "adj", "next_adj", "agent_state"],
-    defaults=(None, None, None),
+     "agent_node", "next_node_obs", "next_agent_node", "adj", "next_adj", "agent_state", "node_aux"],
+    defaults=(None, None, None, None),
 )
 
 
 class ReplayBuffer:
     def __init__(self, seed, capacity, n_env, n_agents, obs_dim, n_nodes, node_obs_dim, node_state_size,
-                 device, half_precision=False, nbr_width=3, agent_state_size=0, store_adj=False):
+                 device, half_precision=False, nbr_width=3, agent_state_size=0, store_adj=False, node_aux_size=0):
         """capacity: transitions (env-steps) like the reference; the ring holds
         ceil(capacity / n_env) vector steps. agent_state_size > 0 stores the recurrent
         models' agent state (DQNR / CommNet), store_adj the agent adjacency (DGN / CommNet),
-        src/replaybuffer.py:64-99."""
+        src/replaybuffer.py:64-99; node_aux_size > 0 stores the env's node aux targets
+        (get_node_aux, [N][node_aux_size]) for the NetMon aux loss (--aux-loss-coeff)."""
         self.n_env, self.A, self.N = n_env, n_agents, n_nodes
         self.slots = max(1, -(-int(capacity) // n_env))
         self.capacity = self.slots * n_env
@@ -59,20 +67,26 @@ class ReplayBuffer:
             self.next_agent_node = z(S, B, A, dtype=torch.int8)
             self.node_state = z(S, B, N, node_state_size)
         self.agent_state = z(S, B, A, agent_state_size) if agent_state_size > 0 else None
+        self.node_aux = z(S, B, N, node_aux_size) if node_aux_size > 0 else None
         self.adj = z(S, B, A, A, dtype=torch.bool) if store_adj else None
         self.next_adj = z(S, B, A, A, dtype=torch.bool) if store_adj else None
-        self.gen = torch.Generator(device=device)
-        self.gen.manual_seed(seed)
+        st = L.PCG64()
+        L.check(L.lib().gm_pcg64_seed(C.c_uint64(int(seed) & 0xFFFFFFFFFFFFFFFF), C.byref(st)))
+        self.rng = torch.frombuffer(bytearray(bytes(st)), dtype=torch.uint8).to(device)  # gm_pcg64 in HBM
 
     def nbytes(self):
         return sum(t.numel() * t.element_size() for t in self.__dict__.values() if torch.is_tensor(t))
 
-    def add_pre(self, obs, node_state=None, node_obs=None, nbr=None, agent_node=None, adj=None, agent_state=None):
+    def add_pre(self, obs, node_state=None, node_obs=None, nbr=None, agent_node=None, adj=None, agent_state=None,
+                node_aux=None):
         """First half of a transition, recorded before the env step: the observation and the
         NetMon inputs that produced it (node_state = the NetMon state before that call), the
-        agent adjacency and the agent state the model starts the step from (None = zeros)."""
+        agent adjacency, the agent state the model starts the step from (None = zeros) and the
+        node aux targets (src/main.py:697-699)."""
         i = self.index
         self.obs[i].copy_(obs)
+        if self.node_aux is not None:
+            self.node_aux[i].copy_(node_aux)
         if self.adj is not None:
             self.adj[i].copy_(adj != 0)
         if self.agent_state is not None:
@@ -127,22 +141,37 @@ class ReplayBuffer:
             self.adj[slot, env].to(f) if self.adj is not None else None,
             self.next_adj[slot, env].to(f) if self.next_adj is not None else None,
             self.agent_state[slot, env].to(f) if self.agent_state is not None else None,
+            self.node_aux[slot, env].to(f) if self.node_aux is not None else None,
         )
+
+    def choice(self, n, size):
+        """np.random.default_rng(seed).choice(n, size, replace=True) continuing this buffer's
+        stream, as a device int64 tensor (gm_pcg64_choice)."""
+        out = torch.empty(size, dtype=torch.int64, device=self.device)
+        L.check(L.lib().gm_pcg64_choice(L.ptr(self.rng), int(n), int(size), L.ptr(out), L.stream_ptr(self.device)))
+        return out
+
+    def rng_state(self):
+        """The sampling stream's numpy bit_generator.state fields (synchronous)."""
+        st = L.PCG64.from_buffer_copy(self.rng.cpu().numpy().tobytes())
+        return {"state": (st.state_hi << 64) | st.state_lo, "inc": (st.inc_hi << 64) | st.inc_lo,
+                "has_uint32": st.has_uint32, "uinteger": st.uinteger}
 
     def get_batch(self, batch_size, sequence_length=1):
         """Yields sequence_length TransitionBatches of batch_size transitions
-        (src/replaybuffer.py:103-130): uniform env and start slot; sequences are
-        consecutive slots of one env, starting from the oldest slot and wrapping."""
-        dev = self.device
-        env = torch.randint(0, self.n_env, (batch_size,), device=dev, generator=self.gen)
+        (src/replaybuffer.py:103-130): uniform (slot, env); sequences are consecutive slots of
+        one env, starting from the oldest slot and wrapping."""
+        if self.count == 0:
+            raise ValueError("empty replay buffer")
         if sequence_length <= 1:
-            slot = torch.randint(0, self.count, (batch_size,), device=dev, generator=self.gen)
-            yield self._gather(slot, env)
+            f = self.choice(self.count * self.n_env, batch_size)
+            yield self._gather(f // self.n_env, f % self.n_env)
             return
         if self.count <= sequence_length:
             raise ValueError("not enough transitions for the requested sequence length")
-        start = self.index % self.count
-        off = torch.randint(0, self.count - sequence_length, (batch_size,), device=dev, generator=self.gen)
-        first = (start + off) % self.count
+        span = self.count - sequence_length
+        f = self.choice(self.n_env * span, batch_size)
+        env = f // span
+        first = (self.index % self.count + f % span) % self.count
         for o in range(sequence_length):
             yield self._gather((first + o) % self.count, env)

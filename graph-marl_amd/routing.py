@@ -337,6 +337,30 @@ class Routing:
         L.check(L.lib().gm_env_get_state(self._h, C.byref(st)))
         return arrs
 
+    def set_state(self, arrs):
+        """Restore a get_state() dump (gm_env_set_state) and re-emit the observations; keys
+        missing from `arrs` keep their current device values."""
+        B, A, N, E = self.n_env, self.n_data, self.n_nodes, 3 * self.n_nodes // 2
+        shapes = dict(now=(B, A), target=(B, A), edge=(B, A), time=(B, A), ttl=(B, A), start=(B, A), spw=(B, A),
+                      agent_steps=(B, A), size=(B, A), visited=(B, A, 2), amask=(B, A, 4), loads=(B, E),
+                      topo_seed=(B,), topo_reps=(B,), edge_a=(B, E), edge_b=(B, E), edge_len=(B, E),
+                      nbr_edge=(B, N, 3), apsp=(B, N, N), rng_key=(B, 624), rng_pos=(B,))
+        dtypes = dict(size=np.float64, loads=np.float64, visited=np.uint64, amask=np.uint8, topo_seed=np.int64,
+                      rng_key=np.uint32)
+        st = L.EnvState()
+        keep = []
+        for k, shp in shapes.items():
+            if k not in arrs:
+                continue
+            a = np.ascontiguousarray(np.asarray(arrs[k], dtype=dtypes.get(k, np.int32)).reshape(shp))
+            keep.append(a)
+            setattr(st, k, a.ctypes.data)
+        torch.cuda.synchronize(self.device)
+        L.check(L.lib().gm_env_set_state(self._h, C.byref(st)))
+        self.observe()
+        L.check(L.lib().gm_env_topology(self._h, L.ptr(self.nbr), None, None, None, self._stream()))
+        torch.cuda.synchronize(self.device)
+
     @property
     def action_mask(self):
         return torch.as_tensor(self.get_state()["amask"].astype(bool), device=self.device)

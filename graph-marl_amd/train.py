@@ -106,14 +106,16 @@ def _fused_next_q(netmon, model_tar, batch):
     return q.view(B, A, -1)
 
 
-def dqn_loss(netmon, model, model_tar, batches, gamma, att_coeff=0.0):
-    """Sequence loss of src/main.py:840-960 for DQN / DGN / DQNR / CommNet (no aux term);
-    netmon may be None. Recurrent models start from the stored agent state, the target
-    model runs from the online model's next state, and the state is reset for done agents
-    and at episode ends. Returns (loss, list of q, list of q_target)."""
+def dqn_loss(netmon, model, model_tar, batches, gamma, att_coeff=0.0, aux_model=None, aux_coeff=0.0, parts=None):
+    """Sequence loss of src/main.py:840-1000 for DQN / DGN / DQNR / CommNet; netmon may be None.
+    Recurrent models start from the stored agent state, the target model runs from the online
+    model's next state, and the state is reset for done agents and at episode ends. aux_model
+    (with netmon): the NetMon aux head on the new NetMon state, MSE against the stored node aux
+    targets, weighted by aux_coeff (src/main.py:586-594, 868-875, 996-1000). parts (a dict)
+    receives the loss terms. Returns (loss, list of q, list of q_target)."""
     L = len(batches)
     has_state = hasattr(model, "state")
-    loss_q = loss_att = None
+    loss_q = loss_att = loss_aux = None
     qs, qts = [], []
     last_state = last_ep_done = None
     fused_tar = not has_state and _fused_target_ok(netmon, model_tar) and FUSED_TARGET
@@ -128,6 +130,9 @@ def dqn_loss(netmon, model, model_tar, batches, gamma, att_coeff=0.0):
             else:
                 netmon.state = last_state * (~last_ep_done).view(-1, 1, 1)
             obs = joint_obs(batch.obs, netmon.forward_graph(batch.node_obs, batch.nbr, batch.agent_node))
+            if aux_model is not None:
+                term = torch.mean((aux_model(netmon.state) - batch.node_aux) ** 2) / L
+                loss_aux = term if loss_aux is None else loss_aux + term
             last_state = netmon.state
             last_ep_done = batch.episode_done.expand(batch.obs.shape[0]) if batch.episode_done.dim() == 0 \
                 else batch.episode_done
@@ -157,12 +162,18 @@ def dqn_loss(netmon, model, model_tar, batches, gamma, att_coeff=0.0):
         qs.append(q)
         qts.append(q_target)
     loss = loss_q if loss_att is None else loss_q + att_coeff * loss_att
+    if loss_aux is not None:
+        loss = loss + aux_coeff * loss_aux
+    if parts is not None:
+        parts.update(loss_q=loss_q, loss_att=loss_att, loss_aux=loss_aux)
     return loss, qs, qts
 
 
 def dqn_update(netmon, model, model_tar, optimizer, params, batches, gamma, tau, target_update_steps=0,
-               iteration=1, group=None, att_coeff=0.0):
-    loss, qs, qts = dqn_loss(netmon, model, model_tar, batches, gamma, att_coeff)
+               iteration=1, group=None, att_coeff=0.0, aux_model=None, aux_coeff=0.0, parts=None):
+    """One update (src/main.py:840-1026). params must include aux_model's parameters when
+    the aux loss is on (src/main.py:594)."""
+    loss, qs, qts = dqn_loss(netmon, model, model_tar, batches, gamma, att_coeff, aux_model, aux_coeff, parts)
     optimizer.zero_grad(set_to_none=False)
     loss.backward()
     allreduce_gradients(params, group)

@@ -171,6 +171,12 @@ typedef struct {
     int32_t* rng_pos;    /* [n_env]                          */
 } gm_env_state;
 int gm_env_get_state(gm_env* env, gm_env_state* st);
+/* Inverse of gm_env_get_state (synchronous): restores every non-NULL field (host arrays, same
+ * layout); the neighbour table is rebuilt from nbr_edge + edge_a/edge_b, the numpy stream from
+ * (rng_key, rng_pos) (both or neither). Observation buffers are left as they are: call
+ * gm_env_observe. Replaces restoring a pickled Routing/Network (the reference has no state API;
+ * its parity dumps are the numpy RandomState + object state, src/env/routing.py:30-178). */
+int gm_env_set_state(gm_env* env, const gm_env_state* st);
 
 /* ---- NetMon message passing (graphs of fixed max degree, ELL neighbour table) ----
  * h: float32 [G*N, H] rows; nbr: int32 [G, N, deg] neighbour ids (-1 = none).
@@ -359,6 +365,22 @@ int gm_simple_observe(gm_simple_env* env, const gm_simple_obs* obs, void* stream
 int gm_simple_policy_egreedy(gm_simple_env* env, const float* q, double epsilon, int32_t* actions, void* stream);
 /* synchronous; fails with GM_ERR_INVALID_ARG if an invalid action was stepped since the last call */
 int gm_simple_get_state(gm_simple_env* env, gm_simple_state* st);
+
+/* ---- Replay sampling stream (reference src/replaybuffer.py:101-130: np.random.default_rng(seed)
+ * .choice(n, size, replace=True)) ----
+ * numpy Generator state: PCG64 128-bit state and increment plus the buffered high half of the
+ * last 64-bit output (has_uint32 / uinteger), exactly numpy's bit_generator.state. */
+typedef struct gm_pcg64 {
+    uint64_t state_hi, state_lo, inc_hi, inc_lo;
+    uint32_t has_uint32, uinteger;
+} gm_pcg64;
+/* Host: numpy.random.default_rng(seed)'s initial state (SeedSequence(seed).generate_state(4,
+ * uint64), PCG64 srandom) for 0 <= seed < 2^64. */
+int gm_pcg64_seed(uint64_t seed, gm_pcg64* out);
+/* Device: out[0..count) = Generator.choice(n, count, replace=True) (= integers(0, n, int64):
+ * Lemire's bounded 32-bit draws with numpy's rejection rule) continuing the stream in `state`
+ * (device memory, advanced in place, stream-ordered). 1 <= n <= 2^32 - 1. */
+int gm_pcg64_choice(gm_pcg64* state, int64_t n, int64_t count, int64_t* out, void* stream);
 
 #ifdef __cplusplus
 }

@@ -316,8 +316,9 @@ def gen_env(out_dir, Network, Routing, EVAL_SEEDS, names=None):
 # ---------------------------------------------------------------------------
 # NetMon / DQN / training-step goldens
 # ---------------------------------------------------------------------------
-def collect_graph_inputs(Network, Routing, EVAL_SEEDS, n, a, B, steps, seed):
-    """node obs / adj / node-agent for B independent envs over `steps` consecutive steps."""
+def collect_graph_inputs(Network, Routing, EVAL_SEEDS, n, a, B, steps, seed, aux=None):
+    """node obs / adj / node-agent for B independent envs over `steps` consecutive steps
+    (aux: a list that receives get_node_aux() per step, src/env/routing.py:237-254)."""
     obs_l, adj_l, na_l, aobs_l = [], [], [], []
     rng = np.random.RandomState(seed + 77)
     envs = []
@@ -334,6 +335,8 @@ def collect_graph_inputs(Network, Routing, EVAL_SEEDS, n, a, B, steps, seed):
             ad.append(env.get_nodes_adjacency().astype(np.float32))
             na.append(env.get_node_agent_matrix().astype(np.float32))
             ao.append(env._get_observation())
+            if aux is not None:
+                aux.append(np.asarray(env.get_node_aux(), np.float32))
             env.step(rng.randint(4, size=a))
         obs_l.append(np.stack(o))
         adj_l.append(np.stack(ad))
@@ -513,15 +516,18 @@ def gen_models(out, Network, Routing, EVAL_SEEDS, DGN, DQNR, CommNet):
     print("models done", flush=True)
 
 
-def gen_train(out, Network, Routing, EVAL_SEEDS, NetMon, DQN, interpolate_model):
-    """One DQN+NetMon update exactly as src/main.py:832-1022 performs it (sequence replay)."""
+def gen_train(out, Network, Routing, EVAL_SEEDS, NetMon, DQN, interpolate_model, aux_coeff=0.0, MLP=None):
+    """One DQN+NetMon update exactly as src/main.py:832-1022 performs it (sequence replay);
+    aux_coeff > 0 adds the NetMon aux head and loss (src/main.py:586-594, 868-875, 996-1000)."""
     import torch
     import torch.nn.functional as F
     import torch.optim as optim
 
     d = {}
     n, a, B, L = 20, 20, 3, 3
-    node_obs, node_adj, node_agent, agent_obs = collect_graph_inputs(Network, Routing, EVAL_SEEDS, n, a, B, L + 1, 200)
+    aux_l = [] if aux_coeff > 0 else None
+    node_obs, node_adj, node_agent, agent_obs = collect_graph_inputs(Network, Routing, EVAL_SEEDS, n, a, B, L + 1, 200,
+                                                                     aux=aux_l)
     rng = np.random.RandomState(5)
     torch.manual_seed(3)
     netmon = NetMon(node_obs.shape[-1], 32, [64, 48], 1, F.leaky_relu, rnn_type="lstm",
@@ -536,6 +542,14 @@ def gen_train(out, Network, Routing, EVAL_SEEDS, NetMon, DQN, interpolate_model)
     sd_to_npz("netmon_", netmon.state_dict(), d)
     sd_to_npz("model_", model.state_dict(), d)
     sd_to_npz("target_", model_tar.state_dict(), d)
+    aux_model = None
+    if aux_coeff > 0:
+        S = netmon.get_state_size()
+        aux_model = MLP(S, (S, n), F.leaky_relu, activation_on_output=False)
+        sd_to_npz("aux_", aux_model.state_dict(), d)
+        node_aux = np.stack(aux_l).reshape(L + 1, B, n, n)
+        d["node_aux"] = node_aux
+        d["aux_coeff"] = np.float64(aux_coeff)
     node_state0 = (0.1 * rng.standard_normal((B, n, netmon.get_state_size()))).astype(np.float32)
     actions = rng.randint(4, size=(L, B, a))
     reward = rng.choice(np.array([0.0, -0.2, 10.0, -10.0, 9.8], dtype=np.float32), size=(L, B, a)).astype(np.float32)
@@ -547,10 +561,13 @@ def gen_train(out, Network, Routing, EVAL_SEEDS, NetMon, DQN, interpolate_model)
     gamma, lr, tau = 0.9, 1e-3, 0.01
     d["gamma"], d["lr"], d["tau"] = np.float64(gamma), np.float64(lr), np.float64(tau)
     parameters = list(model.parameters()) + list(netmon.parameters())
+    if aux_model is not None:
+        parameters = parameters + list(aux_model.parameters())
     optimizer = optim.AdamW(parameters, lr=lr)
     netmon.train()
     model.train()
     loss_q = torch.zeros(1)
+    loss_aux = torch.zeros(1)
     for t in range(L):
         obs = np.concatenate([agent_obs[t], np.zeros((B, a, netmon.get_out_features()), np.float32)], -1)
         next_obs = np.concatenate([agent_obs[t + 1], np.zeros((B, a, netmon.get_out_features()), np.float32)], -1)
@@ -561,6 +578,9 @@ def gen_train(out, Network, Routing, EVAL_SEEDS, NetMon, DQN, interpolate_model)
         else:
             netmon.state = last_netmon_state * (~last_ep_done).view(-1, 1, 1)  # noqa: F821
         network_obs = netmon(torch.tensor(node_obs[t]), torch.tensor(node_adj[t]), torch.tensor(node_agent[t]))
+        if aux_model is not None:
+            aux_prediction = aux_model(netmon.state)
+            loss_aux = loss_aux + torch.mean((aux_prediction - torch.tensor(node_aux[t])) ** 2) / L
         obs[:, :, -network_obs.shape[-1]:] = network_obs
         last_netmon_state = netmon.state
         last_ep_done = torch.tensor(episode_done[t])
@@ -576,9 +596,14 @@ def gen_train(out, Network, Routing, EVAL_SEEDS, NetMon, DQN, interpolate_model)
         d[f"q_{t}"] = q_values.detach().numpy()
         d[f"qtarget_{t}"] = q_target.numpy()
     optimizer.zero_grad()
-    loss_q.backward()
-    d["loss"] = loss_q.detach().numpy()
+    loss = loss_q + aux_coeff * loss_aux if aux_model is not None else loss_q
+    loss.backward()
+    d["loss"] = loss.detach().numpy()
+    if aux_model is not None:
+        d["loss_aux"] = loss_aux.detach().numpy()
     names = [f"model_{k}" for k, _ in model.named_parameters()] + [f"netmon_{k}" for k, _ in netmon.named_parameters()]
+    if aux_model is not None:
+        names += [f"aux_{k}" for k, _ in aux_model.named_parameters()]
     for nm_, p in zip(names, parameters):
         d["grad_raw_" + nm_] = p.grad.detach().numpy().copy()
     torch.nn.utils.clip_grad_value_(parameters, 0.5)
@@ -823,6 +848,96 @@ def gen_sl(out, Network, Routing, EVAL_SEEDS, NetMon, n=20, seeds=None, H=32, en
     print("sl:", out)
 
 
+def gen_replay(out, ReplayBuffer):
+    """ReplayBuffer sampling indices (src/replaybuffer.py:101-130): transitions t = 0, 1, ...
+    inserted in order (obs = t), then a script of get_batch calls (uniform and sequence) with
+    interleaved inserts, including ring wrap-around; the yielded TransitionBatch.indices of
+    every call are recorded in call order."""
+    d = {}
+    scripts = {
+        # name: (seed, buffer_size, [("add", n) | ("get", batch, seq_len)])
+        "a": (7, 64, [("add", 40), ("get", 32, 1), ("get", 17, 1), ("get", 16, 8), ("get", 5, 3), ("add", 60),
+                      ("get", 32, 1), ("get", 33, 8), ("get", 1, 2), ("get", 32, 0)]),
+        "b": (0, 1000, [("add", 523), ("get", 4096, 8), ("get", 3, 1), ("add", 900), ("get", 2049, 8),
+                        ("get", 4097, 1)]),
+        "c": (123456789, 10, [("add", 9), ("get", 7, 8), ("get", 5, 1), ("add", 3), ("get", 6, 2)]),
+    }
+    for name, (seed, size, script) in scripts.items():
+        rb = ReplayBuffer(seed, size, 2, 3, 0)
+        t = 0
+        calls = []
+        for op in script:
+            if op[0] == "add":
+                for _ in range(op[1]):
+                    z2 = np.zeros((2, 2), bool)
+                    rb.add(np.full((2, 3), t, np.float32), np.zeros(2, np.int8), np.zeros(2, np.float32),
+                           np.zeros((2, 3), np.float32), z2, z2, np.zeros(2, bool), False, np.zeros((1, 2, 0)),
+                           np.zeros((0, 0)), np.zeros((0, 0)), np.zeros((0, 0)), np.zeros((0, 0), bool),
+                           np.zeros((0, 2), bool), np.zeros((0, 0)), np.zeros((0, 0), bool), np.zeros((0, 2), bool))
+                    t += 1
+            else:
+                idx = [np.asarray(b.idx, np.int64) for b in rb.get_batch(op[1], "cpu", sequence_length=op[2])]
+                calls.append(np.stack(idx))
+        d[f"{name}_seed"] = np.int64(seed)
+        d[f"{name}_size"] = np.int64(size)
+        d[f"{name}_script"] = np.array([[0, op[1], 0] if op[0] == "add" else [1, op[1], op[2]] for op in script],
+                                       np.int64)
+        for i, c in enumerate(calls):
+            d[f"{name}_idx{i}"] = c
+        st = rb._random_generator.bit_generator.state
+        d[f"{name}_final_state"] = np.array([st["state"]["state"] >> 64, st["state"]["state"] & (2**64 - 1),
+                                             st["has_uint32"], st["uinteger"]], np.uint64)
+    np.savez_compressed(out, **d)
+    print("replay:", out)
+
+
+def gen_checkpoint(out_pt, out_npz, ref, Network, Routing, EVAL_SEEDS, NetMon, DQN, get_state_dict):
+    """A checkpoint written by the reference's own get_state_dict (src/util.py:26-35) with the
+    args.__dict__ of the reference's own parser (src/main.py:40-381, the parser statements executed
+    here) for a small NetMon + DQN, saved with torch.save as src/main.py:812-817 does; plus the
+    reference models' Q-values over 3 carried NetMon steps on 2 graphs (NetMonWrapper +
+    EpsilonGreedy.q, src/env/wrapper.py:66-109, src/model.py:187-203)."""
+    import torch
+    import torch.nn.functional as F
+
+    import types
+
+    tb = types.ModuleType("torch.utils.tensorboard")
+    tbw = types.ModuleType("torch.utils.tensorboard.writer")
+    tbw.SummaryWriter = type("SummaryWriter", (), {})  # imported by main.py, never used by the parser
+    tb.writer = tbw
+    sys.modules.setdefault("torch.utils.tensorboard", tb)
+    sys.modules.setdefault("torch.utils.tensorboard.writer", tbw)
+    src = open(os.path.join(ref, "main.py")).read()
+    ns = {"__name__": "reference_main_parser"}
+    exec(compile(src[: src.index("args = parser.parse_args()")], "main.py", "exec"), ns)
+    args = ns["parser"].parse_args(["--env-type=routing", "--model=dqn", "--netmon", "--netmon-dim=16",
+                                    "--netmon-encoder-dim=32,16", "--netmon-iterations=2", "--hidden-dim=32,24",
+                                    "--seed=3"])
+    n, a, B, steps = 20, 20, 2, 3
+    node_obs, node_adj, node_agent, agent_obs = collect_graph_inputs(Network, Routing, EVAL_SEEDS, n, a, B, steps, 300)
+    torch.manual_seed(21)
+    act = getattr(F, args.activation_function)
+    netmon = NetMon(node_obs.shape[-1], args.netmon_dim, [int(x) for x in args.netmon_encoder_dim.split(",")],
+                    args.netmon_iterations, activation_fn=act, rnn_type=args.netmon_rnn_type,
+                    rnn_carryover=args.netmon_rnn_carryover, agg_type=args.netmon_agg_type,
+                    output_neighbor_hidden=True, output_global_hidden=args.netmon_global)
+    model = DQN(agent_obs.shape[-1] + netmon.get_out_features(), [int(x) for x in args.hidden_dim.split(",")], 4,
+                act)
+    torch.save(get_state_dict(model, netmon, args.__dict__), out_pt)
+    d = {"node_obs": node_obs, "node_adj": node_adj, "node_agent": node_agent, "agent_obs": agent_obs}
+    netmon.eval()
+    model.eval()
+    netmon.state = None
+    with torch.no_grad():
+        for t in range(steps):
+            h = netmon(torch.tensor(node_obs[t]), torch.tensor(node_adj[t]), torch.tensor(node_agent[t]))
+            joint = torch.cat([torch.tensor(agent_obs[t]), h], -1)
+            d[f"q_{t}"] = model(joint, None).numpy()
+    np.savez_compressed(out_npz, **d)
+    print("checkpoint:", out_pt, out_npz)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--ref", default="/root/reference/src")
@@ -835,11 +950,12 @@ def main():
     from env.network import Network  # noqa: E402
     from env.routing import Routing  # noqa: E402
     from env.constants import EVAL_SEEDS  # noqa: E402
-    from model import NetMon, DQN, DGN, DQNR, CommNet  # noqa: E402
-    from util import interpolate_model  # noqa: E402
+    from model import MLP, NetMon, DQN, DGN, DQNR, CommNet  # noqa: E402
+    from util import get_state_dict, interpolate_model  # noqa: E402
     from env.simple_environment import SimpleEnvironment  # noqa: E402
     from policy import ShortestPath  # noqa: E402
     from eval import evaluate  # noqa: E402
+    from replaybuffer import ReplayBuffer  # noqa: E402
 
     only = set(args.only.split(",")) if args.only else None
     if only is None or "seeds" in only:
@@ -862,6 +978,12 @@ def main():
         gen_models(os.path.join(HERE, "models.npz"), Network, Routing, EVAL_SEEDS, DGN, DQNR, CommNet)
     if only is None or "train" in only:
         gen_train(os.path.join(HERE, "train.npz"), Network, Routing, EVAL_SEEDS, NetMon, DQN, interpolate_model)
+    if only is None or "train_aux" in only:
+        gen_train(os.path.join(HERE, "train_aux.npz"), Network, Routing, EVAL_SEEDS, NetMon, DQN, interpolate_model,
+                  aux_coeff=0.3, MLP=MLP)
+    if only is None or "checkpoint" in only:
+        gen_checkpoint(os.path.join(HERE, "ref_checkpoint.pt"), os.path.join(HERE, "ref_checkpoint.npz"), args.ref,
+                       Network, Routing, EVAL_SEEDS, NetMon, DQN, get_state_dict)
     if only is None or "shortest" in only:
         gen_shortest(os.path.join(HERE, "shortest.npz"), Network, Routing, EVAL_SEEDS, ShortestPath)
     if only is None or "eval" in only:
@@ -874,6 +996,8 @@ def main():
         seeds100 = np.load(os.path.join(HERE, "topology.npz"))["rand_n100_seed"][:4]
         gen_sl(os.path.join(HERE, "sl_n100.npz"), Network, Routing, EVAL_SEEDS, NetMon, n=100, seeds=seeds100,
                H=128, enc=(512, 256))
+    if only is None or "replay" in only:
+        gen_replay(os.path.join(HERE, "replay.npz"), ReplayBuffer)
     if only is None or "simple" in only:
         gen_simple(os.path.join(HERE, "simple.npz"), SimpleEnvironment)
 

@@ -37,6 +37,18 @@ def test_routing_netmon_train_checkpoint_and_reload(tmp_path):
     assert np.isfinite(m2["reward_mean"])
 
 
+def test_routing_netmon_aux_loss_train(tmp_path, capsys):
+    """--aux-loss-coeff > 0: the NetMon aux head trains with the update (src/main.py:586-594,
+    868-875, 996-1009) and its loss is logged."""
+    main = importlib.import_module("graph-marl_amd.main")
+    m = main.main(["--env-type=routing", "--model=dqn", "--netmon", "--netmon-iterations=1", "--n-env=32",
+                   "--episode-steps=50", "--total-steps=1000", "--step-before-train=100", "--mini-batch-size=32",
+                   "--sequence-length=4", "--capacity=40000", "--aux-loss-coeff=0.5", "--eval-episodes=32",
+                   "--eval-episode-steps=20", "--disable-progressbar", f"--log-dir={tmp_path}"])
+    assert np.isfinite(m["reward_mean"])
+    assert "loss_aux" in capsys.readouterr().out
+
+
 def test_routing_no_netmon_train(tmp_path):
     main = importlib.import_module("graph-marl_amd.main")
     m = main.main(["--env-type=routing", "--model=dqn", "--random-topology=0", "--n-env=32", "--total-steps=200",

@@ -289,3 +289,57 @@ def test_topology_from_seed_matches_reference_golden(gm, n):
         assert st["topo_seed"][b] == seeds[b]
     adj = env.get_nodes_adjacency().cpu().numpy()
     np.testing.assert_array_equal(adj, g[f"rand_n{n}_adj"].astype(np.int8))
+
+
+def test_set_state_restores_a_dump(gm, oracle_mod):
+    """gm_env_set_state (Routing.set_state) restores a get_state() dump into an env created with
+    other seeds: observations are re-emitted identically and the next 40 steps (with resets of
+    done packets drawing from the restored numpy streams) match the original env bit for bit;
+    a dump taken from the C oracle (same state layout) restores into the device env too."""
+    n, a, B = 20, 20, 12
+    net = gm.Network(n, random_topology=True, excluded_seeds=R.EVAL_SEEDS)
+    e1 = gm.Routing(net, a, n_env=B, seed=5)
+    e2 = gm.Routing(net, a, n_env=B, seed=900)
+    e1.reset_()
+    e2.reset_()
+    rng = np.random.RandomState(0)
+    for _ in range(25):
+        e1.step_(torch.as_tensor(rng.randint(4, size=(B, a)), dtype=torch.int32, device="cuda"))
+    dump = e1.get_state()
+    e2.set_state(dump)
+    np.testing.assert_array_equal(e2.obs_buf.cpu().numpy(), e1.obs_buf.cpu().numpy())
+    np.testing.assert_array_equal(e2.node_obs.cpu().numpy(), e1.node_obs.cpu().numpy())
+    np.testing.assert_array_equal(e2.nbr.cpu().numpy(), e1.nbr.cpu().numpy())
+    for _ in range(40):
+        act = torch.as_tensor(rng.randint(4, size=(B, a)), dtype=torch.int32, device="cuda")
+        e1.step_(act)
+        e2.step_(act)
+    s1, s2 = e1.get_state(), e2.get_state()
+    for k in s1:
+        np.testing.assert_array_equal(s1[k], s2[k], err_msg=k)
+    np.testing.assert_array_equal(e2.obs_buf.cpu().numpy(), e1.obs_buf.cpu().numpy())
+    # oracle -> device: one oracle env advanced 30 steps, its packet/load/stream state written
+    # into env 0 of e2 (topology taken from the oracle as well)
+    cfg = oracle_mod.make_config(n, a, topo_mode=oracle_mod.TOPO_RANDOM, excluded=R.EVAL_SEEDS)
+    o = oracle_mod.OracleEnv(cfg, 77)
+    o.reset()
+    for _ in range(30):
+        o.step(rng.randint(4, size=a))
+    os_, ot = o.state(), o.topology()
+    d = e2.get_state()
+    for k in ("now", "target", "edge", "time", "ttl", "start", "spw", "agent_steps", "size", "visited", "amask"):
+        d[k][0] = os_[k]
+    E = 3 * n // 2
+    d["loads"][0] = os_["loads"]
+    d["topo_seed"][0] = os_["topo_seed"]
+    d["edge_a"][0], d["edge_b"][0], d["edge_len"][0] = ot["edges"][:E, 0], ot["edges"][:E, 1], ot["edges"][:E, 2]
+    d["nbr_edge"][0] = ot["node_edges"]
+    d["apsp"][0] = ot["apsp"]
+    d["rng_key"][0], d["rng_pos"][0] = os_["rng_key"], os_["rng_pos"]
+    e2.set_state(d)
+    for t in range(30):
+        act = rng.randint(4, size=(B, a))
+        o.step(act[0])
+        e2.step_(torch.as_tensor(act, dtype=torch.int32, device="cuda"))
+        np.testing.assert_array_equal(e2.obs_buf[0, :, : 6 * n + 10].cpu().numpy(), o.observe()["obs"],
+                                      err_msg=f"step {t}")

@@ -19,12 +19,16 @@ def mods():
 
 def _sd(g, prefix):
     return {k[len(prefix):]: torch.as_tensor(g[k]) for k in g.files
-            if k.startswith(prefix) and not k.startswith(prefix + "after_")}
+            if k.startswith(prefix) and not k.startswith(prefix + "after_") and k != "aux_coeff"}
 
 
-def test_update_matches_reference_golden():
+@pytest.mark.parametrize("name", ["train.npz", "train_aux.npz"])
+def test_update_matches_reference_golden(name):
+    """train_aux.npz: the same update with --aux-loss-coeff 0.3 (NetMon aux MLP on the new NetMon
+    state, MSE against get_node_aux, src/main.py:586-594, 868-875, 996-1000)."""
     M, T, RB = mods()
-    g = np.load(f"{R.GOLDEN}/train.npz")
+    g = np.load(f"{R.GOLDEN}/{name}")
+    aux = "aux_coeff" in g.files
     dev = torch.device("cuda")
     nd = g["node_obs"].shape[-1]
     netmon = M.NetMon(nd, 32, [64, 48], 1).to(dev)
@@ -34,6 +38,11 @@ def test_update_matches_reference_golden():
     model.load_state_dict(_sd(g, "model_"))
     target = M.DQN(obs_dim, [64, 32], 4).to(dev)
     target.load_state_dict(_sd(g, "target_"))
+    aux_model = None
+    if aux:
+        S = netmon.get_state_size()
+        aux_model = M.MLP(S, [S, g["node_aux"].shape[-1]], activation_on_output=False).to(dev)
+        aux_model.load_state_dict(_sd(g, "aux_"))
     L = g["actions"].shape[0]
     f = lambda a: torch.as_tensor(a, device=dev)  # noqa: E731
     batches = []
@@ -42,15 +51,23 @@ def test_update_matches_reference_golden():
             None, f(g["agent_obs"][t]), f(g["actions"][t]).long(), f(g["reward"][t]), f(g["agent_obs"][t + 1]),
             f(g["done"][t]).bool(), f(g["episode_done"][t]).bool(), f(g["node_obs"][t]),
             M.dense_to_nbr(f(g["node_adj"][t])), f(g["node_state0"]), M.node_agent_to_index(f(g["node_agent"][t])),
-            f(g["node_obs"][t + 1]), M.node_agent_to_index(f(g["node_agent"][t + 1]))))
+            f(g["node_obs"][t + 1]), M.node_agent_to_index(f(g["node_agent"][t + 1])),
+            node_aux=f(g["node_aux"][t]) if aux else None))
     params = list(model.parameters()) + list(netmon.parameters())
     names = [f"model_{k}" for k, _ in model.named_parameters()] + [f"netmon_{k}" for k, _ in
                                                                     netmon.named_parameters()]
+    if aux:
+        params += list(aux_model.parameters())
+        names += [f"aux_{k}" for k, _ in aux_model.named_parameters()]
     assert names == list(g["param_names"])
     opt = torch.optim.AdamW(params, lr=float(g["lr"]))
     netmon.train()
     model.train()
-    loss, qs, qts = T.dqn_loss(netmon, model, target, batches, float(g["gamma"]))
+    parts = {}
+    loss, qs, qts = T.dqn_loss(netmon, model, target, batches, float(g["gamma"]), aux_model=aux_model,
+                               aux_coeff=float(g["aux_coeff"]) if aux else 0.0, parts=parts)
+    if aux:
+        np.testing.assert_allclose(parts["loss_aux"].item(), g["loss_aux"].item(), rtol=1e-5, atol=1e-6)
     for t in range(L):
         np.testing.assert_allclose(qs[t].detach().cpu().numpy(), g[f"q_{t}"], atol=1e-5, rtol=0, err_msg=f"q_{t}")
         np.testing.assert_allclose(qts[t].cpu().numpy(), g[f"qtarget_{t}"], atol=1e-5, rtol=0,
