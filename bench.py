@@ -40,6 +40,7 @@ def parse():
     p.add_argument("--n-router", type=int, default=20)
     p.add_argument("--n-data", type=int, default=20)
     p.add_argument("--netmon-iterations", type=int, default=1)
+    p.add_argument("--netmon-rnn-type", default="lstm", choices=["lstm", "lnlstm", "gru"])
     p.add_argument("--no-netmon", action="store_true",
                    help="DQN on the env observation alone (BASELINE config 2: the reference without --netmon)")
     p.add_argument("--episode-steps", type=int, default=50)
@@ -226,7 +227,7 @@ def main():
     net = gm.Network(N, random_topology=bool(args.random_topology), excluded_seeds=gm.EVAL_SEEDS,
                      device=dev.index)
     torch.manual_seed(0)
-    netmon = None if args.no_netmon else M.NetMon(4 * N + 8, 128, [512, 256], K).to(dev)
+    netmon = None if args.no_netmon else M.NetMon(4 * N + 8, 128, [512, 256], K, rnn_type=args.netmon_rnn_type).to(dev)
     dqn = M.DQN(6 * N + 10 + (0 if netmon is None else netmon.get_out_features()), [512, 256], 4).to(dev)
     if netmon is not None:
         M.tag_modules(netmon, "netmon.")
@@ -383,7 +384,7 @@ def main():
             "dtype": "f32 (GEMMs: 3xf16-split MFMA, f32 accumulate)" if x3 else "f32",
             "data": "synthetic: random-init NetMon+DQN weights, on-device random topologies and packets",
             "config": {"workload": ("routing rollout (no NetMon) + " if netmon is None else
-                                    f"routing rollout --netmon (NetMon K={K}, H=128, enc 512,256, lstm, sum) + ") +
+                                    f"routing rollout --netmon (NetMon K={K}, H=128, enc 512,256, {args.netmon_rnn_type}, sum) + ") +
                                    f"DQN 512,256 eps-greedy, {'random' if args.random_topology else 'fixed'} "
                                    f"{N}-node topologies, episode {args.episode_steps} steps",
                        "n_env_per_gpu": B, "n_nodes": N, "n_data": A, "netmon_iterations": K,

@@ -89,6 +89,7 @@ struct Epi {
     float* q;
     long long ldq;
     unsigned* range_flag;     // X3: set to 1 when an accumulator is not finite (host-mapped; nullable)
+    int cell;                 // EPI_LSTM tiles: 0 LSTM (i, f, g, o), 1 GRU (r, z, n_x, n_h; c_in = h)
 };
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const float* p, unsigned bytes) {
@@ -225,6 +226,13 @@ __device__ __forceinline__ void epilogue(floatx16 (&acc)[TM][TN], const Epi& ep,
             for (int r = 0; r < 16; r++) {
                 const int row = rb0 + (r & 3) + 8 * (r >> 2);
                 if (row >= M || unit >= H) continue;
+                if (ep.cell == 1) {  // GRU (torch.nn.GRUCell): the 4th tile is W_hn h, kept apart for r * (.)
+                    const float rg = sigm(acc[i][0][r] + bgate[0]);
+                    const float zg = sigm(acc[i][1][r] + bgate[1]);
+                    const float ng = tanh_fast(acc[i][2][r] + bgate[2] + rg * (acc[i][3][r] + bgate[3]));
+                    ep.y[(long long)row * ep.ldy + unit] = (1.f - zg) * ng + zg * cin.v[i][r];
+                    continue;
+                }
                 float gi = sigm(acc[i][0][r] + bgate[0]);
                 float gf = sigm(acc[i][1][r] + bgate[1]);
                 float gg = tanh_fast(acc[i][2][r] + bgate[2]);
@@ -1320,7 +1328,12 @@ int gemm_entry(bool x3, const gm_a_src* a0, const gm_a_src* a1, const void* w, i
     ep.ldc = ldc;
     ep.act_out = act_out;
     if (x3 && (rc = range_flag(&ep.range_flag))) return rc;
-    if (epilogue == GM_EPI_LSTM) {
+    if (epilogue == GM_EPI_GRU) {  // the LSTM gate-tile kernels with the GRU gate math
+        if (n % 128 || !c_in || act_out)
+            return gm_fail(GM_ERR_INVALID_ARG, std::string(fn) + ": GRU epilogue needs 4H % 128 == 0, c_in = h, no act_out");
+        ep.cell = 1;
+        epilogue = GM_EPI_LSTM;
+    } else if (epilogue == GM_EPI_LSTM) {
         if (n % 128 || !y2 || !c_in) return gm_fail(GM_ERR_INVALID_ARG, std::string(fn) + ": LSTM epilogue needs 4H % 128 == 0");
     } else if (epilogue != GM_EPI_BIAS && epilogue != GM_EPI_BIAS_LEAKY) {
         return gm_fail(GM_ERR_INVALID_ARG, std::string(fn) + ": unknown epilogue");

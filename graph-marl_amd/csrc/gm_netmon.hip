@@ -555,3 +555,131 @@ extern "C" int gm_routing_node_encoder(const float* x, int64_t ldx, const int32_
                            wt, b, n, act, y, (long long)ldy, rows);
     return launched();
 }
+
+// ---------------------------------------------------------------------------
+// LayerNorm-LSTM cell after its two gate GEMMs (reference src/layernormlstm.py:24-42):
+//   g  = LN_in(x W_ih^T) + LN_hid(h W_hh^T) + b_ih      (LN over the 4H gate pre-activations)
+//   c' = LN_cell(sigma(f) c + sigma(i) tanh(g_c)),  h' = sigma(o) tanh(c')   (LN over H)
+// One wave per row, the row's 8H raw products (gi | gh, columns in the original gate order)
+// held in registers: lane l owns units u = l + 64 q (q < UPL) of all four gates, so every load
+// and store is a 64-wide coalesced run and the three LayerNorm statistics are two-pass wave
+// reductions over registers (mean, then the sum of squared deviations, like torch's fp32
+// LayerNorm, eps 1e-5). HBM-bound: 8H floats in, c in, h' and c' out per row.
+// ---------------------------------------------------------------------------
+namespace {
+__device__ __forceinline__ float wsum(float v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    return v;
+}
+// precise expf / tanhf (not the GEMM epilogues' 1e-6 hardware approximations): the cell LayerNorm
+// divides by the spread of c, which would amplify gate errors; the kernel is HBM-bound anyway
+__device__ __forceinline__ float sig_f(float x) { return 1.0f / (1.0f + expf(-x)); }
+__device__ __forceinline__ float tanh_f(float x) { return tanhf(x); }
+
+struct LnLstmP {
+    const float *gi_w, *gi_b, *gh_w, *gh_b, *bias, *lc_w, *lc_b;
+};
+
+template <int UPL>
+__global__ __launch_bounds__(256) void k_lnlstm_pw(const float* __restrict__ G, long long ldg,
+                                                   const float* __restrict__ c_in, long long ldc, LnLstmP p, int M,
+                                                   int H, float eps, float* __restrict__ y, long long ldy,
+                                                   float* __restrict__ y2, long long ldy2) {
+    const int lane = threadIdx.x & 63;
+    const long long row = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (row >= M) return;  // wave-uniform
+    const float* gi = G + row * ldg;
+    const float* gh = gi + 4 * H;
+    float a[UPL][4], b[UPL][4];
+    float si = 0.f, sh = 0.f;
+#pragma unroll
+    for (int q = 0; q < UPL; q++) {
+        const int u = lane + 64 * q;
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const bool ok = u < H;
+            a[q][k] = ok ? gi[k * H + u] : 0.f;
+            b[q][k] = ok ? gh[k * H + u] : 0.f;
+            si += a[q][k];
+            sh += b[q][k];
+        }
+    }
+    const float inv4h = 1.0f / (float)(4 * H);
+    const float mi = wsum(si) * inv4h, mh = wsum(sh) * inv4h;
+    float vi = 0.f, vh = 0.f;
+#pragma unroll
+    for (int q = 0; q < UPL; q++)
+        if (lane + 64 * q < H)
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                const float di = a[q][k] - mi, dh = b[q][k] - mh;
+                vi += di * di;
+                vh += dh * dh;
+            }
+    const float ri = 1.0f / sqrtf(wsum(vi) * inv4h + eps), rh = 1.0f / sqrtf(wsum(vh) * inv4h + eps);
+    float cp[UPL], og[UPL], sc = 0.f;
+#pragma unroll
+    for (int q = 0; q < UPL; q++) {
+        const int u = lane + 64 * q;
+        cp[q] = og[q] = 0.f;
+        if (u >= H) continue;
+        float g[4];
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const int col = k * H + u;
+            g[k] = ((a[q][k] - mi) * ri * p.gi_w[col] + p.gi_b[col]) + ((b[q][k] - mh) * rh * p.gh_w[col] + p.gh_b[col]) +
+                   p.bias[col];
+        }
+        cp[q] = sig_f(g[1]) * c_in[row * ldc + u] + sig_f(g[0]) * tanh_f(g[2]);
+        og[q] = sig_f(g[3]);
+        sc += cp[q];
+    }
+    const float invh = 1.0f / (float)H;
+    const float mc = wsum(sc) * invh;
+    float vc = 0.f;
+#pragma unroll
+    for (int q = 0; q < UPL; q++)
+        if (lane + 64 * q < H) {
+            const float d = cp[q] - mc;
+            vc += d * d;
+        }
+    const float rc = 1.0f / sqrtf(wsum(vc) * invh + eps);
+#pragma unroll
+    for (int q = 0; q < UPL; q++) {
+        const int u = lane + 64 * q;
+        if (u >= H) continue;
+        const float cn = (cp[q] - mc) * rc * p.lc_w[u] + p.lc_b[u];
+        y[row * ldy + u] = og[q] * tanh_f(cn);
+        y2[row * ldy2 + u] = cn;
+    }
+}
+}  // namespace
+
+extern "C" int gm_lnlstm_pointwise(const float* g, int64_t ldg, const float* c, int64_t ldc, const float* ln_in_w,
+                                   const float* ln_in_b, const float* ln_hid_w, const float* ln_hid_b,
+                                   const float* bias, const float* ln_cell_w, const float* ln_cell_b, int32_t m,
+                                   int32_t H, float eps, float* h1, int64_t ldh, float* c1, int64_t ldc1,
+                                   void* stream) {
+    if (!g || !c || !h1 || !c1 || !ln_in_w || !ln_in_b || !ln_hid_w || !ln_hid_b || !bias || !ln_cell_w ||
+        !ln_cell_b || m <= 0 || H <= 0 || H > 512 || ldg < 8 * (int64_t)H || ldc < H || ldh < H || ldc1 < H)
+        return gm_fail(GM_ERR_INVALID_ARG, "gm_lnlstm_pointwise: bad arguments (H <= 512, ldg >= 8H)");
+    LnLstmP p{ln_in_w, ln_in_b, ln_hid_w, ln_hid_b, bias, ln_cell_w, ln_cell_b};
+    const dim3 grid((m + 3) / 4), blk(256);
+    hipStream_t st = (hipStream_t)stream;
+#define GM_LN(U) \
+    hipLaunchKernelGGL(k_lnlstm_pw<U>, grid, blk, 0, st, g, (long long)ldg, c, (long long)ldc, p, m, H, eps, h1, \
+                       (long long)ldh, c1, (long long)ldc1)
+    if (H <= 64)
+        GM_LN(1);
+    else if (H <= 128)
+        GM_LN(2);
+    else if (H <= 256)
+        GM_LN(4);
+    else
+        GM_LN(8);
+#undef GM_LN
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return gm_fail(GM_ERR_HIP, std::string("gm_lnlstm_pointwise: ") + hipGetErrorString(e));
+    return GM_OK;
+}

@@ -21,7 +21,7 @@ import torch.nn.functional as F
 from . import _lib as L
 
 GM_A_DENSE, GM_A_AGGREGATE, GM_A_READOUT = 0, 1, 2
-GM_EPI_BIAS, GM_EPI_BIAS_LEAKY, GM_EPI_LSTM = 0, 1, 2
+GM_EPI_BIAS, GM_EPI_BIAS_LEAKY, GM_EPI_LSTM, GM_EPI_GRU = 0, 1, 2, 3
 
 # LSTM update cell: a strided aggregate pass (gm_mp_aggregate_rows, 26-29 us at 81920 nodes) +
 # the cell on dense [Σ h | h] (103-111 us) instead of the AGGREGATE A source inside the GEMM
@@ -162,6 +162,58 @@ def pack_lstm(cell):
     return cell._packed.get(_key(cell.weight_ih, cell.weight_hh, cell.bias_ih, cell.bias_hh) + (L.GEMM_MODE,), build)
 
 
+def _interleave(w, b, H):
+    """Rows of a gate-major [4H, K] matrix (gates g = 0..3 of H rows) in the gate-tile order of the
+    LSTM/GRU epilogues: row 128t + 32g + u holds gate g of unit 32t + u."""
+    t = torch.arange(H // 32, device=w.device)
+    g = torch.arange(4, device=w.device)
+    u = torch.arange(32, device=w.device)
+    orig = (g[None, :, None] * H + 32 * t[:, None, None] + u[None, None, :]).reshape(-1)
+    return w[orig], b[orig]
+
+
+def pack_gru(cell):
+    """torch.nn.GRUCell (r, z, n) as four gate tiles on A = [x | h] for GM_EPI_GRU: r and z rows
+    [W_ih | W_hh], n_x rows [W_in | 0], n_h rows [0 | W_hn] (W_hn h stays apart for r * (W_hn h +
+    b_hn)); biases b_ir + b_hr, b_iz + b_hz, b_in, b_hn."""
+    if not hasattr(cell, "_packed"):
+        cell._packed = Packed()
+
+    def build():
+        with torch.no_grad():
+            H = cell.hidden_size
+            assert H % 32 == 0, "fused GRU needs H % 32 == 0"
+            wi, wh, bi, bh = cell.weight_ih, cell.weight_hh, cell.bias_ih, cell.bias_hh
+            z = torch.zeros(H, H, device=wi.device)
+            w = torch.cat([torch.cat([wi[:2 * H], wh[:2 * H]], 1), torch.cat([wi[2 * H:], z], 1),
+                           torch.cat([z, wh[2 * H:]], 1)], 0)
+            b = torch.cat([bi[:2 * H] + bh[:2 * H], bi[2 * H:], bh[2 * H:]])
+            w, b = _interleave(w, b, H)
+            wp, ldw = _pad_cols(w)
+            x3 = X3(wp, ldw, 4 * H, 2 * H) if use_x3(4 * H) else None
+            return wp, ldw, b.contiguous(), x3
+
+    return cell._packed.get(_key(cell.weight_ih, cell.weight_hh, cell.bias_ih, cell.bias_hh) + (L.GEMM_MODE,), build)
+
+
+def pack_lnlstm(cell):
+    """LayerNormLSTMCell: W_ih and W_hh as two separate GEMM weights (each product gets its own
+    LayerNorm before they are summed), split-f16 packs when that form runs."""
+    if not hasattr(cell, "_packed"):
+        cell._packed = Packed()
+
+    def build():
+        with torch.no_grad():
+            H = cell.hidden_size
+            out = []
+            for w in (cell.weight_ih, cell.weight_hh):
+                wp, ldw = _pad_cols(w)
+                out.append((wp, ldw, X3(wp, ldw, 4 * H, w.shape[1]) if use_x3(4 * H) else None))
+            return out
+
+    return cell._packed.get(_key(cell.weight_ih, cell.weight_hh) + (L.GEMM_MODE,), build)
+
+
 def pack_dqn_first(lin, obs_dim):
     """W1 columns reordered to [graph part | env obs part] to match A = [readout | env obs]."""
     if not hasattr(lin, "_packed_first"):
@@ -294,16 +346,58 @@ def routing_encoder(lin, x, nbr, G, N, out):
     return out
 
 
+def _cell_step(netmon, cell, x_src, h_ptr, ldh, c_ptr, ldc, S, M, tag_kind):
+    """One NetMon RNN cell on A = [x_src | h] writing the new state rows S ([h | c] for the
+    LSTMs, h for GRU): lstm / gru one gate-tile GEMM with the gate math in its epilogue; lnlstm
+    two GEMMs (x W_ih^T, h W_hh^T) + gm_lnlstm_pointwise (the LayerNorms need whole rows)."""
+    H = netmon.hidden_features
+    SW = S.stride(0)
+    rnn = netmon.rnn_type
+    ctag = getattr(cell, "tag", None)
+    tag = ctag and f"{tag_kind}:{ctag}:{M}x{4 * H}x{2 * H}"
+    if rnn == "lstm":
+        wp, ldw, bp, x3 = pack_lstm(cell)
+        gemm(x_src, dense(h_ptr, ldh, H), wp.data_ptr(), ldw, bp.data_ptr(), M, 4 * H, GM_EPI_LSTM, S.data_ptr(), SW,
+             S.data_ptr() + 4 * H, SW, c_ptr, ldc, tag=tag, x3=x3)
+    elif rnn == "gru":
+        wp, ldw, bp, x3 = pack_gru(cell)
+        gemm(x_src, dense(h_ptr, ldh, H), wp.data_ptr(), ldw, bp.data_ptr(), M, 4 * H, GM_EPI_GRU, S.data_ptr(), SW,
+             c_in=h_ptr, ldc=ldh, tag=tag, x3=x3)
+    elif rnn == "lnlstm":
+        (wi, ldi, xi), (wh, ldhw, xh) = pack_lnlstm(cell)
+        G = torch.empty(M, 8 * H, device=S.device)  # stream-ordered allocator: safe across stream groups
+        with L.timed(tag):
+            gemm(x_src, None, wi.data_ptr(), ldi, None, M, 4 * H, GM_EPI_BIAS, G.data_ptr(), 8 * H, x3=xi)
+            gemm(dense(h_ptr, ldh, H), None, wh.data_ptr(), ldhw, None, M, 4 * H, GM_EPI_BIAS, G.data_ptr() + 16 * H,
+                 8 * H, x3=xh)
+            li, lh, lc = cell.ln_input, cell.ln_hidden, cell.ln_cell
+            L.check(L.lib().gm_lnlstm_pointwise(G.data_ptr(), 8 * H, c_ptr, ldc, li.weight.data_ptr(), li.bias.data_ptr(),
+                                                lh.weight.data_ptr(), lh.bias.data_ptr(), cell.bias_ih.data_ptr(),
+                                                lc.weight.data_ptr(), lc.bias.data_ptr(), M, H, float(li.eps),
+                                                S.data_ptr(), SW, S.data_ptr() + 4 * H, SW, L.stream_ptr()))
+    else:
+        raise NotImplementedError(f"fused NetMon step: rnn_type {rnn!r}")
+
+
+def fused_ok(netmon):
+    """The fused no-grad NetMon step covers lstm / lnlstm / gru with state carry-over and the
+    neighbour readout (the reference's NetMonWrapper configuration on routing graphs)."""
+    return (netmon.rnn_type in ("lstm", "lnlstm", "gru") and netmon.rnn_carryover and netmon.output_neighbor_hidden
+            and not netmon.output_global_hidden and netmon.hidden_features % 32 == 0)
+
+
 @torch.no_grad()
 def netmon_step(netmon, node_obs, nbr, state, out=None, last_out=None):
     """One NetMon step for B graphs. node_obs [B, N, F]; nbr int32 [B, N, deg]; state
-    [B, N, 2H] or None. Returns (new state [B, N, 2H], h_prev rows [B*N, 2H] whose first
-    H columns are the last pre-aggregation h). out / last_out ([B*N, 2H], optional) receive
-    the new state and h_prev, so a caller can keep them in fixed buffers (graph replay)."""
-    if netmon.rnn_type != "lstm":
-        raise NotImplementedError("fused NetMon step: lstm only (lnlstm/gru use NetMon.forward_graph)")
+    [B, N, S] (S = 2H [h | c] for lstm / lnlstm, H for gru) or None. Returns (new state
+    [B, N, S], h_prev rows [B*N, S] whose first H columns are the last pre-aggregation h).
+    out / last_out ([B*N, S], optional) receive the new state and h_prev, so a caller can keep
+    them in fixed buffers (graph replay)."""
+    if not fused_ok(netmon):
+        raise NotImplementedError("fused NetMon step: lstm / lnlstm / gru with carry-over (else NetMon.forward_graph)")
     B, N, Fd = node_obs.shape
     H = netmon.hidden_features
+    SW = netmon.state_size
     M = B * N
     dev = node_obs.device
     x = node_obs.reshape(M, Fd)
@@ -314,59 +408,56 @@ def netmon_step(netmon, node_obs, nbr, state, out=None, last_out=None):
     for lin in layers:
         x = _linear(x, x.stride(0), x.shape[1], lin, torch.empty(M, lin.out_features, device=dev))
     if state is None:
-        state = torch.zeros(B, N, 2 * H, device=dev)
-    st = state.reshape(M, 2 * H)
-    wp, ldw, bp, x3 = pack_lstm(netmon.rnn_obs)
+        state = torch.zeros(B, N, SW, device=dev)
+    st = state.reshape(M, SW)
     K = netmon.iterations
+    cstate = SW > H  # LSTMs carry c in the second half of the row
 
     def buf(i):  # storage of S_i (S_0 = obs cell output, S_K = new state, S_{K-1} = h_prev)
         if i == K and out is not None:
-            return out.reshape(M, 2 * H)
+            return out.reshape(M, SW)
         if i == K - 1 and last_out is not None:
-            return last_out.reshape(M, 2 * H)
-        return torch.empty(M, 2 * H, device=dev)
+            return last_out.reshape(M, SW)
+        return torch.empty(M, SW, device=dev)
 
     S = buf(0)
-    gemm(dense(x.data_ptr(), x.stride(0), H), dense(st.data_ptr(), 2 * H, H), wp.data_ptr(), ldw, bp.data_ptr(),
-         M, 4 * H, GM_EPI_LSTM, S.data_ptr(), 2 * H, S[:, H:].data_ptr(), 2 * H, st[:, H:].data_ptr(), 2 * H,
-         tag=netmon.rnn_obs.tag and f"lstm:{netmon.rnn_obs.tag}:{M}x{4 * H}x{2 * H}", x3=x3)
-    wu, ldu, bu, xu = pack_lstm(netmon.rnn_update)
+    _cell_step(netmon, netmon.rnn_obs, dense(x.data_ptr(), x.stride(0), H), st.data_ptr(), SW,
+               st.data_ptr() + 4 * H if cstate else None, SW, S, M, "lstm")
     last = S
     mean = netmon.agg_mode == 1
     agg = torch.empty(M, H, device=dev) if PRE_AGG else None
-    for it in range(netmon.iterations):
+    for it in range(K):
         last = S
         S2 = buf(it + 1)
         if PRE_AGG:  # aggregate pass, then the update cell on dense [Σ h | h]
             with L.timed(f"mp_aggregate:{M}x{H}"):
-                L.check(L.lib().gm_mp_aggregate_rows(S.data_ptr(), 2 * H, nbr.data_ptr(), B, N, nbr.shape[-1], H,
+                L.check(L.lib().gm_mp_aggregate_rows(S.data_ptr(), SW, nbr.data_ptr(), B, N, nbr.shape[-1], H,
                                                      int(mean), agg.data_ptr(), H, L.stream_ptr()))
             a_src = dense(agg.data_ptr(), H, H)
         else:
-            a_src = aggregate(S.data_ptr(), 2 * H, H, nbr, N, mean)
-        gemm(a_src, dense(S.data_ptr(), 2 * H, H), wu.data_ptr(), ldu,
-             bu.data_ptr(), M, 4 * H, GM_EPI_LSTM, S2.data_ptr(), 2 * H, S2[:, H:].data_ptr(), 2 * H,
-             S[:, H:].data_ptr(), 2 * H,
-             tag=netmon.rnn_update.tag and f"lstm_agg:{netmon.rnn_update.tag}:{M}x{4 * H}x{2 * H}", x3=xu)
+            a_src = aggregate(S.data_ptr(), SW, H, nbr, N, mean)
+        _cell_step(netmon, netmon.rnn_update, a_src, S.data_ptr(), SW, S.data_ptr() + 4 * H if cstate else None, SW,
+                   S2, M, "lstm_agg")
         S = S2
-    if netmon.iterations <= 0:
+    if K <= 0:
         last = torch.zeros_like(S)
-    netmon.state = S.view(B, N, 2 * H)
+    netmon.state = S.view(B, N, SW)
     return netmon.state, last
 
 
 @torch.no_grad()
-def dqn_q(dqn, env_obs, obs_dim, state, h_prev, nbr, agent_node, scratch):
+def dqn_q(dqn, env_obs, obs_dim, state, h_prev, nbr, agent_node, scratch, hidden=None):
     """Q [B*A, actions] of the DQN on [env obs | NetMon readout] with the readout gathered
-    inside the first GEMM. env_obs: [B, A, stride] (first obs_dim columns used)."""
+    inside the first GEMM. env_obs: [B, A, stride] (first obs_dim columns used); state rows
+    [h | ...] of width state.shape[-1] (hidden H: default half the width, the LSTM layout)."""
     B, A, stride = env_obs.shape
     N = nbr.shape[1]
-    H = state.shape[-1] // 2
+    H = hidden or state.shape[-1] // 2
     M = B * A
     lin0 = dqn.encoder.linear_layers[0]
     wp, ldw, b, x3 = pack_dqn_first(lin0, obs_dim)
     h1 = scratch(0, M, lin0.out_features)
-    a0 = readout(state.data_ptr(), 2 * H, h_prev.data_ptr(), h_prev.stride(0), nbr, agent_node, N, H)
+    a0 = readout(state.data_ptr(), state.shape[-1], h_prev.data_ptr(), h_prev.stride(0), nbr, agent_node, N, H)
     gemm(a0, dense(env_obs.data_ptr(), stride, obs_dim), wp.data_ptr(), ldw, b.data_ptr(), M, lin0.out_features,
          GM_EPI_BIAS_LEAKY if lin0.act == 1 else GM_EPI_BIAS, h1.data_ptr(), h1.stride(0),
          tag=lin0.tag and f"linear:{lin0.tag}:{M}x{lin0.out_features}x{a0.k + obs_dim}", x3=x3)

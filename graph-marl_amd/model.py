@@ -689,7 +689,7 @@ class DQN(nn.Module):
 def tag_modules(root, prefix=""):
     """Name every Linear/LSTMCell by its module path (kernel timer tags)."""
     for name, m in root.named_modules():
-        if isinstance(m, (Linear, LSTMCell)):
+        if isinstance(m, (Linear, LSTMCell, LayerNormLSTMCell, GRUCell)):
             m.tag = prefix + name
 
 

@@ -74,7 +74,7 @@ class EpsilonGreedy:
             return self(wenv.obs)
         e = wenv.env
         q = FU.dqn_q(self._model, e.obs_buf, e.obs_dim, wenv.current_netmon_state, wenv.h_prev, e.nbr,
-                     e.agent_node, self._buf)
+                     e.agent_node, self._buf, hidden=wenv.netmon.hidden_features)
         actions = self.select(q.view(e.n_env, e.n_data, -1))
         self._decay_step()
         return actions

@@ -81,11 +81,10 @@ def attention_kl(att_weights, tar_att_weights, done):
 def _fused_target_ok(netmon, model_tar):
     """The no-grad target pass can run the rollout's fused kernels (fused.netmon_step +
     fused.dqn_q) under the same conditions as a fused NetMonWrapper with a DQN."""
+    from . import fused as FU
     from .model import DQN
 
-    return (netmon is not None and isinstance(model_tar, DQN) and netmon.rnn_type == "lstm"
-            and netmon.rnn_carryover and netmon.output_neighbor_hidden and not netmon.output_global_hidden
-            and netmon.hidden_features % 32 == 0)
+    return netmon is not None and isinstance(model_tar, DQN) and FU.fused_ok(netmon)
 
 
 @torch.no_grad()
@@ -102,7 +101,7 @@ def _fused_next_q(netmon, model_tar, batch):
                                    netmon.state.detach().contiguous())
     dev = env_obs.device
     q = FU.dqn_q(model_tar, env_obs, od, state, h_prev, batch.nbr.contiguous(), batch.next_agent_node.contiguous(),
-                 lambda i, m, n: torch.empty(m, n, device=dev))
+                 lambda i, m, n: torch.empty(m, n, device=dev), hidden=netmon.hidden_features)
     return q.view(B, A, -1)
 
 

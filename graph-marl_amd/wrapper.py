@@ -2,8 +2,9 @@
 src/env/wrapper.py:7-109 NetMonWrapper).
 
 After every env step one NetMon step runs on the device over all n_env graphs.
-Fused mode (lstm NetMon, default): the step is three encoder GEMMs plus one GEMM per LSTM
-cell with the aggregate and gate math fused (fused.netmon_step); the graph part of the joint
+Fused mode (lstm / lnlstm / gru NetMon with carry-over, default): the step is three encoder
+GEMMs plus the RNN cells on the HIP kernels (fused.netmon_step: lstm / gru one gate-tile GEMM
+with the gate math in its epilogue, lnlstm two GEMMs + the LayerNorm-LSTM pointwise kernel); the graph part of the joint
 observation is NOT materialised — the DQN gathers it inside its first GEMM
 (policy.EpsilonGreedy.act). Reading `.obs` (the reference API) materialises the joint
 observation [env obs | readout] on demand. Unfused mode runs NetMon.forward_graph and writes
@@ -35,8 +36,7 @@ class NetMonWrapper:
         self.h_prev = None
         self.obs_dim = need
         if fused is None:
-            fused = (netmon.rnn_type == "lstm" and netmon.rnn_carryover and netmon.output_neighbor_hidden
-                     and not netmon.output_global_hidden and H % 32 == 0)
+            fused = FU.fused_ok(netmon)
         self.fused = fused
         self._dirty = False
         # fused mode: the state and h_prev alternate between two fixed buffer pairs, so a
@@ -72,7 +72,7 @@ class NetMonWrapper:
         with torch.no_grad():
             self.last_netmon_state = self.current_netmon_state
             if self.fused:
-                B, N, H2 = e.n_env, e.n_nodes, 2 * self.netmon.hidden_features
+                B, N, H2 = e.n_env, e.n_nodes, self.netmon.get_state_size()
                 if self._bufs is None:
                     self._bufs = [(torch.empty(B, N, H2, device=e.device), torch.empty(B * N, H2, device=e.device))
                                   for _ in range(2)]

@@ -187,6 +187,15 @@ int gm_mp_aggregate(const float* h, const int32_t* nbr, int32_t n_graphs, int32_
  * [h | c] state rows in place of the GEMM's AGGREGATE A source. */
 int gm_mp_aggregate_rows(const float* h, int64_t ldh, const int32_t* nbr, int32_t n_graphs, int32_t n_nodes,
                          int32_t deg, int32_t hidden, int32_t mode, float* out, int64_t ldo, void* stream);
+/* LayerNorm-LSTM cell after its gate GEMMs (src/layernormlstm.py:24-42, NetMon rnn_type lnlstm):
+ * g rows [m][ldg] hold [x W_ih^T | h W_hh^T] (8H floats, gate order i, f, g, o, no bias);
+ * gates = LN(gi; ln_in_w, ln_in_b) + LN(gh; ln_hid_w, ln_hid_b) + bias, c1 = LN(sigma(f) c +
+ * sigma(i) tanh(g); ln_cell_w, ln_cell_b), h1 = sigma(o) tanh(c1); LayerNorm eps as given
+ * (torch default 1e-5). H <= 512; c, h1, c1 strided rows. */
+int gm_lnlstm_pointwise(const float* g, int64_t ldg, const float* c, int64_t ldc, const float* ln_in_w,
+                        const float* ln_in_b, const float* ln_hid_w, const float* ln_hid_b, const float* bias,
+                        const float* ln_cell_w, const float* ln_cell_b, int32_t m, int32_t H, float eps, float* h1,
+                        int64_t ldh, float* c1, int64_t ldc1, void* stream);
 /* Backward of a Linear followed by leaky_relu (MLP layers, src/model.py:13-42): g = dY where
  * Y >= 0 else slope * dY ([rows][cols] contiguous), and per-block column sums of g for the bias
  * gradient: part[ceil(rows / rows_per_block)][cols] (the caller sums the blocks); g_scale
@@ -226,7 +235,7 @@ int gm_linear_f32(const float* x, int64_t ldx, const float* w, int64_t ldw, cons
  * LSTMCell gate GEMM (src/model.py:379-382) with the aggregate (206-229) and the readout +
  * agent gather (582-631) folded into the A-operand load. */
 enum { GM_A_DENSE = 0, GM_A_AGGREGATE = 1, GM_A_READOUT = 2 };
-enum { GM_EPI_BIAS = 0, GM_EPI_BIAS_LEAKY = 1, GM_EPI_LSTM = 2 };
+enum { GM_EPI_BIAS = 0, GM_EPI_BIAS_LEAKY = 1, GM_EPI_LSTM = 2, GM_EPI_GRU = 3 };
 typedef struct {
     int32_t mode;              /* GM_A_*                                                           */
     const float* p0;           /* DENSE: rows; AGGREGATE: node rows h; READOUT: h_final node rows  */
@@ -245,7 +254,11 @@ typedef struct {
 /* src1 (nullable) must be DENSE and src0->k a multiple of 32. W: [n][ldw] (ldw >= K, zero
  * padded to a multiple of 4). GM_EPI_LSTM: W rows packed so that rows [128t, 128t+128) are
  * gates i,f,g,o (32 rows each) of hidden units [32t, 32t+32); n = 4H; writes h' to y, c' to y2,
- * reads c from c_in, optional activations [M][4H] (original gate order) to act_out. */
+ * reads c from c_in, optional activations [M][4H] (original gate order) to act_out.
+ * GM_EPI_GRU (torch.nn.GRUCell, reference NetMon rnn_type gru, src/model.py:387-389): A = [x | h],
+ * n = 4H with rows [128t, 128t+128) = tiles r, z, n_x, n_h of hidden units [32t, 32t+32) where
+ * r, z rows are [W_ih | W_hh], n_x rows [W_in | 0], n_h rows [0 | W_hn] (biases b_ir + b_hr,
+ * b_iz + b_hz, b_in, b_hn); c_in = h; y = h' = (1 - z) n + z h with n = tanh(n_x + r n_h); y2 unused. */
 int gm_gemm_f32(const gm_a_src* src0, const gm_a_src* src1, const float* w, int64_t ldw, const float* b, int32_t m,
                 int32_t n, int32_t epilogue, float* y, int64_t ldy, float* y2, int64_t ldy2, const float* c_in,
                 int64_t ldc, float* act_out, void* stream);

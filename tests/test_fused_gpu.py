@@ -86,20 +86,29 @@ def test_gemm_two_sources_and_lstm_epilogue(form, monkeypatch):
     torch.testing.assert_close(S[:, H:], rc, atol=1e-5, rtol=0)
 
 
-def _setup_env(gm, W, M, B=64, seed=5, fused=True):
+def _setup_env(gm, W, M, B=64, seed=5, fused=True, rnn="lstm", K=1):
     N, A = 20, 20
     env = gm.Routing(gm.Network(N, random_topology=True, excluded_seeds=gm.EVAL_SEEDS), A, n_env=B, seed=seed,
                      obs_extra=512, agent_adjacency=False)
     torch.manual_seed(1)
-    nm = M.NetMon(4 * N + 8, 128, [512, 256], 1).cuda()
+    nm = M.NetMon(4 * N + 8, 128, [512, 256], K, rnn_type=rnn).cuda()
     return env, nm, W.NetMonWrapper(env, nm, 1, fused=fused)
 
 
-def test_fused_rollout_matches_unfused_path():
+@pytest.mark.parametrize("rnn,K", [("lstm", 1), ("lnlstm", 1), ("gru", 2)])
+def test_fused_rollout_matches_unfused_path(rnn, K):
+    """Fused rollout (readout gathered in the DQN GEMM; lstm / gru gate math in the GEMM epilogue;
+    lnlstm GEMMs + the LayerNorm-LSTM pointwise kernel) == NetMon.forward_graph + joint obs."""
     gm, M, FU, W = mods()
     P = importlib.import_module("graph-marl_amd.policy")
-    e1, nm1, w1 = _setup_env(gm, W, M, fused=True)
-    e2, nm2, w2 = _setup_env(gm, W, M, fused=False)
+    e1, nm1, w1 = _setup_env(gm, W, M, fused=True, rnn=rnn, K=K)
+    e2, nm2, w2 = _setup_env(gm, W, M, fused=False, rnn=rnn, K=K)
+    assert w1.fused
+    # lnlstm: the cell LayerNorm divides by the spread of c, so both fp32 paths sit ~4e-6 from an
+    # fp64 evaluation per step already with exact f32 GEMMs (tools/diag_lnlstm.py); after 6
+    # carried steps they differ by up to ~1.2e-5 from each other. The 1e-5 contract against the
+    # reference holds per step (test_fused_netmon_vs_reference_golden, lnlstm variants).
+    tol = 3e-5 if rnn == "lnlstm" else 1e-5
     torch.manual_seed(2)
     dqn = M.DQN(e1.obs_dim + 512, [512, 256], 4).cuda()
     p1 = P.EpsilonGreedy(w1, dqn, epsilon=0.5, epsilon_decay=1.0, step_before_train=0)
@@ -108,21 +117,23 @@ def test_fused_rollout_matches_unfused_path():
     w2.reset()
     for t in range(6):
         q1 = FU.dqn_q(dqn, e1.obs_buf, e1.obs_dim, w1.current_netmon_state, w1.h_prev, e1.nbr, e1.agent_node,
-                      p1._buf).view(e1.n_env, e1.n_data, -1).clone()
+                      p1._buf, hidden=128).view(e1.n_env, e1.n_data, -1).clone()
         q2 = p2.q_values(w2.obs)
-        torch.testing.assert_close(q1, q2, atol=1e-5, rtol=0)
+        torch.testing.assert_close(q1, q2, atol=tol, rtol=0)
         a1 = p1.select(q1).clone()
         a2 = p2.select(q2).clone()
         # identical draws; argmax may only differ on exact near-ties
         assert (a1 != a2).float().mean().item() < 1e-3
         w1.step_(a2)
         w2.step_(a2)
-        torch.testing.assert_close(w1.current_netmon_state, w2.current_netmon_state, atol=1e-5, rtol=0)
-        torch.testing.assert_close(w1.obs, w2.obs, atol=1e-5, rtol=0)
+        torch.testing.assert_close(w1.current_netmon_state, w2.current_netmon_state, atol=tol, rtol=0)
+        torch.testing.assert_close(w1.obs, w2.obs, atol=tol, rtol=0)
 
 
-@pytest.mark.parametrize("vi", [0, 1, 2])
+@pytest.mark.parametrize("vi", [0, 1, 2, 3, 4, 5])
 def test_fused_netmon_vs_reference_golden(vi):
+    """Every carry-over variant of tests/golden/netmon.npz (lstm sum/mean K=1..3, lnlstm sum/mean,
+    gru) through the fused step vs the reference's states and readouts over 3 carried steps."""
     gm, M, FU, W = mods()
     g = np.load(f"{R.GOLDEN}/netmon.npz")
     rnn, agg, K, H, enc = g["variants"][vi].split("|")
@@ -139,6 +150,7 @@ def test_fused_netmon_vs_reference_golden(vi):
         np.testing.assert_allclose(state.cpu().numpy(), g[f"v{vi}_state_{t}"], atol=1e-5, rtol=0)
         B, N = x.shape[:2]
         Hh = int(H)
+        hprev = hprev.reshape(B * N, -1)
         out = M.netmon_readout(state.reshape(B * N, -1)[:, :Hh].contiguous(), hprev[:, :Hh].contiguous(), nbr, an)
         np.testing.assert_allclose(out.view(B, -1, 4 * Hh).cpu().numpy(), g[f"v{vi}_mapped_{t}"], atol=1e-5, rtol=0)
 
@@ -187,7 +199,8 @@ def test_gemm_lds_dma_tiles(tile):
         try:
             test_gemm_two_sources_and_lstm_epilogue("x3", MP())
             FU.L.GEMM_MODE = "x3"
-            test_fused_rollout_matches_unfused_path()
+            test_fused_rollout_matches_unfused_path("lstm", 1)
+            test_fused_rollout_matches_unfused_path("gru", 2)
         finally:
             FU.L.GEMM_MODE = old
     finally:
@@ -432,3 +445,32 @@ def test_gemm_x3_range_guard(m, n, k, epi):
     assert L.range_status(clear=True) == 1
     run(x)
     assert L.range_status() == 0
+
+
+@pytest.mark.parametrize("rows,H", [(4096, 128), (1000, 32), (333, 96), (2048, 256)])
+def test_lnlstm_pointwise_vs_torch(rows, H):
+    """gm_lnlstm_pointwise == the reference's LayerNormLSTMCell arithmetic after its two GEMMs
+    (src/layernormlstm.py:24-42) in fp64 torch, on strided c / h' / c' rows."""
+    gm, M, FU, W = mods()
+    L = gm._lib
+    torch.manual_seed(H)
+    G = torch.randn(rows, 8 * H, device="cuda") * 3 + 0.5
+    st = torch.randn(rows, 3 * H, device="cuda")
+    c = st[:, H:2 * H]
+    p = [torch.randn(4 * H, device="cuda") * s + o for s, o in ((0.2, 1), (0.1, 0), (0.2, 1), (0.1, 0), (0.3, 0))]
+    lc = [torch.randn(H, device="cuda") * 0.2 + 1, torch.randn(H, device="cuda") * 0.1]
+    out = torch.zeros(rows, 3 * H, device="cuda")
+    L.check(L.lib().gm_lnlstm_pointwise(G.data_ptr(), 8 * H, c.data_ptr(), 3 * H, *[t.data_ptr() for t in p],
+                                        lc[0].data_ptr(), lc[1].data_ptr(), rows, H, 1e-5, out.data_ptr(), 3 * H,
+                                        out[:, H:].data_ptr(), 3 * H, L.stream_ptr()))
+    d = lambda t: t.double()  # noqa: E731
+    gi = F.layer_norm(d(G[:, :4 * H]), (4 * H,), d(p[0]), d(p[1]))
+    gh = F.layer_norm(d(G[:, 4 * H:]), (4 * H,), d(p[2]), d(p[3]))
+    g = gi + gh + d(p[4])
+    i, f, gg, o = torch.sigmoid(g[:, :H]), torch.sigmoid(g[:, H:2 * H]), torch.tanh(g[:, 2 * H:3 * H]), \
+        torch.sigmoid(g[:, 3 * H:])
+    cy = F.layer_norm(f * d(c) + i * gg, (H,), d(lc[0]), d(lc[1]))
+    hy = o * torch.tanh(cy)
+    torch.testing.assert_close(out[:, :H].double(), hy, atol=2e-6, rtol=0)
+    torch.testing.assert_close(out[:, H:2 * H].double(), cy, atol=4e-6, rtol=0)
+    assert (out[:, 2 * H:] == 0).all()
