@@ -434,7 +434,8 @@ def main(argv=None):
             loss, qs, qts = T.dqn_update(netmon, model, model_tar, optimizer, params, batches, args.gamma, args.tau,
                                          args.target_update_steps, iteration,
                                          att_coeff=args.att_regularization_coeff if args.model == "dgn" else 0.0,
-                                         aux_model=aux_model, aux_coeff=args.aux_loss_coeff, parts=parts)
+                                         aux_model=aux_model, aux_coeff=args.aux_loss_coeff, parts=parts,
+                                         consecutive=True)  # replay sequences: the target pass reuses online steps
             model.eval()
             if netmon is not None:
                 netmon.eval()

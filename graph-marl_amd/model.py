@@ -207,35 +207,64 @@ class LinearFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, gy):
         x2, w, y = ctx.saved_tensors
-        gy = gy.reshape(-1, w.shape[0])
-        gb = None
-        sc = None
-        if ctx.act == 1:
-            if gy.is_contiguous() and y.is_contiguous() and gy.shape[0] >= 4096:
-                # leaky_relu backward + per-block bias-gradient partial sums + max|g| (the
-                # gradient GEMMs' operand scale) in one pass
-                rows, cols = gy.shape
-                rpb = 64
-                g2 = torch.empty_like(gy)
-                part = torch.empty((rows + rpb - 1) // rpb, cols, device=gy.device)
-                sc = torch.empty(1, device=gy.device)
-                L.check(L.lib().gm_leaky_bwd(gy.data_ptr(), y.data_ptr(), rows, cols, 0.01, g2.data_ptr(),
-                                             part.data_ptr(), rpb, sc.data_ptr(), _s()))
-                gy = g2
-                if ctx.needs_input_grad[2]:
-                    gb = part.sum(0)
-            else:
-                gy = torch.where(y >= 0, gy, 0.01 * gy)
-        if sc is None and ctx.needs_input_grad[0] and ctx.needs_input_grad[1] and gy.is_contiguous() \
-                and gy.shape[0] >= 4096:
-            sc = _gy_scale(gy)  # one scale for both gradient GEMMs
-        gx = _dgrad(gy, w, ctx.wcache, sc) if ctx.needs_input_grad[0] else None
-        gw = _wgrad(gy, x2, w.shape[1], sc, ctx.xs) if ctx.needs_input_grad[1] else None
-        if gb is None and ctx.needs_input_grad[2]:
-            gb = gy.sum(0)
+        gx, gw, gb = _linear_backward(ctx, gy, x2, w, y, *ctx.needs_input_grad[:3])
         if gx is not None:
             gx = gx.reshape(*ctx.saved_tensors[0].shape[:-1], w.shape[1])
         return gx, gw, gb, None, None, None
+
+
+def _linear_backward(ctx, gy, x2, w, y, need_x, need_w, need_b):
+    """Gradients of y = act(x2 @ w^T + b) (ctx.act, ctx.wcache, ctx.xs = published max|x| scale
+    or None): fused leaky backward + bias partials + max|g|, then the split-f16 input- and
+    weight-gradient GEMMs sharing one gradient scale."""
+    gy = gy.reshape(-1, w.shape[0])
+    gb = None
+    sc = None
+    if ctx.act == 1:
+        if gy.is_contiguous() and y.is_contiguous() and gy.shape[0] >= 4096:
+            # leaky_relu backward + per-block bias-gradient partial sums + max|g| (the
+            # gradient GEMMs' operand scale) in one pass
+            rows, cols = gy.shape
+            rpb = 64
+            g2 = torch.empty_like(gy)
+            part = torch.empty((rows + rpb - 1) // rpb, cols, device=gy.device)
+            sc = torch.empty(1, device=gy.device)
+            L.check(L.lib().gm_leaky_bwd(gy.data_ptr(), y.data_ptr(), rows, cols, 0.01, g2.data_ptr(),
+                                         part.data_ptr(), rpb, sc.data_ptr(), _s()))
+            gy = g2
+            if need_b:
+                gb = part.sum(0)
+        else:
+            gy = torch.where(y >= 0, gy, 0.01 * gy)
+    if sc is None and need_x and need_w and gy.is_contiguous() and gy.shape[0] >= 4096:
+        sc = _gy_scale(gy)  # one scale for both gradient GEMMs
+    gx = _dgrad(gy, w, ctx.wcache, sc) if need_x else None
+    gw = _wgrad(gy, x2, w.shape[1], sc, ctx.xs) if need_w else None
+    if gb is None and need_b:
+        gb = gy.sum(0)
+    return gx, gw, gb
+
+
+class _RoutingEncFn(torch.autograd.Function):
+    """First NetMon encoder layer on routing node observations with gradient: forward on the
+    12-column gather (gm_routing_node_encoder, exact fp32), backward as a Linear (the node
+    observations are data: no input gradient)."""
+
+    @staticmethod
+    def forward(ctx, x, w, b, nbr, lin, G, N):
+        from . import fused as FU
+
+        y = torch.empty(x.shape[0], w.shape[0], device=x.device)
+        FU.routing_encoder(lin, x, nbr, G, N, y)
+        ctx.act, ctx.wcache, ctx.xs = lin.act, lin._wc, None
+        ctx.save_for_backward(x, w, y)
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, w, y = ctx.saved_tensors
+        _, gw, gb = _linear_backward(ctx, gy, x, w, y, False, ctx.needs_input_grad[1], ctx.needs_input_grad[2])
+        return None, gw, gb, None, None, None, None
 
 
 class Linear(nn.Linear):
@@ -391,17 +420,27 @@ class _LSTMCellFn(torch.autograd.Function):
     scale costs a pass of its own."""
 
     @staticmethod
-    def forward(ctx, xh, w, b, c, wcache, tag):
+    def forward(ctx, xh, w, b, c, wcache, tag, packed=None):
         x2, ldx, k = _as_rows(xh)
         xs = _amax_slot(x2, ldx, w.shape[0], ctx.needs_input_grad[1])
-        gates = linear_raw(x2, ldx, k, w, b, 0, wcache=wcache, tag=tag, amax=xs)
-        ctx.xs = None if xs is None else _finish_scale(xs)
-        M, H4 = gates.shape
+        M, H4 = x2.shape[0], w.shape[0]
         H = H4 // 4
-        h1 = torch.empty(M, H, device=gates.device)
-        c1 = torch.empty(M, H, device=gates.device)
-        act = torch.empty_like(gates)
-        L.check(L.lib().gm_lstm_pointwise(L.ptr(gates), L.ptr(c), M, H, L.ptr(h1), L.ptr(c1), L.ptr(act), _s()))
+        h1 = torch.empty(M, H, device=x2.device)
+        c1 = torch.empty(M, H, device=x2.device)
+        act = torch.empty(M, H4, device=x2.device)
+        if packed is not None:
+            # gate math in the GEMM epilogue (interleaved gate tiles, fused.pack_lstm): h', c' and
+            # the gate activations for backward straight from the accumulators, no gates tensor
+            from . import fused as FU
+
+            wp, ldw, bp, x3 = packed
+            FU.gemm(FU.dense(x2.data_ptr(), ldx, k, amax=None if xs is None else xs.data_ptr()), None, wp.data_ptr(),
+                    ldw, bp.data_ptr(), M, H4, FU.GM_EPI_LSTM, h1.data_ptr(), H, c1.data_ptr(), H, c.data_ptr(), H,
+                    act.data_ptr(), tag=tag and f"lstm:{tag}:{M}x{H4}x{k}", x3=x3)
+        else:
+            gates = linear_raw(x2, ldx, k, w, b, 0, wcache=wcache, tag=tag, amax=xs)
+            L.check(L.lib().gm_lstm_pointwise(L.ptr(gates), L.ptr(c), M, H, L.ptr(h1), L.ptr(c1), L.ptr(act), _s()))
+        ctx.xs = None if xs is None else _finish_scale(xs)
         ctx.wcache = wcache
         ctx.save_for_backward(x2[:, :k] if x2.shape[1] != k else x2, w, act, c, c1)
         return h1, c1
@@ -421,7 +460,7 @@ class _LSTMCellFn(torch.autograd.Function):
         gx = _dgrad(dg, w, ctx.wcache, sc) if n[0] else None
         gw = _wgrad(dg, x2, w.shape[1], sc, ctx.xs) if n[1] else None
         gb = dg.sum(0) if n[2] else None
-        return gx, gw, gb, dc if n[3] else None, None, None
+        return gx, gw, gb, dc if n[3] else None, None, None, None
 
 
 class LSTMCell(nn.Module):
@@ -448,7 +487,10 @@ class LSTMCell(nn.Module):
         b = self.bias_ih + self.bias_hh
         if torch.is_grad_enabled() and (w.requires_grad or xh.requires_grad):
             if xh.shape[0] >= 4096 and _x3_rows_ok(xh, xh.stride(0), w.shape[0]):
-                return _LSTMCellFn.apply(xh, w, b, c.contiguous(), None, self.tag)
+                from . import fused as FU
+
+                packed = FU.pack_lstm(self) if self.hidden_size % 32 == 0 else None
+                return _LSTMCellFn.apply(xh, w, b, c.contiguous(), None, self.tag, packed)
             gates = LinearFn.apply(xh, w, b, 0, None, self.tag)
         else:
             gates = linear_raw(xh, xh.stride(0), xh.shape[1], w, b, 0, tag=self.tag)
@@ -580,6 +622,21 @@ class NetMon(nn.Module):
     def get_state_size(self):
         return self.state_size
 
+    def _encode(self, x2, nbr, B, N):
+        """Encoder MLP; with gradient at training batch sizes the first layer runs on the routing
+        node-observation gather (_RoutingEncFn) instead of the dense K = 4N+8 GEMM."""
+        from . import fused as FU
+
+        layers = self.encode.linear_layers
+        if torch.is_grad_enabled() and x2.shape[0] >= 4096 and not x2.requires_grad and \
+                FU.routing_encoder_ok(layers[0], N, x2.shape[1], nbr):
+            lin = layers[0]
+            h = _RoutingEncFn.apply(x2.contiguous(), lin.weight, lin.bias, nbr.contiguous(), lin, B, N)
+            for lin in layers[1:]:
+                h = lin(h)
+            return h
+        return self.encode(x2)
+
     def _cell(self, cell, x, h, c):
         if self.rnn_type == "gru":
             return cell(x, h), None
@@ -594,7 +651,7 @@ class NetMon(nn.Module):
             self.state = torch.zeros(B, N, self.state_size, device=x.device)
         nc = self.cell_states
         st = self.state.reshape(B * N, self.num_states, H)
-        h = self.encode(x.reshape(B * N, Fdim))
+        h = self._encode(x.reshape(B * N, Fdim), nbr, B, N)
         hs, cs = st[:, 0], (st[:, 1] if nc == 2 else None)
         h, c = self._cell(self.rnn_obs, h, hs.contiguous(), None if cs is None else cs.contiguous())
         h0, c0 = h, c

@@ -127,20 +127,23 @@ class ReplayBuffer:
         self.add_pre(obs, node_state, node_obs, nbr, agent_node)
         self.add_post(action, reward, next_obs, done, episode_done, next_node_obs, next_agent_node)
 
-    def _gather(self, slot, env):
+    def _gather(self, slot, env, first=True):
+        """One TransitionBatch of the (slot, env) pairs. The stored start states (NetMon node state,
+        agent state) are read by the update at the first step of a sequence only
+        (src/main.py:846-851, 858-859), so later steps leave them out (None)."""
         f = torch.float32
         g = self.graph
         return TransitionBatch(
             (slot, env), self.obs[slot, env].to(f), self.action[slot, env].long(), self.reward[slot, env].to(f),
             self.next_obs[slot, env].to(f), self.done[slot, env], self.episode_done[slot],
             self.node_obs[slot, env].to(f) if g else None, self.nbr[slot, env].int().contiguous() if g else None,
-            self.node_state[slot, env].to(f) if g else None,
+            self.node_state[slot, env].to(f) if g and first else None,
             self.agent_node[slot, env].int().contiguous() if g else None,
             self.next_node_obs[slot, env].to(f) if g else None,
             self.next_agent_node[slot, env].int().contiguous() if g else None,
             self.adj[slot, env].to(f) if self.adj is not None else None,
             self.next_adj[slot, env].to(f) if self.next_adj is not None else None,
-            self.agent_state[slot, env].to(f) if self.agent_state is not None else None,
+            self.agent_state[slot, env].to(f) if self.agent_state is not None and first else None,
             self.node_aux[slot, env].to(f) if self.node_aux is not None else None,
         )
 
@@ -174,4 +177,4 @@ class ReplayBuffer:
         env = f // span
         first = (self.index % self.count + f % span) % self.count
         for o in range(sequence_length):
-            yield self._gather((first + o) % self.count, env)
+            yield self._gather((first + o) % self.count, env, first=o == 0)

@@ -62,7 +62,14 @@ FUSED_TARGET = True
 
 
 def joint_obs(env_obs, network_obs):
-    return torch.cat([env_obs, network_obs], -1)
+    """[env obs | NetMon graph obs] as a view of a buffer whose rows are padded to a multiple of 4
+    floats, so the DQN's first GEMM reads it in place (16-byte rows) instead of a padded copy."""
+    w = env_obs.shape[-1] + network_obs.shape[-1]
+    pad = (w + 3) // 4 * 4 - w
+    if pad == 0:
+        return torch.cat([env_obs, network_obs], -1)
+    z = env_obs.new_zeros(*env_obs.shape[:-1], pad)
+    return torch.cat([env_obs, network_obs, z], -1)[..., :w]
 
 
 def attention_kl(att_weights, tar_att_weights, done):
@@ -88,36 +95,79 @@ def _fused_target_ok(netmon, model_tar):
 
 
 @torch.no_grad()
-def _fused_next_q(netmon, model_tar, batch):
+def _fused_next_q(netmon, model_tar, next_obs, next_node_obs, nbr, next_agent_node, state):
     """Q_target(next obs) [B, A, actions] without materialising the joint next observation:
-    the NetMon step on the next node observations (continuing from netmon.state) and the
-    target DQN with the readout gathered inside its first GEMM (the rollout's path)."""
+    the NetMon step on the next node observations (continuing from `state`, the online NetMon
+    state after the step) and the target DQN with the readout gathered inside its first GEMM
+    (the rollout's path). netmon.state is left as it was."""
     from . import fused as FU
 
-    B, A, od = batch.next_obs.shape
+    B, A, od = next_obs.shape
     odp = (od + 3) // 4 * 4  # 16-byte rows for the GEMM's dense source
-    env_obs = batch.next_obs.contiguous() if odp == od else F.pad(batch.next_obs, (0, odp - od))
-    state, h_prev = FU.netmon_step(netmon, batch.next_node_obs, batch.nbr.contiguous(),
-                                   netmon.state.detach().contiguous())
+    env_obs = next_obs.contiguous() if odp == od else F.pad(next_obs, (0, odp - od))
+    keep = netmon.state
+    st, h_prev = FU.netmon_step(netmon, next_node_obs, nbr.contiguous(), state.detach().contiguous())
+    netmon.state = keep
     dev = env_obs.device
-    q = FU.dqn_q(model_tar, env_obs, od, state, h_prev, batch.nbr.contiguous(), batch.next_agent_node.contiguous(),
+    q = FU.dqn_q(model_tar, env_obs, od, st, h_prev, nbr.contiguous(), next_agent_node.contiguous(),
                  lambda i, m, n: torch.empty(m, n, device=dev), hidden=netmon.hidden_features)
     return q.view(B, A, -1)
 
 
-def dqn_loss(netmon, model, model_tar, batches, gamma, att_coeff=0.0, aux_model=None, aux_coeff=0.0, parts=None):
+@torch.no_grad()
+def _reused_next_q(netmon, model_tar, batches, joints, states):
+    """max_a Q_target(next obs) for every step of a sequence of CONSECUTIVE transitions
+    (replay sequences): for t < L-1 the next observation of step t is the observation of step
+    t + 1 and the target NetMon (the online NetMon without gradient, continuing from the online
+    state after step t) is exactly the online NetMon step t + 1 — unless the episode ended at
+    t, where the online state was reset. So the target DQN runs on the online joint observation
+    of step t + 1, and only the samples whose episode ended at t (and the last step) get their
+    own NetMon step on the stored next observation (src/main.py:878-915 evaluated per step)."""
+    L_ = len(batches)
+    ep = torch.stack([b.episode_done.expand(b.obs.shape[0]) if b.episode_done.dim() == 0 else b.episode_done
+                      for b in batches[:-1]]) if L_ > 1 else None
+    done_rows = ep.nonzero().cpu() if ep is not None else None  # one host read per update
+    out = []
+    for t, batch in enumerate(batches):
+        if t == L_ - 1:
+            q = _fused_next_q(netmon, model_tar, batch.next_obs, batch.next_node_obs, batch.nbr,
+                              batch.next_agent_node, states[t])
+            out.append(q.max(dim=2)[0])
+            continue
+        x = joints[t + 1]
+        B, A, w = x.shape
+        x2 = x.reshape(B * A, w)
+        dev = x.device
+        q = model_tar.forward_rows(x2, x2.stride(0), w, lambda i, m, n: torch.empty(m, n, device=dev))
+        qmax = q.view(B, A, -1).max(dim=2)[0]
+        rows = done_rows[done_rows[:, 0] == t, 1]
+        if len(rows):
+            r = rows.to(dev)
+            sub = _fused_next_q(netmon, model_tar, batch.next_obs[r], batch.next_node_obs[r], batch.nbr[r],
+                                batch.next_agent_node[r], states[t][r])
+            qmax[r] = sub.max(dim=2)[0]
+        out.append(qmax)
+    return out
+
+
+def dqn_loss(netmon, model, model_tar, batches, gamma, att_coeff=0.0, aux_model=None, aux_coeff=0.0, parts=None,
+             consecutive=False):
     """Sequence loss of src/main.py:840-1000 for DQN / DGN / DQNR / CommNet; netmon may be None.
     Recurrent models start from the stored agent state, the target model runs from the online
     model's next state, and the state is reset for done agents and at episode ends. aux_model
     (with netmon): the NetMon aux head on the new NetMon state, MSE against the stored node aux
-    targets, weighted by aux_coeff (src/main.py:586-594, 868-875, 996-1000). parts (a dict)
-    receives the loss terms. Returns (loss, list of q, list of q_target)."""
+    targets, weighted by aux_coeff (src/main.py:586-594, 868-875, 996-1000). consecutive: the
+    batches are a replay sequence (step t + 1 continues step t; ReplayBuffer.get_batch), which
+    lets the target pass reuse the online NetMon steps (_reused_next_q). parts (a dict) receives
+    the loss terms. Returns (loss, list of q, list of q_target)."""
     L = len(batches)
     has_state = hasattr(model, "state")
     loss_q = loss_att = loss_aux = None
     qs, qts = [], []
     last_state = last_ep_done = None
     fused_tar = not has_state and _fused_target_ok(netmon, model_tar) and FUSED_TARGET
+    reuse = fused_tar and consecutive and att_coeff == 0
+    joints, states, next_max = [], [], []
     for t, batch in enumerate(batches):
         if has_state and t == 0:
             model.state = batch.agent_state
@@ -137,28 +187,38 @@ def dqn_loss(netmon, model, model_tar, batches, gamma, att_coeff=0.0, aux_model=
                 else batch.episode_done
             next_obs = None
         q = model(obs, batch.adj)
+        qs.append(q)
+        if reuse:  # targets after the online pass over the whole sequence
+            joints.append(obs.detach())
+            states.append(last_state.detach())
+            continue
         with torch.no_grad():
             if has_state:
                 model_tar.state = model.state.detach()
             if fused_tar:
-                next_q_max = _fused_next_q(netmon, model_tar, batch).max(dim=2)[0]
+                next_q_max = _fused_next_q(netmon, model_tar, batch.next_obs, batch.next_node_obs, batch.nbr,
+                                           batch.next_agent_node, netmon.state).max(dim=2)[0]
             else:
                 if netmon is not None:
                     nno = netmon.forward_graph(batch.next_node_obs, batch.nbr, batch.next_agent_node)
                     next_obs = joint_obs(batch.next_obs, nno)
                 next_q_max = model_tar(next_obs, batch.next_adj).max(dim=2)[0]
+        next_max.append(next_q_max)
         if has_state:
             ep = batch.episode_done.expand(batch.obs.shape[0]) if batch.episode_done.dim() == 0 \
                 else batch.episode_done
             model.state = model.state * (~batch.done * (~ep).view(-1, 1)).unsqueeze(-1)
-        target = batch.reward + (~batch.done) * gamma * next_q_max
-        q_target = torch.scatter(q.detach(), -1, batch.action.unsqueeze(-1), target.unsqueeze(-1))
-        term = torch.mean((q - q_target).pow(2)) / L
-        loss_q = term if loss_q is None else loss_q + term
         if att_coeff > 0 and hasattr(model, "att_weights"):
             kl = attention_kl(model.att_weights, model_tar.att_weights, batch.done) / L
             loss_att = kl if loss_att is None else loss_att + kl
-        qs.append(q)
+    if reuse:
+        next_max = _reused_next_q(netmon, model_tar, batches, joints, states)
+    for t, batch in enumerate(batches):
+        q = qs[t]
+        target = batch.reward + (~batch.done) * gamma * next_max[t]
+        q_target = torch.scatter(q.detach(), -1, batch.action.unsqueeze(-1), target.unsqueeze(-1))
+        term = torch.mean((q - q_target).pow(2)) / L
+        loss_q = term if loss_q is None else loss_q + term
         qts.append(q_target)
     loss = loss_q if loss_att is None else loss_q + att_coeff * loss_att
     if loss_aux is not None:
@@ -169,10 +229,11 @@ def dqn_loss(netmon, model, model_tar, batches, gamma, att_coeff=0.0, aux_model=
 
 
 def dqn_update(netmon, model, model_tar, optimizer, params, batches, gamma, tau, target_update_steps=0,
-               iteration=1, group=None, att_coeff=0.0, aux_model=None, aux_coeff=0.0, parts=None):
+               iteration=1, group=None, att_coeff=0.0, aux_model=None, aux_coeff=0.0, parts=None, consecutive=False):
     """One update (src/main.py:840-1026). params must include aux_model's parameters when
     the aux loss is on (src/main.py:594)."""
-    loss, qs, qts = dqn_loss(netmon, model, model_tar, batches, gamma, att_coeff, aux_model, aux_coeff, parts)
+    loss, qs, qts = dqn_loss(netmon, model, model_tar, batches, gamma, att_coeff, aux_model, aux_coeff, parts,
+                             consecutive)
     optimizer.zero_grad(set_to_none=False)
     loss.backward()
     allreduce_gradients(params, group)

@@ -139,6 +139,15 @@ def test_replay_sequences_and_full_update_on_env_data():
     for a, b in zip(t1, t0):
         torch.testing.assert_close(a, b, rtol=0, atol=1e-5)
     torch.testing.assert_close(l1, l0, rtol=1e-5, atol=1e-7)
+    # consecutive replay sequences (episodes of 10 steps inside the 4-step windows): the target
+    # pass that reuses the online NetMon steps gives the same targets and loss
+    with torch.no_grad():
+        l2, q2, t2 = T.dqn_loss(netmon, model, target, seqs, 0.9, consecutive=True)
+    for a, b in zip(t2, t0):
+        torch.testing.assert_close(a, b, rtol=0, atol=1e-5)
+    torch.testing.assert_close(l2, l0, rtol=1e-5, atol=1e-7)
+    eps = torch.stack([s.episode_done for s in seqs[:-1]])
+    assert eps.any() and not eps.all()  # both target branches ran
     params = list(model.parameters()) + list(netmon.parameters())
     before = [p.detach().clone() for p in params]
     opt = torch.optim.AdamW(params, lr=1e-3)
