@@ -470,3 +470,29 @@ def dqn_q(dqn, env_obs, obs_dim, state, h_prev, nbr, agent_node, scratch, hidden
     if fuse:  # last hidden layer + Q head in one kernel
         h = linear_head(hidden[-1], fc, h, h.stride(0), h.shape[1], scratch(len(hidden) + 1, M, fc.out_features))
     return h
+
+
+@torch.no_grad()
+def dqn_q_dense(dqn, env_obs, graph, scratch):
+    """Q [B*A, actions] of the DQN on [env obs | graph obs] given as two dense sources (the training
+    target pass on the online graph observations): env_obs [B, A, od] with 16-byte rows, graph
+    [B, A, G] contiguous."""
+    B, A, od = env_obs.shape
+    M = B * A
+    g2 = graph.reshape(M, graph.shape[-1])
+    lin0 = dqn.encoder.linear_layers[0]
+    wp, ldw, b, x3 = pack_dqn_first(lin0, od)
+    h1 = scratch(0, M, lin0.out_features)
+    gemm(dense(g2.data_ptr(), g2.stride(0), g2.shape[1]), dense(env_obs.data_ptr(), env_obs.stride(1), od),
+         wp.data_ptr(), ldw, b.data_ptr(), M, lin0.out_features, GM_EPI_BIAS_LEAKY if lin0.act == 1 else GM_EPI_BIAS,
+         h1.data_ptr(), h1.stride(0), tag=lin0.tag and f"linear:{lin0.tag}:{M}x{lin0.out_features}x{g2.shape[1]}+{od}",
+         x3=x3)
+    h = h1
+    hidden = list(dqn.encoder.linear_layers[1:])
+    fc = dqn.q_net.fc
+    fuse = len(hidden) > 0 and head_ok(hidden[-1], fc)
+    for i, lin in enumerate(hidden[:-1] if fuse else hidden + [fc]):
+        h = _linear(h, h.stride(0), h.shape[1], lin, scratch(i + 1, M, lin.out_features))
+    if fuse:
+        h = linear_head(hidden[-1], fc, h, h.stride(0), h.shape[1], scratch(len(hidden) + 1, M, fc.out_features))
+    return h

@@ -213,17 +213,13 @@ class LinearFn(torch.autograd.Function):
         return gx, gw, gb, None, None, None
 
 
-def _linear_backward(ctx, gy, x2, w, y, need_x, need_w, need_b):
-    """Gradients of y = act(x2 @ w^T + b) (ctx.act, ctx.wcache, ctx.xs = published max|x| scale
-    or None): fused leaky backward + bias partials + max|g|, then the split-f16 input- and
-    weight-gradient GEMMs sharing one gradient scale."""
-    gy = gy.reshape(-1, w.shape[0])
-    gb = None
-    sc = None
-    if ctx.act == 1:
+def _act_grad(act, gy, y, need_b, want_scale):
+    """Backward through the layer activation: (g, bias gradient or None, gradient scale or None).
+    leaky_relu at training sizes: one fused pass (gm_leaky_bwd: mask, per-block bias partials,
+    max|g| for the gradient GEMMs' operand scale)."""
+    gb = sc = None
+    if act == 1:
         if gy.is_contiguous() and y.is_contiguous() and gy.shape[0] >= 4096:
-            # leaky_relu backward + per-block bias-gradient partial sums + max|g| (the
-            # gradient GEMMs' operand scale) in one pass
             rows, cols = gy.shape
             rpb = 64
             g2 = torch.empty_like(gy)
@@ -236,13 +232,71 @@ def _linear_backward(ctx, gy, x2, w, y, need_x, need_w, need_b):
                 gb = part.sum(0)
         else:
             gy = torch.where(y >= 0, gy, 0.01 * gy)
-    if sc is None and need_x and need_w and gy.is_contiguous() and gy.shape[0] >= 4096:
+    if sc is None and want_scale and gy.is_contiguous() and gy.shape[0] >= 4096:
         sc = _gy_scale(gy)  # one scale for both gradient GEMMs
-    gx = _dgrad(gy, w, ctx.wcache, sc) if need_x else None
-    gw = _wgrad(gy, x2, w.shape[1], sc, ctx.xs) if need_w else None
     if gb is None and need_b:
         gb = gy.sum(0)
+    return gy, gb, sc
+
+
+def _linear_backward(ctx, gy, x2, w, y, need_x, need_w, need_b):
+    """Gradients of y = act(x2 @ w^T + b) (ctx.act, ctx.wcache, ctx.xs = published max|x| scale
+    or None): the activation backward, then the split-f16 input- and weight-gradient GEMMs
+    sharing one gradient scale."""
+    gy, gb, sc = _act_grad(ctx.act, gy.reshape(-1, w.shape[0]), y, need_b, need_x and need_w)
+    gx = _dgrad(gy, w, ctx.wcache, sc) if need_x else None
+    gw = _wgrad(gy, x2, w.shape[1], sc, ctx.xs) if need_w else None
     return gx, gw, gb
+
+
+class _JointLinearFn(torch.autograd.Function):
+    """First DQN layer on the joint observation [env obs | NetMon graph obs] (src/model.py:187-203
+    with src/env/wrapper.py:106-109) without materialising it: one split-f16 GEMM over two dense
+    A sources [graph | env] (weights column-reordered once, fused.pack_dqn_first) that publishes
+    max|A| for the weight gradient; backward computes the input gradient of the graph part only
+    (the env observation is data) and the weight gradient per source."""
+
+    @staticmethod
+    def forward(ctx, graph, env_obs, w, b, lin):
+        from . import fused as FU
+
+        R, G = graph.shape
+        od = env_obs.shape[1]
+        wp, ldw, bp, x3 = FU.pack_dqn_first(lin, od)
+        xs = torch.zeros(1, device=graph.device) if ctx.needs_input_grad[2] else None
+        y = torch.empty(R, w.shape[0], device=graph.device)
+        FU.gemm(FU.dense(graph.data_ptr(), G, G, amax=None if xs is None else xs.data_ptr()),
+                FU.dense(env_obs.data_ptr(), env_obs.stride(0), od), wp.data_ptr(), ldw, bp.data_ptr(), R, w.shape[0],
+                FU.GM_EPI_BIAS_LEAKY if lin.act == 1 else FU.GM_EPI_BIAS, y.data_ptr(), w.shape[0],
+                tag=lin.tag and f"linear:{lin.tag}:{R}x{w.shape[0]}x{G}+{od}", x3=x3)
+        ctx.xs = None if xs is None else _finish_scale(xs)
+        ctx.act = lin.act
+        if not hasattr(lin, "_wc_graph"):
+            lin._wc_graph = _WeightCache()
+        ctx.wcache_graph = lin._wc_graph
+        ctx.save_for_backward(graph, env_obs, w, y)
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        graph, env_obs, w, y = ctx.saved_tensors
+        od = env_obs.shape[1]
+        n = ctx.needs_input_grad
+        g, gb, sc = _act_grad(ctx.act, gy, y, n[3], n[0] and n[2])
+        gg = _dgrad(g, w[:, od:], ctx.wcache_graph, sc) if n[0] else None
+        gw = None
+        if n[2]:
+            gw = torch.cat([_wgrad(g, env_obs, od, sc, ctx.xs), _wgrad(g, graph, graph.shape[1], sc, ctx.xs)], 1)
+        return gg, None, gw, gb, None
+
+
+def joint_first_layer_ok(graph2d, env2d):
+    """The two-source first layer needs the split-f16 form, training batch sizes and 16-byte rows."""
+    from . import fused as FU
+
+    return (FU.use_x3(512) and graph2d.shape[0] >= 4096 and graph2d.is_contiguous() and graph2d.shape[1] % 32 == 0
+            and env2d.stride(1) == 1 and env2d.stride(0) % 4 == 0 and env2d.data_ptr() % 16 == 0
+            and graph2d.data_ptr() % 16 == 0)
 
 
 class _RoutingEncFn(torch.autograd.Function):
@@ -727,6 +781,24 @@ class DQN(nn.Module):
 
     def forward(self, x, mask=None):
         return self.q_net(self.encoder(x))
+
+    def forward_split(self, env_obs, graph_obs):
+        """forward(joint_obs(env_obs, graph_obs)) without the joint tensor: the first layer reads the
+        env observation [B, A, od] (rows padded to 16 bytes, e.g. replay batches) and the NetMon
+        graph observation [B, A, G] as two GEMM sources (_JointLinearFn)."""
+        B, A, od = env_obs.shape
+        e2 = env_obs.reshape(B * A, od)
+        g2 = graph_obs.reshape(B * A, graph_obs.shape[-1])
+        layers = self.encoder.linear_layers
+        if not joint_first_layer_ok(g2, e2) or layers[0].in_features != od + g2.shape[1]:
+            from .train import joint_obs
+
+            return self(joint_obs(env_obs, graph_obs))
+        lin = layers[0]
+        h = _JointLinearFn.apply(g2, e2, lin.weight, lin.bias, lin)
+        for lin in layers[1:]:
+            h = lin(h)
+        return self.q_net(h).view(B, A, -1)
 
     def forward_rows(self, x2d, ldx, k, scratch, **unused):
         """no-grad fast path: q [rows, actions] from a strided observation buffer; the last

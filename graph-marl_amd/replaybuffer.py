@@ -52,8 +52,12 @@ class ReplayBuffer:
         def z(*shape, dtype=ft):
             return torch.zeros(*shape, dtype=dtype, device=device)
 
-        self.obs = z(S, B, A, obs_dim)
-        self.next_obs = z(S, B, A, obs_dim)
+        # observation rows padded to a multiple of 4 floats: a sampled batch is a view whose rows the
+        # GEMM kernels read in place (16-byte rows), no padded copy per update step
+        self.obs_dim = obs_dim
+        odp = (obs_dim + 3) // 4 * 4
+        self.obs = z(S, B, A, odp)
+        self.next_obs = z(S, B, A, odp)
         self.action = z(S, B, A, dtype=torch.int8)
         self.reward = z(S, B, A)
         self.done = z(S, B, A, dtype=torch.bool)
@@ -84,7 +88,7 @@ class ReplayBuffer:
         agent adjacency, the agent state the model starts the step from (None = zeros) and the
         node aux targets (src/main.py:697-699)."""
         i = self.index
-        self.obs[i].copy_(obs)
+        self.obs[i, ..., : self.obs_dim].copy_(obs)
         if self.node_aux is not None:
             self.node_aux[i].copy_(node_aux)
         if self.adj is not None:
@@ -111,7 +115,7 @@ class ReplayBuffer:
             self.next_adj[i].copy_(next_adj != 0)
         self.action[i].copy_(action)
         self.reward[i].copy_(reward)
-        self.next_obs[i].copy_(next_obs)
+        self.next_obs[i, ..., : self.obs_dim].copy_(next_obs)
         self.done[i].copy_(done)
         self.episode_done[i] = bool(episode_done)
         if self.graph:
@@ -134,8 +138,9 @@ class ReplayBuffer:
         f = torch.float32
         g = self.graph
         return TransitionBatch(
-            (slot, env), self.obs[slot, env].to(f), self.action[slot, env].long(), self.reward[slot, env].to(f),
-            self.next_obs[slot, env].to(f), self.done[slot, env], self.episode_done[slot],
+            (slot, env), self.obs[slot, env].to(f)[..., : self.obs_dim], self.action[slot, env].long(),
+            self.reward[slot, env].to(f), self.next_obs[slot, env].to(f)[..., : self.obs_dim], self.done[slot, env],
+            self.episode_done[slot],
             self.node_obs[slot, env].to(f) if g else None, self.nbr[slot, env].int().contiguous() if g else None,
             self.node_state[slot, env].to(f) if g and first else None,
             self.agent_node[slot, env].int().contiguous() if g else None,

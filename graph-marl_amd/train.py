@@ -135,10 +135,18 @@ def _reused_next_q(netmon, model_tar, batches, joints, states):
             out.append(q.max(dim=2)[0])
             continue
         x = joints[t + 1]
-        B, A, w = x.shape
-        x2 = x.reshape(B * A, w)
-        dev = x.device
-        q = model_tar.forward_rows(x2, x2.stride(0), w, lambda i, m, n: torch.empty(m, n, device=dev))
+        if isinstance(x, tuple):  # (env obs, graph obs): the two-source first layer
+            from . import fused as FU
+
+            env_obs, graph = x
+            B, A = env_obs.shape[:2]
+            dev = graph.device
+            q = FU.dqn_q_dense(model_tar, env_obs, graph, lambda i, m, n: torch.empty(m, n, device=dev))
+        else:
+            B, A, w = x.shape
+            x2 = x.reshape(B * A, w)
+            dev = x.device
+            q = model_tar.forward_rows(x2, x2.stride(0), w, lambda i, m, n: torch.empty(m, n, device=dev))
         qmax = q.view(B, A, -1).max(dim=2)[0]
         rows = done_rows[done_rows[:, 0] == t, 1]
         if len(rows):
@@ -167,6 +175,8 @@ def dqn_loss(netmon, model, model_tar, batches, gamma, att_coeff=0.0, aux_model=
     last_state = last_ep_done = None
     fused_tar = not has_state and _fused_target_ok(netmon, model_tar) and FUSED_TARGET
     reuse = fused_tar and consecutive and att_coeff == 0
+    # DQN on NetMon: the first layer reads the env obs and the graph obs as two GEMM sources
+    split = netmon is not None and type(model).__name__ == "DQN" and hasattr(model, "forward_split")
     joints, states, next_max = [], [], []
     for t, batch in enumerate(batches):
         if has_state and t == 0:
@@ -178,7 +188,8 @@ def dqn_loss(netmon, model, model_tar, batches, gamma, att_coeff=0.0, aux_model=
                 netmon.state = batch.node_state
             else:
                 netmon.state = last_state * (~last_ep_done).view(-1, 1, 1)
-            obs = joint_obs(batch.obs, netmon.forward_graph(batch.node_obs, batch.nbr, batch.agent_node))
+            graph = netmon.forward_graph(batch.node_obs, batch.nbr, batch.agent_node)
+            obs = (batch.obs, graph) if split else joint_obs(batch.obs, graph)
             if aux_model is not None:
                 term = torch.mean((aux_model(netmon.state) - batch.node_aux) ** 2) / L
                 loss_aux = term if loss_aux is None else loss_aux + term
@@ -186,10 +197,10 @@ def dqn_loss(netmon, model, model_tar, batches, gamma, att_coeff=0.0, aux_model=
             last_ep_done = batch.episode_done.expand(batch.obs.shape[0]) if batch.episode_done.dim() == 0 \
                 else batch.episode_done
             next_obs = None
-        q = model(obs, batch.adj)
+        q = model.forward_split(*obs) if split else model(obs, batch.adj)
         qs.append(q)
         if reuse:  # targets after the online pass over the whole sequence
-            joints.append(obs.detach())
+            joints.append((obs[0], obs[1].detach()) if split else obs.detach())
             states.append(last_state.detach())
             continue
         with torch.no_grad():

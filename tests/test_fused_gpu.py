@@ -474,3 +474,44 @@ def test_lnlstm_pointwise_vs_torch(rows, H):
     torch.testing.assert_close(out[:, :H].double(), hy, atol=2e-6, rtol=0)
     torch.testing.assert_close(out[:, H:2 * H].double(), cy, atol=4e-6, rtol=0)
     assert (out[:, 2 * H:] == 0).all()
+
+
+@pytest.mark.parametrize("rows", [4096, 65540])
+def test_joint_first_layer_split_vs_fp64(rows):
+    """DQN first layer on [env obs | graph obs] as two GEMM sources (_JointLinearFn, training): the
+    output, the graph-obs input gradient and the weight / bias gradients vs fp64, relative to the
+    magnitude of each gradient's terms (the leaky mask from the kernel's own forward, as in
+    test_linear_backward_large_batch); the env observation is a padded-row view like replay
+    batches (130 of 132 columns)."""
+    gm, M, FU, W = mods()
+    torch.manual_seed(rows)
+    A = 20
+    B = (rows + A - 1) // A
+    dqn = M.DQN(130 + 512, [512, 256], 4).cuda()
+    envp = torch.randn(B, A, 132, device="cuda")
+    env = envp[..., :130]
+    graph = (torch.randn(B, A, 512, device="cuda") * 0.3).requires_grad_(True)
+    lin = dqn.encoder.linear_layers[0]
+    g2, e2 = graph.reshape(-1, 512), env.reshape(-1, 130)
+    assert M.joint_first_layer_ok(g2, e2)
+    y = M._JointLinearFn.apply(g2, e2, lin.weight, lin.bias, lin)
+    xd = torch.cat([e2, g2.detach()], 1).double()
+    wd = lin.weight.detach().double()
+    pre = xd @ wd.t() + lin.bias.detach().double()
+    yd = torch.where(pre >= 0, pre, 0.01 * pre)
+    mag = xd.abs() @ wd.abs().t()
+    assert ((y.detach().double() - yd).abs() / mag).max().item() < 4e-6
+    gy = torch.randn_like(y) * 1e-4
+    y.backward(gy)
+    gyd = gy.double() * torch.where(y.detach() >= 0, 1.0, 0.01)
+    refs = ((graph.grad.reshape(-1, 512), gyd @ wd[:, 130:], gyd.abs() @ wd[:, 130:].abs()),
+            (lin.weight.grad, gyd.t() @ xd, gyd.abs().t() @ xd.abs()), (lin.bias.grad, gyd.sum(0), gyd.abs().sum(0)))
+    for got, ref, mg in refs:
+        rel = ((got.double() - ref).abs() / mg.clamp_min(1e-300)).max().item()
+        assert rel < 1e-5, rel
+    # the whole DQN: forward_split == forward on the joint observation
+    with torch.no_grad():
+        T = importlib.import_module("graph-marl_amd.train")
+        q1 = dqn.forward_split(env, graph.detach())
+        q0 = dqn(T.joint_obs(env, graph.detach()))
+        torch.testing.assert_close(q1, q0, atol=1e-5, rtol=0)
