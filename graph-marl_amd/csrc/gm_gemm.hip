@@ -1651,6 +1651,153 @@ __global__ __launch_bounds__(256, 2) void k_gemm3_kmajor(const float* __restrict
         }
 }
 
+// Weight-gradient GEMM, transposed-read form (default): the same arithmetic as k_gemm3_kmajor
+// (both operands scaled by device powers of two and split into f16 pieces, hi*hi in one
+// accumulator and the two 2^-12 cross terms in a second), but the K-major operands are staged in
+// their natural layout: 16-byte loads of 4 consecutive m (n) columns of one k row, split in
+// registers, stored as 8-byte [k][column] f16 rows (hi and lo images), and the MFMA fragments
+// (8 consecutive k of one column) are read with ds_read_b64_tr_b16, which transposes 4 k rows x 16
+// columns per 16-lane group. No register transpose, 4x fewer global load instructions than the
+// dword form, and a 64 x (BN/2) wave tile. Row stride of an image = columns * 2 + 64 B: the four
+// k rows of a 32-lane half then start 16 banks apart (conflict-free transposed reads).
+template <int BN>
+__global__ __launch_bounds__(256, BN == 128 ? 2 : 1) void k_wgrad_tr(const float* __restrict__ A, long long lda,
+                                                                   unsigned abytes, const float* __restrict__ B,
+                                                                   long long ldb, unsigned bbytes, int M, int N, int K,
+                                                                   int kchunk, const float* __restrict__ sa,
+                                                                   const float* __restrict__ sb, float* __restrict__ C,
+                                                                   long long ldc, long long cz) {
+    constexpr int BM = 128, BK = 32, TM = 2, TN = BN / 64;
+    constexpr int RA = BM * 2 + 64, RB = BN * 2 + 64;  // image row strides (bytes)
+    constexpr int LA = BM / 4 * BK / 256, LB = BN / 4 * BK / 256;  // float4 loads per thread
+    __shared__ __attribute__((aligned(16))) char smem[2][2 * BK * RA + 2 * BK * RB];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wr = wave >> 1, wc = wave & 1;
+    const int nN = (N + BN - 1) / BN;
+    const int m0 = (blockIdx.x / nN) * BM, n0 = (blockIdx.x % nN) * BN;
+    const int kb = blockIdx.y * kchunk, ke = min(K, kb + kchunk);
+    const int nk = (ke - kb + BK - 1) / BK;
+    const float s_a = *sa, s_b = *sb;
+    const __amdgpu_buffer_rsrc_t ra = rsrc(A, abytes), rb = rsrc(B, bbytes);
+    // loader map: A tile 32 k x 128 m = 32 float4 per k row -> lane q = tid & 31 (m = 4q), rows
+    // (tid >> 5) + 8 j; B tile 32 x BN: BN / 4 float4 per row
+    constexpr int QB = BN / 4, RB_STEP = 256 / QB;
+    const int qa = tid & 31, ka0 = tid >> 5, qb = tid % QB, kb0 = tid / QB;
+    float4 va[LA], vb[LB];
+    auto load = [&](int kt) {
+        const int k0 = kb + kt * BK;
+#pragma unroll
+        for (int j = 0; j < LA; j++) {
+            const int k = k0 + ka0 + 8 * j, m = m0 + 4 * qa;
+            const int off = (k < ke && m < M) ? (int)(((long long)k * lda + m) * 4) : OOB;
+            va[j] = bload(ra, off);
+        }
+#pragma unroll
+        for (int j = 0; j < LB; j++) {
+            const int k = k0 + kb0 + RB_STEP * j, n = n0 + 4 * qb;
+            const int off = (k < ke && n < N) ? (int)(((long long)k * ldb + n) * 4) : OOB;
+            vb[j] = bload(rb, off);
+        }
+    };
+    auto store = [&](int buf) {
+        char* ah = smem[buf];
+        char* al = ah + BK * RA;
+        char* bh = al + BK * RA;
+        char* bl = bh + BK * RB;
+#pragma unroll
+        for (int j = 0; j < LA; j++) {
+            half4 hi, lo;
+            split4(make_float4(va[j].x * s_a, va[j].y * s_a, va[j].z * s_a, va[j].w * s_a), hi, lo);
+            const int o = (ka0 + 8 * j) * RA + 8 * qa;
+            *reinterpret_cast<half4*>(ah + o) = hi;
+            *reinterpret_cast<half4*>(al + o) = lo;
+        }
+#pragma unroll
+        for (int j = 0; j < LB; j++) {
+            half4 hi, lo;
+            split4(make_float4(vb[j].x * s_b, vb[j].y * s_b, vb[j].z * s_b, vb[j].w * s_b), hi, lo);
+            const int o = (kb0 + RB_STEP * j) * RB + 8 * qb;
+            *reinterpret_cast<half4*>(bh + o) = hi;
+            *reinterpret_cast<half4*>(bl + o) = lo;
+        }
+    };
+    floatx16 acc[TM][TN], acc2[TM][TN];
+#pragma unroll
+    for (int i = 0; i < TM; i++)
+#pragma unroll
+        for (int j = 0; j < TN; j++)
+#pragma unroll
+            for (int r = 0; r < 16; r++) acc[i][j][r] = acc2[i][j][r] = 0.f;
+    // transposed-read address of this lane inside a 32-column fragment (T10): 16-lane group g reads
+    // k rows 8 (g >> 1) + 4 h + q (h = 0, 1: the two reads of 4 rows), columns 16 (g & 1) + 4 p
+    const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+    const int trk = 8 * (g >> 1) + q, trc = 16 * (g & 1) + 4 * p;
+    typedef __fp16 v4fp16 __attribute__((__vector_size__(8)));
+    auto frag = [&](const char* img, int rs, int col0, int k0) {
+        const char* a0 = img + (k0 + trk) * rs + 2 * (col0 + trc);
+        const half4 x0 = __builtin_bit_cast(
+            half4, __builtin_amdgcn_ds_read_tr16_b64_v4f16((__attribute__((address_space(3))) v4fp16*)(a0)));
+        const half4 x1 = __builtin_bit_cast(
+            half4, __builtin_amdgcn_ds_read_tr16_b64_v4f16((__attribute__((address_space(3))) v4fp16*)(a0 + 4 * rs)));
+        return half8{x0[0], x0[1], x0[2], x0[3], x1[0], x1[1], x1[2], x1[3]};
+    };
+    auto compute = [&](int buf) {
+        const char* ah = smem[buf];
+        const char* al = ah + BK * RA;
+        const char* bh = al + BK * RA;
+        const char* bl = bh + BK * RB;
+#pragma unroll
+        for (int kk = 0; kk < BK; kk += 16) {
+            half8 fah[TM], fal[TM], fbh[TN], fbl[TN];
+#pragma unroll
+            for (int i = 0; i < TM; i++) {
+                fah[i] = frag(ah, RA, wr * TM * 32 + 32 * i, kk);
+                fal[i] = frag(al, RA, wr * TM * 32 + 32 * i, kk);
+            }
+#pragma unroll
+            for (int j = 0; j < TN; j++) {
+                fbh[j] = frag(bh, RB, wc * TN * 32 + 32 * j, kk);
+                fbl[j] = frag(bl, RB, wc * TN * 32 + 32 * j, kk);
+            }
+#pragma unroll
+            for (int i = 0; i < TM; i++)
+#pragma unroll
+                for (int j = 0; j < TN; j++) {
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fah[i], fbh[j], acc[i][j], 0, 0, 0);
+                    acc2[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fal[i], fbh[j], acc2[i][j], 0, 0, 0);
+                    acc2[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fah[i], fbl[j], acc2[i][j], 0, 0, 0);
+                }
+        }
+    };
+    if (nk > 0) {
+        load(0);
+        store(0);
+    }
+    __syncthreads();
+    for (int kt = 0; kt < nk; kt++) {
+        if (kt + 1 < nk) load(kt + 1);
+        compute(kt & 1);
+        if (kt + 1 < nk) store((kt + 1) & 1);
+        __syncthreads();
+    }
+    const float inv = 1.0f / (s_a * s_b);  // powers of two: exact
+    float* Cz = C + (size_t)blockIdx.y * cz;
+    const int hh = lane >> 5, l32 = lane & 31;
+#pragma unroll
+    for (int i = 0; i < TM; i++)
+#pragma unroll
+        for (int j = 0; j < TN; j++) {
+            const int n = n0 + wc * TN * 32 + j * 32 + l32;
+#pragma unroll
+            for (int r = 0; r < 16; r++) {
+                const int m = m0 + wr * TM * 32 + i * 32 + 4 * hh + (r & 3) + 8 * (r >> 2);
+                if (m < M && n < N) Cz[(long long)m * ldc + n] = (acc[i][j][r] + acc2[i][j][r] * (1.0f / 4096.0f)) * inv;
+            }
+        }
+}
+
+int g_wgrad = -1;  // weight-gradient kernel: -1 / 1 transposed reads 128 x 128 (default), 2 the same 128 x 256, 0 dword form
+
 extern "C" int gm_gemm_x3_wgrad(const float* a, int64_t lda, const float* b, int64_t ldb, int32_t m, int32_t n, int32_t k,
                                 int32_t kchunk, const float* sa, const float* sb, float* c, int64_t ldc, void* stream) {
     if (!a || !b || !sa || !sb || !c || m <= 0 || n <= 0 || k <= 0 || kchunk <= 0 || (kchunk % 16) || (m % 4) ||
@@ -1658,10 +1805,27 @@ extern "C" int gm_gemm_x3_wgrad(const float* a, int64_t lda, const float* b, int
         (reinterpret_cast<uintptr_t>(b) & 15))
         return gm_fail(GM_ERR_INVALID_ARG, "gm_gemm_x3_wgrad: bad arguments (m, n, ld multiples of 4, 16-B bases, "
                                            "kchunk % 16 == 0)");
-    const int T = ((m + 127) / 128) * ((n + 127) / 128);
     const int S = (k + kchunk - 1) / kchunk;
-    hipLaunchKernelGGL(k_gemm3_kmajor, dim3(T, S), dim3(256), 0, (hipStream_t)stream, a, (long long)lda, b,
-                       (long long)ldb, m, n, k, kchunk, sa, sb, c, (long long)ldc, (long long)m * ldc);
+    if (g_wgrad == 0) {
+        const int T = ((m + 127) / 128) * ((n + 127) / 128);
+        hipLaunchKernelGGL(k_gemm3_kmajor, dim3(T, S), dim3(256), 0, (hipStream_t)stream, a, (long long)lda, b,
+                           (long long)ldb, m, n, k, kchunk, sa, sb, c, (long long)ldc, (long long)m * ldc);
+    } else {
+        const long long ab = (long long)k * lda * 4, bb = (long long)k * ldb * 4;
+        if (ab >= 0x7ff00000LL || bb >= 0x7ff00000LL)
+            return gm_fail(GM_ERR_UNSUPPORTED, "gm_gemm_x3_wgrad: operand larger than 2 GB (split the batch)");
+        if (g_wgrad != 2) {  // 128 x 128 tiles at 2 blocks/CU: 8-24 % faster than 128 x 256 at 1 block/CU
+            const int T = ((m + 127) / 128) * ((n + 127) / 128);
+            hipLaunchKernelGGL(k_wgrad_tr<128>, dim3(T, S), dim3(256), 0, (hipStream_t)stream, a, (long long)lda,
+                               (unsigned)ab, b, (long long)ldb, (unsigned)bb, m, n, k, kchunk, sa, sb, c, (long long)ldc,
+                               (long long)m * ldc);
+        } else {
+            const int T = ((m + 127) / 128) * ((n + 255) / 256);
+            hipLaunchKernelGGL(k_wgrad_tr<256>, dim3(T, S), dim3(256), 0, (hipStream_t)stream, a, (long long)lda,
+                               (unsigned)ab, b, (long long)ldb, (unsigned)bb, m, n, k, kchunk, sa, sb, c, (long long)ldc,
+                               (long long)m * ldc);
+        }
+    }
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return gm_fail(GM_ERR_HIP, std::string("gm_gemm_x3_wgrad: ") + hipGetErrorString(e));
     return GM_OK;
@@ -1688,6 +1852,12 @@ extern "C" int gm_gemm_pack_x3(const float* w, int64_t ldw, int32_t n, int32_t k
                        static_cast<_Float16*>(wp), wscale_inv);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return gm_fail(GM_ERR_HIP, std::string("gm_gemm_pack_x3: ") + hipGetErrorString(e));
+    return GM_OK;
+}
+
+extern "C" int gm_gemm_set_wgrad(int32_t form) {
+    if (form < -1 || form > 2) return gm_fail(GM_ERR_INVALID_ARG, "gm_gemm_set_wgrad: form in [-1, 2]");
+    g_wgrad = form;
     return GM_OK;
 }
 

@@ -272,12 +272,18 @@ def test_weight_gradient_kmajor(Mb, o, k, ldx, mag):
     gy = torch.randn(Mb, o, device="cuda") * mag
     xb = torch.randn(Mb, ldx, device="cuda")
     x = xb[:, :k]
-    gw = M_._wgrad(gy, x, k)
-    assert gw.shape == (o, k)
     ref = gy.double().t() @ x.double()
     mag_ref = gy.abs().double().t() @ x.abs().double()
-    rel = ((gw.double() - ref).abs() / mag_ref.clamp_min(1e-300)).max().item()
-    assert rel < 4e-6, rel
+    lib = FU._setup()
+    try:
+        for form in (-1, 2, 0):  # transposed reads 128x128 (default), 128x256, dword form
+            lib.gm_gemm_set_wgrad(form)
+            gw = M_._wgrad(gy, x, k)
+            assert gw.shape == (o, k)
+            rel = ((gw.double() - ref).abs() / mag_ref.clamp_min(1e-300)).max().item()
+            assert rel < 4e-6, (form, rel)
+    finally:
+        lib.gm_gemm_set_wgrad(-1)
 
 
 @pytest.mark.parametrize("rows,k,n,act", [(8192, 642, 512, 1), (5000, 256, 128, 1), (4096, 512, 4, 0),

@@ -26,13 +26,20 @@ def timeit(fn, reps=10):
 
 def main():
     torch.manual_seed(0)
-    Mb = 131072
+    Mb = int(os.environ.get("ROWS", "262160"))
+    lib = M.L.lib()
     out = {}
-    for o, k, ldx in ((512, 642, 644), (256, 512, 512), (512, 256, 256), (128, 256, 256)):
+    for o, k, ldx in ((512, 642, 644), (512, 512, 512), (256, 512, 512), (512, 256, 256), (128, 256, 256),
+                      (512, 130, 132)):
         gy = torch.randn(Mb, o, device="cuda") * 1e-6
         x = torch.randn(Mb, ldx, device="cuda")[:, :k]
-        out[f"{o}x{k}"] = {"x3_kmajor_us": round(timeit(lambda: M._wgrad(gy, x, k)), 1),
-                           "fp32_lib_us": round(timeit(lambda: gy.t() @ x), 1)}
+        r = {}
+        for form, name in ((2, "tr256"), (1, "tr128"), (0, "dword")):
+            lib.gm_gemm_set_wgrad(form)
+            r[name + "_us"] = round(timeit(lambda: M._wgrad(gy, x, k)), 1)
+        lib.gm_gemm_set_wgrad(-1)
+        r["fp32_lib_us"] = round(timeit(lambda: gy.t() @ x), 1)
+        out[f"{o}x{k}"] = r
     print(json.dumps(out))
 
 
