@@ -91,9 +91,10 @@ struct EnvLds {
     uint64_t nbrmask[NC][2];
     int8_t kn[MAX_AGENTS][MAX_KNBR];  // variant 2: the first k packets on the same / an adjacent node
     float node_cnt[NC], node_load[NC];
-    uint32_t rbuf[RNG_BUF];
+    alignas(16) uint32_t rbuf[RNG_BUF];  // rbuf + rtmp (contiguous): also the observation staging image
     uint32_t rtmp[MT_N];
 };
+constexpr int STG_FLOATS = RNG_BUF + MT_N;  // >= one row of either observation at N = 128
 
 template <class ES>
 __device__ void load_topology_lds(const EnvDev& d, int env, ES& s) {
@@ -196,30 +197,43 @@ __device__ void emit_obs(const EnvDev& d, int env, ES& s, const gm_obs_buffers& 
         }
         __syncthreads();
         if (o.node_obs) {
-            // routing.py:187-235. Rows are mostly zeros: zero-fill the env's N x (4N+8) block
-            // (contiguous), then each lane writes the 12 nonzero-capable entries of node v
+            // routing.py:187-235. Rows are mostly zeros: batches of rows are built in an LDS image
+            // (zero-fill, then each lane writes the 12 nonzero-capable entries of its node) and
+            // leave as full 16-byte stores of the env's contiguous N x (4N+8) block, so every HBM
+            // byte is written once (a zero-fill + scatter in HBM costs partial-line rewrites)
             const int ND = 4 * N + 8;
             float* base = o.node_obs + (size_t)env * N * ND;
-            if ((reinterpret_cast<uintptr_t>(base) & 15) == 0) {  // N*ND is a multiple of 4
-                for (int idx = l; idx < N * ND / 4; idx += WAVE)
-                    reinterpret_cast<float4*>(base)[idx] = make_float4(0.f, 0.f, 0.f, 0.f);
-            } else {
-                for (int idx = l; idx < N * ND; idx += WAVE) base[idx] = 0.f;
-            }
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // zeros land before the entries
-            for (int v = l; v < N; v += WAVE) {
-                float* row = base + (size_t)v * ND;
-                row[v] = 1.f;
-                row[N] = s.node_cnt[v];
-                row[N + 1] = s.node_load[v];
+            float* stg = reinterpret_cast<float*>(s.rbuf);  // rbuf + rtmp: the RNG is closed here
+            const int per = STG_FLOATS / ND;
+            const bool vec = (reinterpret_cast<uintptr_t>(base) & 15) == 0;  // N*ND is a multiple of 4
+            for (int v0 = 0; v0 < N; v0 += per) {
+                const int nr = min(per, N - v0), nf = nr * ND;  // nf is a multiple of 4 (ND = 4N+8)
+                for (int i = l; i < nf / 4; i += WAVE) reinterpret_cast<float4*>(stg)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+                __syncthreads();
+                if (l < nr) {
+                    const int v = v0 + l;
+                    float* row = stg + l * ND;
+                    row[v] = 1.f;
+                    row[N] = s.node_cnt[v];
+                    row[N + 1] = s.node_load[v];
 #pragma unroll
-                for (int k = 0; k < 3; k++) {
-                    float* blk = row + N + 2 + k * (N + 2);
-                    const int ne = s.nbr_edge[v * 3 + k];
-                    blk[s.nbr[v * 3 + k]] = 1.f;
-                    blk[N] = (float)s.elen[ne];
-                    blk[N + 1] = (float)s.load[ne];
+                    for (int k = 0; k < 3; k++) {
+                        float* blk = row + N + 2 + k * (N + 2);
+                        const int ne = s.nbr_edge[v * 3 + k];
+                        blk[s.nbr[v * 3 + k]] = 1.f;
+                        blk[N] = (float)s.elen[ne];
+                        blk[N + 1] = (float)s.load[ne];
+                    }
                 }
+                __syncthreads();
+                float* dst = base + (size_t)v0 * ND;
+                if (vec) {
+                    for (int i = l; i < nf / 4; i += WAVE)
+                        reinterpret_cast<float4*>(dst)[i] = reinterpret_cast<const float4*>(stg)[i];
+                } else {
+                    for (int i = l; i < nf; i += WAVE) dst[i] = stg[i];
+                }
+                __syncthreads();
             }
         }
     }
@@ -244,42 +258,59 @@ __device__ void emit_obs(const EnvDev& d, int env, ES& s, const gm_obs_buffers& 
         const int D1 = 6 * N + 10, D = obs_dim_of(N, d.env_var, d.k);
         const size_t ld = o.obs_row_stride;
         float* base = o.obs + (size_t)env * A * ld;
-        {
-            // 16-B stores over the first 4*floor(D1/4) columns when rows are 16-B aligned
-            const int Q = ((ld & 3) == 0 && (reinterpret_cast<uintptr_t>(base) & 15) == 0) ? D1 / 4 : 0;
-            if (Q) {
-                int a = l / Q, q = l - a * Q;
-                for (int idx = l; idx < A * Q; idx += WAVE) {
-                    *reinterpret_cast<float4*>(base + (size_t)a * ld + 4 * q) = make_float4(0.f, 0.f, 0.f, 0.f);
-                    for (q += WAVE; q >= Q; q -= Q) a++;
+        // routing.py:269-315. The INDEPENDENT part of a row has at most 16 nonzero entries:
+        // batches of rows are built in the LDS image (row stride SR = D1 rounded up to 4 floats),
+        // then copied out row by row as 16-byte stores (the last 2 columns of D1 = 4q + 2 as a
+        // pair), each HBM byte written once
+        float* stg = reinterpret_cast<float*>(s.rbuf);
+        const int SR = (D1 + 3) & ~3, Q = D1 / 4, T = D1 - 4 * Q, per = STG_FLOATS / SR;
+        const bool vec = (ld & 3) == 0 && (reinterpret_cast<uintptr_t>(base) & 15) == 0;
+        for (int a0 = 0; a0 < A; a0 += per) {
+            const int nr = min(per, A - a0);
+            for (int i = l; i < nr * SR / 4; i += WAVE) reinterpret_cast<float4*>(stg)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+            __syncthreads();
+            if (l < nr) {
+                const int a = a0 + l;
+                float* row = stg + l * SR;
+                const int now = s.now[a], e = s.edge[a];
+                row[now] = 1.f;
+                row[N + s.target[a]] = 1.f;
+                row[2 * N] = (float)(e != -1);
+                if (e >= 0) row[2 * N + 1 + (s.ea[e] ^ s.eb[e] ^ now)] = 1.f;
+                row[3 * N + 1] = (float)s.time[a];
+                row[3 * N + 2] = (float)s.size[a];
+                row[3 * N + 3] = (float)a;
+#pragma unroll
+                for (int k = 0; k < 3; k++) {
+                    float* blk = row + 3 * N + 4 + k * (N + 2);
+                    const int ne = s.nbr_edge[now * 3 + k];
+                    blk[s.nbr[now * 3 + k]] = 1.f;
+                    blk[N] = (float)s.elen[ne];
+                    blk[N + 1] = (float)s.load[ne];
                 }
             }
-            const int T = D1 - 4 * Q;  // remaining columns [4Q, D1) of every row
-            int a = l / T, c = l - a * T;
-            for (int idx = l; idx < A * T; idx += WAVE) {
-                base[(size_t)a * ld + 4 * Q + c] = 0.f;
-                for (c += WAVE; c >= T; c -= T) a++;
+            __syncthreads();
+            if (vec) {
+                const int Qr = Q + (T ? 1 : 0);  // 16-B chunks per row, the last one partial (T = 2)
+                for (int i = l; i < nr * Qr; i += WAVE) {
+                    const int r = i / Qr, q = i - r * Qr;
+                    const float4 v = *reinterpret_cast<const float4*>(stg + r * SR + 4 * q);
+                    float* dst = base + (size_t)(a0 + r) * ld + 4 * q;
+                    if (q < Q) {
+                        *reinterpret_cast<float4*>(dst) = v;
+                    } else if (T == 2) {  // D1 = 6N + 10 with N even
+                        *reinterpret_cast<float2*>(dst) = make_float2(v.x, v.y);
+                    } else {
+                        for (int c = 0; c < T; c++) dst[c] = stg[r * SR + 4 * q + c];
+                    }
+                }
+            } else {
+                for (int i = l; i < nr * D1; i += WAVE) {
+                    const int r = i / D1, c = i - r * D1;
+                    base[(size_t)(a0 + r) * ld + c] = stg[r * SR + c];
+                }
             }
-        }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // zeros land before the entries
-        if (l < A) {
-            float* row = base + (size_t)l * ld;
-            const int now = s.now[l], e = s.edge[l];
-            row[now] = 1.f;
-            row[N + s.target[l]] = 1.f;
-            row[2 * N] = (float)(e != -1);
-            if (e >= 0) row[2 * N + 1 + (s.ea[e] ^ s.eb[e] ^ now)] = 1.f;
-            row[3 * N + 1] = (float)s.time[l];
-            row[3 * N + 2] = (float)s.size[l];
-            row[3 * N + 3] = (float)l;
-#pragma unroll
-            for (int k = 0; k < 3; k++) {
-                float* blk = row + 3 * N + 4 + k * (N + 2);
-                const int ne = s.nbr_edge[now * 3 + k];
-                blk[s.nbr[now * 3 + k]] = 1.f;
-                blk[N] = (float)s.elen[ne];
-                blk[N + 1] = (float)s.load[ne];
-            }
+            __syncthreads();
         }
         if (D > D1) {  // variant columns (2: k neighbour slots, 3: global), lane-strided per row
             for (int a = 0; a < A; a++) {
