@@ -66,6 +66,15 @@ __device__ __forceinline__ int members(const int32_t* nb, int deg, int n, int* o
     return cnt;
 }
 
+// XCD-aware block order: the hardware deals block b to XCD b % 8; logical block numbers are
+// handed out so that each XCD gets one contiguous run of rows, and the 4 rows every node reads
+// (itself + 3 neighbours of the same graph) sit in that XCD's L2 instead of being fetched once per
+// XCD that touches the graph (a graph's 20 rows span 3 consecutive 8-row blocks)
+__device__ __forceinline__ unsigned xcd_block(unsigned bid, unsigned T) {
+    const unsigned q = T / 8, r = T % 8, x = bid % 8, loc = bid / 8;
+    return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + loc;
+}
+
 // forward: out[n] = Σ_{m ∈ {n} ∪ nbr(n)} h[m]  (/ count for mean)
 // backward (symmetric adjacency): dh[j] = Σ_{n ∈ {j} ∪ nbr(j)} dout[n] * scale(n)
 template <bool BWD, int V>
@@ -73,7 +82,7 @@ __global__ __launch_bounds__(256) void k_mp_aggregate(const float* __restrict__ 
                                                       int G, int N, int deg, int H, int mode, float* __restrict__ out,
                                                       long long ldh, long long ldo) {
     const int HV = H / V;
-    const long long gid = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    const long long gid = (long long)xcd_block(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x;
     const long long total = (long long)G * N * HV;
     if (gid >= total) return;
     const int cv = (int)(gid % HV);
@@ -84,6 +93,26 @@ __global__ __launch_bounds__(256) void k_mp_aggregate(const float* __restrict__ 
     const int cnt = members(nb, deg, n, mem);
     const float* src = h + (size_t)g * N * ldh + (size_t)cv * V;
     Vec<V> acc = zerov<V>();
+    if (!BWD && deg <= 3) {
+        // routing graphs (degree 3): the up to 4 member rows are loaded back to back (independent
+        // loads in flight together), then summed in ascending id order like the general loop
+        Vec<V> x[4];
+#pragma unroll
+        for (int q = 0; q < 4; q++) x[q] = q < cnt ? ldv<V>(src + (size_t)mem[q] * ldh) : zerov<V>();
+        acc = x[0];
+#pragma unroll
+        for (int q = 1; q < 4; q++)
+            if (q < cnt) {
+#pragma unroll
+                for (int i = 0; i < V; i++) acc.v[i] = acc.v[i] + x[q].v[i];
+            }
+        if (mode == 1) {
+#pragma unroll
+            for (int i = 0; i < V; i++) acc.v[i] = acc.v[i] / cnt;
+        }
+        stv<V>(out + row * ldo + (size_t)cv * V, acc);
+        return;
+    }
     for (int q = 0; q < cnt; q++) {
         Vec<V> x = ldv<V>(src + (size_t)mem[q] * ldh);
         if (BWD && mode == 1) {
