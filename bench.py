@@ -169,7 +169,7 @@ def measure_train(args, gm, M, W, P, net, netmon, dqn, dev, world, rank):
         if update:
             dqn.train()
             netmon.train()
-            batches = list(buff.get_batch(bsz, sequence_length=L_))
+            batches = list(buff.get_batch(bsz, sequence_length=L_, lazy_next=True))
             T.dqn_update(netmon, dqn, model_tar, opt, params, batches, 0.98, 0.01, consecutive=True)
             dqn.eval()
             netmon.eval()

@@ -429,7 +429,8 @@ def main(argv=None):
             model.train()
             if netmon is not None:
                 netmon.train()
-            batches = list(buff.get_batch(args.mini_batch_size, sequence_length=args.sequence_length))
+            batches = list(buff.get_batch(args.mini_batch_size, sequence_length=args.sequence_length,
+                                          lazy_next=True))
             parts = {}
             loss, qs, qts = T.dqn_update(netmon, model, model_tar, optimizer, params, batches, args.gamma, args.tau,
                                          args.target_update_steps, iteration,

@@ -639,6 +639,7 @@ class NetMon(nn.Module):
             raise ValueError("rnn_carryover=False needs netmon iterations >= 1 (the reference's update "
                              "cell output is the stored state)")
         self.encode = MLP(in_features, (*encoder_units, hidden_features))
+        self._hc = None  # carry-over LSTM state kept as its (h, c) rows (training), see state
         self.state = None
         self.iterations = iterations
         self.output_neighbor_hidden = output_neighbor_hidden
@@ -667,6 +668,35 @@ class NetMon(nn.Module):
             self.num_states *= 2
         self.hidden_features = hidden_features
         self.state_size = hidden_features * self.num_states
+
+    # The reference's mutable state tensor [B, N, state_size] (src/model.py:403-415, 447-449). A
+    # carry-over lstm / lnlstm step with gradient leaves it as its (h, c) row tensors instead
+    # (no stack, no split copies on the next step); reading .state stacks them on demand.
+    @property
+    def state(self):
+        if self._state is None and self._hc is not None:
+            h, c, B, N = self._hc
+            self._state = torch.stack((h, c), 1).reshape(B, N, self.state_size)
+        return self._state
+
+    @state.setter
+    def state(self, value):
+        self._state = value
+        self._hc = None
+
+    def state_hc(self):
+        """(h, c, B, N) of a state held as rows, or None."""
+        return self._hc
+
+    def set_state_hc(self, h, c, B, N):
+        self._state = None
+        self._hc = (h, c, B, N)
+
+    def save_state(self):
+        return self._state, self._hc
+
+    def restore_state(self, tok):
+        self._state, self._hc = tok
 
     def get_out_features(self):
         """src/model.py:403-415 for routing graphs (max degree 3): h, [global mean], [3 neighbours]."""
@@ -701,13 +731,17 @@ class NetMon(nn.Module):
         Returns [B, A or N, 4H] (or writes into `out` [B, A, W] at column out_col)."""
         B, N, Fdim = x.shape
         H = self.hidden_features
-        if self.state is None:
-            self.state = torch.zeros(B, N, self.state_size, device=x.device)
         nc = self.cell_states
-        st = self.state.reshape(B * N, self.num_states, H)
+        if self._hc is not None:
+            hs, cs = self._hc[0], self._hc[1]
+            st = None
+        else:
+            if self.state is None:
+                self.state = torch.zeros(B, N, self.state_size, device=x.device)
+            st = self.state.reshape(B * N, self.num_states, H)
+            hs, cs = st[:, 0].contiguous(), (st[:, 1].contiguous() if nc == 2 else None)
         h = self._encode(x.reshape(B * N, Fdim), nbr, B, N)
-        hs, cs = st[:, 0], (st[:, 1] if nc == 2 else None)
-        h, c = self._cell(self.rnn_obs, h, hs.contiguous(), None if cs is None else cs.contiguous())
+        h, c = self._cell(self.rnn_obs, h, hs, cs)
         h0, c0 = h, c
         last_nbr = torch.zeros_like(h) if self.iterations <= 0 else None
         for it in range(self.iterations):
@@ -719,7 +753,9 @@ class NetMon(nn.Module):
                 hin = st[:, nc].contiguous()
                 cin = st[:, nc + 1].contiguous() if nc == 2 else None
             h, c = self._cell(self.rnn_update, M, hin, cin)
-        if self.rnn_carryover:
+        if self.rnn_carryover and c is not None and torch.is_grad_enabled():
+            self.set_state_hc(h, c, B, N)  # stacked only when .state is read
+        elif self.rnn_carryover:
             self.state = (torch.stack((h, c), 1) if c is not None else h.unsqueeze(1)).reshape(B, N, self.state_size)
         elif nc == 2:
             self.state = torch.stack((h0, c0, h, c), 1).reshape(B, N, self.state_size)

@@ -32,6 +32,25 @@ TransitionBatch = namedtuple(
 )
 
 
+class LazyRows:
+    """A field of a sampled batch gathered on demand: [r] gathers the rows r of the batch,
+    full() all of them (ReplayBuffer.get_batch(lazy_next=True): the update's target pass needs
+    the next observations only at the last step of a sequence and at episode ends)."""
+
+    def __init__(self, src, slot, env, conv):
+        self.src, self.slot, self.env, self.conv = src, slot, env, conv
+
+    def __getitem__(self, r):
+        return self.conv(self.src[self.slot[r], self.env[r]])
+
+    def full(self):
+        return self.conv(self.src[self.slot, self.env])
+
+
+def materialize(x):
+    return x.full() if isinstance(x, LazyRows) else x
+
+
 class ReplayBuffer:
     def __init__(self, seed, capacity, n_env, n_agents, obs_dim, n_nodes, node_obs_dim, node_state_size,
                  device, half_precision=False, nbr_width=3, agent_state_size=0, store_adj=False, node_aux_size=0):
@@ -131,12 +150,28 @@ class ReplayBuffer:
         self.add_pre(obs, node_state, node_obs, nbr, agent_node)
         self.add_post(action, reward, next_obs, done, episode_done, next_node_obs, next_agent_node)
 
-    def _gather(self, slot, env, first=True):
+    def _gather(self, slot, env, first=True, lazy_next=False):
         """One TransitionBatch of the (slot, env) pairs. The stored start states (NetMon node state,
         agent state) are read by the update at the first step of a sequence only
         (src/main.py:846-851, 858-859), so later steps leave them out (None)."""
         f = torch.float32
         g = self.graph
+        if lazy_next:
+            od = self.obs_dim
+            return TransitionBatch(
+                (slot, env), self.obs[slot, env].to(f)[..., :od], self.action[slot, env].long(),
+                self.reward[slot, env].to(f), LazyRows(self.next_obs, slot, env, lambda t: t.to(f)[..., :od]),
+                self.done[slot, env], self.episode_done[slot], self.node_obs[slot, env].to(f) if g else None,
+                self.nbr[slot, env].int().contiguous() if g else None,
+                self.node_state[slot, env].to(f) if g and first else None,
+                self.agent_node[slot, env].int().contiguous() if g else None,
+                LazyRows(self.next_node_obs, slot, env, lambda t: t.to(f)) if g else None,
+                LazyRows(self.next_agent_node, slot, env, lambda t: t.int().contiguous()) if g else None,
+                self.adj[slot, env].to(f) if self.adj is not None else None,
+                LazyRows(self.next_adj, slot, env, lambda t: t.to(f)) if self.next_adj is not None else None,
+                self.agent_state[slot, env].to(f) if self.agent_state is not None and first else None,
+                self.node_aux[slot, env].to(f) if self.node_aux is not None else None,
+            )
         return TransitionBatch(
             (slot, env), self.obs[slot, env].to(f)[..., : self.obs_dim], self.action[slot, env].long(),
             self.reward[slot, env].to(f), self.next_obs[slot, env].to(f)[..., : self.obs_dim], self.done[slot, env],
@@ -165,10 +200,11 @@ class ReplayBuffer:
         return {"state": (st.state_hi << 64) | st.state_lo, "inc": (st.inc_hi << 64) | st.inc_lo,
                 "has_uint32": st.has_uint32, "uinteger": st.uinteger}
 
-    def get_batch(self, batch_size, sequence_length=1):
+    def get_batch(self, batch_size, sequence_length=1, lazy_next=False):
         """Yields sequence_length TransitionBatches of batch_size transitions
         (src/replaybuffer.py:103-130): uniform (slot, env); sequences are consecutive slots of
-        one env, starting from the oldest slot and wrapping."""
+        one env, starting from the oldest slot and wrapping. lazy_next: the next-step fields of
+        every step but the last are LazyRows (gathered on demand)."""
         if self.count == 0:
             raise ValueError("empty replay buffer")
         if sequence_length <= 1:
@@ -182,4 +218,5 @@ class ReplayBuffer:
         env = f // span
         first = (self.index % self.count + f % span) % self.count
         for o in range(sequence_length):
-            yield self._gather((first + o) % self.count, env, first=o == 0)
+            yield self._gather((first + o) % self.count, env, first=o == 0,
+                               lazy_next=lazy_next and o < sequence_length - 1)

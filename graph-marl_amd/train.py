@@ -105,13 +105,30 @@ def _fused_next_q(netmon, model_tar, next_obs, next_node_obs, nbr, next_agent_no
     B, A, od = next_obs.shape
     odp = (od + 3) // 4 * 4  # 16-byte rows for the GEMM's dense source
     env_obs = next_obs.contiguous() if odp == od else F.pad(next_obs, (0, odp - od))
-    keep = netmon.state
+    keep = netmon.save_state()
     st, h_prev = FU.netmon_step(netmon, next_node_obs, nbr.contiguous(), state.detach().contiguous())
-    netmon.state = keep
+    netmon.restore_state(keep)
     dev = env_obs.device
     q = FU.dqn_q(model_tar, env_obs, od, st, h_prev, nbr.contiguous(), next_agent_node.contiguous(),
                  lambda i, m, n: torch.empty(m, n, device=dev), hidden=netmon.hidden_features)
     return q.view(B, A, -1)
+
+
+class _StateRows:
+    """A NetMon state held as its (h, c) rows [B*N, H] (NetMon.state_hc), detached; full() is the
+    [B, N, 2H] tensor, [r] the rows of the samples r stacked ([len(r), N, 2H])."""
+
+    def __init__(self, hc):
+        h, c, self.B, self.N = hc
+        self.h, self.c = h.detach(), c.detach()
+
+    def full(self):
+        return torch.stack((self.h, self.c), 1).reshape(self.B, self.N, -1)
+
+    def __getitem__(self, r):
+        H = self.h.shape[-1]
+        return torch.stack((self.h.view(self.B, self.N, H)[r], self.c.view(self.B, self.N, H)[r]), 2).reshape(
+            len(r), self.N, 2 * H)
 
 
 @torch.no_grad()
@@ -130,8 +147,9 @@ def _reused_next_q(netmon, model_tar, batches, joints, states):
     out = []
     for t, batch in enumerate(batches):
         if t == L_ - 1:
+            st_t = states[t].full() if isinstance(states[t], _StateRows) else states[t]
             q = _fused_next_q(netmon, model_tar, batch.next_obs, batch.next_node_obs, batch.nbr,
-                              batch.next_agent_node, states[t])
+                              batch.next_agent_node, st_t)
             out.append(q.max(dim=2)[0])
             continue
         x = joints[t + 1]
@@ -172,12 +190,18 @@ def dqn_loss(netmon, model, model_tar, batches, gamma, att_coeff=0.0, aux_model=
     has_state = hasattr(model, "state")
     loss_q = loss_att = loss_aux = None
     qs, qts = [], []
-    last_state = last_ep_done = None
+    last_state = last_ep_done = last_hc = None
     fused_tar = not has_state and _fused_target_ok(netmon, model_tar) and FUSED_TARGET
     reuse = fused_tar and consecutive and att_coeff == 0
     # DQN on NetMon: the first layer reads the env obs and the graph obs as two GEMM sources
     split = netmon is not None and type(model).__name__ == "DQN" and hasattr(model, "forward_split")
     joints, states, next_max = [], [], []
+    if not reuse:  # lazily gathered next-step fields (ReplayBuffer.get_batch(lazy_next=True)) in full
+        from .replaybuffer import materialize
+
+        batches = [b._replace(next_obs=materialize(b.next_obs), next_node_obs=materialize(b.next_node_obs),
+                              next_agent_node=materialize(b.next_agent_node), next_adj=materialize(b.next_adj))
+                   for b in batches]
     for t, batch in enumerate(batches):
         if has_state and t == 0:
             model.state = batch.agent_state
@@ -186,6 +210,10 @@ def dqn_loss(netmon, model, model_tar, batches, gamma, att_coeff=0.0, aux_model=
         else:
             if t == 0:
                 netmon.state = batch.node_state
+            elif last_hc is not None:  # (h, c) rows: mask them apart, no stacked state
+                h_, c_, B_, N_ = last_hc
+                m = (~last_ep_done).repeat_interleave(N_).view(-1, 1)
+                netmon.set_state_hc(h_ * m, c_ * m, B_, N_)
             else:
                 netmon.state = last_state * (~last_ep_done).view(-1, 1, 1)
             graph = netmon.forward_graph(batch.node_obs, batch.nbr, batch.agent_node)
@@ -193,7 +221,8 @@ def dqn_loss(netmon, model, model_tar, batches, gamma, att_coeff=0.0, aux_model=
             if aux_model is not None:
                 term = torch.mean((aux_model(netmon.state) - batch.node_aux) ** 2) / L
                 loss_aux = term if loss_aux is None else loss_aux + term
-            last_state = netmon.state
+            last_hc = netmon.state_hc()
+            last_state = netmon.state if last_hc is None else None
             last_ep_done = batch.episode_done.expand(batch.obs.shape[0]) if batch.episode_done.dim() == 0 \
                 else batch.episode_done
             next_obs = None
@@ -201,14 +230,16 @@ def dqn_loss(netmon, model, model_tar, batches, gamma, att_coeff=0.0, aux_model=
         qs.append(q)
         if reuse:  # targets after the online pass over the whole sequence
             joints.append((obs[0], obs[1].detach()) if split else obs.detach())
-            states.append(last_state.detach())
+            states.append(_StateRows(last_hc) if last_hc is not None else last_state.detach())
             continue
         with torch.no_grad():
             if has_state:
                 model_tar.state = model.state.detach()
             if fused_tar:
+                hc = netmon.state_hc()
+                st_now = _StateRows(hc).full() if hc is not None else netmon.state
                 next_q_max = _fused_next_q(netmon, model_tar, batch.next_obs, batch.next_node_obs, batch.nbr,
-                                           batch.next_agent_node, netmon.state).max(dim=2)[0]
+                                           batch.next_agent_node, st_now).max(dim=2)[0]
             else:
                 if netmon is not None:
                     nno = netmon.forward_graph(batch.next_node_obs, batch.nbr, batch.next_agent_node)

@@ -121,6 +121,7 @@ def test_replay_sequences_and_full_update_on_env_data():
         if (t + 1) % 10 == 0:
             wenv.reset()
     assert rb.count == 30
+    rng0 = rb.rng.clone()
     seqs = list(rb.get_batch(16, sequence_length=4))
     slots = torch.stack([s.idx[0] for s in seqs])
     envs = torch.stack([s.idx[1] for s in seqs])
@@ -148,6 +149,15 @@ def test_replay_sequences_and_full_update_on_env_data():
     torch.testing.assert_close(l2, l0, rtol=1e-5, atol=1e-7)
     eps = torch.stack([s.episode_done for s in seqs[:-1]])
     assert eps.any() and not eps.all()  # both target branches ran
+    # the same sequences with the next-step fields gathered on demand (lazy_next)
+    rb.rng.copy_(rng0)
+    lazy = list(rb.get_batch(16, sequence_length=4, lazy_next=True))
+    assert all(torch.equal(a.idx[0], b.idx[0]) for a, b in zip(lazy, seqs))
+    with torch.no_grad():
+        l3, _, t3 = T.dqn_loss(netmon, model, target, lazy, 0.9, consecutive=True)
+        l4, _, t4 = T.dqn_loss(netmon, model, target, lazy, 0.9)  # plain pass materialises them
+    assert torch.equal(l3, l2) and all(torch.equal(a, b) for a, b in zip(t3, t2))
+    torch.testing.assert_close(l4, l0, rtol=1e-5, atol=1e-7)
     params = list(model.parameters()) + list(netmon.parameters())
     before = [p.detach().clone() for p in params]
     opt = torch.optim.AdamW(params, lr=1e-3)
