@@ -27,7 +27,7 @@ EXPORTS = [
     "gm_env_step", "gm_env_observe", "gm_env_topology", "gm_env_final_info", "gm_policy_egreedy",
     "gm_env_get_state", "gm_env_set_state", "gm_build_seed_list", "gm_mp_aggregate", "gm_mp_aggregate_rows", "gm_mp_aggregate_bwd", "gm_leaky_bwd", "gm_netmon_readout",
     "gm_netmon_readout_bwd", "gm_lstm_pointwise", "gm_lstm_pointwise_bwd", "gm_linear_f32", "gm_gemm_f32",
-    "gm_gemm_set_tile", "gm_gemm_set_wgrad", "gm_simple_create", "gm_simple_destroy", "gm_simple_reset", "gm_simple_step",
+    "gm_gemm_set_tile", "gm_gemm_set_wgrad", "gm_gemm_set_mfma", "gm_simple_create", "gm_simple_destroy", "gm_simple_reset", "gm_simple_step",
     "gm_simple_observe", "gm_simple_policy_egreedy", "gm_simple_get_state", "gm_env_set_topology",
     "gm_policy_shortest_path", "gm_env_first_hops", "gm_routing_node_encoder", "gm_gemm_x3", "gm_gemm_x3_head", "gm_absmax_scale", "gm_absmax_scale_rows", "gm_gemm_x3_wgrad", "gm_absmax_finish",
     "gm_gemm_pack_x3", "gm_gemm_pack_x3_bytes", "gm_gemm_range_status",
@@ -40,6 +40,12 @@ EXPORTS = [
 GEMM_MODE = os.environ.get("GM_GEMM", "x3")
 if GEMM_MODE not in ("x3", "f32"):
     raise ValueError(f"GM_GEMM must be 'x3' or 'f32', not {GEMM_MODE!r}")
+# MFMA shape of the LDS-DMA split-f16 kernel (gm_gemm_set_mfma): GM_MFMA=16 (16x16x32 except the
+# fused Q head: the library default), 32 (32x32x16) or 16all (16x16x32 everywhere); unset leaves
+# the library default
+MFMA_SHAPE = os.environ.get("GM_MFMA")
+if MFMA_SHAPE not in (None, "16", "32", "16all"):
+    raise ValueError(f"GM_MFMA must be '16', '32' or '16all', not {MFMA_SHAPE!r}")
 
 
 class EnvConfig(C.Structure):
@@ -113,6 +119,7 @@ def lib():
     L.gm_linear_f32.argtypes = [vp, i64, vp, i64, vp, i32, i32, i32, i32, vp, i64, vp]
     L.gm_gemm_set_tile.argtypes = [i32]
     L.gm_gemm_set_wgrad.argtypes = [i32]
+    L.gm_gemm_set_mfma.argtypes = [i32]
     L.gm_env_set_topology.argtypes = [vp, i32, i64, vp, i32, i32]
     L.gm_policy_shortest_path.argtypes = [vp, vp, vp]
     L.gm_env_first_hops.argtypes = [vp, vp, vp]
@@ -126,6 +133,9 @@ def lib():
     L.gm_pcg64_seed.argtypes = [C.c_uint64, C.POINTER(PCG64)]
     L.gm_pcg64_choice.argtypes = [vp, i64, i64, vp, vp]
     L.gm_lnlstm_pointwise.argtypes = [vp, i64, vp, i64] + [vp] * 7 + [i32, i32, C.c_float, vp, i64, vp, i64, vp]
+    if MFMA_SHAPE is not None:
+        if L.gm_gemm_set_mfma({"16": 1, "32": 0, "16all": 2}[MFMA_SHAPE]) != 0:
+            raise GMError(L.gm_last_error().decode())
     _lib = L
     return L
 

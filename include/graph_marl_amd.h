@@ -345,6 +345,11 @@ int gm_agent_comm(const float* h, int64_t ldh, const int8_t* adj, int32_t B, int
  * with 128 x 256 tiles, 0 = the dword-load register-transpose form (tools/wgrad_bench.py). */
 int gm_gemm_set_wgrad(int32_t form);
 int gm_gemm_set_tile(int32_t tile);
+/* MFMA shape of the LDS-DMA split-f16 kernel (gm_gemm_x3's dense / readout tiles, gm_gemm_x3_head):
+ * 1 (default) = v_mfma_f32_16x16x32_f16 except gm_gemm_x3_head (32x32x16), 0 = v_mfma_f32_32x32x16_f16
+ * everywhere, 2 = 16x16x32 everywhere. Same tiles and operand images; the summation order inside
+ * an MFMA differs (fp32-order results either way). */
+int gm_gemm_set_mfma(int32_t shape);
 
 /* ---------------------------------------------------------------------------
  * SimpleEnvironment (src/env/simple_environment.py:45-334; BASELINE config 1):

@@ -178,13 +178,16 @@ def test_routing_node_encoder_vs_torch(n, out):
     assert err < 1e-5, err
 
 
+@pytest.mark.parametrize("mfma", [1, 0])
 @pytest.mark.parametrize("tile", [8, 9, 10, 11, 12, 13, 14])
-def test_gemm_lds_dma_tiles(tile):
-    """The LDS-DMA x3 kernel (tiles 8..14): dense (ragged M/N/K, padded rows), two sources
-    with the LSTM epilogue, and the DQN readout gather of the fused rollout, vs fp64 / torch."""
+def test_gemm_lds_dma_tiles(tile, mfma):
+    """The LDS-DMA x3 kernel (tiles 8..14, 16x16x32 and 32x32x16 MFMA forms): dense (ragged M/N/K,
+    padded rows), two sources with the LSTM epilogue, and the DQN readout gather of the fused
+    rollout, vs fp64 / torch."""
     gm, M, FU, W = mods()
     lib = FU._setup()
     lib.gm_gemm_set_tile(tile)
+    FU.L.check(lib.gm_gemm_set_mfma(mfma))
     try:
         for (m, n, k, ldx) in [(81920, 512, 642, 644), (1000, 256, 512, 512), (777, 130, 90, 92),
                                (4097, 33, 129, 132), (300, 64, 16, 16)]:
@@ -205,15 +208,26 @@ def test_gemm_lds_dma_tiles(tile):
             FU.L.GEMM_MODE = old
     finally:
         lib.gm_gemm_set_tile(-1)
+        lib.gm_gemm_set_mfma(1)
 
 
 @pytest.mark.parametrize("m,n,k,ldx,nq", [(81920, 256, 512, 512, 4), (1000, 256, 512, 516, 4), (777, 100, 90, 92, 2),
                                           (33, 256, 256, 256, 3), (5, 64, 16, 16, 1)])
 @pytest.mark.parametrize("act", [0, 1])
-def test_gemm_x3_head_vs_torch(m, n, k, ldx, nq, act):
-    """gm_gemm_x3_head (last DQN layer + Q head in one kernel) vs fp64: q within the rollout
-    tolerance, and the optional hidden output equal to the plain split-f16 GEMM's."""
+@pytest.mark.parametrize("mfma", [1, 2])
+def test_gemm_x3_head_vs_torch(m, n, k, ldx, nq, act, mfma):
+    """gm_gemm_x3_head (last DQN layer + Q head in one kernel; 32x32x16 and 16x16x32 MFMA forms)
+    vs fp64: q within the rollout tolerance, and the optional hidden output equal to the plain
+    split-f16 GEMM's."""
     gm, M, FU, W = mods()
+    FU.L.check(FU._setup().gm_gemm_set_mfma(mfma))
+    try:
+        _head_case(M, FU, m, n, k, ldx, nq, act)
+    finally:
+        FU._setup().gm_gemm_set_mfma(1)
+
+
+def _head_case(M, FU, m, n, k, ldx, nq, act):
     torch.manual_seed(m + n + k + nq)
     buf = torch.randn(m, ldx, device="cuda")
     x = buf[:, :k]

@@ -9,7 +9,7 @@ rows = list(csv.DictReader(open(sys.argv[1] if len(sys.argv) > 1 else "gpurun_ou
 rows.sort(key=lambda r: int(r["Start_Timestamp"]))
 idx = [i for i, r in enumerate(rows) if "pcg64" in r["Kernel_Name"]]
 seq = rows[idx[-1]:]
-b = [i for i, r in enumerate(seq) if "kmajor" in r["Kernel_Name"]][0]
+b = [i for i, r in enumerate(seq) if "kmajor" in r["Kernel_Name"] or "wgrad" in r["Kernel_Name"]][0]
 
 
 def dur(r):
