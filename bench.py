@@ -63,6 +63,8 @@ def parse():
     p.add_argument("--train-batch", type=int, default=0,
                    help="sequences per update (0: 32 * n_env / 10 = the reference replay ratio, SURVEY 8d)")
     p.add_argument("--train-seq", type=int, default=8, help="sequence length of an update")
+    p.add_argument("--train-autograd", action="store_true",
+                   help="training leg on the per-step autograd path (train.dqn_update) instead of train_seq")
     p.add_argument("--cpu-envs", type=int, default=1024)
     p.add_argument("--cpu-steps", type=int, default=50, help="one full episode (includes its reset)")
     return p.parse_args()
@@ -136,6 +138,7 @@ def measure_train(args, gm, M, W, P, net, netmon, dqn, dev, world, rank):
     import importlib as il
 
     T = il.import_module("graph-marl_amd.train")
+    TS = il.import_module("graph-marl_amd.train_seq")
     RB = il.import_module("graph-marl_amd.replaybuffer")
     B = args.n_env
     env = gm.Routing(net, args.n_data, n_env=B, seed=rank * B, obs_extra=netmon.get_out_features(),
@@ -153,6 +156,7 @@ def measure_train(args, gm, M, W, P, net, netmon, dqn, dev, world, rank):
     buff = RB.ReplayBuffer(0, slots * B, B, env.n_data, env.obs_dim, env.n_nodes, env.node_obs_dim,
                            netmon.get_state_size(), dev, nbr_width=env.nbr.shape[-1])
     ep = {"n": 0}
+    seq_path = not args.train_autograd and TS.seq_ok(netmon, dqn, model_tar)
 
     def vstep(update):
         if ep["n"] == 0:
@@ -169,8 +173,11 @@ def measure_train(args, gm, M, W, P, net, netmon, dqn, dev, world, rank):
         if update:
             dqn.train()
             netmon.train()
-            batches = list(buff.get_batch(bsz, sequence_length=L_, lazy_next=True))
-            T.dqn_update(netmon, dqn, model_tar, opt, params, batches, 0.98, 0.01, consecutive=True)
+            if seq_path:  # sequence-batched update with the hand-written backward (train_seq.py)
+                TS.dqn_update_seq(netmon, dqn, model_tar, opt, params, buff.get_sequences(bsz, L_), 0.98, 0.01)
+            else:
+                batches = list(buff.get_batch(bsz, sequence_length=L_, lazy_next=True))
+                T.dqn_update(netmon, dqn, model_tar, opt, params, batches, 0.98, 0.01, consecutive=True)
             dqn.eval()
             netmon.eval()
             netmon.state = None
@@ -196,6 +203,7 @@ def measure_train(args, gm, M, W, P, net, netmon, dqn, dev, world, rank):
     return {"value": round(B * world * args.train_steps / el, 1), "unit": "env-steps/s", "n_env_per_gpu": B,
             "ms_per_step": round(1e3 * el / args.train_steps, 3), "steps": args.train_steps,
             "update": {"sequences": bsz, "seq_len": L_, "graph_steps": bsz * L_,
+                       "path": "train_seq (sequence-batched)" if seq_path else "train.dqn_update (autograd)",
                        "per": "vector step of n_env envs (replay ratio 25.6 = reference B=32, L=8 every 10 steps)"}}
 
 

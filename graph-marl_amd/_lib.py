@@ -32,6 +32,7 @@ EXPORTS = [
     "gm_policy_shortest_path", "gm_env_first_hops", "gm_routing_node_encoder", "gm_gemm_x3", "gm_gemm_x3_head", "gm_absmax_scale", "gm_absmax_scale_rows", "gm_gemm_x3_wgrad", "gm_absmax_finish",
     "gm_gemm_pack_x3", "gm_gemm_pack_x3_bytes", "gm_gemm_range_status",
     "gm_pcg64_seed", "gm_pcg64_choice", "gm_lnlstm_pointwise", "gm_agent_attention", "gm_agent_comm",
+    "gm_gemm_x3_dgrad", "gm_lstm_cell_bwd", "gm_qhead_bwd", "gm_netmon_readout_ld",
 ]
 
 # Arithmetic form of the fused rollout GEMMs (graph-marl_amd/fused.py): "x3" = split-f16
@@ -80,6 +81,21 @@ class PCG64(C.Structure):
                 ("has_uint32", C.c_uint32), ("uinteger", C.c_uint32)]
 
 
+class LSTMBwdArgs(C.Structure):
+    """gm_lstm_bwd_args (include/graph_marl_amd.h)."""
+    _fields_ = [
+        ("act", C.c_void_p), ("ld_act", C.c_int64), ("c_in", C.c_void_p), ("ld_cin", C.c_int64),
+        ("c_out", C.c_void_p), ("ld_cout", C.c_int64), ("dh0", C.c_void_p), ("ld_dh0", C.c_int64),
+        ("dh1", C.c_void_p), ("ld_dh1", C.c_int64), ("dm", C.c_void_p), ("ld_dm", C.c_int64),
+        ("nbr", C.c_void_p), ("n_nodes", C.c_int32), ("deg", C.c_int32), ("mean", C.c_int32),
+        ("dh_ext", C.c_void_p), ("ld_ext", C.c_int64), ("dc_ext", C.c_void_p), ("ld_dcext", C.c_int64),
+        ("ext_mask", C.c_void_p), ("rows_per_sample", C.c_int32), ("dc", C.c_void_p), ("ld_dc", C.c_int64),
+        ("m", C.c_int32), ("hidden", C.c_int32), ("dgates", C.c_void_p), ("ld_dg", C.c_int64),
+        ("dc_out", C.c_void_p), ("ld_dco", C.c_int64), ("bias_part", C.c_void_p), ("rows_per_block", C.c_int32),
+        ("dg_scale", C.c_void_p), ("dg_max", C.c_void_p),
+    ]
+
+
 class GMError(RuntimeError):
     pass
 
@@ -120,6 +136,9 @@ def lib():
     L.gm_gemm_set_tile.argtypes = [i32]
     L.gm_gemm_set_wgrad.argtypes = [i32]
     L.gm_gemm_set_mfma.argtypes = [i32]
+    L.gm_lstm_cell_bwd.argtypes = [C.POINTER(LSTMBwdArgs), vp]
+    L.gm_qhead_bwd.argtypes = [vp, i64, i32, vp, i64, vp, i64, i64, i32, i32, vp, i64, vp, vp, vp, i32, vp, vp]
+    L.gm_netmon_readout_ld.argtypes = [vp, i64, vp, i64, vp, vp, i32, i32, i32, i32, i32, vp, i64, vp]
     L.gm_env_set_topology.argtypes = [vp, i32, i64, vp, i32, i32]
     L.gm_policy_shortest_path.argtypes = [vp, vp, vp]
     L.gm_env_first_hops.argtypes = [vp, vp, vp]

@@ -56,7 +56,7 @@ typedef float floatx4 __attribute__((ext_vector_type(4)));
 
 constexpr int BKMAX = 32;            // largest K tile of any configuration (host-side checks)
 constexpr int OOB = 0x7ff00000;       // byte offset beyond any buffer: load returns 0
-enum { EPI_BIAS = 0, EPI_LSTM = 1, EPI_HEAD = 2 };
+enum { EPI_BIAS = 0, EPI_LSTM = 1, EPI_HEAD = 2, EPI_DGRAD = 3 };
 
 struct ASrc {
     int mode;                 // GM_A_DENSE / GM_A_AGGREGATE / GM_A_READOUT
@@ -90,6 +90,15 @@ struct Epi {
     long long ldq;
     unsigned* range_flag;     // X3: set to 1 when an accumulator is not finite (host-mapped; nullable)
     int cell;                 // EPI_LSTM tiles: 0 LSTM (i, f, g, o), 1 GRU (r, z, n_x, n_h; c_in = h)
+    // EPI_DGRAD (input gradient of a layer whose input went through leaky_relu): columns < split get
+    // the leaky derivative of mask[row][col] (the layer's input, nullable = none), go to y, their
+    // per-128-row-tile column sums to part[tile][col] (nullable) and their max |.| to gmax
+    // (nullable); columns >= split go unchanged to y2[row][col - split]
+    const float* mask;
+    long long ldm;
+    int split;
+    float* part;
+    unsigned* gmax;
 };
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const float* p, unsigned bytes) {
@@ -530,6 +539,66 @@ __global__ __launch_bounds__(WGM* WGN * 64, OCC) void k_gemm(ASrc a0, ASrc a1, c
     epilogue<TM, TN, EPI>(acc, ep, m0 + wr * TM * 32, n0 + wc * TN * 32, M, N, lane, cin);
 }
 
+// EPI_DGRAD epilogue of k_gemm3 (32x32 C layout): the leaky_relu derivative of the layer input
+// (mask > 0 ? 1 : 0.01, the reference MLP's F.leaky_relu) applied to the input gradient, per
+// 128-row tile column sums (bias gradient partials: lane sums of its rows, the two lane halves,
+// then the WGM row waves through LDS, a fixed order) and max |g| (the next gradient GEMMs' operand
+// scale). red: >= WGM * WGN * TN * 32 floats of LDS no longer used by the k loop.
+template <int WGM, int WGN, int TM, int TN>
+__device__ __forceinline__ void dgrad_epilogue(floatx16 (&acc)[TM][TN], const Epi& ep, float* red, int m0, int n0,
+                                               int wr, int wc, int M, int N, int lane) {
+    const int h = lane >> 5, l32 = lane & 31;
+    const int wm0 = m0 + wr * TM * 32, wn0 = n0 + wc * TN * 32;
+    float mx = 0.f;
+    float cs[TN];
+#pragma unroll
+    for (int j = 0; j < TN; j++) {
+        const int col = wn0 + j * 32 + l32;
+        const bool lo = col < ep.split;
+        float s = 0.f;
+#pragma unroll
+        for (int i = 0; i < TM; i++)
+#pragma unroll
+            for (int r = 0; r < 16; r++) {
+                const int row = wm0 + i * 32 + 4 * h + (r & 3) + 8 * (r >> 2);
+                if (row >= M || col >= N) continue;
+                float v = acc[i][j][r];
+                if (lo) {
+                    // torch's leaky_relu backward: input > 0 ? g : 0.01 g (leaky(z) > 0 iff z > 0)
+                    if (ep.mask && !(ep.mask[(long long)row * ep.ldm + col] > 0.f)) v *= 0.01f;
+                    ep.y[(long long)row * ep.ldy + col] = v;
+                    s += v;
+                    mx = fmaxf(mx, fabsf(v));
+                } else {
+                    ep.y2[(long long)row * ep.ldy2 + col - ep.split] = v;
+                }
+            }
+        cs[j] = s + __shfl_xor(s, 32);
+    }
+    if (ep.gmax) {
+        mx = gm_wave_max(mx);
+        if (lane == 0) gm_amax_publish(ep.gmax, mx);
+    }
+    if (ep.part) {
+        constexpr int BN = WGN * TN * 32;
+        if (h == 0) {
+#pragma unroll
+            for (int j = 0; j < TN; j++) red[wr * BN + wc * TN * 32 + j * 32 + l32] = cs[j];
+        }
+        __syncthreads();
+        if (wr == 0 && h == 0) {
+#pragma unroll
+            for (int j = 0; j < TN; j++) {
+                const int c = wc * TN * 32 + j * 32 + l32, col = n0 + c;
+                float s = red[c];
+#pragma unroll
+                for (int w = 1; w < WGM; w++) s += red[w * BN + c];
+                if (col < ep.split && col < N) ep.part[(long long)(m0 / (WGM * TM * 32)) * ep.split + col] = s;
+            }
+        }
+    }
+}
+
 // ---------------------------------------------------------------------------------------
 // X3 (split-f16) kernel. LDS row image of A and B tiles (4*BK + 16 bytes, conflict-free
 // ds_read_b128 on the 32 rows of an MFMA operand): per 16-deep k block s, bytes
@@ -766,9 +835,13 @@ __global__ __launch_bounds__(WGM* WGN * 64, OCC) void k_gemm3(ASrc a0, ASrc a1, 
 #pragma unroll
             for (int r = 0; r < 16; r++) acc[i][j][r] *= si;
     range_guard<TM, TN>(acc, ep.range_flag, lane);
-    CIn<TM, EPI> cin;
-    cin_load<TM, EPI>(cin, ep, m0 + wr * TM * 32, n0 + wc * TN * 32, M, lane);
-    epilogue<TM, TN, EPI>(acc, ep, m0 + wr * TM * 32, n0 + wc * TN * 32, M, N, lane, cin);
+    if constexpr (EPI == EPI_DGRAD) {
+        dgrad_epilogue<WGM, WGN, TM, TN>(acc, ep, reinterpret_cast<float*>(As), m0, n0, wr, wc, M, N, lane);
+    } else {
+        CIn<TM, EPI> cin;
+        cin_load<TM, EPI>(cin, ep, m0 + wr * TM * 32, n0 + wc * TN * 32, M, lane);
+        epilogue<TM, TN, EPI>(acc, ep, m0 + wr * TM * 32, n0 + wc * TN * 32, M, N, lane, cin);
+    }
 }
 
 // ---- 16x16x32 MFMA form of the LDS-DMA kernel (k_gemm3g MF = 1) ----
@@ -1706,6 +1779,38 @@ extern "C" int gm_gemm_x3(const gm_a_src* a0, const gm_a_src* a1, const void* wp
                       stream);
 }
 
+extern "C" int gm_gemm_x3_dgrad(const gm_a_src* a0, const void* wp, const float* wscale_inv, int32_t m, int32_t n,
+                                int32_t split, const float* mask, int64_t ldm, float* y, int64_t ldy, float* y2,
+                                int64_t ldy2, float* part, float* gmax, void* stream) {
+    if (!a0 || a0->mode != GM_A_DENSE || !wp || !wscale_inv || !y || m <= 0 || n <= 0 || split <= 0 || split > n ||
+        ldy < split || (split < n && (!y2 || ldy2 < n - split)) || (mask && ldm < split) ||
+        (reinterpret_cast<uintptr_t>(wp) & 15))
+        return gm_fail(GM_ERR_INVALID_ARG, "gm_gemm_x3_dgrad: bad arguments (dense source, 0 < split <= n)");
+    ASrc s0, s1;
+    int rc = to_asrc(a0, m, s0);
+    if (rc) return rc;
+    if (s0.amax) return gm_fail(GM_ERR_INVALID_ARG, "gm_gemm_x3_dgrad: no amax on the A source");
+    memset(&s1, 0, sizeof(s1));
+    const int K = s0.k;
+    const long long ldw = (long long)((K + BKMAX - 1) / BKMAX * BKMAX) / 16 * 64, wb = (long long)n * ldw;
+    if (!fits(wb)) return gm_fail(GM_ERR_UNSUPPORTED, "gm_gemm_x3_dgrad: weights larger than 2 GB");
+    Epi ep;
+    memset(&ep, 0, sizeof(ep));
+    ep.y = y;
+    ep.ldy = ldy;
+    ep.y2 = y2;
+    ep.ldy2 = ldy2;
+    ep.mask = mask;
+    ep.ldm = ldm;
+    ep.split = split;
+    ep.part = part;
+    ep.gmax = reinterpret_cast<unsigned*>(gmax);
+    if ((rc = range_flag(&ep.range_flag))) return rc;
+    return launch<2, 2, 2, 2, 16, GM_A_DENSE, EPI_DGRAD, 2, true>(s0, s1, static_cast<const float*>(wp), ldw,
+                                                                 (unsigned)wb, m, n, K, ep, (hipStream_t)stream,
+                                                                 wscale_inv);
+}
+
 extern "C" int gm_gemm_range_status(int32_t* status, int32_t clear) {
     if (!status) return gm_fail(GM_ERR_INVALID_ARG, "gm_gemm_range_status: null status");
     *status = g_range_host ? (int32_t)*reinterpret_cast<volatile unsigned*>(g_range_host) : 0;
@@ -1723,7 +1828,7 @@ extern "C" int gm_gemm_x3_head(const gm_a_src* a0, const void* wp, const float* 
     ASrc s0, s1;
     int rc = to_asrc(a0, m, s0);
     if (rc) return rc;
-    if (s0.scale || s0.amax) return gm_fail(GM_ERR_INVALID_ARG, "gm_gemm_x3_head: no A scale / amax");
+    if (s0.scale) return gm_fail(GM_ERR_INVALID_ARG, "gm_gemm_x3_head: no A scale");
     memset(&s1, 0, sizeof(s1));
     const int K = s0.k;
     const long long ldw = (long long)((K + BKMAX - 1) / BKMAX * BKMAX) / 16 * 64, wb = (long long)n * ldw;
@@ -1741,6 +1846,10 @@ extern "C" int gm_gemm_x3_head(const gm_a_src* a0, const void* wp, const float* 
     ep.q = q;
     ep.ldq = ldq;
     if ((rc = range_flag(&ep.range_flag))) return rc;
+    if (s0.amax)  // training forward: max |A| for the layer's weight gradient
+        return launch_g<4, 2, 1, 4, 2, GM_A_DENSE, EPI_HEAD, 1, 1>(s0, s1, static_cast<const float*>(wp), ldw,
+                                                                  (unsigned)wb, m, n, K, ep, (hipStream_t)stream,
+                                                                  wscale_inv, g_mfma16 == 2);
     return launch_g<4, 2, 1, 4, 2, GM_A_DENSE, EPI_HEAD, 1>(s0, s1, static_cast<const float*>(wp), ldw, (unsigned)wb, m,
                                                           n, K, ep, (hipStream_t)stream, wscale_inv, g_mfma16 == 2);
 }

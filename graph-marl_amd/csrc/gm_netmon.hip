@@ -138,7 +138,7 @@ template <int V>
 __global__ __launch_bounds__(256) void k_readout(const float* __restrict__ hf, const float* __restrict__ hp,
                                                  const int32_t* __restrict__ nbr, const int32_t* __restrict__ agent_node,
                                                  int G, int N, int R, int deg, int H, float* __restrict__ out,
-                                                 long long stride) {
+                                                 long long stride, long long ldf, long long ldp) {
     const int HV = H / V;
     const int WV = (deg + 1) * HV;
     const long long gid = (long long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -151,10 +151,10 @@ __global__ __launch_bounds__(256) void k_readout(const float* __restrict__ hf, c
     const int seg = cv / HV, off = (cv - seg * HV) * V;
     Vec<V> val;
     if (seg == 0) {
-        val = ldv<V>(hf + ((size_t)g * N + v) * H + off);
+        val = ldv<V>(hf + ((size_t)g * N + v) * ldf + off);
     } else {
         int m = nbr[((size_t)g * N + v) * deg + seg - 1];
-        val = m >= 0 ? ldv<V>(hp + ((size_t)g * N + m) * H + off) : zerov<V>();
+        val = m >= 0 ? ldv<V>(hp + ((size_t)g * N + m) * ldp + off) : zerov<V>();
     }
     stv<V>(out + row * stride + (size_t)cv * V, val);
 }
@@ -401,7 +401,7 @@ __global__ __launch_bounds__(256) void k_leaky_bwd(const float* __restrict__ gy,
         float acc = 0.f;
         for (long long r = r0; r < r1; r++) {
             const long long i = r * cols + c;
-            const float v = y[i] >= 0.f ? gy[i] : slope * gy[i];
+            const float v = y[i] > 0.f ? gy[i] : slope * gy[i];  // torch: input > 0 ? g : slope g
             g[i] = v;
             acc += v;
             m = fmaxf(m, fabsf(v));
@@ -448,21 +448,27 @@ extern "C" int gm_mp_aggregate_bwd(const float* dout, const int32_t* nbr, int32_
     return launch_agg<true>(dout, nbr, G, N, deg, H, mode, dh, stream);
 }
 
-extern "C" int gm_netmon_readout(const float* hf, const float* hp, const int32_t* nbr, const int32_t* agent_node,
-                                 int32_t G, int32_t N, int32_t R, int32_t deg, int32_t H, float* out, int64_t stride,
-                                 void* stream) {
+extern "C" int gm_netmon_readout_ld(const float* hf, int64_t ldf, const float* hp, int64_t ldp, const int32_t* nbr,
+                                    const int32_t* agent_node, int32_t G, int32_t N, int32_t R, int32_t deg, int32_t H,
+                                    float* out, int64_t stride, void* stream) {
     if (!hf || !hp || !nbr || !out || G <= 0 || N <= 0 || R <= 0 || deg < 0 || H <= 0 ||
-        stride < (int64_t)(deg + 1) * H)
+        stride < (int64_t)(deg + 1) * H || ldf < H || ldp < H)
         return gm_fail(GM_ERR_INVALID_ARG, "gm_netmon_readout: bad arguments");
     if (!agent_node && R != N) return gm_fail(GM_ERR_INVALID_ARG, "gm_netmon_readout: R must equal N without agent map");
     int V = vec_width(H, stride, out);
-    int v2 = vec_width(H, H, hf), v3 = vec_width(H, H, hp);
+    int v2 = vec_width(H, ldf, hf), v3 = vec_width(H, ldp, hp);
     V = V < v2 ? V : v2;
     V = V < v3 ? V : v3;
     long long total = (long long)G * R * (deg + 1) * (H / V);
     GM_VLAUNCH(k_readout, V, dim3(nblocks(total, 256)), hf, hp, nbr, agent_node, G, N, R, deg, H, out,
-               (long long)stride);
+               (long long)stride, (long long)ldf, (long long)ldp);
     return launched();
+}
+
+extern "C" int gm_netmon_readout(const float* hf, const float* hp, const int32_t* nbr, const int32_t* agent_node,
+                                 int32_t G, int32_t N, int32_t R, int32_t deg, int32_t H, float* out, int64_t stride,
+                                 void* stream) {
+    return gm_netmon_readout_ld(hf, H, hp, H, nbr, agent_node, G, N, R, deg, H, out, stride, stream);
 }
 
 // Same gather, one block per graph: the graph's agent nodes and their neighbour lists are
@@ -560,6 +566,188 @@ extern "C" int gm_lstm_pointwise_bwd(const float* dh1, const float* dc1, const f
                        reinterpret_cast<unsigned*>(dgates_scale));
     int rc = launched();
     if (rc == GM_OK && dgates_scale) rc = gm_absmax_finish(dgates_scale, stream);
+    return rc;
+}
+
+// ---------------------------------------------------------------------------
+// Sequence-batched training backward (graph-marl_amd/train_seq.py)
+// ---------------------------------------------------------------------------
+namespace {
+
+// max over the block through LDS (any block size <= 1024), published once per block
+__device__ void block_max_publish(float m, unsigned* slot) {
+    __shared__ float red[1024];
+    red[threadIdx.x] = m;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int i = 1; i < (int)blockDim.x; i++) m = fmaxf(m, red[i]);
+        gm_amax_publish(slot, m);
+    }
+}
+
+// LSTM cell backward with its gradient sources summed on the fly (gm_lstm_cell_bwd). Thread
+// (rl, u) of a block of RL x H threads owns unit u of the rows r0 + rl, r0 + rl + RL, ... of the
+// block's rows_per_block rows: loads and stores are unit-contiguous; the per-block bias sums are
+// the RL row lanes combined in LDS in a fixed order.
+__global__ __launch_bounds__(1024) void k_lstm_cell_bwd(gm_lstm_bwd_args a, unsigned* sc_slot, unsigned* max_slot) {
+    __shared__ float red[4][1024];
+    const int H = a.hidden, RL = blockDim.x / H;
+    const int u = threadIdx.x % H, rl = threadIdx.x / H;
+    const long long r0 = (long long)blockIdx.x * a.rows_per_block;
+    const long long r1 = min((long long)a.m, r0 + a.rows_per_block);
+    float p0 = 0.f, p1 = 0.f, p2 = 0.f, p3 = 0.f, mx = 0.f;
+    for (long long r = r0 + rl; r < r1; r += RL) {
+        const float* ar = a.act + r * a.ld_act + u;
+        const float gi = ar[0], gf = ar[H], gg = ar[2 * H], go = ar[3 * H];
+        const float c = a.c_in[r * a.ld_cin + u];
+        const float tc = tanhf(a.c_out[r * a.ld_cout + u]);
+        float dh = 0.f;
+        if (a.dh0) dh += a.dh0[r * a.ld_dh0 + u];
+        if (a.dh1) dh += a.dh1[r * a.ld_dh1 + u];
+        if (a.dm) {  // transpose of the (I + A) aggregate: members of row r's node, ascending id
+            const int N = a.n_nodes;
+            const long long g = r / N;
+            const int n = (int)(r - g * N);
+            int mem[MAXDEG + 1];
+            const int cnt = members(a.nbr + r * a.deg, a.deg, n, mem);
+            for (int q = 0; q < cnt; q++) {
+                float v = a.dm[(g * N + mem[q]) * a.ld_dm + u];
+                if (a.mean) {
+                    const int32_t* nbm = a.nbr + (g * N + mem[q]) * a.deg;
+                    int cm = 1;
+                    for (int k = 0; k < a.deg; k++) cm += nbm[k] >= 0;
+                    v = v * (1.0f / (float)cm);
+                }
+                dh += v;
+            }
+        }
+        float dcn = a.dc ? a.dc[r * a.ld_dc + u] : 0.f;
+        const bool ext = !a.ext_mask || !a.ext_mask[r / a.rows_per_sample];
+        if (ext) {
+            if (a.dh_ext) dh += a.dh_ext[r * a.ld_ext + u];
+            if (a.dc_ext) dcn += a.dc_ext[r * a.ld_dcext + u];
+        }
+        const float dct = dcn + dh * go * (1.f - tc * tc);
+        const float d0 = dct * gg * gi * (1.f - gi), d1 = dct * c * gf * (1.f - gf);
+        const float d2 = dct * gi * (1.f - gg * gg), d3 = dh * tc * go * (1.f - go);
+        float* dg = a.dgates + r * a.ld_dg + u;
+        dg[0] = d0;
+        dg[H] = d1;
+        dg[2 * H] = d2;
+        dg[3 * H] = d3;
+        if (a.dc_out) a.dc_out[r * a.ld_dco + u] = dct * gf;
+        p0 += d0;
+        p1 += d1;
+        p2 += d2;
+        p3 += d3;
+        mx = fmaxf(mx, fmaxf(fmaxf(fabsf(d0), fabsf(d1)), fmaxf(fabsf(d2), fabsf(d3))));
+    }
+    if (a.bias_part) {
+        red[0][threadIdx.x] = p0;
+        red[1][threadIdx.x] = p1;
+        red[2][threadIdx.x] = p2;
+        red[3][threadIdx.x] = p3;
+        __syncthreads();
+        if (rl == 0) {
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                float s = red[k][u];
+                for (int l = 1; l < RL; l++) s += red[k][l * H + u];
+                a.bias_part[(long long)blockIdx.x * 4 * H + k * H + u] = s;
+            }
+        }
+        __syncthreads();
+    }
+    if (sc_slot || max_slot) {
+        __shared__ float mred[1024];
+        mred[threadIdx.x] = mx;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            for (int i = 1; i < (int)blockDim.x; i++) mx = fmaxf(mx, mred[i]);
+            if (sc_slot) gm_amax_publish(sc_slot, mx);
+            if (max_slot) gm_amax_publish(max_slot, mx);
+        }
+    }
+}
+
+// Q head + leaky hidden layer backward (gm_qhead_bwd): thread c owns column c of the block's rows
+__global__ __launch_bounds__(1024) void k_qhead_bwd(const float* __restrict__ dq, long long ldq, int nq,
+                                                   const float* __restrict__ wq, long long ldwq,
+                                                   const float* __restrict__ y, long long ldy, long long rows, int cols,
+                                                   int act, float* __restrict__ g, long long ldg,
+                                                   float* __restrict__ part_b, float* __restrict__ part_wq,
+                                                   float* __restrict__ part_bq, int rpb, unsigned* __restrict__ amax) {
+    const int c = threadIdx.x;
+    const bool ok = c < cols;
+    float w[4] = {0.f, 0.f, 0.f, 0.f};
+    for (int q = 0; q < nq; q++) w[q] = ok ? wq[q * ldwq + c] : 0.f;
+    const long long r0 = (long long)blockIdx.x * rpb, r1 = min(rows, r0 + rpb);
+    float pb = 0.f, mx = 0.f, pw[4] = {0.f, 0.f, 0.f, 0.f}, pq[4] = {0.f, 0.f, 0.f, 0.f};
+    for (long long r = r0; r < r1; r++) {
+        float d[4] = {0.f, 0.f, 0.f, 0.f};
+        for (int q = 0; q < nq; q++) d[q] = dq[r * ldq + q];
+#pragma unroll
+        for (int q = 0; q < 4; q++) pq[q] += d[q];
+        if (ok) {
+            const float yv = y[r * ldy + c];
+            float gv = 0.f;
+            for (int q = 0; q < nq; q++) gv = fmaf(d[q], w[q], gv);
+            if (act && !(yv > 0.f)) gv *= 0.01f;
+            g[r * ldg + c] = gv;
+            pb += gv;
+            mx = fmaxf(mx, fabsf(gv));
+#pragma unroll
+            for (int q = 0; q < 4; q++) pw[q] = fmaf(d[q], yv, pw[q]);
+        }
+    }
+    if (ok) {
+        part_b[(long long)blockIdx.x * cols + c] = pb;
+        for (int q = 0; q < nq; q++) part_wq[((long long)blockIdx.x * nq + q) * cols + c] = pw[q];
+    }
+    if (c == 0)
+        for (int q = 0; q < nq; q++) part_bq[(long long)blockIdx.x * nq + q] = pq[q];
+    if (amax) block_max_publish(mx, amax);
+}
+
+}  // namespace
+
+extern "C" int gm_lstm_cell_bwd(const gm_lstm_bwd_args* a, void* stream) {
+    if (!a || !a->act || !a->c_in || !a->c_out || !a->dgates || a->m <= 0 || a->hidden <= 0 || a->hidden > 1024 ||
+        (a->hidden > 256 && a->hidden % 64) || (a->dm && (!a->nbr || a->n_nodes <= 0 || a->deg < 0 || a->deg > MAXDEG)) ||
+        (a->ext_mask && a->rows_per_sample <= 0) || (a->bias_part && a->rows_per_block <= 0))
+        return gm_fail(GM_ERR_INVALID_ARG, "gm_lstm_cell_bwd: bad arguments");
+    hipStream_t st = (hipStream_t)stream;
+    const int H = a->hidden;
+    const int RL = H >= 256 ? 1 : 256 / H;
+    const int threads = H * RL;
+    gm_lstm_bwd_args b = *a;
+    if (b.rows_per_block <= 0) b.rows_per_block = 64;
+    if (b.dg_scale && hipMemsetAsync(b.dg_scale, 0, sizeof(float), st) != hipSuccess)
+        return gm_fail(GM_ERR_HIP, "gm_lstm_cell_bwd: memset");
+    const long long nb = (b.m + b.rows_per_block - 1) / b.rows_per_block;
+    hipLaunchKernelGGL(k_lstm_cell_bwd, dim3((unsigned)nb), dim3(threads), 0, st, b,
+                       reinterpret_cast<unsigned*>(b.dg_scale), reinterpret_cast<unsigned*>(b.dg_max));
+    int rc = launched();
+    if (rc == GM_OK && b.dg_scale) rc = gm_absmax_finish(b.dg_scale, stream);
+    return rc;
+}
+
+extern "C" int gm_qhead_bwd(const float* dq, int64_t ldq, int32_t nq, const float* wq, int64_t ldwq, const float* y,
+                            int64_t ldy, int64_t rows, int32_t cols, int32_t act, float* g, int64_t ldg, float* part_b,
+                            float* part_wq, float* part_bq, int32_t rows_per_block, float* g_scale, void* stream) {
+    if (!dq || !wq || !y || !g || !part_b || !part_wq || !part_bq || nq <= 0 || nq > 4 || rows <= 0 || cols <= 0 ||
+        cols > 1024 || ldq < nq || ldwq < cols || ldy < cols || ldg < cols || rows_per_block <= 0)
+        return gm_fail(GM_ERR_INVALID_ARG, "gm_qhead_bwd: bad arguments (nq <= 4, cols <= 1024)");
+    hipStream_t st = (hipStream_t)stream;
+    if (g_scale && hipMemsetAsync(g_scale, 0, sizeof(float), st) != hipSuccess)
+        return gm_fail(GM_ERR_HIP, "gm_qhead_bwd: memset");
+    const long long nb = (rows + rows_per_block - 1) / rows_per_block;
+    const int threads = (cols + 63) / 64 * 64;
+    hipLaunchKernelGGL(k_qhead_bwd, dim3((unsigned)nb), dim3(threads), 0, st, dq, (long long)ldq, nq, wq,
+                       (long long)ldwq, y, (long long)ldy, (long long)rows, cols, act, g, (long long)ldg, part_b,
+                       part_wq, part_bq, rows_per_block, reinterpret_cast<unsigned*>(g_scale));
+    int rc = launched();
+    if (rc == GM_OK && g_scale) rc = gm_absmax_finish(g_scale, stream);
     return rc;
 }
 

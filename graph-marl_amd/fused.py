@@ -53,6 +53,8 @@ def _setup():
                                          vp, vp, vp, C.c_int64, vp]
         lib.gm_gemm_x3_head.argtypes = [C.POINTER(ASrc), vp, vp, vp, C.c_int32, C.c_int32, C.c_int32, vp, C.c_int64,
                                         vp, C.c_int32, vp, C.c_int64, vp, C.c_int64, vp]
+        lib.gm_gemm_x3_dgrad.argtypes = [C.POINTER(ASrc), vp, vp, C.c_int32, C.c_int32, C.c_int32, vp, C.c_int64, vp,
+                                         C.c_int64, vp, C.c_int64, vp, vp, vp]
         lib._gemm_ready = True
     return lib
 

@@ -45,6 +45,7 @@ M = importlib.import_module("graph-marl_amd.model")
 W = importlib.import_module("graph-marl_amd.wrapper")
 P = importlib.import_module("graph-marl_amd.policy")
 T = importlib.import_module("graph-marl_amd.train")
+TS = importlib.import_module("graph-marl_amd.train_seq")
 RB = importlib.import_module("graph-marl_amd.replaybuffer")
 S = importlib.import_module("graph-marl_amd.simple")
 HEU = importlib.import_module("graph-marl_amd.heuristics")
@@ -429,14 +430,22 @@ def main(argv=None):
             model.train()
             if netmon is not None:
                 netmon.train()
-            batches = list(buff.get_batch(args.mini_batch_size, sequence_length=args.sequence_length,
-                                          lazy_next=True))
             parts = {}
-            loss, qs, qts = T.dqn_update(netmon, model, model_tar, optimizer, params, batches, args.gamma, args.tau,
-                                         args.target_update_steps, iteration,
-                                         att_coeff=args.att_regularization_coeff if args.model == "dgn" else 0.0,
-                                         aux_model=aux_model, aux_coeff=args.aux_loss_coeff, parts=parts,
-                                         consecutive=True)  # replay sequences: the target pass reuses online steps
+            att = args.att_regularization_coeff if args.model == "dgn" else 0.0
+            if args.sequence_length > 1 and TS.seq_ok(netmon, model, model_tar, att, aux_model):
+                # sequence-batched update with the hand-written backward (train_seq.py)
+                loss, q_all, qt_all = TS.dqn_update_seq(netmon, model, model_tar, optimizer, params,
+                                                        buff.get_sequences(args.mini_batch_size,
+                                                                           args.sequence_length),
+                                                        args.gamma, args.tau, args.target_update_steps, iteration)
+                qs, qts = list(q_all), list(qt_all)
+            else:
+                batches = list(buff.get_batch(args.mini_batch_size, sequence_length=args.sequence_length,
+                                              lazy_next=True))
+                loss, qs, qts = T.dqn_update(netmon, model, model_tar, optimizer, params, batches, args.gamma,
+                                             args.tau, args.target_update_steps, iteration, att_coeff=att,
+                                             aux_model=aux_model, aux_coeff=args.aux_loss_coeff, parts=parts,
+                                             consecutive=True)  # replay sequences: the target reuses online steps
             model.eval()
             if netmon is not None:
                 netmon.eval()

@@ -200,6 +200,37 @@ class ReplayBuffer:
         return {"state": (st.state_hi << 64) | st.state_lo, "inc": (st.inc_hi << 64) | st.inc_lo,
                 "has_uint32": st.has_uint32, "uinteger": st.uinteger}
 
+    def get_sequences(self, batch_size, sequence_length):
+        """The sequences get_batch(batch_size, sequence_length) draws (same stream, same indices), as
+        one train_seq.SeqBatch with every step's fields stacked ([L, B, ...], one gather per field);
+        the next-step fields are gathered on demand (next_fields(t, rows))."""
+        from .train_seq import SeqBatch
+
+        if not self.graph:
+            raise ValueError("get_sequences: NetMon transitions only")
+        if self.count <= sequence_length:
+            raise ValueError("not enough transitions for the requested sequence length")
+        Lq = sequence_length
+        span = self.count - Lq
+        f = self.choice(self.n_env * span, batch_size)
+        env = f // span
+        first = (self.index % self.count + f % span) % self.count
+        slots = (first.unsqueeze(0) + torch.arange(Lq, device=f.device).unsqueeze(1)) % self.count  # [L, B]
+        envs = env.unsqueeze(0).expand(Lq, -1)
+        fl = torch.float32
+        od = self.obs_dim
+
+        def next_fields(t, rows):
+            s, e = (slots[t], env) if rows is None else (slots[t][rows], env[rows])
+            return (self.next_obs[s, e].to(fl), self.next_node_obs[s, e].to(fl),
+                    self.next_agent_node[s, e].int().contiguous())
+
+        return SeqBatch(self.obs[slots, envs].to(fl), od, self.action[slots, envs].long(),
+                        self.reward[slots, envs].to(fl), self.done[slots, envs], self.episode_done[slots],
+                        self.node_obs[slots, envs].to(fl), self.nbr[slots, envs].int().contiguous(),
+                        self.agent_node[slots, envs].int().contiguous(), self.node_state[first, env].to(fl),
+                        next_fields, (slots, env))
+
     def get_batch(self, batch_size, sequence_length=1, lazy_next=False):
         """Yields sequence_length TransitionBatches of batch_size transitions
         (src/replaybuffer.py:103-130): uniform (slot, env); sequences are consecutive slots of

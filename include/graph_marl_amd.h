@@ -25,6 +25,8 @@
  *   gm_gemm_x3_head                  last DQN layer + Q head in one kernel
  *   gm_absmax_scale(_rows/_finish)   power-of-two operand scale for gm_gemm_x3 (input gradients)
  *   gm_gemm_x3_wgrad                 split-K weight-gradient GEMM over K-major operands
+ *   gm_gemm_x3_dgrad / gm_lstm_cell_bwd / gm_qhead_bwd   backward of Linear+leaky_relu, LSTMCell and
+ *                                    Q_Net.fc (torch autograd of the update, src/main.py:996)
  *   gm_agent_attention               AttModel attention core (DGN)          src/model.py:86-117
  *   gm_agent_comm                    CommNet communication step             src/model.py:780-787
  */
@@ -224,6 +226,51 @@ int gm_lstm_pointwise(const float* gates, const float* c, int32_t m, int32_t hid
 int gm_lstm_pointwise_bwd(const float* dh_new, const float* dc_new, const float* act, const float* c,
                           const float* c_new, int32_t m, int32_t hidden, float* dgates, float* dc,
                           float* dgates_scale, void* stream);
+/* LSTM cell backward of the sequence-batched training path (nn.LSTMCell, src/model.py:379-382,
+ * 491, 543, backward of torch autograd): per row r and unit u, with gate activations act (i, f,
+ * g, o), cell input c and output c' = c_out:
+ *   dh = dh0 + dh1 + sum_{n in {r} U nbr(r)} dm[n] s(n) + (ext_mask[r / rows_per_sample] ? 0 : dh_ext)
+ *   dc' = dc + (ext_mask[...] ? 0 : dc_ext)
+ * (every source nullable; dm = the input gradient of the aggregate input of the next cell,
+ * s(n) = 1 or 1 / |{n} U nbr(n)| for mean); writes dgates (i, f, g, o pre-activation gradients),
+ * dc_out = dc'_total * f (nullable), per-block column sums of dgates to bias_part
+ * [ceil(m / rows_per_block)][4H] (nullable), max |dgates| to dg_scale as a power-of-two scale
+ * (gm_absmax_scale semantics, nullable) and as float bits into dg_max (nullable, accumulated by
+ * atomicMax). H <= 256, 256 % H == 0 or H % 64 == 0 with H <= 1024. */
+typedef struct {
+    const float* act; int64_t ld_act;
+    const float* c_in; int64_t ld_cin;
+    const float* c_out; int64_t ld_cout;
+    const float* dh0; int64_t ld_dh0;
+    const float* dh1; int64_t ld_dh1;
+    const float* dm; int64_t ld_dm;
+    const int32_t* nbr; int32_t n_nodes, deg, mean;
+    const float* dh_ext; int64_t ld_ext;
+    const float* dc_ext; int64_t ld_dcext;
+    const uint8_t* ext_mask; int32_t rows_per_sample;
+    const float* dc; int64_t ld_dc;
+    int32_t m, hidden;
+    float* dgates; int64_t ld_dg;
+    float* dc_out; int64_t ld_dco;
+    float* bias_part; int32_t rows_per_block;
+    float* dg_scale;
+    float* dg_max;
+} gm_lstm_bwd_args;
+int gm_lstm_cell_bwd(const gm_lstm_bwd_args* a, void* stream);
+/* Q head + last hidden layer backward (Q_Net.fc after a leaky_relu MLP layer, src/model.py:119-125,
+ * 187-203): g[r][c] = (sum_a dq[r][a] wq[a][c]) * (act && y[r][c] <= 0 ? 0.01 : 1) for the layer
+ * output y; per block of rows_per_block rows: part_b[blk][c] = sum g (the layer's bias gradient),
+ * part_wq[blk][a][c] = sum dq[r][a] y[r][c] (the head's weight gradient), part_bq[blk][a] =
+ * sum dq[r][a]; g_scale (nullable): power-of-two scale of g (gm_absmax_scale semantics).
+ * nq <= 4, cols <= 1024. */
+int gm_qhead_bwd(const float* dq, int64_t ldq, int32_t nq, const float* wq, int64_t ldwq, const float* y,
+                 int64_t ldy, int64_t rows, int32_t cols, int32_t act, float* g, int64_t ldg, float* part_b,
+                 float* part_wq, float* part_bq, int32_t rows_per_block, float* g_scale, void* stream);
+/* gm_netmon_readout with strided h rows (h_final [.][ldf], h_prev [.][ldp]; e.g. the [h | c]
+ * state rows of the LSTM, ld = 2H). */
+int gm_netmon_readout_ld(const float* h_final, int64_t ldf, const float* h_prev, int64_t ldp, const int32_t* nbr,
+                         const int32_t* agent_node, int32_t n_graphs, int32_t n_nodes, int32_t n_rows, int32_t deg,
+                         int32_t hidden, float* out, int64_t out_stride, void* stream);
 /* Fused f32 MFMA linear layer: y[M,N] = act(x[M,K] @ w[N,K]^T + b[N]); row strides ldx, ldw
  * (multiples of 4 floats, 16-byte aligned bases), ldy; K may be ragged; b nullable;
  * act 0 = none, 1 = leaky_relu(0.01). */
@@ -283,11 +330,23 @@ int gm_gemm_range_status(int32_t* status, int32_t clear);
 /* Last DQN encoder layer + Q head in one kernel (split-f16 form for the layer, fp32 head):
  * q[m][nq] = Wq · act(src0 · W^T + b) + bq, act 0 none / 1 leaky_relu(0.01); the hidden
  * activation stays in registers (also written to y when y != NULL). src0 DENSE, n <= 256,
- * nq <= 4, wq [nq][ldwq] fp32. Replaces encoder.linear_layers[-1] + Q_Net.fc of the
- * reference DQN (src/model.py:119-125, 187-203). */
+ * nq <= 4, wq [nq][ldwq] fp32; src0->amax (nullable) receives max |src0| (training forward).
+ * Replaces encoder.linear_layers[-1] + Q_Net.fc of the reference DQN (src/model.py:119-125,
+ * 187-203). */
 int gm_gemm_x3_head(const gm_a_src* src0, const void* wp, const float* wscale_inv, const float* b, int32_t m,
                     int32_t n, int32_t act, const float* wq, int64_t ldwq, const float* bq, int32_t nq, float* q,
                     int64_t ldq, float* y, int64_t ldy, void* stream);
+/* Input-gradient GEMM of a layer whose input went through leaky_relu (the reference MLP's
+ * F.leaky_relu, src/model.py:13-42, backward of torch autograd, src/main.py:996): D = src0 . W^T
+ * in split-f16 form over wp = gm_gemm_pack_x3 of W^T ([n][K], K = src0->k; src0 DENSE, its
+ * power-of-two scale in src0->scale); columns < split: g = D * (mask > 0 ? 1 : 0.01) (mask
+ * [m][ldm] = the layer input, nullable = no derivative) to y [m][ldy], per-128-row-tile column
+ * sums to part [ceil(m / 128)][split] (nullable; the bias gradient of the previous layer) and
+ * max |g| as float bits to gmax (nullable, zeroed by the caller; gm_absmax_finish); columns >= split
+ * unchanged to y2 [m][ldy2] (e.g. the LSTM [x | h] input gradient split into its parts). */
+int gm_gemm_x3_dgrad(const gm_a_src* src0, const void* wp, const float* wscale_inv, int32_t m, int32_t n,
+                     int32_t split, const float* mask, int64_t ldm, float* y, int64_t ldy, float* y2, int64_t ldy2,
+                     float* part, float* gmax, void* stream);
 /* Weight-gradient GEMM of the training path: C_z = A_z^T B_z for k-splits z of kchunk rows
  * (K = batch rows): A = dY [k][lda], B = X [k][ldb], both K-major fp32, scaled by the device
  * powers of two sa, sb (gm_absmax_scale) and split into f16 pieces on the way into LDS;
