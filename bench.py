@@ -364,7 +364,12 @@ def main():
         try:
             train = measure_train(args, gm, M, W, P, net, netmon, dqn, dev, world, rank)
         except Exception as ex:  # the training figure must never break the rollout line
-            train = {"value": None, "error": repr(ex)[:300]}
+            if os.environ.get("GM_BENCH_RAISE") == "1":
+                raise
+            import traceback
+
+            where = " <- ".join(f"{fs.name}:{fs.lineno}" for fs in traceback.extract_tb(ex.__traceback__)[::-1][:4])
+            train = {"value": None, "error": repr(ex)[:300], "where": where}
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -184,7 +184,7 @@ def _wgrad(gy, x, k, sa=None, sb=None):
         L.check(lib.gm_absmax_scale_rows(x.data_ptr(), Mb, k, ldx, sb.data_ptr(), L.stream_ptr()))
     tiles = ((o + 127) // 128) * ((N + 127) // 128)
     # the kernel addresses each operand with 32-bit byte offsets: batches past 2 GB run in row blocks
-    rows_max = ((1 << 31) - (1 << 24)) // (4 * max(ldx, o)) // 2048 * 2048
+    rows_max = ((1 << 31) - (1 << 25)) // (4 * max(ldx, o)) // 2048 * 2048
     total = None
     for r0 in range(0, Mb, rows_max):
         mb = min(rows_max, Mb - r0)

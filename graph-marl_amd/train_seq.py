@@ -65,7 +65,7 @@ _LIMIT = (1 << 31) - (1 << 24)  # the GEMM kernels address an operand with 32-bi
 def _row_blocks(m, *widths):
     """Row blocks (r0, rows) of an m-row GEMM whose operands have the given row widths (floats) so
     that no operand block reaches 2 GB; blocks are multiples of 128 rows (the GEMM tile)."""
-    step = max(128, _LIMIT // (4 * max(widths)) // 128 * 128)
+    step = max(128, (_LIMIT - (1 << 20)) // (4 * max(widths)) // 128 * 128)
     return [(r0, min(step, m - r0)) for r0 in range(0, m, step)]
 
 
