@@ -1904,9 +1904,15 @@ extern "C" int gm_absmax_scale_rows(const float* x, int64_t rows, int32_t cols, 
     hipStream_t st = (hipStream_t)stream;
     hipError_t e = hipMemsetAsync(scale, 0, sizeof(float), st);
     if (e != hipSuccess) return gm_fail(GM_ERR_HIP, std::string("gm_absmax_scale_rows: ") + hipGetErrorString(e));
-    const long long blocks = std::min<long long>(1024, (rows + 3) / 4);
-    hipLaunchKernelGGL(k_absmax_rows, dim3((unsigned)blocks), dim3(256), 0, st, x, (long long)rows, (int)cols,
-                       (long long)ld, reinterpret_cast<unsigned*>(scale));
+    if (ld == cols) {  // contiguous rows: one flat grid-stride pass
+        const long long n = rows * (long long)cols;
+        hipLaunchKernelGGL(k_absmax_atomic, dim3((unsigned)std::min<long long>(2048, (n + 255) / 256)), dim3(256), 0, st,
+                           x, n, reinterpret_cast<unsigned*>(scale));
+    } else {
+        const long long blocks = std::min<long long>(1024, (rows + 3) / 4);
+        hipLaunchKernelGGL(k_absmax_rows, dim3((unsigned)blocks), dim3(256), 0, st, x, (long long)rows, (int)cols,
+                           (long long)ld, reinterpret_cast<unsigned*>(scale));
+    }
     hipLaunchKernelGGL(k_scale_from_max, dim3(1), dim3(1), 0, st, scale);
     e = hipGetLastError();
     if (e != hipSuccess) return gm_fail(GM_ERR_HIP, std::string("gm_absmax_scale_rows: ") + hipGetErrorString(e));

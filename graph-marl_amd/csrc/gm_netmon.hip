@@ -66,6 +66,10 @@ __device__ __forceinline__ int members(const int32_t* nb, int deg, int n, int* o
     return cnt;
 }
 
+__device__ __forceinline__ float4 f4add(float4 a, float4 b) {
+    return make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w);
+}
+
 // XCD-aware block order: the hardware deals block b to XCD b % 8; logical block numbers are
 // handed out so that each XCD gets one contiguous run of rows, and the 4 rows every node reads
 // (itself + 3 neighbours of the same graph) sit in that XCD's L2 instead of being fetched once per
@@ -448,6 +452,78 @@ extern "C" int gm_mp_aggregate_bwd(const float* dout, const int32_t* nbr, int32_
     return launch_agg<true>(dout, nbr, G, N, deg, H, mode, dh, stream);
 }
 
+// readout, one wave per output row (the row's node and neighbour ids read once, as wave-uniform
+// loads), 16-byte lanes over the (deg + 1) * H columns; two rows per iteration keep 4 independent
+// loads in flight per lane. Requires H % 4 == 0 and 16-byte aligned rows (host-checked).
+__global__ __launch_bounds__(256) void k_readout_rows(const float* __restrict__ hf, const float* __restrict__ hp,
+                                                      const int32_t* __restrict__ nbr,
+                                                      const int32_t* __restrict__ agent_node, long long rows, int N,
+                                                      int R, int deg, int H, float* __restrict__ out,
+                                                      long long stride, long long ldf, long long ldp) {
+    const int lane = threadIdx.x & 63;
+    const long long wave = ((long long)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const long long nw = ((long long)gridDim.x * blockDim.x) >> 6;
+    const int H4 = H >> 2, W4 = (deg + 1) * H4;
+    for (long long row = wave; row < rows; row += nw) {
+        const long long g = row / R;
+        const int r = (int)(row - g * R);
+        const int v = __builtin_amdgcn_readfirstlane(agent_node ? agent_node[row] : r);
+        const int32_t* nb = nbr + (g * N + v) * deg;
+        float* orow = out + row * stride;
+        for (int c = lane; c < W4; c += 64) {
+            const int seg = c / H4, off = (c - seg * H4) * 4;
+            float4 val = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (seg == 0) {
+                val = *reinterpret_cast<const float4*>(hf + (g * N + v) * ldf + off);
+            } else {
+                const int m = nb[seg - 1];
+                if (m >= 0) val = *reinterpret_cast<const float4*>(hp + (g * N + m) * ldp + off);
+            }
+            *reinterpret_cast<float4*>(orow + 4 * c) = val;
+        }
+    }
+}
+
+// readout backward, one block per graph: the graph's R output rows ((deg + 1) H floats each) are
+// staged in LDS with coalesced 16-byte loads, then thread (node, 4 columns) sums the rows that read
+// it in the same (row, segment) order as k_readout_bwd (identical results)
+__global__ __launch_bounds__(1024) void k_readout_bwd_lds(const float* __restrict__ dout, long long stride,
+                                                          const int32_t* __restrict__ nbr,
+                                                          const int32_t* __restrict__ agent_node, int N, int R,
+                                                          int deg, int H, float* __restrict__ dhf,
+                                                          float* __restrict__ dhp) {
+    extern __shared__ float sd[];  // [R][(deg + 1) H]
+    __shared__ int su[64];
+    __shared__ int snb[64 * MAXDEG];
+    const long long g = blockIdx.x;
+    const int W = (deg + 1) * H, W4 = W >> 2;
+    for (int i = threadIdx.x; i < R; i += blockDim.x) su[i] = agent_node ? agent_node[g * R + i] : i;
+    for (int i = threadIdx.x; i < R * W4; i += blockDim.x) {
+        const int r = i / W4, c = i - r * W4;
+        reinterpret_cast<float4*>(sd)[i] = *reinterpret_cast<const float4*>(dout + (g * R + r) * stride + 4 * c);
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < R * deg; i += blockDim.x) {
+        const int r = i / deg, k = i - r * deg;
+        snb[i] = nbr[(g * N + su[r]) * deg + k];
+    }
+    __syncthreads();
+    const int H4 = H >> 2;
+    for (int t = threadIdx.x; t < N * H4; t += blockDim.x) {
+        const int v = t / H4, off = (t - v * H4) * 4;
+        float4 af = make_float4(0.f, 0.f, 0.f, 0.f), ap = af;
+        for (int r = 0; r < R; r++) {
+            const float* drow = sd + r * W;
+            if (su[r] == v) af = f4add(af, *reinterpret_cast<const float4*>(drow + off));
+            for (int k = 0; k < deg; k++)
+                if (snb[r * deg + k] == v) ap = f4add(ap, *reinterpret_cast<const float4*>(drow + (k + 1) * H + off));
+        }
+        const long long node = g * N + v;
+        if (dhf) *reinterpret_cast<float4*>(dhf + node * H + off) = af;
+        if (dhp) *reinterpret_cast<float4*>(dhp + node * H + off) = ap;
+    }
+}
+
 extern "C" int gm_netmon_readout_ld(const float* hf, int64_t ldf, const float* hp, int64_t ldp, const int32_t* nbr,
                                     const int32_t* agent_node, int32_t G, int32_t N, int32_t R, int32_t deg, int32_t H,
                                     float* out, int64_t stride, void* stream) {
@@ -459,6 +535,13 @@ extern "C" int gm_netmon_readout_ld(const float* hf, int64_t ldf, const float* h
     int v2 = vec_width(H, ldf, hf), v3 = vec_width(H, ldp, hp);
     V = V < v2 ? V : v2;
     V = V < v3 ? V : v3;
+    if (V == 4) {
+        const long long rows = (long long)G * R;
+        const long long blocks = std::min<long long>((rows + 3) / 4, 65536);
+        hipLaunchKernelGGL(k_readout_rows, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, hf, hp, nbr,
+                           agent_node, rows, N, R, deg, H, out, (long long)stride, (long long)ldf, (long long)ldp);
+        return launched();
+    }
     long long total = (long long)G * R * (deg + 1) * (H / V);
     GM_VLAUNCH(k_readout, V, dim3(nblocks(total, 256)), hf, hp, nbr, agent_node, G, N, R, deg, H, out,
                (long long)stride, (long long)ldf, (long long)ldp);
@@ -522,6 +605,13 @@ extern "C" int gm_netmon_readout_bwd(const float* dout, int64_t stride, const in
     int V = vec_width(H, stride, dout);
     if (dhf) { int v = vec_width(H, H, dhf); V = V < v ? V : v; }
     if (dhp) { int v = vec_width(H, H, dhp); V = V < v ? V : v; }
+    const size_t lds = (size_t)R * (deg + 1) * H * 4;
+    if (V == 4 && R <= 64 && deg <= MAXDEG && lds <= 48 * 1024) {
+        const int threads = std::min(1024, (N * (H / 4) + 63) / 64 * 64);
+        hipLaunchKernelGGL(k_readout_bwd_lds, dim3(G), dim3(threads), lds, (hipStream_t)stream, dout, (long long)stride,
+                           nbr, agent_node, N, R, deg, H, dhf, dhp);
+        return launched();
+    }
     if (R <= 64 && deg <= MAXDEG && N * (H / V) <= 1024) {
         const int threads = (N * (H / V) + 63) / 64 * 64;
         hipStream_t st = (hipStream_t)stream;
@@ -683,21 +773,34 @@ __global__ __launch_bounds__(1024) void k_qhead_bwd(const float* __restrict__ dq
     for (int q = 0; q < nq; q++) w[q] = ok ? wq[q * ldwq + c] : 0.f;
     const long long r0 = (long long)blockIdx.x * rpb, r1 = min(rows, r0 + rpb);
     float pb = 0.f, mx = 0.f, pw[4] = {0.f, 0.f, 0.f, 0.f}, pq[4] = {0.f, 0.f, 0.f, 0.f};
-    for (long long r = r0; r < r1; r++) {
-        float d[4] = {0.f, 0.f, 0.f, 0.f};
-        for (int q = 0; q < nq; q++) d[q] = dq[r * ldq + q];
+    // U rows per iteration with their loads issued together (independent HBM round trips in flight)
+    constexpr int U = 8;
+    for (long long rb = r0; rb < r1; rb += U) {
+        float d[U][4], yv[U];
 #pragma unroll
-        for (int q = 0; q < 4; q++) pq[q] += d[q];
-        if (ok) {
-            const float yv = y[r * ldy + c];
-            float gv = 0.f;
-            for (int q = 0; q < nq; q++) gv = fmaf(d[q], w[q], gv);
-            if (act && !(yv > 0.f)) gv *= 0.01f;
-            g[r * ldg + c] = gv;
-            pb += gv;
-            mx = fmaxf(mx, fabsf(gv));
+        for (int u = 0; u < U; u++) {
+            const long long r = min(rb + u, r1 - 1);
 #pragma unroll
-            for (int q = 0; q < 4; q++) pw[q] = fmaf(d[q], yv, pw[q]);
+            for (int q = 0; q < 4; q++) d[u][q] = q < nq ? dq[r * ldq + q] : 0.f;
+            yv[u] = ok ? y[r * ldy + c] : 0.f;
+        }
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            if (rb + u >= r1) break;
+            const long long r = rb + u;
+#pragma unroll
+            for (int q = 0; q < 4; q++) pq[q] += d[u][q];
+            if (ok) {
+                float gv = 0.f;
+#pragma unroll
+                for (int q = 0; q < 4; q++) gv = fmaf(d[u][q], w[q], gv);
+                if (act && !(yv[u] > 0.f)) gv *= 0.01f;
+                g[r * ldg + c] = gv;
+                pb += gv;
+                mx = fmaxf(mx, fabsf(gv));
+#pragma unroll
+                for (int q = 0; q < 4; q++) pw[q] = fmaf(d[u][q], yv[u], pw[q]);
+            }
         }
     }
     if (ok) {
