@@ -32,7 +32,7 @@ EXPORTS = [
     "gm_policy_shortest_path", "gm_env_first_hops", "gm_routing_node_encoder", "gm_gemm_x3", "gm_gemm_x3_head", "gm_absmax_scale", "gm_absmax_scale_rows", "gm_gemm_x3_wgrad", "gm_absmax_finish",
     "gm_gemm_pack_x3", "gm_gemm_pack_x3_bytes", "gm_gemm_range_status",
     "gm_pcg64_seed", "gm_pcg64_choice", "gm_lnlstm_pointwise", "gm_agent_attention", "gm_agent_comm",
-    "gm_gemm_x3_dgrad", "gm_lstm_cell_bwd", "gm_qhead_bwd", "gm_netmon_readout_ld",
+    "gm_gemm_x3_dgrad", "gm_lstm_cell_bwd", "gm_qhead_bwd", "gm_netmon_readout_ld", "gm_routing_node_encoder_bits",
 ]
 
 # Arithmetic form of the fused rollout GEMMs (graph-marl_amd/fused.py): "x3" = split-f16
@@ -139,6 +139,7 @@ def lib():
     L.gm_lstm_cell_bwd.argtypes = [C.POINTER(LSTMBwdArgs), vp]
     L.gm_qhead_bwd.argtypes = [vp, i64, i32, vp, i64, vp, i64, i64, i32, i32, vp, i64, vp, vp, vp, i32, vp, vp]
     L.gm_netmon_readout_ld.argtypes = [vp, i64, vp, i64, vp, vp, i32, i32, i32, i32, i32, vp, i64, vp]
+    L.gm_routing_node_encoder_bits.argtypes = [vp, i64, vp, i32, i32, vp, vp, i32, i32, vp, i64, vp, i64, vp]
     L.gm_env_set_topology.argtypes = [vp, i32, i64, vp, i32, i32]
     L.gm_policy_shortest_path.argtypes = [vp, vp, vp]
     L.gm_env_first_hops.argtypes = [vp, vp, vp]

@@ -94,11 +94,15 @@ struct Epi {
     // the leaky derivative of mask[row][col] (the layer's input, nullable = none), go to y, their
     // per-128-row-tile column sums to part[tile][col] (nullable) and their max |.| to gmax
     // (nullable); columns >= split go unchanged to y2[row][col - split]
-    const float* mask;
-    long long ldm;
+    const unsigned* mbits;    // sign bits of the layer input: bit c % 32 of word [row][c / 32] = input > 0
+    long long ldmb;           // words per row (0: one row for all)
     int split;
     float* part;
     unsigned* gmax;
+    // EPI_BIAS: sign bits of y (> 0) out, one uint32 per 32 columns, ldsb words per row (nullable):
+    // the leaky_relu derivative of the layer's output for the training backward, 1/32 of its bytes
+    unsigned* sbits;
+    long long ldsb;
 };
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const float* p, unsigned bytes) {
@@ -219,6 +223,11 @@ __device__ __forceinline__ void epilogue(floatx16 (&acc)[TM][TN], const Epi& ep,
                     float v = acc[i][j][r] + bv;
                     if (ep.act == 1) v = v >= 0.f ? v : 0.01f * v;
                     if (row < M && col < N) ep.y[(long long)row * ep.ldy + col] = v;
+                    if (ep.sbits) {  // lanes 0-31 / 32-63: 32 columns of rows row(h = 0) / row(h = 1)
+                        const unsigned long long b = __ballot(v > 0.f && col < N);
+                        if (l32 == 0 && row < M && wn0 + j * 32 < N)
+                            ep.sbits[(long long)row * ep.ldsb + ((wn0 + j * 32) >> 5)] = (unsigned)(b >> (32 * h));
+                    }
                 }
             }
         }
@@ -540,7 +549,7 @@ __global__ __launch_bounds__(WGM* WGN * 64, OCC) void k_gemm(ASrc a0, ASrc a1, c
 }
 
 // EPI_DGRAD epilogue of k_gemm3 (32x32 C layout): the leaky_relu derivative of the layer input
-// (mask > 0 ? 1 : 0.01, the reference MLP's F.leaky_relu) applied to the input gradient, per
+// (sign bit set ? 1 : 0.01, the reference MLP's F.leaky_relu) applied to the input gradient, per
 // 128-row tile column sums (bias gradient partials: lane sums of its rows, the two lane halves,
 // then the WGM row waves through LDS, a fixed order) and max |g| (the next gradient GEMMs' operand
 // scale). red: >= WGM * WGN * TN * 32 floats of LDS no longer used by the k loop.
@@ -564,8 +573,9 @@ __device__ __forceinline__ void dgrad_epilogue(floatx16 (&acc)[TM][TN], const Ep
                 if (row >= M || col >= N) continue;
                 float v = acc[i][j][r];
                 if (lo) {
-                    // torch's leaky_relu backward: input > 0 ? g : 0.01 g (leaky(z) > 0 iff z > 0)
-                    if (ep.mask && !(ep.mask[(long long)row * ep.ldm + col] > 0.f)) v *= 0.01f;
+                    // torch's leaky_relu backward: input > 0 ? g : 0.01 g (leaky(z) > 0 iff z > 0); the
+                    // 32 lanes of a half read one sign word (a broadcast load)
+                    if (ep.mbits && !((ep.mbits[(long long)row * ep.ldmb + (col >> 5)] >> l32) & 1u)) v *= 0.01f;
                     ep.y[(long long)row * ep.ldy + col] = v;
                     s += v;
                     mx = fmaxf(mx, fabsf(v));
@@ -889,18 +899,34 @@ __device__ __forceinline__ void epilogue16(floatx4 (&acc)[T2][N2], const Epi& ep
                                            int lane, const CIn16<T2, EPI>& cin) {
     const int l16 = lane & 15, rq = 4 * (lane >> 4);
     if constexpr (EPI == EPI_BIAS) {
+        static_assert(N2 % 2 == 0, "column blocks in pairs (32-column sign words)");
 #pragma unroll
-        for (int j = 0; j < N2; j++) {
-            const int col = wn0 + j * 16 + l16;
-            const float bv = (ep.bias && col < N) ? ep.bias[col] : 0.f;
+        for (int jp = 0; jp < N2 / 2; jp++) {
+            float bv[2];
+#pragma unroll
+            for (int b = 0; b < 2; b++) {
+                const int col = wn0 + (2 * jp + b) * 16 + l16;
+                bv[b] = (ep.bias && col < N) ? ep.bias[col] : 0.f;
+            }
 #pragma unroll
             for (int i = 0; i < T2; i++)
 #pragma unroll
                 for (int r = 0; r < 4; r++) {
                     const int row = wm0 + i * 16 + rq + r;
-                    float v = acc[i][j][r] + bv;
-                    if (ep.act == 1) v = v >= 0.f ? v : 0.01f * v;
-                    if (row < M && col < N) ep.y[(long long)row * ep.ldy + col] = v;
+                    unsigned long long bb[2];
+#pragma unroll
+                    for (int b = 0; b < 2; b++) {
+                        const int col = wn0 + (2 * jp + b) * 16 + l16;
+                        float v = acc[i][2 * jp + b][r] + bv[b];
+                        if (ep.act == 1) v = v >= 0.f ? v : 0.01f * v;
+                        if (row < M && col < N) ep.y[(long long)row * ep.ldy + col] = v;
+                        bb[b] = ep.sbits ? __ballot(v > 0.f && col < N) : 0ull;
+                    }
+                    if (ep.sbits && l16 == 0 && row < M && wn0 + jp * 32 < N) {  // group q: 16 columns of row 4q + r
+                        const int q = lane >> 4;
+                        ep.sbits[(long long)row * ep.ldsb + ((wn0 + jp * 32) >> 5)] =
+                            (unsigned)((bb[0] >> (16 * q)) & 0xFFFFull) | ((unsigned)((bb[1] >> (16 * q)) & 0xFFFFull) << 16);
+                    }
                 }
         }
     } else {  // EPI_LSTM: N2 == 8 blocks, gate g of unit 16 b + l16 in block 2 g + b
@@ -1697,6 +1723,14 @@ int gemm_entry(bool x3, const gm_a_src* a0, const gm_a_src* a1, const void* w, i
     ep.c_in = c_in;
     ep.ldc = ldc;
     ep.act_out = act_out;
+    if (epilogue == GM_EPI_BIAS || epilogue == GM_EPI_BIAS_LEAKY) {  // act_out: sign bits of y (x3 form)
+        if (act_out && (!x3 || ldc < (n + 31) / 32))
+            return gm_fail(GM_ERR_INVALID_ARG, std::string(fn) + ": sign bits need the x3 form and ldc >= ceil(n / 32)");
+        ep.sbits = reinterpret_cast<unsigned*>(act_out);
+        ep.ldsb = ldc;
+        ep.act_out = nullptr;
+        ep.c_in = nullptr;
+    }
     if (x3 && (rc = range_flag(&ep.range_flag))) return rc;
     if (epilogue == GM_EPI_GRU) {  // the LSTM gate-tile kernels with the GRU gate math
         if (n % 128 || !c_in || act_out)
@@ -1780,11 +1814,11 @@ extern "C" int gm_gemm_x3(const gm_a_src* a0, const gm_a_src* a1, const void* wp
 }
 
 extern "C" int gm_gemm_x3_dgrad(const gm_a_src* a0, const void* wp, const float* wscale_inv, int32_t m, int32_t n,
-                                int32_t split, const float* mask, int64_t ldm, float* y, int64_t ldy, float* y2,
+                                int32_t split, const uint32_t* mask_bits, int64_t ldm, float* y, int64_t ldy, float* y2,
                                 int64_t ldy2, float* part, float* gmax, void* stream) {
     if (!a0 || a0->mode != GM_A_DENSE || !wp || !wscale_inv || !y || m <= 0 || n <= 0 || split <= 0 || split > n ||
-        ldy < split || (split < n && (!y2 || ldy2 < n - split)) || (mask && ldm < split) ||
-        (reinterpret_cast<uintptr_t>(wp) & 15))
+        ldy < split || (split < n && (!y2 || ldy2 < n - split)) ||
+        (mask_bits && ldm != 0 && ldm < (split + 31) / 32) || (reinterpret_cast<uintptr_t>(wp) & 15))
         return gm_fail(GM_ERR_INVALID_ARG, "gm_gemm_x3_dgrad: bad arguments (dense source, 0 < split <= n)");
     ASrc s0, s1;
     int rc = to_asrc(a0, m, s0);
@@ -1800,8 +1834,8 @@ extern "C" int gm_gemm_x3_dgrad(const gm_a_src* a0, const void* wp, const float*
     ep.ldy = ldy;
     ep.y2 = y2;
     ep.ldy2 = ldy2;
-    ep.mask = mask;
-    ep.ldm = ldm;
+    ep.mbits = mask_bits;
+    ep.ldmb = ldm;
     ep.split = split;
     ep.part = part;
     ep.gmax = reinterpret_cast<unsigned*>(gmax);

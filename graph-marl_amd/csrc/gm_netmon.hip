@@ -254,6 +254,15 @@ __global__ __launch_bounds__(256) void k_lstm_pw_bwd(const float* __restrict__ d
 }
 
 
+// bits 0..15 of x to the even bit positions 0, 2, .., 30
+__device__ __forceinline__ unsigned spread16(unsigned x) {
+    x = (x | (x << 8)) & 0x00FF00FFu;
+    x = (x | (x << 4)) & 0x0F0F0F0Fu;
+    x = (x | (x << 2)) & 0x33333333u;
+    x = (x | (x << 1)) & 0x55555555u;
+    return x;
+}
+
 // First NetMon encoder layer on routing node observations (src/model.py:272-276 on the
 // node obs of src/env/routing.py:187-235). Row n of graph g is
 //   [onehot(n) | cnt | load | 3 x (onehot(nbr_k) | len_k | load_k)]
@@ -265,7 +274,8 @@ __global__ __launch_bounds__(256) void k_routing_enc(const float* __restrict__ x
                                                      const int32_t* __restrict__ nbr, int G, int N,
                                                      const float* __restrict__ wt, const float* __restrict__ b,
                                                      int n, int act, float* __restrict__ y, long long ldy,
-                                                     int rows_per_block) {
+                                                     int rows_per_block, unsigned* __restrict__ sbits,
+                                                     long long ldsb) {
     constexpr int BN = 64 * CPL;
     extern __shared__ float sw[];  // [K][BN]
     const int K = 4 * N + 8;
@@ -343,9 +353,22 @@ __global__ __launch_bounds__(256) void k_routing_enc(const float* __restrict__ x
                 a1 = a1 >= 0.f ? a1 : 0.01f * a1;
             }
             *reinterpret_cast<float2*>(yr) = make_float2(a0, a1);
+            if (sbits) {  // 32-column sign words: lanes 16k..16k+15 hold columns 32k..32k+31, two each
+                const unsigned long long b0 = __ballot(a0 > 0.f), b1 = __ballot(a1 > 0.f);
+                if ((lane & 15) == 0) {
+                    const int k = lane >> 4;
+                    sbits[(base + i) * ldsb + (c0 >> 5) + k] =
+                        spread16((unsigned)(b0 >> (16 * k)) & 0xFFFFu) | (spread16((unsigned)(b1 >> (16 * k)) & 0xFFFFu) << 1);
+                }
+            }
         } else {
 #pragma unroll
             for (int j = 0; j < CPL; j++) yr[j] = act ? (acc[j] >= 0.f ? acc[j] : 0.01f * acc[j]) : acc[j];
+            if (sbits) {
+                const float a0 = act ? (acc[0] >= 0.f ? acc[0] : 0.01f * acc[0]) : acc[0];
+                const unsigned long long b0 = __ballot(a0 > 0.f);
+                if ((lane & 31) == 0) sbits[(base + i) * ldsb + (c0 >> 5) + (lane >> 5)] = (unsigned)(b0 >> lane);
+            }
         }
     }
     }
@@ -857,8 +880,15 @@ extern "C" int gm_qhead_bwd(const float* dq, int64_t ldq, int32_t nq, const floa
 extern "C" int gm_routing_node_encoder(const float* x, int64_t ldx, const int32_t* nbr, int32_t G, int32_t N,
                                        const float* wt, const float* b, int32_t n, int32_t act, float* y, int64_t ldy,
                                        void* stream) {
+    return gm_routing_node_encoder_bits(x, ldx, nbr, G, N, wt, b, n, act, y, ldy, nullptr, 0, stream);
+}
+
+extern "C" int gm_routing_node_encoder_bits(const float* x, int64_t ldx, const int32_t* nbr, int32_t G, int32_t N,
+                                            const float* wt, const float* b, int32_t n, int32_t act, float* y,
+                                            int64_t ldy, uint32_t* sbits, int64_t ldsb, void* stream) {
     if (!x || !nbr || !wt || !y || G <= 0 || N < 4 || n <= 0 || (n % 64) || act < 0 || act > 1 ||
-        ldx < 4 * N + 8 || ldy < n || (ldy % 2) || (reinterpret_cast<uintptr_t>(wt) & 15))
+        ldx < 4 * N + 8 || ldy < n || (ldy % 2) || (reinterpret_cast<uintptr_t>(wt) & 15) ||
+        (sbits && ldsb < n / 32))
         return gm_fail(GM_ERR_INVALID_ARG, "gm_routing_node_encoder: bad arguments (n % 64 == 0, 16-byte W^T)");
     const int K = 4 * N + 8;
     const int cpl = (n % 128 == 0 && (size_t)K * 128 * 4 <= 65536) ? 2 : 1;
@@ -869,10 +899,10 @@ extern "C" int gm_routing_node_encoder(const float* x, int64_t ldx, const int32_
     dim3 grid((unsigned)((M + rows - 1) / rows), (unsigned)(n / (64 * cpl)));
     if (cpl == 2)
         hipLaunchKernelGGL(k_routing_enc<2>, grid, dim3(256), lds, (hipStream_t)stream, x, (long long)ldx, nbr, G, N,
-                           wt, b, n, act, y, (long long)ldy, rows);
+                           wt, b, n, act, y, (long long)ldy, rows, reinterpret_cast<unsigned*>(sbits), (long long)ldsb);
     else
         hipLaunchKernelGGL(k_routing_enc<1>, grid, dim3(256), lds, (hipStream_t)stream, x, (long long)ldx, nbr, G, N,
-                           wt, b, n, act, y, (long long)ldy, rows);
+                           wt, b, n, act, y, (long long)ldy, rows, reinterpret_cast<unsigned*>(sbits), (long long)ldsb);
     return launched();
 }
 

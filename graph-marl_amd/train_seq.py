@@ -146,19 +146,27 @@ def _ptr(t):
     return t if isinstance(t, int) else t.data_ptr()
 
 
-def _gemm_amax(x, ldx, k, x3, b, m, n, epi, y, ldy, slot, a1=None):
+def _sign_bits(rows, n, dev):
+    """uint32 sign words of an activation (bit c % 32 of word c / 32: value > 0), int32 storage."""
+    return torch.empty(rows, (n + 31) // 32, dtype=torch.int32, device=dev)
+
+
+def _gemm_amax(x, ldx, k, x3, b, m, n, epi, y, ldy, slot, a1=None, sbits=None):
     """y = epi([x | a1] @ W^T + b) in split-f16 form, max |A| published into slot; a1 = (tensor, ld,
-    k1) or None. Row blocks below 2 GB per operand."""
+    k1) or None; sbits (optional) receives y's sign bits. Row blocks below 2 GB per operand."""
+    ldsb = 0 if sbits is None else sbits.stride(0)
     for r0, mb in _row_blocks(m, ldx, ldy, a1[1] if a1 else 1):
         src1 = None if a1 is None else FU.dense(_ptr(a1[0]) + 4 * r0 * a1[1], a1[1], a1[2])
         FU.gemm(FU.dense(_ptr(x) + 4 * r0 * ldx, ldx, k, amax=slot.data_ptr()), src1, None, 0,
-                None if b is None else b.data_ptr(), mb, n, epi, _ptr(y) + 4 * r0 * ldy, ldy, x3=x3)
+                None if b is None else b.data_ptr(), mb, n, epi, _ptr(y) + 4 * r0 * ldy, ldy,
+                ldc=ldsb, act_out=None if sbits is None else sbits.data_ptr() + 4 * r0 * ldsb, x3=x3)
 
 
 def _dgrad(g, ldg, k, sc, x3t, m, n, split, mask, ldm, y, ldy, y2=None, ldy2=0, part=None, gmax=None):
-    """gm_gemm_x3_dgrad in row blocks below 2 GB per operand (part rows = 128-row tiles)."""
+    """gm_gemm_x3_dgrad in row blocks below 2 GB per operand (part rows = 128-row tiles); mask = the
+    layer input's sign bits (int32 words, ldm words per row) or None."""
     lib = FU._setup()
-    for r0, mb in _row_blocks(m, ldg, ldy, ldm or 1, ldy2 or 1):
+    for r0, mb in _row_blocks(m, ldg, ldy, ldy2 or 1):
         a = FU.dense(_ptr(g) + 4 * r0 * ldg, ldg, k, scale=sc.data_ptr())
         L.check(lib.gm_gemm_x3_dgrad(C.byref(a), x3t.wp.data_ptr(), x3t.sinv.data_ptr(), mb, n, split,
                                      None if mask is None else _ptr(mask) + 4 * r0 * ldm, ldm, _ptr(y) + 4 * r0 * ldy,
@@ -198,21 +206,23 @@ def _forward(p):
 
     # ---- NetMon encoder over all steps ----
     enc = list(netmon.encode.linear_layers)
-    p.enc_in, p.enc_out = [], []
+    p.enc_in, p.enc_out, p.enc_bits = [], [], []
     x, ldx, kx = X, X.stride(0), F
     for i, lin in enumerate(enc):
         n = lin.out_features
         y = torch.empty(LM, n, device=dev)
+        yb = _sign_bits(LM, n, dev)  # the leaky mask of this output for the backward
         if i == 0 and FU.routing_encoder_ok(lin, N, F, nbr):
-            FU.routing_encoder(lin, X, nbr, Ls * B, N, y)
+            FU.routing_encoder(lin, X, nbr, Ls * B, N, y, sbits=yb)
             sx = torch.empty(1, device=dev)
             L.check(FU._setup().gm_absmax_scale_rows(X.data_ptr(), LM, F, X.stride(0), sx.data_ptr(), L.stream_ptr()))
         else:
             sx = _zeros1(dev)
-            _gemm_amax(x, ldx, kx, _lin_x3(lin), lin.bias, LM, n, FU.GM_EPI_BIAS_LEAKY, y, n, sx)
+            _gemm_amax(x, ldx, kx, _lin_x3(lin), lin.bias, LM, n, FU.GM_EPI_BIAS_LEAKY, y, n, sx, sbits=yb)
             _finish(sx)
         p.enc_in.append((x, ldx, kx, sx))
         p.enc_out.append(y)
+        p.enc_bits.append(yb)
         x, ldx, kx = y, n, n
     E = p.enc_out[-1]  # [LM][H], the obs cell's x
 
@@ -259,16 +269,18 @@ def _forward(p):
     dl = list(dqn.encoder.linear_layers)
     fc = dqn.q_net.fc
     nq = fc.out_features
-    p.d, p.d_in_scale = [], []
+    p.d, p.d_in_scale, p.d_bits = [], [], []
     q = torch.empty(LMa, nq, device=dev)
     for i, lin in enumerate(dl):
         n = lin.out_features
         y = torch.empty(LMa, n, device=dev)
         sx = _zeros1(dev)
         last = i == len(dl) - 1
+        yb = None if last else _sign_bits(LMa, n, dev)
+        p.d_bits.append(yb)
         if i == 0:
             _gemm_amax(R, 4 * H, 4 * H, _dqn_first_x3(lin, od), lin.bias, LMa, n, FU.GM_EPI_BIAS_LEAKY, y, n, sx,
-                       a1=(env, odp, od))
+                       a1=(env, odp, od), sbits=yb)
             if last:
                 torch.addmm(fc.bias.detach(), y, fc.weight.detach().t(), out=q)
         elif last and n <= 256:  # last hidden layer + Q head in one kernel (hidden output written too)
@@ -284,7 +296,7 @@ def _forward(p):
         else:
             prev = p.d[-1]
             _gemm_amax(prev, prev.shape[1], prev.shape[1], _lin_x3(lin), lin.bias, LMa, n, FU.GM_EPI_BIAS_LEAKY, y, n,
-                       sx)
+                       sx, sbits=yb)
             if last:
                 torch.addmm(fc.bias.detach(), y, fc.weight.detach().t(), out=q)
         p.d.append(y)
@@ -336,8 +348,9 @@ def _backward(p, dq):
         gn = torch.empty(LMa, kin, device=dev)
         part = torch.empty((LMa + 127) // 128, kin, device=dev)
         gmax = _zeros1(dev)
-        _dgrad(g, lin.out_features, lin.out_features, sc, _lin_x3t(lin), LMa, kin, kin, xin, kin, gn, kin, part=part,
-               gmax=gmax)
+        xb = p.d_bits[i - 1]
+        _dgrad(g, lin.out_features, lin.out_features, sc, _lin_x3t(lin), LMa, kin, kin, xb, xb.stride(0), gn, kin,
+               part=part, gmax=gmax)
         grads[dl[i - 1].bias] = part.sum(0)
         g, sc = gn, _finish(gmax)
     lin0 = dl[0]
@@ -417,7 +430,8 @@ def _backward(p, dq):
                 # [x | h] input gradient of the obs cell: x part through the encoder's last leaky_relu
                 # (bias partials and max for the batched encoder backward), h part = the state gradient
                 dh0 = dh0_buf[t % 2]
-                _dgrad(dG[0, t], 4 * H, 4 * H, sc_cell, wt_obs, M, S2, H, E[t * M:(t + 1) * M], H,
+                Eb = p.enc_bits[-1]
+                _dgrad(dG[0, t], 4 * H, 4 * H, sc_cell, wt_obs, M, S2, H, Eb[t * M:(t + 1) * M], Eb.stride(0),
                        gE[t * M:(t + 1) * M], H, dh0, H, part=partE[t], gmax=gmaxE)
                 dh_ext, dc_ext = dh0, dco
             dc_next = dco
@@ -445,7 +459,8 @@ def _backward(p, dq):
             gn = torch.empty(LM, kin, device=dev)
             part = torch.empty((LM + 127) // 128, kin, device=dev)
             gmax = _zeros1(dev)
-            _dgrad(g, lin.out_features, lin.out_features, sc, _lin_x3t(lin), LM, kin, kin, xin, ldx, gn, kin,
+            xb = p.enc_bits[i - 1]
+            _dgrad(g, lin.out_features, lin.out_features, sc, _lin_x3t(lin), LM, kin, kin, xb, xb.stride(0), gn, kin,
                    part=part, gmax=gmax)
             grads[enc[i - 1].bias] = part.sum(0)
             g, sc = gn, _finish(gmax)

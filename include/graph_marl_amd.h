@@ -322,6 +322,9 @@ int gm_gemm_f32(const gm_a_src* src0, const gm_a_src* src1, const float* w, int6
 int gm_gemm_x3(const gm_a_src* src0, const gm_a_src* src1, const void* wp, const float* wscale_inv, const float* b,
                int32_t m, int32_t n, int32_t epilogue, float* y, int64_t ldy, float* y2, int64_t ldy2,
                const float* c_in, int64_t ldc, float* act_out, void* stream);
+/* (gm_gemm_x3, GM_EPI_BIAS / GM_EPI_BIAS_LEAKY: act_out, when given, receives the sign bits of y
+ * (bit c % 32 of uint32 word [row][c / 32] set when y > 0; ldc = words per row >= ceil(n / 32)):
+ * the leaky_relu derivative the training backward's gm_gemm_x3_dgrad reads, 1/32 of y's bytes.) */
 /* Status of the split-f16 range guard (no stream synchronisation: the word is host memory the
  * kernels write): *status = 1 when a gm_gemm_x3 / gm_gemm_x3_head launch that has finished
  * produced a non-finite accumulator since the last clear; clear != 0 resets it. Callers check
@@ -339,14 +342,16 @@ int gm_gemm_x3_head(const gm_a_src* src0, const void* wp, const float* wscale_in
 /* Input-gradient GEMM of a layer whose input went through leaky_relu (the reference MLP's
  * F.leaky_relu, src/model.py:13-42, backward of torch autograd, src/main.py:996): D = src0 . W^T
  * in split-f16 form over wp = gm_gemm_pack_x3 of W^T ([n][K], K = src0->k; src0 DENSE, its
- * power-of-two scale in src0->scale); columns < split: g = D * (mask > 0 ? 1 : 0.01) (mask
- * [m][ldm] = the layer input, nullable = no derivative) to y [m][ldy], per-128-row-tile column
+ * power-of-two scale in src0->scale); columns < split: g = D * (input > 0 ? 1 : 0.01), the layer
+ * input's sign given as bits (mask_bits [m][ldm] uint32 words: bit c % 32 of word c / 32 set when
+ * input[c] > 0, as the forward epilogues write them; nullable = no derivative; ldm 0: one row for
+ * all) to y [m][ldy], per-128-row-tile column
  * sums to part [ceil(m / 128)][split] (nullable; the bias gradient of the previous layer) and
  * max |g| as float bits to gmax (nullable, zeroed by the caller; gm_absmax_finish); columns >= split
  * unchanged to y2 [m][ldy2] (e.g. the LSTM [x | h] input gradient split into its parts). */
 int gm_gemm_x3_dgrad(const gm_a_src* src0, const void* wp, const float* wscale_inv, int32_t m, int32_t n,
-                     int32_t split, const float* mask, int64_t ldm, float* y, int64_t ldy, float* y2, int64_t ldy2,
-                     float* part, float* gmax, void* stream);
+                     int32_t split, const uint32_t* mask_bits, int64_t ldm, float* y, int64_t ldy, float* y2,
+                     int64_t ldy2, float* part, float* gmax, void* stream);
 /* Weight-gradient GEMM of the training path: C_z = A_z^T B_z for k-splits z of kchunk rows
  * (K = batch rows): A = dY [k][lda], B = X [k][ldb], both K-major fp32, scaled by the device
  * powers of two sa, sb (gm_absmax_scale) and split into f16 pieces on the way into LDS;
@@ -381,6 +386,10 @@ int gm_gemm_pack_x3(const float* w, int64_t ldw, int32_t n, int32_t k, void* wp,
 int gm_routing_node_encoder(const float* x, int64_t ldx, const int32_t* nbr, int32_t G, int32_t N,
                             const float* wt, const float* b, int32_t n, int32_t act, float* y, int64_t ldy,
                             void* stream);
+/* The same, also writing the sign bits of y (as gm_gemm_x3's act_out; ldsb words per row). */
+int gm_routing_node_encoder_bits(const float* x, int64_t ldx, const int32_t* nbr, int32_t G, int32_t N,
+                                 const float* wt, const float* b, int32_t n, int32_t act, float* y, int64_t ldy,
+                                 uint32_t* sbits, int64_t ldsb, void* stream);
 /* ---- Agent models (DGN, CommNet): per-env A x A agent communication ----
  * gm_agent_attention (AttModel.forward, src/model.py:86-117): for every env b, agent i and
  * head h: w_ij = <q_i, k_j> / sqrt(dk); p = softmax_j(adj_ij ? w_ij : -1e9); out_i =

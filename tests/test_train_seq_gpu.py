@@ -24,6 +24,51 @@ def _rel(a, b):
     return (a.double() - b.double()).abs().max().item() / max(b.double().abs().max().item(), 1e-30)
 
 
+def _pack_bits(b):
+    """bool [rows][cols] -> int32 words [rows][ceil(cols / 32)], bit c % 32 of word c / 32."""
+    rows, cols = b.shape
+    W = (cols + 31) // 32
+    x = torch.zeros(rows, W * 32, dtype=torch.int64, device=b.device)
+    x[:, :cols] = b.long()
+    w = (x.view(rows, W, 32) << torch.arange(32, device=b.device)).sum(-1)
+    return torch.where(w >= 2 ** 31, w - 2 ** 32, w).to(torch.int32).contiguous()
+
+
+@pytest.mark.parametrize("n,mfma", [(512, 1), (256, 0), (96, 1), (40, 1)])
+def test_forward_sign_bits(n, mfma):
+    """Sign bits written by the forward epilogues (k_gemm3g 16x16 / 32x32, k_gemm3, routing encoder)
+    equal the activation's y > 0."""
+    M, T, S, FU, L = mods()
+    gm = importlib.import_module("graph-marl_amd")
+    torch.manual_seed(n)
+    m, k = 40000, 256
+    x = torch.randn(m, k, device="cuda")
+    lin = M.Linear(k, n, act=1).cuda()
+    y = torch.empty(m, n, device="cuda")
+    bits = S._sign_bits(m, n, "cuda")
+    slot = torch.zeros(1, device="cuda")
+    FU.L.check(FU._setup().gm_gemm_set_mfma(mfma))
+    try:
+        for tile in (-1, 0):
+            FU._setup().gm_gemm_set_tile(tile)
+            bits.fill_(-7)
+            S._gemm_amax(x, k, k, S._lin_x3(lin), lin.bias, m, n, FU.GM_EPI_BIAS_LEAKY, y, n, slot, sbits=bits)
+            assert torch.equal(bits, _pack_bits(y > 0)), tile
+    finally:
+        FU._setup().gm_gemm_set_tile(-1)
+        FU._setup().gm_gemm_set_mfma(1)
+    B, N = 64, 20
+    env = gm.Routing(gm.Network(N, random_topology=True, excluded_seeds=gm.EVAL_SEEDS), 20, n_env=B, seed=3)
+    env.reset()
+    for out in (512, 64):
+        lin0 = M.Linear(4 * N + 8, out, act=1).cuda()
+        x0 = env.node_obs.reshape(-1, 4 * N + 8)
+        y0 = torch.empty(B * N, out, device="cuda")
+        b0 = S._sign_bits(B * N, out, "cuda")
+        FU.routing_encoder(lin0, x0, env.nbr, B, N, y0, sbits=b0)
+        assert torch.equal(b0, _pack_bits(y0 > 0)), out
+
+
 def _fro(a, b):
     return (a.double() - b.double()).norm().item() / max(b.double().norm().item(), 1e-30)
 
@@ -45,7 +90,9 @@ def test_dgrad_epilogue_vs_torch(m, n, k, split):
     y2 = torch.empty(m, max(n - split, 1), device="cuda")
     part = torch.empty((m + 127) // 128, split, device="cuda")
     gmax = torch.zeros(1, device="cuda")
-    S._dgrad(g, k, k, sc, x3, m, n, split, mask, split, y, split, y2 if split < n else None, n - split, part, gmax)
+    bits = _pack_bits(mask > 0)
+    S._dgrad(g, k, k, sc, x3, m, n, split, bits, bits.stride(0), y, split, y2 if split < n else None, n - split, part,
+             gmax)
     ref = g.double() @ w.double()
     lo = torch.where(mask.double() > 0, ref[:, :split], 0.01 * ref[:, :split])
     assert _rel(y, lo) < 1e-5
