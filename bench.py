@@ -75,15 +75,21 @@ def pmc_traffic(tag):
     rocprofv3 PMC passes (profiles/*/pmc_traffic.json); None when not profiled."""
     import glob
 
-    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "*", "pmc_traffic.json")), reverse=True):
+    found = []
+    for path in glob.glob(os.path.join(ROOT, "profiles", "*", "*", "pmc_traffic.json")):
         try:
             with open(path) as f:
-                k = json.load(f)["kernels"].get(tag)
+                d = json.load(f)
+            k = d["kernels"].get(tag)
         except (OSError, ValueError, KeyError):
             continue
-        if k:
-            return k["fetch_bytes"] + k["write_bytes"], os.path.relpath(path, ROOT)
-    return None, None
+        if k:  # newest = highest round directory, then the profile's own "seq" within the round
+            rnd = os.path.basename(os.path.dirname(os.path.dirname(path)))
+            found.append(((rnd, d.get("seq", 0)), k["fetch_bytes"] + k["write_bytes"], os.path.relpath(path, ROOT)))
+    if not found:
+        return None, None
+    _, tb, src = max(found)
+    return tb, src
 
 
 def cpu_model():

@@ -3,8 +3,9 @@
 Two spawned ranks share cuda:0 (gloo process group: the one GPU of a test box cannot host two
 RCCL ranks of the same device) and run the real training path of bench.py / main.py: each rank
 rolls out its own env shard (disjoint seeds, train.shard_seeds), fills its device replay, and
-runs train.dqn_update (NetMon + DQN, split-f16 GEMMs, HIP backward kernels) on its own sampled
-sequences, with the one flattened gradient all-reduce before clipping (reference
+runs train.dqn_update or the sequence-batched train_seq.dqn_update_seq (NetMon + DQN, split-f16
+GEMMs, HIP backward kernels) on its own sampled sequences, with the one flattened gradient
+all-reduce before clipping (reference
 src/main.py:840-1026 per rank). Checks: the all-reduced gradient is the mean of
 the ranks' local gradients, the ranks' local losses differ (disjoint shards), and after two
 updates every parameter of NetMon, DQN and the target DQN is bit-identical across ranks.
@@ -39,7 +40,7 @@ def _gather(t, world):
     return out
 
 
-def _worker(rank, world, port, q):
+def _worker(rank, world, port, q, seq_path=False):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     torch.cuda.set_device(0)
@@ -88,8 +89,14 @@ def _worker(rank, world, port, q):
         for _ in range(2):
             dqn.train()
             netmon.train()
-            batches = list(buff.get_batch(BATCH, sequence_length=SEQ))
-            loss, _, _ = T.dqn_update(netmon, dqn, target, opt, params, batches, 0.98, 0.01)
+            if seq_path:  # the sequence-batched update (bench.py / main.py default for this model)
+                TS = importlib.import_module("graph-marl_amd.train_seq")
+                assert TS.seq_ok(netmon, dqn, target)
+                loss, _, _ = TS.dqn_update_seq(netmon, dqn, target, opt, params, buff.get_sequences(BATCH, SEQ), 0.98,
+                                               0.01)
+            else:
+                batches = list(buff.get_batch(BATCH, sequence_length=SEQ))
+                loss, _, _ = T.dqn_update(netmon, dqn, target, opt, params, batches, 0.98, 0.01)
             netmon.state = None
             losses.append(float(loss))
             loc = _gather(rec["local"], world)
@@ -112,11 +119,12 @@ def _worker(rank, world, port, q):
         dist.destroy_process_group()
 
 
-def test_two_rank_dqn_update_keeps_replicas_identical():
+@pytest.mark.parametrize("seq_path", [False, True])
+def test_two_rank_dqn_update_keeps_replicas_identical(seq_path):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q, seq_path)) for r in range(2)]
     for p in procs:
         p.start()
     res = {}
