@@ -66,7 +66,8 @@ struct ASrc {
     const int* nbr;           // [G][N][deg]
     const int* agent_node;    // READOUT: [G*R]
     int n_nodes, deg, mean, rows_per_graph, k, hidden;
-    unsigned bytes0, bytes1;  // buffer extents for the bounds check
+    long long bytes0, bytes1; // buffer extents for the bounds check (DENSE: of the whole operand; the
+                              // kernels address its rows relative to their block's first row)
     const float* scale;       // k_gemm3 DENSE source: power-of-two A scale (nullable)
     unsigned* amax;           // k_gemm3: max |A| float bits published here (nullable)
 };
@@ -107,6 +108,14 @@ struct Epi {
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const float* p, unsigned bytes) {
     return __builtin_amdgcn_make_buffer_rsrc((void*)p, (short)0, (int)bytes, 0x00020000);
+}
+// buffer resource over the rows [r0, ..) of a row-major operand of `bytes` bytes: 32-bit offsets stay
+// small whatever the operand's size; the extent is clamped below the OOB sentinel
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc_rows(const float* p, long long ld, long long r0,
+                                                           long long bytes) {
+    long long rem = bytes - r0 * ld * 4;
+    rem = rem < 0 ? 0 : (rem > 0x7fe00000LL ? 0x7fe00000LL : rem);
+    return rsrc(p + r0 * ld, (unsigned)rem);
 }
 __device__ __forceinline__ float4 bload(__amdgpu_buffer_rsrc_t r, int byte_off) {
     u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(r, byte_off, 0, 0);
@@ -390,8 +399,8 @@ __global__ __launch_bounds__(WGM* WGN * 64, OCC) void k_gemm(ASrc a0, ASrc a1, c
 #pragma unroll
     for (int q = 0; q < C::AQ; q++) {
         int row = min(m0 + rbase + q * C::RSTEP, M - 1);
-        rowoff0[q] = (int)(row * a0.ld0);
-        rowoff1[q] = (int)(row * a1.ld0);
+        rowoff0[q] = AMODE == GM_A_DENSE ? (int)((row - m0) * a0.ld0) : (int)(row * a0.ld0);
+        rowoff1[q] = (int)((row - m0) * a1.ld0);
         scale[q] = 1.0f;
         if (AMODE == GM_A_AGGREGATE) {
             const int g = row / a0.n_nodes, n = row - g * a0.n_nodes;
@@ -427,9 +436,10 @@ __global__ __launch_bounds__(WGM* WGN * 64, OCC) void k_gemm(ASrc a0, ASrc a1, c
 #pragma unroll
     for (int q = 0; q < C::BQ; q++) woff[q] = (int)(min(n0 + rbase + q * C::RSTEP, N - 1) * ldw);
 
-    const __amdgpu_buffer_rsrc_t r0a = rsrc(a0.p0, a0.bytes0);
-    const __amdgpu_buffer_rsrc_t r0b = rsrc(a0.p1 ? a0.p1 : a0.p0, a0.p1 ? a0.bytes1 : a0.bytes0);
-    const __amdgpu_buffer_rsrc_t r1 = rsrc(a1.p0 ? a1.p0 : a0.p0, a1.p0 ? a1.bytes0 : 0u);
+    const __amdgpu_buffer_rsrc_t r0a =
+        AMODE == GM_A_DENSE ? rsrc_rows(a0.p0, a0.ld0, m0, a0.bytes0) : rsrc(a0.p0, (unsigned)a0.bytes0);
+    const __amdgpu_buffer_rsrc_t r0b = rsrc(a0.p1 ? a0.p1 : a0.p0, (unsigned)(a0.p1 ? a0.bytes1 : a0.bytes0));
+    const __amdgpu_buffer_rsrc_t r1 = a1.p0 ? rsrc_rows(a1.p0, a1.ld0, m0, a1.bytes0) : rsrc(a0.p0, 0u);
     const __amdgpu_buffer_rsrc_t rw = rsrc(w, wbytes);
 
     float4 ra[C::AQ], rb[C::BQ];
@@ -646,12 +656,12 @@ __global__ __launch_bounds__(WGM* WGN * 64, OCC) void k_gemm3(ASrc a0, ASrc a1, 
 #pragma unroll
     for (int q = 0; q < AQ; q++) {
         const int row = min(m0 + rbase + q * RSTEP, M - 1);
-        off1[q] = (int)(row * a1.ld0) * 4;
+        off1[q] = (int)((row - m0) * a1.ld0) * 4;
         scale[q] = 1.0f;
 #pragma unroll
         for (int j = 0; j < 4; j++) so[q][j] = OOB;
         if (AMODE == GM_A_DENSE) {
-            so[q][0] = (int)(row * a0.ld0) * 4;
+            so[q][0] = (int)((row - m0) * a0.ld0) * 4;
         } else if (AMODE == GM_A_AGGREGATE) {
             // members of (I + A) row n in ascending node id (SimpleAggregation's bmm order)
             const int g = row / a0.n_nodes, n = row - g * a0.n_nodes;
@@ -684,9 +694,10 @@ __global__ __launch_bounds__(WGM* WGN * 64, OCC) void k_gemm3(ASrc a0, ASrc a1, 
 #pragma unroll
     for (int q = 0; q < BQ; q++) woff[q] = (int)(min(n0 + rbase + q * RSTEP, N - 1) * ldw) + 16 * c4;
 
-    const __amdgpu_buffer_rsrc_t r0a = rsrc(a0.p0, a0.bytes0);
-    const __amdgpu_buffer_rsrc_t r0b = rsrc(a0.p1 ? a0.p1 : a0.p0, a0.p1 ? a0.bytes1 : a0.bytes0);
-    const __amdgpu_buffer_rsrc_t r1 = rsrc(a1.p0 ? a1.p0 : a0.p0, a1.p0 ? a1.bytes0 : 0u);
+    const __amdgpu_buffer_rsrc_t r0a =
+        AMODE == GM_A_DENSE ? rsrc_rows(a0.p0, a0.ld0, m0, a0.bytes0) : rsrc(a0.p0, (unsigned)a0.bytes0);
+    const __amdgpu_buffer_rsrc_t r0b = rsrc(a0.p1 ? a0.p1 : a0.p0, (unsigned)(a0.p1 ? a0.bytes1 : a0.bytes0));
+    const __amdgpu_buffer_rsrc_t r1 = a1.p0 ? rsrc_rows(a1.p0, a1.ld0, m0, a1.bytes0) : rsrc(a0.p0, 0u);
     const __amdgpu_buffer_rsrc_t rw = rsrc(reinterpret_cast<const float*>(w), wbytes);
 
     float4 ra[2][AQ][NR], rb[2][BQ];
@@ -1085,11 +1096,11 @@ __global__ __launch_bounds__(WGM* WGN * 64, OCC) void k_gemm3g(ASrc a0, ASrc a1,
         const int R = (wave * NA + j) * 8 + sub;
         const int c = (lane & 7) ^ ((R >> 1) & 7);
         const int row = min(m0 + R, M - 1);
-        o1[j] = (int)(row * a1.ld0) * 4 + 16 * c;
+        o1[j] = (int)((row - m0) * a1.ld0) * 4 + 16 * c;
 #pragma unroll
         for (int s = 0; s < 4; s++) so[j][s] = OOB;
         if (AMODE == GM_A_DENSE) {
-            so[j][0] = (int)(row * a0.ld0) * 4 + 16 * c;
+            so[j][0] = (int)((row - m0) * a0.ld0) * 4 + 16 * c;
         } else {  // READOUT: [h_final[v] | h_prev[nbr(v, 0..2)]], v = agent_node[row]
             const int g = row / a0.rows_per_graph;
             const int v = a0.agent_node[row];
@@ -1110,9 +1121,10 @@ __global__ __launch_bounds__(WGM* WGN * 64, OCC) void k_gemm3g(ASrc a0, ASrc a1,
         wo[j] = (int)(min(n0 + R, N - 1) * ldw) + 16 * c;
     }
 
-    const __amdgpu_buffer_rsrc_t r0a = rsrc(a0.p0, a0.bytes0);
-    const __amdgpu_buffer_rsrc_t r0b = rsrc(a0.p1 ? a0.p1 : a0.p0, a0.p1 ? a0.bytes1 : a0.bytes0);
-    const __amdgpu_buffer_rsrc_t r1 = rsrc(a1.p0 ? a1.p0 : a0.p0, a1.p0 ? a1.bytes0 : 0u);
+    const __amdgpu_buffer_rsrc_t r0a =
+        AMODE == GM_A_DENSE ? rsrc_rows(a0.p0, a0.ld0, m0, a0.bytes0) : rsrc(a0.p0, (unsigned)a0.bytes0);
+    const __amdgpu_buffer_rsrc_t r0b = rsrc(a0.p1 ? a0.p1 : a0.p0, (unsigned)(a0.p1 ? a0.bytes1 : a0.bytes0));
+    const __amdgpu_buffer_rsrc_t r1 = a1.p0 ? rsrc_rows(a1.p0, a1.ld0, m0, a1.bytes0) : rsrc(a0.p0, 0u);
     const __amdgpu_buffer_rsrc_t rw = rsrc(reinterpret_cast<const float*>(w), wbytes);
 
     // DMA of k tile kt into stage ST (all LDS bases wave-uniform)
@@ -1501,15 +1513,17 @@ int to_asrc(const gm_a_src* s, int M, ASrc& o) {
             rows0 = (long long)(M / s->rows_per_graph) * s->n_nodes;
             long long b1 = ((rows0 - 1) * s->ld1 + s->hidden) * 4;
             if (!fits(b1)) return gm_fail(GM_ERR_UNSUPPORTED, "gm_gemm_f32: source larger than 2 GB");
-            o.bytes1 = (unsigned)b1;
+            o.bytes1 = b1;
         } else {
             return gm_fail(GM_ERR_INVALID_ARG, "gm_gemm_f32: unknown A source mode");
         }
     }
     long long width = s->mode == GM_A_READOUT ? s->hidden : s->k;
     long long b0 = ((rows0 - 1) * s->ld0 + width) * 4;
-    if (!fits(b0)) return gm_fail(GM_ERR_UNSUPPORTED, "gm_gemm_f32: source larger than 2 GB (split M)");
-    o.bytes0 = (unsigned)b0;
+    // dense rows are addressed from the block's first row (any size); gathered sources are not
+    if (s->mode != GM_A_DENSE && !fits(b0))
+        return gm_fail(GM_ERR_UNSUPPORTED, "gm_gemm_f32: gathered source larger than 2 GB (split M)");
+    o.bytes0 = b0;
     return GM_OK;
 }
 
@@ -2124,7 +2138,9 @@ __global__ __launch_bounds__(256, BN == 128 ? 2 : 1) void k_wgrad_tr(const float
     const int kb = blockIdx.y * kchunk, ke = min(K, kb + kchunk);
     const int nk = (ke - kb + BK - 1) / BK;
     const float s_a = *sa, s_b = *sb;
-    const __amdgpu_buffer_rsrc_t ra = rsrc(A, abytes), rb = rsrc(B, bbytes);
+    // buffer resources over this block's k chunk only: 32-bit offsets stay small whatever the batch
+    // (abytes / bbytes: the bytes of one chunk of rows, host-checked)
+    const __amdgpu_buffer_rsrc_t ra = rsrc(A + (long long)kb * lda, abytes), rb = rsrc(B + (long long)kb * ldb, bbytes);
     // loader map: A tile 32 k x 128 m = 32 float4 per k row -> lane q = tid & 31 (m = 4q), rows
     // (tid >> 5) + 8 j; B tile 32 x BN: BN / 4 float4 per row
     constexpr int QB = BN / 4, RB_STEP = 256 / QB;
@@ -2135,13 +2151,13 @@ __global__ __launch_bounds__(256, BN == 128 ? 2 : 1) void k_wgrad_tr(const float
 #pragma unroll
         for (int j = 0; j < LA; j++) {
             const int k = k0 + ka0 + 8 * j, m = m0 + 4 * qa;
-            const int off = (k < ke && m < M) ? (int)(((long long)k * lda + m) * 4) : OOB;
+            const int off = (k < ke && m < M) ? (int)(((long long)(k - kb) * lda + m) * 4) : OOB;
             va[j] = bload(ra, off);
         }
 #pragma unroll
         for (int j = 0; j < LB; j++) {
             const int k = k0 + kb0 + RB_STEP * j, n = n0 + 4 * qb;
-            const int off = (k < ke && n < N) ? (int)(((long long)k * ldb + n) * 4) : OOB;
+            const int off = (k < ke && n < N) ? (int)(((long long)(k - kb) * ldb + n) * 4) : OOB;
             vb[j] = bload(rb, off);
         }
     };
@@ -2257,9 +2273,11 @@ extern "C" int gm_gemm_x3_wgrad(const float* a, int64_t lda, const float* b, int
         hipLaunchKernelGGL(k_gemm3_kmajor, dim3(T, S), dim3(256), 0, (hipStream_t)stream, a, (long long)lda, b,
                            (long long)ldb, m, n, k, kchunk, sa, sb, c, (long long)ldc, (long long)m * ldc);
     } else {
-        const long long ab = (long long)k * lda * 4, bb = (long long)k * ldb * 4;
+        // per-block buffer resources cover one k chunk (any batch size; a chunk below 2 GB)
+        const long long kc = std::min<long long>(kchunk, k);
+        const long long ab = kc * lda * 4, bb = kc * ldb * 4;
         if (ab >= 0x7ff00000LL || bb >= 0x7ff00000LL)
-            return gm_fail(GM_ERR_UNSUPPORTED, "gm_gemm_x3_wgrad: operand larger than 2 GB (split the batch)");
+            return gm_fail(GM_ERR_UNSUPPORTED, "gm_gemm_x3_wgrad: one k chunk of an operand larger than 2 GB");
         if (g_wgrad != 2) {  // 128 x 128 tiles at 2 blocks/CU: 8-24 % faster than 128 x 256 at 1 block/CU
             const int T = ((m + 127) / 128) * ((n + 127) / 128);
             hipLaunchKernelGGL(k_wgrad_tr<128>, dim3(T, S), dim3(256), 0, (hipStream_t)stream, a, (long long)lda,

@@ -183,19 +183,13 @@ def _wgrad(gy, x, k, sa=None, sb=None):
         sb = torch.empty(1, device=dev)
         L.check(lib.gm_absmax_scale_rows(x.data_ptr(), Mb, k, ldx, sb.data_ptr(), L.stream_ptr()))
     tiles = ((o + 127) // 128) * ((N + 127) // 128)
-    # the kernel addresses each operand with 32-bit byte offsets: batches past 2 GB run in row blocks
-    rows_max = ((1 << 31) - (1 << 25)) // (4 * max(ldx, o)) // 2048 * 2048
-    total = None
-    for r0 in range(0, Mb, rows_max):
-        mb = min(rows_max, Mb - r0)
-        splits = max(1, min(mb // 2048, (1024 + tiles - 1) // tiles))
-        kchunk = ((mb + splits - 1) // splits + 31) // 32 * 32  # the kernel's k tile is 32 deep
-        splits = (mb + kchunk - 1) // kchunk
-        part = torch.empty(splits, o, N, device=dev)
-        L.check(lib.gm_gemm_x3_wgrad(gy.data_ptr() + 4 * r0 * o, o, x.data_ptr() + 4 * r0 * ldx, ldx, o, N, mb, kchunk,
-                                     sa.data_ptr(), sb.data_ptr(), part.data_ptr(), N, L.stream_ptr()))
-        total = part.sum(0) if total is None else total + part.sum(0)
-    return total[:, :k]
+    splits = max(1, min(Mb // 2048, (1024 + tiles - 1) // tiles))
+    kchunk = ((Mb + splits - 1) // splits + 31) // 32 * 32  # the kernel's k tile is 32 deep
+    splits = (Mb + kchunk - 1) // kchunk
+    part = torch.empty(splits, o, N, device=dev)
+    L.check(lib.gm_gemm_x3_wgrad(gy.data_ptr(), o, x.data_ptr(), ldx, o, N, Mb, kchunk, sa.data_ptr(), sb.data_ptr(),
+                                 part.data_ptr(), N, L.stream_ptr()))
+    return part.sum(0)[:, :k]
 
 
 class LinearFn(torch.autograd.Function):

@@ -59,16 +59,6 @@ def seq_ok(netmon, model, model_tar, att_coeff=0.0, aux_model=None):
             and dq[-1].out_features <= 1024)
 
 
-_LIMIT = (1 << 31) - (1 << 24)  # the GEMM kernels address an operand with 32-bit byte offsets
-
-
-def _row_blocks(m, *widths):
-    """Row blocks (r0, rows) of an m-row GEMM whose operands have the given row widths (floats) so
-    that no operand block reaches 2 GB; blocks are multiples of 128 rows (the GEMM tile)."""
-    step = max(128, (_LIMIT - (1 << 20)) // (4 * max(widths)) // 128 * 128)
-    return [(r0, min(step, m - r0)) for r0 in range(0, m, step)]
-
-
 def _zeros1(dev):
     return torch.zeros(1, device=dev)
 
@@ -153,26 +143,21 @@ def _sign_bits(rows, n, dev):
 
 def _gemm_amax(x, ldx, k, x3, b, m, n, epi, y, ldy, slot, a1=None, sbits=None):
     """y = epi([x | a1] @ W^T + b) in split-f16 form, max |A| published into slot; a1 = (tensor, ld,
-    k1) or None; sbits (optional) receives y's sign bits. Row blocks below 2 GB per operand."""
-    ldsb = 0 if sbits is None else sbits.stride(0)
-    for r0, mb in _row_blocks(m, ldx, ldy, a1[1] if a1 else 1):
-        src1 = None if a1 is None else FU.dense(_ptr(a1[0]) + 4 * r0 * a1[1], a1[1], a1[2])
-        FU.gemm(FU.dense(_ptr(x) + 4 * r0 * ldx, ldx, k, amax=slot.data_ptr()), src1, None, 0,
-                None if b is None else b.data_ptr(), mb, n, epi, _ptr(y) + 4 * r0 * ldy, ldy,
-                ldc=ldsb, act_out=None if sbits is None else sbits.data_ptr() + 4 * r0 * ldsb, x3=x3)
+    k1) or None; sbits (optional) receives y's sign bits."""
+    src1 = None if a1 is None else FU.dense(_ptr(a1[0]), a1[1], a1[2])
+    FU.gemm(FU.dense(_ptr(x), ldx, k, amax=slot.data_ptr()), src1, None, 0, None if b is None else b.data_ptr(), m,
+            n, epi, _ptr(y), ldy, ldc=0 if sbits is None else sbits.stride(0),
+            act_out=None if sbits is None else sbits.data_ptr(), x3=x3)
 
 
 def _dgrad(g, ldg, k, sc, x3t, m, n, split, mask, ldm, y, ldy, y2=None, ldy2=0, part=None, gmax=None):
-    """gm_gemm_x3_dgrad in row blocks below 2 GB per operand (part rows = 128-row tiles); mask = the
-    layer input's sign bits (int32 words, ldm words per row) or None."""
-    lib = FU._setup()
-    for r0, mb in _row_blocks(m, ldg, ldy, ldy2 or 1):
-        a = FU.dense(_ptr(g) + 4 * r0 * ldg, ldg, k, scale=sc.data_ptr())
-        L.check(lib.gm_gemm_x3_dgrad(C.byref(a), x3t.wp.data_ptr(), x3t.sinv.data_ptr(), mb, n, split,
-                                     None if mask is None else _ptr(mask) + 4 * r0 * ldm, ldm, _ptr(y) + 4 * r0 * ldy,
-                                     ldy, None if y2 is None else _ptr(y2) + 4 * r0 * ldy2, ldy2,
-                                     None if part is None else part.data_ptr() + 4 * (r0 // 128) * split,
-                                     None if gmax is None else gmax.data_ptr(), L.stream_ptr()))
+    """gm_gemm_x3_dgrad (part rows = 128-row tiles); mask = the layer input's sign bits (int32 words,
+    ldm words per row) or None."""
+    a = FU.dense(_ptr(g), ldg, k, scale=sc.data_ptr())
+    L.check(FU._setup().gm_gemm_x3_dgrad(C.byref(a), x3t.wp.data_ptr(), x3t.sinv.data_ptr(), m, n, split,
+                                         None if mask is None else _ptr(mask), ldm, _ptr(y), ldy,
+                                         None if y2 is None else _ptr(y2), ldy2, None if part is None else part.data_ptr(),
+                                         None if gmax is None else gmax.data_ptr(), L.stream_ptr()))
 
 
 class _Plan:
@@ -288,11 +273,10 @@ def _forward(p):
             kp = prev.shape[1]
             x3 = _lin_x3(lin)
             wq = fc.weight.detach().contiguous()
-            for r0, mb in _row_blocks(LMa, kp, n):
-                L.check(FU._setup().gm_gemm_x3_head(
-                    C.byref(FU.dense(prev.data_ptr() + 4 * r0 * kp, kp, kp, amax=sx.data_ptr())), x3.wp.data_ptr(),
-                    x3.sinv.data_ptr(), lin.bias.data_ptr(), mb, n, 1, wq.data_ptr(), wq.stride(0), fc.bias.data_ptr(),
-                    nq, q.data_ptr() + 4 * r0 * nq, nq, y.data_ptr() + 4 * r0 * n, n, L.stream_ptr()))
+            L.check(FU._setup().gm_gemm_x3_head(
+                C.byref(FU.dense(prev.data_ptr(), kp, kp, amax=sx.data_ptr())), x3.wp.data_ptr(), x3.sinv.data_ptr(),
+                lin.bias.data_ptr(), LMa, n, 1, wq.data_ptr(), wq.stride(0), fc.bias.data_ptr(), nq, q.data_ptr(), nq,
+                y.data_ptr(), n, L.stream_ptr()))
         else:
             prev = p.d[-1]
             _gemm_amax(prev, prev.shape[1], prev.shape[1], _lin_x3(lin), lin.bias, LMa, n, FU.GM_EPI_BIAS_LEAKY, y, n,
@@ -499,12 +483,8 @@ def _target_max(p, model_tar, gamma_unused=None):
     if Ls > 1:
         env = sb.obs[1:].reshape((Ls - 1) * B, A, odp)[..., :od]
         graph = p.R[Ma:].view((Ls - 1) * B, A, 4 * H)
-        width = max(4 * H, max(l.out_features for l in model_tar.encoder.linear_layers))
-        o = out[:-1].view((Ls - 1) * B, A)
-        for s0, ns in _row_blocks((Ls - 1) * B, A * width):  # samples per block: operands below 2 GB
-            q = FU.dqn_q_dense(model_tar, env[s0:s0 + ns], graph[s0:s0 + ns],
-                               lambda i, m, n: torch.empty(m, n, device=dev))
-            o[s0:s0 + ns] = q.view(ns, A, -1).max(dim=-1)[0]
+        q = FU.dqn_q_dense(model_tar, env, graph, lambda i, m, n: torch.empty(m, n, device=dev))
+        out[:-1] = q.view(Ls - 1, B, A, -1).max(dim=-1)[0]
         done_rows = sb.episode_done[:-1].nonzero().cpu()  # one host read per update
         for t in torch.unique(done_rows[:, 0]).tolist():
             r = done_rows[done_rows[:, 0] == t, 1].to(dev)

@@ -341,3 +341,27 @@ def _compare_paths(M, T, S, L, netmon, model, target, batches, seq, params):
     print("Frobenius-relative gradient error vs exact fp32 (autograd x3, sequence-batched x3):", errs)
     for n, (e_old, e_new) in errs.items():
         assert e_new < max(2e-5, 2 * e_old), (n, e_old, e_new)
+
+
+def test_operands_beyond_2gb():
+    """Dense GEMM sources and weight-gradient operands past 2 GB (the kernels address rows relative
+    to their block / k chunk with 32-bit offsets): split-f16 forward GEMM and weight gradient vs
+    fp64 on a 1.1 M x 512 operand (2.25 GB)."""
+    M, T, S, FU, L = mods()
+    torch.manual_seed(5)
+    m, k, n = 1_100_000, 512, 64
+    x = torch.randn(m, k, device="cuda")
+    assert x.numel() * 4 > 2 ** 31
+    lin = M.Linear(k, n, act=1).cuda()
+    y = torch.empty(m, n, device="cuda")
+    slot = torch.zeros(1, device="cuda")
+    S._gemm_amax(x, k, k, S._lin_x3(lin), lin.bias, m, n, FU.GM_EPI_BIAS_LEAKY, y, n, slot)
+    rows = torch.cat([torch.arange(0, 256, device="cuda"), torch.arange(m - 256, m, device="cuda"),
+                      torch.randint(0, m, (4096,), device="cuda")])
+    ref = F.leaky_relu(F.linear(x[rows].double(), lin.weight.double(), lin.bias.double()), 0.01)
+    assert (y[rows].double() - ref).abs().max().item() < 1e-4
+    assert slot.item() == x.abs().max().item()
+    gy = torch.randn(m, n, device="cuda") * 1e-3
+    gw = M._wgrad(gy, x, k)
+    refw = gy.double().t() @ x.double()
+    assert _rel(gw, refw) < 1e-5
