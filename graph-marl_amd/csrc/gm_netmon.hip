@@ -487,22 +487,60 @@ __global__ __launch_bounds__(256) void k_readout_rows(const float* __restrict__ 
     const long long wave = ((long long)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     const long long nw = ((long long)gridDim.x * blockDim.x) >> 6;
     const int H4 = H >> 2, W4 = (deg + 1) * H4;
-    for (long long row = wave; row < rows; row += nw) {
-        const long long g = row / R;
-        const int r = (int)(row - g * R);
-        const int v = __builtin_amdgcn_readfirstlane(agent_node ? agent_node[row] : r);
-        const int32_t* nb = nbr + (g * N + v) * deg;
-        float* orow = out + row * stride;
-        for (int c = lane; c < W4; c += 64) {
-            const int seg = c / H4, off = (c - seg * H4) * 4;
-            float4 val = make_float4(0.f, 0.f, 0.f, 0.f);
-            if (seg == 0) {
-                val = *reinterpret_cast<const float4*>(hf + (g * N + v) * ldf + off);
-            } else {
-                const int m = nb[seg - 1];
-                if (m >= 0) val = *reinterpret_cast<const float4*>(hp + (g * N + m) * ldp + off);
+    // U rows per iteration: their node ids first, then every row's loads, then the stores
+    constexpr int U = 4, C = 2;  // C float4 per lane and row cover W4 <= 128 (larger W4: the loop below)
+    for (long long rb = wave * U; rb < rows; rb += nw * U) {
+        long long src[U][C];
+        float* dst[U];
+        bool okc[U][C];
+#pragma unroll
+        for (int k = 0; k < U; k++) {
+            const long long row = min(rb + k, rows - 1);
+            const long long g = row / R;
+            const int r = (int)(row - g * R);
+            const int v = agent_node ? agent_node[row] : r;
+            dst[k] = (rb + k < rows) ? out + row * stride : nullptr;
+#pragma unroll
+            for (int cc = 0; cc < C; cc++) {
+                const int c = lane + 64 * cc;
+                const int seg = c / H4, off = (c - seg * H4) * 4;
+                okc[k][cc] = c < W4;
+                const int m = seg == 0 ? v : (c < W4 ? nbr[(g * N + v) * deg + seg - 1] : -1);
+                src[k][cc] = m < 0 ? -1 : (seg == 0 ? (g * N + m) * ldf + off : -(2 + (g * N + m) * ldp + off));
             }
-            *reinterpret_cast<float4*>(orow + 4 * c) = val;
+        }
+        float4 val[U][C];
+#pragma unroll
+        for (int k = 0; k < U; k++)
+#pragma unroll
+            for (int cc = 0; cc < C; cc++) {
+                const long long o = src[k][cc];
+                val[k][cc] = make_float4(0.f, 0.f, 0.f, 0.f);
+                if (okc[k][cc] && o != -1) val[k][cc] = o >= 0 ? *reinterpret_cast<const float4*>(hf + o)
+                                                                : *reinterpret_cast<const float4*>(hp + (-o - 2));
+            }
+#pragma unroll
+        for (int k = 0; k < U; k++)
+#pragma unroll
+            for (int cc = 0; cc < C; cc++)
+                if (dst[k] && okc[k][cc]) *reinterpret_cast<float4*>(dst[k] + 4 * (lane + 64 * cc)) = val[k][cc];
+        for (int k = 0; k < U && W4 > 64 * C; k++) {  // columns past 64 C float4 (wide readouts)
+            const long long row = rb + k;
+            if (row >= rows) break;
+            const long long g = row / R;
+            const int r = (int)(row - g * R);
+            const int v = agent_node ? agent_node[row] : r;
+            for (int c = lane + 64 * C; c < W4; c += 64) {
+                const int seg = c / H4, off = (c - seg * H4) * 4;
+                float4 x = make_float4(0.f, 0.f, 0.f, 0.f);
+                if (seg == 0) {
+                    x = *reinterpret_cast<const float4*>(hf + (g * N + v) * ldf + off);
+                } else {
+                    const int m = nbr[(g * N + v) * deg + seg - 1];
+                    if (m >= 0) x = *reinterpret_cast<const float4*>(hp + (g * N + m) * ldp + off);
+                }
+                *reinterpret_cast<float4*>(out + row * stride + 4 * c) = x;
+            }
         }
     }
 }
