@@ -568,6 +568,18 @@ __device__ __forceinline__ void dgrad_epilogue(floatx16 (&acc)[TM][TN], const Ep
                                                int wr, int wc, int M, int N, int lane) {
     const int h = lane >> 5, l32 = lane & 31;
     const int wm0 = m0 + wr * TM * 32, wn0 = n0 + wc * TN * 32;
+    constexpr int BM = WGM * TM * 32, BN = WGN * TN * 32, WPR = BN / 32;
+    // the tile's sign words (BM rows x BN / 32) staged in LDS with coalesced loads (all ones = no
+    // derivative where there is no mask or the column lies past split)
+    unsigned* smb = reinterpret_cast<unsigned*>(red + WGM * BN);
+    if (ep.mbits) {
+        for (int e = threadIdx.x; e < BM * WPR; e += WGM * WGN * 64) {
+            const int r = e / WPR, w = e - r * WPR;
+            const int row = m0 + r, col0 = n0 + 32 * w;
+            smb[e] = (row < M && col0 < ep.split) ? ep.mbits[(long long)row * ep.ldmb + (col0 >> 5)] : ~0u;
+        }
+        __syncthreads();
+    }
     float mx = 0.f;
     float cs[TN];
 #pragma unroll
@@ -585,7 +597,7 @@ __device__ __forceinline__ void dgrad_epilogue(floatx16 (&acc)[TM][TN], const Ep
                 if (lo) {
                     // torch's leaky_relu backward: input > 0 ? g : 0.01 g (leaky(z) > 0 iff z > 0); the
                     // 32 lanes of a half read one sign word (a broadcast load)
-                    if (ep.mbits && !((ep.mbits[(long long)row * ep.ldmb + (col >> 5)] >> l32) & 1u)) v *= 0.01f;
+                    if (ep.mbits && !((smb[(row - m0) * WPR + ((col - n0) >> 5)] >> l32) & 1u)) v *= 0.01f;
                     ep.y[(long long)row * ep.ldy + col] = v;
                     s += v;
                     mx = fmaxf(mx, fabsf(v));
@@ -600,7 +612,6 @@ __device__ __forceinline__ void dgrad_epilogue(floatx16 (&acc)[TM][TN], const Ep
         if (lane == 0) gm_amax_publish(ep.gmax, mx);
     }
     if (ep.part) {
-        constexpr int BN = WGN * TN * 32;
         if (h == 0) {
 #pragma unroll
             for (int j = 0; j < TN; j++) red[wr * BN + wc * TN * 32 + j * 32 + l32] = cs[j];

@@ -28,10 +28,10 @@ def timeit(fn, reps=5):
 
 m = int(os.environ.get("ROWS", "1040384"))
 out = {}
-for n, k in ((512, 256), (256, 128), (512, 512)):
+for n, k in ((512, 256), (256, 128), (256, 512)):
     g = torch.randn(m, k, device="cuda") * 1e-6
     w = torch.randn(k, n, device="cuda") / k ** 0.5
-    mask = torch.randn(m, n, device="cuda")
+    mask = torch.randint(-2 ** 31, 2 ** 31 - 1, (m, (n + 31) // 32), dtype=torch.int32, device="cuda")  # sign words
     sc = torch.empty(1, device="cuda")
     L.check(FU._setup().gm_absmax_scale(g.data_ptr(), g.numel(), sc.data_ptr(), L.stream_ptr()))
     x3 = S._x3(w.t().contiguous())
@@ -48,7 +48,8 @@ for n, k in ((512, 256), (256, 128), (512, 512)):
                                      None if msk is None else msk.data_ptr(), ldm, y.data_ptr(), n, None, 0,
                                      None if prt is None else prt.data_ptr(), None if gm is None else gm.data_ptr(),
                                      L.stream_ptr()))
-    for name, msk, ldm, prt, gm in (("mask+part+max", mask, n, part, gmax), ("mask_cached+part+max", mask, 0, part, gmax),
+    for name, msk, ldm, prt, gm in (("mask+part+max", mask, (n + 31) // 32, part, gmax),
+                                    ("mask_cached+part+max", mask, 0, part, gmax),
                                     ("part+max", None, 0, part, gmax), ("bare", None, 0, None, None)):
         us = min(timeit(lambda: raw(msk, ldm, prt, gm)) for _ in range(3))
         r[name] = round(us, 1)
