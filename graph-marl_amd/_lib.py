@@ -27,7 +27,7 @@ EXPORTS = [
     "gm_env_step", "gm_env_observe", "gm_env_topology", "gm_env_final_info", "gm_policy_egreedy",
     "gm_env_get_state", "gm_env_set_state", "gm_build_seed_list", "gm_mp_aggregate", "gm_mp_aggregate_rows", "gm_mp_aggregate_bwd", "gm_leaky_bwd", "gm_netmon_readout",
     "gm_netmon_readout_bwd", "gm_lstm_pointwise", "gm_lstm_pointwise_bwd", "gm_linear_f32", "gm_gemm_f32",
-    "gm_gemm_set_tile", "gm_gemm_set_wgrad", "gm_gemm_set_mfma", "gm_simple_create", "gm_simple_destroy", "gm_simple_reset", "gm_simple_step",
+    "gm_gemm_set_tile", "gm_gemm_set_wgrad", "gm_gemm_set_mfma", "gm_gemm_set_dgrad", "gm_simple_create", "gm_simple_destroy", "gm_simple_reset", "gm_simple_step",
     "gm_simple_observe", "gm_simple_policy_egreedy", "gm_simple_get_state", "gm_env_set_topology",
     "gm_policy_shortest_path", "gm_env_first_hops", "gm_routing_node_encoder", "gm_gemm_x3", "gm_gemm_x3_head", "gm_absmax_scale", "gm_absmax_scale_rows", "gm_gemm_x3_wgrad", "gm_absmax_finish",
     "gm_gemm_pack_x3", "gm_gemm_pack_x3_bytes", "gm_gemm_range_status",
@@ -47,6 +47,10 @@ if GEMM_MODE not in ("x3", "f32"):
 MFMA_SHAPE = os.environ.get("GM_MFMA")
 if MFMA_SHAPE not in (None, "16", "32", "16all"):
     raise ValueError(f"GM_MFMA must be '16', '32' or '16all', not {MFMA_SHAPE!r}")
+# input-gradient kernel form of gm_gemm_x3_dgrad (gm_gemm_set_dgrad: -1 per-shape default, 0 / 1 / 2)
+DGRAD_FORM = os.environ.get("GM_DGRAD")
+if DGRAD_FORM not in (None, "-1", "0", "1", "2"):
+    raise ValueError(f"GM_DGRAD must be -1, 0, 1 or 2, not {DGRAD_FORM!r}")
 
 
 class EnvConfig(C.Structure):
@@ -136,6 +140,7 @@ def lib():
     L.gm_gemm_set_tile.argtypes = [i32]
     L.gm_gemm_set_wgrad.argtypes = [i32]
     L.gm_gemm_set_mfma.argtypes = [i32]
+    L.gm_gemm_set_dgrad.argtypes = [i32]
     L.gm_lstm_cell_bwd.argtypes = [C.POINTER(LSTMBwdArgs), vp]
     L.gm_qhead_bwd.argtypes = [vp, i64, i32, vp, i64, vp, i64, i64, i32, i32, vp, i64, vp, vp, vp, i32, vp, vp]
     L.gm_netmon_readout_ld.argtypes = [vp, i64, vp, i64, vp, vp, i32, i32, i32, i32, i32, vp, i64, vp]
@@ -156,6 +161,8 @@ def lib():
     if MFMA_SHAPE is not None:
         if L.gm_gemm_set_mfma({"16": 1, "32": 0, "16all": 2}[MFMA_SHAPE]) != 0:
             raise GMError(L.gm_last_error().decode())
+    if DGRAD_FORM is not None and L.gm_gemm_set_dgrad(int(DGRAD_FORM)) != 0:
+        raise GMError(L.gm_last_error().decode())
     _lib = L
     return L
 

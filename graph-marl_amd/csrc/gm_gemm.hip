@@ -563,7 +563,7 @@ __global__ __launch_bounds__(WGM* WGN * 64, OCC) void k_gemm(ASrc a0, ASrc a1, c
 // 128-row tile column sums (bias gradient partials: lane sums of its rows, the two lane halves,
 // then the WGM row waves through LDS, a fixed order) and max |g| (the next gradient GEMMs' operand
 // scale). red: >= WGM * WGN * TN * 32 floats of LDS no longer used by the k loop.
-template <int WGM, int WGN, int TM, int TN>
+template <int WGM, int WGN, int TM, int TN, bool STAGED = false>
 __device__ __forceinline__ void dgrad_epilogue(floatx16 (&acc)[TM][TN], const Epi& ep, float* red, int m0, int n0,
                                                int wr, int wc, int M, int N, int lane) {
     const int h = lane >> 5, l32 = lane & 31;
@@ -572,7 +572,7 @@ __device__ __forceinline__ void dgrad_epilogue(floatx16 (&acc)[TM][TN], const Ep
     // the tile's sign words (BM rows x BN / 32) staged in LDS with coalesced loads (all ones = no
     // derivative where there is no mask or the column lies past split)
     unsigned* smb = reinterpret_cast<unsigned*>(red + WGM * BN);
-    if (ep.mbits) {
+    if (ep.mbits && !STAGED) {
         for (int e = threadIdx.x; e < BM * WPR; e += WGM * WGN * 64) {
             const int r = e / WPR, w = e - r * WPR;
             const int row = m0 + r, col0 = n0 + 32 * w;
@@ -989,6 +989,75 @@ __device__ __forceinline__ void epilogue16(floatx4 (&acc)[T2][N2], const Epi& ep
         }
     }
 }
+// EPI_DGRAD on the 16x16 layout (dgrad_epilogue's contract): block j covers columns wn0 + 16 j +
+// (l & 15), so a 32-column sign word spans block pair (2p, 2p + 1); column sums over the lane's 4
+// rows, its 4 row groups (xor 16, 32), then the WGM row waves through LDS.
+template <int WGM, int WGN, int T2, int N2, bool STAGED = false>
+__device__ __forceinline__ void dgrad_epilogue16(floatx4 (&acc)[T2][N2], const Epi& ep, float* red, int m0, int n0,
+                                                 int wr, int wc, int M, int N, int lane) {
+    const int l16 = lane & 15, rq = 4 * (lane >> 4);
+    const int wm0 = m0 + wr * T2 * 16, wn0 = n0 + wc * N2 * 16;
+    constexpr int BM = WGM * T2 * 16, BN = WGN * N2 * 16, WPR = BN / 32;
+    static_assert(N2 % 2 == 0, "column blocks in pairs (32-column sign words)");
+    unsigned* smb = reinterpret_cast<unsigned*>(red + WGM * BN);
+    if (ep.mbits && !STAGED) {
+        for (int e = threadIdx.x; e < BM * WPR; e += WGM * WGN * 64) {
+            const int r = e / WPR, w = e - r * WPR;
+            const int row = m0 + r, col0 = n0 + 32 * w;
+            smb[e] = (row < M && col0 < ep.split) ? ep.mbits[(long long)row * ep.ldmb + (col0 >> 5)] : ~0u;
+        }
+        __syncthreads();
+    }
+    float mx = 0.f;
+    float cs[N2];
+#pragma unroll
+    for (int j = 0; j < N2; j++) {
+        const int col = wn0 + j * 16 + l16;
+        const int bit = (j & 1) * 16 + l16, wofs = (col - n0) >> 5;
+        const bool lo = col < ep.split;
+        float s = 0.f;
+#pragma unroll
+        for (int i = 0; i < T2; i++)
+#pragma unroll
+            for (int r = 0; r < 4; r++) {
+                const int row = wm0 + i * 16 + rq + r;
+                if (row >= M || col >= N) continue;
+                float v = acc[i][j][r];
+                if (lo) {
+                    if (ep.mbits && !((smb[(row - m0) * WPR + wofs] >> bit) & 1u)) v *= 0.01f;
+                    ep.y[(long long)row * ep.ldy + col] = v;
+                    s += v;
+                    mx = fmaxf(mx, fabsf(v));
+                } else {
+                    ep.y2[(long long)row * ep.ldy2 + col - ep.split] = v;
+                }
+            }
+        s += __shfl_xor(s, 16);
+        cs[j] = s + __shfl_xor(s, 32);
+    }
+    if (ep.gmax) {
+        mx = gm_wave_max(mx);
+        if (lane == 0) gm_amax_publish(ep.gmax, mx);
+    }
+    if (ep.part) {
+        if (lane < 16) {
+#pragma unroll
+            for (int j = 0; j < N2; j++) red[wr * BN + wc * N2 * 16 + j * 16 + l16] = cs[j];
+        }
+        __syncthreads();
+        if (wr == 0 && lane < 16) {
+#pragma unroll
+            for (int j = 0; j < N2; j++) {
+                const int c = wc * N2 * 16 + j * 16 + l16, col = n0 + c;
+                float s = red[c];
+#pragma unroll
+                for (int w = 1; w < WGM; w++) s += red[w * BN + c];
+                if (col < ep.split && col < N) ep.part[(long long)(m0 / BM) * ep.split + col] = s;
+            }
+        }
+    }
+}
+
 // EPI_HEAD on the 16x16 layout: per row block i, a lane's partial dot products (4 rows x 4 heads)
 // are reduce-scattered over its 16-lane group (xor 8..1: 15 shuffles; lane ends with entry l & 15
 // = row 4 (l >> 4) + (e >> 2), head e & 3), the WGN column waves summed through LDS.
@@ -1178,6 +1247,21 @@ __global__ __launch_bounds__(WGM* WGN * 64, OCC) void k_gemm3g(ASrc a0, ASrc a1,
         for (int j = 0; j < NB; j++) dma16(rw, bbase + j * 1024, wo[j], k0 * 4);
     };
 
+    // EPI_DGRAD: the tile's sign words are loaded before the k loop (their latency hides under it)
+    // and staged in LDS after it; MW words per thread
+    constexpr int MW = EPI == EPI_DGRAD ? BM * (BN / 32) / (NW * 64) : 0;
+    static_assert(EPI != EPI_DGRAD || MW * NW * 64 == BM * (BN / 32), "sign words per thread");
+    unsigned mw[MW > 0 ? MW : 1];
+    if constexpr (EPI == EPI_DGRAD) {
+        if (ep.mbits) {
+#pragma unroll
+            for (int q = 0; q < MW; q++) {
+                const int e = tid + q * NW * 64, r = e / (BN / 32), wd = e - r * (BN / 32);
+                const int row = m0 + r, col0 = n0 + 32 * wd;
+                mw[q] = (row < M && col0 < ep.split) ? ep.mbits[(long long)row * ep.ldmb + (col0 >> 5)] : ~0u;
+            }
+        }
+    }
     std::conditional_t<MF == 1, CIn16<2 * TM, EPI>, CIn<TM, EPI>> cin;
     if constexpr (MF == 1)
         cin_load16<2 * TM, EPI>(cin, ep, m0 + wr * TM * 32, n0 + wc * TN * 32, M, lane);
@@ -1426,7 +1510,17 @@ __global__ __launch_bounds__(WGM* WGN * 64, OCC) void k_gemm3g(ASrc a0, ASrc a1,
 #pragma unroll
                 for (int r = 0; r < 4; r++) acc4[i][j][r] *= si;
         range_guard16<2 * TM, 2 * TN>(acc4, ep.range_flag, lane);
-        if constexpr (EPI == EPI_HEAD)
+        if constexpr (EPI == EPI_DGRAD) {
+            __syncthreads();  // every wave is past its last fragment reads: LDS is scratch from here
+            if (ep.mbits) {
+                unsigned* smb = reinterpret_cast<unsigned*>(lds) + WGM * BN;
+#pragma unroll
+                for (int q = 0; q < MW; q++) smb[tid + q * NW * 64] = mw[q];
+                __syncthreads();
+            }
+            dgrad_epilogue16<WGM, WGN, 2 * TM, 2 * TN, true>(acc4, ep, reinterpret_cast<float*>(lds), m0, n0, wr, wc, M,
+                                                             N, lane);
+        } else if constexpr (EPI == EPI_HEAD)
             head_epilogue16<2 * TM, 2 * TN, WGN, BM>(acc4, ep, lds, m0, wr, wc, M, N, lane, tid);
         else
             epilogue16<2 * TM, 2 * TN, EPI>(acc4, ep, m0 + wr * TM * 32, n0 + wc * TN * 32, M, N, lane, cin);
@@ -1438,7 +1532,16 @@ __global__ __launch_bounds__(WGM* WGN * 64, OCC) void k_gemm3g(ASrc a0, ASrc a1,
 #pragma unroll
                 for (int r = 0; r < 16; r++) acc[i][j][r] *= si;
         range_guard<TM, TN>(acc, ep.range_flag, lane);
-        if constexpr (EPI == EPI_HEAD)
+        if constexpr (EPI == EPI_DGRAD) {
+            __syncthreads();
+            if (ep.mbits) {
+                unsigned* smb = reinterpret_cast<unsigned*>(lds) + WGM * BN;
+#pragma unroll
+                for (int q = 0; q < MW; q++) smb[tid + q * NW * 64] = mw[q];
+                __syncthreads();
+            }
+            dgrad_epilogue<WGM, WGN, TM, TN, true>(acc, ep, reinterpret_cast<float*>(lds), m0, n0, wr, wc, M, N, lane);
+        } else if constexpr (EPI == EPI_HEAD)
             head_epilogue<TM, TN, WGN, BM>(acc, ep, lds, m0, wr, wc, M, N, lane, tid);
         else
             epilogue<TM, TN, EPI>(acc, ep, m0 + wr * TM * 32, n0 + wc * TN * 32, M, N, lane, cin);
@@ -1449,6 +1552,9 @@ __global__ __launch_bounds__(WGM* WGN * 64, OCC) void k_gemm3g(ASrc a0, ASrc a1,
 // stays on 32x32x16 (tools/mfma_ab.sh: rollout kernels 2-5 % faster on 16x16x32, except the
 // head, 89.5 -> 105 us per 81920 rows); 2 = 16x16x32 for the head too
 int g_mfma16 = 1;
+// input-gradient kernel (gm_gemm_set_dgrad): -1 per-shape default, 0 k_gemm3 128x128, 1 k_gemm3g
+// 128x128 (4 waves), 2 k_gemm3g 128x256 (8 waves)
+int g_dgrad = -1;
 
 template <int WGM, int WGN, int TM, int TN, int STAGES, int AMODE, int EPI, int OCC, int AX = 0>
 int launch_g(const ASrc& a0, const ASrc& a1, const float* w, long long ldw, unsigned wbytes, int M, int N, int K,
@@ -1865,8 +1971,22 @@ extern "C" int gm_gemm_x3_dgrad(const gm_a_src* a0, const void* wp, const float*
     ep.part = part;
     ep.gmax = reinterpret_cast<unsigned*>(gmax);
     if ((rc = range_flag(&ep.range_flag))) return rc;
-    return launch<2, 2, 2, 2, 16, GM_A_DENSE, EPI_DGRAD, 2, true>(s0, s1, static_cast<const float*>(wp), ldw,
-                                                                 (unsigned)wb, m, n, K, ep, (hipStream_t)stream,
+    const float* w = static_cast<const float*>(wp);
+    hipStream_t st = (hipStream_t)stream;
+    // tools/dgrad_bench.py at 1.04 M rows: the LDS-DMA tile gains 13-15 % at K = 512 and 2-3 % at
+    // K = 256; the register-staged tile stays ahead at K = 128 (four k tiles)
+    const int form = g_dgrad >= 0 ? g_dgrad : (m >= 32768 && K >= 256 ? 1 : 0);
+    if (form == 1)  // LDS-DMA 128x128, 4 waves, 2 blocks/CU
+        return s0.scale ? launch_g<4, 1, 1, 4, 2, GM_A_DENSE, EPI_DGRAD, 2, 2>(s0, s1, w, ldw, (unsigned)wb, m, n, K, ep,
+                                                                               st, wscale_inv)
+                        : launch_g<4, 1, 1, 4, 2, GM_A_DENSE, EPI_DGRAD, 2, 0>(s0, s1, w, ldw, (unsigned)wb, m, n, K, ep,
+                                                                               st, wscale_inv);
+    if (form == 2)  // LDS-DMA 128x256, 8 waves, 1 block/CU
+        return s0.scale ? launch_g<4, 2, 1, 4, 2, GM_A_DENSE, EPI_DGRAD, 1, 2>(s0, s1, w, ldw, (unsigned)wb, m, n, K, ep,
+                                                                               st, wscale_inv)
+                        : launch_g<4, 2, 1, 4, 2, GM_A_DENSE, EPI_DGRAD, 1, 0>(s0, s1, w, ldw, (unsigned)wb, m, n, K, ep,
+                                                                               st, wscale_inv);
+    return launch<2, 2, 2, 2, 16, GM_A_DENSE, EPI_DGRAD, 2, true>(s0, s1, w, ldw, (unsigned)wb, m, n, K, ep, st,
                                                                  wscale_inv);
 }
 
@@ -2333,6 +2453,12 @@ extern "C" int gm_gemm_pack_x3(const float* w, int64_t ldw, int32_t n, int32_t k
 extern "C" int gm_gemm_set_wgrad(int32_t form) {
     if (form < -1 || form > 2) return gm_fail(GM_ERR_INVALID_ARG, "gm_gemm_set_wgrad: form in [-1, 2]");
     g_wgrad = form;
+    return GM_OK;
+}
+
+extern "C" int gm_gemm_set_dgrad(int32_t form) {
+    if (form < -1 || form > 2) return gm_fail(GM_ERR_INVALID_ARG, "gm_gemm_set_dgrad: form -1..2");
+    g_dgrad = form;
     return GM_OK;
 }
 

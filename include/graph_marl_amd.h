@@ -418,6 +418,10 @@ int gm_gemm_set_tile(int32_t tile);
  * everywhere, 2 = 16x16x32 everywhere. Same tiles and operand images; the summation order inside
  * an MFMA differs (fp32-order results either way). */
 int gm_gemm_set_mfma(int32_t shape);
+/* Input-gradient kernel of gm_gemm_x3_dgrad (same arithmetic and epilogue contract; A-B timing):
+ * -1 (default) = per-shape choice, 0 = register-staged 128 x 128 tile (k_gemm3), 1 = LDS-DMA
+ * 128 x 128 tile (4 waves, 2 blocks/CU), 2 = LDS-DMA 128 x 256 tile (8 waves). Process-wide. */
+int gm_gemm_set_dgrad(int32_t form);
 
 /* ---------------------------------------------------------------------------
  * SimpleEnvironment (src/env/simple_environment.py:45-334; BASELINE config 1):

@@ -73,11 +73,24 @@ def _fro(a, b):
     return (a.double() - b.double()).norm().item() / max(b.double().norm().item(), 1e-30)
 
 
+@pytest.mark.parametrize("form,mfma", [(-1, 1), (0, 1), (1, 1), (1, 0), (2, 1), (2, 0)])
 @pytest.mark.parametrize("m,n,k,split", [(70000, 512, 256, 512), (4099, 256, 512, 128), (300, 64, 48, 40)])
-def test_dgrad_epilogue_vs_torch(m, n, k, split):
+def test_dgrad_epilogue_vs_torch(m, n, k, split, form, mfma):
     """gm_gemm_x3_dgrad: D = g W (scaled split-f16 A), leaky derivative of the mask on columns < split,
-    bias partials, max |g|; columns >= split unchanged into y2."""
+    bias partials, max |g|; columns >= split unchanged into y2. Every kernel form (gm_gemm_set_dgrad)
+    and MFMA shape of the LDS-DMA forms."""
     M, T, S, FU, L = mods()
+    lib = FU._setup()
+    L.check(lib.gm_gemm_set_dgrad(form))
+    L.check(lib.gm_gemm_set_mfma(mfma))
+    try:
+        _dgrad_case(M, T, S, FU, L, m, n, k, split)
+    finally:
+        lib.gm_gemm_set_dgrad(-1)
+        lib.gm_gemm_set_mfma(1)
+
+
+def _dgrad_case(M, T, S, FU, L, m, n, k, split):
     torch.manual_seed(m)
     g = torch.randn(m, k, device="cuda") * 1e-4
     w = torch.randn(k, n, device="cuda") / k ** 0.5  # gx = g @ w, w = W of a Linear [k out][n in]

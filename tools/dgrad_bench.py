@@ -28,7 +28,7 @@ def timeit(fn, reps=5):
 
 m = int(os.environ.get("ROWS", "1040384"))
 out = {}
-for n, k in ((512, 256), (256, 128), (256, 512)):
+for n, k in ((512, 256), (512, 512), (256, 128), (256, 512)):
     g = torch.randn(m, k, device="cuda") * 1e-6
     w = torch.randn(k, n, device="cuda") / k ** 0.5
     mask = torch.randint(-2 ** 31, 2 ** 31 - 1, (m, (n + 31) // 32), dtype=torch.int32, device="cuda")  # sign words
@@ -48,12 +48,25 @@ for n, k in ((512, 256), (256, 128), (256, 512)):
                                      None if msk is None else msk.data_ptr(), ldm, y.data_ptr(), n, None, 0,
                                      None if prt is None else prt.data_ptr(), None if gm is None else gm.data_ptr(),
                                      L.stream_ptr()))
-    for name, msk, ldm, prt, gm in (("mask+part+max", mask, (n + 31) // 32, part, gmax),
-                                    ("mask_cached+part+max", mask, 0, part, gmax),
-                                    ("part+max", None, 0, part, gmax), ("bare", None, 0, None, None)):
-        us = min(timeit(lambda: raw(msk, ldm, prt, gm)) for _ in range(3))
-        r[name] = round(us, 1)
-    r["tflops_bare"] = round(6.0 * m * n * k / (r["bare"] * 1e-6) / 1e12, 1)
+    forms = [(int(f.split(":")[0]), int(f.split(":")[1])) for f in os.environ.get("FORMS", "0:1").split(",")]
+    y0 = None
+    for form, mf in forms:  # gm_gemm_set_dgrad form : gm_gemm_set_mfma shape
+        L.check(lib.gm_gemm_set_dgrad(form))
+        L.check(lib.gm_gemm_set_mfma(mf))
+        tag = f"f{form}m{mf}:"
+        for name, msk, ldm, prt, gm in (("mask+part+max", mask, (n + 31) // 32, part, gmax),
+                                        ("part+max", None, 0, part, gmax), ("bare", None, 0, None, None)):
+            us = min(timeit(lambda: raw(msk, ldm, prt, gm)) for _ in range(3))
+            r[tag + name] = round(us, 1)
+        r[tag + "tflops_bare"] = round(6.0 * m * n * k / (r[tag + "bare"] * 1e-6) / 1e12, 1)
+        raw(mask, (n + 31) // 32, part, gmax)
+        torch.cuda.synchronize()
+        if y0 is None:
+            y0 = y.clone()
+        else:
+            r[tag + "rel_vs_first"] = float((y - y0).abs().max() / y0.abs().max())
+    lib.gm_gemm_set_dgrad(-1)
+    lib.gm_gemm_set_mfma(1)
     out[f"{n}x{k}"] = r
     print(n, k, r, flush=True)
 print(json.dumps(out))
