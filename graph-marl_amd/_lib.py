@@ -32,7 +32,7 @@ EXPORTS = [
     "gm_policy_shortest_path", "gm_env_first_hops", "gm_routing_node_encoder", "gm_gemm_x3", "gm_gemm_x3_head", "gm_absmax_scale", "gm_absmax_scale_rows", "gm_gemm_x3_wgrad", "gm_absmax_finish",
     "gm_gemm_pack_x3", "gm_gemm_pack_x3_bytes", "gm_gemm_range_status",
     "gm_pcg64_seed", "gm_pcg64_choice", "gm_lnlstm_pointwise", "gm_agent_attention", "gm_agent_comm",
-    "gm_gemm_x3_dgrad", "gm_lstm_cell_bwd", "gm_qhead_bwd", "gm_netmon_readout_ld", "gm_routing_node_encoder_bits",
+    "gm_gemm_x3_dgrad", "gm_lstm_cell_bwd", "gm_qhead_bwd", "gm_netmon_readout_ld", "gm_routing_node_encoder_bits", "gm_gather_records",
 ]
 
 # Arithmetic form of the fused rollout GEMMs (graph-marl_amd/fused.py): "x3" = split-f16
@@ -157,6 +157,7 @@ def lib():
     L.gm_gemm_range_status.argtypes = [C.POINTER(i32), i32]
     L.gm_pcg64_seed.argtypes = [C.c_uint64, C.POINTER(PCG64)]
     L.gm_pcg64_choice.argtypes = [vp, i64, i64, vp, vp]
+    L.gm_gather_records.argtypes = [vp, i64, i64, vp, vp, i32, i64, i64, vp, vp]
     L.gm_lnlstm_pointwise.argtypes = [vp, i64, vp, i64] + [vp] * 7 + [i32, i32, C.c_float, vp, i64, vp, i64, vp]
     if MFMA_SHAPE is not None:
         if L.gm_gemm_set_mfma({"16": 1, "32": 0, "16all": 2}[MFMA_SHAPE]) != 0:

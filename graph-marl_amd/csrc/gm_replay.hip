@@ -229,3 +229,51 @@ extern "C" int gm_pcg64_choice(gm_pcg64* state, int64_t n, int64_t count, int64_
     if (e != hipSuccess) return gm_fail(GM_ERR_HIP, std::string("gm_pcg64_choice launch: ") + hipGetErrorString(e));
     return GM_OK;
 }
+
+// ---- sampled-field gather (replaybuffer.get_sequences): dst row i = the (slot[i], env[i % n_env_idx])
+// record of a ring field, `bytes` (a multiple of 16) per record. The records of a sampled batch are
+// scattered KB-sized blocks; the flattened float4 index space is split into 1024-float4 chunks per
+// workgroup with U loads in flight per thread (torch's advanced indexing reads them at ~1.9 TB/s).
+constexpr int GU = 4;
+__global__ __launch_bounds__(256) void k_gather_records(const char* __restrict__ src, long long ld_slot,
+                                                        long long ld_env, const long long* __restrict__ slot,
+                                                        const long long* __restrict__ env, int n_env_idx,
+                                                        unsigned total, unsigned q, float4* __restrict__ dst) {
+    const unsigned base = blockIdx.x * (256u * GU) + threadIdx.x;
+    float4 v[GU];
+#pragma unroll
+    for (int u = 0; u < GU; u++) {
+        const unsigned e = base + u * 256u;
+        if (e < total) {
+            const unsigned r = e / q, c = e - r * q;
+            const long long off = slot[r] * ld_slot + env[r % (unsigned)n_env_idx] * ld_env;
+            v[u] = *reinterpret_cast<const float4*>(src + off + 16ll * c);
+        }
+    }
+#pragma unroll
+    for (int u = 0; u < GU; u++) {
+        const unsigned e = base + u * 256u;
+        if (e < total) dst[e] = v[u];
+    }
+}
+
+extern "C" int gm_gather_records(const void* src, int64_t ld_slot, int64_t ld_env, const int64_t* slot,
+                                 const int64_t* env, int32_t n_env_idx, int64_t n, int64_t bytes, void* dst,
+                                 void* stream) {
+    if (!src || !slot || !env || !dst || n < 0 || n_env_idx <= 0 || bytes <= 0 || (bytes & 15) || (ld_slot & 15) ||
+        (ld_env & 15) || (reinterpret_cast<uintptr_t>(src) & 15) || (reinterpret_cast<uintptr_t>(dst) & 15))
+        return gm_fail(GM_ERR_INVALID_ARG, "gm_gather_records: bad arguments (16-byte records, strides, bases)");
+    const long long q = bytes / 16;
+    if (n == 0) return GM_OK;
+    if (n * q >= (1ll << 31) - 256ll * GU)
+        return gm_fail(GM_ERR_UNSUPPORTED, "gm_gather_records: more than 2^31 float4 per call");
+    const unsigned total = (unsigned)(n * q);
+    const unsigned blocks = (total + 256u * GU - 1) / (256u * GU);
+    hipLaunchKernelGGL(k_gather_records, dim3(blocks), dim3(256), 0, (hipStream_t)stream,
+                       static_cast<const char*>(src), (long long)ld_slot, (long long)ld_env,
+                       reinterpret_cast<const long long*>(slot), reinterpret_cast<const long long*>(env), n_env_idx,
+                       total, (unsigned)q, static_cast<float4*>(dst));
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return gm_fail(GM_ERR_HIP, std::string("gm_gather_records launch: ") + hipGetErrorString(e));
+    return GM_OK;
+}

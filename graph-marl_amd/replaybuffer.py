@@ -222,14 +222,32 @@ class ReplayBuffer:
 
         def next_fields(t, rows):
             s, e = (slots[t], env) if rows is None else (slots[t][rows], env[rows])
-            return (self.next_obs[s, e].to(fl), self.next_node_obs[s, e].to(fl),
+            return (self._records(self.next_obs, s, e), self._records(self.next_node_obs, s, e),
                     self.next_agent_node[s, e].int().contiguous())
 
-        return SeqBatch(self.obs[slots, envs].to(fl), od, self.action[slots, envs].long(),
+        return SeqBatch(self._records(self.obs, slots, env), od, self.action[slots, envs].long(),
                         self.reward[slots, envs].to(fl), self.done[slots, envs], self.episode_done[slots],
-                        self.node_obs[slots, envs].to(fl), self.nbr[slots, envs].int().contiguous(),
-                        self.agent_node[slots, envs].int().contiguous(), self.node_state[first, env].to(fl),
+                        self._records(self.node_obs, slots, env), self.nbr[slots, envs].int().contiguous(),
+                        self.agent_node[slots, envs].int().contiguous(), self._records(self.node_state, first, env),
                         next_fields, (slots, env))
+
+    @staticmethod
+    def _records(src, slots, env):
+        """src[slots, env] as float32 (slots [..., B'] int64 slot indices, env [B'] env indices): one
+        gm_gather_records launch for float32 ring fields with 16-byte records, torch indexing otherwise."""
+        rec = src.shape[2:]
+        nbytes = src[0, 0].numel() * src.element_size()
+        if not src.is_cuda or src.dtype != torch.float32 or nbytes % 16 or not src.is_contiguous():
+            return src[slots, env.expand_as(slots)].to(torch.float32)
+        sl = slots.contiguous()
+        ev = env.contiguous()
+        out = torch.empty(*sl.shape, *rec, dtype=torch.float32, device=src.device)
+        if out.numel() == 0:
+            return out
+        L.check(L.lib().gm_gather_records(src.data_ptr(), src.stride(0) * 4, src.stride(1) * 4, sl.data_ptr(),
+                                          ev.data_ptr(), ev.numel(), sl.numel(), nbytes, out.data_ptr(),
+                                          L.stream_ptr()))
+        return out
 
     def get_batch(self, batch_size, sequence_length=1, lazy_next=False):
         """Yields sequence_length TransitionBatches of batch_size transitions

@@ -475,6 +475,12 @@ int gm_pcg64_seed(uint64_t seed, gm_pcg64* out);
  * Lemire's bounded 32-bit draws with numpy's rejection rule) continuing the stream in `state`
  * (device memory, advanced in place, stream-ordered). 1 <= n <= 2^32 - 1. */
 int gm_pcg64_choice(gm_pcg64* state, int64_t n, int64_t count, int64_t* out, void* stream);
+/* Device: gather of sampled ring records (replaybuffer.get_sequences; the reference copies the sampled
+ * rows of its host arrays, src/replaybuffer.py:103-130): dst + i * bytes <- src + slot[i] * ld_slot +
+ * env[i % n_env_idx] * ld_env, `bytes` bytes, for i < n. Strides in bytes; records, strides and bases
+ * 16-byte aligned; n * bytes / 16 < 2^31. */
+int gm_gather_records(const void* src, int64_t ld_slot, int64_t ld_env, const int64_t* slot, const int64_t* env,
+                      int32_t n_env_idx, int64_t n, int64_t bytes, void* dst, void* stream);
 
 #ifdef __cplusplus
 }

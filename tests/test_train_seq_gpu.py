@@ -378,3 +378,20 @@ def test_operands_beyond_2gb():
     gw = M._wgrad(gy, x, k)
     refw = gy.double().t() @ x.double()
     assert _rel(gw, refw) < 1e-5
+
+
+@pytest.mark.parametrize("rec", [(20, 132), (20, 88), (20, 256), (4,)])
+def test_gather_records_matches_indexing(rec):
+    """gm_gather_records (replaybuffer.get_sequences' field gather) == torch advanced indexing
+    src[slots, env], bit for bit: [L, B] slots with per-column envs, a 1-D row subset, no rows."""
+    RB = importlib.import_module("graph-marl_amd.replaybuffer")
+    torch.manual_seed(len(rec))
+    S_, B_ = 37, 64
+    src = torch.randn(S_, B_, *rec, device="cuda")
+    slots = torch.randint(0, S_, (8, 300), device="cuda")
+    env = torch.randint(0, B_, (300,), device="cuda")
+    assert torch.equal(RB.ReplayBuffer._records(src, slots, env), src[slots, env.expand_as(slots)])
+    rows = torch.randint(0, 300, (77,), device="cuda")
+    assert torch.equal(RB.ReplayBuffer._records(src, slots[3][rows], env[rows]), src[slots[3][rows], env[rows]])
+    e = torch.empty(0, dtype=torch.long, device="cuda")
+    assert RB.ReplayBuffer._records(src, e, e).shape == (0, *rec)
