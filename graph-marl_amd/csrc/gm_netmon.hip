@@ -10,6 +10,8 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
+#include <cstring>
 #include <string>
 
 #include "../../include/graph_marl_amd.h"
@@ -821,6 +823,120 @@ __global__ __launch_bounds__(1024) void k_lstm_cell_bwd(gm_lstm_bwd_args a, unsi
     }
 }
 
+// k_lstm_cell_bwd with 4 consecutive units per thread (16-byte loads and stores; every ld and base
+// 16-byte aligned, H % 4 == 0): thread (rl, u4) of RL x H/4 threads; per element the same arithmetic
+// in the same order as k_lstm_cell_bwd. Bias partials: the RL row lanes combined in LDS in a fixed
+// order; max |dgates| per wave, then over the block's waves.
+__global__ __launch_bounds__(256) void k_lstm_cell_bwd4(gm_lstm_bwd_args a, unsigned* sc_slot, unsigned* max_slot) {
+    __shared__ float4 red[4][256];
+    __shared__ float wmx[4];
+    const int H = a.hidden, H4 = H >> 2, RL = blockDim.x / H4;
+    const int u = (threadIdx.x % H4) * 4, rl = threadIdx.x / H4;
+    const long long r0 = (long long)blockIdx.x * a.rows_per_block;
+    const long long r1 = min((long long)a.m, r0 + a.rows_per_block);
+    auto ld4 = [](const float* p) { return *reinterpret_cast<const float4*>(p); };
+    auto add4 = [](float4& x, float4 y) {
+        x.x += y.x;
+        x.y += y.y;
+        x.z += y.z;
+        x.w += y.w;
+    };
+    float4 p[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) p[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+    float mx = 0.f;
+    for (long long r = r0 + rl; r < r1; r += RL) {
+        const float* ar = a.act + r * a.ld_act + u;
+        const float4 gi4 = ld4(ar), gf4 = ld4(ar + H), gg4 = ld4(ar + 2 * H), go4 = ld4(ar + 3 * H);
+        const float4 c4 = ld4(a.c_in + r * a.ld_cin + u), co4 = ld4(a.c_out + r * a.ld_cout + u);
+        float4 dh4 = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (a.dh0) add4(dh4, ld4(a.dh0 + r * a.ld_dh0 + u));
+        if (a.dh1) add4(dh4, ld4(a.dh1 + r * a.ld_dh1 + u));
+        if (a.dm) {
+            const int N = a.n_nodes;
+            const long long g = r / N;
+            const int n = (int)(r - g * N);
+            int mem[MAXDEG + 1];
+            const int cnt = members(a.nbr + r * a.deg, a.deg, n, mem);
+            for (int q = 0; q < cnt; q++) {
+                float4 v = ld4(a.dm + (g * N + mem[q]) * a.ld_dm + u);
+                if (a.mean) {
+                    const int32_t* nbm = a.nbr + (g * N + mem[q]) * a.deg;
+                    int cm = 1;
+                    for (int k = 0; k < a.deg; k++) cm += nbm[k] >= 0;
+                    const float f = 1.0f / (float)cm;
+                    v = make_float4(v.x * f, v.y * f, v.z * f, v.w * f);
+                }
+                add4(dh4, v);
+            }
+        }
+        float4 dc4 = a.dc ? ld4(a.dc + r * a.ld_dc + u) : make_float4(0.f, 0.f, 0.f, 0.f);
+        const bool ext = !a.ext_mask || !a.ext_mask[r / a.rows_per_sample];
+        if (ext) {
+            if (a.dh_ext) add4(dh4, ld4(a.dh_ext + r * a.ld_ext + u));
+            if (a.dc_ext) add4(dc4, ld4(a.dc_ext + r * a.ld_dcext + u));
+        }
+        const float* gi = &gi4.x;
+        const float* gf = &gf4.x;
+        const float* gg = &gg4.x;
+        const float* go = &go4.x;
+        const float* c = &c4.x;
+        const float* co = &co4.x;
+        const float* dh = &dh4.x;
+        const float* dcn = &dc4.x;
+        float4 o0, o1, o2, o3, oc;
+        float* d0 = &o0.x;
+        float* d1 = &o1.x;
+        float* d2 = &o2.x;
+        float* d3 = &o3.x;
+        float* dco = &oc.x;
+#pragma unroll
+        for (int e = 0; e < 4; e++) {
+            const float tc = tanhf(co[e]);
+            const float dct = dcn[e] + dh[e] * go[e] * (1.f - tc * tc);
+            d0[e] = dct * gg[e] * gi[e] * (1.f - gi[e]);
+            d1[e] = dct * c[e] * gf[e] * (1.f - gf[e]);
+            d2[e] = dct * gi[e] * (1.f - gg[e] * gg[e]);
+            d3[e] = dh[e] * tc * go[e] * (1.f - go[e]);
+            dco[e] = dct * gf[e];
+            mx = fmaxf(mx, fmaxf(fmaxf(fabsf(d0[e]), fabsf(d1[e])), fmaxf(fabsf(d2[e]), fabsf(d3[e]))));
+        }
+        float* dg = a.dgates + r * a.ld_dg + u;
+        *reinterpret_cast<float4*>(dg) = o0;
+        *reinterpret_cast<float4*>(dg + H) = o1;
+        *reinterpret_cast<float4*>(dg + 2 * H) = o2;
+        *reinterpret_cast<float4*>(dg + 3 * H) = o3;
+        if (a.dc_out) *reinterpret_cast<float4*>(a.dc_out + r * a.ld_dco + u) = oc;
+        add4(p[0], o0);
+        add4(p[1], o1);
+        add4(p[2], o2);
+        add4(p[3], o3);
+    }
+    if (a.bias_part) {
+#pragma unroll
+        for (int k = 0; k < 4; k++) red[k][threadIdx.x] = p[k];
+        __syncthreads();
+        if (rl == 0) {
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                float4 s = red[k][threadIdx.x];
+                for (int l = 1; l < RL; l++) add4(s, red[k][l * H4 + threadIdx.x]);
+                *reinterpret_cast<float4*>(a.bias_part + (long long)blockIdx.x * 4 * H + k * H + u) = s;
+            }
+        }
+    }
+    if (sc_slot || max_slot) {
+        mx = gm_wave_max(mx);
+        if ((threadIdx.x & 63) == 0) wmx[threadIdx.x >> 6] = mx;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            for (int w = 1; w < (int)(blockDim.x >> 6); w++) mx = fmaxf(mx, wmx[w]);
+            if (sc_slot) gm_amax_publish(sc_slot, mx);
+            if (max_slot) gm_amax_publish(max_slot, mx);
+        }
+    }
+}
+
 // Q head + leaky hidden layer backward (gm_qhead_bwd): thread c owns column c of the block's rows
 __global__ __launch_bounds__(1024) void k_qhead_bwd(const float* __restrict__ dq, long long ldq, int nq,
                                                    const float* __restrict__ wq, long long ldwq,
@@ -875,6 +991,12 @@ __global__ __launch_bounds__(1024) void k_qhead_bwd(const float* __restrict__ dq
 
 }  // namespace
 
+// GM_LSTM_BWD=scalar selects the one-unit-per-thread kernel (A-B timing)
+const bool g_lstm_bwd_vec = [] {
+    const char* e = getenv("GM_LSTM_BWD");
+    return !(e && strcmp(e, "scalar") == 0);
+}();
+
 extern "C" int gm_lstm_cell_bwd(const gm_lstm_bwd_args* a, void* stream) {
     if (!a || !a->act || !a->c_in || !a->c_out || !a->dgates || a->m <= 0 || a->hidden <= 0 || a->hidden > 1024 ||
         (a->hidden > 256 && a->hidden % 64) || (a->dm && (!a->nbr || a->n_nodes <= 0 || a->deg < 0 || a->deg > MAXDEG)) ||
@@ -889,8 +1011,20 @@ extern "C" int gm_lstm_cell_bwd(const gm_lstm_bwd_args* a, void* stream) {
     if (b.dg_scale && hipMemsetAsync(b.dg_scale, 0, sizeof(float), st) != hipSuccess)
         return gm_fail(GM_ERR_HIP, "gm_lstm_cell_bwd: memset");
     const long long nb = (b.m + b.rows_per_block - 1) / b.rows_per_block;
-    hipLaunchKernelGGL(k_lstm_cell_bwd, dim3((unsigned)nb), dim3(threads), 0, st, b,
-                       reinterpret_cast<unsigned*>(b.dg_scale), reinterpret_cast<unsigned*>(b.dg_max));
+    auto a16 = [](const void* p, long long ld) { return !p || ((reinterpret_cast<uintptr_t>(p) & 15) == 0 && ld % 4 == 0); };
+    const bool vec = g_lstm_bwd_vec && H % 4 == 0 && H / 4 <= 256 && ((256 / (H / 4)) * (H / 4)) % 64 == 0 &&
+                     a16(b.act, b.ld_act) && a16(b.c_in, b.ld_cin) && a16(b.c_out, b.ld_cout) &&
+                     a16(b.dh0, b.ld_dh0) && a16(b.dh1, b.ld_dh1) && a16(b.dm, b.ld_dm) && a16(b.dh_ext, b.ld_ext) &&
+                     a16(b.dc_ext, b.ld_dcext) && a16(b.dc, b.ld_dc) && a16(b.dgates, b.ld_dg) &&
+                     a16(b.dc_out, b.ld_dco) && a16(b.bias_part, 4);
+    if (vec) {
+        const int rl4 = 256 / (H / 4);
+        hipLaunchKernelGGL(k_lstm_cell_bwd4, dim3((unsigned)nb), dim3(rl4 * (H / 4)), 0, st, b,
+                           reinterpret_cast<unsigned*>(b.dg_scale), reinterpret_cast<unsigned*>(b.dg_max));
+    } else {
+        hipLaunchKernelGGL(k_lstm_cell_bwd, dim3((unsigned)nb), dim3(threads), 0, st, b,
+                           reinterpret_cast<unsigned*>(b.dg_scale), reinterpret_cast<unsigned*>(b.dg_max));
+    }
     int rc = launched();
     if (rc == GM_OK && b.dg_scale) rc = gm_absmax_finish(b.dg_scale, stream);
     return rc;

@@ -144,7 +144,7 @@ def test_qhead_bwd_vs_torch(rows, cols, nq):
 
 
 @pytest.mark.parametrize("mean", [0, 1])
-@pytest.mark.parametrize("H", [128, 32])
+@pytest.mark.parametrize("H", [128, 32, 30])
 def test_lstm_cell_bwd_vs_autograd(mean, H):
     """gm_lstm_cell_bwd with every gradient source (two plain dh, the transposed aggregate of dm,
     masked external dh / dc, plain dc) against torch autograd of nn.LSTMCell gate math."""
