@@ -587,6 +587,51 @@ __global__ __launch_bounds__(1024) void k_readout_bwd_lds(const float* __restric
     }
 }
 
+// k_readout_bwd_lds over S column chunks per graph (block = (graph, chunk)): a quarter of the LDS per
+// block, so 4x as many blocks stay resident. The (row, segment) -> node map is inverted once per block
+// into per-node row bitmasks (LDS atomic OR: order-free), so a (node, column) thread visits only the
+// rows that read its node, in ascending (row, segment) order: the same summation order as
+// k_readout_bwd (identical results).
+__global__ __launch_bounds__(256) void k_readout_bwd_cs(const float* __restrict__ dout, long long stride,
+                                                        const int32_t* __restrict__ nbr,
+                                                        const int32_t* __restrict__ agent_node, int N, int R, int deg,
+                                                        int H, int S, float* __restrict__ dhf, float* __restrict__ dhp) {
+    extern __shared__ float4 sq[];  // [R][deg + 1][C4]
+    __shared__ int su[64];
+    __shared__ unsigned long long smask[128][4];  // node -> rows reading it, per segment (deg <= 3)
+    const long long g = blockIdx.x / S;
+    const int cs = blockIdx.x - (int)(g * S);
+    const int C4 = (H >> 2) / S, SEG = deg + 1;
+    for (int i = threadIdx.x; i < R; i += blockDim.x) su[i] = agent_node ? agent_node[g * R + i] : i;
+    for (int i = threadIdx.x; i < N * SEG; i += blockDim.x) smask[i / SEG][i % SEG] = 0ull;
+    for (int i = threadIdx.x; i < R * SEG * C4; i += blockDim.x) {
+        const int r = i / (SEG * C4), rem = i - r * SEG * C4, sg = rem / C4, c = rem - sg * C4;
+        sq[i] = *reinterpret_cast<const float4*>(dout + (g * R + r) * stride + sg * H + (cs * C4 + c) * 4);
+    }
+    __syncthreads();
+    for (int e = threadIdx.x; e < R * SEG; e += blockDim.x) {
+        const int r = e / SEG, sg = e - r * SEG;
+        const int v = sg == 0 ? su[r] : nbr[(g * N + su[r]) * deg + sg - 1];
+        if (v >= 0 && v < N) atomicOr(&smask[v][sg], 1ull << r);
+    }
+    __syncthreads();
+    for (int t = threadIdx.x; t < N * C4; t += blockDim.x) {
+        const int v = t / C4, c = t - v * C4;
+        float4 af = make_float4(0.f, 0.f, 0.f, 0.f), ap = af;
+        for (unsigned long long m = smask[v][0]; m; m &= m - 1) af = f4add(af, sq[(__ffsll(m) - 1) * SEG * C4 + c]);
+        unsigned long long mk[3], any = 0ull;
+        for (int k = 0; k < deg; k++) any |= (mk[k] = smask[v][k + 1]);
+        for (; any; any &= any - 1) {
+            const int r = __ffsll(any) - 1;
+            for (int k = 0; k < deg; k++)
+                if ((mk[k] >> r) & 1ull) ap = f4add(ap, sq[(r * SEG + k + 1) * C4 + c]);
+        }
+        const long long o = (g * N + v) * H + (cs * C4 + c) * 4;
+        if (dhf) *reinterpret_cast<float4*>(dhf + o) = af;
+        if (dhp) *reinterpret_cast<float4*>(dhp + o) = ap;
+    }
+}
+
 extern "C" int gm_netmon_readout_ld(const float* hf, int64_t ldf, const float* hp, int64_t ldp, const int32_t* nbr,
                                     const int32_t* agent_node, int32_t G, int32_t N, int32_t R, int32_t deg, int32_t H,
                                     float* out, int64_t stride, void* stream) {
@@ -660,6 +705,12 @@ __global__ __launch_bounds__(1024) void k_readout_bwd_g(const float* __restrict_
     if (dhp) stv<V>(dhp + node * H + off, ap);
 }
 
+// GM_READOUT_BWD=graph keeps one block per graph (A-B timing)
+const bool g_readout_bwd_cs = [] {
+    const char* e = getenv("GM_READOUT_BWD");
+    return !(e && strcmp(e, "graph") == 0);
+}();
+
 extern "C" int gm_netmon_readout_bwd(const float* dout, int64_t stride, const int32_t* nbr, const int32_t* agent_node,
                                      int32_t G, int32_t N, int32_t R, int32_t deg, int32_t H, float* dhf, float* dhp,
                                      void* stream) {
@@ -669,6 +720,13 @@ extern "C" int gm_netmon_readout_bwd(const float* dout, int64_t stride, const in
     if (dhf) { int v = vec_width(H, H, dhf); V = V < v ? V : v; }
     if (dhp) { int v = vec_width(H, H, dhp); V = V < v ? V : v; }
     const size_t lds = (size_t)R * (deg + 1) * H * 4;
+    if (V == 4 && R <= 64 && N <= 128 && deg <= 3 && (H / 4) % 4 == 0 && lds / 4 <= 48 * 1024 &&
+        g_readout_bwd_cs) {
+        const int S = 4, threads = std::min(256, (N * (H / 16) + 63) / 64 * 64);
+        hipLaunchKernelGGL(k_readout_bwd_cs, dim3((unsigned)((long long)G * S)), dim3(threads), lds / S,
+                           (hipStream_t)stream, dout, (long long)stride, nbr, agent_node, N, R, deg, H, S, dhf, dhp);
+        return launched();
+    }
     if (V == 4 && R <= 64 && deg <= MAXDEG && lds <= 48 * 1024) {
         const int threads = std::min(1024, (N * (H / 4) + 63) / 64 * 64);
         hipLaunchKernelGGL(k_readout_bwd_lds, dim3(G), dim3(threads), lds, (hipStream_t)stream, dout, (long long)stride,
