@@ -2251,7 +2251,10 @@ __global__ __launch_bounds__(256, 2) void k_gemm3_kmajor(const float* __restrict
 // columns per 16-lane group. No register transpose, 4x fewer global load instructions than the
 // dword form, and a 64 x (BN/2) wave tile. Row stride of an image = columns * 2 + 64 B: the four
 // k rows of a 32-lane half then start 16 banks apart (conflict-free transposed reads).
-template <int BN>
+// MF = 1: v_mfma_f32_16x16x32_f16 (16-lane group g reads k rows 8 g .. 8 g + 7 of its 16 columns; the
+// images' 32-byte column segments are XOR-swizzled by bit 3 of the k row so that the two groups of a
+// 32-lane half (rows 8 g + q, 8 (g + 1) + q) hit disjoint banks)
+template <int BN, int MF = 0>
 __global__ __launch_bounds__(256, BN == 128 ? 2 : 1) void k_wgrad_tr(const float* __restrict__ A, long long lda,
                                                                    unsigned abytes, const float* __restrict__ B,
                                                                    long long ldb, unsigned bbytes, int M, int N, int K,
@@ -2301,7 +2304,7 @@ __global__ __launch_bounds__(256, BN == 128 ? 2 : 1) void k_wgrad_tr(const float
         for (int j = 0; j < LA; j++) {
             half4 hi, lo;
             split4(make_float4(va[j].x * s_a, va[j].y * s_a, va[j].z * s_a, va[j].w * s_a), hi, lo);
-            const int o = (ka0 + 8 * j) * RA + 8 * qa;
+            const int o = (ka0 + 8 * j) * RA + ((8 * qa) ^ (MF ? (((ka0 + 8 * j) >> 3) & 1) << 5 : 0));
             *reinterpret_cast<half4*>(ah + o) = hi;
             *reinterpret_cast<half4*>(al + o) = lo;
         }
@@ -2309,11 +2312,18 @@ __global__ __launch_bounds__(256, BN == 128 ? 2 : 1) void k_wgrad_tr(const float
         for (int j = 0; j < LB; j++) {
             half4 hi, lo;
             split4(make_float4(vb[j].x * s_b, vb[j].y * s_b, vb[j].z * s_b, vb[j].w * s_b), hi, lo);
-            const int o = (kb0 + RB_STEP * j) * RB + 8 * qb;
+            const int o = (kb0 + RB_STEP * j) * RB + ((8 * qb) ^ (MF ? (((kb0 + RB_STEP * j) >> 3) & 1) << 5 : 0));
             *reinterpret_cast<half4*>(bh + o) = hi;
             *reinterpret_cast<half4*>(bl + o) = lo;
         }
     };
+    floatx4 c4[2 * TM][2 * TN], c4b[2 * TM][2 * TN];  // MF = 1: 16 x 16 blocks (hi*hi, cross terms)
+#pragma unroll
+    for (int i = 0; i < 2 * TM; i++)
+#pragma unroll
+        for (int j = 0; j < 2 * TN; j++)
+#pragma unroll
+            for (int r = 0; r < 4; r++) c4[i][j][r] = c4b[i][j][r] = 0.f;
     floatx16 acc[TM][TN], acc2[TM][TN];
 #pragma unroll
     for (int i = 0; i < TM; i++)
@@ -2334,7 +2344,47 @@ __global__ __launch_bounds__(256, BN == 128 ? 2 : 1) void k_wgrad_tr(const float
             half4, __builtin_amdgcn_ds_read_tr16_b64_v4f16((__attribute__((address_space(3))) v4fp16*)(a0 + 4 * rs)));
         return half8{x0[0], x0[1], x0[2], x0[3], x1[0], x1[1], x1[2], x1[3]};
     };
+    // 16x16x32 form: group g = lane >> 4 reads rows 8 g + q (+ 4), columns 4 p of its 16-column block,
+    // segment swizzle g & 1 (bit 3 of the row)
+    const int swz16 = ((lane >> 4) & 1) << 5;
+    auto frag16 = [&](const char* img, int rs, int col0) {
+        const char* a0 = img + (8 * g + q) * rs + ((2 * col0 + 8 * p) ^ swz16);
+        const half4 x0 = __builtin_bit_cast(
+            half4, __builtin_amdgcn_ds_read_tr16_b64_v4f16((__attribute__((address_space(3))) v4fp16*)(a0)));
+        const half4 x1 = __builtin_bit_cast(
+            half4, __builtin_amdgcn_ds_read_tr16_b64_v4f16((__attribute__((address_space(3))) v4fp16*)(a0 + 4 * rs)));
+        return half8{x0[0], x0[1], x0[2], x0[3], x1[0], x1[1], x1[2], x1[3]};
+    };
+    auto compute16 = [&](int buf) {
+        const char* ah = smem[buf];
+        const char* al = ah + BK * RA;
+        const char* bh = al + BK * RA;
+        const char* bl = bh + BK * RB;
+        half8 fah[2 * TM], fal[2 * TM], fbh[2 * TN], fbl[2 * TN];
+#pragma unroll
+        for (int i = 0; i < 2 * TM; i++) {
+            fah[i] = frag16(ah, RA, wr * TM * 32 + 16 * i);
+            fal[i] = frag16(al, RA, wr * TM * 32 + 16 * i);
+        }
+#pragma unroll
+        for (int j = 0; j < 2 * TN; j++) {
+            fbh[j] = frag16(bh, RB, wc * TN * 32 + 16 * j);
+            fbl[j] = frag16(bl, RB, wc * TN * 32 + 16 * j);
+        }
+#pragma unroll
+        for (int i = 0; i < 2 * TM; i++)
+#pragma unroll
+            for (int j = 0; j < 2 * TN; j++) {
+                c4[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fah[i], fbh[j], c4[i][j], 0, 0, 0);
+                c4b[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fal[i], fbh[j], c4b[i][j], 0, 0, 0);
+                c4b[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fah[i], fbl[j], c4b[i][j], 0, 0, 0);
+            }
+    };
     auto compute = [&](int buf) {
+        if constexpr (MF == 1) {
+            compute16(buf);
+            return;
+        }
         const char* ah = smem[buf];
         const char* al = ah + BK * RA;
         const char* bh = al + BK * RA;
@@ -2375,6 +2425,20 @@ __global__ __launch_bounds__(256, BN == 128 ? 2 : 1) void k_wgrad_tr(const float
     }
     const float inv = 1.0f / (s_a * s_b);  // powers of two: exact
     float* Cz = C + (size_t)blockIdx.y * cz;
+    if constexpr (MF == 1) {
+#pragma unroll
+        for (int i = 0; i < 2 * TM; i++)
+#pragma unroll
+            for (int j = 0; j < 2 * TN; j++) {
+                const int n = n0 + wc * TN * 32 + j * 16 + (lane & 15);
+#pragma unroll
+                for (int r = 0; r < 4; r++) {
+                    const int m = m0 + wr * TM * 32 + i * 16 + 4 * (lane >> 4) + r;
+                    if (m < M && n < N) Cz[(long long)m * ldc + n] = (c4[i][j][r] + c4b[i][j][r] * (1.0f / 4096.0f)) * inv;
+                }
+            }
+        return;
+    }
     const int hh = lane >> 5, l32 = lane & 31;
 #pragma unroll
     for (int i = 0; i < TM; i++)
@@ -2409,7 +2473,12 @@ extern "C" int gm_gemm_x3_wgrad(const float* a, int64_t lda, const float* b, int
         const long long ab = kc * lda * 4, bb = kc * ldb * 4;
         if (ab >= 0x7ff00000LL || bb >= 0x7ff00000LL)
             return gm_fail(GM_ERR_UNSUPPORTED, "gm_gemm_x3_wgrad: one k chunk of an operand larger than 2 GB");
-        if (g_wgrad != 2) {  // 128 x 128 tiles at 2 blocks/CU: 8-24 % faster than 128 x 256 at 1 block/CU
+        if (g_wgrad == 3) {  // 16x16x32 MFMA
+            const int T = ((m + 127) / 128) * ((n + 127) / 128);
+            hipLaunchKernelGGL((k_wgrad_tr<128, 1>), dim3(T, S), dim3(256), 0, (hipStream_t)stream, a, (long long)lda,
+                               (unsigned)ab, b, (long long)ldb, (unsigned)bb, m, n, k, kchunk, sa, sb, c, (long long)ldc,
+                               (long long)m * ldc);
+        } else if (g_wgrad != 2) {  // 128 x 128 tiles at 2 blocks/CU: 8-24 % faster than 128 x 256 at 1 block/CU
             const int T = ((m + 127) / 128) * ((n + 127) / 128);
             hipLaunchKernelGGL(k_wgrad_tr<128>, dim3(T, S), dim3(256), 0, (hipStream_t)stream, a, (long long)lda,
                                (unsigned)ab, b, (long long)ldb, (unsigned)bb, m, n, k, kchunk, sa, sb, c, (long long)ldc,
@@ -2451,7 +2520,7 @@ extern "C" int gm_gemm_pack_x3(const float* w, int64_t ldw, int32_t n, int32_t k
 }
 
 extern "C" int gm_gemm_set_wgrad(int32_t form) {
-    if (form < -1 || form > 2) return gm_fail(GM_ERR_INVALID_ARG, "gm_gemm_set_wgrad: form in [-1, 2]");
+    if (form < -1 || form > 3) return gm_fail(GM_ERR_INVALID_ARG, "gm_gemm_set_wgrad: form in [-1, 3]");
     g_wgrad = form;
     return GM_OK;
 }

@@ -410,7 +410,8 @@ int gm_agent_comm(const float* h, int64_t ldh, const int8_t* adj, int32_t B, int
  * 2 = 128x128x32 (LSTM: 256x128x16)). Process-wide. */
 /* Weight-gradient kernel of gm_gemm_x3_wgrad (same arithmetic, diagnostics / A-B timing):
  * -1 (default) or 1 = transposed LDS reads (ds_read_b64_tr_b16) with 128 x 128 tiles, 2 = the same
- * with 128 x 256 tiles, 0 = the dword-load register-transpose form (tools/wgrad_bench.py). */
+ * with 128 x 256 tiles, 3 = 128 x 128 tiles on v_mfma_f32_16x16x32_f16, 0 = the dword-load
+ * register-transpose form (tools/wgrad_bench.py). */
 int gm_gemm_set_wgrad(int32_t form);
 int gm_gemm_set_tile(int32_t tile);
 /* MFMA shape of the LDS-DMA split-f16 kernel (gm_gemm_x3's dense / readout tiles, gm_gemm_x3_head):

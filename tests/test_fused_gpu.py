@@ -290,7 +290,7 @@ def test_weight_gradient_kmajor(Mb, o, k, ldx, mag):
     mag_ref = gy.abs().double().t() @ x.abs().double()
     lib = FU._setup()
     try:
-        for form in (-1, 2, 0):  # transposed reads 128x128 (default), 128x256, dword form
+        for form in (-1, 3, 2, 0):  # transposed reads 128x128 (default), 16x16x32 MFMA, 128x256, dword form
             lib.gm_gemm_set_wgrad(form)
             gw = M_._wgrad(gy, x, k)
             assert gw.shape == (o, k)

@@ -30,15 +30,21 @@ def main():
     lib = M.L.lib()
     out = {}
     for o, k, ldx in ((512, 642, 644), (512, 512, 512), (256, 512, 512), (512, 256, 256), (128, 256, 256),
-                      (512, 130, 132)):
+                      (512, 128, 128), (512, 88, 88)):
         gy = torch.randn(Mb, o, device="cuda") * 1e-6
         x = torch.randn(Mb, ldx, device="cuda")[:, :k]
         r = {}
-        for form, name in ((2, "tr256"), (1, "tr128"), (0, "dword")):
+        for form, name in ((1, "tr128"), (3, "tr128_mfma16"), (2, "tr256")):
             lib.gm_gemm_set_wgrad(form)
             r[name + "_us"] = round(timeit(lambda: M._wgrad(gy, x, k)), 1)
         lib.gm_gemm_set_wgrad(-1)
-        r["fp32_lib_us"] = round(timeit(lambda: gy.t() @ x), 1)
+        lib.gm_gemm_set_wgrad(1)
+        g1 = M._wgrad(gy, x, k)
+        lib.gm_gemm_set_wgrad(3)
+        g3 = M._wgrad(gy, x, k)
+        lib.gm_gemm_set_wgrad(-1)
+        r["rel_16_vs_32"] = float((g3 - g1).abs().max() / g1.abs().max())
+        print(o, k, r, flush=True)
         out[f"{o}x{k}"] = r
     print(json.dumps(out))
 
