@@ -22,7 +22,9 @@ if os.environ.get("SHAPES") == "train":  # the update's dense layers at 131072 r
     SHAPES = [("dqn.l1", 131072, 512, 642), ("dqn.l2", 131072, 256, 512), ("enc.l1", 131072, 256, 512),
               ("enc.l2", 131072, 128, 256), ("lstm", 131072, 512, 256)]
 
-TILES = [int(t) for t in os.environ.get("TILES", "-1").split(",")]
+if os.environ.get("ROWS"):  # e.g. one stream group of the rollout (40960 rows)
+    SHAPES = [(nm, int(os.environ["ROWS"]), n, k) for nm, _, n, k in SHAPES]
+TILES = [int(t) for t in os.environ.get("TILES", "-1").split(",") if t]
 X3_TILES = [int(t) for t in os.environ.get("X3_TILES", "-1,1,2").split(",")]
 
 
