@@ -12,4 +12,4 @@ for f in sys.argv[1:]:
     ks = d.get("kernels", {})
     sel = {k.split(":")[0] + ":" + k.split(":")[-1]: round(v["avg_us"], 1) for k, v in ks.items() if "avg_us" in v}
     rt = (d.get("rollout_train") or {}).get("value")
-    print(f, d["value"], d.get("roofline", {}).get("frac"), rt, sel)
+    print(f, d["value"], (d.get("roofline") or {}).get("frac"), rt, sel)
