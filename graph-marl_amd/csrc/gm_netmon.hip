@@ -1047,6 +1047,111 @@ __global__ __launch_bounds__(1024) void k_qhead_bwd(const float* __restrict__ dq
     if (amax) block_max_publish(mx, amax);
 }
 
+// k_qhead_bwd with 4 columns per thread (16-byte loads / stores; cols % 4 == 0, 16-byte bases and
+// strides): RL row lanes x cols/4 threads, U rows per lane in flight; per element the arithmetic of
+// k_qhead_bwd; the row lanes' partial sums combined in LDS in a fixed order.
+__global__ __launch_bounds__(256) void k_qhead_bwd4(const float* __restrict__ dq, long long ldq, int nq,
+                                                   const float* __restrict__ wq, long long ldwq,
+                                                   const float* __restrict__ y, long long ldy, long long rows, int cols,
+                                                   int act, float* __restrict__ g, long long ldg,
+                                                   float* __restrict__ part_b, float* __restrict__ part_wq,
+                                                   float* __restrict__ part_bq, int rpb, unsigned* __restrict__ amax) {
+    __shared__ float4 red[5][256];
+    __shared__ float rq[4][256];
+    __shared__ float wmx[4];
+    const int C4 = cols >> 2, RL = blockDim.x / C4;
+    const int c4 = threadIdx.x % C4, rl = threadIdx.x / C4, c = 4 * c4;
+    float4 w[4];
+#pragma unroll
+    for (int q = 0; q < 4; q++)
+        w[q] = q < nq ? *reinterpret_cast<const float4*>(wq + q * ldwq + c) : make_float4(0.f, 0.f, 0.f, 0.f);
+    const long long r0 = (long long)blockIdx.x * rpb, r1 = min(rows, r0 + rpb);
+    float4 pb = make_float4(0.f, 0.f, 0.f, 0.f), pw[4];
+    float pq[4] = {0.f, 0.f, 0.f, 0.f}, mx = 0.f;
+#pragma unroll
+    for (int q = 0; q < 4; q++) pw[q] = pb;
+    constexpr int U = 4;
+    for (long long rb = r0 + rl; rb < r1; rb += (long long)U * RL) {
+        float d[U][4];
+        float4 yv[U];
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            const long long r = min(rb + (long long)u * RL, r1 - 1);
+#pragma unroll
+            for (int q = 0; q < 4; q++) d[u][q] = q < nq ? dq[r * ldq + q] : 0.f;
+            yv[u] = *reinterpret_cast<const float4*>(y + r * ldy + c);
+        }
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            const long long r = rb + (long long)u * RL;
+            if (r >= r1) break;
+            if (c4 == 0)
+#pragma unroll
+                for (int q = 0; q < 4; q++) pq[q] += d[u][q];
+            const float* ye = &yv[u].x;
+            float4 gv4;
+            float* gv = &gv4.x;
+#pragma unroll
+            for (int e = 0; e < 4; e++) {
+                float v = 0.f;
+#pragma unroll
+                for (int q = 0; q < 4; q++) v = fmaf(d[u][q], (&w[q].x)[e], v);
+                if (act && !(ye[e] > 0.f)) v *= 0.01f;
+                gv[e] = v;
+                mx = fmaxf(mx, fabsf(v));
+            }
+            *reinterpret_cast<float4*>(g + r * ldg + c) = gv4;
+            pb.x += gv4.x;
+            pb.y += gv4.y;
+            pb.z += gv4.z;
+            pb.w += gv4.w;
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                pw[q].x = fmaf(d[u][q], ye[0], pw[q].x);
+                pw[q].y = fmaf(d[u][q], ye[1], pw[q].y);
+                pw[q].z = fmaf(d[u][q], ye[2], pw[q].z);
+                pw[q].w = fmaf(d[u][q], ye[3], pw[q].w);
+            }
+        }
+    }
+    red[0][threadIdx.x] = pb;
+#pragma unroll
+    for (int q = 0; q < 4; q++) red[1 + q][threadIdx.x] = pw[q];
+    if (c4 == 0)
+#pragma unroll
+        for (int q = 0; q < 4; q++) rq[q][rl] = pq[q];
+    __syncthreads();
+    if (rl == 0) {
+        for (int k = 0; k <= nq; k++) {
+            float4 sm = red[k][c4];
+            for (int l = 1; l < RL; l++) {
+                const float4 o = red[k][l * C4 + c4];
+                sm.x += o.x;
+                sm.y += o.y;
+                sm.z += o.z;
+                sm.w += o.w;
+            }
+            float* dst = k == 0 ? part_b + (long long)blockIdx.x * cols : part_wq + ((long long)blockIdx.x * nq + k - 1) * cols;
+            *reinterpret_cast<float4*>(dst + c) = sm;
+        }
+        if (c4 == 0)
+            for (int q = 0; q < nq; q++) {
+                float sm = rq[q][0];
+                for (int l = 1; l < RL; l++) sm += rq[q][l];
+                part_bq[(long long)blockIdx.x * nq + q] = sm;
+            }
+    }
+    if (amax) {
+        mx = gm_wave_max(mx);
+        if ((threadIdx.x & 63) == 0) wmx[threadIdx.x >> 6] = mx;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            for (int k = 1; k < (int)(blockDim.x >> 6); k++) mx = fmaxf(mx, wmx[k]);
+            gm_amax_publish(amax, mx);
+        }
+    }
+}
+
 }  // namespace
 
 // GM_LSTM_BWD=scalar selects the one-unit-per-thread kernel (A-B timing)
@@ -1088,6 +1193,12 @@ extern "C" int gm_lstm_cell_bwd(const gm_lstm_bwd_args* a, void* stream) {
     return rc;
 }
 
+// GM_QHEAD_BWD=scalar selects the one-column-per-thread kernel (A-B timing)
+const bool g_qhead_vec = [] {
+    const char* e = getenv("GM_QHEAD_BWD");
+    return !(e && strcmp(e, "scalar") == 0);
+}();
+
 extern "C" int gm_qhead_bwd(const float* dq, int64_t ldq, int32_t nq, const float* wq, int64_t ldwq, const float* y,
                             int64_t ldy, int64_t rows, int32_t cols, int32_t act, float* g, int64_t ldg, float* part_b,
                             float* part_wq, float* part_bq, int32_t rows_per_block, float* g_scale, void* stream) {
@@ -1098,6 +1209,17 @@ extern "C" int gm_qhead_bwd(const float* dq, int64_t ldq, int32_t nq, const floa
     if (g_scale && hipMemsetAsync(g_scale, 0, sizeof(float), st) != hipSuccess)
         return gm_fail(GM_ERR_HIP, "gm_qhead_bwd: memset");
     const long long nb = (rows + rows_per_block - 1) / rows_per_block;
+    auto a16 = [](const void* p, long long ld) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0 && ld % 4 == 0; };
+    if (g_qhead_vec && cols % 4 == 0 && cols <= 1024 && ((256 / (cols / 4)) * (cols / 4)) % 64 == 0 && a16(wq, ldwq) &&
+        a16(y, ldy) && a16(g, ldg) && a16(part_b, cols) && a16(part_wq, cols)) {
+        const int rl = 256 / (cols / 4);
+        hipLaunchKernelGGL(k_qhead_bwd4, dim3((unsigned)nb), dim3(rl * (cols / 4)), 0, st, dq, (long long)ldq, nq, wq,
+                           (long long)ldwq, y, (long long)ldy, (long long)rows, cols, act, g, (long long)ldg, part_b,
+                           part_wq, part_bq, rows_per_block, reinterpret_cast<unsigned*>(g_scale));
+        int rc = launched();
+        if (rc == GM_OK && g_scale) rc = gm_absmax_finish(g_scale, stream);
+        return rc;
+    }
     const int threads = (cols + 63) / 64 * 64;
     hipLaunchKernelGGL(k_qhead_bwd, dim3((unsigned)nb), dim3(threads), 0, st, dq, (long long)ldq, nq, wq,
                        (long long)ldwq, y, (long long)ldy, (long long)rows, cols, act, g, (long long)ldg, part_b,

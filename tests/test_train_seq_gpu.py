@@ -115,7 +115,7 @@ def _dgrad_case(M, T, S, FU, L, m, n, k, split):
     assert gmax.item() == y.abs().max().item()  # the slot holds the max's float bits
 
 
-@pytest.mark.parametrize("rows,cols,nq", [(100000, 256, 4), (777, 32, 3), (5, 64, 1)])
+@pytest.mark.parametrize("rows,cols,nq", [(100000, 256, 4), (777, 32, 3), (5, 64, 1), (300, 100, 2)])
 def test_qhead_bwd_vs_torch(rows, cols, nq):
     M, T, S, FU, L = mods()
     torch.manual_seed(rows)
