@@ -1145,6 +1145,16 @@ __device__ __forceinline__ void head_epilogue16(floatx4 (&acc)[T2][N2], const Ep
 // MF: 0 v_mfma_f32_32x32x16_f16 fragments, 1 v_mfma_f32_16x16x32_f16 (same tiles, LDS image and
 // pipeline; the 16x16 form splits a k tile's MFMAs into two column halves and keeps the split A
 // of the tile in registers for the second half).
+// Row swizzle of the LDS-DMA images: 16-B chunk c of row R sits at position c ^ swz(R >> 1 & 7).
+// 32x32x16 reads: the identity. 16x16x32 reads: a row's 16-lane ds_read_b128 group holds rows 0..15
+// with two k groups (q) split by (R >> 1) in {2..5}, and the identity puts two of its lanes on one
+// bank quadruple (2-way for the A fragments, MI355X_MICROARCH §LDS lane groups); this permutation
+// keeps both the A chunks (2q + p) and the B chunks (2p + q) of every group on distinct banks
+template <int MF>
+__device__ __forceinline__ int gswz(int k) {
+    return MF == 1 ? (int)((0x32765410u >> (4 * k)) & 7u) : k;
+}
+
 template <int WGM, int WGN, int TM, int TN, int STAGES, int AMODE, int EPI, int OCC, int AX = 0, int MF = 0>
 __global__ __launch_bounds__(WGM* WGN * 64, OCC) void k_gemm3g(ASrc a0, ASrc a1, const _Float16* __restrict__ w,
                                                               long long ldw, unsigned wbytes, int M, int N, int K,
@@ -1174,7 +1184,7 @@ __global__ __launch_bounds__(WGM* WGN * 64, OCC) void k_gemm3g(ASrc a0, ASrc a1,
 #pragma unroll
     for (int j = 0; j < NA; j++) {
         const int R = (wave * NA + j) * 8 + sub;
-        const int c = (lane & 7) ^ ((R >> 1) & 7);
+        const int c = (lane & 7) ^ gswz<MF>((R >> 1) & 7);
         const int row = min(m0 + R, M - 1);
         o1[j] = (int)((row - m0) * a1.ld0) * 4 + 16 * c;
 #pragma unroll
@@ -1197,7 +1207,7 @@ __global__ __launch_bounds__(WGM* WGN * 64, OCC) void k_gemm3g(ASrc a0, ASrc a1,
 #pragma unroll
     for (int j = 0; j < NB; j++) {
         const int R = (wave * NB + j) * 8 + sub;
-        const int c = (lane & 7) ^ ((R >> 1) & 7);
+        const int c = (lane & 7) ^ gswz<MF>((R >> 1) & 7);
         wo[j] = (int)(min(n0 + R, N - 1) * ldw) + 16 * c;
     }
 
@@ -1298,7 +1308,7 @@ __global__ __launch_bounds__(WGM* WGN * 64, OCC) void k_gemm3g(ASrc a0, ASrc a1,
     // of rows (l & 15) + 16 x block; the row swizzle ((row >> 1) & 7) is the same for every block
     int aoff16[2], boff16[2];
     {
-        const int q = lane >> 4, r16 = lane & 15, sw = (r16 >> 1) & 7;
+        const int q = lane >> 4, r16 = lane & 15, sw = gswz<MF>((r16 >> 1) & 7);
 #pragma unroll
         for (int p = 0; p < 2; p++) {
             aoff16[p] = (wr * TM * 32 + r16) * 128 + (((2 * q + p) ^ sw) << 4);
@@ -1418,7 +1428,7 @@ __global__ __launch_bounds__(WGM* WGN * 64, OCC) void k_gemm3g(ASrc a0, ASrc a1,
         for (int e = tid; e < BM * BK; e += NW * 64) {
             const int r = e / BK, c = e % BK;
             if ((nk - 1) * BK + c >= kend_last)
-                *reinterpret_cast<float*>(sa + r * 128 + ((((c >> 2) ^ ((r >> 1) & 7))) << 4) + (c & 3) * 4) = 0.f;
+                *reinterpret_cast<float*>(sa + r * 128 + ((((c >> 2) ^ gswz<MF>((r >> 1) & 7))) << 4) + (c & 3) * 4) = 0.f;
         }
         __syncthreads();
     };
