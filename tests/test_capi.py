@@ -54,3 +54,23 @@ def test_product_refuses_cpu(gm):
         pytest.skip("GPU present")
     with pytest.raises(gm._lib.GMError):
         gm.Routing(gm.Network(20), n_env=2)
+
+
+def test_training_entry_points_reject_bad_arguments(gm):
+    """The round-2 training entry points validate their arguments before any device call."""
+    L = gm._lib.lib()
+    vp = ctypes.c_void_p
+    assert L.gm_gemm_set_dgrad(3) == -1 and b"form" in L.gm_last_error()
+    assert L.gm_gemm_set_dgrad(-1) == 0
+    assert L.gm_gemm_set_wgrad(4) == -1
+    assert L.gm_gemm_set_wgrad(-1) == 0
+    # gather of 12-byte records (not a multiple of 16) and a null source
+    assert L.gm_gather_records(vp(16), 16, 16, vp(16), vp(16), 1, 1, 12, vp(16), None) == -1
+    assert b"16-byte" in L.gm_last_error()
+    assert L.gm_gather_records(None, 16, 16, vp(16), vp(16), 1, 1, 16, vp(16), None) == -1
+    # LSTM cell backward without its operands
+    args = gm._lib.LSTMBwdArgs()
+    assert L.gm_lstm_cell_bwd(ctypes.byref(args), None) == -1
+    # Q-head backward with more than 4 heads
+    assert L.gm_qhead_bwd(vp(16), 5, 5, vp(16), 8, vp(16), 8, 8, 8, 1, vp(16), 8, vp(16), vp(16), vp(16), 8, None,
+                          None) == -1
