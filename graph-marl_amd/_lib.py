@@ -41,9 +41,9 @@ EXPORTS = [
 GEMM_MODE = os.environ.get("GM_GEMM", "x3")
 if GEMM_MODE not in ("x3", "f32"):
     raise ValueError(f"GM_GEMM must be 'x3' or 'f32', not {GEMM_MODE!r}")
-# MFMA shape of the LDS-DMA split-f16 kernel (gm_gemm_set_mfma): GM_MFMA=16 (16x16x32 except the
-# fused Q head: the library default), 32 (32x32x16) or 16all (16x16x32 everywhere); unset leaves
-# the library default
+# MFMA shape of the LDS-DMA split-f16 kernel (gm_gemm_set_mfma): GM_MFMA=16all (16x16x32
+# everywhere: the library default), 16 (16x16x32 except the fused Q head) or 32 (32x32x16); unset
+# leaves the library default
 MFMA_SHAPE = os.environ.get("GM_MFMA")
 if MFMA_SHAPE not in (None, "16", "32", "16all"):
     raise ValueError(f"GM_MFMA must be '16', '32' or '16all', not {MFMA_SHAPE!r}")

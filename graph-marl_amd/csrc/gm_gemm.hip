@@ -1558,10 +1558,12 @@ __global__ __launch_bounds__(WGM* WGN * 64, OCC) void k_gemm3g(ASrc a0, ASrc a1,
     }
 }
 
-// k_gemm3g MFMA shape (gm_gemm_set_mfma): 1 16x16x32 (default), 0 32x32x16. The fused Q head
-// stays on 32x32x16 (tools/mfma_ab.sh: rollout kernels 2-5 % faster on 16x16x32, except the
-// head, 89.5 -> 105 us per 81920 rows); 2 = 16x16x32 for the head too
-int g_mfma16 = 1;
+// k_gemm3g MFMA shape (gm_gemm_set_mfma): 2 16x16x32 everywhere (default), 1 16x16x32 except the
+// fused Q head (32x32x16), 0 32x32x16 everywhere. The head on 16x16x32 measured 89.5 -> 105 us per
+// 81920 rows before the 16x16 row swizzle (gswz) removed its 2-way ds_read_b128 conflicts; since
+// then it runs as fast as on 32x32x16 and the whole rollout gains 0.6 % with every GEMM on one shape
+// (5.54-5.55 -> 5.57-5.59 M env-steps/s, three interleaved pairs on one box)
+int g_mfma16 = 2;
 // input-gradient kernel (gm_gemm_set_dgrad): -1 per-shape default, 0 k_gemm3 128x128, 1 k_gemm3g
 // 128x128 (4 waves), 2 k_gemm3g 128x256 (8 waves)
 int g_dgrad = -1;

@@ -415,8 +415,8 @@ int gm_agent_comm(const float* h, int64_t ldh, const int8_t* adj, int32_t B, int
 int gm_gemm_set_wgrad(int32_t form);
 int gm_gemm_set_tile(int32_t tile);
 /* MFMA shape of the LDS-DMA split-f16 kernel (gm_gemm_x3's dense / readout tiles, gm_gemm_x3_head):
- * 1 (default) = v_mfma_f32_16x16x32_f16 except gm_gemm_x3_head (32x32x16), 0 = v_mfma_f32_32x32x16_f16
- * everywhere, 2 = 16x16x32 everywhere. Same tiles and operand images; the summation order inside
+ * 2 (default) = v_mfma_f32_16x16x32_f16 everywhere, 1 = 16x16x32 except gm_gemm_x3_head (32x32x16),
+ * 0 = v_mfma_f32_32x32x16_f16 everywhere. Same tiles and operand images; the summation order inside
  * an MFMA differs (fp32-order results either way). */
 int gm_gemm_set_mfma(int32_t shape);
 /* Input-gradient kernel of gm_gemm_x3_dgrad (same arithmetic and epilogue contract; A-B timing):

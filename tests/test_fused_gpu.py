@@ -208,7 +208,7 @@ def test_gemm_lds_dma_tiles(tile, mfma):
             FU.L.GEMM_MODE = old
     finally:
         lib.gm_gemm_set_tile(-1)
-        lib.gm_gemm_set_mfma(1)
+        lib.gm_gemm_set_mfma(2)
 
 
 @pytest.mark.parametrize("m,n,k,ldx,nq", [(81920, 256, 512, 512, 4), (1000, 256, 512, 516, 4), (777, 100, 90, 92, 2),
@@ -224,7 +224,7 @@ def test_gemm_x3_head_vs_torch(m, n, k, ldx, nq, act, mfma):
     try:
         _head_case(M, FU, m, n, k, ldx, nq, act)
     finally:
-        FU._setup().gm_gemm_set_mfma(1)
+        FU._setup().gm_gemm_set_mfma(2)
 
 
 def _head_case(M, FU, m, n, k, ldx, nq, act):

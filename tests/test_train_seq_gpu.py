@@ -56,7 +56,7 @@ def test_forward_sign_bits(n, mfma):
             assert torch.equal(bits, _pack_bits(y > 0)), tile
     finally:
         FU._setup().gm_gemm_set_tile(-1)
-        FU._setup().gm_gemm_set_mfma(1)
+        FU._setup().gm_gemm_set_mfma(2)
     B, N = 64, 20
     env = gm.Routing(gm.Network(N, random_topology=True, excluded_seeds=gm.EVAL_SEEDS), 20, n_env=B, seed=3)
     env.reset()
@@ -87,7 +87,7 @@ def test_dgrad_epilogue_vs_torch(m, n, k, split, form, mfma):
         _dgrad_case(M, T, S, FU, L, m, n, k, split)
     finally:
         lib.gm_gemm_set_dgrad(-1)
-        lib.gm_gemm_set_mfma(1)
+        lib.gm_gemm_set_mfma(2)
 
 
 def _dgrad_case(M, T, S, FU, L, m, n, k, split):

@@ -66,7 +66,7 @@ for n, k in ((512, 256), (512, 512), (256, 128), (256, 512)):
         else:
             r[tag + "rel_vs_first"] = float((y - y0).abs().max() / y0.abs().max())
     lib.gm_gemm_set_dgrad(-1)
-    lib.gm_gemm_set_mfma(1)
+    lib.gm_gemm_set_mfma(2)
     out[f"{n}x{k}"] = r
     print(n, k, r, flush=True)
 print(json.dumps(out))
