@@ -126,10 +126,17 @@ def kernel_cost(tag, n_env, N, A, E, x3=False):
         # compact state (78A + 22E + 12N) + materialised fp32 obs
         b_state = 78 * A + 22 * E + 12 * N
         b_obs = 4 * A * (6 * N + 10) + 4 * N * (4 * N + 8)
-        return "hbm", float(n_env * (b_state + b_obs))
+        # with the ε-greedy prologue (gm_env_policy_step): + Q rows, actions, RNG words per agent
+        b_pol = A * (16 + 4 + 12) if _fused_policy_step() else 0
+        return "hbm", float(n_env * (b_state + b_obs + b_pol))
     if kind == "egreedy":
         return "hbm", float(n_env * A * (16 + 4 + 12))
     return None, None
+
+
+def _fused_policy_step():
+    import importlib
+    return importlib.import_module("graph-marl_amd.policy").FUSED_POLICY_STEP
 
 
 def measure_train(args, gm, M, W, P, net, netmon, dqn, dev, world, rank):
@@ -169,8 +176,7 @@ def measure_train(args, gm, M, W, P, net, netmon, dqn, dev, world, rank):
             wenv.reset()
         buff.add_pre(env.obs, wenv.last_netmon_state, env.node_obs, env.nbr, env.agent_node)
         with torch.no_grad():
-            act = policy.act(wenv)
-        wenv.step_(act)
+            act = policy.act_step(wenv)
         ep["n"] += 1
         done_ep = ep["n"] >= args.episode_steps
         buff.add_post(act, env.reward, env.obs, env.done.bool(), done_ep, env.node_obs, env.agent_node)

@@ -24,7 +24,7 @@ EVAL_KEYS = ["total_edge_load", "occupied_edges", "packets_on_edges", "total_pac
 # every symbol the header declares (checked by tests/test_capi.py)
 EXPORTS = [
     "gm_last_error", "gm_version", "gm_env_create", "gm_env_destroy", "gm_env_dims", "gm_env_reset",
-    "gm_env_step", "gm_env_observe", "gm_env_topology", "gm_env_final_info", "gm_policy_egreedy",
+    "gm_env_step", "gm_env_observe", "gm_env_topology", "gm_env_final_info", "gm_policy_egreedy", "gm_env_policy_step",
     "gm_env_get_state", "gm_env_set_state", "gm_build_seed_list", "gm_mp_aggregate", "gm_mp_aggregate_rows", "gm_mp_aggregate_bwd", "gm_leaky_bwd", "gm_netmon_readout",
     "gm_netmon_readout_bwd", "gm_lstm_pointwise", "gm_lstm_pointwise_bwd", "gm_linear_f32", "gm_gemm_f32",
     "gm_gemm_set_tile", "gm_gemm_set_wgrad", "gm_gemm_set_mfma", "gm_gemm_set_dgrad", "gm_simple_create", "gm_simple_destroy", "gm_simple_reset", "gm_simple_step",
@@ -125,6 +125,8 @@ def lib():
     L.gm_env_topology.argtypes = [vp, vp, vp, vp, vp, vp]
     L.gm_env_final_info.argtypes = [vp, vp, vp]
     L.gm_policy_egreedy.argtypes = [vp, vp, C.c_double, vp, vp]
+    L.gm_env_policy_step.argtypes = [vp, vp, C.c_double, vp, vp, vp, vp, C.POINTER(StepDetail), C.POINTER(ObsBuffers),
+                                     vp]
     L.gm_env_get_state.argtypes = [vp, C.POINTER(EnvState)]
     L.gm_env_set_state.argtypes = [vp, C.POINTER(EnvState)]
     L.gm_build_seed_list.argtypes = [i32, i64, i32, vp, i32, i32, vp]

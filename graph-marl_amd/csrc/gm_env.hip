@@ -679,11 +679,34 @@ __global__ __launch_bounds__(64) void k_env_reset(EnvDev d, const uint8_t* mask,
     }
 }
 
+// action of packet lane l from the 3 A prefetched words: randint(4, size=A) uses word l (mask 3),
+// rand(A) words A + 2 l, A + 2 l + 1; first maximum of the (masked) Q row unless the draw < eps
+__device__ __forceinline__ int egreedy_lane(const EnvDev& d, const float* q, double eps, size_t p,
+                                            const uint32_t* rbuf, int l, int A) {
+    const float4 qv = reinterpret_cast<const float4*>(q)[p];
+    float v[4] = {qv.x, qv.y, qv.z, qv.w};
+    if (d.amask_on) {
+        const uint32_t m = reinterpret_cast<const uint32_t*>(d.amask)[p];
+        for (int k = 0; k < 4; k++)
+            if ((m >> (8 * k)) & 0xffu) v[k] = -__builtin_inff();
+    }
+    int best = 0;
+    for (int k = 1; k < 4; k++)
+        if (v[k] > v[best]) best = k;
+    const int ra = (int)(rbuf[l] & 3u);
+    const uint32_t w0 = rbuf[A + 2 * l], w1 = rbuf[A + 2 * l + 1];
+    const double u = ((int32_t)(w0 >> 5) * 67108864.0 + (int32_t)(w1 >> 6)) / 9007199254740992.0;
+    return u < eps ? ra : best;
+}
+
 struct StepOut {
     float* reward;
     uint8_t* done;
     double* info;
     gm_step_detail det;
+    const float* q;    // gm_env_policy_step: Q [n_env, A, 4] -> ε-greedy prologue (nullable)
+    double eps;
+    int32_t* act_out;  // the actions drawn by the prologue, [n_env, A]
 };
 
 // src/env/routing.py:360-520
@@ -701,11 +724,26 @@ __global__ __launch_bounds__(64) void k_env_step(EnvDev d, const int32_t* act, S
     int now = 0, target = 0, edge = -1, time = 0, ttl = 0, steps = 0, spw = 0, start = 0, a_t = 0;
     double size = 0.0;
     uint64_t vis[2] = {0ull, 0ull};  // visited node set (N <= 128)
+    // ε-greedy prologue (gm_policy_egreedy's draws, same stream order: the policy draws before
+    // the step's respawns); the stream position stays in registers for the respawn draws below
+    int rng_cur = 0, rng_pos = 0, rng_next = 0;
+    const bool pol = out.q != nullptr;
+    if (pol) {
+        MainRng r = open_rng(d, env, s);
+        r.prefetch(3 * A);
+        if (own) a_t = egreedy_lane(d, out.q, out.eps, p, s.rbuf, l, A);
+        r.k = 3 * A;
+        close_rng(d, env, r);
+        rng_cur = r.cur;
+        rng_pos = r.pos;
+        rng_next = r.has_next;
+        if (own) out.act_out[p] = a_t;
+    }
     if (own) {
         now = d.now[p]; target = d.target[p]; edge = d.edge[p]; time = d.time[p];
         ttl = d.ttl_[p]; steps = d.steps[p]; spw = d.spw[p]; start = d.start[p];
         size = d.size[p]; vis[0] = d.visited[p * 2]; vis[1] = d.visited[p * 2 + 1];
-        a_t = act[p];
+        if (!pol) a_t = act[p];
         if (a_t < 0 || a_t > 3) {  // the reference raises IndexError; flag and idle
             atomicExch(d.err, GM_ERR_INVALID_ARG);
             a_t = 0;
@@ -861,6 +899,11 @@ __global__ __launch_bounds__(64) void k_env_step(EnvDev d, const int32_t* act, S
     // respawn finished packets in id order (reset_packet draws, routing.py:130-134)
     if (finm) {
         MainRng r = open_rng(d, env, s);
+        if (pol) {  // the prologue's position (its lane-0 stores are not read back)
+            r.cur = rng_cur;
+            r.pos = rng_pos;
+            r.has_next = rng_next;
+        }
         r.prefetch(6 * __popcll(finm) + 8);
         uint64_t m = finm;
         while (m) {
@@ -933,20 +976,7 @@ __global__ __launch_bounds__(64) void k_policy_egreedy(EnvDev d, const float* q,
     r.prefetch(3 * A);
     if (l < A) {
         size_t p = (size_t)env * A + l;
-        float4 qv = reinterpret_cast<const float4*>(q)[p];
-        float v[4] = {qv.x, qv.y, qv.z, qv.w};
-        if (d.amask_on) {
-            uint32_t m = reinterpret_cast<const uint32_t*>(d.amask)[p];
-            for (int k = 0; k < 4; k++)
-                if ((m >> (8 * k)) & 0xffu) v[k] = -__builtin_inff();
-        }
-        int best = 0;
-        for (int k = 1; k < 4; k++)
-            if (v[k] > v[best]) best = k;
-        int ra = (int)(rbuf[l] & 3u);
-        uint32_t w0 = rbuf[A + 2 * l], w1 = rbuf[A + 2 * l + 1];
-        double u = ((int32_t)(w0 >> 5) * 67108864.0 + (int32_t)(w1 >> 6)) / 9007199254740992.0;
-        actions[p] = u < eps ? ra : best;
+        actions[p] = egreedy_lane(d, q, eps, p, rbuf, l, A);
     }
     r.k = 3 * A;
     r.commit();
@@ -1329,9 +1359,9 @@ extern "C" int gm_env_reset(gm_env* env, const uint8_t* reset_mask, const gm_obs
     return check_launch();
 }
 
-extern "C" int gm_env_step(gm_env* env, const int32_t* actions, float* reward, uint8_t* done, double* info,
-                           const gm_step_detail* detail, const gm_obs_buffers* obs, void* stream) {
-    if (!env || !actions || !reward || !done) return gm_fail(GM_ERR_INVALID_ARG, "null argument");
+static int launch_step(gm_env* env, const int32_t* actions, const float* q, double epsilon, int32_t* act_out,
+                       float* reward, uint8_t* done, double* info, const gm_step_detail* detail,
+                       const gm_obs_buffers* obs, void* stream) {
     int rc = check_obs(env, obs);
     if (rc) return rc;
     StepOut so;
@@ -1339,10 +1369,27 @@ extern "C" int gm_env_step(gm_env* env, const int32_t* actions, float* reward, u
     so.done = done;
     so.info = info;
     so.det = detail ? *detail : gm_step_detail{};
+    so.q = q;
+    so.eps = epsilon;
+    so.act_out = act_out;
     gm_obs_buffers o = obs ? *obs : gm_obs_buffers{};
     if (ncap(env->d.N) == 64) hipLaunchKernelGGL(k_env_step<64>, dim3(env->d.n_env), dim3(64), 0, (hipStream_t)stream, env->d, actions, so, o);
     else hipLaunchKernelGGL(k_env_step<128>, dim3(env->d.n_env), dim3(64), 0, (hipStream_t)stream, env->d, actions, so, o);
     return check_launch();
+}
+
+extern "C" int gm_env_step(gm_env* env, const int32_t* actions, float* reward, uint8_t* done, double* info,
+                           const gm_step_detail* detail, const gm_obs_buffers* obs, void* stream) {
+    if (!env || !actions || !reward || !done) return gm_fail(GM_ERR_INVALID_ARG, "null argument");
+    return launch_step(env, actions, nullptr, 0.0, nullptr, reward, done, info, detail, obs, stream);
+}
+
+extern "C" int gm_env_policy_step(gm_env* env, const float* q, double epsilon, int32_t* actions, float* reward,
+                                  uint8_t* done, double* info, const gm_step_detail* detail, const gm_obs_buffers* obs,
+                                  void* stream) {
+    if (!env || !q || !actions || !reward || !done) return gm_fail(GM_ERR_INVALID_ARG, "null argument");
+    if ((reinterpret_cast<uintptr_t>(q) & 15) != 0) return gm_fail(GM_ERR_INVALID_ARG, "q must be 16-byte aligned");
+    return launch_step(env, nullptr, q, epsilon, actions, reward, done, info, detail, obs, stream);
 }
 
 __global__ void k_topology_rewind(EnvDev d, int interleave) {

@@ -392,8 +392,11 @@ def main(argv=None):
             else:
                 buff.add_pre(base.obs, adj=adj, agent_state=last_state)
             with torch.no_grad():
-                actions = policy.act(env)
-            env.step_(actions)
+                if hasattr(policy, "act_step"):  # ε-greedy draws fused into the env step kernel
+                    actions = policy.act_step(env)
+                else:
+                    actions = policy.act(env)
+                    env.step_(actions)
             if has_state:  # done agents restart from a zero state (src/main.py:710-716)
                 last_state = model.state * ~base.done.bool().unsqueeze(-1)
             episode_step += 1

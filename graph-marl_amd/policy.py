@@ -5,8 +5,12 @@ Q-values come from the agent model (DQN, DGN, DQNR, CommNet) on the HIP kernels;
 stream) and the argmax/mix run in the env's egreedy kernel (gm_policy_egreedy /
 gm_simple_policy_egreedy).
 """
+import os
+
 import torch
 
+# GM_POLICY_STEP=split keeps ε-greedy and the env step as two launches (A-B timing)
+FUSED_POLICY_STEP = os.environ.get("GM_POLICY_STEP", "fused") != "split"
 
 
 class EpsilonGreedy:
@@ -78,6 +82,27 @@ class EpsilonGreedy:
         actions = self.select(q.view(e.n_env, e.n_data, -1))
         self._decay_step()
         return actions
+
+    def act_step(self, wenv, detail=None):
+        """act(wenv) then wenv.step_(actions). On the fused NetMon path the ε-greedy draws run
+        as the env step kernel's prologue (gm_env_policy_step: one launch instead of two, the
+        same draws and actions)."""
+        from . import fused as FU
+        from .model import DQN
+
+        if not (getattr(wenv, "fused", False) and isinstance(self._model, DQN) and FUSED_POLICY_STEP):
+            actions = self.act(wenv)
+            if detail is None:
+                wenv.step_(actions)
+            else:
+                wenv.step_(actions, detail)
+            return actions
+        e = wenv.env
+        q = FU.dqn_q(self._model, e.obs_buf, e.obs_dim, wenv.current_netmon_state, wenv.h_prev, e.nbr,
+                     e.agent_node, self._buf, hidden=wenv.netmon.hidden_features)
+        wenv.policy_step_(q.view(e.n_env, e.n_data, -1).contiguous(), self._epsilon, self.actions, detail)
+        self._decay_step()
+        return self.actions
 
     def _eps_changes(self):
         """True when ε still decays (its value is a kernel argument)."""

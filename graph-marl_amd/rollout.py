@@ -98,8 +98,7 @@ class StreamedRollout:
     def _enqueue_step(self):
         for g in range(self.groups):
             with self._on(g):
-                act = self.policies[g].act(self.wenvs[g])
-                self.wenvs[g].step_(act)
+                self.policies[g].act_step(self.wenvs[g])
 
     @torch.no_grad()
     def step(self):

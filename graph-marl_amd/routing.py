@@ -228,6 +228,25 @@ class Routing:
         if a.dtype != torch.int32 or not a.is_contiguous():
             self._actions.copy_(a)
             a = self._actions
+        det = self._detail(detail)
+        with L.timed("env_step"):
+            L.check(L.lib().gm_env_step(self._h, L.ptr(a), L.ptr(self.reward), L.ptr(self.done), L.ptr(self.info),
+                                        None if det is None else C.byref(det), C.byref(self._obsbufs),
+                                        self._stream()))
+
+    def policy_step_(self, q, epsilon, actions, detail=None):
+        """egreedy(q, epsilon, actions) then step_(actions) as one kernel (gm_env_policy_step):
+        identical draws, actions and results; q [n_env, A, 4] contiguous, actions int32 [n_env, A]."""
+        assert q.is_contiguous() and actions.dtype == torch.int32 and actions.is_contiguous()
+        det = self._detail(detail)
+        with L.timed("env_step"):
+            L.check(L.lib().gm_env_policy_step(self._h, L.ptr(q), float(epsilon), L.ptr(actions), L.ptr(self.reward),
+                                               L.ptr(self.done), L.ptr(self.info),
+                                               None if det is None else C.byref(det), C.byref(self._obsbufs),
+                                               self._stream()))
+        return actions
+
+    def _detail(self, detail):
         det = None
         if detail is not None or self.eval_info_enabled:
             det = L.StepDetail()
@@ -237,10 +256,7 @@ class Routing:
                                                              detail["success"].data_ptr())
             if self.eval_info_enabled:
                 det.eval = self.eval_stats.data_ptr()
-        with L.timed("env_step"):
-            L.check(L.lib().gm_env_step(self._h, L.ptr(a), L.ptr(self.reward), L.ptr(self.done), L.ptr(self.info),
-                                        None if det is None else C.byref(det), C.byref(self._obsbufs),
-                                        self._stream()))
+        return det
 
     def step(self, act):
         """Routing.step (routing.py:360-520) -> (obs, adj, reward, done, info) with a

@@ -106,6 +106,11 @@ class NetMonWrapper:
         self.env.step_(actions, detail)
         self._netmon_step()
 
+    def policy_step_(self, q, epsilon, actions, detail=None):
+        """ε-greedy on q + env step in one launch (Routing.policy_step_), then the NetMon step."""
+        self.env.policy_step_(q, epsilon, actions, detail)
+        self._netmon_step()
+
     def get_netmon_info(self):
         return self.env.node_obs, self.env.nbr, self.env.agent_node
 

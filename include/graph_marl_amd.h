@@ -16,6 +16,7 @@
  *   gm_env_final_info                Routing.get_final_info                 src/env/routing.py:541-546
  *   gm_build_seed_list               Network.build_seed_list                src/env/network.py:100-120
  *   gm_policy_egreedy                EpsilonGreedy.__call__ (draws + select) src/policy.py:20-64
+ *   gm_env_policy_step               EpsilonGreedy.__call__ + Routing.step in one launch (src/main.py:701-703)
  *   gm_mp_aggregate(_bwd)            SimpleAggregation.forward              src/model.py:206-229
  *   gm_netmon_readout(_bwd)          NetMon._get_neighbor_h + output_to_network_obs src/model.py:582-631
  *   gm_lstm_pointwise(_bwd)          nn.LSTMCell gate math / LayerNorm-free part    src/model.py:379-382, 491, 543
@@ -155,6 +156,11 @@ int gm_build_seed_list(int32_t n_nodes, int64_t init_seed, int32_t count, const 
 /* ε-greedy action selection: q float32 [n_env, A, 4]; epsilon as the reference's
  * float64; draws randint(4,size=A) then rand(A) from every env's stream. */
 int gm_policy_egreedy(gm_env* env, const float* q, double epsilon, int32_t* actions, void* stream);
+/* gm_policy_egreedy followed by gm_env_step as one kernel: the same draws in the same stream
+ * order, so actions and every output are identical to the two calls; actions (device int32
+ * [n_env, A]) receives the drawn actions. q must be 16-byte aligned. */
+int gm_env_policy_step(gm_env* env, const float* q, double epsilon, int32_t* actions, float* reward, uint8_t* done,
+                       double* info, const gm_step_detail* detail, const gm_obs_buffers* obs, void* stream);
 
 /* Host-side state export/import for parity tests (synchronous). Arrays are host
  * pointers sized [n_env, ...]; any may be NULL. */

@@ -222,6 +222,54 @@ def test_egreedy_batch_vs_oracle(gm, oracle_mod):
         np.testing.assert_array_equal(st["rng_key"][b], o.state()["rng_key"])
 
 
+@pytest.mark.parametrize("mask,ttl", [(False, 0), (True, 9)])
+def test_policy_step_fused_matches_split(gm, oracle_mod, mask, ttl):
+    """gm_env_policy_step (ε-greedy as the env step kernel's prologue) == gm_policy_egreedy +
+    gm_env_step, bit for bit: actions, rewards, done, info, observations and the whole env state
+    incl. the MT streams, over 120 steps with resets every 50 (respawn draws after the policy's
+    draws in one kernel); the actions also match the oracle's draws on a sample of envs."""
+    B, n, a = 256, 20, 20
+    net = gm.Network(n, random_topology=True, excluded_seeds=gm.EVAL_SEEDS)
+    seeds = list(range(300, 300 + B))
+    kw = dict(enable_action_mask=mask, ttl=ttl, n_env=B, seeds=seeds)
+    ea, eb = gm.Routing(net, a, 1, **kw), gm.Routing(net, a, 1, **kw)
+    sample = [0, 5, 255]
+    orc = [_oracle_env(oracle_mod, n, a, "random", 476, seeds[b], mask=mask, ttl=ttl) for b in sample]
+    from importlib import import_module
+
+    L = import_module("graph-marl_amd._lib")
+    rng = np.random.RandomState(17)
+    act_a = torch.zeros(B, a, dtype=torch.int32, device=ea.device)
+    act_b = torch.zeros_like(act_a)
+    for t in range(120):
+        if t % 50 == 0:
+            ea.reset_()
+            eb.reset_()
+            for o in orc:
+                o.reset()
+        q = rng.standard_normal((B, a, 4)).astype(np.float32)
+        eps = [0.0, 0.3, 1.0][t % 3]
+        qt = torch.as_tensor(q, device=ea.device)
+        L.check(L.lib().gm_policy_egreedy(ea._h, L.ptr(qt), eps, L.ptr(act_a), L.stream_ptr()))
+        ea.step_(act_a)
+        eb.policy_step_(qt, eps, act_b)
+        got = act_b.cpu().numpy()
+        np.testing.assert_array_equal(got, act_a.cpu().numpy(), err_msg=f"actions t {t}")
+        for name in ("reward", "done", "info", "obs_buf", "node_obs", "nbr", "agent_node"):
+            x, y = getattr(ea, name), getattr(eb, name)
+            assert torch.equal(x, y), f"{name} differs at t {t}"
+        for i, o in zip(sample, orc):
+            want = o.draw_egreedy(q[i], eps)  # the oracle's draws ignore the action mask
+            if not mask:
+                np.testing.assert_array_equal(got[i], want, err_msg=f"oracle t {t} env {i}")
+            o.step(got[i])
+    sa, sb = ea.get_state(), eb.get_state()
+    for k in sa:
+        np.testing.assert_array_equal(np.asarray(sa[k]), np.asarray(sb[k]), err_msg=f"state {k}")
+    for i, o in zip(sample, orc):
+        np.testing.assert_array_equal(sb["rng_key"][i], o.state()["rng_key"])
+
+
 def test_large_batch_invariants(gm, oracle_mod):
     """4096 envs (the benchmark size): conservation laws every step, and a sample of
     envs replayed bit-exactly on the oracle."""

@@ -63,6 +63,14 @@ def test_benched_rollout_long_horizon(form, monkeypatch, oracle_mod):
             return orig(q)
 
         pol.select = select
+        wenv = ro.wenvs[g]
+        orig_ps = wenv.policy_step_
+
+        def policy_step_(q, eps, actions, detail=None, g=g, orig_ps=orig_ps):  # fused ε-greedy + env step
+            qrec[g] = q.clone()
+            return orig_ps(q, eps, actions, detail)
+
+        wenv.policy_step_ = policy_step_
 
     cfg = oracle_mod.make_config(N, A, topo_mode=oracle_mod.TOPO_RANDOM, excluded=gm.EVAL_SEEDS)
     orc = {e: oracle_mod.OracleEnv(cfg, e) for e in SAMPLE}
