@@ -604,12 +604,17 @@ class GRUCell(nn.Module):
         return (1 - z) * n + z * h
 
 
-def dense_to_nbr(mask):
-    """(I + A) float mask [B, N, N] -> neighbour table int32 [B, N, deg] (ascending, -1 pad)."""
+def dense_to_nbr(mask, max_degree=None):
+    """(I + A) float mask [B, N, N] -> neighbour table int32 [B, N, deg] (ascending, -1 pad).
+    deg = max_degree when given (the reference's NetMon.forward argument, src/model.py:451-474;
+    no host sync), else the largest degree in the batch (one device -> host read)."""
     B, N, _ = mask.shape
     m = (mask != 0) & ~torch.eye(N, dtype=torch.bool, device=mask.device)
-    deg = int(m.sum(-1).max().item()) if m.numel() else 0
-    deg = max(deg, 1)
+    if max_degree is not None:
+        deg = int(max_degree)
+    else:
+        deg = int(m.sum(-1).max().item()) if m.numel() else 0
+    deg = min(max(deg, 1), N)
     ids = torch.arange(N, device=mask.device).expand(B, N, N)
     key = torch.where(m, ids, ids + N)
     srt = key.sort(-1).values[..., :deg]
@@ -789,7 +794,7 @@ class NetMon(nn.Module):
         return res.reshape(B, R, -1)
 
     def forward(self, x, mask, node_agent_matrix=None, max_degree=None, no_agent_mapping=False):
-        nbr = dense_to_nbr(mask)
+        nbr = dense_to_nbr(mask, max_degree)
         an = None if (no_agent_mapping or node_agent_matrix is None) else node_agent_to_index(node_agent_matrix)
         return self.forward_graph(x, nbr, an)
 
