@@ -1263,7 +1263,15 @@ extern "C" int gm_routing_node_encoder_bits(const float* x, int64_t ldx, const i
     const size_t lds = (size_t)K * 64 * cpl * 4;
     if (lds > 65536) return gm_fail(GM_ERR_UNSUPPORTED, "gm_routing_node_encoder: 4N+8 too large for the LDS slice");
     const long long M = (long long)G * N;
-    const int rows = 256;  // 64 rows per wave (512 / 1024 / 2048: +/-0 / +17 / +52 % time)
+    // rows per block: the block's W^T slice (K x BN) is staged once for them, so larger graphs take more
+    // rows. Measured per launch (4096 envs): N = 20 256 / 512 / 1024 rows 60.9 / 61.3 / 75.8 us;
+    // N = 30 117 / 103 / 92 us; N = 40 196 / 178 / 160 us. GM_RENC_ROWS overrides (A-B)
+    static const int rows_env = [] {
+        const char* e = getenv("GM_RENC_ROWS");
+        const int v = e ? atoi(e) : 0;
+        return (v >= 256 && v % 256 == 0) ? v : 0;
+    }();
+    const int rows = rows_env ? rows_env : (K <= 88 ? 256 : (K <= 128 ? 512 : 1024));
     dim3 grid((unsigned)((M + rows - 1) / rows), (unsigned)(n / (64 * cpl)));
     if (cpl == 2)
         hipLaunchKernelGGL(k_routing_enc<2>, grid, dim3(256), lds, (hipStream_t)stream, x, (long long)ldx, nbr, G, N,

@@ -155,7 +155,7 @@ def test_fused_netmon_vs_reference_golden(vi):
         np.testing.assert_allclose(out.view(B, -1, 4 * Hh).cpu().numpy(), g[f"v{vi}_mapped_{t}"], atol=1e-5, rtol=0)
 
 
-@pytest.mark.parametrize("n,out", [(20, 512), (50, 512), (10, 64), (20, 192)])
+@pytest.mark.parametrize("n,out", [(20, 512), (50, 512), (10, 64), (20, 192), (30, 512), (40, 256)])
 def test_routing_node_encoder_vs_torch(n, out):
     """Sparse first encoder layer on real routing node observations vs the dense fp32 product."""
     gm = importlib.import_module("graph-marl_amd")
