@@ -128,7 +128,9 @@ def kernel_cost(tag, n_env, N, A, E, x3=False):
         b_obs = 4 * A * (6 * N + 10) + 4 * N * (4 * N + 8)
         # with the ε-greedy prologue (gm_env_policy_step): + Q rows, actions, RNG words per agent
         b_pol = A * (16 + 4 + 12) if _fused_policy_step() else 0
-        return "hbm", float(n_env * (b_state + b_obs + b_pol))
+        # the GEMM-ready copy of the agent rows the fused DQN reads (gm_obs_buffers.obs_gemm)
+        b_gemm = 4 * A * (6 * N + 8) if _gemm_obs() else 0
+        return "hbm", float(n_env * (b_state + b_obs + b_pol + b_gemm))
     if kind == "egreedy":
         return "hbm", float(n_env * A * (16 + 4 + 12))
     return None, None
@@ -137,6 +139,13 @@ def kernel_cost(tag, n_env, N, A, E, x3=False):
 def _fused_policy_step():
     import importlib
     return importlib.import_module("graph-marl_amd.policy").FUSED_POLICY_STEP
+
+
+_GEMM_OBS_ON = [False]  # set from the timed rollout's env (Routing.obs_gemm allocated)
+
+
+def _gemm_obs():
+    return _GEMM_OBS_ON[0]
 
 
 def measure_train(args, gm, M, W, P, net, netmon, dqn, dev, world, rank):
@@ -256,6 +265,7 @@ def main():
     ro = RO.StreamedRollout(net, A, B, netmon, dqn, groups=args.groups, seed=rank * B, epsilon=args.epsilon,
                             episode_steps=args.episode_steps, device=dev.index,
                             stagger=args.stagger and not args.graph)
+    _GEMM_OBS_ON[0] = ro.envs[0].obs_gemm is not None
     if args.unfused:
         for w in ro.wenvs:
             w.fused = False

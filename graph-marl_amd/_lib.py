@@ -65,7 +65,8 @@ class EnvConfig(C.Structure):
 
 class ObsBuffers(C.Structure):
     _fields_ = [("obs", C.c_void_p), ("obs_row_stride", C.c_int64), ("node_obs", C.c_void_p),
-                ("agent_node", C.c_void_p), ("agent_adj", C.c_void_p)]
+                ("agent_node", C.c_void_p), ("agent_adj", C.c_void_p), ("obs_gemm", C.c_void_p),
+                ("obs_gemm_stride", C.c_int64)]
 
 
 class StepDetail(C.Structure):

@@ -310,6 +310,21 @@ __device__ void emit_obs(const EnvDev& d, int env, ES& s, const gm_obs_buffers& 
                     base[(size_t)(a0 + r) * ld + c] = stg[r * SR + c];
                 }
             }
+            if (o.obs_gemm) {  // the GEMM copy without columns N-1 and 2N (host-checked: var 1, 16-B rows)
+                const int Qg = (D1 - 2) / 4;  // 6N+8 = 4 Qg (N even)
+                float* gb = o.obs_gemm + ((size_t)env * A + a0) * o.obs_gemm_stride;
+                for (int i = l; i < nr * Qg; i += WAVE) {
+                    const int r = i / Qg, q = i - r * Qg;
+                    float v[4];
+#pragma unroll
+                    for (int j = 0; j < 4; j++) {
+                        const int c = 4 * q + j;
+                        v[j] = stg[r * SR + (c < N - 1 ? c : (c < 2 * N - 1 ? c + 1 : c + 2))];
+                    }
+                    *reinterpret_cast<float4*>(gb + (size_t)r * o.obs_gemm_stride + 4 * q) =
+                        make_float4(v[0], v[1], v[2], v[3]);
+                }
+            }
             __syncthreads();
         }
         if (D > D1) {  // variant columns (2: k neighbour slots, 3: global), lane-strided per row
@@ -1344,6 +1359,10 @@ extern "C" int gm_env_dims(const gm_env* env, int32_t* n_env, int32_t* n_nodes, 
 static int check_obs(const gm_env* env, const gm_obs_buffers* o) {
     if (o && o->obs && o->obs_row_stride < obs_dim_of(env->d.N, env->d.env_var, env->d.k))
         return gm_fail(GM_ERR_INVALID_ARG, "obs_row_stride smaller than the observation size");
+    if (o && o->obs_gemm &&
+        (!o->obs || env->d.env_var != 1 || o->obs_gemm_stride < 6 * env->d.N + 8 || (o->obs_gemm_stride % 4) ||
+         (reinterpret_cast<uintptr_t>(o->obs_gemm) & 15)))
+        return gm_fail(GM_ERR_INVALID_ARG, "obs_gemm: env_var 1 with obs, stride >= 6N+8 and 16-byte rows");
     return GM_OK;
 }
 

@@ -216,20 +216,36 @@ def pack_lnlstm(cell):
     return cell._packed.get(_key(cell.weight_ih, cell.weight_hh) + (L.GEMM_MODE,), build)
 
 
-def pack_dqn_first(lin, obs_dim):
-    """W1 columns reordered to [graph part | env obs part] to match A = [readout | env obs]."""
+def fold_env_weight(we, n):
+    """Env-obs weight columns [out, 6N+10] -> [out, 6N+8] for the GEMM-ready obs copy
+    (gm_obs_buffers.obs_gemm), exact in real arithmetic (src/env/routing.py:269-315 rows):
+    position one-hot column N-1 = sum(target one-hot) - sum(position one-hots 0..N-2), and the
+    edge flag (column 2N) = sum of the next-hop one-hot (columns 2N+1..3N). Summed in fp64,
+    rounded once."""
+    w = we.double()
+    last, flag = w[:, n - 1:n], w[:, 2 * n:2 * n + 1]
+    out = torch.cat([w[:, :n - 1] - last, w[:, n:2 * n] + last, w[:, 2 * n + 1:3 * n + 1] + flag, w[:, 3 * n + 1:]], 1)
+    return out.to(we.dtype)
+
+
+def pack_dqn_first(lin, obs_dim, fold_n=None):
+    """W1 columns reordered to [graph part | env obs part] to match A = [readout | env obs];
+    fold_n = N: env part folded to the 6N+8 columns of the GEMM-ready obs copy."""
     if not hasattr(lin, "_packed_first"):
         lin._packed_first = Packed()
 
     def build():
         with torch.no_grad():
-            w = torch.cat([lin.weight[:, obs_dim:], lin.weight[:, :obs_dim]], 1)
+            we = lin.weight[:, :obs_dim]
+            if fold_n is not None:
+                we = fold_env_weight(we, fold_n)
+            w = torch.cat([lin.weight[:, obs_dim:], we], 1).contiguous()
             wp, ldw = _pad_cols(w)
             n = lin.out_features
-            x3 = X3(wp, ldw, n, lin.in_features) if use_x3(n) else None
+            x3 = X3(wp, ldw, n, w.shape[1]) if use_x3(n) else None
             return wp, ldw, lin.bias.contiguous(), x3
 
-    return lin._packed_first.get(_key(lin.weight, lin.bias) + (obs_dim, L.GEMM_MODE), build)
+    return lin._packed_first.get(_key(lin.weight, lin.bias) + (obs_dim, fold_n, L.GEMM_MODE), build)
 
 
 def pack_x3(lin):
@@ -450,21 +466,28 @@ def netmon_step(netmon, node_obs, nbr, state, out=None, last_out=None):
 
 
 @torch.no_grad()
-def dqn_q(dqn, env_obs, obs_dim, state, h_prev, nbr, agent_node, scratch, hidden=None):
+def dqn_q(dqn, env_obs, obs_dim, state, h_prev, nbr, agent_node, scratch, hidden=None, obs_gemm=None):
     """Q [B*A, actions] of the DQN on [env obs | NetMon readout] with the readout gathered
     inside the first GEMM. env_obs: [B, A, stride] (first obs_dim columns used); state rows
-    [h | ...] of width state.shape[-1] (hidden H: default half the width, the LSTM layout)."""
+    [h | ...] of width state.shape[-1] (hidden H: default half the width, the LSTM layout).
+    obs_gemm: the env's GEMM-ready copy [B, A, 6N+8] (Routing.enable_gemm_obs): read instead of
+    env_obs with the folded weights (K two columns shorter: whole k tiles at N = 20)."""
     B, A, stride = env_obs.shape
     N = nbr.shape[1]
     H = hidden or state.shape[-1] // 2
     M = B * A
     lin0 = dqn.encoder.linear_layers[0]
-    wp, ldw, b, x3 = pack_dqn_first(lin0, obs_dim)
+    fold = obs_gemm is not None and obs_dim == 6 * N + 10
+    wp, ldw, b, x3 = pack_dqn_first(lin0, obs_dim, N if fold else None)
+    if fold:
+        src, ks = dense(obs_gemm.data_ptr(), obs_gemm.stride(1), obs_dim - 2), obs_dim - 2
+    else:
+        src, ks = dense(env_obs.data_ptr(), stride, obs_dim), obs_dim
     h1 = scratch(0, M, lin0.out_features)
     a0 = readout(state.data_ptr(), state.shape[-1], h_prev.data_ptr(), h_prev.stride(0), nbr, agent_node, N, H)
-    gemm(a0, dense(env_obs.data_ptr(), stride, obs_dim), wp.data_ptr(), ldw, b.data_ptr(), M, lin0.out_features,
+    gemm(a0, src, wp.data_ptr(), ldw, b.data_ptr(), M, lin0.out_features,
          GM_EPI_BIAS_LEAKY if lin0.act == 1 else GM_EPI_BIAS, h1.data_ptr(), h1.stride(0),
-         tag=lin0.tag and f"linear:{lin0.tag}:{M}x{lin0.out_features}x{a0.k + obs_dim}", x3=x3)
+         tag=lin0.tag and f"linear:{lin0.tag}:{M}x{lin0.out_features}x{a0.k + ks}", x3=x3)
     h = h1
     hidden = list(dqn.encoder.linear_layers[1:])
     fc = dqn.q_net.fc

@@ -78,7 +78,7 @@ class EpsilonGreedy:
             return self(wenv.obs)
         e = wenv.env
         q = FU.dqn_q(self._model, e.obs_buf, e.obs_dim, wenv.current_netmon_state, wenv.h_prev, e.nbr,
-                     e.agent_node, self._buf, hidden=wenv.netmon.hidden_features)
+                     e.agent_node, self._buf, hidden=wenv.netmon.hidden_features, obs_gemm=e.obs_gemm)
         actions = self.select(q.view(e.n_env, e.n_data, -1))
         self._decay_step()
         return actions
@@ -99,7 +99,7 @@ class EpsilonGreedy:
             return actions
         e = wenv.env
         q = FU.dqn_q(self._model, e.obs_buf, e.obs_dim, wenv.current_netmon_state, wenv.h_prev, e.nbr,
-                     e.agent_node, self._buf, hidden=wenv.netmon.hidden_features)
+                     e.agent_node, self._buf, hidden=wenv.netmon.hidden_features, obs_gemm=e.obs_gemm)
         wenv.policy_step_(q.view(e.n_env, e.n_data, -1).contiguous(), self._epsilon, self.actions, detail)
         self._decay_step()
         return self.actions

@@ -16,6 +16,9 @@ import torch
 
 from . import _lib as L
 
+# GM_GEMM_OBS=0: the fused DQN reads the env obs with K = 6N+10 instead of the GEMM-ready copy (A-B)
+GEMM_OBS = os.environ.get("GM_GEMM_OBS", "1") != "0"
+
 EVAL_SEEDS = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "data", "eval_seeds.npy"))
 
 
@@ -154,6 +157,8 @@ class Routing:
         self.info = torch.zeros(n_env, L.GM_INFO_FIELDS, dtype=torch.float64, device=dev)
         self.nbr = torch.zeros(n_env, N, 3, dtype=torch.int32, device=dev)
         self._actions = torch.zeros(n_env, A, dtype=torch.int32, device=dev)
+        self.obs_gemm = None  # GEMM-ready env obs copy (enable_gemm_obs)
+        self._has_state = False
         self._obsbufs = self._make_obsbufs(self.agent_adjacency)
 
     # -- plumbing ---------------------------------------------------------------
@@ -164,7 +169,22 @@ class Routing:
         o.node_obs = self.node_obs.data_ptr()
         o.agent_node = self.agent_node.data_ptr()
         o.agent_adj = self.agent_adj.data_ptr() if adj else None
+        if self.obs_gemm is not None:
+            o.obs_gemm = self.obs_gemm.data_ptr()
+            o.obs_gemm_stride = self.obs_gemm.stride(1)
         return o
+
+    def enable_gemm_obs(self):
+        """Have every reset / step / observe also write the GEMM-ready copy of the agent rows
+        (gm_obs_buffers.obs_gemm: 6N+8 columns, the two linearly dependent ones dropped) that the
+        fused DQN's first layer reads with K = 6N+8. Variant 1 only; GM_GEMM_OBS=0 disables."""
+        if self.obs_gemm is not None or self.env_var != 1 or not GEMM_OBS:
+            return self.obs_gemm
+        self.obs_gemm = torch.zeros(self.n_env, self.n_data, 6 * self.n_nodes + 8, device=self.device)
+        self._obsbufs = self._make_obsbufs(self.agent_adjacency)
+        if self._has_state:  # fill it for the current state
+            L.check(L.lib().gm_env_observe(self._h, C.byref(self._obsbufs), self._stream()))
+        return self.obs_gemm
 
     def _stream(self):
         return L.stream_ptr(self.device)
@@ -215,6 +235,7 @@ class Routing:
         m = None if mask is None else mask.to(torch.uint8)
         with L.timed("env_reset"):
             L.check(L.lib().gm_env_reset(self._h, L.ptr(m), C.byref(self._obsbufs), self._stream()))
+        self._has_state = True
         L.check(L.lib().gm_env_topology(self._h, L.ptr(self.nbr), None, None, None, self._stream()))
 
     def reset(self):
@@ -373,6 +394,7 @@ class Routing:
             setattr(st, k, a.ctypes.data)
         torch.cuda.synchronize(self.device)
         L.check(L.lib().gm_env_set_state(self._h, C.byref(st)))
+        self._has_state = True
         self.observe()
         L.check(L.lib().gm_env_topology(self._h, L.ptr(self.nbr), None, None, None, self._stream()))
         torch.cuda.synchronize(self.device)

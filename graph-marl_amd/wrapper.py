@@ -38,6 +38,8 @@ class NetMonWrapper:
         if fused is None:
             fused = FU.fused_ok(netmon)
         self.fused = fused
+        if fused and hasattr(env, "enable_gemm_obs"):
+            env.enable_gemm_obs()  # the fused DQN reads the GEMM-ready env obs copy
         self._dirty = False
         # fused mode: the state and h_prev alternate between two fixed buffer pairs, so a
         # captured 2-step HIP graph (rollout.StreamedRollout.capture) reads and writes the

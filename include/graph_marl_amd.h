@@ -84,6 +84,13 @@ typedef struct {
     float* node_obs;        /* [n_env, N, 4N+8]                                           */
     int32_t* agent_node;    /* [n_env, A] node index of every agent (node-agent matrix)   */
     int8_t* agent_adj;      /* [n_env, A, A] agent adjacency                              */
+    /* env_var 1 only: a GEMM-ready copy of each agent row without its two linearly dependent
+     * columns, N-1 (= sum of the target one-hot - the other N-1 position one-hots) and 2N (edge
+     * flag = sum of the next-hop one-hot): 6N+8 columns, column c = obs column c (c < N-1),
+     * c+1 (c < 2N-1), c+2 (else). The DQN's first layer folds the two weight columns into the
+     * others and runs with K = 6N+8 (640 with the readout at N = 20: whole 32-deep k tiles). */
+    float* obs_gemm;        /* [n_env, A, obs_gemm_stride], 16-byte rows (nullable)        */
+    int64_t obs_gemm_stride;
 } gm_obs_buffers;
 
 /* Per-env statistics of one step (src/env/routing.py:499-508), float64 [n_env, GM_INFO_FIELDS]. */

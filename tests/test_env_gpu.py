@@ -270,6 +270,26 @@ def test_policy_step_fused_matches_split(gm, oracle_mod, mask, ttl):
         np.testing.assert_array_equal(sb["rng_key"][i], o.state()["rng_key"])
 
 
+@pytest.mark.parametrize("n", [20, 30])
+def test_obs_gemm_copy(gm, n):
+    """gm_obs_buffers.obs_gemm (the fused DQN's env operand) == the agent obs without columns N-1
+    and 2N, after reset, steps and a late enable_gemm_obs (filled from the current state)."""
+    B, a = 64, 20
+    net = gm.Network(n, random_topology=True, excluded_seeds=gm.EVAL_SEEDS)
+    env = gm.Routing(net, a, 1, n_env=B, seed=11)
+    keep = [c for c in range(6 * n + 10) if c not in (n - 1, 2 * n)]
+    rng = np.random.RandomState(5)
+    env.reset_()
+    env.step_(torch.as_tensor(rng.randint(0, 4, (B, a)), dtype=torch.int32, device=env.device))
+    g = env.enable_gemm_obs()
+    assert torch.equal(g, env.obs[..., keep])
+    for t in range(60):
+        if t == 30:
+            env.reset_()
+        env.step_(torch.as_tensor(rng.randint(0, 4, (B, a)), dtype=torch.int32, device=env.device))
+        assert torch.equal(env.obs_gemm, env.obs[..., keep]), f"step {t}"
+
+
 def test_large_batch_invariants(gm, oracle_mod):
     """4096 envs (the benchmark size): conservation laws every step, and a sample of
     envs replayed bit-exactly on the oracle."""

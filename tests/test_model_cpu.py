@@ -56,3 +56,36 @@ def test_dense_to_nbr_max_degree():
     wide = M.dense_to_nbr(mask, max_degree=3)
     assert wide.shape == (2, 5, 3)
     assert torch.equal(wide[..., :2], nbr) and (wide[..., 2] == -1).all()
+
+
+def test_fold_env_weight_exact_on_routing_rows():
+    """fused.fold_env_weight: W x == W' x' for agent rows of the routing observation layout
+    (src/env/routing.py:269-315), x' = x without columns N-1 and 2N (gm_obs_buffers.obs_gemm)."""
+    import numpy as np
+    import torch
+
+    _, FU = mods()
+    rng = np.random.RandomState(3)
+    for n in (4, 20, 30):
+        D = 6 * n + 10
+        rows = []
+        for _ in range(64):
+            o = np.zeros(D)
+            now, tgt = rng.randint(n), rng.randint(n)
+            o[now] = 1
+            o[n + tgt] = 1
+            if rng.rand() < 0.5:
+                o[2 * n] = 1
+                o[2 * n + 1 + rng.randint(n)] = 1
+            o[3 * n + 1:3 * n + 4] = rng.rand(3) * 10
+            for k in range(3):
+                blk = 3 * n + 4 + k * (n + 2)
+                o[blk + rng.randint(n)] = 1
+                o[blk + n:blk + n + 2] = rng.rand(2)
+            rows.append(o)
+        x = torch.tensor(np.array(rows))
+        keep = [c for c in range(D) if c not in (n - 1, 2 * n)]
+        w = torch.tensor(rng.standard_normal((16, D)))
+        wf = FU.fold_env_weight(w, n)
+        assert wf.shape == (16, D - 2)
+        torch.testing.assert_close(x @ w.t(), x[:, keep] @ wf.t(), rtol=1e-12, atol=1e-12)
