@@ -60,11 +60,12 @@ def relabel(rows, episode_steps, dqn_g=DQN_G):
     return rows
 
 
-def bench_tag(name, grid, rows):
-    """bench.py timer tag of a relabelled kernel (default rollout: N=20, H=128, M = rows)."""
+def bench_tag(name, grid, rows, env_k=128):
+    """bench.py timer tag of a relabelled kernel (default rollout: N=20, H=128, M = rows; env_k:
+    the env-obs columns of DQN layer 1, 128 with the GEMM-ready obs copy, 130 without)."""
     M = rows
     gemm = {
-        "dqn.enc0(K=512 readout+130)": f"linear:dqn.encoder.linear_layers.0:{M}x512x642",
+        "dqn.enc0(K=512 readout+130)": f"linear:dqn.encoder.linear_layers.0:{M}x512x{512 + env_k}",
         "dqn.enc1+q(K=512, Q head fused)": f"linear:dqn.encoder.linear_layers.1+head:{M}x256x512",
         "netmon.enc1(K=512)": f"linear:netmon.encode.linear_layers.1:{M}x256x512",
         "netmon.enc2(K=256)": f"linear:netmon.encode.linear_layers.2:{M}x128x256",
@@ -94,6 +95,8 @@ def main():
     ap.add_argument("--unfused-head", action="store_true", help="profiles taken before gm_gemm_x3_head")
     ap.add_argument("--json", help="write per-launch HBM bytes keyed by bench.py timer tags (pmc_traffic.json)")
     ap.add_argument("--rows", type=int, default=81920, help="GEMM rows of the profiled rollout (n_env * N)")
+    ap.add_argument("--env-k", type=int, default=128,
+                    help="env-obs columns of DQN layer 1 (128: GEMM-ready obs copy, 130: GM_GEMM_OBS=0 profiles)")
     a = ap.parse_args()
     dqn_g = DQN_G3 if a.unfused_head else DQN_G
     dur = defaultdict(list)
@@ -129,7 +132,7 @@ def main():
 
         out = {}
         for (n, g, w), p in pmc.items():
-            tag = bench_tag(n, g, a.rows)
+            tag = bench_tag(n, g, a.rows, a.env_k)
             if tag and "FETCH_SIZE" in p and "WRITE_SIZE" in p and tag not in out:
                 # KiB per launch; FETCH_SIZE doubled (gfx950 counts half of a 16-B/lane stream)
                 out[tag] = {"fetch_bytes": int(2 * p["FETCH_SIZE"] * 1024), "write_bytes": int(p["WRITE_SIZE"] * 1024),
