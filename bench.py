@@ -65,6 +65,9 @@ def parse():
     p.add_argument("--train-seq", type=int, default=8, help="sequence length of an update")
     p.add_argument("--train-autograd", action="store_true",
                    help="training leg on the per-step autograd path (train.dqn_update) instead of train_seq")
+    p.add_argument("--no-extras", action="store_true",
+                   help="skip the other BASELINE configurations (K=3, configs 2/3, config 5 SL) timed after the headline")
+    p.add_argument("--extra-steps", type=int, default=100, help="timed vector steps of each extra rollout configuration")
     p.add_argument("--cpu-envs", type=int, default=1024)
     p.add_argument("--cpu-steps", type=int, default=50, help="one full episode (includes its reset)")
     return p.parse_args()
@@ -123,17 +126,23 @@ def kernel_cost(tag, n_env, N, A, E, x3=False):
         rows, H = (int(v) for v in tag.split(":")[1].split("x"))
         return "hbm", rows * H * 4 * (4 + 1 + 2)  # gates, c in; h, c out
     if kind == "env_step":
-        # compact state (78A + 22E + 12N) + materialised fp32 obs
+        # SURVEY §8(d) B_env: compact state (78A + 22E + 12N) + materialised fp32 obs (19 900 B
+        # at N = A = 20), plus the ε-greedy prologue's Q rows, actions and RNG words per agent
+        # (gm_env_policy_step). The GEMM-ready duplicate of the agent rows is NOT algorithmic
+        # (env_step_overhead_bytes)
         b_state = 78 * A + 22 * E + 12 * N
         b_obs = 4 * A * (6 * N + 10) + 4 * N * (4 * N + 8)
-        # with the ε-greedy prologue (gm_env_policy_step): + Q rows, actions, RNG words per agent
         b_pol = A * (16 + 4 + 12) if _fused_policy_step() else 0
-        # the GEMM-ready copy of the agent rows the fused DQN reads (gm_obs_buffers.obs_gemm)
-        b_gemm = 4 * A * (6 * N + 8) if _gemm_obs() else 0
-        return "hbm", float(n_env * (b_state + b_obs + b_pol + b_gemm))
+        return "hbm", float(n_env * (b_state + b_obs + b_pol))
     if kind == "egreedy":
         return "hbm", float(n_env * A * (16 + 4 + 12))
     return None, None
+
+
+def env_step_overhead_bytes(n_env, N, A):
+    """Bytes k_env_step writes beyond SURVEY §8(d)'s B_env: the GEMM-ready copy of the agent
+    rows (gm_obs_buffers.obs_gemm) that DQN layer 1 reads at K = 512 + 6N + 8."""
+    return float(n_env * 4 * A * (6 * N + 8)) if _gemm_obs() else 0.0
 
 
 def _fused_policy_step():
@@ -146,6 +155,70 @@ _GEMM_OBS_ON = [False]  # set from the timed rollout's env (Routing.obs_gemm all
 
 def _gemm_obs():
     return _GEMM_OBS_ON[0]
+
+
+def sl_gemm_flops(N, B, L, K, H=128, enc=(512, 256)):
+    """f16 MFMA FLOPs one config-5 SL iteration issues on its split-f16 GEMMs (3 f16 products per
+    fp32 multiply-add; forward, input gradient and weight gradient of each GEMM): per step and node
+    row the encoder layers 1..2 (enc[0]->enc[1]->H; layer 0 is the routing gather, no GEMM), the
+    LSTM obs cell [x | h] (2H -> 4H) and K update cells (2H -> 4H). The three narrow output heads
+    (exact f32) are left out."""
+    macs = enc[0] * enc[1] + enc[1] * H + (1 + K) * 2 * H * 4 * H
+    return 3.0 * 2.0 * 3.0 * macs * N * B * L
+
+
+def measure_extras(args, gm, M, RO, timed_region, dev, N, A, x3):
+    """The other BASELINE.json configurations, timed in the same process after the headline:
+    NetMon with the CLI default --netmon-iterations 3 (src/main.py:153-157), config 3 (fixed
+    20-node topology, seed 476), config 2 (no NetMon, fixed topology, 1024 envs) and config 5
+    (src/sl.py at N = 100, batch 8192, sequence length 8, NetMon K = 1)."""
+    out = {}
+    steps = args.extra_steps
+
+    def rollout(name, n_env, K, random_topology, netmon_on, desc):
+        try:
+            net = gm.Network(N, random_topology=random_topology, excluded_seeds=gm.EVAL_SEEDS, device=dev.index)
+            torch.manual_seed(0)
+            nm = M.NetMon(4 * N + 8, 128, [512, 256], K).to(dev) if netmon_on else None
+            dq = M.DQN(6 * N + 10 + (nm.get_out_features() if nm is not None else 0), [512, 256], 4).to(dev)
+            ro = RO.StreamedRollout(net, A, n_env, nm, dq, groups=args.groups, seed=0, epsilon=args.epsilon,
+                                    episode_steps=args.episode_steps, device=dev.index)
+            el, _ = timed_region(5, steps, False, ro=ro)
+            out[name] = {"value": round(n_env * steps / el, 1), "unit": "env-steps/s",
+                         "ms_per_step": round(1e3 * el / steps, 4), "steps": steps, "n_env": n_env,
+                         "resets_in_window": -(-steps // args.episode_steps), "workload": desc}
+            del ro, nm, dq
+        except Exception as ex:  # an extra configuration must never break the headline line
+            if os.environ.get("GM_BENCH_RAISE") == "1":
+                raise
+            out[name] = {"value": None, "error": repr(ex)[:300]}
+        torch.cuda.empty_cache()
+
+    rollout("netmon_k3", args.n_env, 3, True, True,
+            f"headline with the CLI default --netmon-iterations 3: random {N}-node topologies, NetMon K=3")
+    rollout("config3_fixed_topology", args.n_env, 1, False, True,
+            f"config 3: --random-topology 0 (fixed {N}-node graph, seed 476), NetMon K=1")
+    rollout("config2_no_netmon", 1024, 1, False, False,
+            f"config 2: --random-topology 0, no NetMon, DQN 512,256 on the env obs, 1024 envs")
+    try:
+        SL = importlib.import_module("graph-marl_amd.sl")
+        n, b, sl_len, k = 100, 8192, 8, 1
+        line = SL.main(["--bench", "--n-nodes", str(n), "--batch-size", str(b), "--sequence-length", str(sl_len),
+                        "--netmon-iterations", str(k), "--iterations", "3", "--warmup", "2"], quiet=True)
+        sec = line["ms_per_iteration"] * 1e-3
+        fl = sl_gemm_flops(n, b, sl_len, k) if x3 else None
+        line["roofline"] = None if fl is None else {
+            "kernel": "all GEMMs of one iteration (fwd + input grad + weight grad), iteration wall time",
+            "bound": "mfma", "achieved": round(fl / sec / 1e12, 2), "peak": F16_MFMA_PEAK_TFS,
+            "unit": "TFLOP/s (f16 MFMA, 3 per fp32 multiply-add)", "frac": round(fl / sec / 1e12 / F16_MFMA_PEAK_TFS, 4),
+            "traffic": None}
+        out["config5_sl"] = line
+    except Exception as ex:
+        if os.environ.get("GM_BENCH_RAISE") == "1":
+            raise
+        out["config5_sl"] = {"value": None, "error": repr(ex)[:300]}
+    torch.cuda.empty_cache()
+    return out
 
 
 def measure_train(args, gm, M, W, P, net, netmon, dqn, dev, world, rank):
@@ -380,6 +453,15 @@ def main():
                              "frac": round(ach / HBM_PEAK_GBS, 4), "algorithmic_bytes": units, "traffic": tb,
                              "traffic_note": None if tb is None else f"HBM bytes per launch (rocprofv3 PMC, {src})",
                              "avg_us": round(kv["avg_us"], 2)}
+            if tag == "env_step":
+                ov = env_step_overhead_bytes(B, N, A)
+                roof_hbm[tag]["overhead_bytes"] = ov
+                roof_hbm[tag]["overhead_note"] = ("GEMM-ready duplicate of the agent rows (obs_gemm), written by the "
+                                                  "same launch, excluded from achieved/frac")
+
+    extras = None
+    if world == 1 and not args.no_extras and netmon is not None:
+        extras = measure_extras(args, gm, M, RO, timed_region, dev, N, A, x3)
 
     train = None
     if not args.no_train and netmon is not None:
@@ -429,6 +511,7 @@ def main():
                        "resets_in_window": resets},
             "host_enqueue_ms_per_step": round(host_ms, 4),
             "roofline": roof, "roofline_hbm": roof_hbm or None, "cpu_baseline": cpu, "f32_exact_gemms": f32cmp, "rollout_train": train,
+            "other_configs": extras,
             "kernels": kernels,
         }
         print(json.dumps(line))

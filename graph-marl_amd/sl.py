@@ -226,7 +226,7 @@ def test(args, model, data, batch_size, sequence_length):
     return res
 
 
-def main(argv=None):
+def main(argv=None, quiet=False):
     args = build_parser().parse_args(argv)
     args.test_sequence_lengths = dim_str_to_list(args.test_sequence_lengths)
     L.require_gpu()
@@ -246,7 +246,8 @@ def main(argv=None):
     t0 = time.time()
     train = build_dataset(N, args.n_packets, n_train, args.seed)
     torch.cuda.synchronize()
-    print(f"train dataset: {len(train)} graphs of {N} nodes in {time.time() - t0:.2f} s", flush=True)
+    if not quiet:
+        print(f"train dataset: {len(train)} graphs of {N} nodes in {time.time() - t0:.2f} s", flush=True)
 
     if args.bench:
         # config 5: every graph of the batch once per iteration (fixed batch = the dataset)
@@ -266,7 +267,8 @@ def main(argv=None):
                 "config": {"n_nodes": N, "batch": args.batch_size, "seq_len": args.sequence_length,
                            "netmon_iterations": args.netmon_iterations, "netmon_dim": args.netmon_dim,
                            "encoder": args.netmon_encoder_dim, "rnn": args.netmon_rnn_type}}
-        print(json.dumps(line))
+        if not quiet:
+            print(json.dumps(line))
         return line
 
     seeds_val = gm.build_seed_list(N, 476, args.num_samples_test, gm.EVAL_SEEDS)

@@ -23,6 +23,8 @@ import textwrap
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, HERE)
+import detparams  # noqa: E402
 
 
 def write_stubs(root):
@@ -516,32 +518,72 @@ def gen_models(out, Network, Routing, EVAL_SEEDS, DGN, DQNR, CommNet):
     print("models done", flush=True)
 
 
-def gen_train(out, Network, Routing, EVAL_SEEDS, NetMon, DQN, interpolate_model, aux_coeff=0.0, MLP=None):
+def _store(d, key, arr, compact, seed):
+    """Full array, or (compact, > 8192 elements) values at sample_index + row and column sums."""
+    arr = np.asarray(arr)
+    if not compact or arr.size <= 8192:
+        d[key] = arr.copy()
+        return
+    import zlib
+
+    idx = detparams.sample_index(arr.size, 4096, (seed + zlib.crc32(key.encode())) & 0x7FFFFFFF)
+    d[key + "__idx"] = idx
+    d[key + "__val"] = arr.reshape(-1)[idx].copy()
+    d[key + "__shape"] = np.array(arr.shape, np.int64)
+    a64 = arr.astype(np.float64)
+    d[key + "__rowsum"] = a64.reshape(arr.shape[0], -1).sum(1)
+    if arr.ndim == 2:
+        d[key + "__colsum"] = a64.sum(0)
+
+
+def gen_train(out, Network, Routing, EVAL_SEEDS, NetMon, DQN, interpolate_model, aux_coeff=0.0, MLP=None,
+              rnn_type="lstm", agg="sum", K=1, H=32, enc=(64, 48), dqn_hidden=(64, 32), B=3, L=3, compact=False,
+              det_seed=0):
     """One DQN+NetMon update exactly as src/main.py:832-1022 performs it (sequence replay);
-    aux_coeff > 0 adds the NetMon aux head and loss (src/main.py:586-594, 868-875, 996-1000)."""
+    aux_coeff > 0 adds the NetMon aux head and loss (src/main.py:586-594, 868-875, 996-1000).
+    rnn_type / agg / K / H / enc / dqn_hidden select the architecture (src/model.py:451-631,
+    src/layernormlstm.py). compact (production sizes): parameters, target perturbation and the
+    initial NetMon state come from detparams (regenerated by the tests, not stored); gradients and
+    updated parameters above 8192 elements are stored at 4096 sampled positions plus their row and
+    column sums (_store)."""
     import torch
     import torch.nn.functional as F
     import torch.optim as optim
 
     d = {}
-    n, a, B, L = 20, 20, 3, 3
+    n, a = 20, 20
     aux_l = [] if aux_coeff > 0 else None
     node_obs, node_adj, node_agent, agent_obs = collect_graph_inputs(Network, Routing, EVAL_SEEDS, n, a, B, L + 1, 200,
                                                                      aux=aux_l)
     rng = np.random.RandomState(5)
     torch.manual_seed(3)
-    netmon = NetMon(node_obs.shape[-1], 32, [64, 48], 1, F.leaky_relu, rnn_type="lstm",
-                    rnn_carryover=True, agg_type="sum", output_neighbor_hidden=True)
+    netmon = NetMon(node_obs.shape[-1], H, list(enc), K, F.leaky_relu, rnn_type=rnn_type,
+                    rnn_carryover=True, agg_type=agg, output_neighbor_hidden=True)
     obs_dim = agent_obs.shape[-1] + netmon.get_out_features()
-    model = DQN(obs_dim, [64, 32], 4, F.leaky_relu)
+    model = DQN(obs_dim, list(dqn_hidden), 4, F.leaky_relu)
+    d["arch"] = np.array(f"{rnn_type}|{agg}|{K}|{H}|{enc[0]},{enc[1]}|{dqn_hidden[0]},{dqn_hidden[1]}")
+    if compact:
+        with torch.no_grad():
+            for prefix, mod in (("netmon.", netmon), ("model.", model)):
+                sd = mod.state_dict()
+                vals = detparams.det_state_dict(det_seed, {prefix + k: v.shape for k, v in sd.items()})
+                mod.load_state_dict({k: torch.tensor(vals[prefix + k]) for k in sd})
+        d["compact"] = np.int64(1)
+        d["det_seed"] = np.int64(det_seed)
     model_tar = copy.deepcopy(model)
     # perturb target so that it differs from the online model
     with torch.no_grad():
-        for p in model_tar.parameters():
-            p.add_(0.01 * torch.randn_like(p))
-    sd_to_npz("netmon_", netmon.state_dict(), d)
-    sd_to_npz("model_", model.state_dict(), d)
-    sd_to_npz("target_", model_tar.state_dict(), d)
+        if compact:
+            sd = model_tar.state_dict()
+            model_tar.load_state_dict({k: torch.tensor(detparams.det_perturb(det_seed, "target." + k, v.numpy()))
+                                       for k, v in sd.items()})
+        else:
+            for p in model_tar.parameters():
+                p.add_(0.01 * torch.randn_like(p))
+    if not compact:
+        sd_to_npz("netmon_", netmon.state_dict(), d)
+        sd_to_npz("model_", model.state_dict(), d)
+        sd_to_npz("target_", model_tar.state_dict(), d)
     aux_model = None
     if aux_coeff > 0:
         S = netmon.get_state_size()
@@ -550,14 +592,19 @@ def gen_train(out, Network, Routing, EVAL_SEEDS, NetMon, DQN, interpolate_model,
         node_aux = np.stack(aux_l).reshape(L + 1, B, n, n)
         d["node_aux"] = node_aux
         d["aux_coeff"] = np.float64(aux_coeff)
-    node_state0 = (0.1 * rng.standard_normal((B, n, netmon.get_state_size()))).astype(np.float32)
+    if compact:
+        node_state0 = detparams.det_state(det_seed, (B, n, netmon.get_state_size()))
+    else:
+        node_state0 = (0.1 * rng.standard_normal((B, n, netmon.get_state_size()))).astype(np.float32)
     actions = rng.randint(4, size=(L, B, a))
     reward = rng.choice(np.array([0.0, -0.2, 10.0, -10.0, 9.8], dtype=np.float32), size=(L, B, a)).astype(np.float32)
     done = rng.rand(L, B, a) < 0.1
     episode_done = rng.rand(L, B) < 0.3
-    d.update(node_obs=node_obs, node_adj=node_adj, node_agent=node_agent, agent_obs=agent_obs,
-             node_state0=node_state0, actions=actions, reward=reward, done=done.astype(np.int8),
+    d.update(node_obs=node_obs, node_adj=node_adj.astype(np.int8), node_agent=node_agent.astype(np.int8),
+             agent_obs=agent_obs, actions=actions.astype(np.int8), reward=reward, done=done.astype(np.int8),
              episode_done=episode_done.astype(np.int8))
+    if not compact:
+        d["node_state0"] = node_state0
     gamma, lr, tau = 0.9, 1e-3, 0.01
     d["gamma"], d["lr"], d["tau"] = np.float64(gamma), np.float64(lr), np.float64(tau)
     parameters = list(model.parameters()) + list(netmon.parameters())
@@ -605,18 +652,21 @@ def gen_train(out, Network, Routing, EVAL_SEEDS, NetMon, DQN, interpolate_model,
     if aux_model is not None:
         names += [f"aux_{k}" for k, _ in aux_model.named_parameters()]
     for nm_, p in zip(names, parameters):
-        d["grad_raw_" + nm_] = p.grad.detach().numpy().copy()
+        _store(d, "grad_raw_" + nm_, p.grad.detach().numpy(), compact, det_seed)
     torch.nn.utils.clip_grad_value_(parameters, 0.5)
-    torch.nn.utils.clip_grad_norm_(parameters, 1.0)
+    total_norm = torch.nn.utils.clip_grad_norm_(parameters, 1.0)
+    d["clip_total_norm"] = np.float64(total_norm.item())
     for nm_, p in zip(names, parameters):
-        d["grad_clip_" + nm_] = p.grad.detach().numpy().copy()
+        _store(d, "grad_clip_" + nm_, p.grad.detach().numpy(), compact, det_seed)
     optimizer.step()
     for nm_, p in zip(names, parameters):
-        d["param_after_" + nm_] = p.detach().numpy().copy()
+        _store(d, "param_after_" + nm_, p.detach().numpy(), compact, det_seed)
     interpolate_model(model, model_tar, tau, model_tar)
-    sd_to_npz("target_after_", model_tar.state_dict(), d)
+    for k, v in model_tar.state_dict().items():
+        _store(d, "target_after_" + k, v.detach().numpy(), compact, det_seed)
     d["param_names"] = np.array(names)
     np.savez_compressed(out, **d)
+    print(os.path.basename(out), "done", flush=True)
 
 
 # ---------------------------------------------------------------------------
@@ -981,6 +1031,17 @@ def main():
     if only is None or "train_aux" in only:
         gen_train(os.path.join(HERE, "train_aux.npz"), Network, Routing, EVAL_SEEDS, NetMon, DQN, interpolate_model,
                   aux_coeff=0.3, MLP=MLP)
+    if only is None or "train_lnlstm" in only:
+        gen_train(os.path.join(HERE, "train_lnlstm.npz"), Network, Routing, EVAL_SEEDS, NetMon, DQN,
+                  interpolate_model, rnn_type="lnlstm", agg="mean", K=2, B=4)
+    if only is None or "train_gru" in only:
+        gen_train(os.path.join(HERE, "train_gru.npz"), Network, Routing, EVAL_SEEDS, NetMon, DQN,
+                  interpolate_model, rnn_type="gru", agg="sum", K=2, B=4)
+    if only is None or "train_big" in only:
+        # the CLI-default architecture at row counts where every training kernel runs its HIP form
+        # (256 graphs x 20 nodes = 5120 rows per step, 20480 over the 4 steps)
+        gen_train(os.path.join(HERE, "train_big.npz"), Network, Routing, EVAL_SEEDS, NetMon, DQN, interpolate_model,
+                  H=128, enc=(512, 256), dqn_hidden=(512, 256), B=256, L=4, compact=True, det_seed=11)
     if only is None or "checkpoint" in only:
         gen_checkpoint(os.path.join(HERE, "ref_checkpoint.pt"), os.path.join(HERE, "ref_checkpoint.npz"), args.ref,
                        Network, Routing, EVAL_SEEDS, NetMon, DQN, get_state_dict)

@@ -1,8 +1,13 @@
-"""Full-size, long-horizon parity of the benched rollout (bench.py's default workload).
+"""Full-size, long-horizon parity of the benched rollout (bench.py's default workload) and of
+config 4's other node counts.
 
 StreamedRollout exactly as bench.py runs it: 4096 envs in 2 stream groups, N = 20 random
 topologies (EVAL_SEEDS excluded), A = 20 packets, NetMon K = 1 (lstm, sum) + DQN 512,256,
 ε = 0.5, 50-step episodes, 120 vector steps (two topology resets + NetMon start-ups inside).
+Config 4 (random 10-50-node topologies) at N = 10, 30, 40, 50: 512 envs in 2 groups, 30-step
+episodes, 70 steps (two resets) — this covers the N-dependent rows per block of the routing
+encoder, DQN layer 1 on the folded GEMM-ready obs (K = 512 + 6N + 8, not a whole number of k
+tiles off N = 20), the aggregate and the readout at those sizes.
 Eight envs spread over both groups are shadowed every step by
   * the C oracle env (oracle/gm_oracle.c) fed the GPU's Q-values, which must take the same
     ε-greedy actions and give bit-identical rewards, done flags, agent and node observations
@@ -21,12 +26,13 @@ import torch
 
 pytestmark = pytest.mark.gpu
 
-N, A, B, G, EP, STEPS, EPS = 20, 20, 4096, 2, 50, 120, 0.5
-SAMPLE = [0, 1, 777, 2047, 2048, 2049, 3333, 4095]
+A, G, EPS = 20, 2, 0.5
 TOL = 1e-5
+# (N, envs, episode steps, vector steps)
+CASES = [(20, 4096, 50, 120), (10, 512, 30, 70), (30, 512, 30, 70), (40, 512, 30, 70), (50, 512, 30, 70)]
 
 
-def adjacency(topo):
+def adjacency(topo, N):
     m = np.eye(N, dtype=np.int8)
     for i, row in enumerate(topo["nbr"]):
         for j in row:
@@ -35,9 +41,13 @@ def adjacency(topo):
     return m
 
 
+@pytest.mark.parametrize("case", CASES, ids=[f"N{c[0]}" for c in CASES])
 @pytest.mark.parametrize("form", ["x3", "f32"])
-def test_benched_rollout_long_horizon(form, monkeypatch, oracle_mod):
+def test_benched_rollout_long_horizon(form, case, monkeypatch, oracle_mod):
     import netmon_ref
+
+    N, B, EP, STEPS = case
+    SAMPLE = sorted({0, 1, B // 5, B // 2 - 1, B // 2, B // 2 + 1, (4 * B) // 5, B - 1})
 
     gm = importlib.import_module("graph-marl_amd")
     M = importlib.import_module("graph-marl_amd.model")
@@ -94,7 +104,7 @@ def test_benched_rollout_long_horizon(form, monkeypatch, oracle_mod):
         ob = o.observe()
         assert (v["obs"] == ob["obs"]).all(), f"step {t} env {e}: agent obs"
         assert (v["node_obs"] == ob["node_obs"]).all(), f"step {t} env {e}: node obs"
-        adj = adjacency(o.topology())
+        adj = adjacency(o.topology(), N)
         assert (v["adj"] == adj).all(), f"step {t} env {e}: I+A adjacency"
         out, st = netmon_ref.netmon_forward(Wn, ob["node_obs"][None], adj[None], state64.get(e), "lstm", "sum", 1)
         state64[e] = st
@@ -132,4 +142,4 @@ def test_benched_rollout_long_horizon(form, monkeypatch, oracle_mod):
         resets += t % EP == 0
     assert resets == STEPS // EP >= 2
     gm._lib.check_range()
-    print(f"form {form}: worst |err| over {STEPS} steps x {len(SAMPLE)} envs: {worst}")
+    print(f"N={N} form {form}: worst |err| over {STEPS} steps x {len(SAMPLE)} envs: {worst}")

@@ -142,25 +142,28 @@ def test_oracle_bench_driver_runs(oracle_mod):
     assert (obs[..., :20].sum(-1) == 1).all() and (obs[..., 20:40].sum(-1) == 1).all()
 
 
-def test_train_golden_forward_matches_restatement():
-    """The golden DQN+NetMon update's Q / Q-target / loss follow from its saved
-    weights through the fp64 restatement (pins the fixture itself)."""
-    g = np.load(f"{R.GOLDEN}/train.npz")
-    Wn = netmon_ref.weights_from_npz(g, "netmon_")
-    Wm = {k[6:]: g[k].astype(np.float64) for k in g.files if k.startswith("model_")}
-    Wt = {k[7:]: g[k].astype(np.float64) for k in g.files if k.startswith("target_") and "after" not in k}
-    state, tot, L = g["node_state0"].astype(np.float64), 0.0, g["actions"].shape[0]
+@pytest.mark.parametrize("name", ["train.npz", "train_big.npz", "train_lnlstm.npz", "train_gru.npz"])
+def test_train_golden_forward_matches_restatement(name):
+    """The golden DQN+NetMon updates' Q / Q-target / loss follow from their weights (stored, or for
+    the compact production-size golden regenerated by tests/golden/detparams.py) through the fp64
+    restatement — pins the fixtures and the detparams regeneration itself."""
+    import golden_update as GU
+
+    g = np.load(f"{R.GOLDEN}/{name}")
+    Wn, Wm, Wt, state = GU.weights_np(g)
+    rnn, agg, K, H, enc, dq = GU.arch(g)
+    tot, L = 0.0, g["actions"].shape[0]
     gamma = float(g["gamma"])
     for t in range(L):
-        out, ns = netmon_ref.netmon_forward(Wn, g["node_obs"][t], g["node_adj"][t], state, "lstm", "sum", 1)
+        out, ns = netmon_ref.netmon_forward(Wn, g["node_obs"][t], g["node_adj"][t], state, rnn, agg, K)
         obs = np.concatenate([g["agent_obs"][t], netmon_ref.to_network_obs(out, g["node_agent"][t])], -1)
         q = netmon_ref.dqn_forward(Wm, obs)
-        out2, _ = netmon_ref.netmon_forward(Wn, g["node_obs"][t + 1], g["node_adj"][t + 1], ns, "lstm", "sum", 1)
+        out2, _ = netmon_ref.netmon_forward(Wn, g["node_obs"][t + 1], g["node_adj"][t + 1], ns, rnn, agg, K)
         nobs = np.concatenate([g["agent_obs"][t + 1], netmon_ref.to_network_obs(out2, g["node_agent"][t + 1])], -1)
         nq = netmon_ref.dqn_forward(Wt, nobs).max(-1)
         qt = q.copy()
         tgt = g["reward"][t] + (1 - g["done"][t]) * gamma * nq
-        np.put_along_axis(qt, g["actions"][t][..., None], tgt[..., None], -1)
+        np.put_along_axis(qt, g["actions"][t][..., None].astype(np.int64), tgt[..., None], -1)
         np.testing.assert_allclose(q, g[f"q_{t}"], atol=1e-5, rtol=0)
         np.testing.assert_allclose(qt, g[f"qtarget_{t}"], atol=1e-5, rtol=0)
         tot += ((q - qt) ** 2).mean() / L

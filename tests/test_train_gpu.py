@@ -8,6 +8,7 @@ import pytest
 import torch
 
 import golden_replay as R
+import golden_update as GU
 
 pytestmark = pytest.mark.gpu
 
@@ -18,31 +19,11 @@ def mods():
 
 
 def _sd(g, prefix):
-    return {k[len(prefix):]: torch.as_tensor(g[k]) for k in g.files
-            if k.startswith(prefix) and not k.startswith(prefix + "after_") and k != "aux_coeff"}
+    return GU._sd(g, prefix)
 
 
-@pytest.mark.parametrize("name", ["train.npz", "train_aux.npz"])
-def test_update_matches_reference_golden(name):
-    """train_aux.npz: the same update with --aux-loss-coeff 0.3 (NetMon aux MLP on the new NetMon
-    state, MSE against get_node_aux, src/main.py:586-594, 868-875, 996-1000)."""
-    M, T, RB = mods()
-    g = np.load(f"{R.GOLDEN}/{name}")
+def golden_batches(g, M, RB, dev, state0):
     aux = "aux_coeff" in g.files
-    dev = torch.device("cuda")
-    nd = g["node_obs"].shape[-1]
-    netmon = M.NetMon(nd, 32, [64, 48], 1).to(dev)
-    netmon.load_state_dict(_sd(g, "netmon_"))
-    obs_dim = g["agent_obs"].shape[-1] + netmon.get_out_features()
-    model = M.DQN(obs_dim, [64, 32], 4).to(dev)
-    model.load_state_dict(_sd(g, "model_"))
-    target = M.DQN(obs_dim, [64, 32], 4).to(dev)
-    target.load_state_dict(_sd(g, "target_"))
-    aux_model = None
-    if aux:
-        S = netmon.get_state_size()
-        aux_model = M.MLP(S, [S, g["node_aux"].shape[-1]], activation_on_output=False).to(dev)
-        aux_model.load_state_dict(_sd(g, "aux_"))
     L = g["actions"].shape[0]
     f = lambda a: torch.as_tensor(a, device=dev)  # noqa: E731
     batches = []
@@ -50,9 +31,36 @@ def test_update_matches_reference_golden(name):
         batches.append(RB.TransitionBatch(
             None, f(g["agent_obs"][t]), f(g["actions"][t]).long(), f(g["reward"][t]), f(g["agent_obs"][t + 1]),
             f(g["done"][t]).bool(), f(g["episode_done"][t]).bool(), f(g["node_obs"][t]),
-            M.dense_to_nbr(f(g["node_adj"][t])), f(g["node_state0"]), M.node_agent_to_index(f(g["node_agent"][t])),
-            f(g["node_obs"][t + 1]), M.node_agent_to_index(f(g["node_agent"][t + 1])),
+            M.dense_to_nbr(f(g["node_adj"][t]).float()), state0, M.node_agent_to_index(f(g["node_agent"][t]).float()),
+            f(g["node_obs"][t + 1]), M.node_agent_to_index(f(g["node_agent"][t + 1]).float()),
             node_aux=f(g["node_aux"][t]) if aux else None))
+    return batches
+
+
+# train_big: the CLI-default architecture (H 128, encoder 512,256, DQN 512,256) with 256 graphs per
+# step (5120 node / agent rows), where every training kernel runs its HIP form (split-K weight
+# gradients, fused leaky backward, split-f16 input gradients); train_lnlstm / train_gru: the
+# LayerNorm-LSTM (mean aggregation, K = 2) and GRU (K = 2) cells under grad (src/layernormlstm.py,
+# nn.GRUCell via src/model.py:387-393)
+GOLDENS = ["train.npz", "train_aux.npz", "train_big.npz", "train_lnlstm.npz", "train_gru.npz"]
+
+
+@pytest.mark.parametrize("name", GOLDENS)
+def test_update_matches_reference_golden(name):
+    """train_aux.npz: the same update with --aux-loss-coeff 0.3 (NetMon aux MLP on the new NetMon
+    state, MSE against get_node_aux, src/main.py:586-594, 868-875, 996-1000)."""
+    M, T, RB = mods()
+    g = np.load(f"{R.GOLDEN}/{name}")
+    aux = "aux_coeff" in g.files
+    dev = torch.device("cuda")
+    netmon, model, target, state0 = GU.build(g, M, dev)
+    aux_model = None
+    if aux:
+        S = netmon.get_state_size()
+        aux_model = M.MLP(S, [S, g["node_aux"].shape[-1]], activation_on_output=False).to(dev)
+        aux_model.load_state_dict(_sd(g, "aux_"))
+    L = g["actions"].shape[0]
+    batches = golden_batches(g, M, RB, dev, state0)
     params = list(model.parameters()) + list(netmon.parameters())
     names = [f"model_{k}" for k, _ in model.named_parameters()] + [f"netmon_{k}" for k, _ in
                                                                     netmon.named_parameters()]
@@ -75,18 +83,25 @@ def test_update_matches_reference_golden(name):
     np.testing.assert_allclose(loss.item(), g["loss"].item(), rtol=1e-5, atol=1e-6)
     opt.zero_grad()
     loss.backward()
+    check_update(g, names, params, opt, model, target, T)
+
+
+def check_update(g, names, params, opt, model, target, T):
+    """Raw and clipped gradients, the AdamW step and the soft target update vs the golden."""
     for n, p in zip(names, params):
-        np.testing.assert_allclose(p.grad.cpu().numpy(), g["grad_raw_" + n], atol=1e-5, rtol=1e-4, err_msg=n)
+        GU.check(g, "grad_raw_" + n, p.grad, 1e-5, 1e-4)
     torch.nn.utils.clip_grad_value_(params, 0.5)
-    torch.nn.utils.clip_grad_norm_(params, 1.0)
+    norm = torch.nn.utils.clip_grad_norm_(params, 1.0)
+    if "clip_total_norm" in g.files:
+        np.testing.assert_allclose(norm.item(), float(g["clip_total_norm"]), rtol=1e-4)
     for n, p in zip(names, params):
-        np.testing.assert_allclose(p.grad.cpu().numpy(), g["grad_clip_" + n], atol=1e-5, rtol=1e-4, err_msg=n)
+        GU.check(g, "grad_clip_" + n, p.grad, 1e-5, 1e-4)
     opt.step()
     for n, p in zip(names, params):
-        np.testing.assert_allclose(p.detach().cpu().numpy(), g["param_after_" + n], atol=1e-6, rtol=0, err_msg=n)
+        GU.check(g, "param_after_" + n, p, 1e-6, 0)
     T.interpolate_model(model, target, float(g["tau"]), target)
     for k, v in target.state_dict().items():
-        np.testing.assert_allclose(v.cpu().numpy(), g["target_after_" + k], atol=1e-6, rtol=0, err_msg=k)
+        GU.check(g, "target_after_" + k, v, 1e-6, 0)
 
 
 def test_replay_sequences_and_full_update_on_env_data():

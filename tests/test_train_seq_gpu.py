@@ -200,7 +200,7 @@ def test_lstm_cell_bwd_vs_autograd(mean, H):
     assert mx.item() == dg.abs().max().item()
 
 
-def _golden_seq(g, dev, netmon, RBm):
+def _golden_seq(g, dev, netmon, RBm, state0=None):
     """SeqBatch of the reference's golden update (L steps of B sequences; next obs = obs of t + 1)."""
     M, T, S, FU, L = mods()
     f = lambda a: torch.as_tensor(a, device=dev)  # noqa: E731
@@ -208,8 +208,8 @@ def _golden_seq(g, dev, netmon, RBm):
     od = g["agent_obs"].shape[-1]
     odp = (od + 3) // 4 * 4
     obs = F.pad(f(g["agent_obs"]), (0, odp - od))  # [L + 1, B, A, odp]
-    nbr = torch.stack([M.dense_to_nbr(f(g["node_adj"][t])) for t in range(Lq + 1)])
-    an = torch.stack([M.node_agent_to_index(f(g["node_agent"][t])) for t in range(Lq + 1)])
+    nbr = torch.stack([M.dense_to_nbr(f(g["node_adj"][t]).float()) for t in range(Lq + 1)])
+    an = torch.stack([M.node_agent_to_index(f(g["node_agent"][t]).float()) for t in range(Lq + 1)])
     node_obs = f(g["node_obs"])
 
     def next_fields(t, rows):
@@ -218,28 +218,25 @@ def _golden_seq(g, dev, netmon, RBm):
 
     return S.SeqBatch(obs[:Lq].contiguous(), od, f(g["actions"]).long(), f(g["reward"]), f(g["done"]).bool(),
                       f(g["episode_done"]).bool(), node_obs[:Lq].contiguous(), nbr[:Lq].contiguous(),
-                      an[:Lq].contiguous(), f(g["node_state0"]), next_fields)
+                      an[:Lq].contiguous(), f(g["node_state0"]) if state0 is None else state0, next_fields)
 
 
-def test_seq_update_matches_reference_golden():
-    """The sequence-batched update on the reference's golden update (train.npz: NetMon H = 32,
-    encoder [64, 48], DQN [64, 32], L = 3 with episode ends): q, targets, loss, raw and clipped
-    gradients, AdamW step, soft target update at the autograd path's tolerances."""
+@pytest.mark.parametrize("name", ["train.npz", "train_big.npz"])
+def test_seq_update_matches_reference_golden(name):
+    """The sequence-batched update on the reference's golden updates at the autograd path's
+    tolerances: q, targets, loss, raw and clipped gradients, AdamW step, soft target update.
+    train.npz: NetMon H = 32, encoder [64, 48], DQN [64, 32], L = 3 with episode ends;
+    train_big.npz: the CLI-default sizes with 256 graphs x 4 steps (20 480 node and agent rows per
+    batched layer, every kernel in its HIP form)."""
     M, T, S, FU, L = mods()
     RBm = importlib.import_module("graph-marl_amd.replaybuffer")
-    from test_train_gpu import _sd
-    g = np.load(f"{R.GOLDEN}/train.npz")
+    import golden_update as GU
+    from test_train_gpu import check_update
+    g = np.load(f"{R.GOLDEN}/{name}")
     dev = torch.device("cuda")
-    nd = g["node_obs"].shape[-1]
-    netmon = M.NetMon(nd, 32, [64, 48], 1).to(dev)
-    netmon.load_state_dict(_sd(g, "netmon_"))
-    obs_dim = g["agent_obs"].shape[-1] + netmon.get_out_features()
-    model = M.DQN(obs_dim, [64, 32], 4).to(dev)
-    model.load_state_dict(_sd(g, "model_"))
-    target = M.DQN(obs_dim, [64, 32], 4).to(dev)
-    target.load_state_dict(_sd(g, "target_"))
+    netmon, model, target, state0 = GU.build(g, M, dev)
     assert S.seq_ok(netmon, model, target)
-    seq = _golden_seq(g, dev, netmon, RBm)
+    seq = _golden_seq(g, dev, netmon, RBm, state0)
     params = list(model.parameters()) + list(netmon.parameters())
     names = [f"model_{k}" for k, _ in model.named_parameters()] + [f"netmon_{k}" for k, _ in netmon.named_parameters()]
     opt = torch.optim.AdamW(params, lr=float(g["lr"]))
@@ -250,15 +247,7 @@ def test_seq_update_matches_reference_golden():
     np.testing.assert_allclose(loss.item(), g["loss"].item(), rtol=1e-5, atol=1e-6)
     opt.zero_grad()
     loss.backward()
-    for n, p in zip(names, params):
-        np.testing.assert_allclose(p.grad.cpu().numpy(), g["grad_raw_" + n], atol=1e-5, rtol=1e-4, err_msg=n)
-    torch.nn.utils.clip_grad_value_(params, 0.5)
-    torch.nn.utils.clip_grad_norm_(params, 1.0)
-    for n, p in zip(names, params):
-        np.testing.assert_allclose(p.grad.cpu().numpy(), g["grad_clip_" + n], atol=1e-5, rtol=1e-4, err_msg=n)
-    opt.step()
-    for n, p in zip(names, params):
-        np.testing.assert_allclose(p.detach().cpu().numpy(), g["param_after_" + n], atol=1e-6, rtol=0, err_msg=n)
+    check_update(g, names, params, opt, model, target, T)
 
 
 @pytest.mark.parametrize("K,agg", [(1, "sum"), (2, "mean")])

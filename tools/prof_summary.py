@@ -30,8 +30,14 @@ DQN = ["dqn.enc0(K=642)", "dqn.enc1(K=512)", "dqn.q(K=256)"]
 # k_gemm (gm_gemm_f32, fused path): encoder layer 0 runs in k_routing_enc, the LSTM
 # cells carry their gate epilogue, the DQN's first layer gathers the NetMon readout
 NETMON_G = ["netmon.enc1(K=512)", "netmon.enc2(K=256)", "netmon.rnn_obs(K=128+128)", "netmon.rnn_update(K=sum128+128)"]
-DQN_G = ["dqn.enc0(K=512 readout+130)", "dqn.enc1+q(K=512, Q head fused)"]
-DQN_G3 = ["dqn.enc0(K=512 readout+130)", "dqn.enc1(K=512)", "dqn.q(K=256)"]  # before gm_gemm_x3_head
+def dqn_g(env_k=128, fused_head=True):
+    """DQN layer labels of the fused rollout; env_k = env-obs columns of layer 1 (128 with the
+    GEMM-ready obs copy, 130 without); before gm_gemm_x3_head the head was a third GEMM."""
+    l1 = f"dqn.enc0(K=512 readout+{env_k})"
+    return [l1, "dqn.enc1+q(K=512, Q head fused)"] if fused_head else [l1, "dqn.enc1(K=512)", "dqn.q(K=256)"]
+
+
+DQN_G = dqn_g()
 
 
 def linear_labels(n_dispatch, episode_steps, netmon_iters=1, netmon=NETMON, dqn=DQN):
@@ -65,7 +71,7 @@ def bench_tag(name, grid, rows, env_k=128):
     the env-obs columns of DQN layer 1, 128 with the GEMM-ready obs copy, 130 without)."""
     M = rows
     gemm = {
-        "dqn.enc0(K=512 readout+130)": f"linear:dqn.encoder.linear_layers.0:{M}x512x{512 + env_k}",
+        f"dqn.enc0(K=512 readout+{env_k})": f"linear:dqn.encoder.linear_layers.0:{M}x512x{512 + env_k}",
         "dqn.enc1+q(K=512, Q head fused)": f"linear:dqn.encoder.linear_layers.1+head:{M}x256x512",
         "netmon.enc1(K=512)": f"linear:netmon.encode.linear_layers.1:{M}x256x512",
         "netmon.enc2(K=256)": f"linear:netmon.encode.linear_layers.2:{M}x128x256",
@@ -98,11 +104,11 @@ def main():
     ap.add_argument("--env-k", type=int, default=128,
                     help="env-obs columns of DQN layer 1 (128: GEMM-ready obs copy, 130: GM_GEMM_OBS=0 profiles)")
     a = ap.parse_args()
-    dqn_g = DQN_G3 if a.unfused_head else DQN_G
+    dqn_g_ = dqn_g(a.env_k, not a.unfused_head)
     dur = defaultdict(list)
     trace = load(a.trace)
     trace.sort(key=lambda r: int(r["Start_Timestamp"]))
-    for r in relabel(trace, a.episode_steps, dqn_g):
+    for r in relabel(trace, a.episode_steps, dqn_g_):
         dur[key(r)].append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
     pmc = defaultdict(dict)
     for name, path in (("FETCH_SIZE", a.fetch), ("WRITE_SIZE", a.write)):
@@ -111,7 +117,7 @@ def main():
         acc = defaultdict(list)
         rows = [r for r in load(path) if r["Counter_Name"] == name]
         rows.sort(key=lambda r: int(r["Dispatch_Id"]))
-        for r in relabel(rows, a.episode_steps, dqn_g):
+        for r in relabel(rows, a.episode_steps, dqn_g_):
             if r["Counter_Name"] == name:
                 acc[key(r)].append(float(r["Counter_Value"]))
         for k, v in acc.items():
