@@ -1360,9 +1360,10 @@ static int check_obs(const gm_env* env, const gm_obs_buffers* o) {
     if (o && o->obs && o->obs_row_stride < obs_dim_of(env->d.N, env->d.env_var, env->d.k))
         return gm_fail(GM_ERR_INVALID_ARG, "obs_row_stride smaller than the observation size");
     if (o && o->obs_gemm &&
-        (!o->obs || env->d.env_var != 1 || o->obs_gemm_stride < 6 * env->d.N + 8 || (o->obs_gemm_stride % 4) ||
-         (reinterpret_cast<uintptr_t>(o->obs_gemm) & 15)))
-        return gm_fail(GM_ERR_INVALID_ARG, "obs_gemm: env_var 1 with obs, stride >= 6N+8 and 16-byte rows");
+        (!o->obs || env->d.env_var != 1 || (env->d.N & 1) || o->obs_gemm_stride < 6 * env->d.N + 8 ||
+         (o->obs_gemm_stride % 4) || (reinterpret_cast<uintptr_t>(o->obs_gemm) & 15)))
+        // the copy is written as (6N+8)/4 whole float4 chunks per row: N must be even
+        return gm_fail(GM_ERR_INVALID_ARG, "obs_gemm: env_var 1 with obs, even N, stride >= 6N+8 and 16-byte rows");
     return GM_OK;
 }
 

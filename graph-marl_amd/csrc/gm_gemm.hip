@@ -43,6 +43,7 @@
 
 #include "../../include/graph_marl_amd.h"
 #include "gm_amax.hpp"
+#include "gm_act.hpp"
 
 int gm_fail(int code, const std::string& msg);
 
@@ -74,7 +75,7 @@ struct ASrc {
 
 struct Epi {
     const float* bias;
-    int act;                  // EPI_BIAS: 0 none, 1 leaky_relu(0.01)
+    int act;                  // EPI_BIAS / EPI_HEAD: GM_ACT_* (gm_act.hpp)
     float* y;
     long long ldy;
     float* y2;                // EPI_LSTM: c' out
@@ -230,7 +231,7 @@ __device__ __forceinline__ void epilogue(floatx16 (&acc)[TM][TN], const Epi& ep,
                 for (int r = 0; r < 16; r++) {
                     const int row = rb0 + (r & 3) + 8 * (r >> 2);
                     float v = acc[i][j][r] + bv;
-                    if (ep.act == 1) v = v >= 0.f ? v : 0.01f * v;
+                    v = gm_act_fast(v, ep.act);
                     if (row < M && col < N) ep.y[(long long)row * ep.ldy + col] = v;
                     if (ep.sbits) {  // lanes 0-31 / 32-63: 32 columns of rows row(h = 0) / row(h = 1)
                         const unsigned long long b = __ballot(v > 0.f && col < N);
@@ -310,7 +311,7 @@ __device__ __forceinline__ void head_epilogue(floatx16 (&acc)[TM][TN], const Epi
 #pragma unroll
             for (int r = 0; r < 16; r++) {
                 float y = acc[i][j][r] + bv[j];
-                if (ep.act == 1) y = y >= 0.f ? y : 0.01f * y;
+                y = gm_act_fast(y, ep.act);
                 if (ep.y) {
                     const int row = m0 + wr * TM * 32 + i * 32 + 4 * h + (r & 3) + 8 * (r >> 2);
                     if (row < M && col < N) ep.y[(long long)row * ep.ldy + col] = y;
@@ -940,7 +941,7 @@ __device__ __forceinline__ void epilogue16(floatx4 (&acc)[T2][N2], const Epi& ep
                     for (int b = 0; b < 2; b++) {
                         const int col = wn0 + (2 * jp + b) * 16 + l16;
                         float v = acc[i][2 * jp + b][r] + bv[b];
-                        if (ep.act == 1) v = v >= 0.f ? v : 0.01f * v;
+                        v = gm_act_fast(v, ep.act);
                         if (row < M && col < N) ep.y[(long long)row * ep.ldy + col] = v;
                         bb[b] = ep.sbits ? __ballot(v > 0.f && col < N) : 0ull;
                     }
@@ -1086,7 +1087,7 @@ __device__ __forceinline__ void head_epilogue16(floatx4 (&acc)[T2][N2], const Ep
 #pragma unroll
             for (int r = 0; r < 4; r++) {
                 float y = acc[i][j][r] + bv[j];
-                if (ep.act == 1) y = y >= 0.f ? y : 0.01f * y;
+                y = gm_act_fast(y, ep.act);
                 if (ep.y) {
                     const int row = m0 + wr * T2 * 16 + i * 16 + rq + r;
                     if (row < M && col < N) ep.y[(long long)row * ep.ldy + col] = y;
@@ -1600,6 +1601,17 @@ int launch(const ASrc& a0, const ASrc& a1, const float* w, long long ldw, unsign
     return GM_OK;
 }
 
+// activation of a bias epilogue code: GM_EPI_BIAS none, GM_EPI_BIAS_LEAKY leaky_relu, GM_EPI_BIAS_RELU ..
+// GM_EPI_BIAS_SIGMOID -> GM_ACT_RELU .. GM_ACT_SIGMOID
+int epi_act(int epilogue) {
+    if (epilogue == GM_EPI_BIAS_LEAKY) return GM_ACT_LEAKY_RELU;
+    if (epilogue >= GM_EPI_BIAS_RELU && epilogue <= GM_EPI_BIAS_SIGMOID) return GM_ACT_RELU + (epilogue - GM_EPI_BIAS_RELU);
+    return GM_ACT_NONE;
+}
+bool is_bias_epi(int e) {
+    return e == GM_EPI_BIAS || e == GM_EPI_BIAS_LEAKY || (e >= GM_EPI_BIAS_RELU && e <= GM_EPI_BIAS_SIGMOID);
+}
+
 int g_tile = -1;  // tile configuration override (gm_gemm_set_tile), -1 = per-shape default
 
 bool fits(long long bytes) { return bytes >= 0 && bytes < (1ll << 31) - (1 << 24); }
@@ -1698,7 +1710,7 @@ int dispatch(const ASrc& s0, const ASrc& s1, const float* w, long long ldw, unsi
                 ep.hidden = n / 4;
                 return ax == 1 ? GM_GX(4, 1, 1, 4, EPI_LSTM, 1) : GM_GX(4, 1, 1, 4, EPI_LSTM, 2);
             }
-            ep.act = epilogue == GM_EPI_BIAS_LEAKY ? 1 : 0;
+            ep.act = epi_act(epilogue);
             if (gt == 13) return ax == 1 ? GM_GX(2, 2, 2, 2, EPI_BIAS, 1) : GM_GX(2, 2, 2, 2, EPI_BIAS, 2);
             return ax == 1 ? GM_GX(4, 1, 1, 4, EPI_BIAS, 1) : GM_GX(4, 1, 1, 4, EPI_BIAS, 2);
         }
@@ -1717,7 +1729,7 @@ int dispatch(const ASrc& s0, const ASrc& s1, const float* w, long long ldw, unsi
                     default: return GM_G(8, 1, 1, 4, 2, GM_A_DENSE, EPI_LSTM, 1);  // 256x128
                 }
             }
-            ep.act = epilogue == GM_EPI_BIAS_LEAKY ? 1 : 0;
+            ep.act = epi_act(epilogue);
 #define GM_GB(AM)                                                \
     switch (gt) {                                              \
         case 8: return GM_G(4, 2, 2, 4, 2, AM, EPI_BIAS, 1);     \
@@ -1764,7 +1776,7 @@ int dispatch(const ASrc& s0, const ASrc& s1, const float* w, long long ldw, unsi
         }
         return gm_fail(GM_ERR_UNSUPPORTED, "gm_gemm: LSTM epilogue with readout source");
     }
-    ep.act = epilogue == GM_EPI_BIAS_LEAKY ? 1 : 0;
+    ep.act = epi_act(epilogue);
     if constexpr (X3) {
         // 0: 128x128 (4 waves of 64x64); 1: 128x256, 8 waves; 2: 256x128, 8 waves; 3: BK = 32
 #define GM_BIAS3(AM)                                          \
@@ -1866,7 +1878,7 @@ int gemm_entry(bool x3, const gm_a_src* a0, const gm_a_src* a1, const void* w, i
     ep.c_in = c_in;
     ep.ldc = ldc;
     ep.act_out = act_out;
-    if (epilogue == GM_EPI_BIAS || epilogue == GM_EPI_BIAS_LEAKY) {  // act_out: sign bits of y (x3 form)
+    if (is_bias_epi(epilogue)) {  // act_out: sign bits of y (x3 form)
         if (act_out && (!x3 || ldc < (n + 31) / 32))
             return gm_fail(GM_ERR_INVALID_ARG, std::string(fn) + ": sign bits need the x3 form and ldc >= ceil(n / 32)");
         ep.sbits = reinterpret_cast<unsigned*>(act_out);
@@ -1882,7 +1894,7 @@ int gemm_entry(bool x3, const gm_a_src* a0, const gm_a_src* a1, const void* w, i
         epilogue = GM_EPI_LSTM;
     } else if (epilogue == GM_EPI_LSTM) {
         if (n % 128 || !y2 || !c_in) return gm_fail(GM_ERR_INVALID_ARG, std::string(fn) + ": LSTM epilogue needs 4H % 128 == 0");
-    } else if (epilogue != GM_EPI_BIAS && epilogue != GM_EPI_BIAS_LEAKY) {
+    } else if (!is_bias_epi(epilogue)) {
         return gm_fail(GM_ERR_INVALID_ARG, std::string(fn) + ": unknown epilogue");
     } else if (ldy < n) {
         return gm_fail(GM_ERR_INVALID_ARG, std::string(fn) + ": ldy < n");
@@ -2013,7 +2025,7 @@ extern "C" int gm_gemm_x3_head(const gm_a_src* a0, const void* wp, const float* 
                                int32_t m, int32_t n, int32_t act, const float* wq, int64_t ldwq, const float* bq,
                                int32_t nq, float* q, int64_t ldq, float* y, int64_t ldy, void* stream) {
     if (!a0 || a0->mode != GM_A_DENSE || !wp || !wscale_inv || !wq || !q || m <= 0 || n <= 0 || n > 256 ||
-        nq <= 0 || nq > 4 || ldwq < n || ldq < nq || (y && ldy < n) || (act != 0 && act != 1) ||
+        nq <= 0 || nq > 4 || ldwq < n || ldq < nq || (y && ldy < n) || act < GM_ACT_NONE || act > GM_ACT_SIGMOID ||
         (reinterpret_cast<uintptr_t>(wp) & 15))
         return gm_fail(GM_ERR_INVALID_ARG, "gm_gemm_x3_head: bad arguments (dense source, n <= 256, nq <= 4)");
     ASrc s0, s1;
@@ -2558,13 +2570,14 @@ extern "C" int gm_gemm_set_tile(int32_t tile) {
 
 extern "C" int gm_linear_f32(const float* x, int64_t ldx, const float* w, int64_t ldw, const float* b, int32_t m,
                              int32_t n, int32_t k, int32_t act, float* y, int64_t ldy, void* stream) {
-    if (!x || !w || !y || act < 0 || act > 1) return gm_fail(GM_ERR_INVALID_ARG, "gm_linear_f32: bad arguments");
+    if (!x || !w || !y || act < GM_ACT_NONE || act > GM_ACT_SIGMOID)
+        return gm_fail(GM_ERR_INVALID_ARG, "gm_linear_f32: bad arguments");
     gm_a_src a;
     memset(&a, 0, sizeof(a));
     a.mode = GM_A_DENSE;
     a.p0 = x;
     a.ld0 = ldx;
     a.k = k;
-    return gm_gemm_f32(&a, nullptr, w, ldw, b, m, n, act ? GM_EPI_BIAS_LEAKY : GM_EPI_BIAS, y, ldy, nullptr, 0,
+    return gm_gemm_f32(&a, nullptr, w, ldw, b, m, n, act == GM_ACT_NONE ? GM_EPI_BIAS : act == GM_ACT_LEAKY_RELU ? GM_EPI_BIAS_LEAKY : GM_EPI_BIAS_RELU + (act - GM_ACT_RELU), y, ldy, nullptr, 0,
                        nullptr, 0, nullptr, stream);
 }

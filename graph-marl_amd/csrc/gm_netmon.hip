@@ -16,6 +16,7 @@
 
 #include "../../include/graph_marl_amd.h"
 #include "gm_amax.hpp"
+#include "gm_act.hpp"
 
 int gm_fail(int code, const std::string& msg);
 
@@ -366,10 +367,8 @@ __global__ __launch_bounds__(256) void k_routing_enc(const float* __restrict__ x
         float* yr = y + (base + i) * ldy + c0 + col;
         if (CPL == 2) {
             float a0 = acc[0], a1 = acc[CPL - 1];
-            if (act) {
-                a0 = a0 >= 0.f ? a0 : 0.01f * a0;
-                a1 = a1 >= 0.f ? a1 : 0.01f * a1;
-            }
+            a0 = gm_act_fast(a0, act);
+            a1 = gm_act_fast(a1, act);
             *reinterpret_cast<float2*>(yr) = make_float2(a0, a1);
             if (sbits) {  // 32-column sign words: lanes 16k..16k+15 hold columns 32k..32k+31, two each
                 const unsigned long long b0 = __ballot(a0 > 0.f), b1 = __ballot(a1 > 0.f);
@@ -381,9 +380,9 @@ __global__ __launch_bounds__(256) void k_routing_enc(const float* __restrict__ x
             }
         } else {
 #pragma unroll
-            for (int j = 0; j < CPL; j++) yr[j] = act ? (acc[j] >= 0.f ? acc[j] : 0.01f * acc[j]) : acc[j];
+            for (int j = 0; j < CPL; j++) yr[j] = gm_act_fast(acc[j], act);
             if (sbits) {
-                const float a0 = act ? (acc[0] >= 0.f ? acc[0] : 0.01f * acc[0]) : acc[0];
+                const float a0 = gm_act_fast(acc[0], act);
                 const unsigned long long b0 = __ballot(a0 > 0.f);
                 if ((lane & 31) == 0) sbits[(base + i) * ldsb + (c0 >> 5) + (lane >> 5)] = (unsigned)(b0 >> lane);
             }
@@ -435,9 +434,10 @@ static int launch_agg(const float* h, const int32_t* nbr, int32_t G, int32_t N, 
 // src/model.py:13-42): g = dY * (Y >= 0 ? 1 : slope), and per-block column sums of g for the
 // bias gradient (partial[block][col]; the caller sums the blocks: a fixed summation order).
 // Threads own columns, blocks own row chunks; loads and stores are row-contiguous.
+// act < 0: leaky_relu with the given slope; else GM_ACT_* (derivative from the output, gm_act.hpp)
 __global__ __launch_bounds__(256) void k_leaky_bwd(const float* __restrict__ gy, const float* __restrict__ y,
                                                    long long rows, int cols, int rows_per_block, float slope,
-                                                   float* __restrict__ g, float* __restrict__ part,
+                                                   int act, float* __restrict__ g, float* __restrict__ part,
                                                    unsigned* __restrict__ amax) {
     const long long r0 = (long long)blockIdx.x * rows_per_block;
     const long long r1 = min(rows, r0 + rows_per_block);
@@ -446,7 +446,8 @@ __global__ __launch_bounds__(256) void k_leaky_bwd(const float* __restrict__ gy,
         float acc = 0.f;
         for (long long r = r0; r < r1; r++) {
             const long long i = r * cols + c;
-            const float v = y[i] > 0.f ? gy[i] : slope * gy[i];  // torch: input > 0 ? g : slope g
+            const float v = act < 0 ? (y[i] > 0.f ? gy[i] : slope * gy[i])  // torch: input > 0 ? g : slope g
+                                    : gy[i] * gm_act_dy(y[i], act);
             g[i] = v;
             acc += v;
             m = fmaxf(m, fabsf(v));
@@ -456,19 +457,30 @@ __global__ __launch_bounds__(256) void k_leaky_bwd(const float* __restrict__ gy,
     if (amax) gm_block_amax(amax, m);
 }
 
-extern "C" int gm_leaky_bwd(const float* gy, const float* y, int64_t rows, int32_t cols, float slope, float* g,
-                            float* part, int32_t rows_per_block, float* g_scale, void* stream) {
+static int act_bwd(const char* fn, const float* gy, const float* y, int64_t rows, int32_t cols, float slope, int act,
+                   float* g, float* part, int32_t rows_per_block, float* g_scale, void* stream) {
     if (!gy || !y || !g || !part || rows <= 0 || cols <= 0 || rows_per_block <= 0)
-        return gm_fail(GM_ERR_INVALID_ARG, "gm_leaky_bwd: bad arguments");
+        return gm_fail(GM_ERR_INVALID_ARG, std::string(fn) + ": bad arguments");
     hipStream_t st = (hipStream_t)stream;
     if (g_scale && hipMemsetAsync(g_scale, 0, sizeof(float), st) != hipSuccess)
-        return gm_fail(GM_ERR_HIP, "gm_leaky_bwd: memset");
+        return gm_fail(GM_ERR_HIP, std::string(fn) + ": memset");
     const long long nb = (rows + rows_per_block - 1) / rows_per_block;
     hipLaunchKernelGGL(k_leaky_bwd, dim3((unsigned)nb), dim3(256), 0, st, gy, y, (long long)rows, (int)cols,
-                       (int)rows_per_block, slope, g, part, reinterpret_cast<unsigned*>(g_scale));
+                       (int)rows_per_block, slope, act, g, part, reinterpret_cast<unsigned*>(g_scale));
     int rc = launched();
     if (rc == GM_OK && g_scale) rc = gm_absmax_finish(g_scale, stream);
     return rc;
+}
+
+extern "C" int gm_leaky_bwd(const float* gy, const float* y, int64_t rows, int32_t cols, float slope, float* g,
+                            float* part, int32_t rows_per_block, float* g_scale, void* stream) {
+    return act_bwd("gm_leaky_bwd", gy, y, rows, cols, slope, -1, g, part, rows_per_block, g_scale, stream);
+}
+
+extern "C" int gm_act_bwd(const float* gy, const float* y, int64_t rows, int32_t cols, int32_t act, float* g,
+                          float* part, int32_t rows_per_block, float* g_scale, void* stream) {
+    if (act < GM_ACT_NONE || act > GM_ACT_SIGMOID) return gm_fail(GM_ERR_INVALID_ARG, "gm_act_bwd: unknown act");
+    return act_bwd("gm_act_bwd", gy, y, rows, cols, 0.f, act, g, part, rows_per_block, g_scale, stream);
 }
 
 extern "C" int gm_mp_aggregate(const float* h, const int32_t* nbr, int32_t G, int32_t N, int32_t deg, int32_t H,
@@ -1045,7 +1057,7 @@ __global__ __launch_bounds__(1024) void k_qhead_bwd(const float* __restrict__ dq
                 float gv = 0.f;
 #pragma unroll
                 for (int q = 0; q < 4; q++) gv = fmaf(d[u][q], w[q], gv);
-                if (act && !(yv[u] > 0.f)) gv *= 0.01f;
+                if (act) gv *= gm_act_dy(yv[u], act);
                 g[r * ldg + c] = gv;
                 pb += gv;
                 mx = fmaxf(mx, fabsf(gv));
@@ -1112,7 +1124,7 @@ __global__ __launch_bounds__(256) void k_qhead_bwd4(const float* __restrict__ dq
                 float v = 0.f;
 #pragma unroll
                 for (int q = 0; q < 4; q++) v = fmaf(d[u][q], (&w[q].x)[e], v);
-                if (act && !(ye[e] > 0.f)) v *= 0.01f;
+                if (act) v *= gm_act_dy(ye[e], act);
                 gv[e] = v;
                 mx = fmaxf(mx, fabsf(v));
             }
@@ -1254,7 +1266,7 @@ extern "C" int gm_routing_node_encoder(const float* x, int64_t ldx, const int32_
 extern "C" int gm_routing_node_encoder_bits(const float* x, int64_t ldx, const int32_t* nbr, int32_t G, int32_t N,
                                             const float* wt, const float* b, int32_t n, int32_t act, float* y,
                                             int64_t ldy, uint32_t* sbits, int64_t ldsb, void* stream) {
-    if (!x || !nbr || !wt || !y || G <= 0 || N < 4 || n <= 0 || (n % 64) || act < 0 || act > 1 ||
+    if (!x || !nbr || !wt || !y || G <= 0 || N < 4 || n <= 0 || (n % 64) || act < GM_ACT_NONE || act > GM_ACT_SIGMOID ||
         ldx < 4 * N + 8 || ldy < n || (ldy % 2) || (reinterpret_cast<uintptr_t>(wt) & 15) ||
         (sbits && ldsb < n / 32))
         return gm_fail(GM_ERR_INVALID_ARG, "gm_routing_node_encoder: bad arguments (n % 64 == 0, 16-byte W^T)");
@@ -1308,15 +1320,16 @@ struct LnLstmP {
 };
 
 template <int UPL>
-__global__ __launch_bounds__(256) void k_lnlstm_pw(const float* __restrict__ G, long long ldg,
+__global__ __launch_bounds__(256) void k_lnlstm_pw(const float* __restrict__ Gi, long long ldgi,
+                                                   const float* __restrict__ Gh, long long ldgh,
                                                    const float* __restrict__ c_in, long long ldc, LnLstmP p, int M,
                                                    int H, float eps, float* __restrict__ y, long long ldy,
-                                                   float* __restrict__ y2, long long ldy2) {
+                                                   float* __restrict__ y2, long long ldy2, float* __restrict__ stats) {
     const int lane = threadIdx.x & 63;
     const long long row = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
     if (row >= M) return;  // wave-uniform
-    const float* gi = G + row * ldg;
-    const float* gh = gi + 4 * H;
+    const float* gi = Gi + row * ldgi;
+    const float* gh = Gh + row * ldgh;
     float a[UPL][4], b[UPL][4];
     float si = 0.f, sh = 0.f;
 #pragma unroll
@@ -1379,23 +1392,203 @@ __global__ __launch_bounds__(256) void k_lnlstm_pw(const float* __restrict__ G, 
         y[row * ldy + u] = og[q] * tanh_f(cn);
         y2[row * ldy2 + u] = cn;
     }
+    if (stats && lane < 6) {  // the row's LayerNorm statistics for the backward pass
+        const float v = lane == 0 ? mi : lane == 1 ? ri : lane == 2 ? mh : lane == 3 ? rh : lane == 4 ? mc : rc;
+        stats[row * 8 + lane] = v;
+    }
+}
+
+// Backward of k_lnlstm_pw (src/layernormlstm.py:24-42 differentiated by hand). One wave per row, the
+// same unit ownership as the forward; the forward quantities are recomputed from the raw gate GEMM
+// outputs, c and the saved statistics (no activation tensor in HBM). Per row:
+//   dcy = dc1 + dh1 o (1 - tanh^2 cy), do = dh1 tanh cy
+//   LN_cell^T: dn = dcy w_c, du = r_c (dn - mean dn - n_c mean(dn n_c))
+//   di = du g, dg = du i, df = du c, dc = du f; gate pre-activations dG through sigma' / tanh'
+//   LN_in^T / LN_hid^T: dni = dG w_i, d gi = r_i (dni - mean dni - n_i mean(dni n_i)) (same for h)
+// Parameter gradients are accumulated per wave in registers and written as one partial row per wave:
+// part[wave][14H] = [d w_i (4H) | d w_h (4H) | d bias (4H; also d b_i and d b_h) | d w_c (H) | d b_c (H)].
+template <int UPL>
+__global__ __launch_bounds__(256) void k_lnlstm_bwd(const float* __restrict__ Gi, long long ldgi,
+                                                    const float* __restrict__ Gh, long long ldgh,
+                                                    const float* __restrict__ c_in, long long ldc, LnLstmP p,
+                                                    const float* __restrict__ stats, const float* __restrict__ dh1,
+                                                    long long lddh, const float* __restrict__ dc1, long long lddc,
+                                                    int M, int H, int rpw, float* __restrict__ dgi, long long lddgi,
+                                                    float* __restrict__ dgh, long long lddgh, float* __restrict__ dc,
+                                                    long long lddco, float* __restrict__ part) {
+    const int lane = threadIdx.x & 63;
+    const long long wave = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const long long r0 = wave * rpw;
+    if (r0 >= M) return;  // wave-uniform
+    const long long r1 = r0 + rpw < M ? r0 + rpw : M;
+    float pwi[UPL][4], pwh[UPL][4], pb[UPL][4], pwc[UPL], pbc[UPL];
+#pragma unroll
+    for (int q = 0; q < UPL; q++) {
+        pwc[q] = pbc[q] = 0.f;
+#pragma unroll
+        for (int k = 0; k < 4; k++) pwi[q][k] = pwh[q][k] = pb[q][k] = 0.f;
+    }
+    const float inv4h = 1.0f / (float)(4 * H), invh = 1.0f / (float)H;
+    for (long long row = r0; row < r1; row++) {
+        const float mi = stats[row * 8 + 0], ri = stats[row * 8 + 1], mh = stats[row * 8 + 2],
+                    rh = stats[row * 8 + 3], mc = stats[row * 8 + 4], rc = stats[row * 8 + 5];
+        const float* gi = Gi + row * ldgi;
+        const float* gh = Gh + row * ldgh;
+        float ni[UPL][4], nh[UPL][4], act[UPL][4], cx[UPL], nc[UPL], dcy[UPL], dO[UPL];
+        float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+        for (int q = 0; q < UPL; q++) {
+            const int u = lane + 64 * q;
+            cx[q] = nc[q] = dcy[q] = dO[q] = 0.f;
+#pragma unroll
+            for (int k = 0; k < 4; k++) ni[q][k] = nh[q][k] = act[q][k] = 0.f;
+            if (u >= H) continue;
+            float g[4];
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                const int col = k * H + u;
+                ni[q][k] = (gi[col] - mi) * ri;
+                nh[q][k] = (gh[col] - mh) * rh;
+                g[k] = (ni[q][k] * p.gi_w[col] + p.gi_b[col]) + (nh[q][k] * p.gh_w[col] + p.gh_b[col]) + p.bias[col];
+            }
+            act[q][0] = sig_f(g[0]);
+            act[q][1] = sig_f(g[1]);
+            act[q][2] = tanh_f(g[2]);
+            act[q][3] = sig_f(g[3]);
+            cx[q] = c_in[row * ldc + u];
+            const float cp = act[q][1] * cx[q] + act[q][0] * act[q][2];
+            nc[q] = (cp - mc) * rc;
+            const float cy = nc[q] * p.lc_w[u] + p.lc_b[u];
+            const float th = tanh_f(cy);
+            const float gh1 = dh1 ? dh1[row * lddh + u] : 0.f;
+            dcy[q] = (dc1 ? dc1[row * lddc + u] : 0.f) + gh1 * act[q][3] * (1.f - th * th);
+            dO[q] = gh1 * th;
+            pwc[q] += dcy[q] * nc[q];
+            pbc[q] += dcy[q];
+            const float dn = dcy[q] * p.lc_w[u];
+            s1 += dn;
+            s2 += dn * nc[q];
+        }
+        const float m1 = wsum(s1) * invh, m2 = wsum(s2) * invh;
+        float dG[UPL][4];
+        float ti1 = 0.f, ti2 = 0.f, th1 = 0.f, th2 = 0.f;
+#pragma unroll
+        for (int q = 0; q < UPL; q++) {
+            const int u = lane + 64 * q;
+#pragma unroll
+            for (int k = 0; k < 4; k++) dG[q][k] = 0.f;
+            if (u >= H) continue;
+            const float du = rc * (dcy[q] * p.lc_w[u] - m1 - nc[q] * m2);
+            const float i = act[q][0], f = act[q][1], gg = act[q][2], o = act[q][3];
+            dc[row * lddco + u] = du * f;
+            dG[q][0] = du * gg * i * (1.f - i);
+            dG[q][1] = du * cx[q] * f * (1.f - f);
+            dG[q][2] = du * i * (1.f - gg * gg);
+            dG[q][3] = dO[q] * o * (1.f - o);
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                const int col = k * H + u;
+                pb[q][k] += dG[q][k];
+                pwi[q][k] += dG[q][k] * ni[q][k];
+                pwh[q][k] += dG[q][k] * nh[q][k];
+                const float a = dG[q][k] * p.gi_w[col], b = dG[q][k] * p.gh_w[col];
+                ti1 += a;
+                ti2 += a * ni[q][k];
+                th1 += b;
+                th2 += b * nh[q][k];
+            }
+        }
+        const float mi1 = wsum(ti1) * inv4h, mi2 = wsum(ti2) * inv4h;
+        const float mh1 = wsum(th1) * inv4h, mh2 = wsum(th2) * inv4h;
+#pragma unroll
+        for (int q = 0; q < UPL; q++) {
+            const int u = lane + 64 * q;
+            if (u >= H) continue;
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                const int col = k * H + u;
+                dgi[row * lddgi + col] = ri * (dG[q][k] * p.gi_w[col] - mi1 - ni[q][k] * mi2);
+                dgh[row * lddgh + col] = rh * (dG[q][k] * p.gh_w[col] - mh1 - nh[q][k] * mh2);
+            }
+        }
+    }
+    float* pr = part + wave * 14LL * H;
+#pragma unroll
+    for (int q = 0; q < UPL; q++) {
+        const int u = lane + 64 * q;
+        if (u >= H) continue;
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            pr[k * H + u] = pwi[q][k];
+            pr[4 * H + k * H + u] = pwh[q][k];
+            pr[8 * H + k * H + u] = pb[q][k];
+        }
+        pr[12 * H + u] = pwc[q];
+        pr[13 * H + u] = pbc[q];
+    }
+}
+
+// GRU cell gate math (torch.nn.GRUCell, gate order r, z, n): gi = x W_ih^T + b_ih, gh = h W_hh^T + b_hh
+// ([m][3H] each, strided), r = sigma(gi_r + gh_r), z = sigma(gi_z + gh_z), n = tanh(gi_n + r gh_n),
+// h' = (1 - z) n + z h. One thread per (row, unit).
+__global__ __launch_bounds__(256) void k_gru_pw(const float* __restrict__ gi, long long ldgi,
+                                                const float* __restrict__ gh, long long ldgh,
+                                                const float* __restrict__ h, long long ldh, int M, int H,
+                                                float* __restrict__ y, long long ldy) {
+    const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= (long long)M * H) return;
+    const long long row = t / H;
+    const int u = (int)(t - row * H);
+    const float* a = gi + row * ldgi;
+    const float* b = gh + row * ldgh;
+    const float r = sig_f(a[u] + b[u]), z = sig_f(a[H + u] + b[H + u]);
+    const float n = tanh_f(a[2 * H + u] + r * b[2 * H + u]);
+    y[row * ldy + u] = (1.f - z) * n + z * h[row * ldh + u];
+}
+
+// Backward of k_gru_pw: dn = dh' (1 - z), dz = dh' (h - n), dh = dh' z; dn_pre = dn (1 - n^2);
+// d gi = [dr_pre, dz_pre, dn_pre], d gh = [dr_pre, dz_pre, dn_pre r], dr_pre = dn_pre gh_n r (1 - r),
+// dz_pre = dz z (1 - z).
+__global__ __launch_bounds__(256) void k_gru_bwd(const float* __restrict__ gi, long long ldgi,
+                                                 const float* __restrict__ gh, long long ldgh,
+                                                 const float* __restrict__ h, long long ldh,
+                                                 const float* __restrict__ dy, long long lddy, int M, int H,
+                                                 float* __restrict__ dgi, long long lddgi, float* __restrict__ dgh,
+                                                 long long lddgh, float* __restrict__ dh, long long lddh) {
+    const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= (long long)M * H) return;
+    const long long row = t / H;
+    const int u = (int)(t - row * H);
+    const float* a = gi + row * ldgi;
+    const float* b = gh + row * ldgh;
+    const float r = sig_f(a[u] + b[u]), z = sig_f(a[H + u] + b[H + u]);
+    const float ghn = b[2 * H + u];
+    const float n = tanh_f(a[2 * H + u] + r * ghn);
+    const float g = dy[row * lddy + u], hv = h[row * ldh + u];
+    const float dnp = g * (1.f - z) * (1.f - n * n);
+    const float drp = dnp * ghn * r * (1.f - r);
+    const float dzp = g * (hv - n) * z * (1.f - z);
+    dgi[row * lddgi + u] = drp;
+    dgi[row * lddgi + H + u] = dzp;
+    dgi[row * lddgi + 2 * H + u] = dnp;
+    dgh[row * lddgh + u] = drp;
+    dgh[row * lddgh + H + u] = dzp;
+    dgh[row * lddgh + 2 * H + u] = dnp * r;
+    dh[row * lddh + u] = g * z;
 }
 }  // namespace
 
-extern "C" int gm_lnlstm_pointwise(const float* g, int64_t ldg, const float* c, int64_t ldc, const float* ln_in_w,
-                                   const float* ln_in_b, const float* ln_hid_w, const float* ln_hid_b,
-                                   const float* bias, const float* ln_cell_w, const float* ln_cell_b, int32_t m,
-                                   int32_t H, float eps, float* h1, int64_t ldh, float* c1, int64_t ldc1,
-                                   void* stream) {
-    if (!g || !c || !h1 || !c1 || !ln_in_w || !ln_in_b || !ln_hid_w || !ln_hid_b || !bias || !ln_cell_w ||
-        !ln_cell_b || m <= 0 || H <= 0 || H > 512 || ldg < 8 * (int64_t)H || ldc < H || ldh < H || ldc1 < H)
-        return gm_fail(GM_ERR_INVALID_ARG, "gm_lnlstm_pointwise: bad arguments (H <= 512, ldg >= 8H)");
-    LnLstmP p{ln_in_w, ln_in_b, ln_hid_w, ln_hid_b, bias, ln_cell_w, ln_cell_b};
+static int lnlstm_fwd(const char* name, const float* gi, int64_t ldgi, const float* gh, int64_t ldgh, const float* c,
+                      int64_t ldc, const LnLstmP& p, int32_t m, int32_t H, float eps, float* h1, int64_t ldh, float* c1,
+                      int64_t ldc1, float* stats, void* stream) {
+    if (!gi || !gh || !c || !h1 || !c1 || !p.gi_w || !p.gi_b || !p.gh_w || !p.gh_b || !p.bias || !p.lc_w || !p.lc_b ||
+        m <= 0 || H <= 0 || H > 512 || ldgi < 4 * (int64_t)H || ldgh < 4 * (int64_t)H || ldc < H || ldh < H || ldc1 < H)
+        return gm_fail(GM_ERR_INVALID_ARG, std::string(name) + ": bad arguments (H <= 512, gate rows >= 4H)");
     const dim3 grid((m + 3) / 4), blk(256);
     hipStream_t st = (hipStream_t)stream;
-#define GM_LN(U) \
-    hipLaunchKernelGGL(k_lnlstm_pw<U>, grid, blk, 0, st, g, (long long)ldg, c, (long long)ldc, p, m, H, eps, h1, \
-                       (long long)ldh, c1, (long long)ldc1)
+#define GM_LN(U)                                                                                                    \
+    hipLaunchKernelGGL(k_lnlstm_pw<U>, grid, blk, 0, st, gi, (long long)ldgi, gh, (long long)ldgh, c, (long long)ldc, \
+                       p, m, H, eps, h1, (long long)ldh, c1, (long long)ldc1, stats)
     if (H <= 64)
         GM_LN(1);
     else if (H <= 128)
@@ -1406,6 +1599,89 @@ extern "C" int gm_lnlstm_pointwise(const float* g, int64_t ldg, const float* c, 
         GM_LN(8);
 #undef GM_LN
     hipError_t e = hipGetLastError();
-    if (e != hipSuccess) return gm_fail(GM_ERR_HIP, std::string("gm_lnlstm_pointwise: ") + hipGetErrorString(e));
+    if (e != hipSuccess) return gm_fail(GM_ERR_HIP, std::string(name) + ": " + hipGetErrorString(e));
+    return GM_OK;
+}
+
+extern "C" int gm_lnlstm_pointwise(const float* g, int64_t ldg, const float* c, int64_t ldc, const float* ln_in_w,
+                                   const float* ln_in_b, const float* ln_hid_w, const float* ln_hid_b,
+                                   const float* bias, const float* ln_cell_w, const float* ln_cell_b, int32_t m,
+                                   int32_t H, float eps, float* h1, int64_t ldh, float* c1, int64_t ldc1,
+                                   void* stream) {
+    if (!g || ldg < 8 * (int64_t)H)
+        return gm_fail(GM_ERR_INVALID_ARG, "gm_lnlstm_pointwise: bad arguments (H <= 512, ldg >= 8H)");
+    LnLstmP p{ln_in_w, ln_in_b, ln_hid_w, ln_hid_b, bias, ln_cell_w, ln_cell_b};
+    return lnlstm_fwd("gm_lnlstm_pointwise", g, ldg, g + 4 * (int64_t)H, ldg, c, ldc, p, m, H, eps, h1, ldh, c1, ldc1,
+                      nullptr, stream);
+}
+
+extern "C" int gm_lnlstm_fwd(const float* gi, int64_t ldgi, const float* gh, int64_t ldgh, const float* c,
+                             int64_t ldc, const float* ln_in_w, const float* ln_in_b, const float* ln_hid_w,
+                             const float* ln_hid_b, const float* bias, const float* ln_cell_w, const float* ln_cell_b,
+                             int32_t m, int32_t H, float eps, float* h1, int64_t ldh, float* c1, int64_t ldc1,
+                             float* stats, void* stream) {
+    if (!stats) return gm_fail(GM_ERR_INVALID_ARG, "gm_lnlstm_fwd: stats is required");
+    LnLstmP p{ln_in_w, ln_in_b, ln_hid_w, ln_hid_b, bias, ln_cell_w, ln_cell_b};
+    return lnlstm_fwd("gm_lnlstm_fwd", gi, ldgi, gh, ldgh, c, ldc, p, m, H, eps, h1, ldh, c1, ldc1, stats, stream);
+}
+
+extern "C" int gm_lnlstm_bwd(const float* gi, int64_t ldgi, const float* gh, int64_t ldgh, const float* c,
+                             int64_t ldc, const float* ln_in_w, const float* ln_in_b, const float* ln_hid_w,
+                             const float* ln_hid_b, const float* bias, const float* ln_cell_w, const float* ln_cell_b,
+                             const float* stats, const float* dh1, int64_t lddh, const float* dc1, int64_t lddc,
+                             int32_t m, int32_t H, int32_t rows_per_wave, float* dgi, int64_t lddgi, float* dgh,
+                             int64_t lddgh, float* dc, int64_t lddco, float* part, void* stream) {
+    if (!gi || !gh || !c || !stats || !dgi || !dgh || !dc || !part || !ln_in_w || !ln_in_b || !ln_hid_w || !ln_hid_b ||
+        !bias || !ln_cell_w || !ln_cell_b || (!dh1 && !dc1) || m <= 0 || H <= 0 || H > 512 || rows_per_wave <= 0 ||
+        ldgi < 4 * (int64_t)H || ldgh < 4 * (int64_t)H || lddgi < 4 * (int64_t)H || lddgh < 4 * (int64_t)H ||
+        ldc < H || lddco < H || (dh1 && lddh < H) || (dc1 && lddc < H))
+        return gm_fail(GM_ERR_INVALID_ARG, "gm_lnlstm_bwd: bad arguments (H <= 512, gate rows >= 4H)");
+    LnLstmP p{ln_in_w, ln_in_b, ln_hid_w, ln_hid_b, bias, ln_cell_w, ln_cell_b};
+    const long long waves = ((long long)m + rows_per_wave - 1) / rows_per_wave;
+    const dim3 grid((unsigned)((waves + 3) / 4)), blk(256);
+    hipStream_t st = (hipStream_t)stream;
+#define GM_LNB(U)                                                                                                     \
+    hipLaunchKernelGGL(k_lnlstm_bwd<U>, grid, blk, 0, st, gi, (long long)ldgi, gh, (long long)ldgh, c, (long long)ldc, \
+                       p, stats, dh1, (long long)lddh, dc1, (long long)lddc, m, H, rows_per_wave, dgi,                 \
+                       (long long)lddgi, dgh, (long long)lddgh, dc, (long long)lddco, part)
+    if (H <= 64)
+        GM_LNB(1);
+    else if (H <= 128)
+        GM_LNB(2);
+    else if (H <= 256)
+        GM_LNB(4);
+    else
+        GM_LNB(8);
+#undef GM_LNB
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return gm_fail(GM_ERR_HIP, std::string("gm_lnlstm_bwd: ") + hipGetErrorString(e));
+    return GM_OK;
+}
+
+extern "C" int gm_gru_pointwise(const float* gi, int64_t ldgi, const float* gh, int64_t ldgh, const float* h,
+                                int64_t ldh, int32_t m, int32_t H, float* h1, int64_t ldh1, void* stream) {
+    if (!gi || !gh || !h || !h1 || m <= 0 || H <= 0 || ldgi < 3 * (int64_t)H || ldgh < 3 * (int64_t)H || ldh < H ||
+        ldh1 < H)
+        return gm_fail(GM_ERR_INVALID_ARG, "gm_gru_pointwise: bad arguments (gate rows >= 3H)");
+    const long long n = (long long)m * H;
+    hipLaunchKernelGGL(k_gru_pw, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, gi,
+                       (long long)ldgi, gh, (long long)ldgh, h, (long long)ldh, m, H, h1, (long long)ldh1);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return gm_fail(GM_ERR_HIP, std::string("gm_gru_pointwise: ") + hipGetErrorString(e));
+    return GM_OK;
+}
+
+extern "C" int gm_gru_bwd(const float* gi, int64_t ldgi, const float* gh, int64_t ldgh, const float* h, int64_t ldh,
+                          const float* dh1, int64_t lddh1, int32_t m, int32_t H, float* dgi, int64_t lddgi, float* dgh,
+                          int64_t lddgh, float* dh, int64_t lddh, void* stream) {
+    if (!gi || !gh || !h || !dh1 || !dgi || !dgh || !dh || m <= 0 || H <= 0 || ldgi < 3 * (int64_t)H ||
+        ldgh < 3 * (int64_t)H || ldh < H || lddh1 < H || lddgi < 3 * (int64_t)H || lddgh < 3 * (int64_t)H || lddh < H)
+        return gm_fail(GM_ERR_INVALID_ARG, "gm_gru_bwd: bad arguments (gate rows >= 3H)");
+    const long long n = (long long)m * H;
+    hipLaunchKernelGGL(k_gru_bwd, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, gi,
+                       (long long)ldgi, gh, (long long)ldgh, h, (long long)ldh, dh1, (long long)lddh1, m, H, dgi,
+                       (long long)lddgi, dgh, (long long)lddgh, dh, (long long)lddh);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return gm_fail(GM_ERR_HIP, std::string("gm_gru_bwd: ") + hipGetErrorString(e));
     return GM_OK;
 }

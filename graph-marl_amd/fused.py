@@ -23,6 +23,13 @@ from . import _lib as L
 GM_A_DENSE, GM_A_AGGREGATE, GM_A_READOUT = 0, 1, 2
 GM_EPI_BIAS, GM_EPI_BIAS_LEAKY, GM_EPI_LSTM, GM_EPI_GRU = 0, 1, 2, 3
 
+
+def _epi(act):
+    """bias + activation epilogue code of a layer's GM_ACT_* code (model.epi_code)."""
+    from .model import epi_code
+
+    return epi_code(act)
+
 # LSTM update cell: a strided aggregate pass (gm_mp_aggregate_rows, 26-29 us at 81920 nodes) +
 # the cell on dense [Σ h | h] (103-111 us) instead of the AGGREGATE A source inside the GEMM
 # (159 us); False selects the in-GEMM aggregate
@@ -274,7 +281,7 @@ def linear_head(lin, fc, x, ldx, k, q, y=None):
     tag = lin.tag and f"linear:{lin.tag}+head:{M}x{lin.out_features}x{k}"
     with L.timed(tag):
         L.check(lib.gm_gemm_x3_head(C.byref(dense(x.data_ptr(), ldx, k)), x3.wp.data_ptr(), x3.sinv.data_ptr(),
-                                    lin.bias.data_ptr(), M, lin.out_features, int(lin.act == 1), wq.data_ptr(),
+                                    lin.bias.data_ptr(), M, lin.out_features, lin.act, wq.data_ptr(),
                                     wq.stride(0), fc.bias.data_ptr(), fc.out_features, q.data_ptr(), q.stride(0),
                                     None if y is None else y.data_ptr(), 0 if y is None else y.stride(0),
                                     L.stream_ptr()))
@@ -285,7 +292,7 @@ def _linear(x, ldx, k, lin, out):
     wp, ldw = lin._wc.get(lin.weight)
     a = dense(x.data_ptr(), ldx, k)
     gemm(a, None, wp.data_ptr(), ldw, lin.bias.data_ptr(), x.shape[0], lin.out_features,
-         GM_EPI_BIAS_LEAKY if lin.act == 1 else GM_EPI_BIAS, out.data_ptr(), out.stride(0),
+         _epi(lin.act), out.data_ptr(), out.stride(0),
          tag=lin.tag and f"linear:{lin.tag}:{x.shape[0]}x{lin.out_features}x{k}", x3=pack_x3(lin))
     return out
 
@@ -295,7 +302,7 @@ def linear_rows(lin, x, ldx, M, out, ldo, k=None):
     k = lin.in_features if k is None else k
     wp, ldw = lin._wc.get(lin.weight)
     gemm(dense(x.data_ptr(), ldx, k), None, wp.data_ptr(), ldw, lin.bias.data_ptr(), M, lin.out_features,
-         GM_EPI_BIAS_LEAKY if lin.act == 1 else GM_EPI_BIAS, out.data_ptr(), ldo,
+         _epi(lin.act), out.data_ptr(), ldo,
          tag=lin.tag and f"linear:{lin.tag}:{M}x{lin.out_features}x{k}", x3=pack_x3(lin))
     return out
 
@@ -486,7 +493,7 @@ def dqn_q(dqn, env_obs, obs_dim, state, h_prev, nbr, agent_node, scratch, hidden
     h1 = scratch(0, M, lin0.out_features)
     a0 = readout(state.data_ptr(), state.shape[-1], h_prev.data_ptr(), h_prev.stride(0), nbr, agent_node, N, H)
     gemm(a0, src, wp.data_ptr(), ldw, b.data_ptr(), M, lin0.out_features,
-         GM_EPI_BIAS_LEAKY if lin0.act == 1 else GM_EPI_BIAS, h1.data_ptr(), h1.stride(0),
+         _epi(lin0.act), h1.data_ptr(), h1.stride(0),
          tag=lin0.tag and f"linear:{lin0.tag}:{M}x{lin0.out_features}x{a0.k + ks}", x3=x3)
     h = h1
     hidden = list(dqn.encoder.linear_layers[1:])
@@ -511,7 +518,7 @@ def dqn_q_dense(dqn, env_obs, graph, scratch):
     wp, ldw, b, x3 = pack_dqn_first(lin0, od)
     h1 = scratch(0, M, lin0.out_features)
     gemm(dense(g2.data_ptr(), g2.stride(0), g2.shape[1]), dense(env_obs.data_ptr(), env_obs.stride(1), od),
-         wp.data_ptr(), ldw, b.data_ptr(), M, lin0.out_features, GM_EPI_BIAS_LEAKY if lin0.act == 1 else GM_EPI_BIAS,
+         wp.data_ptr(), ldw, b.data_ptr(), M, lin0.out_features, _epi(lin0.act),
          h1.data_ptr(), h1.stride(0), tag=lin0.tag and f"linear:{lin0.tag}:{M}x{lin0.out_features}x{g2.shape[1]}+{od}",
          x3=x3)
     h = h1

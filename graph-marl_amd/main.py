@@ -19,7 +19,7 @@ Differences from the reference, by design:
     consumes exactly the reference's numpy stream); one update per vector step;
   * no tensorboard: the log lines go to stdout and checkpoints / eval metrics to
     --log-dir (default runs/<date>_<host><comment>, like SummaryWriter's logdir);
-  * models: dqn, dgn, dqnr, commnet (comm_rounds 2); activation: leaky_relu only;
+  * models: dqn, dgn, dqnr, commnet (comm_rounds 2); activation: leaky_relu, relu, elu, tanh, sigmoid;
     NetMon: sum/mean aggregation, lstm/lnlstm/gru cells, carry-over on, --netmon-global.
 """
 import argparse
@@ -239,13 +239,14 @@ def build_model(args, agent_obs_size, n_actions):
     """src/main.py:486-523"""
     hidden = dim_str_to_list(args.hidden_dim)
     if args.model == "dgn":
-        return M.DGN(agent_obs_size, hidden, n_actions, args.num_heads, args.num_attention_layers)
+        return M.DGN(agent_obs_size, hidden, n_actions, args.num_heads, args.num_attention_layers,
+                     activation=args.activation_function)
     if args.model == "dqnr":
-        return M.DQNR(agent_obs_size, hidden, n_actions)
+        return M.DQNR(agent_obs_size, hidden, n_actions, activation=args.activation_function)
     if args.model == "commnet":
-        return M.CommNet(agent_obs_size, hidden, n_actions, comm_rounds=2)
+        return M.CommNet(agent_obs_size, hidden, n_actions, comm_rounds=2, activation=args.activation_function)
     if args.model == "dqn":
-        return M.DQN(agent_obs_size, hidden, n_actions)
+        return M.DQN(agent_obs_size, hidden, n_actions, activation=args.activation_function)
     raise ValueError(f"Unknown model type {args.model}")
 
 
@@ -283,8 +284,8 @@ def main(argv=None):
     set_seed(args.seed)
     if args.sequence_length <= 0:
         raise ValueError(f"Invalid sequence length {args.sequence_length}. Must be greater 0.")
-    if args.activation_function != "leaky_relu":
-        raise NotImplementedError("only --activation-function=leaky_relu is built")
+    act = args.activation_function
+    M.act_code(act)  # src/main.py:440-441 getattr(F, name): names outside model.ACTIVATIONS raise here
 
     H = args.netmon_dim
     env = make_env(args, dev, obs_extra=(5 if args.netmon_global else 4) * H if args.netmon else 0)
@@ -295,7 +296,7 @@ def main(argv=None):
         netmon = M.NetMon(node_obs_size, H, dim_str_to_list(args.netmon_encoder_dim), args.netmon_iterations,
                           rnn_type=args.netmon_rnn_type, rnn_carryover=bool(args.netmon_rnn_carryover),
                           agg_type=args.netmon_agg_type, output_neighbor_hidden=True,
-                          output_global_hidden=args.netmon_global).to(dev)
+                          output_global_hidden=args.netmon_global, activation=act).to(dev)
         node_state_size = netmon.get_state_size()
         env = W.NetMonWrapper(env, netmon, args.netmon_startup_iterations)
         env.reset()  # second reset_and_get_sizes (src/main.py:478)
@@ -340,7 +341,8 @@ def main(argv=None):
     node_aux_size = n_nodes if (netmon is not None and isinstance(base, gm.Routing)) else 0
     if netmon is not None and node_aux_size > 0 and args.aux_loss_coeff > 0:
         # NetMon aux head (src/main.py:586-594): MLP(state, (state, aux), activation_on_output=False)
-        aux_model = M.MLP(node_state_size, [node_state_size, node_aux_size], activation_on_output=False).to(dev)
+        aux_model = M.MLP(node_state_size, [node_state_size, node_aux_size], activation_on_output=False,
+                          activation=act).to(dev)
         params = params + list(aux_model.parameters())
     optimizer = torch.optim.AdamW(params, lr=args.lr)
     has_state = hasattr(model, "state")

@@ -22,6 +22,28 @@ from . import _lib as L
 
 SUM, MEAN = 0, 1
 
+# --activation-function (src/main.py:194-197, 440-441): the torch.nn.functional names the kernels
+# build (GM_ACT_* in include/graph_marl_amd.h; derivative from the layer output)
+ACTIVATIONS = {"leaky_relu": 1, "relu": 2, "elu": 3, "tanh": 4, "sigmoid": 5}
+# bias + activation epilogue code of gm_gemm_x3 / gm_gemm_f32 per activation code
+_EPI_OF_ACT = {0: 0, 1: 1, 2: 4, 3: 5, 4: 6, 5: 7}
+
+
+def act_code(activation):
+    """GM_ACT_* code of an activation given by torch.nn.functional name (or function)."""
+    if activation is None:
+        return 0
+    name = activation if isinstance(activation, str) else getattr(activation, "__name__", str(activation))
+    if name not in ACTIVATIONS:
+        raise NotImplementedError(f"--activation-function {name!r} is not built; the kernels provide "
+                                  f"{', '.join(sorted(ACTIVATIONS))}")
+    return ACTIVATIONS[name]
+
+
+def epi_code(act):
+    """gm_gemm epilogue code (GM_EPI_BIAS / GM_EPI_BIAS_<ACT>) of an activation code."""
+    return _EPI_OF_ACT[act]
+
 
 def _s():
     return L.stream_ptr()
@@ -110,7 +132,7 @@ def linear_raw(x2d, ldx, k, w, b, act, out=None, ldy=None, wcache=None, tag=None
         # split-f16 form (fp32-order error, tests/test_fused_gpu.py), as in the rollout
         x3 = (wcache if wcache is not None else _WeightCache()).x3(w)
         FU.gemm(FU.dense(x2d.data_ptr(), ldx, k, amax=None if amax is None else amax.data_ptr()), None,
-                wp.data_ptr(), ldw, L.ptr(b), m, n, act, out.data_ptr(), ldy,
+                wp.data_ptr(), ldw, L.ptr(b), m, n, epi_code(act), out.data_ptr(), ldy,
                 tag=tag and f"linear:{tag}:{m}x{n}x{k}", x3=x3)
         return out
     assert amax is None, "amax needs the split-f16 form"
@@ -215,10 +237,22 @@ class LinearFn(torch.autograd.Function):
 
 def _act_grad(act, gy, y, need_b, want_scale):
     """Backward through the layer activation: (g, bias gradient or None, gradient scale or None).
-    leaky_relu at training sizes: one fused pass (gm_leaky_bwd: mask, per-block bias partials,
+    relu / elu / tanh / sigmoid: one fused pass (gm_act_bwd). leaky_relu at training sizes: one fused pass (gm_leaky_bwd: mask, per-block bias partials,
     max|g| for the gradient GEMMs' operand scale)."""
     gb = sc = None
-    if act == 1:
+    if act > 1 and gy.is_contiguous() and y.is_contiguous():
+        # relu / elu / tanh / sigmoid: derivative from the output (gm_act_bwd), any row count
+        rows, cols = gy.shape
+        rpb = 64
+        g2 = torch.empty_like(gy)
+        part = torch.empty((rows + rpb - 1) // rpb, cols, device=gy.device)
+        sc = torch.empty(1, device=gy.device) if want_scale and rows >= 4096 else None
+        L.check(L.lib().gm_act_bwd(gy.data_ptr(), y.data_ptr(), rows, cols, act, g2.data_ptr(), part.data_ptr(), rpb,
+                                   L.ptr(sc), _s()))
+        gy = g2
+        if need_b:
+            gb = part.sum(0)
+    elif act == 1:
         if gy.is_contiguous() and y.is_contiguous() and gy.shape[0] >= 4096:
             rows, cols = gy.shape
             rpb = 64
@@ -267,7 +301,7 @@ class _JointLinearFn(torch.autograd.Function):
         y = torch.empty(R, w.shape[0], device=graph.device)
         FU.gemm(FU.dense(graph.data_ptr(), G, G, amax=None if xs is None else xs.data_ptr()),
                 FU.dense(env_obs.data_ptr(), env_obs.stride(0), od), wp.data_ptr(), ldw, bp.data_ptr(), R, w.shape[0],
-                FU.GM_EPI_BIAS_LEAKY if lin.act == 1 else FU.GM_EPI_BIAS, y.data_ptr(), w.shape[0],
+                epi_code(lin.act), y.data_ptr(), w.shape[0],
                 tag=lin.tag and f"linear:{lin.tag}:{R}x{w.shape[0]}x{G}+{od}", x3=x3)
         ctx.xs = None if xs is None else _finish_scale(xs)
         ctx.act = lin.act
@@ -322,7 +356,7 @@ class _RoutingEncFn(torch.autograd.Function):
 
 
 class Linear(nn.Linear):
-    """nn.Linear whose forward runs the fused fp32 MFMA kernel (act: 0 none, 1 leaky_relu)."""
+    """nn.Linear whose forward runs the fused MFMA kernel (act: GM_ACT_* code, 0 none, 1 leaky_relu)."""
 
     def __init__(self, in_features, out_features, bias=True, act=0):
         super().__init__(in_features, out_features, bias)
@@ -339,17 +373,19 @@ class Linear(nn.Linear):
 
 
 class MLP(nn.Module):
-    """src/model.py:13-42 (leaky_relu after every layer, including the output by default)."""
+    """src/model.py:13-42 (the activation after every layer, including the output by default;
+    activation: a torch.nn.functional name of ACTIVATIONS, the reference's activation_fn)."""
 
-    def __init__(self, in_features, mlp_units, activation_on_output=True):
+    def __init__(self, in_features, mlp_units, activation_on_output=True, activation="leaky_relu"):
         super().__init__()
         if isinstance(mlp_units, int):
             mlp_units = [mlp_units]
+        act = act_code(activation)
         self.linear_layers = nn.ModuleList()
         prev = in_features
         for i, u in enumerate(mlp_units):
             last = i == len(mlp_units) - 1
-            self.linear_layers.append(Linear(prev, u, act=0 if (last and not activation_on_output) else 1))
+            self.linear_layers.append(Linear(prev, u, act=0 if (last and not activation_on_output) else act))
             prev = u
         self.out_features = prev
 
@@ -551,9 +587,55 @@ class LSTMCell(nn.Module):
         return _LSTMPointwise.apply(gates, c.contiguous())
 
 
+class _LNLSTMFn(torch.autograd.Function):
+    """LayerNorm-LSTM gate math after the two gate GEMMs (src/layernormlstm.py:24-42) as one
+    autograd node on the HIP kernels: gm_lnlstm_fwd (one wave per row, the three LayerNorms as
+    wave reductions, row statistics saved) and gm_lnlstm_bwd (the hand-differentiated cell:
+    gradients of both raw gate rows and of c, per-wave partials of the LayerNorm and bias
+    gradients). The raw gate rows are the GEMMs' own outputs, so no activation tensor is saved."""
+
+    @staticmethod
+    def forward(ctx, gi, gh, c, wi, bi, wh, bh, bias, wc, bc, eps):
+        M, H4 = gi.shape
+        H = H4 // 4
+        h1 = torch.empty(M, H, device=gi.device)
+        c1 = torch.empty(M, H, device=gi.device)
+        stats = torch.empty(M, 8, device=gi.device)
+        L.check(L.lib().gm_lnlstm_fwd(gi.data_ptr(), gi.stride(0), gh.data_ptr(), gh.stride(0), c.data_ptr(),
+                                      c.stride(0), wi.data_ptr(), bi.data_ptr(), wh.data_ptr(), bh.data_ptr(),
+                                      bias.data_ptr(), wc.data_ptr(), bc.data_ptr(), M, H, eps, h1.data_ptr(), H,
+                                      c1.data_ptr(), H, stats.data_ptr(), _s()))
+        ctx.save_for_backward(gi, gh, c, wi, bi, wh, bh, bias, wc, bc, stats)
+        ctx.eps = eps
+        return h1, c1
+
+    @staticmethod
+    def backward(ctx, dh1, dc1):
+        gi, gh, c, wi, bi, wh, bh, bias, wc, bc, stats = ctx.saved_tensors
+        M, H4 = gi.shape
+        H = H4 // 4
+        dh1 = None if dh1 is None else dh1.contiguous()
+        dc1 = None if dc1 is None else dc1.contiguous()
+        dgi = torch.empty(M, H4, device=gi.device)
+        dgh = torch.empty(M, H4, device=gi.device)
+        dc = torch.empty(M, H, device=gi.device)
+        rpw = 8
+        part = torch.empty((M + rpw - 1) // rpw, 14 * H, device=gi.device)
+        L.check(L.lib().gm_lnlstm_bwd(gi.data_ptr(), gi.stride(0), gh.data_ptr(), gh.stride(0), c.data_ptr(),
+                                      c.stride(0), wi.data_ptr(), bi.data_ptr(), wh.data_ptr(), bh.data_ptr(),
+                                      bias.data_ptr(), wc.data_ptr(), bc.data_ptr(), stats.data_ptr(),
+                                      L.ptr(dh1), H, L.ptr(dc1), H, M, H, rpw, dgi.data_ptr(), H4, dgh.data_ptr(), H4,
+                                      dc.data_ptr(), H, part.data_ptr(), _s()))
+        ps = part.sum(0)
+        dwi, dwh, db, dwc, dbc = ps[:H4], ps[H4:2 * H4], ps[2 * H4:3 * H4], ps[3 * H4:3 * H4 + H], ps[3 * H4 + H:]
+        # d ln_in_b = d ln_hid_b = d bias_ih: separate tensors (each may become a .grad modified in place)
+        return dgi, dgh, dc, dwi, db, dwh, db.clone(), db.clone(), dwc, dbc, None
+
+
 class LayerNormLSTMCell(nn.Module):
     """src/layernormlstm.py:8-42 (LN on the input and hidden gate pre-activations and on
-    the cell, single bias). GEMMs on the MFMA kernel; the normalisations use torch."""
+    the cell, single bias): the two gate GEMMs on the MFMA kernel (LinearFn: split-f16 forward,
+    input and weight gradients), the LayerNorms and gate math in gm_lnlstm_fwd / gm_lnlstm_bwd."""
 
     def __init__(self, input_size, hidden_size):
         super().__init__()
@@ -567,21 +649,51 @@ class LayerNormLSTMCell(nn.Module):
         self.ln_input = nn.LayerNorm(4 * hidden_size)
         self.ln_hidden = nn.LayerNorm(4 * hidden_size)
         self.ln_cell = nn.LayerNorm(hidden_size)
+        self._wci, self._wch = _WeightCache(), _WeightCache()
+        self.tag = None
 
     def forward(self, x, state):
         hx, cx = state
-        gi = self.ln_input(LinearFn.apply(x, self.weight_ih, None, 0, None))
-        gh = self.ln_hidden(LinearFn.apply(hx, self.weight_hh, None, 0, None))
-        g = gi + gh + self.bias_ih
-        H = self.hidden_size
-        i, f, gg, o = torch.sigmoid(g[:, :H]), torch.sigmoid(g[:, H:2 * H]), torch.tanh(g[:, 2 * H:3 * H]), \
-            torch.sigmoid(g[:, 3 * H:])
-        cy = self.ln_cell(f * cx + i * gg)
-        return o * torch.tanh(cy), cy
+        gi = LinearFn.apply(x, self.weight_ih, None, 0, self._wci, self.tag)
+        gh = LinearFn.apply(hx, self.weight_hh, None, 0, self._wch, self.tag and self.tag + ".hh")
+        li, lh, lc = self.ln_input, self.ln_hidden, self.ln_cell
+        return _LNLSTMFn.apply(gi.reshape(-1, 4 * self.hidden_size), gh.reshape(-1, 4 * self.hidden_size),
+                               cx.contiguous(), li.weight, li.bias, lh.weight, lh.bias, self.bias_ih, lc.weight,
+                               lc.bias, float(li.eps))
+
+
+class _GRUFn(torch.autograd.Function):
+    """nn.GRUCell gate math after the two gate GEMMs as one autograd node (gm_gru_pointwise /
+    gm_gru_bwd; backward recomputes r, z, n from the saved gate rows)."""
+
+    @staticmethod
+    def forward(ctx, gi, gh, h):
+        M, H3 = gi.shape
+        H = H3 // 3
+        h1 = torch.empty(M, H, device=gi.device)
+        L.check(L.lib().gm_gru_pointwise(gi.data_ptr(), gi.stride(0), gh.data_ptr(), gh.stride(0), h.data_ptr(),
+                                         h.stride(0), M, H, h1.data_ptr(), H, _s()))
+        ctx.save_for_backward(gi, gh, h)
+        return h1
+
+    @staticmethod
+    def backward(ctx, dh1):
+        gi, gh, h = ctx.saved_tensors
+        M, H3 = gi.shape
+        H = H3 // 3
+        dh1 = dh1.contiguous()
+        dgi = torch.empty(M, H3, device=gi.device)
+        dgh = torch.empty(M, H3, device=gi.device)
+        dh = torch.empty(M, H, device=gi.device)
+        L.check(L.lib().gm_gru_bwd(gi.data_ptr(), gi.stride(0), gh.data_ptr(), gh.stride(0), h.data_ptr(), h.stride(0),
+                                   dh1.data_ptr(), H, M, H, dgi.data_ptr(), H3, dgh.data_ptr(), H3, dh.data_ptr(), H,
+                                   _s()))
+        return dgi, dgh, dh
 
 
 class GRUCell(nn.Module):
-    """nn.GRUCell semantics (r, z, n) with the GEMMs on the MFMA kernel."""
+    """nn.GRUCell semantics (r, z, n): the two gate GEMMs on the MFMA kernel (LinearFn), the gate
+    math in gm_gru_pointwise / gm_gru_bwd."""
 
     def __init__(self, input_size, hidden_size):
         super().__init__()
@@ -593,15 +705,14 @@ class GRUCell(nn.Module):
         stdv = 1.0 / math.sqrt(hidden_size)
         for p in self.parameters():
             nn.init.uniform_(p, -stdv, stdv)
+        self._wci, self._wch = _WeightCache(), _WeightCache()
+        self.tag = None
 
     def forward(self, x, h):
-        gi = LinearFn.apply(x, self.weight_ih, self.bias_ih, 0, None)
-        gh = LinearFn.apply(h, self.weight_hh, self.bias_hh, 0, None)
+        gi = LinearFn.apply(x, self.weight_ih, self.bias_ih, 0, self._wci, self.tag)
+        gh = LinearFn.apply(h, self.weight_hh, self.bias_hh, 0, self._wch, self.tag and self.tag + ".hh")
         H = self.hidden_size
-        r = torch.sigmoid(gi[:, :H] + gh[:, :H])
-        z = torch.sigmoid(gi[:, H:2 * H] + gh[:, H:2 * H])
-        n = torch.tanh(gi[:, 2 * H:] + r * gh[:, 2 * H:])
-        return (1 - z) * n + z * h
+        return _GRUFn.apply(gi.reshape(-1, 3 * H), gh.reshape(-1, 3 * H), h.contiguous())
 
 
 def dense_to_nbr(mask, max_degree=None):
@@ -635,7 +746,8 @@ class NetMon(nn.Module):
     """
 
     def __init__(self, in_features, hidden_features, encoder_units, iterations, rnn_type="lstm",
-                 rnn_carryover=True, agg_type="sum", output_neighbor_hidden=True, output_global_hidden=False):
+                 rnn_carryover=True, agg_type="sum", output_neighbor_hidden=True, output_global_hidden=False,
+                 activation="leaky_relu"):
         super().__init__()
         if agg_type not in ("sum", "mean"):
             raise NotImplementedError(f"agg_type {agg_type!r}: only sum/mean are built (torch_geometric variants "
@@ -643,7 +755,7 @@ class NetMon(nn.Module):
         if not rnn_carryover and iterations < 1:
             raise ValueError("rnn_carryover=False needs netmon iterations >= 1 (the reference's update "
                              "cell output is the stored state)")
-        self.encode = MLP(in_features, (*encoder_units, hidden_features))
+        self.encode = MLP(in_features, (*encoder_units, hidden_features), activation=activation)
         self._hc = None  # carry-over LSTM state kept as its (h, c) rows (training), see state
         self.state = None
         self.iterations = iterations
@@ -794,7 +906,17 @@ class NetMon(nn.Module):
         return res.reshape(B, R, -1)
 
     def forward(self, x, mask, node_agent_matrix=None, max_degree=None, no_agent_mapping=False):
-        nbr = dense_to_nbr(mask, max_degree)
+        # the neighbour table holds every neighbour (aggregation always uses the full mask,
+        # src/model.py:582-593); max_degree only sizes the readout: below the true degree the
+        # reference's _get_neighbor_h fails, above it the extra slots read zeros (-1 columns,
+        # which the aggregate skips)
+        nbr = dense_to_nbr(mask)
+        if max_degree is not None:
+            md = int(max_degree)
+            if md < nbr.shape[-1]:
+                raise ValueError(f"max_degree {md} is below the largest node degree {nbr.shape[-1]} of the batch")
+            if md > nbr.shape[-1]:
+                nbr = F.pad(nbr, (0, md - nbr.shape[-1]), value=-1).contiguous()
         an = None if (no_agent_mapping or node_agent_matrix is None) else node_agent_to_index(node_agent_matrix)
         return self.forward_graph(x, nbr, an)
 
@@ -815,9 +937,9 @@ class Q_Net(nn.Module):
 class DQN(nn.Module):
     """src/model.py:187-203: MLP encoder (activation on output) + linear Q head."""
 
-    def __init__(self, in_features, mlp_units, num_actions):
+    def __init__(self, in_features, mlp_units, num_actions, activation="leaky_relu"):
         super().__init__()
-        self.encoder = MLP(in_features, mlp_units)
+        self.encoder = MLP(in_features, mlp_units, activation=activation)
         self.q_net = Q_Net(self.encoder.out_features, num_actions)
 
     def forward(self, x, mask=None):
@@ -879,13 +1001,14 @@ class AttModel(nn.Module):
     masked by the agent adjacency (-1e9), att v + v, heads concatenated, act(fc_out).
     forward returns (out, att_weights) with the weights before masking, like the reference."""
 
-    def __init__(self, in_features, k_features, v_features, out_features, num_heads):
+    def __init__(self, in_features, k_features, v_features, out_features, num_heads, activation="leaky_relu"):
         super().__init__()
         self.k_features, self.v_features, self.num_heads = k_features, v_features, num_heads
-        self.fc_v = Linear(in_features, v_features * num_heads, act=1)
-        self.fc_k = Linear(in_features, k_features * num_heads, act=1)
-        self.fc_q = Linear(in_features, k_features * num_heads, act=1)
-        self.fc_out = Linear(v_features * num_heads, out_features, act=1)
+        act = act_code(activation)  # the reference's DGN passes activation_fn as both vkq and output act
+        self.fc_v = Linear(in_features, v_features * num_heads, act=act)
+        self.fc_k = Linear(in_features, k_features * num_heads, act=act)
+        self.fc_q = Linear(in_features, k_features * num_heads, act=act)
+        self.fc_out = Linear(v_features * num_heads, out_features, act=act)
         self.attention_scale = 1 / (k_features ** 0.5)
 
     def forward(self, x, mask):
@@ -923,12 +1046,13 @@ class DGN(nn.Module):
     the encoder output and every attention layer's output. att_weights holds the
     per-layer weights of the last forward (attention regularisation, src/main.py:924-954)."""
 
-    def __init__(self, in_features, mlp_units, num_actions, num_heads=8, num_attention_layers=2):
+    def __init__(self, in_features, mlp_units, num_actions, num_heads=8, num_attention_layers=2,
+                 activation="leaky_relu"):
         super().__init__()
-        self.encoder = MLP(in_features, mlp_units)
+        self.encoder = MLP(in_features, mlp_units, activation=activation)
         hidden = self.encoder.out_features
         self.att_layers = nn.ModuleList(
-            [AttModel(hidden, 16, 16, hidden, num_heads) for _ in range(num_attention_layers)])
+            [AttModel(hidden, 16, 16, hidden, num_heads, activation) for _ in range(num_attention_layers)])
         self.q_net = Q_Net(hidden * (num_attention_layers + 1), num_actions)
         self.att_weights = []
 
@@ -983,9 +1107,9 @@ class DQNR(nn.Module):
     state, Q head. `state` is [B, A, 2H] ([h | c] per agent) or None (= zeros) between
     calls, like the reference's external layout (_state_reshape_out)."""
 
-    def __init__(self, in_features, mlp_units, num_actions):
+    def __init__(self, in_features, mlp_units, num_actions, activation="leaky_relu"):
         super().__init__()
-        self.encoder = MLP(in_features, mlp_units)
+        self.encoder = MLP(in_features, mlp_units, activation=activation)
         H = self.encoder.out_features
         self.lstm = LSTMCell(H, H)
         self.state = None
@@ -1049,8 +1173,8 @@ class CommNet(DQNR):
     1) and fed through the LSTM again as both input and hidden state (cell states are not
     communicated, as in IC3Net)."""
 
-    def __init__(self, in_features, mlp_units, num_actions, comm_rounds=2):
-        super().__init__(in_features, mlp_units, num_actions)
+    def __init__(self, in_features, mlp_units, num_actions, comm_rounds=2, activation="leaky_relu"):
+        super().__init__(in_features, mlp_units, num_actions, activation)
         assert comm_rounds >= 0
         self.comm_rounds = comm_rounds
 

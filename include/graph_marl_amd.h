@@ -211,12 +211,43 @@ int gm_lnlstm_pointwise(const float* g, int64_t ldg, const float* c, int64_t ldc
                         const float* ln_in_b, const float* ln_hid_w, const float* ln_hid_b, const float* bias,
                         const float* ln_cell_w, const float* ln_cell_b, int32_t m, int32_t H, float eps, float* h1,
                         int64_t ldh, float* c1, int64_t ldc1, void* stream);
+/* Training forms of the LayerNorm-LSTM cell (replace LayerNormLSTMCell.forward under autograd,
+ * src/layernormlstm.py:24-42; the reference differentiates it with torch autograd). gm_lnlstm_fwd:
+ * as gm_lnlstm_pointwise with the two gate GEMM outputs as separate strided row sets gi, gh
+ * ([m][4H] each) and the row statistics stats[m][8] = (mean, 1/std) of gi, gh and the cell
+ * pre-norm saved for gm_lnlstm_bwd. gm_lnlstm_bwd: dh1 / dc1 (either nullable) -> d gi, d gh
+ * ([m][4H] strided), d c ([m][H]) and per-wave parameter-gradient partials part[ceil(m /
+ * rows_per_wave)][14H] = [d ln_in_w (4H) | d ln_hid_w (4H) | d bias (4H; equal to d ln_in_b and
+ * d ln_hid_b) | d ln_cell_w (H) | d ln_cell_b (H)] (the caller sums the rows). */
+int gm_lnlstm_fwd(const float* gi, int64_t ldgi, const float* gh, int64_t ldgh, const float* c, int64_t ldc,
+                  const float* ln_in_w, const float* ln_in_b, const float* ln_hid_w, const float* ln_hid_b,
+                  const float* bias, const float* ln_cell_w, const float* ln_cell_b, int32_t m, int32_t H, float eps,
+                  float* h1, int64_t ldh, float* c1, int64_t ldc1, float* stats, void* stream);
+int gm_lnlstm_bwd(const float* gi, int64_t ldgi, const float* gh, int64_t ldgh, const float* c, int64_t ldc,
+                  const float* ln_in_w, const float* ln_in_b, const float* ln_hid_w, const float* ln_hid_b,
+                  const float* bias, const float* ln_cell_w, const float* ln_cell_b, const float* stats,
+                  const float* dh1, int64_t lddh, const float* dc1, int64_t lddc, int32_t m, int32_t H,
+                  int32_t rows_per_wave, float* dgi, int64_t lddgi, float* dgh, int64_t lddgh, float* dc,
+                  int64_t lddco, float* part, void* stream);
+/* GRU cell gate math (torch.nn.GRUCell, used by NetMon rnn_type gru, src/model.py:387-393) after its
+ * two GEMMs gi = x W_ih^T + b_ih, gh = h W_hh^T + b_hh ([m][3H] strided, gates r, z, n):
+ * h1 = (1 - z) n + z h. gm_gru_bwd: dh1 -> d gi, d gh ([m][3H]) and the direct d h ([m][H]). */
+int gm_gru_pointwise(const float* gi, int64_t ldgi, const float* gh, int64_t ldgh, const float* h, int64_t ldh,
+                     int32_t m, int32_t H, float* h1, int64_t ldh1, void* stream);
+int gm_gru_bwd(const float* gi, int64_t ldgi, const float* gh, int64_t ldgh, const float* h, int64_t ldh,
+               const float* dh1, int64_t lddh1, int32_t m, int32_t H, float* dgi, int64_t lddgi, float* dgh,
+               int64_t lddgh, float* dh, int64_t lddh, void* stream);
 /* Backward of a Linear followed by leaky_relu (MLP layers, src/model.py:13-42): g = dY where
  * Y >= 0 else slope * dY ([rows][cols] contiguous), and per-block column sums of g for the bias
  * gradient: part[ceil(rows / rows_per_block)][cols] (the caller sums the blocks); g_scale
  * (nullable) receives the power-of-two scale of g (as gm_absmax_scale, without a second pass). */
 int gm_leaky_bwd(const float* dy, const float* y, int64_t rows, int32_t cols, float slope, float* g, float* part,
                  int32_t rows_per_block, float* g_scale, void* stream);
+/* The same for any GM_ACT_* layer activation (derivative from the output y: relu y > 0, elu
+ * y > 0 ? 1 : y + 1, tanh 1 - y^2, sigmoid y (1 - y); replaces torch autograd of the reference's
+ * activation_fn, src/model.py:13-42). */
+int gm_act_bwd(const float* dy, const float* y, int64_t rows, int32_t cols, int32_t act, float* g, float* part,
+               int32_t rows_per_block, float* g_scale, void* stream);
 /* Backward of gm_mp_aggregate for symmetric adjacency: dh[j] = Σ_{n ∈ {j} ∪ nbr(j)} dout[n] / cnt(n). */
 int gm_mp_aggregate_bwd(const float* dout, const int32_t* nbr, int32_t n_graphs, int32_t n_nodes, int32_t deg,
                         int32_t hidden, int32_t mode, float* dh, void* stream);
@@ -295,7 +326,12 @@ int gm_linear_f32(const float* x, int64_t ldx, const float* w, int64_t ldw, cons
  * LSTMCell gate GEMM (src/model.py:379-382) with the aggregate (206-229) and the readout +
  * agent gather (582-631) folded into the A-operand load. */
 enum { GM_A_DENSE = 0, GM_A_AGGREGATE = 1, GM_A_READOUT = 2 };
-enum { GM_EPI_BIAS = 0, GM_EPI_BIAS_LEAKY = 1, GM_EPI_LSTM = 2, GM_EPI_GRU = 3 };
+enum { GM_EPI_BIAS = 0, GM_EPI_BIAS_LEAKY = 1, GM_EPI_LSTM = 2, GM_EPI_GRU = 3, GM_EPI_BIAS_RELU = 4,
+       GM_EPI_BIAS_ELU = 5, GM_EPI_BIAS_TANH = 6, GM_EPI_BIAS_SIGMOID = 7 };
+/* Layer activations (--activation-function, src/main.py:194-197, 440-441; MLP / AttModel,
+ * src/model.py:13-42, 86-117): the torch.nn.functional names whose derivative follows from the
+ * layer output. GM_EPI_BIAS_<ACT> = bias + activation epilogue; act arguments take GM_ACT_*. */
+enum { GM_ACT_NONE = 0, GM_ACT_LEAKY_RELU = 1, GM_ACT_RELU = 2, GM_ACT_ELU = 3, GM_ACT_TANH = 4, GM_ACT_SIGMOID = 5 };
 typedef struct {
     int32_t mode;              /* GM_A_*                                                           */
     const float* p0;           /* DENSE: rows; AGGREGATE: node rows h; READOUT: h_final node rows  */

@@ -20,12 +20,27 @@ def linear(x, w, b=None):
     return y if b is None else y + b
 
 
-def mlp(x, W, prefix, n_layers, act_on_output=True):
+def activation(x, name="leaky_relu"):
+    """torch.nn.functional activations selectable by --activation-function (src/main.py:440-441)."""
+    if name == "leaky_relu":
+        return leaky_relu(x)
+    if name == "relu":
+        return np.maximum(x, 0.0)
+    if name == "elu":
+        return np.where(x > 0, x, np.expm1(np.minimum(x, 0.0)))
+    if name == "tanh":
+        return np.tanh(x)
+    if name == "sigmoid":
+        return sigmoid(x)
+    raise ValueError(f"activation {name!r} not restated")
+
+
+def mlp(x, W, prefix, n_layers, act_on_output=True, act="leaky_relu"):
     """src/model.py:13-42 MLP (activation also on the output by default)."""
     for i in range(n_layers):
         x = linear(x, W[f"{prefix}.linear_layers.{i}.weight"], W[f"{prefix}.linear_layers.{i}.bias"])
         if i < n_layers - 1 or act_on_output:
-            x = leaky_relu(x)
+            x = activation(x, act)
     return x
 
 
@@ -66,7 +81,8 @@ def gru_cell(x, h, W, p):
     return (1 - z) * n + z * h
 
 
-def netmon_forward(W, x, adj, state, rnn="lstm", agg="sum", K=1, n_enc_layers=3, global_h=False, carryover=True):
+def netmon_forward(W, x, adj, state, rnn="lstm", agg="sum", K=1, n_enc_layers=3, global_h=False, carryover=True,
+                   act="leaky_relu", dtype=np.float64):
     """src/model.py:451-622 NetMon.forward with output_neighbor_hidden=True,
     no_agent_mapping=True; global_h adds the --netmon-global readout (mean of h over the
     graph's nodes after h, src/model.py:461-462, 624-627). carryover=False
@@ -75,17 +91,20 @@ def netmon_forward(W, x, adj, state, rnn="lstm", agg="sum", K=1, n_enc_layers=3,
     state instead of the obs cell's output.
 
     x [B,N,F], adj [B,N,N] (I+A), state [B,N,S] or None.
+    dtype np.float32 with float32 weights: the same formulas in fp32 arithmetic (what an fp32
+    implementation of the reference, e.g. its own torch CPU run, computes), to measure fp32's own
+    deviation from the fp64 result.
     Returns (out [B,N,4H] ([B,N,5H] with global_h), new_state [B,N,S])."""
-    x = np.asarray(x, np.float64)
-    adj = np.asarray(adj, np.float64)
+    x = np.asarray(x, dtype)
+    adj = np.asarray(adj, dtype)
     B, N, _ = x.shape
     H = W["rnn_obs.weight_hh"].shape[-1]
     nc = 1 if rnn == "gru" else 2  # tensors per cell state
     ns = nc * (1 if carryover else 2)
     if state is None:
-        state = np.zeros((B, N, ns * H))
-    st = np.asarray(state, np.float64).reshape(B * N, ns, H)
-    h = mlp(x.reshape(B * N, -1), W, "encode", n_enc_layers)
+        state = np.zeros((B, N, ns * H), dtype)
+    st = np.asarray(state, dtype).reshape(B * N, ns, H)
+    h = mlp(x.reshape(B * N, -1), W, "encode", n_enc_layers, act=act)
     c = None
     if rnn == "lstm":
         h, c = lstm_cell(h, st[:, 0], st[:, 1], W, "rnn_obs")
@@ -143,9 +162,9 @@ def to_network_obs(out, node_agent):
     return np.einsum("bna,bnf->baf", np.asarray(node_agent, np.float64), out)
 
 
-def dqn_forward(W, obs, n_layers=2):
+def dqn_forward(W, obs, n_layers=2, act="leaky_relu"):
     """src/model.py:187-203 DQN: MLP encoder (activation on output) + linear Q head."""
-    h = mlp(np.asarray(obs, np.float64), W, "encoder", n_layers)
+    h = mlp(np.asarray(obs, np.float64), W, "encoder", n_layers, act=act)
     return linear(h, W["q_net.fc.weight"], W["q_net.fc.bias"])
 
 

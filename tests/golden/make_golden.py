@@ -538,7 +538,7 @@ def _store(d, key, arr, compact, seed):
 
 def gen_train(out, Network, Routing, EVAL_SEEDS, NetMon, DQN, interpolate_model, aux_coeff=0.0, MLP=None,
               rnn_type="lstm", agg="sum", K=1, H=32, enc=(64, 48), dqn_hidden=(64, 32), B=3, L=3, compact=False,
-              det_seed=0):
+              det_seed=0, act="leaky_relu"):
     """One DQN+NetMon update exactly as src/main.py:832-1022 performs it (sequence replay);
     aux_coeff > 0 adds the NetMon aux head and loss (src/main.py:586-594, 868-875, 996-1000).
     rnn_type / agg / K / H / enc / dqn_hidden select the architecture (src/model.py:451-631,
@@ -557,11 +557,12 @@ def gen_train(out, Network, Routing, EVAL_SEEDS, NetMon, DQN, interpolate_model,
                                                                      aux=aux_l)
     rng = np.random.RandomState(5)
     torch.manual_seed(3)
-    netmon = NetMon(node_obs.shape[-1], H, list(enc), K, F.leaky_relu, rnn_type=rnn_type,
+    act_fn = getattr(F, act)  # src/main.py:440-441
+    netmon = NetMon(node_obs.shape[-1], H, list(enc), K, act_fn, rnn_type=rnn_type,
                     rnn_carryover=True, agg_type=agg, output_neighbor_hidden=True)
     obs_dim = agent_obs.shape[-1] + netmon.get_out_features()
-    model = DQN(obs_dim, list(dqn_hidden), 4, F.leaky_relu)
-    d["arch"] = np.array(f"{rnn_type}|{agg}|{K}|{H}|{enc[0]},{enc[1]}|{dqn_hidden[0]},{dqn_hidden[1]}")
+    model = DQN(obs_dim, list(dqn_hidden), 4, act_fn)
+    d["arch"] = np.array(f"{rnn_type}|{agg}|{K}|{H}|{enc[0]},{enc[1]}|{dqn_hidden[0]},{dqn_hidden[1]}|{act}")
     if compact:
         with torch.no_grad():
             for prefix, mod in (("netmon.", netmon), ("model.", model)):
@@ -1042,6 +1043,10 @@ def main():
         # (256 graphs x 20 nodes = 5120 rows per step, 20480 over the 4 steps)
         gen_train(os.path.join(HERE, "train_big.npz"), Network, Routing, EVAL_SEEDS, NetMon, DQN, interpolate_model,
                   H=128, enc=(512, 256), dqn_hidden=(512, 256), B=256, L=4, compact=True, det_seed=11)
+    for act in ("relu", "elu", "tanh", "sigmoid"):  # --activation-function (src/main.py:194-197, 440-441)
+        if only is None or f"train_{act}" in only:
+            gen_train(os.path.join(HERE, f"train_{act}.npz"), Network, Routing, EVAL_SEEDS, NetMon, DQN,
+                      interpolate_model, K=2, B=4, act=act)
     if only is None or "checkpoint" in only:
         gen_checkpoint(os.path.join(HERE, "ref_checkpoint.pt"), os.path.join(HERE, "ref_checkpoint.npz"), args.ref,
                        Network, Routing, EVAL_SEEDS, NetMon, DQN, get_state_dict)

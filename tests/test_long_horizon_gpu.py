@@ -7,7 +7,12 @@ topologies (EVAL_SEEDS excluded), A = 20 packets, NetMon K = 1 (lstm, sum) + DQN
 Config 4 (random 10-50-node topologies) at N = 10, 30, 40, 50: 512 envs in 2 groups, 30-step
 episodes, 70 steps (two resets) — this covers the N-dependent rows per block of the routing
 encoder, DQN layer 1 on the folded GEMM-ready obs (K = 512 + 6N + 8, not a whole number of k
-tiles off N = 20), the aggregate and the readout at those sizes.
+tiles off N = 20), the aggregate and the readout at those sizes. The LayerNorm-LSTM and GRU NetMon
+cells (--netmon-rnn-type lnlstm / gru, src/layernormlstm.py, src/model.py:387-393): 1024 envs,
+N = 20, the same 120 steps. Other --activation-function values (elu, tanh: the GEMM epilogues,
+the routing encoder and the fused Q head): 512 envs, N = 20, 70 steps. The LN-LSTM bound is the fp32
+envelope described at netmon_check (the 1e-5 contract is out of reach for any fp32 evaluation of that
+cell over carried steps).
 Eight envs spread over both groups are shadowed every step by
   * the C oracle env (oracle/gm_oracle.c) fed the GPU's Q-values, which must take the same
     ε-greedy actions and give bit-identical rewards, done flags, agent and node observations
@@ -28,8 +33,11 @@ pytestmark = pytest.mark.gpu
 
 A, G, EPS = 20, 2, 0.5
 TOL = 1e-5
-# (N, envs, episode steps, vector steps)
-CASES = [(20, 4096, 50, 120), (10, 512, 30, 70), (30, 512, 30, 70), (40, 512, 30, 70), (50, 512, 30, 70)]
+# (N, envs, episode steps, vector steps, NetMon cell, --activation-function)
+CASES = [(20, 4096, 50, 120, "lstm", "leaky_relu"), (10, 512, 30, 70, "lstm", "leaky_relu"),
+         (30, 512, 30, 70, "lstm", "leaky_relu"), (40, 512, 30, 70, "lstm", "leaky_relu"),
+         (50, 512, 30, 70, "lstm", "leaky_relu"), (20, 1024, 50, 120, "lnlstm", "leaky_relu"),
+         (20, 1024, 50, 120, "gru", "leaky_relu"), (20, 512, 30, 70, "lstm", "elu"), (20, 512, 30, 70, "lstm", "tanh")]
 
 
 def adjacency(topo, N):
@@ -41,12 +49,12 @@ def adjacency(topo, N):
     return m
 
 
-@pytest.mark.parametrize("case", CASES, ids=[f"N{c[0]}" for c in CASES])
+@pytest.mark.parametrize("case", CASES, ids=[f"N{c[0]}-{c[4]}-{c[5]}" for c in CASES])
 @pytest.mark.parametrize("form", ["x3", "f32"])
 def test_benched_rollout_long_horizon(form, case, monkeypatch, oracle_mod):
     import netmon_ref
 
-    N, B, EP, STEPS = case
+    N, B, EP, STEPS, RNN, ACT = case
     SAMPLE = sorted({0, 1, B // 5, B // 2 - 1, B // 2, B // 2 + 1, (4 * B) // 5, B - 1})
 
     gm = importlib.import_module("graph-marl_amd")
@@ -56,8 +64,8 @@ def test_benched_rollout_long_horizon(form, case, monkeypatch, oracle_mod):
     gm._lib.range_status(clear=True)
     net = gm.Network(N, random_topology=True, excluded_seeds=gm.EVAL_SEEDS, device=0)
     torch.manual_seed(0)
-    netmon = M.NetMon(4 * N + 8, 128, [512, 256], 1).cuda()
-    dqn = M.DQN(6 * N + 10 + netmon.get_out_features(), [512, 256], 4).cuda()
+    netmon = M.NetMon(4 * N + 8, 128, [512, 256], 1, rnn_type=RNN, activation=ACT).cuda()
+    dqn = M.DQN(6 * N + 10 + netmon.get_out_features(), [512, 256], 4, activation=ACT).cuda()
     ro = RO.StreamedRollout(net, A, B, netmon, dqn, groups=G, seed=0, epsilon=EPS, episode_steps=EP, device=0)
     per = B // G
     Wn = {k: v.detach().double().cpu().numpy() for k, v in netmon.state_dict().items()}
@@ -99,6 +107,14 @@ def test_benched_rollout_long_horizon(form, case, monkeypatch, oracle_mod):
         return out
 
     state64, worst = {}, {"state": 0.0, "readout": 0.0, "q": 0.0}
+    # LN-LSTM: the carried state is ill-conditioned (the cell LayerNorm divides by the spread of
+    # c), so an fp32 evaluation of the reference's own formula drifts from fp64 far beyond 1e-5
+    # (tests/test_long_horizon_gpu.py history: 7.5e-4 over 50 steps on the C-oracle env). The
+    # same formulas in fp32 (netmon_ref, dtype float32, carried from their own fp32 state) run
+    # beside the fp64 ones, and the GPU must stay within max(1e-5, 4 x the worst fp32 drift so far)
+    fp32_envelope = RNN == "lnlstm"
+    Wn32 = {k: v.astype(np.float32) for k, v in Wn.items()}
+    state32, worst32 = {}, {"state": 0.0, "readout": 0.0}
 
     def netmon_check(e, o, v, t):
         ob = o.observe()
@@ -106,13 +122,23 @@ def test_benched_rollout_long_horizon(form, case, monkeypatch, oracle_mod):
         assert (v["node_obs"] == ob["node_obs"]).all(), f"step {t} env {e}: node obs"
         adj = adjacency(o.topology(), N)
         assert (v["adj"] == adj).all(), f"step {t} env {e}: I+A adjacency"
-        out, st = netmon_ref.netmon_forward(Wn, ob["node_obs"][None], adj[None], state64.get(e), "lstm", "sum", 1)
+        out, st = netmon_ref.netmon_forward(Wn, ob["node_obs"][None], adj[None], state64.get(e), RNN, "sum", 1, act=ACT)
         state64[e] = st
         ro_ = netmon_ref.to_network_obs(out, ob["node_agent"][None])[0]
+        tol_s = tol_r = TOL
+        if fp32_envelope:
+            out32, st32 = netmon_ref.netmon_forward(Wn32, ob["node_obs"][None].astype(np.float32),
+                                                    adj[None].astype(np.float32), state32.get(e), RNN, "sum", 1,
+                                                    act=ACT, dtype=np.float32)
+            state32[e] = st32
+            ro32 = netmon_ref.to_network_obs(out32, ob["node_agent"][None])[0]
+            worst32["state"] = max(worst32["state"], np.abs(st32 - st).max())
+            worst32["readout"] = max(worst32["readout"], np.abs(ro32 - ro_).max())
+            tol_s, tol_r = max(TOL, 4 * worst32["state"]), max(TOL, 4 * worst32["readout"])
         es = np.abs(v["state"] - st[0]).max()
         er = np.abs(v["readout"] - ro_).max()
         worst["state"], worst["readout"] = max(worst["state"], es), max(worst["readout"], er)
-        assert es < TOL and er < TOL, f"step {t} env {e}: NetMon state err {es}, readout err {er}"
+        assert es < tol_s and er < tol_r, f"step {t} env {e}: NetMon state err {es}, readout err {er} (tol {tol_s}, {tol_r})"
         return np.concatenate([ob["obs"].astype(np.float64), ro_], -1)
 
     ro.reset()
@@ -127,10 +153,10 @@ def test_benched_rollout_long_horizon(form, case, monkeypatch, oracle_mod):
         for e, o in orc.items():
             g, i = loc[e]
             q = qrec[g][i].cpu().numpy()
-            q64 = netmon_ref.dqn_forward(Wd, joint[e])
+            q64 = netmon_ref.dqn_forward(Wd, joint[e], act=ACT)
             eq = np.abs(q - q64).max()
             worst["q"] = max(worst["q"], eq)
-            assert eq < TOL, f"step {t} env {e}: Q err {eq}"
+            assert eq < (max(TOL, 4 * worst32["readout"]) if fp32_envelope else TOL), f"step {t} env {e}: Q err {eq}"
             exp = o.draw_egreedy(q, EPS)
             assert (exp == acts[g][i]).all(), f"step {t} env {e}: ε-greedy actions"
             rew, done, _ = o.step(acts[g][i])
@@ -138,8 +164,10 @@ def test_benched_rollout_long_horizon(form, case, monkeypatch, oracle_mod):
             if t % EP == 0:  # the rollout reset the episode after this step: new topology, NetMon start-up
                 o.reset()
                 state64.pop(e)
+                state32.pop(e, None)
             joint[e] = netmon_check(e, o, v[e], t)
         resets += t % EP == 0
     assert resets == STEPS // EP >= 2
     gm._lib.check_range()
-    print(f"N={N} form {form}: worst |err| over {STEPS} steps x {len(SAMPLE)} envs: {worst}")
+    print(f"N={N} {RNN} {ACT} form {form}: worst |err| over {STEPS} steps x {len(SAMPLE)} envs: {worst}"
+          + (f"; fp32 restatement of the reference formula vs fp64: {worst32}" if fp32_envelope else ""))

@@ -142,7 +142,8 @@ def test_oracle_bench_driver_runs(oracle_mod):
     assert (obs[..., :20].sum(-1) == 1).all() and (obs[..., 20:40].sum(-1) == 1).all()
 
 
-@pytest.mark.parametrize("name", ["train.npz", "train_big.npz", "train_lnlstm.npz", "train_gru.npz"])
+@pytest.mark.parametrize("name", ["train.npz", "train_big.npz", "train_lnlstm.npz", "train_gru.npz", "train_relu.npz",
+                                  "train_elu.npz", "train_tanh.npz", "train_sigmoid.npz"])
 def test_train_golden_forward_matches_restatement(name):
     """The golden DQN+NetMon updates' Q / Q-target / loss follow from their weights (stored, or for
     the compact production-size golden regenerated by tests/golden/detparams.py) through the fp64
@@ -152,15 +153,16 @@ def test_train_golden_forward_matches_restatement(name):
     g = np.load(f"{R.GOLDEN}/{name}")
     Wn, Wm, Wt, state = GU.weights_np(g)
     rnn, agg, K, H, enc, dq = GU.arch(g)
+    act = GU.activation(g)
     tot, L = 0.0, g["actions"].shape[0]
     gamma = float(g["gamma"])
     for t in range(L):
-        out, ns = netmon_ref.netmon_forward(Wn, g["node_obs"][t], g["node_adj"][t], state, rnn, agg, K)
+        out, ns = netmon_ref.netmon_forward(Wn, g["node_obs"][t], g["node_adj"][t], state, rnn, agg, K, act=act)
         obs = np.concatenate([g["agent_obs"][t], netmon_ref.to_network_obs(out, g["node_agent"][t])], -1)
-        q = netmon_ref.dqn_forward(Wm, obs)
-        out2, _ = netmon_ref.netmon_forward(Wn, g["node_obs"][t + 1], g["node_adj"][t + 1], ns, rnn, agg, K)
+        q = netmon_ref.dqn_forward(Wm, obs, act=act)
+        out2, _ = netmon_ref.netmon_forward(Wn, g["node_obs"][t + 1], g["node_adj"][t + 1], ns, rnn, agg, K, act=act)
         nobs = np.concatenate([g["agent_obs"][t + 1], netmon_ref.to_network_obs(out2, g["node_agent"][t + 1])], -1)
-        nq = netmon_ref.dqn_forward(Wt, nobs).max(-1)
+        nq = netmon_ref.dqn_forward(Wt, nobs, act=act).max(-1)
         qt = q.copy()
         tgt = g["reward"][t] + (1 - g["done"][t]) * gamma * nq
         np.put_along_axis(qt, g["actions"][t][..., None].astype(np.int64), tgt[..., None], -1)
