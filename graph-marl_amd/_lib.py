@@ -78,7 +78,7 @@ class EnvState(C.Structure):
     _fields_ = [(k, C.c_void_p) for k in [
         "now", "target", "edge", "time", "ttl", "start", "spw", "agent_steps", "size", "visited", "amask",
         "loads", "topo_seed", "topo_reps", "edge_a", "edge_b", "edge_len", "nbr_edge", "apsp", "rng_key",
-        "rng_pos"]]
+        "rng_pos", "seq_index"]]
 
 
 class PCG64(C.Structure):

@@ -1557,7 +1557,8 @@ extern "C" int gm_env_get_state(gm_env* env, gm_env_state* st) {
         (rc = d2h(st->amask, d.amask, B * A * 4)) || (rc = d2h(st->loads, d.load, B * E)) ||
         (rc = d2h(st->topo_seed, d.topo_seed, B)) || (rc = d2h(st->topo_reps, d.topo_reps, B)) ||
         (rc = d2h(st->edge_a, d.edge_a, B * E)) || (rc = d2h(st->edge_b, d.edge_b, B * E)) ||
-        (rc = d2h(st->edge_len, d.edge_len, B * E)) || (rc = d2h(st->nbr_edge, d.nbr_edge, B * N * 3)))
+        (rc = d2h(st->edge_len, d.edge_len, B * E)) || (rc = d2h(st->nbr_edge, d.nbr_edge, B * N * 3)) ||
+        (rc = d2h(st->seq_index, d.seq_index, B)))
         return rc;
     if (st->apsp) {
         std::vector<int16_t> tmp(B * N * N);
@@ -1600,6 +1601,10 @@ extern "C" int gm_env_set_state(gm_env* env, const gm_env_state* st) {
         for (size_t b = 0; b < B; b++)
             if (st->rng_pos[b] < 0 || st->rng_pos[b] > (int32_t)MT_N)
                 return gm_fail(GM_ERR_INVALID_ARG, "gm_env_set_state: rng_pos outside [0, 624]");
+    if (st->seq_index)
+        for (size_t b = 0; b < B; b++)
+            if (st->seq_index[b] < 0 || (d.n_list > 0 && st->seq_index[b] >= d.n_list))
+                return gm_fail(GM_ERR_INVALID_ARG, "gm_env_set_state: seq_index outside the topology-seed list");
     if (st->nbr_edge && (!st->edge_a || !st->edge_b))
         return gm_fail(GM_ERR_INVALID_ARG, "gm_env_set_state: nbr_edge needs edge_a and edge_b");
     if (st->nbr_edge)
@@ -1615,7 +1620,8 @@ extern "C" int gm_env_set_state(gm_env* env, const gm_env_state* st) {
         (rc = h2d(d.amask, st->amask, B * A * 4)) || (rc = h2d(d.load, st->loads, B * E)) ||
         (rc = h2d(d.topo_seed, st->topo_seed, B)) || (rc = h2d(d.topo_reps, st->topo_reps, B)) ||
         (rc = h2d(d.edge_a, st->edge_a, B * E)) || (rc = h2d(d.edge_b, st->edge_b, B * E)) ||
-        (rc = h2d(d.edge_len, st->edge_len, B * E)) || (rc = h2d(d.nbr_edge, st->nbr_edge, B * N * 3)))
+        (rc = h2d(d.edge_len, st->edge_len, B * E)) || (rc = h2d(d.nbr_edge, st->nbr_edge, B * N * 3)) ||
+        (rc = h2d(d.seq_index, st->seq_index, B)))
         return rc;
     if (st->nbr_edge) {  // neighbour ids in the per-node edge order (ascending neighbour id)
         std::vector<int32_t> nbr(B * N * 3);

@@ -240,8 +240,9 @@ def _act_grad(act, gy, y, need_b, want_scale):
     relu / elu / tanh / sigmoid: one fused pass (gm_act_bwd). leaky_relu at training sizes: one fused pass (gm_leaky_bwd: mask, per-block bias partials,
     max|g| for the gradient GEMMs' operand scale)."""
     gb = sc = None
-    if act > 1 and gy.is_contiguous() and y.is_contiguous():
+    if act > 1:
         # relu / elu / tanh / sigmoid: derivative from the output (gm_act_bwd), any row count
+        gy, y = gy.contiguous(), y.contiguous()  # e.g. the slice of a torch.cat's gradient
         rows, cols = gy.shape
         rpb = 64
         g2 = torch.empty_like(gy)

@@ -365,7 +365,7 @@ class Routing:
             topo_seed=np.zeros(B, np.int64), topo_reps=np.zeros(B, np.int32), edge_a=np.zeros((B, E), np.int32),
             edge_b=np.zeros((B, E), np.int32), edge_len=np.zeros((B, E), np.int32),
             nbr_edge=np.zeros((B, N, 3), np.int32), apsp=np.zeros((B, N, N), np.int32),
-            rng_key=np.zeros((B, 624), np.uint32), rng_pos=np.zeros(B, np.int32),
+            rng_key=np.zeros((B, 624), np.uint32), rng_pos=np.zeros(B, np.int32), seq_index=np.zeros(B, np.int32),
         )
         st = L.EnvState()
         for k, v in arrs.items():
@@ -381,7 +381,7 @@ class Routing:
         shapes = dict(now=(B, A), target=(B, A), edge=(B, A), time=(B, A), ttl=(B, A), start=(B, A), spw=(B, A),
                       agent_steps=(B, A), size=(B, A), visited=(B, A, 2), amask=(B, A, 4), loads=(B, E),
                       topo_seed=(B,), topo_reps=(B,), edge_a=(B, E), edge_b=(B, E), edge_len=(B, E),
-                      nbr_edge=(B, N, 3), apsp=(B, N, N), rng_key=(B, 624), rng_pos=(B,))
+                      nbr_edge=(B, N, 3), apsp=(B, N, N), rng_key=(B, 624), rng_pos=(B,), seq_index=(B,))
         dtypes = dict(size=np.float64, loads=np.float64, visited=np.uint64, amask=np.uint8, topo_seed=np.int64,
                       rng_key=np.uint32)
         st = L.EnvState()

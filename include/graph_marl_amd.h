@@ -184,6 +184,8 @@ typedef struct {
     int32_t* apsp;                                                         /* [n_env, N, N] */
     uint32_t* rng_key;   /* [n_env, 624] current MT block  */
     int32_t* rng_pos;    /* [n_env]                          */
+    int32_t* seq_index;  /* [n_env] next position in a sequential topology-seed list
+                            (Network.sequential_topology_index, src/env/network.py:356-364) */
 } gm_env_state;
 int gm_env_get_state(gm_env* env, gm_env_state* st);
 /* Inverse of gm_env_get_state (synchronous): restores every non-NULL field (host arrays, same

@@ -411,3 +411,33 @@ def test_set_state_restores_a_dump(gm, oracle_mod):
         e2.step_(torch.as_tensor(act, dtype=torch.int32, device="cuda"))
         np.testing.assert_array_equal(e2.obs_buf[0, :, : 6 * n + 10].cpu().numpy(), o.observe()["obs"],
                                       err_msg=f"step {t}")
+
+
+def test_set_state_restores_the_topology_seed_list_position(gm):
+    """gm_env_state.seq_index: the position in a sequential topology-seed list
+    (Network.sequential_topology_index, src/env/network.py:356-371) survives a dump/restore, so a
+    restored env walks the list from the same place (the EVAL_SEEDS walk of evaluation)."""
+    n, a, B = 20, 20, 4
+    seeds = [int(s) for s in R.EVAL_SEEDS[:9]]
+
+    def make(seed):
+        e = gm.Routing(gm.Network(n, random_topology=True, excluded_seeds=None), a, n_env=B, seed=seed)
+        e.set_topology_seeds(seeds, sequential=True)
+        return e
+
+    e1, e2 = make(5), make(6)
+    for _ in range(4):
+        e1.reset_()
+    d = e1.get_state()
+    assert (d["seq_index"] == 4 % len(seeds)).all()
+    e2.reset_()
+    e2.set_state(d)
+    assert (e2.get_state()["seq_index"] == d["seq_index"]).all()
+    for k in range(7):  # both walk on from position 4 (wrapping past the list end)
+        e1.reset_()
+        e2.reset_()
+        s1, s2 = e1.get_state(), e2.get_state()
+        assert (s1["topo_seed"] == seeds[(4 + k) % len(seeds)]).all()
+        np.testing.assert_array_equal(s1["topo_seed"], s2["topo_seed"])
+        np.testing.assert_array_equal(s1["edge_a"], s2["edge_a"])
+        np.testing.assert_array_equal(s1["seq_index"], s2["seq_index"])
