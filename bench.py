@@ -47,8 +47,12 @@ def parse():
     p.add_argument("--random-topology", type=int, default=1)
     p.add_argument("--epsilon", type=float, default=0.5)
     p.add_argument("--no-kernel-timers", action="store_true")
-    p.add_argument("--graph", type=int, default=0,
-                   help="replay the rollout as a HIP graph of this many (even) vector steps (0: eager launches)")
+    p.add_argument("--graph", type=int, default=10,
+                   help="replay the rollout as HIP graphs of this many (even) vector steps, one graph per stream "
+                        "group on its own stream (0: eager launches; DESIGN.md §9.5: host enqueue 0.36 -> 0.02 ms "
+                        "per step, rollout +0.5 %%)")
+    p.add_argument("--graph-single", action="store_true",
+                   help="with --graph: every group in ONE graph (default: one graph per group on its own stream)")
     p.add_argument("--stagger", action="store_true",
                    help="stagger the stream groups' episodes so their resets overlap the other group's GEMMs "
                         "(measured neutral at 4096 envs: the reset is ~2%% of a 50-step episode)")
@@ -359,7 +363,7 @@ def main():
                 # capture after the eager warmup (packed weights, scratch buffers exist), then
                 # one untimed replay; the timed loop replays steps/graph graphs
                 assert steps % graph == 0, "--steps must be a multiple of --graph"
-                ro.capture(graph)
+                ro.capture(graph, per_group=not args.graph_single)
                 ro.run(graph)
             while ro.ep != EP - g:  # position: the first timed step (replay) triggers a reset
                 ro.run(g) if graph else ro.step()

@@ -9,12 +9,15 @@ overlaps one group's latency-bound kernels (env step, ε-greedy draws, routing e
 and GEMM tails with another group's GEMMs. Results are identical to running the groups
 one after another: the groups share no mutable state.
 
-capture() records an even number of vector steps of all groups as ONE HIP graph (the
-NetMon state and h_prev alternate between two fixed buffer pairs, so the graph reads and
-writes the same addresses on every replay); run() then replays it, which removes the
-per-kernel launch gaps and the host launch cost. Graph replay bakes the kernel arguments
-in: it is for fixed-ε rollouts (ε decay 1.0: benchmarks, evaluation); episode resets stay
-eager between replays.
+capture() records an even number of vector steps as HIP graphs (the NetMon state and h_prev
+alternate between two fixed buffer pairs, so a graph reads and writes the same addresses on
+every replay): by default one graph per group, captured on and replayed on that group's own
+stream, so the groups keep the cross-group slack of eager launching (a single graph forks the
+groups from the capturing stream and joins them at its end, which re-synchronises them on every
+replay); run() then replays them, which removes the per-kernel launch gaps and most of the host
+launch cost (one replay call per group per captured length). Graph replay bakes the kernel
+arguments in: it is for fixed-ε rollouts (ε decay 1.0: benchmarks, evaluation); episode resets
+stay eager between replays.
 """
 import torch
 
@@ -79,6 +82,7 @@ class StreamedRollout:
         self.stagger = stagger and groups > 1
         self._offs = [(g * episode_steps) // groups if self.stagger else 0 for g in range(groups)]
         self._graph = None
+        self._graphs = None
         self._gsteps = 0
 
     def _on(self, g):
@@ -117,15 +121,26 @@ class StreamedRollout:
             self.ep = 0
 
     @torch.no_grad()
-    def capture(self, steps=2):
-        """Record `steps` (even, dividing episode_steps) vector steps of every group as one
-        graph. Call after reset() and a few eager steps (packed weights and scratch exist)."""
+    def capture(self, steps=2, per_group=True):
+        """Record `steps` (even, dividing episode_steps) vector steps: per_group, one graph per
+        group on its own stream; else every group in one graph. Call after reset() and a few
+        eager steps (packed weights and scratch exist)."""
         assert steps % 2 == 0 and self.episode_steps % steps == 0, "steps must be even and divide episode_steps"
         if self.stagger:
             raise ValueError("graph replay needs aligned group resets (stagger=False)")
         if any(w._eps_changes() for w in self.policies):
             raise ValueError("graph replay needs a fixed epsilon (epsilon_decay = 1.0)")
         torch.cuda.synchronize()
+        if per_group:
+            graphs = []
+            for g in range(self.groups):
+                gr = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(gr, stream=self.streams[g]):
+                    for _ in range(steps):
+                        self.policies[g].act_step(self.wenvs[g])
+                graphs.append(gr)
+            self._graph, self._graphs, self._gsteps = None, graphs, steps
+            return
         graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(graph):
             cap = torch.cuda.current_stream()
@@ -135,14 +150,14 @@ class StreamedRollout:
                 self._enqueue_step()
             for s in self.streams:
                 cap.wait_stream(s)
-        self._graph, self._gsteps = graph, steps
+        self._graph, self._graphs, self._gsteps = graph, None, steps
         # the capture only recorded: the env / NetMon state is where it was before it; the
         # ping-pong buffer parity advanced by `steps` (even): unchanged
 
     @torch.no_grad()
     def run(self, n):
         """n vector steps (graph replays of capture()'s length when captured, else eager)."""
-        if self._graph is None:
+        if self._graph is None and self._graphs is None:
             for _ in range(n):
                 self.step()
             return
@@ -150,6 +165,18 @@ class StreamedRollout:
         for _ in range(n // self._gsteps):
             if self.ep % self._gsteps:
                 raise RuntimeError("graph replay must start at a multiple of the captured length")
+            if self._graphs is not None:
+                for g, gr in enumerate(self._graphs):
+                    with self._on(g):
+                        gr.replay()
+                self.ep += self._gsteps
+                if self.ep >= self.episode_steps:
+                    L.check_range()
+                    for g in range(self.groups):
+                        with self._on(g):
+                            self.wenvs[g].reset()
+                    self.ep = 0
+                continue
             self._graph.replay()
             self.ep += self._gsteps
             if self.ep >= self.episode_steps:

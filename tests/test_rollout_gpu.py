@@ -103,9 +103,11 @@ def test_stagger_refuses_graph():
         ro.capture(2)
 
 
+@pytest.mark.parametrize("per_group", [True, False])
 @pytest.mark.parametrize("groups,gsteps,warm", [(1, 2, 4), (2, 2, 4), (2, 10, 10)])
-def test_graph_replay_matches_eager(groups, gsteps, warm):
-    """Replays cross episode resets (episode 10 steps), which run eagerly in between."""
+def test_graph_replay_matches_eager(groups, gsteps, warm, per_group):
+    """Replays cross episode resets (episode 10 steps), which run eagerly in between; one graph
+    per group on its own stream (default) or every group in one graph."""
     eager = build(groups)
     eager.reset()
     eager.run(warm + 40)
@@ -115,9 +117,9 @@ def test_graph_replay_matches_eager(groups, gsteps, warm):
     ro.reset()
     for _ in range(warm):
         ro.step()
-    ro.capture(gsteps)
+    ro.capture(gsteps, per_group=per_group)
     ro.run(40)
-    assert ro._graph is not None
+    assert (ro._graphs is not None and len(ro._graphs) == groups) if per_group else ro._graph is not None
     for a, b in zip(snapshot(ro), ref):
         assert_same(a, b)
 
