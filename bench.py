@@ -163,12 +163,13 @@ def _gemm_obs():
 
 def sl_gemm_flops(N, B, L, K, H=128, enc=(512, 256)):
     """f16 MFMA FLOPs one config-5 SL iteration issues on its split-f16 GEMMs (3 f16 products per
-    fp32 multiply-add; forward, input gradient and weight gradient of each GEMM): per step and node
-    row the encoder layers 1..2 (enc[0]->enc[1]->H; layer 0 is the routing gather, no GEMM), the
-    LSTM obs cell [x | h] (2H -> 4H) and K update cells (2H -> 4H). The three narrow output heads
-    (exact f32) are left out."""
-    macs = enc[0] * enc[1] + enc[1] * H + (1 + K) * 2 * H * 4 * H
-    return 3.0 * 2.0 * 3.0 * macs * N * B * L
+    fp32 multiply-add; forward, input gradient and weight gradient of each GEMM): per node row the
+    encoder layers 1..2 once per iteration (enc[0]->enc[1]->H; layer 0 is the routing gather, no
+    GEMM; sl.train_step encodes the unrolled steps' shared observations once), and per step the LSTM
+    obs cell [x | h] (2H -> 4H) and K update cells (2H -> 4H). The three narrow output heads (exact
+    f32) are left out."""
+    macs = (enc[0] * enc[1] + enc[1] * H) + L * (1 + K) * 2 * H * 4 * H
+    return 3.0 * 2.0 * 3.0 * macs * N * B
 
 
 def measure_extras(args, gm, M, RO, timed_region, dev, N, A, x3):

@@ -615,23 +615,25 @@ __global__ __launch_bounds__(1024) void k_readout_bwd_lds(const float* __restric
     }
 }
 
-// k_readout_bwd_lds over S column chunks per graph (block = (graph, chunk)): a quarter of the LDS per
-// block, so 4x as many blocks stay resident. The (row, segment) -> node map is inverted once per block
-// into per-node row bitmasks (LDS atomic OR: order-free), so a (node, column) thread visits only the
+// k_readout_bwd_lds over S column chunks per graph (block = (graph, chunk)): 1/S of the LDS per
+// block, so S times as many blocks stay resident. The (row, segment) -> node map is inverted once per
+// block into per-node row bitmasks (LDS atomic OR: order-free; MW 64-bit words per mask, rows up to
+// 64 MW: every node of a 100-node graph without agent map), so a (node, column) thread visits only the
 // rows that read its node, in ascending (row, segment) order: the same summation order as
 // k_readout_bwd (identical results).
+template <int MW>
 __global__ __launch_bounds__(256) void k_readout_bwd_cs(const float* __restrict__ dout, long long stride,
                                                         const int32_t* __restrict__ nbr,
                                                         const int32_t* __restrict__ agent_node, int N, int R, int deg,
                                                         int H, int S, float* __restrict__ dhf, float* __restrict__ dhp) {
     extern __shared__ float4 sq[];  // [R][deg + 1][C4]
-    __shared__ int su[64];
-    __shared__ unsigned long long smask[128][4];  // node -> rows reading it, per segment (deg <= 3)
+    __shared__ int su[64 * MW];
+    __shared__ unsigned long long smask[128][4][MW];  // node -> rows reading it, per segment (deg <= 3)
     const long long g = blockIdx.x / S;
     const int cs = blockIdx.x - (int)(g * S);
     const int C4 = (H >> 2) / S, SEG = deg + 1;
     for (int i = threadIdx.x; i < R; i += blockDim.x) su[i] = agent_node ? agent_node[g * R + i] : i;
-    for (int i = threadIdx.x; i < N * SEG; i += blockDim.x) smask[i / SEG][i % SEG] = 0ull;
+    for (int i = threadIdx.x; i < N * SEG * MW; i += blockDim.x) smask[i / (SEG * MW)][(i / MW) % SEG][i % MW] = 0ull;
     for (int i = threadIdx.x; i < R * SEG * C4; i += blockDim.x) {
         const int r = i / (SEG * C4), rem = i - r * SEG * C4, sg = rem / C4, c = rem - sg * C4;
         sq[i] = *reinterpret_cast<const float4*>(dout + (g * R + r) * stride + sg * H + (cs * C4 + c) * 4);
@@ -640,19 +642,25 @@ __global__ __launch_bounds__(256) void k_readout_bwd_cs(const float* __restrict_
     for (int e = threadIdx.x; e < R * SEG; e += blockDim.x) {
         const int r = e / SEG, sg = e - r * SEG;
         const int v = sg == 0 ? su[r] : nbr[(g * N + su[r]) * deg + sg - 1];
-        if (v >= 0 && v < N) atomicOr(&smask[v][sg], 1ull << r);
+        if (v >= 0 && v < N) atomicOr(&smask[v][sg][r >> 6], 1ull << (r & 63));
     }
     __syncthreads();
     for (int t = threadIdx.x; t < N * C4; t += blockDim.x) {
         const int v = t / C4, c = t - v * C4;
         float4 af = make_float4(0.f, 0.f, 0.f, 0.f), ap = af;
-        for (unsigned long long m = smask[v][0]; m; m &= m - 1) af = f4add(af, sq[(__ffsll(m) - 1) * SEG * C4 + c]);
-        unsigned long long mk[3], any = 0ull;
-        for (int k = 0; k < deg; k++) any |= (mk[k] = smask[v][k + 1]);
-        for (; any; any &= any - 1) {
-            const int r = __ffsll(any) - 1;
-            for (int k = 0; k < deg; k++)
-                if ((mk[k] >> r) & 1ull) ap = f4add(ap, sq[(r * SEG + k + 1) * C4 + c]);
+#pragma unroll
+        for (int w = 0; w < MW; w++)
+            for (unsigned long long m = smask[v][0][w]; m; m &= m - 1)
+                af = f4add(af, sq[(64 * w + __ffsll(m) - 1) * SEG * C4 + c]);
+#pragma unroll
+        for (int w = 0; w < MW; w++) {
+            unsigned long long mk[3], any = 0ull;
+            for (int k = 0; k < deg; k++) any |= (mk[k] = smask[v][k + 1][w]);
+            for (; any; any &= any - 1) {
+                const int rb = __ffsll(any) - 1, r = 64 * w + rb;
+                for (int k = 0; k < deg; k++)
+                    if ((mk[k] >> rb) & 1ull) ap = f4add(ap, sq[(r * SEG + k + 1) * C4 + c]);
+            }
         }
         const long long o = (g * N + v) * H + (cs * C4 + c) * 4;
         if (dhf) *reinterpret_cast<float4*>(dhf + o) = af;
@@ -748,11 +756,17 @@ extern "C" int gm_netmon_readout_bwd(const float* dout, int64_t stride, const in
     if (dhf) { int v = vec_width(H, H, dhf); V = V < v ? V : v; }
     if (dhp) { int v = vec_width(H, H, dhp); V = V < v ? V : v; }
     const size_t lds = (size_t)R * (deg + 1) * H * 4;
-    if (V == 4 && R <= 64 && N <= 128 && deg <= 3 && (H / 4) % 4 == 0 && lds / 4 <= 48 * 1024 &&
+    // column chunks per graph: 4, or 8 when a quarter of the graph's rows exceeds 48 KB of LDS
+    const int S = (lds / 4 <= 48 * 1024 || (H / 4) % 8) ? 4 : 8;
+    if (V == 4 && R <= 128 && N <= 128 && deg <= 3 && (H / 4) % S == 0 && lds / S <= 48 * 1024 &&
         g_readout_bwd_cs) {
-        const int S = 4, threads = std::min(256, (N * (H / 16) + 63) / 64 * 64);
-        hipLaunchKernelGGL(k_readout_bwd_cs, dim3((unsigned)((long long)G * S)), dim3(threads), lds / S,
-                           (hipStream_t)stream, dout, (long long)stride, nbr, agent_node, N, R, deg, H, S, dhf, dhp);
+        const int threads = std::min(256, (N * (H / (4 * S)) + 63) / 64 * 64);
+        if (R <= 64)
+            hipLaunchKernelGGL(k_readout_bwd_cs<1>, dim3((unsigned)((long long)G * S)), dim3(threads), lds / S,
+                               (hipStream_t)stream, dout, (long long)stride, nbr, agent_node, N, R, deg, H, S, dhf, dhp);
+        else  // up to 128 rows per graph (e.g. every node of a 100-node graph, no agent map)
+            hipLaunchKernelGGL(k_readout_bwd_cs<2>, dim3((unsigned)((long long)G * S)), dim3(threads), lds / S,
+                               (hipStream_t)stream, dout, (long long)stride, nbr, agent_node, N, R, deg, H, S, dhf, dhp);
         return launched();
     }
     if (V == 4 && R <= 64 && deg <= MAXDEG && lds <= 48 * 1024) {

@@ -844,8 +844,15 @@ class NetMon(nn.Module):
             return cell(x, h), None
         return cell(x, (h, c))
 
-    def forward_graph(self, x, nbr, agent_node=None, out=None, out_col=0):
-        """x [B, N, F] node observations, nbr int32 [B, N, deg], agent_node int32 [B, A] or None.
+    def encode_nodes(self, x, nbr):
+        """The encoder MLP over every node row ([B*N, H]): forward_graph's first stage, for callers
+        that unroll NetMon several times on the same observations (sl.py) and pass it as `enc`."""
+        B, N, Fdim = x.shape
+        return self._encode(x.reshape(B * N, Fdim), nbr, B, N)
+
+    def forward_graph(self, x, nbr, agent_node=None, out=None, out_col=0, enc=None):
+        """x [B, N, F] node observations, nbr int32 [B, N, deg], agent_node int32 [B, A] or None;
+        enc: encode_nodes(x, nbr) computed once by the caller (the same values the encoder gives).
         Returns [B, A or N, 4H] (or writes into `out` [B, A, W] at column out_col)."""
         B, N, Fdim = x.shape
         H = self.hidden_features
@@ -858,7 +865,7 @@ class NetMon(nn.Module):
                 self.state = torch.zeros(B, N, self.state_size, device=x.device)
             st = self.state.reshape(B * N, self.num_states, H)
             hs, cs = st[:, 0].contiguous(), (st[:, 1].contiguous() if nc == 2 else None)
-        h = self._encode(x.reshape(B * N, Fdim), nbr, B, N)
+        h = enc if enc is not None else self._encode(x.reshape(B * N, Fdim), nbr, B, N)
         h, c = self._cell(self.rnn_obs, h, hs, cs)
         h0, c0 = h, c
         last_nbr = torch.zeros_like(h) if self.iterations <= 0 else None

@@ -104,8 +104,8 @@ class NetMonSL(torch.nn.Module):
         self.linear_reg_all = M.Linear(F, nb_nodes)
         self.class_logits = None
 
-    def forward(self, node_obs, nbr):
-        node_features = self.netmon.forward_graph(node_obs, nbr, None)
+    def forward(self, node_obs, nbr, enc=None):
+        node_features = self.netmon.forward_graph(node_obs, nbr, None, enc=enc)
         class_logits = self.linear(node_features)
         pred = self.linear_reg(node_features)
         pred_all = self.linear_reg_all(node_features)
@@ -188,8 +188,12 @@ def train_step(args, model, optim, data, batch_idx):
     tgt_all, tgt, labels = data.targets_all[batch_idx], data.targets[batch_idx], data.labels[batch_idx]
     seq = []
     terms = {}
+    # the reference re-encodes the same observations at every unroll step (src/sl.py:360-424); the
+    # encoder output is identical each time, so it is computed once and its gradient (the sum of
+    # the steps' contributions) runs back through the encoder once
+    enc = model.netmon.encode_nodes(obs, nbr)
     for _ in range(max(args.sequence_length, 1)):
-        loss, terms = _loss_terms(args, model(obs, nbr), tgt_all, tgt, labels)
+        loss, terms = _loss_terms(args, model(obs, nbr, enc), tgt_all, tgt, labels)
         seq.append(loss)
     total = torch.mean(torch.stack(seq))
     optim.zero_grad()
@@ -207,8 +211,9 @@ def test(args, model, data, batch_size, sequence_length):
     for i0 in range(0, S, batch_size):
         idx = torch.arange(i0, min(S, i0 + batch_size), device=data.node_obs.device)
         model.netmon.state = None
+        enc = model.netmon.encode_nodes(data.node_obs[idx], data.nbr[idx])
         for _ in range(max(sequence_length, 1)):
-            out = model(data.node_obs[idx], data.nbr[idx])
+            out = model(data.node_obs[idx], data.nbr[idx], enc)
         _, terms = _loss_terms(args, out, data.targets_all[idx], data.targets[idx], data.labels[idx], "sum")
         for k, v in terms.items():
             tot[k] += float(v)

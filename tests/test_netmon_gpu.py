@@ -78,14 +78,24 @@ def test_mp_aggregate_fwd_bwd(mode):
     torch.testing.assert_close(h.grad, h2.grad, atol=ATOL, rtol=0)
 
 
-def test_readout_fwd_bwd_with_agent_map():
+@pytest.mark.parametrize("G,N,A", [(32, 20, 20), (16, 100, None), (8, 128, None), (8, 64, None), (12, 40, 64)])
+def test_readout_fwd_bwd_with_agent_map(G, N, A):
+    """A = None: every node reads out (no agent map, the SL task: up to 128 rows per graph in the
+    bitmask backward)."""
     M = model_mod()
-    G, N, A, H = 32, 20, 20, 128
+    H = 128
     nbr, _ = random_graphs(G, N, seed=3)
     hf = torch.randn(G * N, H, device="cuda", requires_grad=True)
     hp = torch.randn(G * N, H, device="cuda", requires_grad=True)
-    an = torch.randint(0, N, (G, A), device="cuda", dtype=torch.int32)
-    out = M.netmon_readout(hf, hp, nbr, an).view(G, A, 4 * H)
+    if A is None:
+        A = N
+        an = torch.arange(N, device="cuda", dtype=torch.int32).repeat(G, 1)
+        out = M.netmon_readout(hf, hp, nbr, None).view(G, A, 4 * H)
+    else:
+        an = torch.randint(0, N, (G, A), device="cuda", dtype=torch.int32)
+        out = None
+    if out is None:
+        out = M.netmon_readout(hf, hp, nbr, an).view(G, A, 4 * H)
     nb = hp.detach().view(G, N, H)
     parts = [torch.gather(hf.detach().view(G, N, H), 1, an.long().unsqueeze(-1).expand(-1, -1, H))]
     for k in range(3):

@@ -34,8 +34,11 @@ def test_sl_samples_match_reference(name):
     np.testing.assert_array_equal(data.nbr.cpu().numpy(), nbr_ref.cpu().numpy())
 
 
+@pytest.mark.parametrize("shared_enc", [False, True])
 @pytest.mark.parametrize("name", GOLDENS)
-def test_sl_iteration_matches_reference(name):
+def test_sl_iteration_matches_reference(name, shared_enc):
+    """shared_enc: the encoder output computed once and reused by both unroll steps (sl.train_step)
+    instead of re-encoding at every step like the reference: same predictions and gradients."""
     SL = importlib.import_module("graph-marl_amd.sl")
     M = importlib.import_module("graph-marl_amd.model")
     g, n, H, enc = _golden(name)
@@ -51,8 +54,9 @@ def test_sl_iteration_matches_reference(name):
     tgt = torch.as_tensor(g["targets_all"], device="cuda")
     model.netmon.state = None
     seq = []
+    enc = model.netmon.encode_nodes(x, nbr) if shared_enc else None
     for t in range(2):
-        _, _, pred_all = model(x, nbr)
+        _, _, pred_all = model(x, nbr, enc)
         np.testing.assert_allclose(pred_all.detach().cpu().numpy(), g[f"pred_all_{t}"], atol=1e-5, rtol=0,
                                    err_msg=f"pred_all step {t}")
         seq.append(torch.nn.functional.mse_loss(pred_all, tgt))
