@@ -117,6 +117,9 @@ def kernel_cost(tag, n_env, N, A, E, x3=False):
     if kind in ("linear", "lstm", "lstm_agg"):
         m, n, k = (int(v) for v in tag.split(":")[2].split("x"))
         return ("mfma16" if x3 and n > 32 else "mfma"), (3.0 if x3 and n > 32 else 1.0) * 2.0 * m * n * k
+    if kind == "dqn_fused":  # gm_dqn_x3: layer 1 (K) + layer 2 (512 -> 256) + Q head, 3 f16 products each
+        m, n, k = (int(v) for v in tag.split(":")[2].split("x"))
+        return "mfma16", 3.0 * 2.0 * m * (n * k + 256 * n + 4 * 256)
     if kind == "routing_enc":
         rows, n = (int(v) for v in tag.split(":")[2].split("x"))
         return "hbm", rows * n * 4 + rows * 11 * 4  # write y, read the 11 nonzero features per row

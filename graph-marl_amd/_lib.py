@@ -33,7 +33,7 @@ EXPORTS = [
     "gm_gemm_pack_x3", "gm_gemm_pack_x3_bytes", "gm_gemm_range_status",
     "gm_pcg64_seed", "gm_pcg64_choice", "gm_lnlstm_pointwise", "gm_agent_attention", "gm_agent_comm",
     "gm_gemm_x3_dgrad", "gm_lstm_cell_bwd", "gm_qhead_bwd", "gm_netmon_readout_ld", "gm_routing_node_encoder_bits", "gm_gather_records",
-    "gm_lnlstm_fwd", "gm_lnlstm_bwd", "gm_gru_pointwise", "gm_gru_bwd", "gm_act_bwd",
+    "gm_lnlstm_fwd", "gm_lnlstm_bwd", "gm_gru_pointwise", "gm_gru_bwd", "gm_act_bwd", "gm_dqn_x3",
 ]
 
 # Arithmetic form of the fused rollout GEMMs (graph-marl_amd/fused.py): "x3" = split-f16
@@ -135,7 +135,6 @@ def lib():
     L.gm_mp_aggregate.argtypes = [vp, vp, i32, i32, i32, i32, i32, vp, vp]
     L.gm_mp_aggregate_rows.argtypes = [vp, C.c_int64, vp, i32, i32, i32, i32, i32, vp, C.c_int64, vp]
     L.gm_leaky_bwd.argtypes = [vp, vp, C.c_int64, i32, C.c_float, vp, vp, i32, vp, vp]
-    L.gm_act_bwd.argtypes = [vp, vp, C.c_int64, i32, i32, vp, vp, i32, vp, vp]
     L.gm_mp_aggregate_bwd.argtypes = [vp, vp, i32, i32, i32, i32, i32, vp, vp]
     L.gm_netmon_readout.argtypes = [vp, vp, vp, vp, i32, i32, i32, i32, i32, vp, i64, vp]
     L.gm_netmon_readout_bwd.argtypes = [vp, i64, vp, vp, i32, i32, i32, i32, i32, vp, vp, vp]
@@ -164,11 +163,18 @@ def lib():
     L.gm_pcg64_choice.argtypes = [vp, i64, i64, vp, vp]
     L.gm_gather_records.argtypes = [vp, i64, i64, vp, vp, i32, i64, i64, vp, vp]
     L.gm_lnlstm_pointwise.argtypes = [vp, i64, vp, i64] + [vp] * 7 + [i32, i32, C.c_float, vp, i64, vp, i64, vp]
-    L.gm_lnlstm_fwd.argtypes = [vp, i64, vp, i64, vp, i64] + [vp] * 7 + [i32, i32, C.c_float, vp, i64, vp, i64, vp, vp]
-    L.gm_lnlstm_bwd.argtypes = [vp, i64, vp, i64, vp, i64] + [vp] * 8 + [vp, i64, vp, i64, i32, i32, i32, vp, i64, vp,
-                                                                          i64, vp, i64, vp, vp]
-    L.gm_gru_pointwise.argtypes = [vp, i64, vp, i64, vp, i64, i32, i32, vp, i64, vp]
-    L.gm_gru_bwd.argtypes = [vp, i64, vp, i64, vp, i64, vp, i64, i32, i32, vp, i64, vp, i64, vp, i64, vp]
+    # round-3 entry points; GM_LIB may name an older build for A-B timing, which lacks them
+    newer = {
+        "gm_lnlstm_fwd": [vp, i64, vp, i64, vp, i64] + [vp] * 7 + [i32, i32, C.c_float, vp, i64, vp, i64, vp, vp],
+        "gm_lnlstm_bwd": [vp, i64, vp, i64, vp, i64] + [vp] * 8 + [vp, i64, vp, i64, i32, i32, i32, vp, i64, vp, i64, vp,
+                                                                   i64, vp, vp],
+        "gm_gru_pointwise": [vp, i64, vp, i64, vp, i64, i32, i32, vp, i64, vp],
+        "gm_gru_bwd": [vp, i64, vp, i64, vp, i64, vp, i64, i32, i32, vp, i64, vp, i64, vp, i64, vp],
+        "gm_act_bwd": [vp, vp, C.c_int64, i32, i32, vp, vp, i32, vp, vp],
+    }
+    for name, at in newer.items():
+        if hasattr(L, name) or not os.environ.get("GM_LIB"):
+            getattr(L, name).argtypes = at
     if MFMA_SHAPE is not None:
         if L.gm_gemm_set_mfma({"16": 1, "32": 0, "16all": 2}[MFMA_SHAPE]) != 0:
             raise GMError(L.gm_last_error().decode())

@@ -57,7 +57,7 @@ typedef float floatx4 __attribute__((ext_vector_type(4)));
 
 constexpr int BKMAX = 32;            // largest K tile of any configuration (host-side checks)
 constexpr int OOB = 0x7ff00000;       // byte offset beyond any buffer: load returns 0
-enum { EPI_BIAS = 0, EPI_LSTM = 1, EPI_HEAD = 2, EPI_DGRAD = 3 };
+enum { EPI_BIAS = 0, EPI_LSTM = 1, EPI_HEAD = 2, EPI_DGRAD = 3, EPI_DQN = 4 };
 
 struct ASrc {
     int mode;                 // GM_A_DENSE / GM_A_AGGREGATE / GM_A_READOUT
@@ -105,6 +105,14 @@ struct Epi {
     // the leaky_relu derivative of the layer's output for the training backward, 1/32 of its bytes
     unsigned* sbits;
     long long ldsb;
+    // EPI_DQN (the DQN's second layer + Q head after the first layer, in the same block): packed
+    // split-f16 layer-2 weights (gm_gemm_pack_x3 layout, n2 rows of ldw2 bytes), their 1/S, bias, act
+    const _Float16* w2;
+    long long ldw2;
+    unsigned w2bytes;
+    const float* wsi2;
+    const float* b2;
+    int act2;
 };
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const float* p, unsigned bytes) {
@@ -140,6 +148,29 @@ __device__ __forceinline__ float sigm(float x) {
     return __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(-1.44269504088896341f * x));
 }
 __device__ __forceinline__ float tanh_fast(float x) { return 2.0f * sigm(2.0f * x) - 1.0f; }
+
+// Layer activation in the epilogues with the common cases resolved at compile time: A = 0 none,
+// 1 leaky_relu, -1 any GM_ACT_* at run time (a per-element branch tree: relu / elu / tanh / sigmoid
+// only). act_dispatch calls f with A chosen from the wave-uniform act, so the default epilogues carry
+// no activation branches per element.
+template <int A>
+__device__ __forceinline__ float act_t(float v, int act) {
+    if constexpr (A == 0)
+        return v;
+    else if constexpr (A == 1)
+        return v >= 0.f ? v : 0.01f * v;
+    else
+        return gm_act_fast(v, act);
+}
+template <typename F>
+__device__ __forceinline__ void act_dispatch(int act, F&& f) {
+    if (act == 1)
+        f(std::integral_constant<int, 1>{});
+    else if (act == 0)
+        f(std::integral_constant<int, 0>{});
+    else
+        f(std::integral_constant<int, -1>{});
+}
 
 // Range guard of the split-f16 form: an A element whose pieces leave the f16 range (|a| >=
 // 65520, or a low piece (a - a_hi) * 2^12 >= 65520, possible from |a| >= 2^15) makes every
@@ -215,7 +246,7 @@ __device__ __forceinline__ void cin_load(CIn<TM, EPI>& c, const Epi& ep, int wm0
 
 // Epilogue of both forms. C/D map of the 32x32 MFMA tiles: col = lane & 31, row =
 // (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5); wave tile origin (wm0, wn0).
-template <int TM, int TN, int EPI>
+template <int TM, int TN, int EPI, int A = -1>
 __device__ __forceinline__ void epilogue(floatx16 (&acc)[TM][TN], const Epi& ep, int wm0, int wn0, int M, int N,
                                          int lane, const CIn<TM, EPI>& cin) {
     const int h = lane >> 5, l32 = lane & 31;
@@ -231,7 +262,7 @@ __device__ __forceinline__ void epilogue(floatx16 (&acc)[TM][TN], const Epi& ep,
                 for (int r = 0; r < 16; r++) {
                     const int row = rb0 + (r & 3) + 8 * (r >> 2);
                     float v = acc[i][j][r] + bv;
-                    v = gm_act_fast(v, ep.act);
+                    v = act_t<A>(v, ep.act);
                     if (row < M && col < N) ep.y[(long long)row * ep.ldy + col] = v;
                     if (ep.sbits) {  // lanes 0-31 / 32-63: 32 columns of rows row(h = 0) / row(h = 1)
                         const unsigned long long b = __ballot(v > 0.f && col < N);
@@ -286,7 +317,7 @@ __device__ __forceinline__ void epilogue(floatx16 (&acc)[TM][TN], const Epi& ep,
 // dot products of its TN columns for its 16 rows x 4 heads (64 values) are reduce-scattered
 // over the 32 lanes of its half (xor 16..1: 62 shuffles, lane l ends with entries 2l, 2l+1
 // of row r = l >> 1, heads 2 (l & 1) + t); the WGN column waves are summed through LDS.
-template <int TM, int TN, int WGN, int BM>
+template <int TM, int TN, int WGN, int BM, int A = -1>
 __device__ __forceinline__ void head_epilogue(floatx16 (&acc)[TM][TN], const Epi& ep, char* lds, int m0, int wr,
                                               int wc, int M, int N, int lane, int tid) {
     const int h = lane >> 5, l32 = lane & 31;
@@ -311,7 +342,7 @@ __device__ __forceinline__ void head_epilogue(floatx16 (&acc)[TM][TN], const Epi
 #pragma unroll
             for (int r = 0; r < 16; r++) {
                 float y = acc[i][j][r] + bv[j];
-                y = gm_act_fast(y, ep.act);
+                y = act_t<A>(y, ep.act);
                 if (ep.y) {
                     const int row = m0 + wr * TM * 32 + i * 32 + 4 * h + (r & 3) + 8 * (r >> 2);
                     if (row < M && col < N) ep.y[(long long)row * ep.ldy + col] = y;
@@ -556,7 +587,13 @@ __global__ __launch_bounds__(WGM* WGN * 64, OCC) void k_gemm(ASrc a0, ASrc a1, c
 
     CIn<TM, EPI> cin;
     cin_load<TM, EPI>(cin, ep, m0 + wr * TM * 32, n0 + wc * TN * 32, M, lane);
-    epilogue<TM, TN, EPI>(acc, ep, m0 + wr * TM * 32, n0 + wc * TN * 32, M, N, lane, cin);
+    if constexpr (EPI == EPI_BIAS)
+        act_dispatch(ep.act, [&](auto A) {
+            epilogue<TM, TN, EPI, decltype(A)::value>(acc, ep, m0 + wr * TM * 32, n0 + wc * TN * 32, M, N, lane,
+                                                      cin);
+        });
+    else
+        epilogue<TM, TN, EPI>(acc, ep, m0 + wr * TM * 32, n0 + wc * TN * 32, M, N, lane, cin);
 }
 
 // EPI_DGRAD epilogue of k_gemm3 (32x32 C layout): the leaky_relu derivative of the layer input
@@ -873,7 +910,13 @@ __global__ __launch_bounds__(WGM* WGN * 64, OCC) void k_gemm3(ASrc a0, ASrc a1, 
     } else {
         CIn<TM, EPI> cin;
         cin_load<TM, EPI>(cin, ep, m0 + wr * TM * 32, n0 + wc * TN * 32, M, lane);
-        epilogue<TM, TN, EPI>(acc, ep, m0 + wr * TM * 32, n0 + wc * TN * 32, M, N, lane, cin);
+        if constexpr (EPI == EPI_BIAS)
+            act_dispatch(ep.act, [&](auto A) {
+                epilogue<TM, TN, EPI, decltype(A)::value>(acc, ep, m0 + wr * TM * 32, n0 + wc * TN * 32, M, N, lane,
+                                                          cin);
+            });
+        else
+            epilogue<TM, TN, EPI>(acc, ep, m0 + wr * TM * 32, n0 + wc * TN * 32, M, N, lane, cin);
     }
 }
 
@@ -917,7 +960,7 @@ __device__ __forceinline__ void range_guard16(const floatx4 (&acc)[T2][N2], unsi
             for (int r = 0; r < 4; r++) bad |= !__builtin_isfinite(acc[i][j][r]);
     if (__ballot(bad) != 0ull && lane == 0) *reinterpret_cast<volatile unsigned*>(flag) = 1u;
 }
-template <int T2, int N2, int EPI>
+template <int T2, int N2, int EPI, int A = -1>
 __device__ __forceinline__ void epilogue16(floatx4 (&acc)[T2][N2], const Epi& ep, int wm0, int wn0, int M, int N,
                                            int lane, const CIn16<T2, EPI>& cin) {
     const int l16 = lane & 15, rq = 4 * (lane >> 4);
@@ -941,7 +984,7 @@ __device__ __forceinline__ void epilogue16(floatx4 (&acc)[T2][N2], const Epi& ep
                     for (int b = 0; b < 2; b++) {
                         const int col = wn0 + (2 * jp + b) * 16 + l16;
                         float v = acc[i][2 * jp + b][r] + bv[b];
-                        v = gm_act_fast(v, ep.act);
+                        v = act_t<A>(v, ep.act);
                         if (row < M && col < N) ep.y[(long long)row * ep.ldy + col] = v;
                         bb[b] = ep.sbits ? __ballot(v > 0.f && col < N) : 0ull;
                     }
@@ -1062,7 +1105,7 @@ __device__ __forceinline__ void dgrad_epilogue16(floatx4 (&acc)[T2][N2], const E
 // EPI_HEAD on the 16x16 layout: per row block i, a lane's partial dot products (4 rows x 4 heads)
 // are reduce-scattered over its 16-lane group (xor 8..1: 15 shuffles; lane ends with entry l & 15
 // = row 4 (l >> 4) + (e >> 2), head e & 3), the WGN column waves summed through LDS.
-template <int T2, int N2, int WGN, int BM>
+template <int T2, int N2, int WGN, int BM, int A = -1>
 __device__ __forceinline__ void head_epilogue16(floatx4 (&acc)[T2][N2], const Epi& ep, char* lds, int m0, int wr,
                                                 int wc, int M, int N, int lane, int tid) {
     const int l16 = lane & 15, rq = 4 * (lane >> 4);
@@ -1087,7 +1130,7 @@ __device__ __forceinline__ void head_epilogue16(floatx4 (&acc)[T2][N2], const Ep
 #pragma unroll
             for (int r = 0; r < 4; r++) {
                 float y = acc[i][j][r] + bv[j];
-                y = gm_act_fast(y, ep.act);
+                y = act_t<A>(y, ep.act);
                 if (ep.y) {
                     const int row = m0 + wr * T2 * 16 + i * 16 + rq + r;
                     if (row < M && col < N) ep.y[(long long)row * ep.ldy + col] = y;
@@ -1123,6 +1166,157 @@ __device__ __forceinline__ void head_epilogue16(floatx4 (&acc)[T2][N2], const Ep
         for (int w = 0; w < WGN; w++) v += qp[(w * BM + rl) * 4 + a];
         ep.q[(long long)row * ep.ldq + a] = v;
     }
+}
+
+// ---- EPI_DQN: the DQN's layers 2 + Q head in the block that computed layer 1 (src/model.py:187-203) ----
+// A 64-row block holds its rows' whole layer-1 output (8 waves x 64 columns, 16x16x32 accumulators).
+// It goes through bias + activation, is split into f16 hi / lo pieces exactly like a dense A tile of
+// the unfused layer-2 kernel (split4: the same bits), and is stored K-major in two LDS images
+// ([layer-1 column = layer-2 k][64 rows] f16, 128-B rows). Layer 2 then reads its A fragments (8
+// consecutive k of one row) with ds_read_b64_tr_b16 and its weight fragments straight from
+// global/L2 into registers, two k tiles ahead; the Q head is head_epilogue16. The 81920 x 512 layer-1
+// activation never reaches HBM (168 MB written + read per rollout step unfused).
+// Image swizzle: the 8-byte slot of row k is XOR'd with dqn_swz(k) = k & 15 with bits 1 and 2
+// swapped, so the epilogue's 16 consecutive-k writes and the transposed reads (rows 8g + q, 4 lanes
+// per row) both hit distinct banks.
+__device__ __forceinline__ int dqn_swz(int k) {
+    return (k & 9) | ((k & 2) << 1) | ((k & 4) >> 1);
+}
+
+template <int T2, int N2, int WGN, int BM, int A = -1>
+__device__ __forceinline__ void dqn_tail(floatx4 (&acc)[T2][N2], const Epi& ep, char* lds, int m0, int wc, int M,
+                                         int lane, int tid) {
+    static_assert(T2 * 16 == BM, "one wave row holds the block's rows");
+#if GM_DIAG == 20  // diagnostic build 20: layer 1 only (timing only, wrong Q)
+    if (acc[0][0][0] == 12345.f) ep.q[m0] = 1.f;
+    return;
+#endif
+    constexpr int K2 = WGN * N2 * 16;  // layer-2 K = layer-1 width
+    constexpr int RS = BM * 2;         // image row bytes
+    constexpr int NK = K2 / 32;        // layer-2 k tiles
+    constexpr int J2 = 2;              // layer-2 16-column blocks per wave (WGN * 32 columns)
+    char* ih = lds;
+    char* il = lds + K2 * RS;
+    const int l16 = lane & 15, rq = 4 * (lane >> 4);
+    __syncthreads();  // every wave is past its last reads of the layer-1 operand stages
+#pragma unroll
+    for (int j = 0; j < N2; j++) {
+        const int n = wc * N2 * 16 + j * 16 + l16;  // layer-1 column = layer-2 k
+        const float bj = ep.bias ? ep.bias[n] : 0.f;
+        const int sw = dqn_swz(n) << 3;
+#pragma unroll
+        for (int i = 0; i < T2; i++) {
+            const int m = i * 16 + rq;
+            float4 v;
+            v.x = act_t<A>(acc[i][j][0] + bj, ep.act);
+            v.y = act_t<A>(acc[i][j][1] + bj, ep.act);
+            v.z = act_t<A>(acc[i][j][2] + bj, ep.act);
+            v.w = act_t<A>(acc[i][j][3] + bj, ep.act);
+            half4 hi, lo;
+            split4(v, hi, lo);
+            const int off = n * RS + ((2 * m) ^ sw);
+            *reinterpret_cast<half4*>(ih + off) = hi;
+            *reinterpret_cast<half4*>(il + off) = lo;
+        }
+    }
+    // layer-2 weight fragments of this wave's 32 columns: lane reads row n2 = 32 wc + 16 jb + l16,
+    // k 8 q .. 8 q + 7 of each 32-deep tile: 16-k block 2 kt + (q >> 1), halves (q & 1) x 8 (hi at +0,
+    // lo at +32 of the block's 64 bytes)
+    const int q = lane >> 4;
+    const __amdgpu_buffer_rsrc_t rw = rsrc(reinterpret_cast<const float*>(ep.w2), ep.w2bytes);
+    int wo[J2];
+#pragma unroll
+    for (int jb = 0; jb < J2; jb++) wo[jb] = (int)((wc * 32 + jb * 16 + l16) * ep.ldw2) + (q >> 1) * 64 + (q & 1) * 16;
+    constexpr int NB2 = 3;  // weight tiles in flight
+    u32x4 pbh[NB2][J2], pbl[NB2][J2];
+    auto bfetch = [&](int slot, int kt) {
+#pragma unroll
+        for (int jb = 0; jb < J2; jb++) {
+            pbh[slot][jb] = __builtin_amdgcn_raw_buffer_load_b128(rw, wo[jb] + kt * 128, 0, 0);
+            pbl[slot][jb] = __builtin_amdgcn_raw_buffer_load_b128(rw, wo[jb] + kt * 128 + 32, 0, 0);
+        }
+    };
+#pragma unroll
+    for (int t = 0; t < NB2; t++) bfetch(t, t);
+    __syncthreads();  // the images are complete
+    floatx4 acc2[T2][J2];
+#pragma unroll
+    for (int i = 0; i < T2; i++)
+#pragma unroll
+        for (int j = 0; j < J2; j++)
+#pragma unroll
+            for (int r = 0; r < 4; r++) acc2[i][j][r] = 0.f;
+    // transposed A reads: 16-lane group g reads k rows 8 g + qq (+ 4), columns 4 p of its 16-row block
+    const int g = lane >> 4, qq = (lane >> 2) & 3, p = lane & 3;
+    typedef __fp16 v4fp16 __attribute__((__vector_size__(8)));
+    auto frag = [&](const char* img, int k0, int col0) {
+        const int r0 = k0 + 8 * g + qq, r1 = r0 + 4;
+        const char* a0 = img + r0 * RS + ((2 * (col0 + 4 * p)) ^ (dqn_swz(r0) << 3));
+        const char* a1 = img + r1 * RS + ((2 * (col0 + 4 * p)) ^ (dqn_swz(r1) << 3));
+        const half4 x0 = __builtin_bit_cast(
+            half4, __builtin_amdgcn_ds_read_tr16_b64_v4f16((__attribute__((address_space(3))) v4fp16*)(a0)));
+        const half4 x1 = __builtin_bit_cast(
+            half4, __builtin_amdgcn_ds_read_tr16_b64_v4f16((__attribute__((address_space(3))) v4fp16*)(a1)));
+        return half8{x0[0], x0[1], x0[2], x0[3], x1[0], x1[1], x1[2], x1[3]};
+    };
+    const _Float16 s12 = (_Float16)(1.0f / 4096.0f);
+    // A fragments double-buffered in registers: tile kt + 1's reads are issued before tile kt's MFMAs
+    half8 fah[2][T2], fal[2][T2];
+#pragma unroll
+    for (int i = 0; i < T2; i++) {
+        fah[0][i] = frag(ih, 0, 16 * i);
+        fal[0][i] = frag(il, 0, 16 * i);
+    }
+#if GM_DIAG == 21  // diagnostic build 21: no layer-2 k loop (timing only, wrong Q)
+    if (acc2[0][0][0] != 0.f) {
+#else
+    {
+#endif
+#pragma unroll
+    for (int kt = 0; kt < NK; kt++) {
+        const int cur = kt & 1, slot = kt % NB2;
+        if (kt + 1 < NK) {
+#pragma unroll
+            for (int i = 0; i < T2; i++) {
+                fah[cur ^ 1][i] = frag(ih, (kt + 1) * 32, 16 * i);
+                fal[cur ^ 1][i] = frag(il, (kt + 1) * 32, 16 * i);
+            }
+        }
+        half8 bh[J2], bl[J2];
+#pragma unroll
+        for (int jb = 0; jb < J2; jb++) {
+            bh[jb] = __builtin_bit_cast(half8, pbh[slot][jb]);
+            bl[jb] = __builtin_bit_cast(half8, pbl[slot][jb]);
+        }
+        if (kt + NB2 < NK) bfetch(slot, kt + NB2);
+#pragma unroll
+        for (int jb = 0; jb < J2; jb++) {
+            const half8 bs = bh[jb] * s12;
+#pragma unroll
+            for (int i = 0; i < T2; i++) {
+                floatx4& c = acc2[i][jb];
+                c = __builtin_amdgcn_mfma_f32_16x16x32_f16(fal[cur][i], bs, c, 0, 0, 0);
+                c = __builtin_amdgcn_mfma_f32_16x16x32_f16(fah[cur][i], bl[jb], c, 0, 0, 0);
+                c = __builtin_amdgcn_mfma_f32_16x16x32_f16(fah[cur][i], bh[jb], c, 0, 0, 0);
+            }
+        }
+    }
+    }
+    const float si = *ep.wsi2;
+#pragma unroll
+    for (int i = 0; i < T2; i++)
+#pragma unroll
+        for (int j = 0; j < J2; j++)
+#pragma unroll
+            for (int r = 0; r < 4; r++) acc2[i][j][r] *= si;
+    range_guard16<T2, J2>(acc2, ep.range_flag, lane);
+    Epi e2 = ep;
+    e2.bias = ep.b2;
+    e2.act = ep.act2;
+    e2.y = nullptr;
+    act_dispatch(e2.act, [&](auto A2) {
+        head_epilogue16<T2, J2, WGN, BM, decltype(A2)::value>(acc2, e2, lds, m0, 0, wc, M, WGN * 32, lane, tid);
+    });
 }
 
 // ---------------------------------------------------------------------------------------
@@ -1532,9 +1726,21 @@ __global__ __launch_bounds__(WGM* WGN * 64, OCC) void k_gemm3g(ASrc a0, ASrc a1,
             dgrad_epilogue16<WGM, WGN, 2 * TM, 2 * TN, true>(acc4, ep, reinterpret_cast<float*>(lds), m0, n0, wr, wc, M,
                                                              N, lane);
         } else if constexpr (EPI == EPI_HEAD)
-            head_epilogue16<2 * TM, 2 * TN, WGN, BM>(acc4, ep, lds, m0, wr, wc, M, N, lane, tid);
+            act_dispatch(ep.act, [&](auto A) {
+                head_epilogue16<2 * TM, 2 * TN, WGN, BM, decltype(A)::value>(acc4, ep, lds, m0, wr, wc, M, N, lane, tid);
+            });
+        else if constexpr (EPI == EPI_DQN)
+            act_dispatch(ep.act, [&](auto A) {
+                dqn_tail<2 * TM, 2 * TN, WGN, BM, decltype(A)::value>(acc4, ep, lds, m0, wc, M, lane, tid);
+            });
         else
-            epilogue16<2 * TM, 2 * TN, EPI>(acc4, ep, m0 + wr * TM * 32, n0 + wc * TN * 32, M, N, lane, cin);
+            if constexpr (EPI == EPI_BIAS)
+                act_dispatch(ep.act, [&](auto A) {
+                    epilogue16<2 * TM, 2 * TN, EPI, decltype(A)::value>(acc4, ep, m0 + wr * TM * 32, n0 + wc * TN * 32, M,
+                                                                        N, lane, cin);
+                });
+            else
+                epilogue16<2 * TM, 2 * TN, EPI>(acc4, ep, m0 + wr * TM * 32, n0 + wc * TN * 32, M, N, lane, cin);
     } else {
 #pragma unroll
         for (int i = 0; i < TM; i++)
@@ -1553,8 +1759,14 @@ __global__ __launch_bounds__(WGM* WGN * 64, OCC) void k_gemm3g(ASrc a0, ASrc a1,
             }
             dgrad_epilogue<WGM, WGN, TM, TN, true>(acc, ep, reinterpret_cast<float*>(lds), m0, n0, wr, wc, M, N, lane);
         } else if constexpr (EPI == EPI_HEAD)
-            head_epilogue<TM, TN, WGN, BM>(acc, ep, lds, m0, wr, wc, M, N, lane, tid);
-        else
+            act_dispatch(ep.act, [&](auto A) {
+                head_epilogue<TM, TN, WGN, BM, decltype(A)::value>(acc, ep, lds, m0, wr, wc, M, N, lane, tid);
+            });
+        else if constexpr (EPI == EPI_BIAS)
+            act_dispatch(ep.act, [&](auto A) {
+                epilogue<TM, TN, EPI, decltype(A)::value>(acc, ep, m0 + wr * TM * 32, n0 + wc * TN * 32, M, N, lane, cin);
+            });
+        else if constexpr (EPI != EPI_DQN)  // EPI_DQN runs on the 16x16x32 form only (gm_dqn_x3)
             epilogue<TM, TN, EPI>(acc, ep, m0 + wr * TM * 32, n0 + wc * TN * 32, M, N, lane, cin);
     }
 }
@@ -2019,6 +2231,52 @@ extern "C" int gm_gemm_range_status(int32_t* status, int32_t clear) {
     *status = g_range_host ? (int32_t)*reinterpret_cast<volatile unsigned*>(g_range_host) : 0;
     if (clear && g_range_host) *reinterpret_cast<volatile unsigned*>(g_range_host) = 0u;
     return GM_OK;
+}
+
+extern "C" int gm_dqn_x3(const gm_a_src* a0, const gm_a_src* a1, const void* w1p, const float* w1sinv, const float* b1,
+                         int32_t act1, const void* w2p, const float* w2sinv, const float* b2, int32_t act2, int32_t m,
+                         int32_t n1, int32_t n2, const float* wq, int64_t ldwq, const float* bq, int32_t nq, float* q,
+                         int64_t ldq, void* stream) {
+    if (!a0 || !w1p || !w1sinv || !b1 || !w2p || !w2sinv || !b2 || !wq || !q || m <= 0 || n1 != 512 || n2 != 256 ||
+        nq <= 0 || nq > 4 || ldwq < n2 || ldq < nq || act1 < GM_ACT_NONE || act1 > GM_ACT_SIGMOID ||
+        act2 < GM_ACT_NONE || act2 > GM_ACT_SIGMOID || (reinterpret_cast<uintptr_t>(w1p) & 15) ||
+        (reinterpret_cast<uintptr_t>(w2p) & 15))
+        return gm_fail(GM_ERR_INVALID_ARG, "gm_dqn_x3: bad arguments (layers 512, 256 wide, nq <= 4)");
+    ASrc s0, s1;
+    int rc = to_asrc(a0, m, s0);
+    if (rc) return rc;
+    rc = to_asrc(a1, m, s1);
+    if (rc) return rc;
+    if (s0.mode == GM_A_AGGREGATE || s0.scale || s0.amax || (a1 && (a1->mode != GM_A_DENSE || (s0.k % BKMAX))))
+        return gm_fail(GM_ERR_INVALID_ARG, "gm_dqn_x3: dense or readout source (+ a dense second source, k % 32 == 0)");
+    const int K = s0.k + (a1 ? s1.k : 0);
+    const long long ldw1 = (long long)((K + BKMAX - 1) / BKMAX * BKMAX) / 16 * 64, wb1 = (long long)n1 * ldw1;
+    const long long ldw2 = (long long)n1 / 16 * 64, wb2 = (long long)n2 * ldw2;  // layer-2 K = n1
+    if (!fits(wb1)) return gm_fail(GM_ERR_UNSUPPORTED, "gm_dqn_x3: weights larger than 2 GB");
+    Epi ep;
+    memset(&ep, 0, sizeof(ep));
+    ep.bias = b1;
+    ep.act = act1;
+    ep.w2 = static_cast<const _Float16*>(w2p);
+    ep.ldw2 = ldw2;
+    ep.w2bytes = (unsigned)wb2;
+    ep.wsi2 = w2sinv;
+    ep.b2 = b2;
+    ep.act2 = act2;
+    ep.wq = wq;
+    ep.ldwq = ldwq;
+    ep.bq = bq;
+    ep.nq = nq;
+    ep.q = q;
+    ep.ldq = ldq;
+    if ((rc = range_flag(&ep.range_flag))) return rc;
+    const float* w1 = static_cast<const float*>(w1p);
+    hipStream_t st = (hipStream_t)stream;
+    // 64-row blocks, 8 waves of 64 layer-1 columns; 2 LDS stages of (64 + 512) x 128 B = 144 KB
+    if (s0.mode == GM_A_READOUT)
+        return launch_g<1, 8, 2, 2, 2, GM_A_READOUT, EPI_DQN, 1>(s0, s1, w1, ldw1, (unsigned)wb1, m, n1, K, ep, st,
+                                                                w1sinv, 1);
+    return launch_g<1, 8, 2, 2, 2, GM_A_DENSE, EPI_DQN, 1>(s0, s1, w1, ldw1, (unsigned)wb1, m, n1, K, ep, st, w1sinv, 1);
 }
 
 extern "C" int gm_gemm_x3_head(const gm_a_src* a0, const void* wp, const float* wscale_inv, const float* b,

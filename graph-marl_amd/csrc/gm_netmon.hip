@@ -272,7 +272,19 @@ __device__ __forceinline__ unsigned spread16(unsigned x) {
 // so W x touches 12 of the 4N+8 weight columns: the dense GEMM's K = 4N+8 collapses to a
 // 12-term gather over W^T staged in LDS (BN output columns per block, 64 lanes x BN/64
 // columns). HBM-bound on the output rows (n floats per node).
-template <int CPL>  // output columns per lane (BN = 64 * CPL)
+template <int AC>
+__device__ __forceinline__ float renc_act(float v, int act) {
+    if constexpr (AC == 0)
+        return v;
+    else if constexpr (AC == 1)
+        return v >= 0.f ? v : 0.01f * v;
+    else
+        return gm_act_fast(v, act);
+}
+
+// AC: the activation at compile time (0 none, 1 leaky_relu) or -1 = GM_ACT_* `act` at run time (a per
+// element branch tree: kept out of the default kernels, it cost 65 -> 76 us per 81 920 rows)
+template <int CPL, int AC>  // output columns per lane (BN = 64 * CPL)
 __global__ __launch_bounds__(256) void k_routing_enc(const float* __restrict__ x, long long ldx,
                                                      const int32_t* __restrict__ nbr, int G, int N,
                                                      const float* __restrict__ wt, const float* __restrict__ b,
@@ -367,8 +379,8 @@ __global__ __launch_bounds__(256) void k_routing_enc(const float* __restrict__ x
         float* yr = y + (base + i) * ldy + c0 + col;
         if (CPL == 2) {
             float a0 = acc[0], a1 = acc[CPL - 1];
-            a0 = gm_act_fast(a0, act);
-            a1 = gm_act_fast(a1, act);
+            a0 = renc_act<AC>(a0, act);
+            a1 = renc_act<AC>(a1, act);
             *reinterpret_cast<float2*>(yr) = make_float2(a0, a1);
             if (sbits) {  // 32-column sign words: lanes 16k..16k+15 hold columns 32k..32k+31, two each
                 const unsigned long long b0 = __ballot(a0 > 0.f), b1 = __ballot(a1 > 0.f);
@@ -380,9 +392,9 @@ __global__ __launch_bounds__(256) void k_routing_enc(const float* __restrict__ x
             }
         } else {
 #pragma unroll
-            for (int j = 0; j < CPL; j++) yr[j] = gm_act_fast(acc[j], act);
+            for (int j = 0; j < CPL; j++) yr[j] = renc_act<AC>(acc[j], act);
             if (sbits) {
-                const float a0 = gm_act_fast(acc[0], act);
+                const float a0 = renc_act<AC>(acc[0], act);
                 const unsigned long long b0 = __ballot(a0 > 0.f);
                 if ((lane & 31) == 0) sbits[(base + i) * ldsb + (c0 >> 5) + (lane >> 5)] = (unsigned)(b0 >> lane);
             }
@@ -1299,12 +1311,19 @@ extern "C" int gm_routing_node_encoder_bits(const float* x, int64_t ldx, const i
     }();
     const int rows = rows_env ? rows_env : (K <= 88 ? 256 : (K <= 128 ? 512 : 1024));
     dim3 grid((unsigned)((M + rows - 1) / rows), (unsigned)(n / (64 * cpl)));
-    if (cpl == 2)
-        hipLaunchKernelGGL(k_routing_enc<2>, grid, dim3(256), lds, (hipStream_t)stream, x, (long long)ldx, nbr, G, N,
-                           wt, b, n, act, y, (long long)ldy, rows, reinterpret_cast<unsigned*>(sbits), (long long)ldsb);
-    else
-        hipLaunchKernelGGL(k_routing_enc<1>, grid, dim3(256), lds, (hipStream_t)stream, x, (long long)ldx, nbr, G, N,
-                           wt, b, n, act, y, (long long)ldy, rows, reinterpret_cast<unsigned*>(sbits), (long long)ldsb);
+#define GM_RENC(C, A)                                                                                              \
+    hipLaunchKernelGGL((k_routing_enc<C, A>), grid, dim3(256), lds, (hipStream_t)stream, x, (long long)ldx, nbr, G, N, \
+                       wt, b, n, act, y, (long long)ldy, rows, reinterpret_cast<unsigned*>(sbits), (long long)ldsb)
+    if (cpl == 2) {
+        if (act == GM_ACT_LEAKY_RELU) GM_RENC(2, 1);
+        else if (act == GM_ACT_NONE) GM_RENC(2, 0);
+        else GM_RENC(2, -1);
+    } else {
+        if (act == GM_ACT_LEAKY_RELU) GM_RENC(1, 1);
+        else if (act == GM_ACT_NONE) GM_RENC(1, 0);
+        else GM_RENC(1, -1);
+    }
+#undef GM_RENC
     return launched();
 }
 

@@ -172,12 +172,17 @@ def _dgrad(gy, w, wcache=None, sc=None):
     if FU.use_x3(k) and n % 4 == 0:
         gy = gy.contiguous()
         if gy.data_ptr() % 16 == 0:
+            import ctypes as C
+
             lib = FU._setup()
             x3 = (wcache if wcache is not None else _WeightCache()).x3t(w)
             sc = _gy_scale(gy) if sc is None else sc
             gx = torch.empty(gy.shape[0], k, device=gy.device)
-            FU.gemm(FU.dense(gy.data_ptr(), n, n, scale=sc.data_ptr()), None, None, 0, None, gy.shape[0], k, 0,
-                    gx.data_ptr(), k, x3=x3)
+            # gm_gemm_x3_dgrad without a mask (split = k): its LDS-DMA tile at training sizes
+            # (the sequence-batched update's input-gradient kernel), the register-staged one otherwise
+            a = FU.dense(gy.data_ptr(), n, n, scale=sc.data_ptr())
+            L.check(lib.gm_gemm_x3_dgrad(C.byref(a), x3.wp.data_ptr(), x3.sinv.data_ptr(), gy.shape[0], k, k, None,
+                                         0, gx.data_ptr(), k, None, 0, None, None, _s()))
             return gx
     return gy @ w
 
@@ -554,6 +559,70 @@ class _LSTMCellFn(torch.autograd.Function):
         return gx, gw, gb, dc if n[3] else None, None, None, None
 
 
+class _LSTMCell2Fn(torch.autograd.Function):
+    """_LSTMCellFn with x and h as the GEMM's two dense A sources (no [x | h] tensor in the forward,
+    no slicing of its gradient in the backward): gates in the epilogue (fused.pack_lstm), max |[x | h]|
+    published for the weight gradient; backward = the gate-math backward, ONE input-gradient GEMM whose
+    split output writes dx and dh apart (gm_gemm_x3_dgrad), and the weight gradients of W_ih / W_hh."""
+
+    @staticmethod
+    def forward(ctx, x, h, w_ih, w_hh, b_ih, b_hh, c, cell):
+        from . import fused as FU
+
+        M, I = x.shape
+        H = h.shape[1]
+        wp, ldw, bp, x3 = FU.pack_lstm(cell)
+        need_w = ctx.needs_input_grad[2] or ctx.needs_input_grad[3]
+        xs = torch.zeros(1, device=x.device) if need_w else None
+        h1 = torch.empty(M, H, device=x.device)
+        c1 = torch.empty(M, H, device=x.device)
+        act = torch.empty(M, 4 * H, device=x.device)
+        tag = cell.tag and f"lstm:{cell.tag}:{M}x{4 * H}x{I + H}"
+        FU.gemm(FU.dense(x.data_ptr(), x.stride(0), I, amax=None if xs is None else xs.data_ptr()),
+                FU.dense(h.data_ptr(), h.stride(0), H), wp.data_ptr(), ldw, bp.data_ptr(), M, 4 * H, FU.GM_EPI_LSTM,
+                h1.data_ptr(), H, c1.data_ptr(), H, c.data_ptr(), c.stride(0), act.data_ptr(), tag=tag, x3=x3)
+        ctx.xs = None if xs is None else _finish_scale(xs)
+        ctx.save_for_backward(x, h, w_ih, w_hh, act, c, c1)
+        return h1, c1
+
+    @staticmethod
+    def backward(ctx, dh1, dc1):
+        import ctypes as C
+
+        from . import fused as FU
+
+        x, h, w_ih, w_hh, act, c, c1 = ctx.saved_tensors
+        M, H = c.shape
+        I = x.shape[1]
+        dg = torch.empty(M, 4 * H, device=c.device)
+        dc = torch.empty(M, H, device=c.device)
+        sc = torch.empty(1, device=c.device)
+        dh1 = None if dh1 is None else dh1.contiguous()
+        dc1 = None if dc1 is None else dc1.contiguous()
+        cc = c.contiguous()
+        L.check(L.lib().gm_lstm_pointwise_bwd(L.ptr(dh1), L.ptr(dc1), L.ptr(act), L.ptr(cc), L.ptr(c1), M, H,
+                                              L.ptr(dg), L.ptr(dc), L.ptr(sc), _s()))
+        n = ctx.needs_input_grad
+        dx = dh = None
+        if n[0] or n[1]:
+            x3 = _WeightCache().x3t(torch.cat([w_ih, w_hh], 1))
+            dx = torch.empty(M, I, device=c.device)
+            dh = torch.empty(M, H, device=c.device)
+            a = FU.dense(dg.data_ptr(), 4 * H, 4 * H, scale=sc.data_ptr())
+            L.check(FU._setup().gm_gemm_x3_dgrad(C.byref(a), x3.wp.data_ptr(), x3.sinv.data_ptr(), M, I + H, I, None,
+                                                 0, dx.data_ptr(), I, dh.data_ptr(), H, None, None, _s()))
+        gwi = _wgrad(dg, x, I, sc, ctx.xs) if n[2] else None
+        gwh = _wgrad(dg, h, H, sc, ctx.xs) if n[3] else None
+        gb = dg.sum(0) if (n[4] or n[5]) else None
+        return (dx if n[0] else None, dh if n[1] else None, gwi, gwh, gb if n[4] else None,
+                (gb.clone() if n[4] else gb) if n[5] else None, dc if n[6] else None, None)
+
+
+def _two_source_ok(x, h):
+    return (x.dim() == 2 and h.dim() == 2 and x.stride(1) == 1 and h.stride(1) == 1 and x.stride(0) % 4 == 0
+            and h.stride(0) % 4 == 0 and x.data_ptr() % 16 == 0 and h.data_ptr() % 16 == 0 and x.shape[1] % 32 == 0)
+
+
 class LSTMCell(nn.Module):
     """nn.LSTMCell parameters/semantics; gates = [x|h] @ [W_ih|W_hh]^T + (b_ih + b_hh)
     in one MFMA GEMM, gate math in gm_lstm_pointwise."""
@@ -573,6 +642,11 @@ class LSTMCell(nn.Module):
 
     def forward(self, x, state):
         h, c = state
+        if (torch.is_grad_enabled() and x.shape[0] >= 4096 and self.hidden_size % 32 == 0
+                and self.input_size == self.hidden_size and _x3_rows_ok(x, x.stride(0), 4 * self.hidden_size)
+                and _two_source_ok(x, h) and c.is_contiguous()
+                and (self.weight_ih.requires_grad or x.requires_grad or h.requires_grad)):
+            return _LSTMCell2Fn.apply(x, h, self.weight_ih, self.weight_hh, self.bias_ih, self.bias_hh, c, self)
         xh = torch.cat([x, h], -1)
         w = torch.cat([self.weight_ih, self.weight_hh], 1)
         b = self.bias_ih + self.bias_hh

@@ -390,6 +390,16 @@ int gm_gemm_range_status(int32_t* status, int32_t clear);
 int gm_gemm_x3_head(const gm_a_src* src0, const void* wp, const float* wscale_inv, const float* b, int32_t m,
                     int32_t n, int32_t act, const float* wq, int64_t ldwq, const float* bq, int32_t nq, float* q,
                     int64_t ldq, float* y, int64_t ldy, void* stream);
+/* The DQN's two hidden layers and its Q head in ONE launch (src/model.py:187-203 DQN with mlp_units
+ * 512, 256 and <= 4 actions; split-f16 form): h1 = act1(A W1^T + b1) with A from a0 (dense rows, or
+ * the NetMon READOUT gather) ++ the optional dense a1 (as gm_gemm_x3, W1 packed for the combined K),
+ * q = act2(h1 W2^T + b2) wq^T + bq. A 64-row block keeps its rows' h1 on chip (LDS, split f16), so
+ * the m x 512 activation is never written; the hidden layer-2 activation neither. w1p / w2p and
+ * w1sinv / w2sinv: gm_gemm_pack_x3 of W1 [512][K] and W2 [256][512]. */
+int gm_dqn_x3(const gm_a_src* a0, const gm_a_src* a1, const void* w1p, const float* w1sinv, const float* b1,
+              int32_t act1, const void* w2p, const float* w2sinv, const float* b2, int32_t act2, int32_t m, int32_t n1,
+              int32_t n2, const float* wq, int64_t ldwq, const float* bq, int32_t nq, float* q, int64_t ldq,
+              void* stream);
 /* Input-gradient GEMM of a layer whose input went through leaky_relu (the reference MLP's
  * F.leaky_relu, src/model.py:13-42, backward of torch autograd, src/main.py:996): D = src0 . W^T
  * in split-f16 form over wp = gm_gemm_pack_x3 of W^T ([n][K], K = src0->k; src0 DENSE, its

@@ -9,6 +9,6 @@ for d in ${DIAGS:-1 2 3}; do
   mkdir -p ../lib/diag$d
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -I../../include -DGM_DIAG=$d -c gm_gemm.hip -o ../lib/diag$d/gm_gemm.o || exit 1
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o ../lib/diag$d/libgraphmarl_amd.so ../lib/obj/gm_env.o \
-      ../lib/obj/gm_netmon.o ../lib/obj/gm_simple.o ../lib/obj/gm_agents.o ../lib/diag$d/gm_gemm.o || exit 1
+      ../lib/obj/gm_netmon.o ../lib/obj/gm_simple.o ../lib/obj/gm_agents.o ../lib/obj/gm_replay.o ../lib/diag$d/gm_gemm.o || exit 1
   rm -f ../lib/diag$d/gm_gemm.o
 done
