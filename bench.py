@@ -361,7 +361,8 @@ def main():
         g = graph or 1
         with torch.no_grad():
             ro.reset()
-            for _ in range(warmup + (warmup % 2 if graph else 0)):
+            # graph replays start at multiples of the captured length: warm up to one
+            for _ in range(-(-warmup // graph) * graph if graph else warmup):
                 ro.step()
             if graph:
                 # capture after the eager warmup (packed weights, scratch buffers exist), then
