@@ -522,6 +522,7 @@ def main():
             "roofline": roof, "roofline_hbm": roof_hbm or None, "cpu_baseline": cpu, "f32_exact_gemms": f32cmp, "rollout_train": train,
             "other_configs": extras,
             "kernels": kernels,
+            "build": L.build_info(),
         }
         print(json.dumps(line))
     if world > 1:

@@ -27,14 +27,16 @@ EXPORTS = [
     "gm_env_step", "gm_env_observe", "gm_env_topology", "gm_env_final_info", "gm_policy_egreedy", "gm_env_policy_step",
     "gm_env_get_state", "gm_env_set_state", "gm_build_seed_list", "gm_mp_aggregate", "gm_mp_aggregate_rows", "gm_mp_aggregate_bwd", "gm_leaky_bwd", "gm_netmon_readout",
     "gm_netmon_readout_bwd", "gm_lstm_pointwise", "gm_lstm_pointwise_bwd", "gm_linear_f32", "gm_gemm_f32",
-    "gm_gemm_set_tile", "gm_gemm_set_wgrad", "gm_gemm_set_mfma", "gm_gemm_set_dgrad", "gm_simple_create", "gm_simple_destroy", "gm_simple_reset", "gm_simple_step",
+    "gm_simple_create", "gm_simple_destroy", "gm_simple_reset", "gm_simple_step",
     "gm_simple_observe", "gm_simple_policy_egreedy", "gm_simple_get_state", "gm_env_set_topology",
     "gm_policy_shortest_path", "gm_env_first_hops", "gm_routing_node_encoder", "gm_gemm_x3", "gm_gemm_x3_head", "gm_absmax_scale", "gm_absmax_scale_rows", "gm_gemm_x3_wgrad", "gm_absmax_finish",
     "gm_gemm_pack_x3", "gm_gemm_pack_x3_bytes", "gm_gemm_range_status",
     "gm_pcg64_seed", "gm_pcg64_choice", "gm_lnlstm_pointwise", "gm_agent_attention", "gm_agent_comm",
     "gm_gemm_x3_dgrad", "gm_lstm_cell_bwd", "gm_qhead_bwd", "gm_netmon_readout_ld", "gm_routing_node_encoder_bits", "gm_gather_records",
-    "gm_lnlstm_fwd", "gm_lnlstm_bwd", "gm_gru_pointwise", "gm_gru_bwd", "gm_act_bwd", "gm_dqn_x3",
+    "gm_lnlstm_fwd", "gm_lnlstm_bwd", "gm_gru_pointwise", "gm_gru_bwd", "gm_act_bwd", "gm_dqn_x3", "gm_build_info",
 ]
+# kernel-form switches (include/graph_marl_amd_tuning.h)
+TUNING_EXPORTS = ["gm_gemm_set_tile", "gm_gemm_set_wgrad", "gm_gemm_set_mfma", "gm_gemm_set_dgrad"]
 
 # Arithmetic form of the fused rollout GEMMs (graph-marl_amd/fused.py): "x3" = split-f16
 # MFMA with fp32 accumulation (default), "f32" = exact fp32 MFMA. GM_GEMM=f32 selects the
@@ -175,6 +177,8 @@ def lib():
     for name, at in newer.items():
         if hasattr(L, name) or not os.environ.get("GM_LIB"):
             getattr(L, name).argtypes = at
+    if hasattr(L, "gm_build_info"):
+        L.gm_build_info.restype = C.c_char_p
     if MFMA_SHAPE is not None:
         if L.gm_gemm_set_mfma({"16": 1, "32": 0, "16all": 2}[MFMA_SHAPE]) != 0:
             raise GMError(L.gm_last_error().decode())
@@ -182,6 +186,37 @@ def lib():
         raise GMError(L.gm_last_error().decode())
     _lib = L
     return L
+
+
+def source_hash():
+    """16 hex digits of the SHA-256 of the kernel sources and public headers, in the order the
+    Makefile hashes them (byte-sorted csrc/gm_*.hip + gm_*.hpp, then include/*.h)."""
+    import glob
+    import hashlib
+
+    csrc, inc = os.path.join(HERE, "csrc"), os.path.join(os.path.dirname(HERE), "include")
+    files = sorted(glob.glob(os.path.join(csrc, "gm_*.hip")) + glob.glob(os.path.join(csrc, "gm_*.hpp")),
+                   key=lambda f: os.path.basename(f).encode())
+    files += sorted(glob.glob(os.path.join(inc, "*.h")), key=lambda f: os.path.basename(f).encode())
+    h = hashlib.sha256()
+    for f in files:
+        with open(f, "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]
+
+
+def build_info():
+    """gm_build_info() of the loaded library as a dict (src, arch, hipcc), plus whether its source
+    hash matches the tree's sources (None when the sources are not present)."""
+    L = lib()
+    if not hasattr(L, "gm_build_info"):
+        return {"src": None, "matches_tree": None}
+    d = dict(kv.split("=", 1) for kv in L.gm_build_info().decode().split())
+    try:
+        d["matches_tree"] = d.get("src") == source_hash()
+    except OSError:
+        d["matches_tree"] = None
+    return d
 
 
 def check(rc):

@@ -465,25 +465,12 @@ int gm_agent_attention(const float* q, const float* k, const float* v, int64_t l
 int gm_agent_comm(const float* h, int64_t ldh, const int8_t* adj, int32_t B, int32_t A, int32_t H, float* out,
                   int64_t ldo, void* stream);
 
-/* Tuning knob: tile configuration of gm_gemm_f32 (-1 = per-shape default; 0 = 128x128x32;
- * 1 = 128x256x16; 2 = 256x128x16 (LSTM: 256x128x16); 3 = 128x128x16; 4 = 128x128x16 at 4
- * blocks/CU); of gm_gemm_x3 (-1/0 = 128x128x16; 1 = 128x256x16 (LSTM: 128x128x32);
- * 2 = 128x128x32 (LSTM: 256x128x16)). Process-wide. */
-/* Weight-gradient kernel of gm_gemm_x3_wgrad (same arithmetic, diagnostics / A-B timing):
- * -1 (default) or 1 = transposed LDS reads (ds_read_b64_tr_b16) with 128 x 128 tiles, 2 = the same
- * with 128 x 256 tiles, 3 = 128 x 128 tiles on v_mfma_f32_16x16x32_f16, 0 = the dword-load
- * register-transpose form (tools/wgrad_bench.py). */
-int gm_gemm_set_wgrad(int32_t form);
-int gm_gemm_set_tile(int32_t tile);
-/* MFMA shape of the LDS-DMA split-f16 kernel (gm_gemm_x3's dense / readout tiles, gm_gemm_x3_head):
- * 2 (default) = v_mfma_f32_16x16x32_f16 everywhere, 1 = 16x16x32 except gm_gemm_x3_head (32x32x16),
- * 0 = v_mfma_f32_32x32x16_f16 everywhere. Same tiles and operand images; the summation order inside
- * an MFMA differs (fp32-order results either way). */
-int gm_gemm_set_mfma(int32_t shape);
-/* Input-gradient kernel of gm_gemm_x3_dgrad (same arithmetic and epilogue contract; A-B timing):
- * -1 (default) = per-shape choice, 0 = register-staged 128 x 128 tile (k_gemm3), 1 = LDS-DMA
- * 128 x 128 tile (4 waves, 2 blocks/CU), 2 = LDS-DMA 128 x 256 tile (8 waves). Process-wide. */
-int gm_gemm_set_dgrad(int32_t form);
+/* Build provenance: "src=<16 hex digits of the SHA-256 of the csrc sources and headers> arch=<gfx> hipcc=<version>",
+ * fixed when the library is linked (tests/test_capi.py checks it against the tree; bench.py reports it). */
+const char* gm_build_info(void);
+
+/* Process-wide kernel-form switches for A/B timing live in graph_marl_amd_tuning.h. */
+#include "graph_marl_amd_tuning.h"
 
 /* ---------------------------------------------------------------------------
  * SimpleEnvironment (src/env/simple_environment.py:45-334; BASELINE config 1):

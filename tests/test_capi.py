@@ -9,16 +9,28 @@ import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 HEADER = os.path.join(ROOT, "include", "graph_marl_amd.h")
+TUNING = os.path.join(ROOT, "include", "graph_marl_amd_tuning.h")
 
 
-def declared_functions():
-    txt = open(HEADER).read()
+def declared_functions(path=None):
+    if path is None:
+        return declared_functions(HEADER) | declared_functions(TUNING)
+    txt = open(path).read()
     txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
     return set(re.findall(r"\b(gm_[a-z0-9_]+)\s*\(", txt))
 
 
 def test_header_and_binding_agree(gm):
-    assert declared_functions() == set(gm._lib.EXPORTS)
+    assert declared_functions(HEADER) == set(gm._lib.EXPORTS)
+    assert declared_functions(TUNING) == set(gm._lib.TUNING_EXPORTS)
+
+
+def test_library_was_built_from_these_sources(gm):
+    """gm_build_info() carries the SHA-256 of the sources the library was linked from: a stale
+    in-tree .so (sources edited, library not rebuilt) fails here."""
+    info = gm._lib.build_info()
+    assert info["arch"] == "gfx950"
+    assert info["src"] == gm._lib.source_hash(), f"library built from other sources: {info}"
 
 
 def test_library_exports_every_declared_symbol(gm):

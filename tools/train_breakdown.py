@@ -22,9 +22,15 @@ for part, s in (("forward+target", seq[:b]), ("backward", seq[b:])):
     agg = collections.Counter()
     cnt = collections.Counter()
     for r in s:
-        k = (r["Kernel_Name"].replace("_ZN12_GLOBAL__N_1", "")[:44], r["Grid_Size_X"])
+        k = (r["Kernel_Name"].replace("_ZN12_GLOBAL__N_1", "")[:44], r["Grid_Size_X"] + "x" + r.get("Grid_Size_Y", "1"))
         agg[k] += dur(r)
         cnt[k] += 1
     print(part)
     for k, v in agg.most_common(int(sys.argv[2]) if len(sys.argv) > 2 else 24):
         print(f"{v:9.1f} us {cnt[k]:4d}x  grid {k[1]:>9}  {k[0]}")
+
+if len(sys.argv) > 3 and sys.argv[3] == "order":  # every backward launch above 50 us, in launch order
+    print("backward launches in order")
+    for r in seq[b:]:
+        if dur(r) > 50:
+            print(f"{dur(r):9.1f} us  grid {r['Grid_Size_X']:>9}x{r.get('Grid_Size_Y', '1'):<5} {r['Kernel_Name'][:60]}")
