@@ -54,6 +54,10 @@ if MFMA_SHAPE not in (None, "16", "32", "16all"):
 DGRAD_FORM = os.environ.get("GM_DGRAD")
 if DGRAD_FORM not in (None, "-1", "0", "1", "2"):
     raise ValueError(f"GM_DGRAD must be -1, 0, 1 or 2, not {DGRAD_FORM!r}")
+# weight-gradient kernel form of gm_gemm_x3_wgrad (gm_gemm_set_wgrad: -1 default, 0..3, +8 dispatch order)
+WGRAD_FORM = os.environ.get("GM_WGRAD")
+if WGRAD_FORM is not None and WGRAD_FORM not in [str(v) for v in (-1, 0, 1, 2, 3, 8, 9, 10, 11)]:
+    raise ValueError(f"GM_WGRAD must be -1, 0..3 or 8..11, not {WGRAD_FORM!r}")
 
 
 class EnvConfig(C.Structure):
@@ -183,6 +187,8 @@ def lib():
         if L.gm_gemm_set_mfma({"16": 1, "32": 0, "16all": 2}[MFMA_SHAPE]) != 0:
             raise GMError(L.gm_last_error().decode())
     if DGRAD_FORM is not None and L.gm_gemm_set_dgrad(int(DGRAD_FORM)) != 0:
+        raise GMError(L.gm_last_error().decode())
+    if WGRAD_FORM is not None and L.gm_gemm_set_wgrad(int(WGRAD_FORM)) != 0:
         raise GMError(L.gm_last_error().decode())
     _lib = L
     return L

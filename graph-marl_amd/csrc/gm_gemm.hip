@@ -2536,13 +2536,17 @@ __global__ __launch_bounds__(256, 2) void k_gemm3_kmajor(const float* __restrict
 // MF = 1: v_mfma_f32_16x16x32_f16 (16-lane group g reads k rows 8 g .. 8 g + 7 of its 16 columns; the
 // images' 32-byte column segments are XOR-swizzled by bit 3 of the k row so that the two groups of a
 // 32-lane half (rows 8 g + q, 8 (g + 1) + q) hit disjoint banks)
+// XCD = 1: the (tile, k chunk) of a block comes from a permutation of the dispatch order that puts
+// every tile of a k chunk on one XCD (workgroups go to the 8 XCDs round-robin by linear id), so the
+// chunk's A and B rows are fetched into that XCD's L2 once and reused by all its tiles there
+// (identity order: the tiles of a chunk spread over the 8 XCDs and each L2 fetches its own copy)
 template <int BN, int MF = 0>
 __global__ __launch_bounds__(256, BN == 128 ? 2 : 1) void k_wgrad_tr(const float* __restrict__ A, long long lda,
                                                                    unsigned abytes, const float* __restrict__ B,
                                                                    long long ldb, unsigned bbytes, int M, int N, int K,
                                                                    int kchunk, const float* __restrict__ sa,
                                                                    const float* __restrict__ sb, float* __restrict__ C,
-                                                                   long long ldc, long long cz) {
+                                                                   long long ldc, long long cz, int xcd) {
     constexpr int BM = 128, BK = 32, TM = 2, TN = BN / 64;
     constexpr int RA = BM * 2 + 64, RB = BN * 2 + 64;  // image row strides (bytes)
     constexpr int LA = BM / 4 * BK / 256, LB = BN / 4 * BK / 256;  // float4 loads per thread
@@ -2550,8 +2554,15 @@ __global__ __launch_bounds__(256, BN == 128 ? 2 : 1) void k_wgrad_tr(const float
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int wr = wave >> 1, wc = wave & 1;
     const int nN = (N + BN - 1) / BN;
-    const int m0 = (blockIdx.x / nN) * BM, n0 = (blockIdx.x % nN) * BN;
-    const int kb = blockIdx.y * kchunk, ke = min(K, kb + kchunk);
+    int tile = blockIdx.x, chunk = blockIdx.y;
+    if (xcd) {  // host guarantees gridDim.x * gridDim.y % 8 == 0
+        const int T = gridDim.x, nb = T * gridDim.y, b = blockIdx.x + blockIdx.y * T;
+        const int l = (b & 7) * (nb >> 3) + (b >> 3);
+        tile = l % T;
+        chunk = l / T;
+    }
+    const int m0 = (tile / nN) * BM, n0 = (tile % nN) * BN;
+    const int kb = chunk * kchunk, ke = min(K, kb + kchunk);
     const int nk = (ke - kb + BK - 1) / BK;
     const float s_a = *sa, s_b = *sb;
     // buffer resources over this block's k chunk only: 32-bit offsets stay small whatever the batch
@@ -2706,7 +2717,7 @@ __global__ __launch_bounds__(256, BN == 128 ? 2 : 1) void k_wgrad_tr(const float
         __syncthreads();
     }
     const float inv = 1.0f / (s_a * s_b);  // powers of two: exact
-    float* Cz = C + (size_t)blockIdx.y * cz;
+    float* Cz = C + (size_t)chunk * cz;
     if constexpr (MF == 1) {
 #pragma unroll
         for (int i = 0; i < 2 * TM; i++)
@@ -2736,6 +2747,7 @@ __global__ __launch_bounds__(256, BN == 128 ? 2 : 1) void k_wgrad_tr(const float
 }
 
 int g_wgrad = -1;  // weight-gradient kernel: -1 / 1 transposed reads 128 x 128 (default), 2 the same 128 x 256, 0 dword form
+int g_wgrad_xcd = 1;  // XCD-grouped k chunks (k_wgrad_tr xcd), when the grid is a multiple of 8
 
 extern "C" int gm_gemm_x3_wgrad(const float* a, int64_t lda, const float* b, int64_t ldb, int32_t m, int32_t n, int32_t k,
                                 int32_t kchunk, const float* sa, const float* sb, float* c, int64_t ldc, void* stream) {
@@ -2755,21 +2767,23 @@ extern "C" int gm_gemm_x3_wgrad(const float* a, int64_t lda, const float* b, int
         const long long ab = kc * lda * 4, bb = kc * ldb * 4;
         if (ab >= 0x7ff00000LL || bb >= 0x7ff00000LL)
             return gm_fail(GM_ERR_UNSUPPORTED, "gm_gemm_x3_wgrad: one k chunk of an operand larger than 2 GB");
+        const int T128 = ((m + 127) / 128) * ((n + 127) / 128);
+        const int xcd = g_wgrad_xcd && (T128 * S) % 8 == 0;
         if (g_wgrad == 3) {  // 16x16x32 MFMA
-            const int T = ((m + 127) / 128) * ((n + 127) / 128);
+            const int T = T128;
             hipLaunchKernelGGL((k_wgrad_tr<128, 1>), dim3(T, S), dim3(256), 0, (hipStream_t)stream, a, (long long)lda,
                                (unsigned)ab, b, (long long)ldb, (unsigned)bb, m, n, k, kchunk, sa, sb, c, (long long)ldc,
-                               (long long)m * ldc);
+                               (long long)m * ldc, xcd);
         } else if (g_wgrad != 2) {  // 128 x 128 tiles at 2 blocks/CU: 8-24 % faster than 128 x 256 at 1 block/CU
-            const int T = ((m + 127) / 128) * ((n + 127) / 128);
+            const int T = T128;
             hipLaunchKernelGGL(k_wgrad_tr<128>, dim3(T, S), dim3(256), 0, (hipStream_t)stream, a, (long long)lda,
                                (unsigned)ab, b, (long long)ldb, (unsigned)bb, m, n, k, kchunk, sa, sb, c, (long long)ldc,
-                               (long long)m * ldc);
+                               (long long)m * ldc, xcd);
         } else {
             const int T = ((m + 127) / 128) * ((n + 255) / 256);
             hipLaunchKernelGGL(k_wgrad_tr<256>, dim3(T, S), dim3(256), 0, (hipStream_t)stream, a, (long long)lda,
                                (unsigned)ab, b, (long long)ldb, (unsigned)bb, m, n, k, kchunk, sa, sb, c, (long long)ldc,
-                               (long long)m * ldc);
+                               (long long)m * ldc, (int)(g_wgrad_xcd && (T * S) % 8 == 0));
         }
     }
     hipError_t e = hipGetLastError();
@@ -2802,8 +2816,9 @@ extern "C" int gm_gemm_pack_x3(const float* w, int64_t ldw, int32_t n, int32_t k
 }
 
 extern "C" int gm_gemm_set_wgrad(int32_t form) {
-    if (form < -1 || form > 3) return gm_fail(GM_ERR_INVALID_ARG, "gm_gemm_set_wgrad: form in [-1, 3]");
-    g_wgrad = form;
+    if (form < -1 || (form >= 0 && ((form & 7) > 3 || form > 11))) return gm_fail(GM_ERR_INVALID_ARG, "gm_gemm_set_wgrad: form in [-1, 3] (+8)");
+    g_wgrad_xcd = form < 0 || !(form & 8);
+    g_wgrad = form < 0 ? form : (form & 7);
     return GM_OK;
 }
 

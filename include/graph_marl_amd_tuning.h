@@ -15,7 +15,8 @@ extern "C" {
 /* Weight-gradient kernel of gm_gemm_x3_wgrad (same arithmetic, diagnostics / A-B timing):
  * -1 (default) or 1 = transposed LDS reads (ds_read_b64_tr_b16) with 128 x 128 tiles, 2 = the same
  * with 128 x 256 tiles, 3 = 128 x 128 tiles on v_mfma_f32_16x16x32_f16, 0 = the dword-load
- * register-transpose form (tools/wgrad_bench.py). */
+ * register-transpose form (tools/wgrad_bench.py). + 8: the same form with the blocks in dispatch order
+ * (default: the tiles of a k chunk grouped on one XCD). */
 int gm_gemm_set_wgrad(int32_t form);
 int gm_gemm_set_tile(int32_t tile);
 /* MFMA shape of the LDS-DMA split-f16 kernel (gm_gemm_x3's dense / readout tiles, gm_gemm_x3_head):

@@ -34,9 +34,18 @@ def main():
         gy = torch.randn(Mb, o, device="cuda") * 1e-6
         x = torch.randn(Mb, ldx, device="cuda")[:, :k]
         r = {}
-        for form, name in ((1, "tr128"), (3, "tr128_mfma16"), (2, "tr256")):
+        sa = M._gy_scale(gy)
+        sb = torch.empty(1, device="cuda")
+        M.L.check(lib.gm_absmax_scale_rows(x.data_ptr(), Mb, k, ldx, sb.data_ptr(), M.L.stream_ptr()))
+        flop = 6.0 * Mb * o * k
+        res = {}
+        for form, name in ((9, "tr128_noxcd"), (1, "tr128"), (3, "tr128_mfma16"), (2, "tr256")):
             lib.gm_gemm_set_wgrad(form)
-            r[name + "_us"] = round(timeit(lambda: M._wgrad(gy, x, k)), 1)
+            us = timeit(lambda: M._wgrad(gy, x, k, sa, sb))
+            r[name + "_us"] = round(us, 1)
+            r[name + "_TF"] = round(flop / us / 1e6, 1)
+            res[name] = M._wgrad(gy, x, k, sa, sb)
+        r["xcd_bitwise_equal"] = bool(torch.equal(res["tr128"], res["tr128_noxcd"]))
         lib.gm_gemm_set_wgrad(-1)
         lib.gm_gemm_set_wgrad(1)
         g1 = M._wgrad(gy, x, k)
