@@ -258,6 +258,45 @@ def stream_ptr(device=None):
     return C.c_void_p(torch.cuda.current_stream(device).cuda_stream)
 
 
+def _tensors(v):
+    """Device tensors held by a cached value (tensor, tuple / list, or an object with __slots__)."""
+    if isinstance(v, torch.Tensor):
+        yield v
+    elif isinstance(v, (tuple, list)):
+        for x in v:
+            yield from _tensors(x)
+    elif v is not None and hasattr(v, "__slots__"):
+        for s in v.__slots__:
+            yield from _tensors(getattr(v, s, None))
+
+
+class Published:
+    """Stream hand-off of a cached device value (packed weights built lazily by whichever stream
+    first needs them). The builder's stream records an event right after the value's kernels;
+    the first use from any other stream makes that stream wait for the event and registers the
+    value's tensors with it (record_stream: their memory is not reused while that stream may still
+    read them after the cache drops the value). StreamedRollout's groups share the caches: without
+    this, group 1's first GEMM could read a pack group 0's stream had not finished writing."""
+    __slots__ = ("ev", "seen")
+
+    def __init__(self):
+        s = torch.cuda.current_stream()
+        self.seen = {s}
+        self.ev = None
+        if not torch.cuda.is_current_stream_capturing():
+            self.ev = torch.cuda.Event()
+            self.ev.record(s)
+
+    def acquire(self, val):
+        s = torch.cuda.current_stream()
+        if s in self.seen or self.ev is None or torch.cuda.is_current_stream_capturing():
+            return  # (a capture starts from a synchronised device: every pack is complete)
+        s.wait_event(self.ev)
+        for t in _tensors(val):
+            t.record_stream(s)
+        self.seen.add(s)
+
+
 def require_gpu():
     if not torch.cuda.is_available():
         raise GMError("graph-marl_amd needs a ROCm GPU (torch.cuda.is_available() is False); there is no CPU path")

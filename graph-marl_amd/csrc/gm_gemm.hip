@@ -1562,12 +1562,21 @@ __global__ __launch_bounds__(WGM* WGN * 64, OCC) void k_gemm3g(ASrc a0, ASrc a1,
                     x0 *= ascale;
                     x1 *= ascale;
                 }
+#if GM_DIAG == 11  // diagnostic build 11: A read as if stored pre-split (timing only)
+                sah[i] = __builtin_bit_cast(half8, x0);
+                sal[i] = __builtin_bit_cast(half8, x1);
+#else
                 split8(x0, x1, sah[i], sal[i]);
+#endif
             }
         }
 #pragma unroll
         for (int j = 0; j < TN; j++) {
+#if GM_DIAG == 11 || GM_DIAG == 12  // diagnostic builds 11, 12: no w_hi scaling (timing only)
+            const half8 bs = f.bh[j];
+#else
             const half8 bs = f.bh[j] * s12;  // w_hi * 2^-12, exact
+#endif
 #pragma unroll
             for (int i = 0; i < 2 * TM; i++) {
                 floatx4& c = acc4[i][sb * TN + j];

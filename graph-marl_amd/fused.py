@@ -134,16 +134,21 @@ def _key(*ts):
 
 
 class Packed:
-    """Per-module cache of packed weights, refreshed when a parameter changes."""
+    """Per-module cache of packed weights, refreshed when a parameter changes; safe to share
+    between streams (L.Published)."""
 
     def __init__(self):
         self.key = None
         self.val = None
+        self.pub = None
 
     def get(self, key, fn):
         if key != self.key:
             self.val = fn()
             self.key = key
+            self.pub = L.Published()
+        else:
+            self.pub.acquire(self.val)
         return self.val
 
 

@@ -58,42 +58,41 @@ class _WeightCache:
     split-f16 packing for gm_gemm_x3 (both refreshed when the parameter changes)."""
 
     def __init__(self):
-        self.key = None
-        self.val = None
-        self.key3 = None
-        self.val3 = None
+        self.slots = {}  # form -> (key, value, L.Published): shared by streams (StreamedRollout groups)
+
+    def _get(self, form, key, build):
+        k, v, pub = self.slots.get(form, (None, None, None))
+        if k != key:
+            v = build()
+            self.slots[form] = (key, v, L.Published())
+        else:
+            pub.acquire(v)
+        return v
 
     def x3(self, w):
         from . import fused as FU
 
-        key = (w.data_ptr(), w._version)
-        if self.key3 != key:
+        def build():
             wp, ldw = self.get(w)
-            self.val3 = FU.X3(wp, ldw, w.shape[0], w.shape[1])
-            self.key3 = key
-        return self.val3
+            return FU.X3(wp, ldw, w.shape[0], w.shape[1])
+        return self._get("x3", (w.data_ptr(), w._version), build)
 
     def x3t(self, w):
         """split-f16 packing of w^T ([in][out]) for the input-gradient GEMM gx = gy @ w."""
         from . import fused as FU
 
-        key = (w.data_ptr(), w._version)
-        if getattr(self, "key3t", None) != key:
+        def build():
             wt, ldt = FU._pad_cols(w.detach().t())
-            self.val3t = FU.X3(wt, ldt, w.shape[1], w.shape[0])
-            self.key3t = key
-        return self.val3t
+            return FU.X3(wt, ldt, w.shape[1], w.shape[0])
+        return self._get("x3t", (w.data_ptr(), w._version), build)
 
     def get(self, w):
         n, k = w.shape
         kp = _pad_stride(k)
         if kp == k and w.is_contiguous():
             return w, k
-        key = (w.data_ptr(), w._version, kp)
-        if self.key != key:
-            self.val = F.pad(w.detach(), (0, kp - k)).contiguous()
-            self.key = key
-        return self.val, kp
+        return self._get("pad", (w.data_ptr(), w._version, kp),
+                         lambda: F.pad(w.detach(), (0, kp - k)).contiguous()), kp
 
 
 def _x3_rows_ok(x2d, ldx, n):
