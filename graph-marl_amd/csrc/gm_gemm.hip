@@ -36,6 +36,9 @@
 #include <cstring>
 #include <type_traits>
 
+#ifndef GM_SPLIT_LDEXP
+#define GM_SPLIT_LDEXP 1  // 0: 4096 x by v_pk_mul_f32 in the split (A/B: rollout -0.9 %, training within noise)
+#endif
 #ifndef GM_DIAG
 #define GM_DIAG 0  // 1: no A split, 2: no loads/stores in the k loop, 3: as 2 without barriers
 #endif
@@ -200,16 +203,24 @@ __device__ __forceinline__ void split4(float4 v, half4& hi, half4& lo) {
 // 4096 x (packed multiply, exact), lo = f16(fma(hi, -4096, X)) = f16(4096 (x - hi)) by
 // v_fma_mix{lo,hi}_f16 (the f16 hi read as f32 by the mixed fma; one rounding, RNE), the
 // same bits as split4.
-__device__ __forceinline__ void split8(floatx4 x0, floatx4 x1, half8& hi, half8& lo) {
+// GM_SPLIT_LDEXP: the split of x * 2^e (e = 0, or a device power-of-two operand scale) with 4096 x by
+// v_ldexp_f32 instead of v_pk_mul_f32 (packed f32 VALU beside MFMAs costs extra issue cycles)
+__device__ __forceinline__ void split8(floatx4 x0, floatx4 x1, half8& hi, half8& lo, int e = 0) {
     typedef float floatx2 __attribute__((ext_vector_type(2)));
     typedef _Float16 half2_t __attribute__((ext_vector_type(2)));
     const float m4096 = -4096.0f;
     unsigned hp[4], lp[4];
 #pragma unroll
     for (int q = 0; q < 4; q++) {
-        const floatx2 x = q < 2 ? floatx2{x0[2 * q], x0[2 * q + 1]} : floatx2{x1[2 * q - 4], x1[2 * q - 3]};
+        floatx2 x = q < 2 ? floatx2{x0[2 * q], x0[2 * q + 1]} : floatx2{x1[2 * q - 4], x1[2 * q - 3]};
+#if GM_SPLIT_LDEXP
+        const floatx2 X = {__builtin_ldexpf(x[0], e + 12), __builtin_ldexpf(x[1], e + 12)};
+        if (e != 0) x = floatx2{__builtin_ldexpf(x[0], e), __builtin_ldexpf(x[1], e)};
+        hp[q] = __builtin_bit_cast(unsigned, __builtin_convertvector(x, half2_t));
+#else
         hp[q] = __builtin_bit_cast(unsigned, __builtin_convertvector(x, half2_t));
         const floatx2 X = x * 4096.0f;
+#endif
         unsigned l;
         asm("v_fma_mixlo_f16 %0, %1, %2, %3 op_sel_hi:[1,0,0]" : "=&v"(l) : "v"(hp[q]), "s"(m4096), "v"(X[0]));
         asm("v_fma_mixhi_f16 %0, %1, %2, %3 op_sel:[1,0,0] op_sel_hi:[1,0,0]"
@@ -220,6 +231,30 @@ __device__ __forceinline__ void split8(floatx4 x0, floatx4 x1, half8& hi, half8&
     typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
     hi = __builtin_bit_cast(half8, u32x4_t{hp[0], hp[1], hp[2], hp[3]});
     lo = __builtin_bit_cast(half8, u32x4_t{lp[0], lp[1], lp[2], lp[3]});
+}
+
+// split4 of v * 2^e (a device power-of-two operand scale) without packed f32 VALU: hi = f16(ldexp(v, e))
+// (cvt_pk), lo = f16(fma(hi, -4096, ldexp(v, e + 12))) by v_fma_mix{lo,hi}_f16; the same bits as
+// split4(v * 2^e) while v * 2^e is finite and normal
+__device__ __forceinline__ void split4e(float4 v, int e, half4& hi, half4& lo) {
+    typedef float floatx2 __attribute__((ext_vector_type(2)));
+    typedef _Float16 half2_t __attribute__((ext_vector_type(2)));
+    const float m4096 = -4096.0f;
+    const float x[4] = {v.x, v.y, v.z, v.w};
+    unsigned hp[2], lp[2];
+#pragma unroll
+    for (int q = 0; q < 2; q++) {
+        const floatx2 xs = {__builtin_ldexpf(x[2 * q], e), __builtin_ldexpf(x[2 * q + 1], e)};
+        hp[q] = __builtin_bit_cast(unsigned, __builtin_convertvector(xs, half2_t));
+        const float X0 = __builtin_ldexpf(x[2 * q], e + 12), X1 = __builtin_ldexpf(x[2 * q + 1], e + 12);
+        unsigned l;
+        asm("v_fma_mixlo_f16 %0, %1, %2, %3 op_sel_hi:[1,0,0]" : "=&v"(l) : "v"(hp[q]), "s"(m4096), "v"(X0));
+        asm("v_fma_mixhi_f16 %0, %1, %2, %3 op_sel:[1,0,0] op_sel_hi:[1,0,0]" : "+v"(l) : "v"(hp[q]), "s"(m4096), "v"(X1));
+        lp[q] = l;
+    }
+    typedef unsigned u32x2_t __attribute__((ext_vector_type(2)));
+    hi = __builtin_bit_cast(half4, u32x2_t{hp[0], hp[1]});
+    lo = __builtin_bit_cast(half4, u32x2_t{lp[0], lp[1]});
 }
 
 // LSTM epilogue input c, loaded into registers before the k loop (the loads retire behind
@@ -788,6 +823,7 @@ __global__ __launch_bounds__(WGM* WGN * 64, OCC) void k_gemm3(ASrc a0, ASrc a1, 
     };
     const bool ascaled = a0.scale != nullptr;  // uniform
     const float ascale = ascaled ? *a0.scale : 1.0f;
+    const int aexp = __builtin_amdgcn_frexp_expf(ascale) - 1;  // ascale = 2^aexp
     unsigned* const amax = a0.amax;  // uniform
     float amx = 0.f;
     auto lstore = [&](auto SET, int buf, int k0) {
@@ -811,12 +847,14 @@ __global__ __launch_bounds__(WGM* WGN * 64, OCC) void k_gemm3(ASrc a0, ASrc a1, 
                 if (kk + 3 >= kend) v.w = 0.f;
             }
             if (amax) amx = fmaxf(amx, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
-            if (ascaled) v = make_float4(v.x * ascale, v.y * ascale, v.z * ascale, v.w * ascale);
             half4 hi, lo;
 #if GM_DIAG == 1  // diagnostic build: raw bits instead of the split
             hi = __builtin_bit_cast(half4, make_float2(v.x, v.y));
             lo = __builtin_bit_cast(half4, make_float2(v.z, v.w));
+#elif GM_SPLIT_LDEXP
+            split4e(v, aexp, hi, lo);
 #else
+            if (ascaled) v = make_float4(v.x * ascale, v.y * ascale, v.z * ascale, v.w * ascale);
             split4(v, hi, lo);
 #endif
             char* row = as + (rbase + q * RSTEP) * ROWB;
@@ -1361,7 +1399,7 @@ __global__ __launch_bounds__(WGM* WGN * 64, OCC) void k_gemm3g(ASrc a0, ASrc a1,
     constexpr int STAGE_B = (BM + BN) * 128;
     static_assert(BM % (8 * NW) == 0 && BN % (8 * NW) == 0, "tile rows per wave");
     static_assert(AMODE != GM_A_AGGREGATE, "aggregate source uses k_gemm3");
-    static_assert(STAGES == 2 || STAGES == 3, "stages");
+    static_assert(STAGES >= 2 && STAGES <= 4, "stages");
     __shared__ __attribute__((aligned(16))) char lds[STAGES * STAGE_B];
 
     const int tid = threadIdx.x, lane = tid & 63;
@@ -1513,6 +1551,7 @@ __global__ __launch_bounds__(WGM* WGN * 64, OCC) void k_gemm3g(ASrc a0, ASrc a1,
     half8 sah[2 * TM], sal[2 * TM];  // 16x16 form: split A of the current k tile (both column halves)
     const _Float16 s12 = (_Float16)(1.0f / 4096.0f);
     const float ascale = AX == 2 ? *a0.scale : 1.0f;
+    const int aexp = __builtin_amdgcn_frexp_expf(ascale) - 1;  // ascale = 2^aexp
     float amx = 0.f;  // AX 1: max |A| over the fragments this lane reads (all A elements of the tile
                       // are read by some lane of every column wave; ragged columns zeroed first)
     // fragments of one 16-deep half (SB) of a k tile: A raw fp32 (split at use), B hi / lo
@@ -1549,16 +1588,17 @@ __global__ __launch_bounds__(WGM* WGN * 64, OCC) void k_gemm3g(ASrc a0, ASrc a1,
             f.bl[j] = *reinterpret_cast<const half8*>(sbase + boff[sb][1] + j * 32 * 128);
         }
     };
-    auto mfma16 = [&](const Frag& f, auto SB) {
+    auto mfma16 = [&](const Frag& f, auto SB, auto J0, auto J1) {
         constexpr int sb = decltype(SB)::value;
-        if constexpr (sb == 0) {
+        constexpr int j0 = decltype(J0)::value, j1 = decltype(J1)::value;
+        if constexpr (sb == 0 && j0 == 0) {
 #pragma unroll
             for (int i = 0; i < 2 * TM; i++) {
                 floatx4 x0 = f.xa[i][0], x1 = f.xa[i][1];
                 if constexpr (AX == 1) {
 #pragma unroll
                     for (int e = 0; e < 4; e++) amx = fmaxf(amx, fmaxf(fabsf(x0[e]), fabsf(x1[e])));
-                } else if constexpr (AX == 2) {
+                } else if constexpr (AX == 2 && !GM_SPLIT_LDEXP) {
                     x0 *= ascale;
                     x1 *= ascale;
                 }
@@ -1566,12 +1606,12 @@ __global__ __launch_bounds__(WGM* WGN * 64, OCC) void k_gemm3g(ASrc a0, ASrc a1,
                 sah[i] = __builtin_bit_cast(half8, x0);
                 sal[i] = __builtin_bit_cast(half8, x1);
 #else
-                split8(x0, x1, sah[i], sal[i]);
+                split8(x0, x1, sah[i], sal[i], AX == 2 && GM_SPLIT_LDEXP ? aexp : 0);
 #endif
             }
         }
 #pragma unroll
-        for (int j = 0; j < TN; j++) {
+        for (int j = j0; j < j1; j++) {
 #if GM_DIAG == 11 || GM_DIAG == 12  // diagnostic builds 11, 12: no w_hi scaling (timing only)
             const half8 bs = f.bh[j];
 #else
@@ -1598,11 +1638,11 @@ __global__ __launch_bounds__(WGM* WGN * 64, OCC) void k_gemm3g(ASrc a0, ASrc a1,
             if constexpr (AX == 1) {
 #pragma unroll
                 for (int e = 0; e < 4; e++) amx = fmaxf(amx, fmaxf(fabsf(x0[e]), fabsf(x1[e])));
-            } else if constexpr (AX == 2) {
+            } else if constexpr (AX == 2 && !GM_SPLIT_LDEXP) {
                 x0 *= ascale;
                 x1 *= ascale;
             }
-            split8(x0, x1, ah[i], al[i]);
+            split8(x0, x1, ah[i], al[i], AX == 2 && GM_SPLIT_LDEXP ? aexp : 0);
 #endif
         }
 #pragma unroll
@@ -1639,6 +1679,7 @@ __global__ __launch_bounds__(WGM* WGN * 64, OCC) void k_gemm3g(ASrc a0, ASrc a1,
     using I0 = std::integral_constant<int, 0>;
     using I1 = std::integral_constant<int, 1>;
     using I2 = std::integral_constant<int, 2>;
+    using I3 = std::integral_constant<int, 3>;
     // Pipeline, one barrier per k tile placed MID-step: tile t lives in stage t % STAGES.
     //   step k: read half 1 of tile k | MFMAs half 0 of tile k | wait own DMA of tile k+1,
     //   lgkmcnt(0), barrier B_k | DMA tile k+STAGES into stage k (every wave is past its reads
@@ -1647,17 +1688,22 @@ __global__ __launch_bounds__(WGM* WGN * 64, OCC) void k_gemm3g(ASrc a0, ASrc a1,
     // steps to land.
     issue(I0{}, 0);
     if (nk > 1) issue(I1{}, 1);
-    if constexpr (STAGES == 3)
+    if constexpr (STAGES >= 3)
         if (nk > 2) issue(I2{}, 2);
-    {
-        const int out = min(STAGES - 1, nk - 1);  // tiles issued after tile 0
-        if (out >= 2)
+    if constexpr (STAGES >= 4)
+        if (nk > 3) issue(I3{}, 3);
+    // wait until this wave's DMA of the oldest tile landed, n younger tiles left in flight
+    auto wait_landed = [&](int n) {
+        if (n >= 3)
+            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(3 * NL) : "memory");
+        else if (n == 2)
             asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * NL) : "memory");
-        else if (out == 1)
+        else if (n == 1)
             asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NL) : "memory");
         else
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
+    };
+    wait_landed(min(STAGES - 1, nk - 1));  // tiles issued after tile 0
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
     if (ragged && nk == 1) zero_tail(I0{});
@@ -1677,17 +1723,14 @@ __global__ __launch_bounds__(WGM* WGN * 64, OCC) void k_gemm3g(ASrc a0, ASrc a1,
         read(ST, I1{}, f1);
         __builtin_amdgcn_sched_barrier(0);
         if constexpr (MF == 1)
-            mfma16(f0, I0{});
+            mfma16(f0, I0{}, I0{}, std::integral_constant<int, TN>{});
         else
             mfma(f0);
         __builtin_amdgcn_sched_barrier(0);
         if (kt + 1 < nk) {
 #endif
             // own DMA of tile kt+1 landed (tiles kt+2 .. kt+STAGES-1 may stay in flight)
-            if (STAGES == 3 && kt + 2 < nk)
-                asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NL) : "memory");
-            else
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            wait_landed(min(STAGES - 2, nk - 2 - kt));
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's reads of tile kt done
             __builtin_amdgcn_s_barrier();
             asm volatile("" ::: "memory");  // no LDS access moves across the barrier
@@ -1697,7 +1740,7 @@ __global__ __launch_bounds__(WGM* WGN * 64, OCC) void k_gemm3g(ASrc a0, ASrc a1,
         }
         __builtin_amdgcn_sched_barrier(0);
         if constexpr (MF == 1)
-            mfma16(f1, I1{});
+            mfma16(f1, I1{}, I0{}, std::integral_constant<int, TN>{});
         else
             mfma(f1);
     };
@@ -1707,8 +1750,10 @@ __global__ __launch_bounds__(WGM* WGN * 64, OCC) void k_gemm3g(ASrc a0, ASrc a1,
     for (int kt = 0; kt < nk; kt += STAGES) {
         step(I0{}, kt);
         if (kt + 1 < nk) step(I1{}, kt + 1);
-        if constexpr (STAGES == 3)
+        if constexpr (STAGES >= 3)
             if (kt + 2 < nk) step(I2{}, kt + 2);
+        if constexpr (STAGES >= 4)
+            if (kt + 3 < nk) step(I3{}, kt + 3);
     }
 
     if constexpr (AX == 1) {
@@ -2574,6 +2619,7 @@ __global__ __launch_bounds__(256, BN == 128 ? 2 : 1) void k_wgrad_tr(const float
     const int kb = chunk * kchunk, ke = min(K, kb + kchunk);
     const int nk = (ke - kb + BK - 1) / BK;
     const float s_a = *sa, s_b = *sb;
+    const int e_a = __builtin_amdgcn_frexp_expf(s_a) - 1, e_b = __builtin_amdgcn_frexp_expf(s_b) - 1;  // 2^e = scale
     // buffer resources over this block's k chunk only: 32-bit offsets stay small whatever the batch
     // (abytes / bbytes: the bytes of one chunk of rows, host-checked)
     const __amdgpu_buffer_rsrc_t ra = rsrc(A + (long long)kb * lda, abytes), rb = rsrc(B + (long long)kb * ldb, bbytes);
@@ -2605,7 +2651,11 @@ __global__ __launch_bounds__(256, BN == 128 ? 2 : 1) void k_wgrad_tr(const float
 #pragma unroll
         for (int j = 0; j < LA; j++) {
             half4 hi, lo;
+#if GM_SPLIT_LDEXP
+            split4e(va[j], e_a, hi, lo);
+#else
             split4(make_float4(va[j].x * s_a, va[j].y * s_a, va[j].z * s_a, va[j].w * s_a), hi, lo);
+#endif
             const int o = (ka0 + 8 * j) * RA + ((8 * qa) ^ (MF ? (((ka0 + 8 * j) >> 3) & 1) << 5 : 0));
             *reinterpret_cast<half4*>(ah + o) = hi;
             *reinterpret_cast<half4*>(al + o) = lo;
@@ -2613,7 +2663,11 @@ __global__ __launch_bounds__(256, BN == 128 ? 2 : 1) void k_wgrad_tr(const float
 #pragma unroll
         for (int j = 0; j < LB; j++) {
             half4 hi, lo;
+#if GM_SPLIT_LDEXP
+            split4e(vb[j], e_b, hi, lo);
+#else
             split4(make_float4(vb[j].x * s_b, vb[j].y * s_b, vb[j].z * s_b, vb[j].w * s_b), hi, lo);
+#endif
             const int o = (kb0 + RB_STEP * j) * RB + ((8 * qb) ^ (MF ? (((kb0 + RB_STEP * j) >> 3) & 1) << 5 : 0));
             *reinterpret_cast<half4*>(bh + o) = hi;
             *reinterpret_cast<half4*>(bl + o) = lo;

@@ -151,6 +151,9 @@ class Packed:
             self.pub.acquire(self.val)
         return self.val
 
+    def __deepcopy__(self, memo):
+        return Packed()  # a copied module (target network) packs its own parameters
+
 
 def _pad_cols(w):
     k = w.shape[1]

@@ -60,6 +60,9 @@ class _WeightCache:
     def __init__(self):
         self.slots = {}  # form -> (key, value, L.Published): shared by streams (StreamedRollout groups)
 
+    def __deepcopy__(self, memo):
+        return _WeightCache()  # a copied module (target network) packs its own parameters
+
     def _get(self, form, key, build):
         k, v, pub = self.slots.get(form, (None, None, None))
         if k != key:

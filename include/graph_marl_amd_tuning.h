@@ -11,7 +11,9 @@ extern "C" {
 /* Tuning knob: tile configuration of gm_gemm_f32 (-1 = per-shape default; 0 = 128x128x32;
  * 1 = 128x256x16; 2 = 256x128x16 (LSTM: 256x128x16); 3 = 128x128x16; 4 = 128x128x16 at 4
  * blocks/CU); of gm_gemm_x3 (-1/0 = 128x128x16; 1 = 128x256x16 (LSTM: 128x128x32);
- * 2 = 128x128x32 (LSTM: 256x128x16)). Process-wide. */
+ * 2 = 128x128x32 (LSTM: 256x128x16)); 8..14 the LDS-DMA tiles of gm_gemm_x3's dense / readout
+ * sources (8 = 256x256, 9 = 128x256 3 stages, 10 = 128x256, 12 = 128x128 2 blocks/CU, 13 = 128x128
+ * of 64x64 waves, 14 = 128x256 of 64x128 waves). Process-wide. */
 /* Weight-gradient kernel of gm_gemm_x3_wgrad (same arithmetic, diagnostics / A-B timing):
  * -1 (default) or 1 = transposed LDS reads (ds_read_b64_tr_b16) with 128 x 128 tiles, 2 = the same
  * with 128 x 256 tiles, 3 = 128 x 128 tiles on v_mfma_f32_16x16x32_f16, 0 = the dword-load

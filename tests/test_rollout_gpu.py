@@ -132,3 +132,29 @@ def test_graph_needs_fixed_epsilon():
     ro.step()
     with pytest.raises(ValueError):
         ro.capture(2)
+
+
+def test_packed_caches_across_streams_and_deepcopy():
+    """The packed-weight caches are shared by the stream groups (each later stream waits for the
+    builder's event, L.Published) and a module copied after packing (the training's target
+    network, copy.deepcopy) gets empty caches and computes the same Q as the original."""
+    import copy
+
+    ro = build(2)
+    ro.reset()
+    ro.run(3)
+    pol = ro.policies[1]
+    dqn = pol._model
+    lin0 = dqn.encoder.linear_layers[0]
+    assert lin0._packed_first.pub is not None and len(lin0._packed_first.pub.seen) >= 2  # both groups read it
+    tar = copy.deepcopy(dqn)
+    assert tar.encoder.linear_layers[0]._packed_first.key is None
+    FU = importlib.import_module("graph-marl_amd.fused")
+    env, wenv = ro.envs[0], ro.wenvs[0]
+    with torch.no_grad():
+        def q(m):
+            bufs = {}
+            return FU.dqn_q(m, env.obs_buf, env.obs_dim, wenv.current_netmon_state, wenv.h_prev, env.nbr,
+                            env.agent_node, lambda i, mm, nn: bufs.setdefault(i, torch.empty(mm, nn, device="cuda")),
+                            hidden=wenv.netmon.hidden_features, obs_gemm=env.obs_gemm).clone()
+        np.testing.assert_array_equal(q(dqn).cpu().numpy(), q(tar).cpu().numpy())
