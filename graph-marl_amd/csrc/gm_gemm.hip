@@ -39,6 +39,14 @@
 #ifndef GM_SPLIT_LDEXP
 #define GM_SPLIT_LDEXP 1  // 0: 4096 x by v_pk_mul_f32 in the split (A/B: rollout -0.9 %, training within noise)
 #endif
+#ifndef GM_SPLIT_ASM
+// lo piece of the split: 0 (default) f32 fma + cvt, compiler-visible; 1 v_fma_mix{lo,hi}_f16 as inline asm;
+// 2 the asm followed by s_nop 1. The compiler's hazard recognizer does not see an asm statement as a VALU
+// write: with form 1 an MFMA could read the lo piece one wait state after the v_fma_mixhi wrote it and
+// take the stale register (32x32x16 k_gemm3g with 3 stages: j = 0 accumulators off by ~1e-4,
+// tools/tile_diag2.py); forms 0 and 2 are exact there, and cost ~1 % on DQN layer 1 (185.4 vs 187.5 us)
+#define GM_SPLIT_ASM 0
+#endif
 #ifndef GM_DIAG
 #define GM_DIAG 0  // 1: no A split, 2: no loads/stores in the k loop, 3: as 2 without barriers
 #endif
@@ -199,16 +207,34 @@ __device__ __forceinline__ void split4(float4 v, half4& hi, half4& lo) {
     lo = __builtin_convertvector((a - __builtin_convertvector(hi, floatx4)) * 4096.0f, half4);
 }
 
-// The same split for 8 floats with 4 vector instructions per pair: hi = cvt_pk (RNE), X =
-// 4096 x (packed multiply, exact), lo = f16(fma(hi, -4096, X)) = f16(4096 (x - hi)) by
-// v_fma_mix{lo,hi}_f16 (the f16 hi read as f32 by the mixed fma; one rounding, RNE), the
-// same bits as split4.
+// lo = f16(fma(hi, -4096, X)) of a pair (hp = the two f16 hi, X = 4096 x): exact in f32, one rounding
+__device__ __forceinline__ unsigned split_lo_pair(unsigned hp, float X0, float X1) {
+    const float m4096 = -4096.0f;
+#if GM_SPLIT_ASM
+    unsigned l;
+    asm("v_fma_mixlo_f16 %0, %1, %2, %3 op_sel_hi:[1,0,0]" : "=&v"(l) : "v"(hp), "s"(m4096), "v"(X0));
+#if GM_SPLIT_ASM == 2
+    asm("v_fma_mixhi_f16 %0, %1, %2, %3 op_sel:[1,0,0] op_sel_hi:[1,0,0]\n\ts_nop 1" : "+v"(l) : "v"(hp), "s"(m4096), "v"(X1));
+#else
+    asm("v_fma_mixhi_f16 %0, %1, %2, %3 op_sel:[1,0,0] op_sel_hi:[1,0,0]" : "+v"(l) : "v"(hp), "s"(m4096), "v"(X1));
+#endif
+    return l;
+#else
+    typedef _Float16 half2_t __attribute__((ext_vector_type(2)));
+    const half2_t h = __builtin_bit_cast(half2_t, hp);
+    const half2_t l = {(_Float16)__builtin_fmaf((float)h[0], m4096, X0), (_Float16)__builtin_fmaf((float)h[1], m4096, X1)};
+    return __builtin_bit_cast(unsigned, l);
+#endif
+}
+
+// The same split for 8 floats: hi = cvt_pk (RNE), X = 4096 x (exact), lo = f16(fma(hi, -4096, X)) =
+// f16(4096 (x - hi)) (the fma is exact in f32, so one rounding, RNE: the same bits as split4;
+// split_lo_pair).
 // GM_SPLIT_LDEXP: the split of x * 2^e (e = 0, or a device power-of-two operand scale) with 4096 x by
 // v_ldexp_f32 instead of v_pk_mul_f32 (packed f32 VALU beside MFMAs costs extra issue cycles)
 __device__ __forceinline__ void split8(floatx4 x0, floatx4 x1, half8& hi, half8& lo, int e = 0) {
     typedef float floatx2 __attribute__((ext_vector_type(2)));
     typedef _Float16 half2_t __attribute__((ext_vector_type(2)));
-    const float m4096 = -4096.0f;
     unsigned hp[4], lp[4];
 #pragma unroll
     for (int q = 0; q < 4; q++) {
@@ -221,12 +247,7 @@ __device__ __forceinline__ void split8(floatx4 x0, floatx4 x1, half8& hi, half8&
         hp[q] = __builtin_bit_cast(unsigned, __builtin_convertvector(x, half2_t));
         const floatx2 X = x * 4096.0f;
 #endif
-        unsigned l;
-        asm("v_fma_mixlo_f16 %0, %1, %2, %3 op_sel_hi:[1,0,0]" : "=&v"(l) : "v"(hp[q]), "s"(m4096), "v"(X[0]));
-        asm("v_fma_mixhi_f16 %0, %1, %2, %3 op_sel:[1,0,0] op_sel_hi:[1,0,0]"
-            : "+v"(l)
-            : "v"(hp[q]), "s"(m4096), "v"(X[1]));
-        lp[q] = l;
+        lp[q] = split_lo_pair(hp[q], X[0], X[1]);
     }
     typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
     hi = __builtin_bit_cast(half8, u32x4_t{hp[0], hp[1], hp[2], hp[3]});
@@ -239,7 +260,6 @@ __device__ __forceinline__ void split8(floatx4 x0, floatx4 x1, half8& hi, half8&
 __device__ __forceinline__ void split4e(float4 v, int e, half4& hi, half4& lo) {
     typedef float floatx2 __attribute__((ext_vector_type(2)));
     typedef _Float16 half2_t __attribute__((ext_vector_type(2)));
-    const float m4096 = -4096.0f;
     const float x[4] = {v.x, v.y, v.z, v.w};
     unsigned hp[2], lp[2];
 #pragma unroll
@@ -247,10 +267,7 @@ __device__ __forceinline__ void split4e(float4 v, int e, half4& hi, half4& lo) {
         const floatx2 xs = {__builtin_ldexpf(x[2 * q], e), __builtin_ldexpf(x[2 * q + 1], e)};
         hp[q] = __builtin_bit_cast(unsigned, __builtin_convertvector(xs, half2_t));
         const float X0 = __builtin_ldexpf(x[2 * q], e + 12), X1 = __builtin_ldexpf(x[2 * q + 1], e + 12);
-        unsigned l;
-        asm("v_fma_mixlo_f16 %0, %1, %2, %3 op_sel_hi:[1,0,0]" : "=&v"(l) : "v"(hp[q]), "s"(m4096), "v"(X0));
-        asm("v_fma_mixhi_f16 %0, %1, %2, %3 op_sel:[1,0,0] op_sel_hi:[1,0,0]" : "+v"(l) : "v"(hp[q]), "s"(m4096), "v"(X1));
-        lp[q] = l;
+        lp[q] = split_lo_pair(hp[q], X0, X1);
     }
     typedef unsigned u32x2_t __attribute__((ext_vector_type(2)));
     hi = __builtin_bit_cast(half4, u32x2_t{hp[0], hp[1]});
