@@ -37,6 +37,7 @@ if ROOT not in sys.path:
 
 gm = importlib.import_module("graph-marl_amd")
 M = importlib.import_module("graph-marl_amd.model")
+SQ = importlib.import_module("graph-marl_amd.sl_seq")
 L = gm._lib
 
 NUM_CLASSES = 4
@@ -112,6 +113,15 @@ class NetMonSL(torch.nn.Module):
         self.class_logits = class_logits.detach()
         return class_logits, pred, pred_all
 
+    def forward_seq(self, node_obs, nbr, steps):
+        """`steps` unrolled NetMon steps from a zero state (src/sl.py:363-368) as one sequence-batched
+        autograd node (sl_seq.readout_seq), then the all-destinations head once over every step's
+        rows: pred_all [steps, B, N, nb_nodes]. The class / distance-to-0 heads are not evaluated
+        (they do not enter the training loss of the reference's default task, src/sl.py:546-548)."""
+        B, N = node_obs.shape[:2]
+        R = SQ.readout_seq(self.netmon, node_obs, nbr, steps)
+        return self.linear_reg_all(R).view(steps, B, N, -1)
+
     def get_class_probabilities(self):
         return torch.softmax(self.class_logits, dim=-1)
 
@@ -181,11 +191,45 @@ def _loss_terms(args, out, tgt_all, tgt, labels, reduction="mean"):
     return loss, terms
 
 
+class _StepMSE(torch.autograd.Function):
+    """Per-step mse_loss of pred [L, ...] against one target [...] (src/sl.py:396-400 at every unroll
+    step): [L] losses. The squares are summed in two stages (a single torch reduction of a few
+    outputs over hundreds of millions of elements ran at ~0.15 TB/s); backward = one elementwise pass
+    over the saved difference."""
+
+    @staticmethod
+    def forward(ctx, pred, tgt):
+        d = pred - tgt
+        steps, n = d.shape[0], d[0].numel()
+        c = next(c for c in (4096, 1024, 256, 64, 16, 4, 1) if n % c == 0)
+        per = d.reshape(steps, c, n // c).pow(2).sum(2).sum(1) / n
+        ctx.save_for_backward(d)
+        ctx.n = n
+        return per
+
+    @staticmethod
+    def backward(ctx, g):
+        (d,) = ctx.saved_tensors
+        return d * (g.view((-1,) + (1,) * (d.dim() - 1)) * (2.0 / ctx.n)), None
+
+
 def train_step(args, model, optim, data, batch_idx):
     """One iteration of src/sl.py:360-424."""
     model.netmon.state = None
     obs, nbr = data.node_obs[batch_idx], data.nbr[batch_idx]
     tgt_all, tgt, labels = data.targets_all[batch_idx], data.targets[batch_idx], data.labels[batch_idx]
+    steps = max(args.sequence_length, 1)
+    if (WITH_REGRESSION_ALL and not WITH_CLASSIFICATION and not WITH_REGRESSION and SQ.seq_ok(model.netmon)
+            and not getattr(args, "sl_autograd", False)):
+        # sequence-batched NetMon (sl_seq.py): the mean of the per-step MSEs over all steps' rows at once
+        k = args.num_targets
+        pred_all = model.forward_seq(obs, nbr, steps)
+        per = _StepMSE.apply(pred_all[..., :k], tgt_all[..., :k])
+        total = per.mean()
+        optim.zero_grad()
+        total.backward()
+        optim.step()
+        return total.detach(), {"reg_all": per[-1].detach()}
     seq = []
     terms = {}
     # the reference re-encodes the same observations at every unroll step (src/sl.py:360-424); the

@@ -1,0 +1,93 @@
+"""Sequence-batched NetMon of the SL driver (graph-marl_amd/sl_seq.py, reference src/sl.py:360-424):
+predictions, loss and every parameter gradient against the reference's own iteration (tests/golden
+sl.npz, sl_n100.npz: seq_len 2) and against the per-step autograd path on longer unrolls."""
+import argparse
+import importlib
+import os
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+HERE = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+def _mods():
+    return importlib.import_module("graph-marl_amd.sl"), importlib.import_module("graph-marl_amd.model")
+
+
+def _args(n, H, enc, K=1, agg="sum"):
+    return argparse.Namespace(netmon_dim=H, netmon_encoder_dim=enc, netmon_iterations=K, netmon_rnn_type="lstm",
+                              netmon_rnn_carryover=1, netmon_agg_type=agg, netmon_last_neighbors=1,
+                              netmon_global=False, num_targets=n)
+
+
+@pytest.mark.parametrize("name", ["sl.npz", "sl_n100.npz"])
+def test_sl_seq_matches_reference(name):
+    SL, M = _mods()
+    g = np.load(os.path.join(HERE, name))
+    n, H, e0, e1 = (int(v) for v in g["config"]) if "config" in g.files else (20, 32, 64, 48)
+    model = SL.NetMonSL(_args(n, H, f"{e0},{e1}"), 4 * n + 8, 4, n).cuda()
+    names = [str(s) for s in g["param_names"]]
+    model.load_state_dict({s: torch.as_tensor(g["w_" + s]) for s in names})
+    assert SL.SQ.seq_ok(model.netmon)
+    x = torch.as_tensor(g["node_obs"], device="cuda")
+    nbr = M.dense_to_nbr(torch.as_tensor(g["node_adj"], device="cuda"))
+    tgt = torch.as_tensor(g["targets_all"], device="cuda")
+    model.netmon.state = None
+    pred = model.forward_seq(x, nbr, 2)
+    for t in range(2):
+        np.testing.assert_allclose(pred[t].detach().cpu().numpy(), g[f"pred_all_{t}"], atol=1e-5, rtol=0,
+                                   err_msg=f"pred_all step {t}")
+    total = (pred - tgt).pow(2).mean(dim=(1, 2, 3)).mean()
+    total.backward()
+    np.testing.assert_allclose(total.item(), float(g["loss"]), rtol=1e-5)
+    params = dict(model.named_parameters())
+    for s in names:
+        if s.startswith("linear.") or s.startswith("linear_reg."):
+            assert params[s].grad is None or float(params[s].grad.abs().max()) == 0.0  # not in the loss
+            continue
+        gr = params[s].grad
+        np.testing.assert_allclose(gr.cpu().numpy(), g["g_" + s], atol=1e-5, rtol=1e-4, err_msg=s)
+
+
+@pytest.mark.parametrize("K,agg,steps", [(1, "sum", 4), (2, "mean", 3), (1, "sum", 1)])
+def test_sl_seq_matches_autograd_path(K, agg, steps):
+    """The sequence-batched unroll == the per-step autograd path (NetMon.forward_graph per step, the
+    encoder output shared) at a size where every kernel runs its production form (>= 4096 rows)."""
+    SL, M = _mods()
+    n, H, B = 20, 128, 256
+    torch.manual_seed(3)
+    models = []
+    for _ in range(2):
+        torch.manual_seed(3)
+        models.append(SL.NetMonSL(_args(n, H, "512,256", K, agg), 4 * n + 8, 4, n).cuda())
+    data = SL.build_dataset(n, 20, B, 7)
+    x, nbr, tgt = data.node_obs, data.nbr, data.targets_all
+    a, b = models
+    a.netmon.state = None
+    enc = a.netmon.encode_nodes(x, nbr)
+    seq = []
+    preds = []
+    for _ in range(steps):
+        _, _, pa = a(x, nbr, enc)
+        preds.append(pa.detach())
+        seq.append(torch.nn.functional.mse_loss(pa, tgt))
+    la = torch.mean(torch.stack(seq))
+    la.backward()
+    b.netmon.state = None
+    pb = b.forward_seq(x, nbr, steps)
+    lb = (pb - tgt).pow(2).mean(dim=(1, 2, 3)).mean()
+    lb.backward()
+    for t in range(steps):
+        torch.testing.assert_close(pb[t].detach(), preds[t], atol=2e-5, rtol=0)
+    torch.testing.assert_close(lb, la, atol=0, rtol=1e-5)
+    pa_, pb_ = dict(a.named_parameters()), dict(b.named_parameters())
+    for s, p in pa_.items():
+        if s.startswith("linear.") or s.startswith("linear_reg."):
+            continue
+        ga, gb = p.grad, pb_[s].grad
+        scale = float(ga.abs().max()) + 1e-12
+        err = float((ga - gb).abs().max()) / scale
+        assert err < 2e-4, (s, err)
