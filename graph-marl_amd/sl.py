@@ -82,6 +82,8 @@ def build_parser():
     a("--bench", action="store_true",
       help="Throughput mode: no validation / test; print one JSON line with node-steps/s")
     a("--warmup", type=int, default=3, help="Untimed iterations before the timed region (--bench)")
+    a("--sl-autograd", dest="sl_autograd", action="store_true",
+      help="Per-step autograd NetMon instead of the sequence-batched unroll (sl_seq.py; A/B and diagnostics)")
     return p
 
 
