@@ -284,8 +284,8 @@ __device__ __forceinline__ float renc_act(float v, int act) {
 
 // AC: the activation at compile time (0 none, 1 leaky_relu) or -1 = GM_ACT_* `act` at run time (a per
 // element branch tree: kept out of the default kernels, it cost 65 -> 76 us per 81 920 rows)
-template <int CPL, int AC>  // output columns per lane (BN = 64 * CPL)
-__global__ __launch_bounds__(256) void k_routing_enc(const float* __restrict__ x, long long ldx,
+template <int CPL, int AC, int TPB = 256>  // output columns per lane (BN = 64 * CPL), threads per block
+__global__ __launch_bounds__(TPB) void k_routing_enc(const float* __restrict__ x, long long ldx,
                                                      const int32_t* __restrict__ nbr, int G, int N,
                                                      const float* __restrict__ wt, const float* __restrict__ b,
                                                      int n, int act, float* __restrict__ y, long long ldy,
@@ -1304,16 +1304,30 @@ extern "C" int gm_routing_node_encoder_bits(const float* x, int64_t ldx, const i
     // rows per block: the block's W^T slice (K x BN) is staged once for them, so larger graphs take more
     // rows. Measured per launch (4096 envs): N = 20 256 / 512 / 1024 rows 60.9 / 61.3 / 75.8 us;
     // N = 30 117 / 103 / 92 us; N = 40 196 / 178 / 160 us. GM_RENC_ROWS overrides (A-B)
+    static const int tpb_env = [] {
+        const char* e = getenv("GM_RENC_TPB");
+        return e ? atoi(e) : 0;
+    }();
     static const int rows_env = [] {
         const char* e = getenv("GM_RENC_ROWS");
         const int v = e ? atoi(e) : 0;
         return (v >= 256 && v % 256 == 0) ? v : 0;
     }();
-    const int rows = rows_env ? rows_env : (K <= 88 ? 256 : (K <= 128 ? 512 : 1024));
+    // 8 waves per block share the staged slice (round 3, interleaved rollout A/B, per-launch times): N = 20
+    // 512 rows 54.9 vs 63.8 us (256 rows, 4 waves), N = 30 1024 rows 88.9 vs 111.7 us, N = 40 157.5 vs
+    // 170.5 us, N = 50 222 vs 240 us (rollout +0.1 / +1.7 / +0.7 % at N = 20 / 40 / 50); GM_RENC_TPB=256
+    // restores 4 waves with half the rows
+    const int tpb = tpb_env == 256 ? 256 : 512;
+    const int rows = rows_env ? rows_env : (K <= 88 ? 256 : (K <= 128 ? 512 : 1024)) * (tpb == 512 && K <= 128 ? 2 : 1);
     dim3 grid((unsigned)((M + rows - 1) / rows), (unsigned)(n / (64 * cpl)));
-#define GM_RENC(C, A)                                                                                              \
-    hipLaunchKernelGGL((k_routing_enc<C, A>), grid, dim3(256), lds, (hipStream_t)stream, x, (long long)ldx, nbr, G, N, \
-                       wt, b, n, act, y, (long long)ldy, rows, reinterpret_cast<unsigned*>(sbits), (long long)ldsb)
+#define GM_RENC(C, A)                                                                                               \
+    if (tpb == 512)                                                                                                 \
+        hipLaunchKernelGGL((k_routing_enc<C, A, 512>), grid, dim3(512), lds, (hipStream_t)stream, x, (long long)ldx, \
+                           nbr, G, N, wt, b, n, act, y, (long long)ldy, rows, reinterpret_cast<unsigned*>(sbits),    \
+                           (long long)ldsb);                                                                        \
+    else                                                                                                            \
+        hipLaunchKernelGGL((k_routing_enc<C, A>), grid, dim3(256), lds, (hipStream_t)stream, x, (long long)ldx, nbr, G, \
+                           N, wt, b, n, act, y, (long long)ldy, rows, reinterpret_cast<unsigned*>(sbits), (long long)ldsb)
     if (cpl == 2) {
         if (act == GM_ACT_LEAKY_RELU) GM_RENC(2, 1);
         else if (act == GM_ACT_NONE) GM_RENC(2, 0);
