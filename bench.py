@@ -10,12 +10,16 @@ rollout (src/main.py:667-748) with NetMonWrapper (src/env/wrapper.py).
 
 Multi-GPU: one process per GPU (torchrun), env shards with disjoint seeds, no
 collective on the rollout path (weak scaling); barrier + max-over-ranks timing.
-Rank 0 prints ONE JSON line.
+Rank 0 prints ONE JSON line. `python bench.py --gpus N` (N > 1) outside a launcher starts
+`torch.distributed.run --nproc-per-node N` on this script as a child process (before any GPU
+call) and exits with its return code; under a launcher WORLD_SIZE must equal --gpus.
 """
 import argparse
 import importlib
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -72,14 +76,19 @@ def parse():
     p.add_argument("--no-extras", action="store_true",
                    help="skip the other BASELINE configurations (K=3, configs 2/3, config 5 SL) timed after the headline")
     p.add_argument("--extra-steps", type=int, default=100, help="timed vector steps of each extra rollout configuration")
+    p.add_argument("--no-pmc", action="store_true",
+                   help="skip the same-run rocprofv3 PMC passes (HBM bytes of DQN layer 1 and k_env_step)")
+    p.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
     p.add_argument("--cpu-envs", type=int, default=1024)
     p.add_argument("--cpu-steps", type=int, default=50, help="one full episode (includes its reset)")
     return p.parse_args()
 
 
-def pmc_traffic(tag):
+def pmc_traffic(tag, build_src=None):
     """HBM bytes per launch of a kernel (FETCH_SIZE x2 + WRITE_SIZE) from the latest committed
-    rocprofv3 PMC passes (profiles/*/pmc_traffic.json); None when not profiled."""
+    rocprofv3 PMC passes (profiles/*/pmc_traffic.json), with a provenance note: whether the profile's
+    recorded source hash equals this library's build.src. (None, None) when not profiled. Used only
+    when the same-run passes (measure_pmc) are unavailable."""
     import glob
 
     found = []
@@ -92,11 +101,108 @@ def pmc_traffic(tag):
             continue
         if k:  # newest = highest round directory, then the profile's own "seq" within the round
             rnd = os.path.basename(os.path.dirname(os.path.dirname(path)))
-            found.append(((rnd, d.get("seq", 0)), k["fetch_bytes"] + k["write_bytes"], os.path.relpath(path, ROOT)))
+            found.append(((rnd, d.get("seq", 0)), k["fetch_bytes"] + k["write_bytes"], os.path.relpath(path, ROOT),
+                          d.get("src")))
     if not found:
         return None, None
-    _, tb, src = max(found)
-    return tb, src
+    _, tb, src, psrc = max(found)
+    same = ("source hash not recorded" if psrc is None else
+            "same sources as this build" if psrc == build_src else f"OTHER sources ({psrc}) than this build")
+    return tb, f"committed profile {src}, {same}"
+
+
+PMC_X, PMC_Y = 6, 6  # DQN forwards, then env steps, in the counted window of the --pmc-child process
+
+
+def pmc_child(args):
+    """The dispatch window the PMC passes count (bench.py under rocprofv3, started by measure_pmc): the
+    headline's rollout as one group, a few warm steps, then PMC_X DQN forwards (layer 1 = the dominant
+    kernel, then layer 2 + Q head) and PMC_Y fused ε-greedy + env steps, nothing else in between."""
+    torch.cuda.set_device(0)
+    gm = importlib.import_module("graph-marl_amd")
+    M = importlib.import_module("graph-marl_amd.model")
+    RO = importlib.import_module("graph-marl_amd.rollout")
+    FU = importlib.import_module("graph-marl_amd.fused")
+    N, A, B = args.n_router, args.n_data, args.n_env
+    net = gm.Network(N, random_topology=bool(args.random_topology), excluded_seeds=gm.EVAL_SEEDS, device=0)
+    torch.manual_seed(0)
+    netmon = M.NetMon(4 * N + 8, 128, [512, 256], args.netmon_iterations).cuda()
+    dqn = M.DQN(6 * N + 10 + netmon.get_out_features(), [512, 256], 4).cuda()
+    ro = RO.StreamedRollout(net, A, B, netmon, dqn, groups=1, seed=0, epsilon=args.epsilon,
+                            episode_steps=args.episode_steps, device=0)
+    with torch.no_grad():
+        ro.reset()
+        ro.run(3)
+        env, wenv, pol = ro.envs[0], ro.wenvs[0], ro.policies[0]
+        torch.cuda.synchronize()
+        for _ in range(PMC_X):
+            q = FU.dqn_q(dqn, env.obs_buf, env.obs_dim, wenv.current_netmon_state, wenv.h_prev, env.nbr,
+                         env.agent_node, pol._buf, hidden=netmon.hidden_features, obs_gemm=env.obs_gemm)
+        torch.cuda.synchronize()
+        qv = q.view(B, A, -1).contiguous()
+        for _ in range(PMC_Y):
+            env.policy_step_(qv, args.epsilon, pol.actions)
+        torch.cuda.synchronize()
+
+
+def _pmc_window(path, counter):
+    """Per-launch counter values of (DQN layer 1, k_env_step) from the child's CSV: the last
+    2 PMC_X + PMC_Y dispatches of this library's kernels must be PMC_X (layer 1, layer 2 + head) pairs
+    (layer 1 = the larger grid) then PMC_Y env steps; None if the window does not look like that."""
+    import csv
+
+    with open(path) as f:
+        rows = [r for r in csv.DictReader(f) if r.get("Counter_Name") == counter]
+    rows.sort(key=lambda r: int(r["Dispatch_Id"]))
+    ours = [r for r in rows if r["Kernel_Name"].lstrip("_ ").startswith(("k_", "ZN12_GLOBAL__N_1"))]
+    win = ours[-(2 * PMC_X + PMC_Y):]
+    if len(win) != 2 * PMC_X + PMC_Y or not all("k_env_step" in r["Kernel_Name"] for r in win[2 * PMC_X:]):
+        return None
+    grid = lambda r: int(r.get("Grid_Size") or r.get("Grid_Size_X"))  # noqa: E731
+    l1 = [a for a, b in zip(win[0:2 * PMC_X:2], win[1:2 * PMC_X:2]) if grid(a) > grid(b)]
+    if len(l1) != PMC_X:
+        return None
+    med = lambda v: sorted(v)[len(v) // 2]  # noqa: E731
+    return (med([float(r["Counter_Value"]) for r in l1]),
+            med([float(r["Counter_Value"]) for r in win[2 * PMC_X:]]))
+
+
+def measure_pmc(args):
+    """Same-run HBM traffic (MI355X_MICROARCH.md §HBM): two rocprofv3 passes over a child bench.py
+    (--pmc-child), FETCH_SIZE and WRITE_SIZE in separate runs (they do not fit one pass), each under
+    a hard time limit; KiB per launch, FETCH_SIZE doubled (gfx950 counts half of a 16-B/lane stream).
+    Returns {"dqn_l1": bytes, "env_step": bytes, ...} or None (no rocprofv3, or a pass failed)."""
+    import shutil
+    import tempfile
+
+    prof = shutil.which("rocprofv3")
+    if prof is None:
+        return None
+    out = {}
+    with tempfile.TemporaryDirectory(dir=os.path.join(ROOT, "gpurun_out") if os.path.isdir(
+            os.path.join(ROOT, "gpurun_out")) else None) as d:
+        for counter in ("FETCH_SIZE", "WRITE_SIZE"):
+            cmd = ["timeout", "-s", "KILL", "150", prof, "--pmc", counter, "-T", "--output-format", "csv", "-d", d,
+                   "-o", counter.lower(), "--", sys.executable, os.path.abspath(__file__), "--pmc-child",
+                   "--n-env", str(args.n_env), "--n-router", str(args.n_router), "--n-data", str(args.n_data),
+                   "--netmon-iterations", str(args.netmon_iterations), "--random-topology", str(args.random_topology),
+                   "--episode-steps", str(args.episode_steps), "--epsilon", str(args.epsilon)]
+            try:
+                r = subprocess.run(cmd, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, timeout=170)
+            except subprocess.TimeoutExpired:
+                return {"error": f"{counter} pass timed out"}
+            if r.returncode != 0:
+                return {"error": f"{counter} pass rc {r.returncode}: {r.stderr.decode(errors='replace')[-200:]}"}
+            csvs = [os.path.join(dp, f) for dp, _, fs in os.walk(d) for f in fs
+                    if f.startswith(counter.lower()) and f.endswith("counter_collection.csv")]
+            got = _pmc_window(csvs[0], counter) if csvs else None
+            if got is None:
+                return {"error": f"{counter}: dispatch window not found in {csvs}"}
+            f = 2.0 if counter == "FETCH_SIZE" else 1.0
+            out[counter] = [f * v * 1024 for v in got]
+    return {"dqn_l1": out["FETCH_SIZE"][0] + out["WRITE_SIZE"][0], "env_step": out["FETCH_SIZE"][1] +
+            out["WRITE_SIZE"][1], "fetch_bytes": out["FETCH_SIZE"], "write_bytes": out["WRITE_SIZE"],
+            "note": "rocprofv3 PMC in this bench run (child process, median of 6 launches; FETCH_SIZE x2, KiB x1024)"}
 
 
 def cpu_model():
@@ -309,9 +415,36 @@ def measure_train(args, gm, M, W, P, net, netmon, dqn, dev, world, rank):
                        "per": "vector step of n_env envs (replay ratio 25.6 = reference B=32, L=8 every 10 steps)"}}
 
 
+def launch_ranks(args, argv=None):
+    """--gpus N > 1 without a launcher: run N ranks of this script under torch.distributed.run as a
+    CHILD process (nothing here has touched the GPU; no exec from this process) and return its exit
+    code. Returns None when this process is already a rank (WORLD_SIZE set) or N == 1."""
+    if args.gpus <= 1 or "WORLD_SIZE" in os.environ:
+        return None
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)]
+    cmd += list(sys.argv[1:] if argv is None else argv)
+    return subprocess.call(cmd, env=dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0"))
+
+
+def check_world(args, world):
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world} ranks were launched")
+
+
 def main():
     args = parse()
+    if args.pmc_child:
+        return pmc_child(args)
+    rc = launch_ranks(args)
+    if rc is not None:
+        sys.exit(rc)
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    check_world(args, world)
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     # GM_BENCH_SHARE_GPU=1 rehearses the N-rank path on one GPU (all ranks on cuda:0, gloo)
@@ -435,7 +568,7 @@ def main():
         if bound in ("mfma", "mfma16"):
             ach = units / sec / 1e12
             peak = F16_MFMA_PEAK_TFS if bound == "mfma16" else F32_MFMA_PEAK_TFS
-            tb, src = pmc_traffic(dom)
+            tb, src = pmc_traffic(dom, L.build_info().get("src"))
             roof = {"kernel": dom, "bound": "mfma", "achieved": round(ach, 2), "peak": peak,
                     "unit": "TFLOP/s" + (" (f16 MFMA, 3 per fp32 multiply-add)" if bound == "mfma16" else " (f32 MFMA)"),
                     "frac": round(ach / peak, 4), "traffic": tb,
@@ -457,7 +590,7 @@ def main():
                 continue
             bound, units = kernel_cost(tag, B, N, A, E, x3)
             ach = units / (kv["avg_us"] * 1e-6) / 1e9
-            tb, src = pmc_traffic(tag)
+            tb, src = pmc_traffic(tag, L.build_info().get("src"))
             roof_hbm[tag] = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                              "frac": round(ach / HBM_PEAK_GBS, 4), "algorithmic_bytes": units, "traffic": tb,
                              "traffic_note": None if tb is None else f"HBM bytes per launch (rocprofv3 PMC, {src})",
@@ -483,6 +616,21 @@ def main():
 
             where = " <- ".join(f"{fs.name}:{fs.lineno}" for fs in traceback.extract_tb(ex.__traceback__)[::-1][:4])
             train = {"value": None, "error": repr(ex)[:300], "where": where}
+
+    pmc = None
+    if rank == 0 and world == 1 and not args.no_pmc and netmon is not None and args.netmon_rnn_type == "lstm":
+        try:
+            pmc = measure_pmc(args)
+        except Exception as ex:  # the traffic probe must never break the GPU line
+            pmc = {"error": repr(ex)[:200]}
+    if roof and pmc and "dqn_l1" in pmc and roof.get("kernel", "").startswith("linear:dqn.encoder.linear_layers.0:"):
+        roof["traffic"] = round(pmc["dqn_l1"])
+        roof["traffic_note"] = "HBM bytes per launch, " + pmc["note"]
+    if pmc and "env_step" in pmc:
+        for tag, kv in roof_hbm.items():
+            if tag.startswith("env_step"):
+                kv["traffic"] = round(pmc["env_step"])
+                kv["traffic_note"] = "HBM bytes per launch, " + pmc["note"]
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -521,6 +669,7 @@ def main():
             "host_enqueue_ms_per_step": round(host_ms, 4),
             "roofline": roof, "roofline_hbm": roof_hbm or None, "cpu_baseline": cpu, "f32_exact_gemms": f32cmp, "rollout_train": train,
             "other_configs": extras,
+            "pmc": pmc,
             "kernels": kernels,
             "build": L.build_info(),
         }

@@ -40,12 +40,15 @@
 #define GM_SPLIT_LDEXP 1  // 0: 4096 x by v_pk_mul_f32 in the split (A/B: rollout -0.9 %, training within noise)
 #endif
 #ifndef GM_SPLIT_ASM
-// lo piece of the split: 0 (default) f32 fma + cvt, compiler-visible; 1 v_fma_mix{lo,hi}_f16 as inline asm;
-// 2 the asm followed by s_nop 1. The compiler's hazard recognizer does not see an asm statement as a VALU
-// write: with form 1 an MFMA could read the lo piece one wait state after the v_fma_mixhi wrote it and
-// take the stale register (32x32x16 k_gemm3g with 3 stages: j = 0 accumulators off by ~1e-4,
-// tools/tile_diag2.py); forms 0 and 2 are exact there, and cost ~1 % on DQN layer 1 (185.4 vs 187.5 us)
+// lo piece of the split: 0 (default) f32 fma + cvt, compiler-visible; 2 v_fma_mix{lo,hi}_f16 as inline asm
+// followed by s_nop 1. The plain asm form (formerly 1) is removed: the compiler's hazard recognizer does
+// not see an asm statement as a VALU write, so an MFMA could read the lo piece one wait state after the
+// v_fma_mixhi wrote it and take the stale register (32x32x16 k_gemm3g with 3 stages: j = 0 accumulators
+// off by ~1e-4, tools/tile_diag2.py); forms 0 and 2 are exact there, and cost ~1 % on DQN layer 1
 #define GM_SPLIT_ASM 0
+#endif
+#if GM_SPLIT_ASM != 0 && GM_SPLIT_ASM != 2
+#error "GM_SPLIT_ASM must be 0 (compiler-visible split) or 2 (asm + s_nop 1): the bare asm form races the MFMA read"
 #endif
 #ifndef GM_DIAG
 #define GM_DIAG 0  // 1: no A split, 2: no loads/stores in the k loop, 3: as 2 without barriers
@@ -210,14 +213,10 @@ __device__ __forceinline__ void split4(float4 v, half4& hi, half4& lo) {
 // lo = f16(fma(hi, -4096, X)) of a pair (hp = the two f16 hi, X = 4096 x): exact in f32, one rounding
 __device__ __forceinline__ unsigned split_lo_pair(unsigned hp, float X0, float X1) {
     const float m4096 = -4096.0f;
-#if GM_SPLIT_ASM
+#if GM_SPLIT_ASM == 2
     unsigned l;
     asm("v_fma_mixlo_f16 %0, %1, %2, %3 op_sel_hi:[1,0,0]" : "=&v"(l) : "v"(hp), "s"(m4096), "v"(X0));
-#if GM_SPLIT_ASM == 2
     asm("v_fma_mixhi_f16 %0, %1, %2, %3 op_sel:[1,0,0] op_sel_hi:[1,0,0]\n\ts_nop 1" : "+v"(l) : "v"(hp), "s"(m4096), "v"(X1));
-#else
-    asm("v_fma_mixhi_f16 %0, %1, %2, %3 op_sel:[1,0,0] op_sel_hi:[1,0,0]" : "+v"(l) : "v"(hp), "s"(m4096), "v"(X1));
-#endif
     return l;
 #else
     typedef _Float16 half2_t __attribute__((ext_vector_type(2)));

@@ -596,6 +596,7 @@ class _LSTMCell2Fn(torch.autograd.Function):
                 FU.dense(h.data_ptr(), h.stride(0), H), wp.data_ptr(), ldw, bp.data_ptr(), M, 4 * H, FU.GM_EPI_LSTM,
                 h1.data_ptr(), H, c1.data_ptr(), H, c.data_ptr(), c.stride(0), act.data_ptr(), tag=tag, x3=x3)
         ctx.xs = None if xs is None else _finish_scale(xs)
+        ctx.cell = cell
         ctx.save_for_backward(x, h, w_ih, w_hh, act, c, c1)
         return h1, c1
 
@@ -619,7 +620,10 @@ class _LSTMCell2Fn(torch.autograd.Function):
         n = ctx.needs_input_grad
         dx = dh = None
         if n[0] or n[1]:
-            x3 = _WeightCache().x3t(torch.cat([w_ih, w_hh], 1))
+            from . import train_seq as TS
+
+            # [W_ih | W_hh]^T packed once per parameter version on the cell (train_seq's cache)
+            x3 = TS._lstm_x3t(ctx.cell)
             dx = torch.empty(M, I, device=c.device)
             dh = torch.empty(M, H, device=c.device)
             a = FU.dense(dg.data_ptr(), 4 * H, 4 * H, scale=sc.data_ptr())

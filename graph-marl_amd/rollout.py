@@ -100,7 +100,9 @@ class StreamedRollout:
         self.ep = 0
 
     def _enqueue_step(self):
+        cur = torch.cuda.current_stream()
         for g in range(self.groups):
+            self.streams[g].wait_stream(cur)  # after whatever the caller enqueued (free when cur is idle)
             with self._on(g):
                 self.policies[g].act_step(self.wenvs[g])
 
@@ -166,7 +168,9 @@ class StreamedRollout:
             if self.ep % self._gsteps:
                 raise RuntimeError("graph replay must start at a multiple of the captured length")
             if self._graphs is not None:
+                cur = torch.cuda.current_stream()
                 for g, gr in enumerate(self._graphs):
+                    self.streams[g].wait_stream(cur)  # ordered after the caller's stream (weight copies, edits)
                     with self._on(g):
                         gr.replay()
                 self.ep += self._gsteps

@@ -221,7 +221,8 @@ def train_step(args, model, optim, data, batch_idx):
     obs, nbr = data.node_obs[batch_idx], data.nbr[batch_idx]
     tgt_all, tgt, labels = data.targets_all[batch_idx], data.targets[batch_idx], data.labels[batch_idx]
     steps = max(args.sequence_length, 1)
-    if (WITH_REGRESSION_ALL and not WITH_CLASSIFICATION and not WITH_REGRESSION and SQ.seq_ok(model.netmon)
+    if (WITH_REGRESSION_ALL and not WITH_CLASSIFICATION and not WITH_REGRESSION
+            and SQ.seq_ok(model.netmon, rows=obs.shape[0] * obs.shape[1], steps=steps)
             and not getattr(args, "sl_autograd", False)):
         # sequence-batched NetMon (sl_seq.py): the mean of the per-step MSEs over all steps' rows at once
         k = args.num_targets

@@ -30,16 +30,35 @@ from . import fused as FU
 from . import train_seq as TS
 
 
-def seq_ok(netmon):
+def seq_bytes(netmon, rows, steps):
+    """Device bytes the unroll keeps for its backward at M = rows node rows and L = steps: per cell and
+    step the [h | c] output (2H), the gate activations (4H) and their gradient (4H), plus the K
+    aggregates (H), all fp32."""
+    H, K = netmon.hidden_features, netmon.iterations
+    return 4 * steps * rows * ((K + 1) * 10 * H + K * H)
+
+
+def _device_room(dev):
+    free, _ = torch.cuda.mem_get_info(dev)
+    return free + torch.cuda.memory_reserved(dev) - torch.cuda.memory_allocated(dev)
+
+
+def seq_ok(netmon, rows=None, steps=None):
     """The configurations this path covers: LSTM cells with carry-over, sum / mean aggregation,
-    neighbour readout without the global mean, leaky encoder layers with biases, split-f16 GEMMs."""
+    neighbour readout without the global mean, leaky encoder layers with biases, split-f16 GEMMs;
+    with rows / steps given, also that the unroll's saved tensors (seq_bytes) fit the device with a
+    margin (otherwise the caller runs the per-step autograd path instead of failing with OOM)."""
     if netmon is None or L.GEMM_MODE != "x3":
         return False
     enc = list(netmon.encode.linear_layers)
     H = netmon.hidden_features
-    return (netmon.rnn_type == "lstm" and netmon.rnn_carryover and netmon.output_neighbor_hidden
-            and not netmon.output_global_hidden and netmon.iterations >= 1 and H % 32 == 0 and H <= 1024
-            and len(enc) >= 1 and all(l.act == 1 and l.bias is not None for l in enc))
+    ok = (netmon.rnn_type == "lstm" and netmon.rnn_carryover and netmon.output_neighbor_hidden
+          and not netmon.output_global_hidden and netmon.iterations >= 1 and H % 32 == 0 and H <= 1024
+          and len(enc) >= 1 and all(l.act == 1 and l.bias is not None for l in enc))
+    if ok and rows is not None and steps is not None:
+        dev = next(netmon.parameters()).device
+        ok = 1.25 * seq_bytes(netmon, rows, steps) < _device_room(dev)
+    return ok
 
 
 class _Plan:

@@ -12,6 +12,8 @@ AdamW, soft target update. With world_size > 1 the gradients of all parameters
 are averaged in ONE flattened RCCL all-reduce before clipping, so every rank
 clips and steps on the global gradient and the replicas stay identical.
 """
+import os
+
 import torch
 import torch.distributed as dist
 import torch.nn.functional as F
@@ -34,6 +36,33 @@ def allreduce_gradients(params, group=None):
         n = g.numel()
         g.copy_(flat[off:off + n].view_as(g))
         off += n
+
+
+def init_distributed(use_gpu=True):
+    """One process per GPU under a launcher (torch.distributed.run sets RANK / WORLD_SIZE /
+    LOCAL_RANK; the reference runs independent jobs per GPU, scripts/start_routing_netmon_runs.sh:50).
+    Returns (rank, world, local_rank); world 1 initialises nothing. Backend: RCCL ("nccl") with rank
+    r on cuda:LOCAL_RANK; gloo when use_gpu is False (CPU tests), when GM_DIST_SHARE_GPU=1, or when
+    the node shows fewer GPUs than local ranks (every rank then shares cuda:0: a one-GPU rehearsal).
+    Counting devices does not initialise the GPU."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", str(rank)))
+    if world <= 1:
+        return 0, 1, 0
+    if dist.is_initialized():
+        return dist.get_rank(), dist.get_world_size(), local
+    local_world = int(os.environ.get("LOCAL_WORLD_SIZE", str(world)))
+    share = os.environ.get("GM_DIST_SHARE_GPU") == "1" or (use_gpu and torch.cuda.device_count() < local_world)
+    if not use_gpu:
+        dist.init_process_group("gloo")
+    elif share:
+        torch.cuda.set_device(0)
+        dist.init_process_group("gloo")
+    else:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    return dist.get_rank(), dist.get_world_size(), local
 
 
 def shard_seeds(rank, world, n_env, base=0):

@@ -33,6 +33,16 @@ def test_library_was_built_from_these_sources(gm):
     assert info["src"] == gm._lib.source_hash(), f"library built from other sources: {info}"
 
 
+def test_library_split_form_is_hazard_free(gm):
+    """The A split of the split-f16 GEMMs is the compiler-visible form (0) or the asm form with its
+    s_nop (2); the bare asm form whose lo register an MFMA could read stale (DESIGN.md §4a Hazard)
+    no longer builds (gm_gemm.hip #error) and the library reports which form it carries."""
+    info = gm._lib.build_info()
+    assert info.get("split_asm") in ("0", "2"), info
+    src = open(os.path.join(ROOT, "graph-marl_amd", "csrc", "gm_gemm.hip")).read()
+    assert "#if GM_SPLIT_ASM != 0 && GM_SPLIT_ASM != 2" in src
+
+
 def test_library_exports_every_declared_symbol(gm):
     path = gm._lib.LIB_PATH
     if not os.path.exists(path):

@@ -73,3 +73,63 @@ def test_env_seed_shards_are_disjoint():
     seeds = [set(T.shard_seeds(r, world, B, base=0)) for r in range(world)]
     assert all(len(s) == B for s in seeds)
     assert len(set().union(*seeds)) == B * world
+
+
+def _init_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE=str(world), RANK=str(rank),
+                      LOCAL_RANK=str(rank))
+    T = importlib.import_module("graph-marl_amd.train")
+    try:
+        r, w, loc = T.init_distributed(use_gpu=False)
+        t = torch.tensor([float(r + 1)])
+        dist.all_reduce(t)
+        q.put((rank, (r, w, loc, float(t), dist.get_backend())))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_init_distributed_from_launcher_env():
+    """train.init_distributed reads the launcher's RANK / WORLD_SIZE / LOCAL_RANK (the entry of
+    main.py and the bench's ranks); world 1 initialises nothing."""
+    T = importlib.import_module("graph-marl_amd.train")
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
+        os.environ.pop(k, None)
+    assert T.init_distributed(use_gpu=False) == (0, 1, 0) and not dist.is_initialized()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_init_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(120)
+        assert p.exitcode == 0
+    res = dict(q.get() for _ in range(2))
+    assert res == {0: (0, 2, 0, 3.0, "gloo"), 1: (1, 2, 1, 3.0, "gloo")}
+
+
+def test_bench_gpus_flag_launches_ranks(monkeypatch):
+    """bench.py --gpus N (N > 1) outside a launcher runs torch.distributed.run with N ranks on itself
+    as a child process; under a launcher WORLD_SIZE must equal --gpus."""
+    import subprocess
+    import sys
+
+    import bench
+
+    monkeypatch.delenv("WORLD_SIZE", raising=False)
+    calls = []
+    monkeypatch.setattr(subprocess, "call", lambda cmd, env=None: calls.append((cmd, env)) or 0)
+    args = type("A", (), {"gpus": 4})()
+    assert bench.launch_ranks(args, ["--gpus", "4", "--steps", "10"]) == 0
+    cmd, env = calls[0]
+    assert cmd[:3] == [sys.executable, "-m", "torch.distributed.run"] and "--nproc-per-node=4" in cmd
+    assert cmd[cmd.index("--master-addr") + 1] == "127.0.0.1" and cmd[-3:] == ["--gpus", "4", "--steps", "10"][-3:]
+    assert env["HSA_ENABLE_IPC_MODE_LEGACY"] == "0"
+    args.gpus = 1
+    assert bench.launch_ranks(args, []) is None
+    monkeypatch.setenv("WORLD_SIZE", "4")
+    args.gpus = 4
+    assert bench.launch_ranks(args, []) is None
+    bench.check_world(args, 4)
+    with pytest.raises(SystemExit):
+        bench.check_world(args, 2)

@@ -139,3 +139,72 @@ def test_two_rank_dqn_update_keeps_replicas_identical(seq_path):
                 p.kill()
     assert res == {0: "ok", 1: "ok"}, res
     assert all(p.exitcode == 0 for p in procs)
+
+
+def _cli_worker(rank, world, port, q, log_dir):
+    """One rank of `torch.distributed.run graph-marl_amd/main.py` (the env a launcher sets), both
+    ranks on cuda:0 over gloo (GM_DIST_SHARE_GPU=1)."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE=str(world), RANK=str(rank),
+                      LOCAL_RANK=str(rank), LOCAL_WORLD_SIZE=str(world), GM_DIST_SHARE_GPU="1")
+    try:
+        main = importlib.import_module("graph-marl_amd.main")
+        T = importlib.import_module("graph-marl_amd.train")
+        TS = importlib.import_module("graph-marl_amd.train_seq")
+        rec = {"seeds": None, "updates": 0}
+        orig_seeds, orig_upd = T.shard_seeds, TS.dqn_update_seq
+
+        def seeds(r, w, n, base=0):
+            rec["seeds"] = orig_seeds(r, w, n, base)
+            return rec["seeds"]
+
+        def upd(netmon, model, *a, **k):
+            out = orig_upd(netmon, model, *a, **k)
+            rec["updates"] += 1
+            rec["flat"] = torch.cat([t.detach().float().reshape(-1).cpu() for m in (model, netmon)
+                                     for t in m.state_dict().values()])
+            rec["loss"] = float(out[0])
+            return out
+
+        T.shard_seeds, TS.dqn_update_seq = seeds, upd
+        m = main.main(["--env-type=routing", "--model=dqn", "--netmon", "--netmon-iterations=1", "--n-env=16",
+                       "--episode-steps=20", "--total-steps=60", "--step-before-train=20", "--mini-batch-size=32",
+                       "--sequence-length=4", "--capacity=20000", "--eval-episodes=16", "--eval-episode-steps=10",
+                       "--disable-progressbar", f"--log-dir={log_dir}"])
+        q.put((rank, {"seeds": rec["seeds"], "updates": rec["updates"], "flat": rec["flat"].numpy(),
+                      "loss": rec["loss"], "metrics": m}))
+    except Exception as ex:
+        q.put((rank, f"error: {ex!r}"))
+        raise
+
+
+def test_two_rank_cli_training_keeps_replicas_identical(tmp_path):
+    """main.py under a 2-rank launch: disjoint env seeds per rank, the same number of updates, every
+    NetMon / DQN parameter bit-identical across ranks after training (rank 0's start broadcast, one
+    gradient all-reduce per update), different local losses, and only rank 0 evaluates and saves."""
+    import numpy as np
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_cli_worker, args=(r, 2, port, q, str(tmp_path))) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = {}
+    try:
+        for _ in range(2):
+            r, msg = q.get(timeout=240)
+            res[r] = msg
+    finally:
+        for p in procs:
+            p.join(30 if len(res) == 2 else 1)
+            if p.is_alive():
+                p.kill()
+    assert all(isinstance(v, dict) for v in res.values()), res
+    a, b = res[0], res[1]
+    assert not set(a["seeds"]) & set(b["seeds"]) and len(a["seeds"]) == 16
+    assert a["updates"] == b["updates"] == 41
+    np.testing.assert_array_equal(a["flat"], b["flat"])
+    assert a["loss"] != b["loss"]
+    assert a["metrics"] is not None and b["metrics"] is None
+    assert (tmp_path / "model_last.pt").exists()
+    assert all(p.exitcode == 0 for p in procs)

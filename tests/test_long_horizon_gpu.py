@@ -13,6 +13,9 @@ N = 20, the same 120 steps. Other --activation-function values (elu, tanh: the G
 the routing encoder and the fused Q head): 512 envs, N = 20, 70 steps. The LN-LSTM bound is the fp32
 envelope described at netmon_check (the 1e-5 contract is out of reach for any fp32 evaluation of that
 cell over carried steps).
+BASELINE config 3 (NetMon K = 1 on the fixed 20-node graph, seed 476) at its own 4096 envs, and
+config 2 (no NetMon: the DQN reads the 130-wide env obs, K = 130, on the fixed graph) at its 1024
+envs, both 120 steps (reference src/main.py:667-748, src/model.py:187-203).
 Eight envs spread over both groups are shadowed every step by
   * the C oracle env (oracle/gm_oracle.c) fed the GPU's Q-values, which must take the same
     ε-greedy actions and give bit-identical rewards, done flags, agent and node observations
@@ -33,11 +36,21 @@ pytestmark = pytest.mark.gpu
 
 A, G, EPS = 20, 2, 0.5
 TOL = 1e-5
-# (N, envs, episode steps, vector steps, NetMon cell, --activation-function)
-CASES = [(20, 4096, 50, 120, "lstm", "leaky_relu"), (10, 512, 30, 70, "lstm", "leaky_relu"),
-         (30, 512, 30, 70, "lstm", "leaky_relu"), (40, 512, 30, 70, "lstm", "leaky_relu"),
-         (50, 512, 30, 70, "lstm", "leaky_relu"), (20, 1024, 50, 120, "lnlstm", "leaky_relu"),
-         (20, 1024, 50, 120, "gru", "leaky_relu"), (20, 512, 30, 70, "lstm", "elu"), (20, 512, 30, 70, "lstm", "tanh")]
+# (N, envs, episode steps, vector steps, NetMon cell (None: no NetMon), --activation-function, random topology)
+CASES = [(20, 4096, 50, 120, "lstm", "leaky_relu", True), (10, 512, 30, 70, "lstm", "leaky_relu", True),
+         (30, 512, 30, 70, "lstm", "leaky_relu", True), (40, 512, 30, 70, "lstm", "leaky_relu", True),
+         (50, 512, 30, 70, "lstm", "leaky_relu", True), (20, 1024, 50, 120, "lnlstm", "leaky_relu", True),
+         (20, 1024, 50, 120, "gru", "leaky_relu", True), (20, 512, 30, 70, "lstm", "elu", True),
+         (20, 512, 30, 70, "lstm", "tanh", True),
+         (20, 4096, 50, 120, "lstm", "leaky_relu", False),  # config 3: NetMon on the fixed graph
+         (20, 1024, 50, 120, None, "leaky_relu", False)]    # config 2: no NetMon, fixed graph
+# LN-LSTM: fixed upper bound of the fp32 envelope (measured 1.9e-3 state / 1.4e-3 readout for the fp32
+# restatement over 120 steps), so a GPU error growing with the envelope still fails
+ENVELOPE_CAP = 8e-3
+
+
+def case_id(c):
+    return f"N{c[0]}-{c[4] or 'no_netmon'}-{c[5]}" + ("" if c[6] else "-fixed")
 
 
 def adjacency(topo, N):
@@ -49,12 +62,12 @@ def adjacency(topo, N):
     return m
 
 
-@pytest.mark.parametrize("case", CASES, ids=[f"N{c[0]}-{c[4]}-{c[5]}" for c in CASES])
+@pytest.mark.parametrize("case", CASES, ids=[case_id(c) for c in CASES])
 @pytest.mark.parametrize("form", ["x3", "f32"])
 def test_benched_rollout_long_horizon(form, case, monkeypatch, oracle_mod):
     import netmon_ref
 
-    N, B, EP, STEPS, RNN, ACT = case
+    N, B, EP, STEPS, RNN, ACT, RANDOM = case
     SAMPLE = sorted({0, 1, B // 5, B // 2 - 1, B // 2, B // 2 + 1, (4 * B) // 5, B - 1})
 
     gm = importlib.import_module("graph-marl_amd")
@@ -62,13 +75,13 @@ def test_benched_rollout_long_horizon(form, case, monkeypatch, oracle_mod):
     RO = importlib.import_module("graph-marl_amd.rollout")
     monkeypatch.setattr(gm._lib, "GEMM_MODE", form)
     gm._lib.range_status(clear=True)
-    net = gm.Network(N, random_topology=True, excluded_seeds=gm.EVAL_SEEDS, device=0)
+    net = gm.Network(N, random_topology=RANDOM, excluded_seeds=gm.EVAL_SEEDS, device=0)
     torch.manual_seed(0)
-    netmon = M.NetMon(4 * N + 8, 128, [512, 256], 1, rnn_type=RNN, activation=ACT).cuda()
-    dqn = M.DQN(6 * N + 10 + netmon.get_out_features(), [512, 256], 4, activation=ACT).cuda()
+    netmon = M.NetMon(4 * N + 8, 128, [512, 256], 1, rnn_type=RNN, activation=ACT).cuda() if RNN else None
+    dqn = M.DQN(6 * N + 10 + (netmon.get_out_features() if RNN else 0), [512, 256], 4, activation=ACT).cuda()
     ro = RO.StreamedRollout(net, A, B, netmon, dqn, groups=G, seed=0, epsilon=EPS, episode_steps=EP, device=0)
     per = B // G
-    Wn = {k: v.detach().double().cpu().numpy() for k, v in netmon.state_dict().items()}
+    Wn = {k: v.detach().double().cpu().numpy() for k, v in netmon.state_dict().items()} if RNN else {}
     Wd = {k: v.detach().double().cpu().numpy() for k, v in dqn.state_dict().items()}
     od = 6 * N + 10
 
@@ -82,6 +95,8 @@ def test_benched_rollout_long_horizon(form, case, monkeypatch, oracle_mod):
 
         pol.select = select
         wenv = ro.wenvs[g]
+        if not RNN:  # no NetMon: act() -> select(), then the env step
+            continue
         orig_ps = wenv.policy_step_
 
         def policy_step_(q, eps, actions, detail=None, g=g, orig_ps=orig_ps):  # fused ε-greedy + env step
@@ -90,7 +105,8 @@ def test_benched_rollout_long_horizon(form, case, monkeypatch, oracle_mod):
 
         wenv.policy_step_ = policy_step_
 
-    cfg = oracle_mod.make_config(N, A, topo_mode=oracle_mod.TOPO_RANDOM, excluded=gm.EVAL_SEEDS)
+    cfg = oracle_mod.make_config(N, A, topo_mode=oracle_mod.TOPO_RANDOM if RANDOM else oracle_mod.TOPO_FIXED,
+                                 excluded=gm.EVAL_SEEDS)
     orc = {e: oracle_mod.OracleEnv(cfg, e) for e in SAMPLE}
     loc = {e: (e // per, e % per) for e in SAMPLE}
 
@@ -100,8 +116,8 @@ def test_benched_rollout_long_horizon(form, case, monkeypatch, oracle_mod):
         for e, (g, i) in loc.items():
             env, wenv = ro.envs[g], ro.wenvs[g]
             out[e] = dict(obs=env.obs_buf[i, :, :od].cpu().numpy(), node_obs=env.node_obs[i].cpu().numpy(),
-                          state=wenv.current_netmon_state[i].cpu().numpy(),
-                          readout=wenv.obs[i, :, od:].cpu().numpy(), reward=env.reward[i].cpu().numpy(),
+                          state=wenv.current_netmon_state[i].cpu().numpy() if RNN else None,
+                          readout=wenv.obs[i, :, od:].cpu().numpy() if RNN else None, reward=env.reward[i].cpu().numpy(),
                           done=env.done[i].cpu().numpy().astype(bool),
                           adj=env.get_nodes_adjacency()[i].cpu().numpy())
         return out
@@ -115,6 +131,7 @@ def test_benched_rollout_long_horizon(form, case, monkeypatch, oracle_mod):
     fp32_envelope = RNN == "lnlstm"
     Wn32 = {k: v.astype(np.float32) for k, v in Wn.items()}
     state32, worst32 = {}, {"state": 0.0, "readout": 0.0}
+    ratio = {"worst": 0.0}  # LN-LSTM: worst GPU error / envelope (printed: a creep shows between runs)
 
     def netmon_check(e, o, v, t):
         ob = o.observe()
@@ -122,6 +139,8 @@ def test_benched_rollout_long_horizon(form, case, monkeypatch, oracle_mod):
         assert (v["node_obs"] == ob["node_obs"]).all(), f"step {t} env {e}: node obs"
         adj = adjacency(o.topology(), N)
         assert (v["adj"] == adj).all(), f"step {t} env {e}: I+A adjacency"
+        if not RNN:  # config 2: the DQN reads the env obs alone
+            return ob["obs"].astype(np.float64)
         out, st = netmon_ref.netmon_forward(Wn, ob["node_obs"][None], adj[None], state64.get(e), RNN, "sum", 1, act=ACT)
         state64[e] = st
         ro_ = netmon_ref.to_network_obs(out, ob["node_agent"][None])[0]
@@ -134,9 +153,11 @@ def test_benched_rollout_long_horizon(form, case, monkeypatch, oracle_mod):
             ro32 = netmon_ref.to_network_obs(out32, ob["node_agent"][None])[0]
             worst32["state"] = max(worst32["state"], np.abs(st32 - st).max())
             worst32["readout"] = max(worst32["readout"], np.abs(ro32 - ro_).max())
-            tol_s, tol_r = max(TOL, 4 * worst32["state"]), max(TOL, 4 * worst32["readout"])
+            tol_s = min(ENVELOPE_CAP, max(TOL, 4 * worst32["state"]))
+            tol_r = min(ENVELOPE_CAP, max(TOL, 4 * worst32["readout"]))
         es = np.abs(v["state"] - st[0]).max()
         er = np.abs(v["readout"] - ro_).max()
+        ratio["worst"] = max(ratio["worst"], es / tol_s, er / tol_r)
         worst["state"], worst["readout"] = max(worst["state"], es), max(worst["readout"], er)
         assert es < tol_s and er < tol_r, f"step {t} env {e}: NetMon state err {es}, readout err {er} (tol {tol_s}, {tol_r})"
         return np.concatenate([ob["obs"].astype(np.float64), ro_], -1)
@@ -156,18 +177,21 @@ def test_benched_rollout_long_horizon(form, case, monkeypatch, oracle_mod):
             q64 = netmon_ref.dqn_forward(Wd, joint[e], act=ACT)
             eq = np.abs(q - q64).max()
             worst["q"] = max(worst["q"], eq)
-            assert eq < (max(TOL, 4 * worst32["readout"]) if fp32_envelope else TOL), f"step {t} env {e}: Q err {eq}"
+            tol_q = min(ENVELOPE_CAP, max(TOL, 4 * worst32["readout"])) if fp32_envelope else TOL
+            ratio["worst"] = max(ratio["worst"], eq / tol_q)
+            assert eq < tol_q, f"step {t} env {e}: Q err {eq}"
             exp = o.draw_egreedy(q, EPS)
             assert (exp == acts[g][i]).all(), f"step {t} env {e}: ε-greedy actions"
             rew, done, _ = o.step(acts[g][i])
             assert (rew == v[e]["reward"]).all() and (done == v[e]["done"]).all(), f"step {t} env {e}: reward/done"
             if t % EP == 0:  # the rollout reset the episode after this step: new topology, NetMon start-up
                 o.reset()
-                state64.pop(e)
+                state64.pop(e, None)
                 state32.pop(e, None)
             joint[e] = netmon_check(e, o, v[e], t)
         resets += t % EP == 0
     assert resets == STEPS // EP >= 2
     gm._lib.check_range()
-    print(f"N={N} {RNN} {ACT} form {form}: worst |err| over {STEPS} steps x {len(SAMPLE)} envs: {worst}"
+    print(f"N={N} {RNN} {ACT} {'random' if RANDOM else 'fixed'} form {form}: worst |err| over {STEPS} steps x "
+          f"{len(SAMPLE)} envs: {worst}; worst err / tolerance {ratio['worst']:.3g}"
           + (f"; fp32 restatement of the reference formula vs fp64: {worst32}" if fp32_envelope else ""))

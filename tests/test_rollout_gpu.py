@@ -13,15 +13,15 @@ pytestmark = pytest.mark.gpu
 N, A, B = 20, 20, 8
 
 
-def build(groups, seed=0, episode_steps=10):
+def build(groups, seed=0, episode_steps=10, n_env=B, K=2, epsilon=0.3):
     gm = importlib.import_module("graph-marl_amd")
     M = importlib.import_module("graph-marl_amd.model")
     RO = importlib.import_module("graph-marl_amd.rollout")
     net = gm.Network(N, random_topology=True, excluded_seeds=gm.EVAL_SEEDS, device=0)
     torch.manual_seed(3)
-    netmon = M.NetMon(4 * N + 8, 128, [512, 256], 2).cuda()
+    netmon = M.NetMon(4 * N + 8, 128, [512, 256], K).cuda()
     dqn = M.DQN(6 * N + 10 + netmon.get_out_features(), [512, 256], 4).cuda()
-    return RO.StreamedRollout(net, A, B, netmon, dqn, groups=groups, seed=seed, epsilon=0.3,
+    return RO.StreamedRollout(net, A, n_env, netmon, dqn, groups=groups, seed=seed, epsilon=epsilon,
                               episode_steps=episode_steps, device=0)
 
 
@@ -122,6 +122,56 @@ def test_graph_replay_matches_eager(groups, gsteps, warm, per_group):
     assert (ro._graphs is not None and len(ro._graphs) == groups) if per_group else ro._graph is not None
     for a, b in zip(snapshot(ro), ref):
         assert_same(a, b)
+
+
+def test_graph_replay_matches_eager_benched_size():
+    """The headline's launch mode at the headline's size (bench.py defaults): 4096 envs in 2 stream
+    groups, NetMon K = 1, ε = 0.5, 50-step episodes, one graph of 10 vector steps per group, 120
+    replayed steps (two resets between replays). At 40 960 rows per group every GEMM runs the tiles
+    the bench replays (LDS-DMA k_gemm3g forms), not the small-batch register-staged ones. Bit-identical
+    to eager launches: env state, RNG keys, joint observations, rewards and NetMon states."""
+    kw = dict(n_env=4096, K=1, epsilon=0.5, episode_steps=50)
+    eager = build(2, **kw)
+    eager.reset()
+    eager.run(10 + 120)
+    ref = snapshot(eager)
+    del eager
+    torch.cuda.empty_cache()
+
+    ro = build(2, **kw)
+    ro.reset()
+    for _ in range(10):
+        ro.step()
+    ro.capture(10, per_group=True)
+    ro.run(120)
+    assert ro._graphs is not None and len(ro._graphs) == 2
+    for a, b in zip(snapshot(ro), ref):
+        assert_same(a, b)
+
+
+def test_rollout_orders_after_caller_stream():
+    """Replays (and eager steps) wait for work the caller enqueued on its own stream before run(): a
+    NetMon state edit made on the current stream behind a busy kernel is seen by every group's next
+    step (graph replay == eager with the same edit, and both differ from no edit)."""
+    def go(graph, edit=True):
+        ro = build(2)
+        ro.reset()
+        for _ in range(2):
+            ro.step()
+        if graph:
+            ro.capture(2)
+        torch.cuda.synchronize()
+        torch.cuda._sleep(50_000_000)  # keep the caller's stream busy: an unordered step would race the edit
+        if edit:
+            for w in ro.wenvs:
+                w.current_netmon_state.mul_(0.5)
+        ro.run(2)
+        return snapshot(ro)
+
+    g = go(True)
+    for a, b in zip(g, go(False)):
+        assert_same(a, b)
+    assert any(not np.array_equal(a["netmon"], b["netmon"]) for a, b in zip(g, go(False, edit=False)))
 
 
 def test_graph_needs_fixed_epsilon():

@@ -100,6 +100,7 @@ def main():
     ap.add_argument("--episode-steps", type=int, default=50)
     ap.add_argument("--unfused-head", action="store_true", help="profiles taken before gm_gemm_x3_head")
     ap.add_argument("--json", help="write per-launch HBM bytes keyed by bench.py timer tags (pmc_traffic.json)")
+    ap.add_argument("--src", help="build.src of the profiled library (recorded; bench.py compares it)")
     ap.add_argument("--rows", type=int, default=81920, help="GEMM rows of the profiled rollout (n_env * N)")
     ap.add_argument("--env-k", type=int, default=128,
                     help="env-obs columns of DQN layer 1 (128: GEMM-ready obs copy, 130: GM_GEMM_OBS=0 profiles)")
@@ -144,7 +145,8 @@ def main():
                 out[tag] = {"fetch_bytes": int(2 * p["FETCH_SIZE"] * 1024), "write_bytes": int(p["WRITE_SIZE"] * 1024),
                             "kernel": n, "grid": g}
         with open(a.json, "w") as f:
-            json.dump({"source": {"trace": a.trace, "fetch": a.fetch, "write": a.write}, "kernels": out}, f, indent=1)
+            json.dump({"source": {"trace": a.trace, "fetch": a.fetch, "write": a.write}, "src": a.src, "kernels": out}, f,
+                      indent=1)
 
 
 if __name__ == "__main__":
