@@ -50,6 +50,27 @@
 #if GM_SPLIT_ASM != 0 && GM_SPLIT_ASM != 2
 #error "GM_SPLIT_ASM must be 0 (compiler-visible split) or 2 (asm + s_nop 1): the bare asm form races the MFMA read"
 #endif
+#ifndef GM_SPLIT_NEXT
+// 1: the 16x16x32 LDS-DMA kernels split tile k+1's A between tile k's second-half MFMAs (two split
+// register sets) instead of as a VALU block at the start of tile k+1's first MFMA segment
+#define GM_SPLIT_NEXT 0
+#endif
+#ifndef GM_K3_REMAP
+// 1: k_gemm3 (BK = 16) maps lanes to (row, chunk) so that each 16-lane group of the split-A
+// ds_write_b64 stores covers 8 rows x 2 adjacent 8-byte chunks (all 32 banks once at the 80-byte row
+// stride; the plain map put rows r and r + 3 of a group on banks 0-3: 2-way) and each 8-lane group
+// of the B ds_write_b128 stores 8 rows of one chunk (conflict-free); the LDS image is unchanged
+#define GM_K3_REMAP 0
+#endif
+#ifndef GM_DMA_SEQ
+// 1: the LDS-DMA kernels walk the A sources in tile order with the current source's buffer and per-lane
+// row offsets held in registers (advanced at segment ends), instead of a division and a branch tree per
+// k tile between the barrier and the next MFMAs (READOUT: k0 / hidden + a 4-way switch)
+#define GM_DMA_SEQ 0
+#endif
+#ifndef GM_PRIO
+#define GM_PRIO 0  // 1: waves 4-7 of the 8-wave LDS-DMA blocks at s_setprio 1 for the k loop (guide: static priority)
+#endif
 #ifndef GM_DIAG
 #define GM_DIAG 0  // 1: no A split, 2: no loads/stores in the k loop, 3: as 2 without barriers
 #endif
@@ -749,7 +770,9 @@ __global__ __launch_bounds__(WGM* WGN * 64, OCC) void k_gemm3(ASrc a0, ASrc a1, 
     const int m0 = (bid / nN) * BM, n0 = (bid % nN) * BN;
 
     // ---- per-thread source byte offsets (fixed over K) ----
-    const int c4 = tid % CPR, rbase = tid / CPR;
+    constexpr bool REMAP = GM_K3_REMAP && CPR == 4 && THREADS % 64 == 0;
+    const int c4 = REMAP ? 2 * ((lane >> 4) & 1) + ((lane >> 3) & 1) : tid % CPR;
+    const int rbase = REMAP ? wave * 16 + 8 * (lane >> 5) + (lane & 7) : tid / CPR;
     int off1[AQ];       // src1 row
     int so[AQ][4];      // DENSE: so[q][0] row; AGGREGATE: member rows; READOUT: segment rows (OOB = none)
     float scale[AQ];
@@ -1466,11 +1489,39 @@ __global__ __launch_bounds__(WGM* WGN * 64, OCC) void k_gemm3g(ASrc a0, ASrc a1,
     const __amdgpu_buffer_rsrc_t r1 = a1.p0 ? rsrc_rows(a1.p0, a1.ld0, m0, a1.bytes0) : rsrc(a0.p0, 0u);
     const __amdgpu_buffer_rsrc_t rw = rsrc(reinterpret_cast<const float*>(w), wbytes);
 
+    // GM_DMA_SEQ: the current A source (issue() is called for kt = 0, 1, 2, .. in order)
+    __amdgpu_buffer_rsrc_t cur_r = r0a;
+    int cur_o[NA];
+#pragma unroll
+    for (int j = 0; j < NA; j++) cur_o[j] = so[j][0];
+    int cur_ko = 0, seg_idx = 0;
+    int seg_left = AMODE == GM_A_DENSE ? a0.k : a0.hidden;  // k columns left in the current segment
     // DMA of k tile kt into stage ST (all LDS bases wave-uniform)
     auto issue = [&](auto ST, int kt) {
         char* base = lds + decltype(ST)::value * STAGE_B + wave * NA * 1024;
         const int k0 = kt * BK;
-        if (k0 < a0.k) {
+        if constexpr (GM_DMA_SEQ) {
+#pragma unroll
+            for (int j = 0; j < NA; j++) dma16(cur_r, base + j * 1024, cur_o[j], cur_ko);
+            cur_ko += BK * 4;
+            seg_left -= BK;
+            if (seg_left <= 0) {  // wave-uniform: next readout segment, or the dense second source
+                seg_idx++;
+                cur_ko = 0;
+                if (AMODE == GM_A_READOUT && seg_idx * a0.hidden < a0.k) {
+                    cur_r = r0b;
+                    seg_left = a0.hidden;
+#pragma unroll
+                    for (int j = 0; j < NA; j++)
+                        cur_o[j] = seg_idx == 1 ? so[j][1] : (seg_idx == 2 ? so[j][2] : so[j][3]);
+                } else {
+                    cur_r = r1;
+                    seg_left = 1 << 30;
+#pragma unroll
+                    for (int j = 0; j < NA; j++) cur_o[j] = o1[j];
+                }
+            }
+        } else if (k0 < a0.k) {
             if (AMODE == GM_A_DENSE) {
 #pragma unroll
                 for (int j = 0; j < NA; j++) dma16(r0a, base + j * 1024, so[j][0], k0 * 4);
@@ -1565,6 +1616,8 @@ __global__ __launch_bounds__(WGM* WGN * 64, OCC) void k_gemm3g(ASrc a0, ASrc a1,
         }
     }
     half8 sah[2 * TM], sal[2 * TM];  // 16x16 form: split A of the current k tile (both column halves)
+    half8 sah2[2 * TM], sal2[2 * TM];  // GM_SPLIT_NEXT: the next tile's split A (register set of odd steps)
+    constexpr bool SPLIT_NEXT = GM_SPLIT_NEXT && MF == 1 && STAGES == 2;
     const _Float16 s12 = (_Float16)(1.0f / 4096.0f);
     const float ascale = AX == 2 ? *a0.scale : 1.0f;
     const int aexp = __builtin_amdgcn_frexp_expf(ascale) - 1;  // ascale = 2^aexp
@@ -1602,6 +1655,41 @@ __global__ __launch_bounds__(WGM* WGN * 64, OCC) void k_gemm3g(ASrc a0, ASrc a1,
         for (int j = 0; j < TN; j++) {
             f.bh[j] = *reinterpret_cast<const half8*>(sbase + boff[sb][0] + j * 32 * 128);
             f.bl[j] = *reinterpret_cast<const half8*>(sbase + boff[sb][1] + j * 32 * 128);
+        }
+    };
+    // split row block i of f's raw A into (h, l) (the same bits as the in-segment split)
+    auto split_blk = [&](const Frag& f, int i, half8& h, half8& l) {
+        floatx4 x0 = f.xa[i][0], x1 = f.xa[i][1];
+        if constexpr (AX == 1) {
+#pragma unroll
+            for (int e = 0; e < 4; e++) amx = fmaxf(amx, fmaxf(fabsf(x0[e]), fabsf(x1[e])));
+        } else if constexpr (AX == 2 && !GM_SPLIT_LDEXP) {
+            x0 *= ascale;
+            x1 *= ascale;
+        }
+        split8(x0, x1, h, l, AX == 2 && GM_SPLIT_LDEXP ? aexp : 0);
+    };
+    // GM_SPLIT_NEXT: the MFMAs of column half sb of the current tile on the split set (ch, cl); with
+    // NEXT, row block j - 1 of the next tile's raw A (fn) is split into (nh, nl) before block j's MFMAs
+    auto mfma16n = [&](const Frag& f, auto SB, half8 (&ch)[2 * TM], half8 (&cl)[2 * TM], const Frag& fn,
+                       half8 (&nh)[2 * TM], half8 (&nl)[2 * TM], auto NEXT) {
+        constexpr int sb = decltype(SB)::value;
+#pragma unroll
+        for (int j = 0; j < TN; j++) {
+            if constexpr (decltype(NEXT)::value) {
+                if (j >= 1 && j - 1 < 2 * TM) split_blk(fn, j - 1, nh[j - 1], nl[j - 1]);
+                if (j == TN - 1)
+#pragma unroll
+                    for (int i = TN - 1; i < 2 * TM; i++) split_blk(fn, i, nh[i], nl[i]);
+            }
+            const half8 bs = f.bh[j] * s12;  // w_hi * 2^-12, exact
+#pragma unroll
+            for (int i = 0; i < 2 * TM; i++) {
+                floatx4& c = acc4[i][sb * TN + j];
+                c = __builtin_amdgcn_mfma_f32_16x16x32_f16(cl[i], bs, c, 0, 0, 0);
+                c = __builtin_amdgcn_mfma_f32_16x16x32_f16(ch[i], f.bl[j], c, 0, 0, 0);
+                c = __builtin_amdgcn_mfma_f32_16x16x32_f16(ch[i], f.bh[j], c, 0, 0, 0);
+            }
         }
     };
     auto mfma16 = [&](const Frag& f, auto SB, auto J0, auto J1) {
@@ -1725,6 +1813,9 @@ __global__ __launch_bounds__(WGM* WGN * 64, OCC) void k_gemm3g(ASrc a0, ASrc a1,
     if (ragged && nk == 1) zero_tail(I0{});
     Frag f0, f1;
     read(I0{}, I0{}, f0);
+    if constexpr (SPLIT_NEXT)
+#pragma unroll
+        for (int i = 0; i < 2 * TM; i++) split_blk(f0, i, sah[i], sal[i]);
 #if GM_DIAG == 10
     read(I0{}, I1{}, f1);
 #endif
@@ -1738,7 +1829,12 @@ __global__ __launch_bounds__(WGM* WGN * 64, OCC) void k_gemm3g(ASrc a0, ASrc a1,
 #else
         read(ST, I1{}, f1);
         __builtin_amdgcn_sched_barrier(0);
-        if constexpr (MF == 1)
+        if constexpr (SPLIT_NEXT) {
+            if constexpr (S == 0)
+                mfma16n(f0, I0{}, sah, sal, f0, sah2, sal2, std::false_type{});
+            else
+                mfma16n(f0, I0{}, sah2, sal2, f0, sah, sal, std::false_type{});
+        } else if constexpr (MF == 1)
             mfma16(f0, I0{}, I0{}, std::integral_constant<int, TN>{});
         else
             mfma(f0);
@@ -1755,11 +1851,20 @@ __global__ __launch_bounds__(WGM* WGN * 64, OCC) void k_gemm3g(ASrc a0, ASrc a1,
             read(SN{}, I0{}, f0);
         }
         __builtin_amdgcn_sched_barrier(0);
-        if constexpr (MF == 1)
+        if constexpr (SPLIT_NEXT) {  // split of tile kt + 1 (f0, just read) between these MFMAs
+            if constexpr (S == 0)
+                mfma16n(f1, I1{}, sah, sal, f0, sah2, sal2, std::true_type{});
+            else
+                mfma16n(f1, I1{}, sah2, sal2, f0, sah, sal, std::true_type{});
+        } else if constexpr (MF == 1)
             mfma16(f1, I1{}, I0{}, std::integral_constant<int, TN>{});
         else
             mfma(f1);
     };
+#if GM_PRIO
+    if constexpr (NW == 8)
+        if (__builtin_amdgcn_readfirstlane(threadIdx.x) >= 256) __builtin_amdgcn_s_setprio(1);
+#endif
 #if GM_DIAG == 7  // diagnostic build 7: prologue + epilogue only (timing only)
     if (nk < 0)
 #endif
@@ -1772,6 +1877,9 @@ __global__ __launch_bounds__(WGM* WGN * 64, OCC) void k_gemm3g(ASrc a0, ASrc a1,
             if (kt + 3 < nk) step(I3{}, kt + 3);
     }
 
+#if GM_PRIO
+    __builtin_amdgcn_s_setprio(0);
+#endif
     if constexpr (AX == 1) {
         amx = gm_wave_max(amx);
         if (lane == 0) gm_amax_publish(a0.amax, amx);

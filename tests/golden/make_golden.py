@@ -1043,6 +1043,11 @@ def main():
         # (256 graphs x 20 nodes = 5120 rows per step, 20480 over the 4 steps)
         gen_train(os.path.join(HERE, "train_big.npz"), Network, Routing, EVAL_SEEDS, NetMon, DQN, interpolate_model,
                   H=128, enc=(512, 256), dqn_hidden=(512, 256), B=256, L=4, compact=True, det_seed=11)
+    if only is None or "train_prod" in only:
+        # the production forward / input-gradient tiles: 512 graphs x 4 steps = 40 960 node and agent rows
+        # per batched layer (>= 32 768: the LDS-DMA k_gemm3g forms of the sequence-batched update)
+        gen_train(os.path.join(HERE, "train_prod.npz"), Network, Routing, EVAL_SEEDS, NetMon, DQN, interpolate_model,
+                  H=128, enc=(512, 256), dqn_hidden=(512, 256), B=512, L=4, compact=True, det_seed=23)
     for act in ("relu", "elu", "tanh", "sigmoid"):  # --activation-function (src/main.py:194-197, 440-441)
         if only is None or f"train_{act}" in only:
             gen_train(os.path.join(HERE, f"train_{act}.npz"), Network, Routing, EVAL_SEEDS, NetMon, DQN,

@@ -133,3 +133,27 @@ def test_bench_gpus_flag_launches_ranks(monkeypatch):
     bench.check_world(args, 4)
     with pytest.raises(SystemExit):
         bench.check_world(args, 2)
+
+
+def test_bench_pmc_window_parser(tmp_path):
+    """bench.py's same-run PMC probe (measure_pmc) reads the child's counter CSV: the last
+    2 PMC_X + PMC_Y dispatches of the library's kernels are PMC_X (DQN layer 1, layer 2 + head)
+    pairs then PMC_Y env steps; medians per launch; a window of another shape is rejected."""
+    import bench
+
+    X, Y = bench.PMC_X, bench.PMC_Y
+    rows = [("at::native::fill", 64, 1.0)] * 3 + [("k_env_reset", 4096, 7.0)]
+    rows += [("k_gemm3g", 655360, 100.0 + i) for i in range(1)]  # older dispatch outside the window
+    for i in range(X):
+        rows += [("k_gemm3g", 655360, 200.0 + i), ("k_gemm3g", 327680, 50.0)]
+    rows += [("k_env_step", 262144, 30.0 + i) for i in range(Y)]
+    p = tmp_path / "c.csv"
+    with open(p, "w") as f:
+        f.write("Dispatch_Id,Kernel_Name,Grid_Size,Counter_Name,Counter_Value\n")
+        for i, (n, g, v) in enumerate(rows):
+            f.write(f"{i},{n},{g},FETCH_SIZE,{v}\n")
+    l1, env = bench._pmc_window(str(p), "FETCH_SIZE")
+    assert l1 == 200.0 + X // 2 and env == 30.0 + Y // 2
+    with open(p, "a") as f:  # one more layer-2 dispatch after the env steps: not the probe's window
+        f.write(f"{len(rows)},k_gemm3g,327680,FETCH_SIZE,1.0\n")
+    assert bench._pmc_window(str(p), "FETCH_SIZE") is None

@@ -143,9 +143,12 @@ def test_two_rank_dqn_update_keeps_replicas_identical(seq_path):
 
 def _cli_worker(rank, world, port, q, log_dir):
     """One rank of `torch.distributed.run graph-marl_amd/main.py` (the env a launcher sets), both
-    ranks on cuda:0 over gloo (GM_DIST_SHARE_GPU=1)."""
+    ranks on cuda:0 over gloo (GM_DIST_SHARE_GPU=1). The rank's output goes to rank<r>.log."""
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE=str(world), RANK=str(rank),
                       LOCAL_RANK=str(rank), LOCAL_WORLD_SIZE=str(world), GM_DIST_SHARE_GPU="1")
+    fd = os.open(os.path.join(log_dir, f"rank{rank}.log"), os.O_WRONLY | os.O_CREAT | os.O_TRUNC)
+    os.dup2(fd, 1)
+    os.dup2(fd, 2)
     try:
         main = importlib.import_module("graph-marl_amd.main")
         T = importlib.import_module("graph-marl_amd.train")
@@ -172,7 +175,10 @@ def _cli_worker(rank, world, port, q, log_dir):
                        "--disable-progressbar", f"--log-dir={log_dir}"])
         q.put((rank, {"seeds": rec["seeds"], "updates": rec["updates"], "flat": rec["flat"].numpy(),
                       "loss": rec["loss"], "metrics": m}))
-    except Exception as ex:
+    except BaseException as ex:  # SystemExit too: report instead of leaving the parent waiting
+        import traceback
+
+        traceback.print_exc()
         q.put((rank, f"error: {ex!r}"))
         raise
 
@@ -192,14 +198,19 @@ def test_two_rank_cli_training_keeps_replicas_identical(tmp_path):
     res = {}
     try:
         for _ in range(2):
-            r, msg = q.get(timeout=240)
+            r, msg = q.get(timeout=150)
             res[r] = msg
+            if not isinstance(msg, dict):  # the other rank would wait in a collective: stop now
+                break
+    except Exception as ex:
+        res["wait"] = repr(ex)
     finally:
         for p in procs:
             p.join(30 if len(res) == 2 else 1)
             if p.is_alive():
                 p.kill()
-    assert all(isinstance(v, dict) for v in res.values()), res
+    logs = {r: (tmp_path / f"rank{r}.log").read_text()[-3000:] for r in range(2) if (tmp_path / f"rank{r}.log").exists()}
+    assert len(res) == 2 and all(isinstance(v, dict) for v in res.values()), (res, logs)
     a, b = res[0], res[1]
     assert not set(a["seeds"]) & set(b["seeds"]) and len(a["seeds"]) == 16
     assert a["updates"] == b["updates"] == 41

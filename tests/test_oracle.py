@@ -142,7 +142,7 @@ def test_oracle_bench_driver_runs(oracle_mod):
     assert (obs[..., :20].sum(-1) == 1).all() and (obs[..., 20:40].sum(-1) == 1).all()
 
 
-@pytest.mark.parametrize("name", ["train.npz", "train_big.npz", "train_lnlstm.npz", "train_gru.npz", "train_relu.npz",
+@pytest.mark.parametrize("name", ["train.npz", "train_big.npz", "train_prod.npz", "train_lnlstm.npz", "train_gru.npz", "train_relu.npz",
                                   "train_elu.npz", "train_tanh.npz", "train_sigmoid.npz"])
 def test_train_golden_forward_matches_restatement(name):
     """The golden DQN+NetMon updates' Q / Q-target / loss follow from their weights (stored, or for

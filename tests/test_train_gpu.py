@@ -43,7 +43,8 @@ def golden_batches(g, M, RB, dev, state0):
 # LayerNorm-LSTM (mean aggregation, K = 2) and GRU (K = 2) cells under grad (src/layernormlstm.py,
 # nn.GRUCell via src/model.py:387-393); train_relu / _elu / _tanh / _sigmoid: --activation-function
 # (src/main.py:194-197, 440-441) through every MLP layer (GEMM epilogues, gm_act_bwd)
-GOLDENS = ["train.npz", "train_aux.npz", "train_big.npz", "train_lnlstm.npz", "train_gru.npz", "train_relu.npz",
+# train_prod: the same architecture at 512 graphs x 4 steps (10 240 rows per step)
+GOLDENS = ["train.npz", "train_aux.npz", "train_big.npz", "train_prod.npz", "train_lnlstm.npz", "train_gru.npz", "train_relu.npz",
            "train_elu.npz", "train_tanh.npz", "train_sigmoid.npz"]
 
 

@@ -221,13 +221,14 @@ def _golden_seq(g, dev, netmon, RBm, state0=None):
                       an[:Lq].contiguous(), f(g["node_state0"]) if state0 is None else state0, next_fields)
 
 
-@pytest.mark.parametrize("name", ["train.npz", "train_big.npz"])
+@pytest.mark.parametrize("name", ["train.npz", "train_big.npz", "train_prod.npz"])
 def test_seq_update_matches_reference_golden(name):
     """The sequence-batched update on the reference's golden updates at the autograd path's
     tolerances: q, targets, loss, raw and clipped gradients, AdamW step, soft target update.
     train.npz: NetMon H = 32, encoder [64, 48], DQN [64, 32], L = 3 with episode ends;
     train_big.npz: the CLI-default sizes with 256 graphs x 4 steps (20 480 node and agent rows per
-    batched layer, every kernel in its HIP form)."""
+    batched layer, every kernel in its HIP form); train_prod.npz: 512 graphs x 4 steps (40 960 rows
+    per batched layer: the production LDS-DMA forward / input-gradient tiles, >= 32 768 rows)."""
     M, T, S, FU, L = mods()
     RBm = importlib.import_module("graph-marl_amd.replaybuffer")
     import golden_update as GU
@@ -250,11 +251,13 @@ def test_seq_update_matches_reference_golden(name):
     check_update(g, names, params, opt, model, target, T)
 
 
-@pytest.mark.parametrize("K,agg", [(1, "sum"), (2, "mean")])
-def test_seq_update_matches_autograd_path_on_rollout(K, agg):
+@pytest.mark.parametrize("K,agg,tiles", [(1, "sum", "common"), (2, "mean", "common"), (1, "sum", "default")])
+def test_seq_update_matches_autograd_path_on_rollout(K, agg, tiles):
     """Replayed rollout data (64 envs x 30 steps, episodes of 10 steps), the CLI-default model sizes:
     the same sampled sequences through train.dqn_loss (autograd, consecutive target reuse) and the
-    sequence-batched path give the same q, targets, loss and gradients (fp32 order)."""
+    sequence-batched path give the same q, targets, loss and gradients (fp32 order). tiles "common":
+    both paths on one GEMM tile (identical forward bits); "default": each path on the tiles it picks
+    in production (the batched path's 40 960-row layers on the LDS-DMA forms), compared kink-tolerantly."""
     gm = importlib.import_module("graph-marl_amd")
     M, T, S, FU, L = mods()
     RB = importlib.import_module("graph-marl_amd.replaybuffer")
@@ -296,6 +299,9 @@ def test_seq_update_matches_autograd_path_on_rollout(K, agg):
     model.train()
     # both paths on the same GEMM tile (k_gemm3, 128x128), so every forward pre-activation has the
     # same bits and leaky_relu's kink cannot flip between them (see below)
+    if tiles == "default":
+        _compare_paths(M, T, S, L, netmon, model, target, batches, seq, params, kink_tolerant=True)
+        return
     lib = FU._setup()
     lib.gm_gemm_set_tile(0)
     try:
@@ -304,7 +310,7 @@ def test_seq_update_matches_autograd_path_on_rollout(K, agg):
         lib.gm_gemm_set_tile(-1)
 
 
-def _compare_paths(M, T, S, L, netmon, model, target, batches, seq, params):
+def _compare_paths(M, T, S, L, netmon, model, target, batches, seq, params, kink_tolerant=False):
     l0, q0, t0 = T.dqn_loss(netmon, model, target, batches, 0.98, consecutive=True)
     for p in params:
         p.grad = None
@@ -342,7 +348,9 @@ def _compare_paths(M, T, S, L, netmon, model, target, batches, seq, params):
         errs[n] = (_fro(a, c), _fro(b, c))
     print("Frobenius-relative gradient error vs exact fp32 (autograd x3, sequence-batched x3):", errs)
     for n, (e_old, e_new) in errs.items():
-        assert e_new < max(2e-5, 2 * e_old), (n, e_old, e_new)
+        # default tiles: a kink flip moves a few gradient elements by ~1e-4 (see above); the bound
+        # still fails any systematic error (a wrong tile gives O(1) relative errors)
+        assert e_new < (max(1e-3, 4 * e_old) if kink_tolerant else max(2e-5, 2 * e_old)), (n, e_old, e_new)
 
 
 def test_operands_beyond_2gb():

@@ -52,10 +52,12 @@ def main():
         FU.gemm(a0, FU.dense(obs.data_ptr(), 128, 128), wp.data_ptr(), ldw, b.data_ptr(), m, 512, 1, y.data_ptr(), 512,
                 x3=x3)
 
+    if os.environ.get("TILE"):  # tile override (gm_gemm_set_tile), e.g. 9 = 3-stage 128x256
+        FU._setup().gm_gemm_set_tile(int(os.environ["TILE"]))
     for _ in range(10):  # ~2 s of back-to-back launches before timing (clock settles)
         timeit(ro, 20)
     us = min(timeit(ro) for _ in range(3))
-    print(json.dumps({"lib": os.environ.get("GM_LIB", "default"), "dqn_l1_us": round(us, 1),
+    print(json.dumps({"lib": os.environ.get("GM_LIB", "default"), "tile": os.environ.get("TILE", "-1"), "dqn_l1_us": round(us, 1),
                       "tflops_f16": round(3 * 2.0 * m * 512 * 640 / (us * 1e-6) / 1e12, 1)}), flush=True)
 
 
