@@ -68,6 +68,12 @@
 // k tile between the barrier and the next MFMAs (READOUT: k0 / hidden + a 4-way switch)
 #define GM_DMA_SEQ 0
 #endif
+#ifndef GM_ORDER
+// 1: in the 8-wave 16x16x32 LDS-DMA kernels, waves 4-7 (the second wave on each SIMD) run their
+// second-half MFMAs right after the tile barrier and issue the DMA / fragment reads after them, while
+// waves 0-3 issue first: the partner waves of a SIMD no longer do their post-barrier work in lockstep
+#define GM_ORDER 0
+#endif
 #ifndef GM_PRIO
 #define GM_PRIO 0  // 1: waves 4-7 of the 8-wave LDS-DMA blocks at s_setprio 1 for the k loop (guide: static priority)
 #endif
@@ -81,6 +87,14 @@
 #include "gm_act.hpp"
 
 int gm_fail(int code, const std::string& msg);
+
+#if GM_DIAG == 30
+// diagnostic build 30: per-segment s_memtime stamps of the LDS-DMA k loop (tools/stamp_bench.py)
+__device__ unsigned long long* g_stamps;
+extern "C" int gm_diag_stamps(void* buf) {
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_stamps), &buf, sizeof(buf)) == hipSuccess ? 0 : -1;
+}
+#endif
 
 namespace {
 
@@ -1439,10 +1453,28 @@ __global__ __launch_bounds__(WGM* WGN * 64, OCC) void k_gemm3g(ASrc a0, ASrc a1,
     static_assert(BM % (8 * NW) == 0 && BN % (8 * NW) == 0, "tile rows per wave");
     static_assert(AMODE != GM_A_AGGREGATE, "aggregate source uses k_gemm3");
     static_assert(STAGES >= 2 && STAGES <= 4, "stages");
+#if GM_DIAG == 30
+    __shared__ __attribute__((aligned(16))) char lds[STAGES * STAGE_B + 1024];
+#else
     __shared__ __attribute__((aligned(16))) char lds[STAGES * STAGE_B];
+#endif
 
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: LDS bases in SGPRs
+#if GM_DIAG == 30
+    // stamps of k steps 4..11 x 8 points by waves 0 and NW / 2 (one SIMD), kept in LDS until the end
+    unsigned long long* stl = reinterpret_cast<unsigned long long*>(lds + STAGES * STAGE_B);
+    const bool stw = lane == 0 && (wave == 0 || wave == NW / 2);
+    auto stamp = [&](int kt, int pt) {
+        if (stw && kt >= 4 && kt < 12) stl[((wave != 0) * 8 + (kt - 4)) * 8 + pt] = __builtin_amdgcn_s_memtime();
+    };
+#define GM_STAMP(kt, pt)                  \
+    __builtin_amdgcn_sched_barrier(0); \
+    stamp(kt, pt);                     \
+    __builtin_amdgcn_sched_barrier(0);
+#else
+#define GM_STAMP(kt, pt)
+#endif
     const int wr = wave / WGN, wc = wave % WGN;
     const int nM = (M + BM - 1) / BM, nN = (N + BN - 1) / BN;
     const int bid = xcd_remap(blockIdx.x, nM * nN);
@@ -1618,6 +1650,8 @@ __global__ __launch_bounds__(WGM* WGN * 64, OCC) void k_gemm3g(ASrc a0, ASrc a1,
     half8 sah[2 * TM], sal[2 * TM];  // 16x16 form: split A of the current k tile (both column halves)
     half8 sah2[2 * TM], sal2[2 * TM];  // GM_SPLIT_NEXT: the next tile's split A (register set of odd steps)
     constexpr bool SPLIT_NEXT = GM_SPLIT_NEXT && MF == 1 && STAGES == 2;
+    constexpr bool ORDER = GM_ORDER && MF == 1 && NW == 8 && !SPLIT_NEXT;
+    const bool late = wave >= NW / 2;  // wave-uniform (readfirstlane)
     const _Float16 s12 = (_Float16)(1.0f / 4096.0f);
     const float ascale = AX == 2 ? *a0.scale : 1.0f;
     const int aexp = __builtin_amdgcn_frexp_expf(ascale) - 1;  // ascale = 2^aexp
@@ -1825,8 +1859,10 @@ __global__ __launch_bounds__(WGM* WGN * 64, OCC) void k_gemm3g(ASrc a0, ASrc a1,
 #if GM_DIAG == 10  // diagnostic build 10: MFMAs only in the k loop (timing only)
         mfma(f0);
         mfma(f1);
+        bool h1_done = false;
         if (kt < 0) {
 #else
+        GM_STAMP(kt, 0);
         read(ST, I1{}, f1);
         __builtin_amdgcn_sched_barrier(0);
         if constexpr (SPLIT_NEXT) {
@@ -1839,19 +1875,34 @@ __global__ __launch_bounds__(WGM* WGN * 64, OCC) void k_gemm3g(ASrc a0, ASrc a1,
         else
             mfma(f0);
         __builtin_amdgcn_sched_barrier(0);
+        GM_STAMP(kt, 1);
+        bool h1_done = false;
         if (kt + 1 < nk) {
 #endif
             // own DMA of tile kt+1 landed (tiles kt+2 .. kt+STAGES-1 may stay in flight)
             wait_landed(min(STAGES - 2, nk - 2 - kt));
+            GM_STAMP(kt, 2);
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's reads of tile kt done
             __builtin_amdgcn_s_barrier();
             asm volatile("" ::: "memory");  // no LDS access moves across the barrier
+            GM_STAMP(kt, 3);
+            if constexpr (ORDER) {
+                if (late) {  // second-half MFMAs first (they read only registers)
+                    __builtin_amdgcn_sched_barrier(0);
+                    mfma16(f1, I1{}, I0{}, std::integral_constant<int, TN>{});
+                    __builtin_amdgcn_sched_barrier(0);
+                    h1_done = true;
+                }
+            }
             if (kt + STAGES < nk) issue(ST, kt + STAGES);
+            GM_STAMP(kt, 4);
             if (ragged && kt + 1 == nk - 1) zero_tail(SN{});
             read(SN{}, I0{}, f0);
         }
+        GM_STAMP(kt, 5);
         __builtin_amdgcn_sched_barrier(0);
-        if constexpr (SPLIT_NEXT) {  // split of tile kt + 1 (f0, just read) between these MFMAs
+        if (ORDER && h1_done) {
+        } else if constexpr (SPLIT_NEXT) {  // split of tile kt + 1 (f0, just read) between these MFMAs
             if constexpr (S == 0)
                 mfma16n(f1, I1{}, sah, sal, f0, sah2, sal2, std::true_type{});
             else
@@ -1860,6 +1911,7 @@ __global__ __launch_bounds__(WGM* WGN * 64, OCC) void k_gemm3g(ASrc a0, ASrc a1,
             mfma16(f1, I1{}, I0{}, std::integral_constant<int, TN>{});
         else
             mfma(f1);
+        GM_STAMP(kt, 6);
     };
 #if GM_PRIO
     if constexpr (NW == 8)
@@ -1879,6 +1931,10 @@ __global__ __launch_bounds__(WGM* WGN * 64, OCC) void k_gemm3g(ASrc a0, ASrc a1,
 
 #if GM_PRIO
     __builtin_amdgcn_s_setprio(0);
+#endif
+#if GM_DIAG == 30
+    if (stw && g_stamps && blockIdx.x < 4096)
+        for (int i = 0; i < 64; i++) g_stamps[((size_t)blockIdx.x * 2 + (wave != 0)) * 64 + i] = stl[(wave != 0) * 64 + i];
 #endif
     if constexpr (AX == 1) {
         amx = gm_wave_max(amx);
@@ -1996,10 +2052,12 @@ int launch(const ASrc& a0, const ASrc& a1, const float* w, long long ldw, unsign
 int epi_act(int epilogue) {
     if (epilogue == GM_EPI_BIAS_LEAKY) return GM_ACT_LEAKY_RELU;
     if (epilogue >= GM_EPI_BIAS_RELU && epilogue <= GM_EPI_BIAS_SIGMOID) return GM_ACT_RELU + (epilogue - GM_EPI_BIAS_RELU);
+    if (epilogue >= GM_EPI_BIAS_ACT && epilogue <= GM_EPI_BIAS_ACT + GM_ACT_LAST) return epilogue - GM_EPI_BIAS_ACT;
     return GM_ACT_NONE;
 }
 bool is_bias_epi(int e) {
-    return e == GM_EPI_BIAS || e == GM_EPI_BIAS_LEAKY || (e >= GM_EPI_BIAS_RELU && e <= GM_EPI_BIAS_SIGMOID);
+    return e == GM_EPI_BIAS || e == GM_EPI_BIAS_LEAKY || (e >= GM_EPI_BIAS_RELU && e <= GM_EPI_BIAS_SIGMOID) ||
+           (e >= GM_EPI_BIAS_ACT && e <= GM_EPI_BIAS_ACT + GM_ACT_LAST);
 }
 
 int g_tile = -1;  // tile configuration override (gm_gemm_set_tile), -1 = per-shape default
@@ -2416,8 +2474,8 @@ extern "C" int gm_dqn_x3(const gm_a_src* a0, const gm_a_src* a1, const void* w1p
                          int32_t n1, int32_t n2, const float* wq, int64_t ldwq, const float* bq, int32_t nq, float* q,
                          int64_t ldq, void* stream) {
     if (!a0 || !w1p || !w1sinv || !b1 || !w2p || !w2sinv || !b2 || !wq || !q || m <= 0 || n1 != 512 || n2 != 256 ||
-        nq <= 0 || nq > 4 || ldwq < n2 || ldq < nq || act1 < GM_ACT_NONE || act1 > GM_ACT_SIGMOID ||
-        act2 < GM_ACT_NONE || act2 > GM_ACT_SIGMOID || (reinterpret_cast<uintptr_t>(w1p) & 15) ||
+        nq <= 0 || nq > 4 || ldwq < n2 || ldq < nq || act1 < GM_ACT_NONE || act1 > GM_ACT_LAST ||
+        act2 < GM_ACT_NONE || act2 > GM_ACT_LAST || (reinterpret_cast<uintptr_t>(w1p) & 15) ||
         (reinterpret_cast<uintptr_t>(w2p) & 15))
         return gm_fail(GM_ERR_INVALID_ARG, "gm_dqn_x3: bad arguments (layers 512, 256 wide, nq <= 4)");
     ASrc s0, s1;
@@ -2461,7 +2519,7 @@ extern "C" int gm_gemm_x3_head(const gm_a_src* a0, const void* wp, const float* 
                                int32_t m, int32_t n, int32_t act, const float* wq, int64_t ldwq, const float* bq,
                                int32_t nq, float* q, int64_t ldq, float* y, int64_t ldy, void* stream) {
     if (!a0 || a0->mode != GM_A_DENSE || !wp || !wscale_inv || !wq || !q || m <= 0 || n <= 0 || n > 256 ||
-        nq <= 0 || nq > 4 || ldwq < n || ldq < nq || (y && ldy < n) || act < GM_ACT_NONE || act > GM_ACT_SIGMOID ||
+        nq <= 0 || nq > 4 || ldwq < n || ldq < nq || (y && ldy < n) || act < GM_ACT_NONE || act > GM_ACT_LAST ||
         (reinterpret_cast<uintptr_t>(wp) & 15))
         return gm_fail(GM_ERR_INVALID_ARG, "gm_gemm_x3_head: bad arguments (dense source, n <= 256, nq <= 4)");
     ASrc s0, s1;
@@ -3030,7 +3088,7 @@ extern "C" int gm_gemm_set_tile(int32_t tile) {
 
 extern "C" int gm_linear_f32(const float* x, int64_t ldx, const float* w, int64_t ldw, const float* b, int32_t m,
                              int32_t n, int32_t k, int32_t act, float* y, int64_t ldy, void* stream) {
-    if (!x || !w || !y || act < GM_ACT_NONE || act > GM_ACT_SIGMOID)
+    if (!x || !w || !y || act < GM_ACT_NONE || act > GM_ACT_LAST)
         return gm_fail(GM_ERR_INVALID_ARG, "gm_linear_f32: bad arguments");
     gm_a_src a;
     memset(&a, 0, sizeof(a));
@@ -3038,6 +3096,6 @@ extern "C" int gm_linear_f32(const float* x, int64_t ldx, const float* w, int64_
     a.p0 = x;
     a.ld0 = ldx;
     a.k = k;
-    return gm_gemm_f32(&a, nullptr, w, ldw, b, m, n, act == GM_ACT_NONE ? GM_EPI_BIAS : act == GM_ACT_LEAKY_RELU ? GM_EPI_BIAS_LEAKY : GM_EPI_BIAS_RELU + (act - GM_ACT_RELU), y, ldy, nullptr, 0,
+    return gm_gemm_f32(&a, nullptr, w, ldw, b, m, n, act == GM_ACT_NONE ? GM_EPI_BIAS : act == GM_ACT_LEAKY_RELU ? GM_EPI_BIAS_LEAKY : GM_EPI_BIAS_ACT + act, y, ldy, nullptr, 0,
                        nullptr, 0, nullptr, stream);
 }

@@ -449,8 +449,8 @@ static int launch_agg(const float* h, const int32_t* nbr, int32_t G, int32_t N, 
 // act < 0: leaky_relu with the given slope; else GM_ACT_* (derivative from the output, gm_act.hpp)
 __global__ __launch_bounds__(256) void k_leaky_bwd(const float* __restrict__ gy, const float* __restrict__ y,
                                                    long long rows, int cols, int rows_per_block, float slope,
-                                                   int act, float* __restrict__ g, float* __restrict__ part,
-                                                   unsigned* __restrict__ amax) {
+                                                   int act, int fromz, float* __restrict__ g,
+                                                   float* __restrict__ part, unsigned* __restrict__ amax) {
     const long long r0 = (long long)blockIdx.x * rows_per_block;
     const long long r1 = min(rows, r0 + rows_per_block);
     float m = 0.f;
@@ -458,8 +458,9 @@ __global__ __launch_bounds__(256) void k_leaky_bwd(const float* __restrict__ gy,
         float acc = 0.f;
         for (long long r = r0; r < r1; r++) {
             const long long i = r * cols + c;
-            const float v = act < 0 ? (y[i] > 0.f ? gy[i] : slope * gy[i])  // torch: input > 0 ? g : slope g
-                                    : gy[i] * gm_act_dy(y[i], act);
+            // torch: input > 0 ? g : slope g; fromz: y holds the pre-activation z (gm_act_bwd_z)
+            const float v = act < 0 ? (y[i] > 0.f ? gy[i] : slope * gy[i])
+                                    : gy[i] * (fromz ? gm_act_dz(y[i], act) : gm_act_dy(y[i], act));
             g[i] = v;
             acc += v;
             m = fmaxf(m, fabsf(v));
@@ -470,7 +471,7 @@ __global__ __launch_bounds__(256) void k_leaky_bwd(const float* __restrict__ gy,
 }
 
 static int act_bwd(const char* fn, const float* gy, const float* y, int64_t rows, int32_t cols, float slope, int act,
-                   float* g, float* part, int32_t rows_per_block, float* g_scale, void* stream) {
+                   float* g, float* part, int32_t rows_per_block, float* g_scale, void* stream, int fromz = 0) {
     if (!gy || !y || !g || !part || rows <= 0 || cols <= 0 || rows_per_block <= 0)
         return gm_fail(GM_ERR_INVALID_ARG, std::string(fn) + ": bad arguments");
     hipStream_t st = (hipStream_t)stream;
@@ -478,7 +479,7 @@ static int act_bwd(const char* fn, const float* gy, const float* y, int64_t rows
         return gm_fail(GM_ERR_HIP, std::string(fn) + ": memset");
     const long long nb = (rows + rows_per_block - 1) / rows_per_block;
     hipLaunchKernelGGL(k_leaky_bwd, dim3((unsigned)nb), dim3(256), 0, st, gy, y, (long long)rows, (int)cols,
-                       (int)rows_per_block, slope, act, g, part, reinterpret_cast<unsigned*>(g_scale));
+                       (int)rows_per_block, slope, act, fromz, g, part, reinterpret_cast<unsigned*>(g_scale));
     int rc = launched();
     if (rc == GM_OK && g_scale) rc = gm_absmax_finish(g_scale, stream);
     return rc;
@@ -491,8 +492,31 @@ extern "C" int gm_leaky_bwd(const float* gy, const float* y, int64_t rows, int32
 
 extern "C" int gm_act_bwd(const float* gy, const float* y, int64_t rows, int32_t cols, int32_t act, float* g,
                           float* part, int32_t rows_per_block, float* g_scale, void* stream) {
-    if (act < GM_ACT_NONE || act > GM_ACT_SIGMOID) return gm_fail(GM_ERR_INVALID_ARG, "gm_act_bwd: unknown act");
+    if (act < GM_ACT_NONE || act > GM_ACT_SOFTPLUS)
+        return gm_fail(GM_ERR_INVALID_ARG, "gm_act_bwd: unknown act (codes >= GM_ACT_GELU: gm_act_bwd_z)");
     return act_bwd("gm_act_bwd", gy, y, rows, cols, 0.f, act, g, part, rows_per_block, g_scale, stream);
+}
+
+extern "C" int gm_act_bwd_z(const float* gy, const float* z, int64_t rows, int32_t cols, int32_t act, float* g,
+                            float* part, int32_t rows_per_block, float* g_scale, void* stream) {
+    if (act < GM_ACT_NONE || act > GM_ACT_LAST) return gm_fail(GM_ERR_INVALID_ARG, "gm_act_bwd_z: unknown act");
+    return act_bwd("gm_act_bwd_z", gy, z, rows, cols, 0.f, act, g, part, rows_per_block, g_scale, stream, 1);
+}
+
+// y = act(z) elementwise (the training forward of the activations whose derivative needs z)
+__global__ __launch_bounds__(256) void k_act_fwd(const float* __restrict__ z, long long n, int act, float* __restrict__ y) {
+    for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x)
+        y[i] = gm_act(z[i], act);
+}
+
+extern "C" int gm_act_fwd(const float* z, int64_t rows, int32_t cols, int32_t act, float* y, void* stream) {
+    if (!z || !y || rows <= 0 || cols <= 0 || act < GM_ACT_NONE || act > GM_ACT_LAST)
+        return gm_fail(GM_ERR_INVALID_ARG, "gm_act_fwd: bad arguments");
+    const long long n = (long long)rows * cols;
+    long long nb = (n + 255) / 256;
+    if (nb > 65536) nb = 65536;
+    hipLaunchKernelGGL(k_act_fwd, dim3((unsigned)nb), dim3(256), 0, (hipStream_t)stream, z, n, (int)act, y);
+    return launched();
 }
 
 extern "C" int gm_mp_aggregate(const float* h, const int32_t* nbr, int32_t G, int32_t N, int32_t deg, int32_t H,
@@ -1292,7 +1316,7 @@ extern "C" int gm_routing_node_encoder(const float* x, int64_t ldx, const int32_
 extern "C" int gm_routing_node_encoder_bits(const float* x, int64_t ldx, const int32_t* nbr, int32_t G, int32_t N,
                                             const float* wt, const float* b, int32_t n, int32_t act, float* y,
                                             int64_t ldy, uint32_t* sbits, int64_t ldsb, void* stream) {
-    if (!x || !nbr || !wt || !y || G <= 0 || N < 4 || n <= 0 || (n % 64) || act < GM_ACT_NONE || act > GM_ACT_SIGMOID ||
+    if (!x || !nbr || !wt || !y || G <= 0 || N < 4 || n <= 0 || (n % 64) || act < GM_ACT_NONE || act > GM_ACT_LAST ||
         ldx < 4 * N + 8 || ldy < n || (ldy % 2) || (reinterpret_cast<uintptr_t>(wt) & 15) ||
         (sbits && ldsb < n / 32))
         return gm_fail(GM_ERR_INVALID_ARG, "gm_routing_node_encoder: bad arguments (n % 64 == 0, 16-byte W^T)");

@@ -404,15 +404,17 @@ def routing_encoder_ok(lin, N, Fd, nbr):
             (4 * N + 8) * 64 * (2 if lin.out_features % 128 == 0 and (4 * N + 8) <= 128 else 1) * 4 <= 65536)
 
 
-def routing_encoder(lin, x, nbr, G, N, out, sbits=None):
+def routing_encoder(lin, x, nbr, G, N, out, sbits=None, act=None):
     """y = act(W x + b) on routing node observations from their nonzero entries; sbits (optional,
-    int32 [rows][ceil(n / 32)]) receives the sign bits of y (the training backward's leaky mask)."""
+    int32 [rows][ceil(n / 32)]) receives the sign bits of y (the training backward's leaky mask);
+    act overrides lin.act (0: the pre-activation)."""
     if not hasattr(lin, "_packed_t"):
         lin._packed_t = Packed()
     wt = lin._packed_t.get(_key(lin.weight), lambda: lin.weight.detach().t().contiguous())
     with L.timed(lin.tag and f"routing_enc:{lin.tag}:{G * N}x{lin.out_features}"):
         L.check(L.lib().gm_routing_node_encoder_bits(L.ptr(x), x.stride(0), L.ptr(nbr), G, N, L.ptr(wt),
-                                                     L.ptr(lin.bias), lin.out_features, lin.act, L.ptr(out),
+                                                     L.ptr(lin.bias), lin.out_features,
+                                                     lin.act if act is None else act, L.ptr(out),
                                                      out.stride(0), L.ptr(sbits),
                                                      0 if sbits is None else sbits.stride(0), L.stream_ptr()))
     return out

@@ -19,7 +19,9 @@ Differences from the reference, by design:
     consumes exactly the reference's numpy stream); one update per vector step;
   * no tensorboard: the log lines go to stdout and checkpoints / eval metrics to
     --log-dir (default runs/<date>_<host><comment>, like SummaryWriter's logdir);
-  * models: dqn, dgn, dqnr, commnet (comm_rounds 2); activation: leaky_relu, relu, elu, tanh, sigmoid;
+  * models: dqn, dgn, dqnr, commnet (comm_rounds 2); activation: any elementwise torch.nn.functional name
+    (model.ACTIVATIONS: leaky_relu, relu, elu, tanh, sigmoid, relu6, hardtanh, hardsigmoid, selu, celu,
+    softsign, logsigmoid, softplus, gelu, silu, mish, hardswish, tanhshrink);
     NetMon: sum/mean aggregation, lstm/lnlstm/gru cells, carry-over on, --netmon-global;
   * data parallel over the GPUs of a node: launched by torch.distributed.run (WORLD_SIZE > 1), each
     rank steps its own --n-env envs (disjoint seeds: --seed + rank * n_env + b), keeps its own replay

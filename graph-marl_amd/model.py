@@ -22,18 +22,27 @@ from . import _lib as L
 
 SUM, MEAN = 0, 1
 
-# --activation-function (src/main.py:194-197, 440-441): the torch.nn.functional names the kernels
-# build (GM_ACT_* in include/graph_marl_amd.h; derivative from the layer output)
-ACTIVATIONS = {"leaky_relu": 1, "relu": 2, "elu": 3, "tanh": 4, "sigmoid": 5}
-# bias + activation epilogue code of gm_gemm_x3 / gm_gemm_f32 per activation code
+# --activation-function (src/main.py:194-197, 440-441: getattr(F, name), applied with its default
+# arguments): the elementwise torch.nn.functional names, GM_ACT_* in include/graph_marl_amd.h. Codes up
+# to softplus have a derivative that follows from the layer output; Z_ACTS need the pre-activation
+# (their training forward keeps z and applies the activation with gm_act_fwd)
+ACTIVATIONS = {"leaky_relu": 1, "relu": 2, "elu": 3, "tanh": 4, "sigmoid": 5, "relu6": 6, "hardtanh": 7,
+               "hardsigmoid": 8, "selu": 9, "celu": 10, "softsign": 11, "logsigmoid": 12, "softplus": 13,
+               "gelu": 14, "silu": 15, "mish": 16, "hardswish": 17, "tanhshrink": 18}
+Z_ACTS = frozenset(range(14, 19))
+# bias + activation epilogue code of gm_gemm_x3 / gm_gemm_f32 per activation code (GM_EPI_BIAS_ACT + act
+# beyond the four named epilogues)
 _EPI_OF_ACT = {0: 0, 1: 1, 2: 4, 3: 5, 4: 6, 5: 7}
+GM_EPI_BIAS_ACT = 64
 
 
 def act_code(activation):
-    """GM_ACT_* code of an activation given by torch.nn.functional name (or function)."""
+    """GM_ACT_* code of an activation given by torch.nn.functional name (or function). Names that are
+    not elementwise with default arguments (softmax, glu, rrelu's random slopes, ..) are refused."""
     if activation is None:
         return 0
     name = activation if isinstance(activation, str) else getattr(activation, "__name__", str(activation))
+    name = {"log_sigmoid": "logsigmoid"}.get(name, name)  # F.logsigmoid.__name__
     if name not in ACTIVATIONS:
         raise NotImplementedError(f"--activation-function {name!r} is not built; the kernels provide "
                                   f"{', '.join(sorted(ACTIVATIONS))}")
@@ -41,8 +50,15 @@ def act_code(activation):
 
 
 def epi_code(act):
-    """gm_gemm epilogue code (GM_EPI_BIAS / GM_EPI_BIAS_<ACT>) of an activation code."""
-    return _EPI_OF_ACT[act]
+    """gm_gemm epilogue code (GM_EPI_BIAS / GM_EPI_BIAS_<ACT> / GM_EPI_BIAS_ACT + act) of an activation code."""
+    return _EPI_OF_ACT.get(act, GM_EPI_BIAS_ACT + act)
+
+
+def act_fwd(z, act):
+    """y = act(z) elementwise on the device (gm_act_fwd), z [rows, cols] contiguous."""
+    y = torch.empty_like(z)
+    L.check(L.lib().gm_act_fwd(z.data_ptr(), z.shape[0], z.shape[1], act, y.data_ptr(), _s()))
+    return y
 
 
 def _s():
@@ -226,11 +242,15 @@ class LinearFn(torch.autograd.Function):
     def forward(ctx, x, w, b, act, wcache, tag=None):
         x2, ldx, k = _as_rows(x)
         xs = _amax_slot(x2, ldx, w.shape[0], ctx.needs_input_grad[1])
-        y = linear_raw(x2, ldx, k, w, b, act, wcache=wcache, tag=tag, amax=xs)
+        zact = act in Z_ACTS and any(ctx.needs_input_grad[:3])
+        y = linear_raw(x2, ldx, k, w, b, 0 if zact else act, wcache=wcache, tag=tag, amax=xs)
+        keep = y  # the layer output, or for Z_ACTS the pre-activation z (_act_grad)
+        if zact:
+            y = act_fwd(keep, act)
         ctx.xs = None if xs is None else _finish_scale(xs)
         ctx.act = act
         ctx.wcache = wcache
-        ctx.save_for_backward(x2[:, :k] if x2.shape[1] != k else x2, w, y)
+        ctx.save_for_backward(x2[:, :k] if x2.shape[1] != k else x2, w, keep)
         return y.reshape(*x.shape[:-1], w.shape[0])
 
     @staticmethod
@@ -244,19 +264,20 @@ class LinearFn(torch.autograd.Function):
 
 def _act_grad(act, gy, y, need_b, want_scale):
     """Backward through the layer activation: (g, bias gradient or None, gradient scale or None).
-    relu / elu / tanh / sigmoid: one fused pass (gm_act_bwd). leaky_relu at training sizes: one fused pass (gm_leaky_bwd: mask, per-block bias partials,
-    max|g| for the gradient GEMMs' operand scale)."""
+    y is the layer output, or for Z_ACTS the pre-activation z. relu / elu / tanh / sigmoid / ..: one
+    fused pass (gm_act_bwd, derivative from y; gm_act_bwd_z from z). leaky_relu at training sizes: one
+    fused pass (gm_leaky_bwd: mask, per-block bias partials, max|g| for the gradient GEMMs' operand scale)."""
     gb = sc = None
     if act > 1:
-        # relu / elu / tanh / sigmoid: derivative from the output (gm_act_bwd), any row count
+        # derivative from the output (gm_act_bwd) or the pre-activation (gm_act_bwd_z), any row count
         gy, y = gy.contiguous(), y.contiguous()  # e.g. the slice of a torch.cat's gradient
         rows, cols = gy.shape
         rpb = 64
         g2 = torch.empty_like(gy)
         part = torch.empty((rows + rpb - 1) // rpb, cols, device=gy.device)
         sc = torch.empty(1, device=gy.device) if want_scale and rows >= 4096 else None
-        L.check(L.lib().gm_act_bwd(gy.data_ptr(), y.data_ptr(), rows, cols, act, g2.data_ptr(), part.data_ptr(), rpb,
-                                   L.ptr(sc), _s()))
+        fn = L.lib().gm_act_bwd_z if act in Z_ACTS else L.lib().gm_act_bwd
+        L.check(fn(gy.data_ptr(), y.data_ptr(), rows, cols, act, g2.data_ptr(), part.data_ptr(), rpb, L.ptr(sc), _s()))
         gy = g2
         if need_b:
             gb = part.sum(0)
@@ -319,17 +340,18 @@ class _JointLinearFn(torch.autograd.Function):
         wp, ldw, bp, x3 = FU.pack_dqn_first(lin, od)
         xs = torch.zeros(1, device=graph.device) if ctx.needs_input_grad[2] else None
         y = torch.empty(R, w.shape[0], device=graph.device)
+        zact = lin.act in Z_ACTS
         FU.gemm(FU.dense(graph.data_ptr(), G, G, amax=None if xs is None else xs.data_ptr()),
                 FU.dense(env_obs.data_ptr(), env_obs.stride(0), od), wp.data_ptr(), ldw, bp.data_ptr(), R, w.shape[0],
-                epi_code(lin.act), y.data_ptr(), w.shape[0],
+                epi_code(0 if zact else lin.act), y.data_ptr(), w.shape[0],
                 tag=lin.tag and f"linear:{lin.tag}:{R}x{w.shape[0]}x{G}+{od}", x3=x3)
         ctx.xs = None if xs is None else _finish_scale(xs)
         ctx.act = lin.act
         if not hasattr(lin, "_wc_graph"):
             lin._wc_graph = _WeightCache()
         ctx.wcache_graph = lin._wc_graph
-        ctx.save_for_backward(graph, env_obs, w, y)
-        return y
+        ctx.save_for_backward(graph, env_obs, w, y)  # Z_ACTS: y holds z (_act_grad)
+        return act_fwd(y, lin.act) if zact else y
 
     @staticmethod
     def backward(ctx, gy):
@@ -363,10 +385,11 @@ class _RoutingEncFn(torch.autograd.Function):
         from . import fused as FU
 
         y = torch.empty(x.shape[0], w.shape[0], device=x.device)
-        FU.routing_encoder(lin, x, nbr, G, N, y)
+        zact = lin.act in Z_ACTS
+        FU.routing_encoder(lin, x, nbr, G, N, y, act=0 if zact else None)
         ctx.act, ctx.wcache, ctx.xs = lin.act, lin._wc, None
-        ctx.save_for_backward(x, w, y)
-        return y
+        ctx.save_for_backward(x, w, y)  # Z_ACTS: y holds z (_act_grad)
+        return act_fwd(y, lin.act) if zact else y
 
     @staticmethod
     def backward(ctx, gy):

@@ -250,6 +250,13 @@ int gm_leaky_bwd(const float* dy, const float* y, int64_t rows, int32_t cols, fl
  * activation_fn, src/model.py:13-42). */
 int gm_act_bwd(const float* dy, const float* y, int64_t rows, int32_t cols, int32_t act, float* g, float* part,
                int32_t rows_per_block, float* g_scale, void* stream);
+/* Activations whose derivative needs the pre-activation z (GM_ACT_GELU.., torch autograd of the
+ * reference's activation_fn, src/model.py:13-42): y = act(z) elementwise ([rows][cols] contiguous),
+ * and the backward g = dY * act'(z) with the per-block column sums and g_scale of gm_act_bwd. Both take
+ * every GM_ACT_* code. */
+int gm_act_fwd(const float* z, int64_t rows, int32_t cols, int32_t act, float* y, void* stream);
+int gm_act_bwd_z(const float* dy, const float* z, int64_t rows, int32_t cols, int32_t act, float* g, float* part,
+                 int32_t rows_per_block, float* g_scale, void* stream);
 /* Backward of gm_mp_aggregate for symmetric adjacency: dh[j] = Σ_{n ∈ {j} ∪ nbr(j)} dout[n] / cnt(n). */
 int gm_mp_aggregate_bwd(const float* dout, const int32_t* nbr, int32_t n_graphs, int32_t n_nodes, int32_t deg,
                         int32_t hidden, int32_t mode, float* dh, void* stream);
@@ -329,11 +336,17 @@ int gm_linear_f32(const float* x, int64_t ldx, const float* w, int64_t ldw, cons
  * agent gather (582-631) folded into the A-operand load. */
 enum { GM_A_DENSE = 0, GM_A_AGGREGATE = 1, GM_A_READOUT = 2 };
 enum { GM_EPI_BIAS = 0, GM_EPI_BIAS_LEAKY = 1, GM_EPI_LSTM = 2, GM_EPI_GRU = 3, GM_EPI_BIAS_RELU = 4,
-       GM_EPI_BIAS_ELU = 5, GM_EPI_BIAS_TANH = 6, GM_EPI_BIAS_SIGMOID = 7 };
-/* Layer activations (--activation-function, src/main.py:194-197, 440-441; MLP / AttModel,
- * src/model.py:13-42, 86-117): the torch.nn.functional names whose derivative follows from the
- * layer output. GM_EPI_BIAS_<ACT> = bias + activation epilogue; act arguments take GM_ACT_*. */
-enum { GM_ACT_NONE = 0, GM_ACT_LEAKY_RELU = 1, GM_ACT_RELU = 2, GM_ACT_ELU = 3, GM_ACT_TANH = 4, GM_ACT_SIGMOID = 5 };
+       GM_EPI_BIAS_ELU = 5, GM_EPI_BIAS_TANH = 6, GM_EPI_BIAS_SIGMOID = 7, GM_EPI_BIAS_ACT = 64 };
+/* Layer activations (--activation-function = any elementwise torch.nn.functional name with its
+ * defaults, src/main.py:194-197, 440-441; MLP / AttModel, src/model.py:13-42, 86-117). Codes
+ * 1..GM_ACT_SOFTPLUS have a derivative that follows from the layer output y (the training backward
+ * keeps y); codes GM_ACT_GELU.. need the pre-activation z (the training forward keeps z and applies
+ * the activation with gm_act_fwd). GM_EPI_BIAS_<ACT> (4..7) or GM_EPI_BIAS_ACT + act (any code) =
+ * bias + activation epilogue; act arguments take GM_ACT_*. */
+enum { GM_ACT_NONE = 0, GM_ACT_LEAKY_RELU = 1, GM_ACT_RELU = 2, GM_ACT_ELU = 3, GM_ACT_TANH = 4, GM_ACT_SIGMOID = 5,
+       GM_ACT_RELU6 = 6, GM_ACT_HARDTANH = 7, GM_ACT_HARDSIGMOID = 8, GM_ACT_SELU = 9, GM_ACT_CELU = 10,
+       GM_ACT_SOFTSIGN = 11, GM_ACT_LOGSIGMOID = 12, GM_ACT_SOFTPLUS = 13, GM_ACT_GELU = 14, GM_ACT_SILU = 15,
+       GM_ACT_MISH = 16, GM_ACT_HARDSWISH = 17, GM_ACT_TANHSHRINK = 18, GM_ACT_LAST = 18 };
 typedef struct {
     int32_t mode;              /* GM_A_*                                                           */
     const float* p0;           /* DENSE: rows; AGGREGATE: node rows h; READOUT: h_final node rows  */

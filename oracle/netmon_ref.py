@@ -32,6 +32,36 @@ def activation(x, name="leaky_relu"):
         return np.tanh(x)
     if name == "sigmoid":
         return sigmoid(x)
+    # the rest of the elementwise torch.nn.functional names with their defaults (round 4)
+    sp = lambda v: np.where(v > 20.0, v, np.log1p(np.exp(np.minimum(v, 20.0))))  # softplus, threshold 20
+    if name == "relu6":
+        return np.clip(x, 0.0, 6.0)
+    if name == "hardtanh":
+        return np.clip(x, -1.0, 1.0)
+    if name == "hardsigmoid":
+        return np.clip(x + 3.0, 0.0, 6.0) / 6.0
+    if name == "selu":
+        a, s = 1.6732632423543772848170429916717, 1.0507009873554804934193349852946
+        return s * np.where(x > 0, x, a * np.expm1(np.minimum(x, 0.0)))
+    if name == "celu":
+        return np.where(x > 0, x, np.expm1(np.minimum(x, 0.0)))
+    if name == "softsign":
+        return x / (1.0 + np.abs(x))
+    if name == "logsigmoid":
+        return np.minimum(x, 0.0) - np.log1p(np.exp(-np.abs(x)))
+    if name == "softplus":
+        return sp(x)
+    if name == "gelu":
+        from scipy.special import erf
+        return 0.5 * x * (1.0 + erf(x / np.sqrt(2.0)))
+    if name == "silu":
+        return x * sigmoid(x)
+    if name == "mish":
+        return x * np.tanh(sp(x))
+    if name == "hardswish":
+        return x * np.clip(x + 3.0, 0.0, 6.0) / 6.0
+    if name == "tanhshrink":
+        return x - np.tanh(x)
     raise ValueError(f"activation {name!r} not restated")
 
 

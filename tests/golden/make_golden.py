@@ -1048,7 +1048,9 @@ def main():
         # per batched layer (>= 32 768: the LDS-DMA k_gemm3g forms of the sequence-batched update)
         gen_train(os.path.join(HERE, "train_prod.npz"), Network, Routing, EVAL_SEEDS, NetMon, DQN, interpolate_model,
                   H=128, enc=(512, 256), dqn_hidden=(512, 256), B=512, L=4, compact=True, det_seed=23)
-    for act in ("relu", "elu", "tanh", "sigmoid"):  # --activation-function (src/main.py:194-197, 440-441)
+    # --activation-function (src/main.py:194-197, 440-441); softplus: derivative from the output, gelu / silu /
+    # mish: from the pre-activation (round 4)
+    for act in ("relu", "elu", "tanh", "sigmoid", "softplus", "gelu", "silu", "mish"):
         if only is None or f"train_{act}" in only:
             gen_train(os.path.join(HERE, f"train_{act}.npz"), Network, Routing, EVAL_SEEDS, NetMon, DQN,
                       interpolate_model, K=2, B=4, act=act)

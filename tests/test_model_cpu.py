@@ -89,3 +89,23 @@ def test_fold_env_weight_exact_on_routing_rows():
         wf = FU.fold_env_weight(w, n)
         assert wf.shape == (16, D - 2)
         torch.testing.assert_close(x @ w.t(), x[:, keep] @ wf.t(), rtol=1e-12, atol=1e-12)
+
+
+def test_activation_names_cover_the_elementwise_functionals():
+    """--activation-function takes any elementwise torch.nn.functional name (src/main.py:440-441
+    getattr(F, name)); each code maps to a GEMM epilogue, the pre-activation ones are flagged; names
+    that are not elementwise with defaults are refused."""
+    import importlib
+
+    import pytest
+    import torch.nn.functional as F
+
+    M = importlib.import_module("graph-marl_amd.model")
+    for name, code in M.ACTIVATIONS.items():
+        assert hasattr(F, name) and M.act_code(name) == code and M.act_code(getattr(F, name)) == code
+        assert M.epi_code(code) in (0, 1, 4, 5, 6, 7) or M.epi_code(code) == M.GM_EPI_BIAS_ACT + code
+    assert {n for n, c in M.ACTIVATIONS.items() if c in M.Z_ACTS} == {"gelu", "silu", "mish", "hardswish", "tanhshrink"}
+    assert len(set(M.ACTIVATIONS.values())) == len(M.ACTIVATIONS) == 18
+    for bad in ("softmax", "glu", "rrelu"):
+        with pytest.raises(NotImplementedError):
+            M.act_code(bad)

@@ -143,7 +143,8 @@ def test_oracle_bench_driver_runs(oracle_mod):
 
 
 @pytest.mark.parametrize("name", ["train.npz", "train_big.npz", "train_prod.npz", "train_lnlstm.npz", "train_gru.npz", "train_relu.npz",
-                                  "train_elu.npz", "train_tanh.npz", "train_sigmoid.npz"])
+                                  "train_elu.npz", "train_tanh.npz", "train_sigmoid.npz",
+                                  "train_softplus.npz", "train_gelu.npz", "train_silu.npz", "train_mish.npz"])
 def test_train_golden_forward_matches_restatement(name):
     """The golden DQN+NetMon updates' Q / Q-target / loss follow from their weights (stored, or for
     the compact production-size golden regenerated by tests/golden/detparams.py) through the fp64

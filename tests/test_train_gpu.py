@@ -45,7 +45,9 @@ def golden_batches(g, M, RB, dev, state0):
 # (src/main.py:194-197, 440-441) through every MLP layer (GEMM epilogues, gm_act_bwd)
 # train_prod: the same architecture at 512 graphs x 4 steps (10 240 rows per step)
 GOLDENS = ["train.npz", "train_aux.npz", "train_big.npz", "train_prod.npz", "train_lnlstm.npz", "train_gru.npz", "train_relu.npz",
-           "train_elu.npz", "train_tanh.npz", "train_sigmoid.npz"]
+           "train_elu.npz", "train_tanh.npz", "train_sigmoid.npz",
+           # round 4: softplus (derivative from the output), gelu / silu / mish (from the pre-activation)
+           "train_softplus.npz", "train_gelu.npz", "train_silu.npz", "train_mish.npz"]
 
 
 @pytest.mark.parametrize("name", GOLDENS)
