@@ -288,7 +288,8 @@ def main(argv=None):
 def _main(args, rank, world):
     lead = rank == 0
     log_print = print if lead else (lambda *a, **k: None)
-    args.capacity = min(args.total_steps, args.capacity)
+    # src/main.py: no more capacity than transitions; with --n-env envs a step stores n_env of them
+    args.capacity = min(args.total_steps * args.n_env, args.capacity)
     if args.model_load_path and not args.model_load_no_args:
         assert os.path.exists(args.model_load_path)
         loaded = load_checkpoint(args.model_load_path)

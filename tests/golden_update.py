@@ -82,6 +82,16 @@ def weights_np(g):
     return sd(netmon), sd(model), sd(target), state0.double().numpy()
 
 
+def count_excess(g, key, actual, atol):
+    """(elements off by more than atol, elements compared) of actual vs the golden `key` (every
+    element, or a compact entry's sampled positions)."""
+    a = (actual.detach().cpu().numpy() if torch.is_tensor(actual) else np.asarray(actual)).astype(np.float64)
+    if key in g.files:
+        return int((np.abs(a - g[key]) > atol).sum()), a.size
+    idx = g[key + "__idx"]
+    return int((np.abs(a.reshape(-1)[idx] - g[key + "__val"]) > atol).sum()), len(idx)
+
+
 def check(g, key, actual, atol, rtol, what=""):
     """actual (tensor / array) vs the golden array `key`, elementwise |a - r| <= atol + rtol |r|;
     for a compact entry at its sampled positions, and its row / column sums within the bound the

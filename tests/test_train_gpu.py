@@ -101,24 +101,25 @@ def check_update(g, names, params, opt, model, target, T):
         np.testing.assert_allclose(norm.item(), float(g["clip_total_norm"]), rtol=1e-4)
     for n, p in zip(names, params):
         GU.check(g, "grad_clip_" + n, p.grad, 1e-5, 1e-4)
-    # the first AdamW step moves a parameter by lr g / (|g| + eps): where |g| is near eps = 1e-8 it
-    # amplifies the gradient's own tolerance (1e-5 + 1e-4 |g|) by lr eps / (|g| + eps)^2, so those
-    # elements get that much more room (capped at 2 lr) -- only where the gradient itself is below the
-    # gradient check's atol (1e-5), i.e. where the check above cannot pin its sign; everywhere else 1e-6.
-    # The relaxed elements must stay few (< 1 % of the nonzero gradients)
+    # the first AdamW step moves a parameter by lr g / (|g| + eps) ~ lr sign(g): where |g| is below the
+    # gradient check's atol (1e-5) that check cannot pin the sign, and near eps = 1e-8 the step amplifies
+    # the gradient's own tolerance (1e-5 + 1e-4 |g|) by lr eps / (|g| + eps)^2; those elements get that much
+    # more room (capped at 2 lr), everywhere else 1e-6. The elements that actually NEED the extra room
+    # (off by more than 1e-6) must stay few: at most 1 % of the compared elements
     lr, eps, gatol = float(g["lr"]), 1e-8, 1e-5
-    step_tol, n_relaxed, n_nonzero = [], 0, 0
+    step_tol = []
     for p in params:
         ga = p.grad.abs()
-        small = ga < gatol
         t = torch.clamp(1e-6 + lr * eps * (gatol + 1e-4 * ga) / (ga + eps) ** 2, max=2 * lr)
-        step_tol.append(torch.where(small, t, torch.full_like(t, 1e-6)))
-        n_relaxed += int((small & (ga > 0)).sum())
-        n_nonzero += int((ga > 0).sum())
-    assert n_relaxed <= 0.01 * max(n_nonzero, 1), f"{n_relaxed} of {n_nonzero} nonzero gradients below {gatol}"
+        step_tol.append(torch.where(ga < gatol, t, torch.full_like(t, 1e-6)))
     opt.step()
+    off = total = 0
     for n, p, t in zip(names, params, step_tol):
         GU.check(g, "param_after_" + n, p, t.cpu().numpy(), 0)
+        o, c = GU.count_excess(g, "param_after_" + n, p, 1e-6)
+        off, total = off + o, total + c
+    print(f"AdamW step: {off} of {total} compared elements beyond 1e-6 (relaxed tolerance used)")
+    assert off <= 0.01 * total, f"{off} of {total} AdamW-step elements needed the relaxed tolerance"
     T.interpolate_model(model, target, float(g["tau"]), target)
     for k, v in target.state_dict().items():
         GU.check(g, "target_after_" + k, v, 1e-6, 0)
