@@ -74,6 +74,14 @@
 // waves 0-3 issue first: the partner waves of a SIMD no longer do their post-barrier work in lockstep
 #define GM_ORDER 0
 #endif
+#ifndef GM_PINGPONG
+// 1: 8-wave 16x16x32 LDS-DMA kernels run the k loop as a ping-pong of the two waves of every SIMD:
+// waves 0..3 do [DMA issue, fragment reads, A split] then the tile's MFMAs; waves 4..7 first run the
+// MFMAs of the tile they read in the previous step, then [DMA, reads, split]; after every barrier one
+// wave of each SIMD feeds the matrix pipe while its partner does the rest (in-kernel stamps showed
+// both waves issuing DMAs and reading fragments in lockstep: ~45 % of a k step without an MFMA)
+#define GM_PINGPONG 0
+#endif
 #ifndef GM_PRIO
 #define GM_PRIO 0  // 1: waves 4-7 of the 8-wave LDS-DMA blocks at s_setprio 1 for the k loop (guide: static priority)
 #endif
@@ -1651,6 +1659,7 @@ __global__ __launch_bounds__(WGM* WGN * 64, OCC) void k_gemm3g(ASrc a0, ASrc a1,
     half8 sah2[2 * TM], sal2[2 * TM];  // GM_SPLIT_NEXT: the next tile's split A (register set of odd steps)
     constexpr bool SPLIT_NEXT = GM_SPLIT_NEXT && MF == 1 && STAGES == 2;
     constexpr bool ORDER = GM_ORDER && MF == 1 && NW == 8 && !SPLIT_NEXT;
+    constexpr bool PINGPONG = GM_PINGPONG && MF == 1 && NW == 8 && STAGES <= 3;
     const bool late = wave >= NW / 2;  // wave-uniform (readfirstlane)
     const _Float16 s12 = (_Float16)(1.0f / 4096.0f);
     const float ascale = AX == 2 ? *a0.scale : 1.0f;
@@ -1824,6 +1833,60 @@ __global__ __launch_bounds__(WGM* WGN * 64, OCC) void k_gemm3g(ASrc a0, ASrc a1,
     //   of tile k) | read half 0 of tile k+1 | MFMAs half 1 of tile k
     // so every fragment read overlaps the MFMAs of the other half, and a DMA has STAGES-1
     // steps to land.
+    if constexpr (PINGPONG) {
+        // one tile read, split and multiplied per barrier; STAGES - 1 tiles in flight
+        Frag fa, fb;
+        auto mfma_all = [&]() {
+            mfma16n(fa, I0{}, sah, sal, fa, sah2, sal2, std::false_type{});
+            mfma16n(fb, I1{}, sah, sal, fb, sah2, sal2, std::false_type{});
+        };
+        issue(I0{}, 0);
+        if constexpr (STAGES == 3)
+            if (nk > 1) issue(I1{}, 1);
+        auto pp_step = [&](auto ST, int kt) {
+            constexpr int S = decltype(ST)::value;
+            using SI = std::integral_constant<int, (S + STAGES - 1) % STAGES>;  // stage of tile kt + STAGES - 1
+            // own DMA of tile kt landed (with 3 stages tile kt + 1 may stay in flight); own reads done
+            if (STAGES == 3 && kt + 1 < nk)
+                asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NL) : "memory");
+            else
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_s_barrier();
+            asm volatile("" ::: "memory");  // no LDS access moves across the barrier
+            GM_STAMP(kt, 0);
+            if (ragged && kt == nk - 1) zero_tail(ST);
+            if (late && kt > 0) {  // the previous tile, from registers
+                __builtin_amdgcn_sched_barrier(0);
+                mfma_all();
+            }
+            __builtin_amdgcn_sched_barrier(0);
+            GM_STAMP(kt, 1);
+            if (kt + STAGES - 1 < nk) issue(SI{}, kt + STAGES - 1);  // into the stage of tile kt - 1
+            GM_STAMP(kt, 2);
+            read(ST, I0{}, fa);
+            read(ST, I1{}, fb);
+#pragma unroll
+            for (int i = 0; i < 2 * TM; i++) split_blk(fa, i, sah[i], sal[i]);
+            __builtin_amdgcn_sched_barrier(0);
+            GM_STAMP(kt, 3);
+            if (!late) {
+                mfma_all();
+                __builtin_amdgcn_sched_barrier(0);
+            }
+            GM_STAMP(kt, 4);
+        };
+#if GM_PRIO
+        if (__builtin_amdgcn_readfirstlane(threadIdx.x) >= 256) __builtin_amdgcn_s_setprio(1);
+#endif
+        for (int kt = 0; kt < nk; kt += STAGES) {
+            pp_step(I0{}, kt);
+            if (kt + 1 < nk) pp_step(I1{}, kt + 1);
+            if constexpr (STAGES == 3)
+                if (kt + 2 < nk) pp_step(I2{}, kt + 2);
+        }
+        if (late) mfma_all();  // the last tile
+    } else {
     issue(I0{}, 0);
     if (nk > 1) issue(I1{}, 1);
     if constexpr (STAGES >= 3)
@@ -1928,6 +1991,7 @@ __global__ __launch_bounds__(WGM* WGN * 64, OCC) void k_gemm3g(ASrc a0, ASrc a1,
         if constexpr (STAGES >= 4)
             if (kt + 3 < nk) step(I3{}, kt + 3);
     }
+    }  // !PINGPONG
 
 #if GM_PRIO
     __builtin_amdgcn_s_setprio(0);

@@ -17,7 +17,7 @@ for i in 1 2 3; do
     [ -n "$TILE9" ] && { GM_LIB=$lib TILE=9 timeout -k 10 120 python tools/presplit_bench.py >> gpurun_out/var_ab.log 2>&1 || exit $?; }
     if [ "$i" = 1 ]; then
       echo "== $v gemm_bench" >> gpurun_out/var_ab.log
-      GM_LIB=$lib X3_TILES=-1 TILES= timeout -k 10 200 python tools/gemm_bench.py 2>/dev/null | grep -v amdgpu.ids >> gpurun_out/var_ab.log || exit $?
+      GM_LIB=$lib X3_TILES=${X3_TILES:--1} TILES= timeout -k 10 200 python tools/gemm_bench.py 2>/dev/null | grep -v amdgpu.ids >> gpurun_out/var_ab.log || exit $?
     fi
   done
 done
