@@ -50,37 +50,17 @@
 #if GM_SPLIT_ASM != 0 && GM_SPLIT_ASM != 2
 #error "GM_SPLIT_ASM must be 0 (compiler-visible split) or 2 (asm + s_nop 1): the bare asm form races the MFMA read"
 #endif
-#ifndef GM_SPLIT_NEXT
-// 1: the 16x16x32 LDS-DMA kernels split tile k+1's A between tile k's second-half MFMAs (two split
-// register sets) instead of as a VALU block at the start of tile k+1's first MFMA segment
-#define GM_SPLIT_NEXT 0
-#endif
-#ifndef GM_K3_REMAP
-// 1: k_gemm3 (BK = 16) maps lanes to (row, chunk) so that each 16-lane group of the split-A
-// ds_write_b64 stores covers 8 rows x 2 adjacent 8-byte chunks (all 32 banks once at the 80-byte row
-// stride; the plain map put rows r and r + 3 of a group on banks 0-3: 2-way) and each 8-lane group
-// of the B ds_write_b128 stores 8 rows of one chunk (conflict-free); the LDS image is unchanged
-#define GM_K3_REMAP 0
-#endif
-#ifndef GM_DMA_SEQ
-// 1: the LDS-DMA kernels walk the A sources in tile order with the current source's buffer and per-lane
-// row offsets held in registers (advanced at segment ends), instead of a division and a branch tree per
-// k tile between the barrier and the next MFMAs (READOUT: k0 / hidden + a 4-way switch)
-#define GM_DMA_SEQ 0
-#endif
-#ifndef GM_ORDER
-// 1: in the 8-wave 16x16x32 LDS-DMA kernels, waves 4-7 (the second wave on each SIMD) run their
-// second-half MFMAs right after the tile barrier and issue the DMA / fragment reads after them, while
-// waves 0-3 issue first: the partner waves of a SIMD no longer do their post-barrier work in lockstep
-#define GM_ORDER 0
-#endif
 #ifndef GM_PINGPONG
-// 1: 8-wave 16x16x32 LDS-DMA kernels run the k loop as a ping-pong of the two waves of every SIMD:
+// 1 (default): 8-wave 16x16x32 LDS-DMA kernels run the k loop as a ping-pong of the two waves of every SIMD:
 // waves 0..3 do [DMA issue, fragment reads, A split] then the tile's MFMAs; waves 4..7 first run the
 // MFMAs of the tile they read in the previous step, then [DMA, reads, split]; after every barrier one
 // wave of each SIMD feeds the matrix pipe while its partner does the rest (in-kernel stamps showed
-// both waves issuing DMAs and reading fragments in lockstep: ~45 % of a k step without an MFMA)
-#define GM_PINGPONG 0
+// both waves issuing DMAs and reading fragments in lockstep: ~45 % of a k step without an MFMA). DQN layer 1
+// 182 -> 177 us (2 stages) / 172 us (3 stages, the readout default since), bit-identical results
+#define GM_PINGPONG 1
+#endif
+#ifndef GM_HEAD_STAGES
+#define GM_HEAD_STAGES 2  // LDS stages of the fused DQN layer 2 + Q head (gm_gemm_x3_head)
 #endif
 #ifndef GM_PRIO
 #define GM_PRIO 0  // 1: waves 4-7 of the 8-wave LDS-DMA blocks at s_setprio 1 for the k loop (guide: static priority)
@@ -792,9 +772,7 @@ __global__ __launch_bounds__(WGM* WGN * 64, OCC) void k_gemm3(ASrc a0, ASrc a1, 
     const int m0 = (bid / nN) * BM, n0 = (bid % nN) * BN;
 
     // ---- per-thread source byte offsets (fixed over K) ----
-    constexpr bool REMAP = GM_K3_REMAP && CPR == 4 && THREADS % 64 == 0;
-    const int c4 = REMAP ? 2 * ((lane >> 4) & 1) + ((lane >> 3) & 1) : tid % CPR;
-    const int rbase = REMAP ? wave * 16 + 8 * (lane >> 5) + (lane & 7) : tid / CPR;
+    const int c4 = tid % CPR, rbase = tid / CPR;
     int off1[AQ];       // src1 row
     int so[AQ][4];      // DENSE: so[q][0] row; AGGREGATE: member rows; READOUT: segment rows (OOB = none)
     float scale[AQ];
@@ -1529,39 +1507,11 @@ __global__ __launch_bounds__(WGM* WGN * 64, OCC) void k_gemm3g(ASrc a0, ASrc a1,
     const __amdgpu_buffer_rsrc_t r1 = a1.p0 ? rsrc_rows(a1.p0, a1.ld0, m0, a1.bytes0) : rsrc(a0.p0, 0u);
     const __amdgpu_buffer_rsrc_t rw = rsrc(reinterpret_cast<const float*>(w), wbytes);
 
-    // GM_DMA_SEQ: the current A source (issue() is called for kt = 0, 1, 2, .. in order)
-    __amdgpu_buffer_rsrc_t cur_r = r0a;
-    int cur_o[NA];
-#pragma unroll
-    for (int j = 0; j < NA; j++) cur_o[j] = so[j][0];
-    int cur_ko = 0, seg_idx = 0;
-    int seg_left = AMODE == GM_A_DENSE ? a0.k : a0.hidden;  // k columns left in the current segment
     // DMA of k tile kt into stage ST (all LDS bases wave-uniform)
     auto issue = [&](auto ST, int kt) {
         char* base = lds + decltype(ST)::value * STAGE_B + wave * NA * 1024;
         const int k0 = kt * BK;
-        if constexpr (GM_DMA_SEQ) {
-#pragma unroll
-            for (int j = 0; j < NA; j++) dma16(cur_r, base + j * 1024, cur_o[j], cur_ko);
-            cur_ko += BK * 4;
-            seg_left -= BK;
-            if (seg_left <= 0) {  // wave-uniform: next readout segment, or the dense second source
-                seg_idx++;
-                cur_ko = 0;
-                if (AMODE == GM_A_READOUT && seg_idx * a0.hidden < a0.k) {
-                    cur_r = r0b;
-                    seg_left = a0.hidden;
-#pragma unroll
-                    for (int j = 0; j < NA; j++)
-                        cur_o[j] = seg_idx == 1 ? so[j][1] : (seg_idx == 2 ? so[j][2] : so[j][3]);
-                } else {
-                    cur_r = r1;
-                    seg_left = 1 << 30;
-#pragma unroll
-                    for (int j = 0; j < NA; j++) cur_o[j] = o1[j];
-                }
-            }
-        } else if (k0 < a0.k) {
+        if (k0 < a0.k) {
             if (AMODE == GM_A_DENSE) {
 #pragma unroll
                 for (int j = 0; j < NA; j++) dma16(r0a, base + j * 1024, so[j][0], k0 * 4);
@@ -1656,9 +1606,6 @@ __global__ __launch_bounds__(WGM* WGN * 64, OCC) void k_gemm3g(ASrc a0, ASrc a1,
         }
     }
     half8 sah[2 * TM], sal[2 * TM];  // 16x16 form: split A of the current k tile (both column halves)
-    half8 sah2[2 * TM], sal2[2 * TM];  // GM_SPLIT_NEXT: the next tile's split A (register set of odd steps)
-    constexpr bool SPLIT_NEXT = GM_SPLIT_NEXT && MF == 1 && STAGES == 2;
-    constexpr bool ORDER = GM_ORDER && MF == 1 && NW == 8 && !SPLIT_NEXT;
     constexpr bool PINGPONG = GM_PINGPONG && MF == 1 && NW == 8 && STAGES <= 3;
     const bool late = wave >= NW / 2;  // wave-uniform (readfirstlane)
     const _Float16 s12 = (_Float16)(1.0f / 4096.0f);
@@ -1712,19 +1659,11 @@ __global__ __launch_bounds__(WGM* WGN * 64, OCC) void k_gemm3g(ASrc a0, ASrc a1,
         }
         split8(x0, x1, h, l, AX == 2 && GM_SPLIT_LDEXP ? aexp : 0);
     };
-    // GM_SPLIT_NEXT: the MFMAs of column half sb of the current tile on the split set (ch, cl); with
-    // NEXT, row block j - 1 of the next tile's raw A (fn) is split into (nh, nl) before block j's MFMAs
-    auto mfma16n = [&](const Frag& f, auto SB, half8 (&ch)[2 * TM], half8 (&cl)[2 * TM], const Frag& fn,
-                       half8 (&nh)[2 * TM], half8 (&nl)[2 * TM], auto NEXT) {
+    // the MFMAs of column half sb of the current tile on a split A held in (ch, cl) (GM_PINGPONG)
+    auto mfma16s = [&](const Frag& f, auto SB, half8 (&ch)[2 * TM], half8 (&cl)[2 * TM]) {
         constexpr int sb = decltype(SB)::value;
 #pragma unroll
         for (int j = 0; j < TN; j++) {
-            if constexpr (decltype(NEXT)::value) {
-                if (j >= 1 && j - 1 < 2 * TM) split_blk(fn, j - 1, nh[j - 1], nl[j - 1]);
-                if (j == TN - 1)
-#pragma unroll
-                    for (int i = TN - 1; i < 2 * TM; i++) split_blk(fn, i, nh[i], nl[i]);
-            }
             const half8 bs = f.bh[j] * s12;  // w_hi * 2^-12, exact
 #pragma unroll
             for (int i = 0; i < 2 * TM; i++) {
@@ -1837,8 +1776,8 @@ __global__ __launch_bounds__(WGM* WGN * 64, OCC) void k_gemm3g(ASrc a0, ASrc a1,
         // one tile read, split and multiplied per barrier; STAGES - 1 tiles in flight
         Frag fa, fb;
         auto mfma_all = [&]() {
-            mfma16n(fa, I0{}, sah, sal, fa, sah2, sal2, std::false_type{});
-            mfma16n(fb, I1{}, sah, sal, fb, sah2, sal2, std::false_type{});
+            mfma16s(fa, I0{}, sah, sal);
+            mfma16s(fb, I1{}, sah, sal);
         };
         issue(I0{}, 0);
         if constexpr (STAGES == 3)
@@ -1910,9 +1849,6 @@ __global__ __launch_bounds__(WGM* WGN * 64, OCC) void k_gemm3g(ASrc a0, ASrc a1,
     if (ragged && nk == 1) zero_tail(I0{});
     Frag f0, f1;
     read(I0{}, I0{}, f0);
-    if constexpr (SPLIT_NEXT)
-#pragma unroll
-        for (int i = 0; i < 2 * TM; i++) split_blk(f0, i, sah[i], sal[i]);
 #if GM_DIAG == 10
     read(I0{}, I1{}, f1);
 #endif
@@ -1922,24 +1858,17 @@ __global__ __launch_bounds__(WGM* WGN * 64, OCC) void k_gemm3g(ASrc a0, ASrc a1,
 #if GM_DIAG == 10  // diagnostic build 10: MFMAs only in the k loop (timing only)
         mfma(f0);
         mfma(f1);
-        bool h1_done = false;
         if (kt < 0) {
 #else
         GM_STAMP(kt, 0);
         read(ST, I1{}, f1);
         __builtin_amdgcn_sched_barrier(0);
-        if constexpr (SPLIT_NEXT) {
-            if constexpr (S == 0)
-                mfma16n(f0, I0{}, sah, sal, f0, sah2, sal2, std::false_type{});
-            else
-                mfma16n(f0, I0{}, sah2, sal2, f0, sah, sal, std::false_type{});
-        } else if constexpr (MF == 1)
+        if constexpr (MF == 1)
             mfma16(f0, I0{}, I0{}, std::integral_constant<int, TN>{});
         else
             mfma(f0);
         __builtin_amdgcn_sched_barrier(0);
         GM_STAMP(kt, 1);
-        bool h1_done = false;
         if (kt + 1 < nk) {
 #endif
             // own DMA of tile kt+1 landed (tiles kt+2 .. kt+STAGES-1 may stay in flight)
@@ -1949,14 +1878,6 @@ __global__ __launch_bounds__(WGM* WGN * 64, OCC) void k_gemm3g(ASrc a0, ASrc a1,
             __builtin_amdgcn_s_barrier();
             asm volatile("" ::: "memory");  // no LDS access moves across the barrier
             GM_STAMP(kt, 3);
-            if constexpr (ORDER) {
-                if (late) {  // second-half MFMAs first (they read only registers)
-                    __builtin_amdgcn_sched_barrier(0);
-                    mfma16(f1, I1{}, I0{}, std::integral_constant<int, TN>{});
-                    __builtin_amdgcn_sched_barrier(0);
-                    h1_done = true;
-                }
-            }
             if (kt + STAGES < nk) issue(ST, kt + STAGES);
             GM_STAMP(kt, 4);
             if (ragged && kt + 1 == nk - 1) zero_tail(SN{});
@@ -1964,13 +1885,7 @@ __global__ __launch_bounds__(WGM* WGN * 64, OCC) void k_gemm3g(ASrc a0, ASrc a1,
         }
         GM_STAMP(kt, 5);
         __builtin_amdgcn_sched_barrier(0);
-        if (ORDER && h1_done) {
-        } else if constexpr (SPLIT_NEXT) {  // split of tile kt + 1 (f0, just read) between these MFMAs
-            if constexpr (S == 0)
-                mfma16n(f1, I1{}, sah, sal, f0, sah2, sal2, std::true_type{});
-            else
-                mfma16n(f1, I1{}, sah2, sal2, f0, sah, sal, std::true_type{});
-        } else if constexpr (MF == 1)
+        if constexpr (MF == 1)
             mfma16(f1, I1{}, I0{}, std::integral_constant<int, TN>{});
         else
             mfma(f1);
@@ -2212,7 +2127,7 @@ int dispatch(const ASrc& s0, const ASrc& s1, const float* w, long long ldw, unsi
         } else if (tile >= 8)
             gt = tile;
         else if (tile == -1 && s0.mode == GM_A_READOUT && n > 128)
-            gt = 10;
+            gt = GM_PINGPONG ? 9 : 10;  // ping-pong: 3 stages (two tiles in flight) 177 -> 172 us for DQN layer 1
         else if (tile == -1 && s0.mode == GM_A_DENSE && n >= 128 && K >= 256 && m >= 32768)
             gt = 12;  // N = 128 (the encoder's last layer): 25.9 -> 21.4 us at 40 960 rows
 #define GM_GX(WGM, WGN, TM, TN, EP, AXV) \
@@ -2608,10 +2523,10 @@ extern "C" int gm_gemm_x3_head(const gm_a_src* a0, const void* wp, const float* 
     ep.ldq = ldq;
     if ((rc = range_flag(&ep.range_flag))) return rc;
     if (s0.amax)  // training forward: max |A| for the layer's weight gradient
-        return launch_g<4, 2, 1, 4, 2, GM_A_DENSE, EPI_HEAD, 1, 1>(s0, s1, static_cast<const float*>(wp), ldw,
+        return launch_g<4, 2, 1, 4, GM_HEAD_STAGES, GM_A_DENSE, EPI_HEAD, 1, 1>(s0, s1, static_cast<const float*>(wp), ldw,
                                                                   (unsigned)wb, m, n, K, ep, (hipStream_t)stream,
                                                                   wscale_inv, g_mfma16 == 2);
-    return launch_g<4, 2, 1, 4, 2, GM_A_DENSE, EPI_HEAD, 1>(s0, s1, static_cast<const float*>(wp), ldw, (unsigned)wb, m,
+    return launch_g<4, 2, 1, 4, GM_HEAD_STAGES, GM_A_DENSE, EPI_HEAD, 1>(s0, s1, static_cast<const float*>(wp), ldw, (unsigned)wb, m,
                                                           n, K, ep, (hipStream_t)stream, wscale_inv, g_mfma16 == 2);
 }
 

@@ -1,8 +1,10 @@
 #!/usr/bin/env python3
-"""Outputs of the rollout GEMM forms for one library build (GM_LIB) on fixed seeded inputs, saved to
-gpurun_out/varcheck_<tag>.npz; `var_check.py --compare a b` asserts two builds agree bit for bit
-(a k-loop schedule change must not change any output bit)."""
+"""Outputs of the rollout GEMM forms for one library build (GM_LIB) on fixed seeded inputs, recorded as
+SHA-256 digests in gpurun_out/varcheck_<tag>.json; `var_check.py --compare a b` asserts two builds agree
+bit for bit (a k-loop schedule change must not change any output bit)."""
+import hashlib
 import importlib
+import json
 import os
 import sys
 
@@ -50,13 +52,18 @@ def run(tag):
         out[f"lstm_{rows}_h"], out[f"lstm_{rows}_c"] = h1.cpu().numpy(), c1.cpu().numpy()
     torch.cuda.synchronize()
     os.makedirs("gpurun_out", exist_ok=True)
-    np.savez(f"gpurun_out/varcheck_{tag}.npz", **out)
+    dig = {k: hashlib.sha256(np.ascontiguousarray(v).tobytes()).hexdigest()[:24] for k, v in out.items()}
+    with open(f"gpurun_out/varcheck_{tag}.json", "w") as f:
+        json.dump(dig, f)
     print("varcheck", tag, {k: float(np.abs(v).sum()) for k, v in out.items()}, flush=True)
 
 
 def compare(a, b):
-    A, B = np.load(f"gpurun_out/varcheck_{a}.npz"), np.load(f"gpurun_out/varcheck_{b}.npz")
-    bad = {k: int((A[k] != B[k]).sum()) for k in A.files if not np.array_equal(A[k], B[k])}
+    with open(f"gpurun_out/varcheck_{a}.json") as f:
+        A = json.load(f)
+    with open(f"gpurun_out/varcheck_{b}.json") as f:
+        B = json.load(f)
+    bad = [k for k in A if A[k] != B.get(k)]
     print("varcheck compare", a, b, "identical" if not bad else f"DIFFERENT {bad}", flush=True)
     return not bad
 
