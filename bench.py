@@ -254,7 +254,8 @@ def kernel_cost(tag, n_env, N, A, E, x3=False):
 
 def env_step_overhead_bytes(n_env, N, A):
     """Bytes k_env_step writes beyond SURVEY §8(d)'s B_env: the GEMM-ready copy of the agent
-    rows (gm_obs_buffers.obs_gemm) that DQN layer 1 reads at K = 512 + 6N + 8."""
+    rows (gm_obs_buffers.obs_gemm) that DQN layer 1 reads at K = 512 + 6N + 8, when the env writes
+    both copies (the rollout's lazy-obs envs write only that copy: no overhead)."""
     return float(n_env * 4 * A * (6 * N + 8)) if _gemm_obs() else 0.0
 
 
@@ -479,7 +480,7 @@ def main():
     ro = RO.StreamedRollout(net, A, B, netmon, dqn, groups=args.groups, seed=rank * B, epsilon=args.epsilon,
                             episode_steps=args.episode_steps, device=dev.index,
                             stagger=args.stagger and not args.graph)
-    _GEMM_OBS_ON[0] = ro.envs[0].obs_gemm is not None
+    _GEMM_OBS_ON[0] = ro.envs[0].obs_gemm is not None and not ro.envs[0]._lazy_obs  # both copies written
     if args.unfused:
         for w in ro.wenvs:
             w.fused = False

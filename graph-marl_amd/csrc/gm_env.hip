@@ -252,12 +252,14 @@ __device__ void emit_obs(const EnvDev& d, int env, ES& s, const gm_obs_buffers& 
         }
         __syncthreads();
     }
-    if (o.obs) {
+    if (o.obs || o.obs_gemm) {
         // routing.py:269-315. The INDEPENDENT part of a row has at most 16 nonzero entries:
-        // zero-fill columns [0, 6N+10) of all A rows, then lane a writes packet a's entries
+        // zero-fill columns [0, 6N+10) of all A rows, then lane a writes packet a's entries.
+        // obs NULL with obs_gemm set: only the GEMM-ready copy is written (gm_obs_from_gemm
+        // rebuilds the agent rows from it on demand)
         const int D1 = 6 * N + 10, D = obs_dim_of(N, d.env_var, d.k);
         const size_t ld = o.obs_row_stride;
-        float* base = o.obs + (size_t)env * A * ld;
+        float* base = o.obs ? o.obs + (size_t)env * A * ld : nullptr;
         // routing.py:269-315. The INDEPENDENT part of a row has at most 16 nonzero entries:
         // batches of rows are built in the LDS image (row stride SR = D1 rounded up to 4 floats),
         // then copied out row by row as 16-byte stores (the last 2 columns of D1 = 4q + 2 as a
@@ -290,7 +292,8 @@ __device__ void emit_obs(const EnvDev& d, int env, ES& s, const gm_obs_buffers& 
                 }
             }
             __syncthreads();
-            if (vec) {
+            if (!base) {
+            } else if (vec) {
                 const int Qr = Q + (T ? 1 : 0);  // 16-B chunks per row, the last one partial (T = 2)
                 for (int i = l; i < nr * Qr; i += WAVE) {
                     const int r = i / Qr, q = i - r * Qr;
@@ -327,7 +330,7 @@ __device__ void emit_obs(const EnvDev& d, int env, ES& s, const gm_obs_buffers& 
             }
             __syncthreads();
         }
-        if (D > D1) {  // variant columns (2: k neighbour slots, 3: global), lane-strided per row
+        if (base && D > D1) {  // variant columns (2: k neighbour slots, 3: global), lane-strided per row
             for (int a = 0; a < A; a++) {
                 float* row = base + (size_t)a * ld;
                 for (int c = D1 + l; c < D; c += WAVE) {
@@ -688,7 +691,7 @@ __global__ __launch_bounds__(64) void k_env_reset(EnvDev d, const uint8_t* mask,
         s.load[e] = 0.0;
     }
     __syncthreads();
-    if (o.obs || o.node_obs || o.agent_node || o.agent_adj) {
+    if (o.obs || o.obs_gemm || o.node_obs || o.agent_node || o.agent_adj) {
         load_topology_lds(d, env, s);
         emit_obs(d, env, s, o);
     }
@@ -959,7 +962,7 @@ __global__ __launch_bounds__(64) void k_env_step(EnvDev d, const int32_t* act, S
     if (l + WAVE < E) { d.load[(size_t)env * E + l + WAVE] = ld1; s.load[l + WAVE] = ld1; }
     if (l + 2 * WAVE < E) { d.load[(size_t)env * E + l + 2 * WAVE] = ld2; s.load[l + 2 * WAVE] = ld2; }
     __syncthreads();
-    if (o.obs || o.node_obs || o.agent_node || o.agent_adj) emit_obs(d, env, s, o);
+    if (o.obs || o.obs_gemm || o.node_obs || o.agent_node || o.agent_adj) emit_obs(d, env, s, o);
 }
 
 template <int NC>
@@ -969,6 +972,44 @@ __global__ __launch_bounds__(64) void k_env_observe(EnvDev d, gm_obs_buffers o) 
     load_topology_lds(d, env, s);
     load_packets_lds(d, env, s);
     emit_obs(d, env, s, o);
+}
+
+// obs rows from the GEMM-ready copy (gm_obs_from_gemm): one wave per row, lane l writes 16-B
+// chunk l of the 6N+10 columns (the last one a float2: 6N+10 = 4q+2 for even N). Copy column c
+// comes from obs column c (c < N-1), c+1 (c < 2N-1), c+2 (else), so obs column j reads copy
+// column j (j < N-1), j-1 (N <= j < 2N), j-2 (j > 2N); column N-1 is the target one-hot's sum
+// minus the other position one-hots, column 2N the next-hop one-hot's sum (0 / 1 sums: exact)
+__global__ __launch_bounds__(256) void k_obs_from_gemm(const float* __restrict__ g, long long ldg, long long rows, int N,
+                                                       float* __restrict__ obs, long long ldo) {
+    const long long r = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (r >= rows) return;
+    const int l = threadIdx.x & 63;
+    const float* gr = g + r * ldg;
+    float* orow = obs + r * ldo;
+    const int D1 = 6 * N + 10, Q = (D1 + 3) / 4;
+    float pos = 0.f, tgt = 0.f, hop = 0.f;  // wave sums of the one-hot blocks
+    for (int c = l; c < N - 1; c += 64) pos += gr[c];
+    for (int c = N - 1 + l; c < 2 * N - 1; c += 64) tgt += gr[c];
+    for (int c = 2 * N - 1 + l; c < 3 * N - 1; c += 64) hop += gr[c];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        pos += __shfl_xor(pos, o);
+        tgt += __shfl_xor(tgt, o);
+        hop += __shfl_xor(hop, o);
+    }
+    for (int q = l; q < Q; q += 64) {
+        float v[4];
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const int c = 4 * q + j;
+            v[j] = c < N - 1 ? gr[c] : c == N - 1 ? tgt - pos : c < 2 * N ? gr[c - 1] : c == 2 * N ? hop
+                 : c < D1 ? gr[c - 2] : 0.f;
+        }
+        if (4 * q + 4 <= D1)
+            *reinterpret_cast<float4*>(orow + 4 * q) = make_float4(v[0], v[1], v[2], v[3]);
+        else
+            *reinterpret_cast<float2*>(orow + 4 * q) = make_float2(v[0], v[1]);
+    }
 }
 
 // EpsilonGreedy.__call__ (src/policy.py:20-64): randint(4, size=A) then rand(A)
@@ -1214,7 +1255,7 @@ __global__ __launch_bounds__(64) void k_build_seed_list(EnvDev d, int count, int
 inline int ncap(int n) { return n <= 64 ? 64 : 128; }
 
 bool has_obs(const gm_obs_buffers* o) {
-    return o && (o->obs || o->node_obs || o->agent_node || o->agent_adj);
+    return o && (o->obs || o->obs_gemm || o->node_obs || o->agent_node || o->agent_adj);
 }
 
 int check_launch() {
@@ -1360,10 +1401,10 @@ static int check_obs(const gm_env* env, const gm_obs_buffers* o) {
     if (o && o->obs && o->obs_row_stride < obs_dim_of(env->d.N, env->d.env_var, env->d.k))
         return gm_fail(GM_ERR_INVALID_ARG, "obs_row_stride smaller than the observation size");
     if (o && o->obs_gemm &&
-        (!o->obs || env->d.env_var != 1 || (env->d.N & 1) || o->obs_gemm_stride < 6 * env->d.N + 8 ||
+        (env->d.env_var != 1 || (env->d.N & 1) || o->obs_gemm_stride < 6 * env->d.N + 8 ||
          (o->obs_gemm_stride % 4) || (reinterpret_cast<uintptr_t>(o->obs_gemm) & 15)))
         // the copy is written as (6N+8)/4 whole float4 chunks per row: N must be even
-        return gm_fail(GM_ERR_INVALID_ARG, "obs_gemm: env_var 1 with obs, even N, stride >= 6N+8 and 16-byte rows");
+        return gm_fail(GM_ERR_INVALID_ARG, "obs_gemm: env_var 1, even N, stride >= 6N+8 and 16-byte rows");
     return GM_OK;
 }
 
@@ -1470,6 +1511,17 @@ extern "C" int gm_env_observe(gm_env* env, const gm_obs_buffers* obs, void* stre
     if (rc) return rc;
     if (ncap(env->d.N) == 64) hipLaunchKernelGGL(k_env_observe<64>, dim3(env->d.n_env), dim3(64), 0, (hipStream_t)stream, env->d, *obs);
     else hipLaunchKernelGGL(k_env_observe<128>, dim3(env->d.n_env), dim3(64), 0, (hipStream_t)stream, env->d, *obs);
+    return check_launch();
+}
+
+extern "C" int gm_obs_from_gemm(const float* obs_gemm, int64_t ld_gemm, int64_t rows, int32_t n_nodes, float* obs,
+                                int64_t ld_obs, void* stream) {
+    if (!obs_gemm || !obs || rows < 0 || n_nodes < 2 || (n_nodes & 1) || ld_gemm < 6 * n_nodes + 8 || (ld_gemm % 4) ||
+        ld_obs < 6 * n_nodes + 10 || (ld_obs % 4) || (reinterpret_cast<uintptr_t>(obs) & 15))
+        return gm_fail(GM_ERR_INVALID_ARG, "gm_obs_from_gemm: even N, ld_gemm >= 6N+8, ld_obs >= 6N+10, 16-byte rows");
+    if (rows == 0) return GM_OK;
+    hipLaunchKernelGGL(k_obs_from_gemm, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, (hipStream_t)stream, obs_gemm,
+                       (long long)ld_gemm, (long long)rows, (int)n_nodes, obs, (long long)ld_obs);
     return check_launch();
 }
 

@@ -62,6 +62,9 @@
 #ifndef GM_HEAD_STAGES
 #define GM_HEAD_STAGES 2  // LDS stages of the fused DQN layer 2 + Q head (gm_gemm_x3_head)
 #endif
+#ifndef GM_K3_ROWPERM
+#define GM_K3_ROWPERM 1  // register-staged k_gemm3: conflict-free LDS stores by a row permutation (see there)
+#endif
 #ifndef GM_PRIO
 #define GM_PRIO 0  // 1: waves 4-7 of the 8-wave LDS-DMA blocks at s_setprio 1 for the k loop (guide: static priority)
 #endif
@@ -773,12 +776,20 @@ __global__ __launch_bounds__(WGM* WGN * 64, OCC) void k_gemm3(ASrc a0, ASrc a1, 
 
     // ---- per-thread source byte offsets (fixed over K) ----
     const int c4 = tid % CPR, rbase = tid / CPR;
+    // GM_K3_ROWPERM: rows permuted inside aligned 8-row blocks (a row's CPR chunks stay on consecutive
+    // lanes, so every load instruction touches the same lines) so that the LDS stores meet distinct banks
+    // at the 4 BK + 16 byte row stride: A (ds_write_b64, 16-lane groups, CPR 4) rows {0,2,4,6} / {1,3,5,7}
+    // per group, (CPR 8: 2 rows per group, offset 2); B (ds_write_b128, 8-lane groups, CPR 4) rows {r, r+4}
+    const int j8 = rbase & 7;
+    const int rba = !GM_K3_ROWPERM ? rbase
+                    : (rbase & ~7) | (CPR == 4 ? ((j8 & 3) << 1) | (j8 >> 2) : CPR == 8 ? (j8 & 4) | ((j8 & 1) << 1) | ((j8 >> 1) & 1) : j8);
+    const int rbb = !GM_K3_ROWPERM || CPR != 4 ? rbase : (rbase & ~7) | ((j8 & 1) << 2) | (j8 >> 1);
     int off1[AQ];       // src1 row
     int so[AQ][4];      // DENSE: so[q][0] row; AGGREGATE: member rows; READOUT: segment rows (OOB = none)
     float scale[AQ];
 #pragma unroll
     for (int q = 0; q < AQ; q++) {
-        const int row = min(m0 + rbase + q * RSTEP, M - 1);
+        const int row = min(m0 + rba + q * RSTEP, M - 1);
         off1[q] = (int)((row - m0) * a1.ld0) * 4;
         scale[q] = 1.0f;
 #pragma unroll
@@ -815,7 +826,7 @@ __global__ __launch_bounds__(WGM* WGN * 64, OCC) void k_gemm3(ASrc a0, ASrc a1, 
     }
     int woff[BQ];
 #pragma unroll
-    for (int q = 0; q < BQ; q++) woff[q] = (int)(min(n0 + rbase + q * RSTEP, N - 1) * ldw) + 16 * c4;
+    for (int q = 0; q < BQ; q++) woff[q] = (int)(min(n0 + rbb + q * RSTEP, N - 1) * ldw) + 16 * c4;
 
     const __amdgpu_buffer_rsrc_t r0a =
         AMODE == GM_A_DENSE ? rsrc_rows(a0.p0, a0.ld0, m0, a0.bytes0) : rsrc(a0.p0, (unsigned)a0.bytes0);
@@ -896,12 +907,12 @@ __global__ __launch_bounds__(WGM* WGN * 64, OCC) void k_gemm3(ASrc a0, ASrc a1, 
             if (ascaled) v = make_float4(v.x * ascale, v.y * ascale, v.z * ascale, v.w * ascale);
             split4(v, hi, lo);
 #endif
-            char* row = as + (rbase + q * RSTEP) * ROWB;
+            char* row = as + (rba + q * RSTEP) * ROWB;
             *reinterpret_cast<half4*>(row) = hi;
             *reinterpret_cast<half4*>(row + 32) = lo;
         }
 #pragma unroll
-        for (int q = 0; q < BQ; q++) *reinterpret_cast<float4*>(Bs[buf] + (rbase + q * RSTEP) * ROWB + 16 * c4) = rb[S][q];
+        for (int q = 0; q < BQ; q++) *reinterpret_cast<float4*>(Bs[buf] + (rbb + q * RSTEP) * ROWB + 16 * c4) = rb[S][q];
     };
 
     floatx16 acc[TM][TN];

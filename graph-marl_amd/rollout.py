@@ -19,6 +19,8 @@ launch cost (one replay call per group per captured length). Graph replay bakes 
 arguments in: it is for fixed-ε rollouts (ε decay 1.0: benchmarks, evaluation); episode resets
 stay eager between replays.
 """
+import os
+
 import torch
 
 from . import _lib as L
@@ -26,6 +28,11 @@ from . import fused as FU  # noqa: F401  (packed-weight caches shared by the gro
 from .policy import EpsilonGreedy
 from .routing import Routing
 from .wrapper import NetMonWrapper
+
+
+# the rollout's envs write only the GEMM-ready obs copy that the fused DQN reads; reading .obs
+# rebuilds the reference rows from it (Routing.set_lazy_obs). GM_LAZY_OBS=0: write both every step
+LAZY_OBS = os.environ.get("GM_LAZY_OBS", "1") != "0"
 
 
 class _PlainEnv:
@@ -43,9 +50,12 @@ class _PlainEnv:
 
     @property
     def obs(self):
-        return self.env.obs_buf[..., : self.env.obs_dim]
+        return self.env.obs
 
     def reset(self):
+        self.env.reset_()
+
+    def reset_(self):
         self.env.reset_()
 
     def step_(self, actions, detail=None):
@@ -74,6 +84,8 @@ class StreamedRollout:
             wenv = NetMonWrapper(env, netmon, 1) if netmon is not None else _PlainEnv(env)
             pol = EpsilonGreedy(wenv, model, epsilon=epsilon, epsilon_decay=1.0, epsilon_update_freq=100,
                                 step_before_train=0)
+            if LAZY_OBS:
+                env.set_lazy_obs(True)  # the fused DQN reads obs_gemm: the reference rows are rebuilt on read
             self.envs.append(env)
             self.wenvs.append(wenv)
             self.policies.append(pol)
@@ -96,7 +108,7 @@ class StreamedRollout:
         for g in range(self.groups):
             self.streams[g].wait_stream(cur)
             with self._on(g):
-                self.wenvs[g].reset()
+                self.wenvs[g].reset_()
         self.ep = 0
 
     def _enqueue_step(self):
@@ -118,7 +130,7 @@ class StreamedRollout:
         for g in range(self.groups):
             if (self.ep + self._offs[g]) % self.episode_steps == 0:
                 with self._on(g):
-                    self.wenvs[g].reset()
+                    self.wenvs[g].reset_()
         if self.ep >= self.episode_steps:
             self.ep = 0
 
@@ -173,15 +185,18 @@ class StreamedRollout:
                     self.streams[g].wait_stream(cur)  # ordered after the caller's stream (weight copies, edits)
                     with self._on(g):
                         gr.replay()
+                    self.envs[g].mark_obs_stale()
                 self.ep += self._gsteps
                 if self.ep >= self.episode_steps:
                     L.check_range()
                     for g in range(self.groups):
                         with self._on(g):
-                            self.wenvs[g].reset()
+                            self.wenvs[g].reset_()
                     self.ep = 0
                 continue
             self._graph.replay()
+            for e in self.envs:
+                e.mark_obs_stale()
             self.ep += self._gsteps
             if self.ep >= self.episode_steps:
                 L.check_range()
@@ -189,7 +204,7 @@ class StreamedRollout:
                 for g in range(self.groups):
                     self.streams[g].wait_stream(cur)
                     with self._on(g):
-                        self.wenvs[g].reset()
+                        self.wenvs[g].reset_()
                 for s in self.streams:
                     cur.wait_stream(s)
                 self.ep = 0

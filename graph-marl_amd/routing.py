@@ -158,13 +158,15 @@ class Routing:
         self.nbr = torch.zeros(n_env, N, 3, dtype=torch.int32, device=dev)
         self._actions = torch.zeros(n_env, A, dtype=torch.int32, device=dev)
         self.obs_gemm = None  # GEMM-ready env obs copy (enable_gemm_obs)
+        self._lazy_obs = False  # kernels write only obs_gemm; obs rows rebuilt on demand (set_lazy_obs)
+        self._obs_stale = False
         self._has_state = False
         self._obsbufs = self._make_obsbufs(self.agent_adjacency)
 
     # -- plumbing ---------------------------------------------------------------
     def _make_obsbufs(self, adj):
         o = L.ObsBuffers()
-        o.obs = self.obs_buf.data_ptr()
+        o.obs = None if (self._lazy_obs and self.obs_gemm is not None) else self.obs_buf.data_ptr()
         o.obs_row_stride = self.obs_stride
         o.node_obs = self.node_obs.data_ptr()
         o.agent_node = self.agent_node.data_ptr()
@@ -186,6 +188,34 @@ class Routing:
             L.check(L.lib().gm_env_observe(self._h, C.byref(self._obsbufs), self._stream()))
         return self.obs_gemm
 
+    def set_lazy_obs(self, on=True):
+        """on: every reset / step writes only the GEMM-ready copy (one HBM copy of the agent rows per
+        step instead of two), and reading .obs rebuilds the reference rows from it
+        (gm_obs_from_gemm, bit-identical). For rollouts whose DQN reads obs_gemm and that do not
+        store every step's obs (benchmarks, evaluation). Needs enable_gemm_obs(); returns whether
+        the mode is on."""
+        if on and self.obs_gemm is None:
+            return False
+        if self._lazy_obs and not on:
+            self.sync_obs()
+        self._lazy_obs = bool(on)
+        self._obsbufs = self._make_obsbufs(self.agent_adjacency)
+        return self._lazy_obs
+
+    def mark_obs_stale(self):
+        """The env kernels ran outside step_ / reset_ (a replayed HIP graph): in lazy mode the obs rows
+        are rebuilt on the next read."""
+        if self._lazy_obs:
+            self._obs_stale = True
+
+    def sync_obs(self):
+        """Rebuild the agent obs rows from the GEMM-ready copy if the last kernels wrote only that."""
+        if self._obs_stale:
+            L.check(L.lib().gm_obs_from_gemm(self.obs_gemm.data_ptr(), self.obs_gemm.stride(1),
+                                             self.n_env * self.n_data, self.n_nodes, self.obs_buf.data_ptr(),
+                                             self.obs_stride, self._stream()))
+            self._obs_stale = False
+
     def _stream(self):
         return L.stream_ptr(self.device)
 
@@ -203,6 +233,7 @@ class Routing:
     @property
     def obs(self):
         """agent observations [n_env, A, 6N+10] (view of the persistent buffer)."""
+        self.sync_obs()
         return self.obs_buf[..., : self.obs_dim]
 
     def __str__(self):
@@ -236,6 +267,7 @@ class Routing:
         with L.timed("env_reset"):
             L.check(L.lib().gm_env_reset(self._h, L.ptr(m), C.byref(self._obsbufs), self._stream()))
         self._has_state = True
+        self.mark_obs_stale()
         L.check(L.lib().gm_env_topology(self._h, L.ptr(self.nbr), None, None, None, self._stream()))
 
     def reset(self):
@@ -254,6 +286,7 @@ class Routing:
             L.check(L.lib().gm_env_step(self._h, L.ptr(a), L.ptr(self.reward), L.ptr(self.done), L.ptr(self.info),
                                         None if det is None else C.byref(det), C.byref(self._obsbufs),
                                         self._stream()))
+        self.mark_obs_stale()
 
     def policy_step_(self, q, epsilon, actions, detail=None):
         """egreedy(q, epsilon, actions) then step_(actions) as one kernel (gm_env_policy_step):
@@ -265,6 +298,7 @@ class Routing:
                                                L.ptr(self.done), L.ptr(self.info),
                                                None if det is None else C.byref(det), C.byref(self._obsbufs),
                                                self._stream()))
+        self.mark_obs_stale()
         return actions
 
     def _detail(self, detail):
@@ -341,7 +375,12 @@ class Routing:
         return info
 
     def observe(self):
-        L.check(L.lib().gm_env_observe(self._h, C.byref(self._make_obsbufs(True)), self._stream()))
+        lazy, self._lazy_obs = self._lazy_obs, False
+        try:  # every buffer, the obs rows included
+            L.check(L.lib().gm_env_observe(self._h, C.byref(self._make_obsbufs(True)), self._stream()))
+        finally:
+            self._lazy_obs = lazy
+        self._obs_stale = False
 
     def get_num_agents(self):
         return self.n_data

@@ -58,6 +58,8 @@ class NetMonWrapper:
         """joint observation [n_env, A, obs_dim + (deg+1)H] (reference: concat of obs and graph obs)."""
         if self._dirty:
             self._materialize()
+        if hasattr(self.env, "sync_obs"):
+            self.env.sync_obs()  # env columns rebuilt when the env wrote only its GEMM-ready copy
         return self.env.obs_buf[..., : self.obs_dim]
 
     def _materialize(self):
@@ -90,13 +92,17 @@ class NetMonWrapper:
                 self.netmon.forward_graph(e.node_obs, e.nbr, e.agent_node, out=e.obs_buf, out_col=e.obs_dim)
                 self.current_netmon_state = self.netmon.state
 
-    def reset(self):
+    def reset_(self):
+        """reset() without materialising the joint observation (the rollout driver's form)."""
         self.current_netmon_state = None
         self.last_netmon_state = None
         self._cur = 1  # the start-up step writes buffer pair 0
         self.env.reset_()
         for _ in range(self.startup_iterations):
             self._netmon_step()
+
+    def reset(self):
+        self.reset_()
         return self.obs, self.env.agent_adj
 
     def step(self, actions):

@@ -12,6 +12,7 @@
  *   gm_env_step                      Routing.step                           src/env/routing.py:360-520
  *   gm_env_observe                   _get_observation / get_node_observation / get_node_agent_matrix /
  *                                    _get_data_adjacency / get_node_aux     src/env/routing.py:187-358, 522-539
+ *   gm_obs_from_gemm                 _get_observation rows rebuilt from the GEMM-ready copy  src/env/routing.py:269-315
  *   gm_env_topology                  get_nodes_adjacency (+ neighbour table) src/env/routing.py:184-185, src/env/network.py:385-389
  *   gm_env_final_info                Routing.get_final_info                 src/env/routing.py:541-546
  *   gm_build_seed_list               Network.build_seed_list                src/env/network.py:100-120
@@ -91,6 +92,8 @@ typedef struct {
      * others and runs with K = 6N+8 (640 with the readout at N = 20: whole 32-deep k tiles). */
     float* obs_gemm;        /* [n_env, A, obs_gemm_stride], 16-byte rows (nullable)        */
     int64_t obs_gemm_stride;
+    /* obs NULL with obs_gemm set: the kernels write the GEMM-ready copy only (one copy of the
+     * agent rows per step instead of two); gm_obs_from_gemm rebuilds obs rows from it. */
 } gm_obs_buffers;
 
 /* Per-env statistics of one step (src/env/routing.py:499-508), float64 [n_env, GM_INFO_FIELDS]. */
@@ -133,6 +136,13 @@ int gm_env_reset(gm_env* env, const uint8_t* reset_mask, const gm_obs_buffers* o
 int gm_env_step(gm_env* env, const int32_t* actions, float* reward, uint8_t* done, double* info,
                 const gm_step_detail* detail, const gm_obs_buffers* obs, void* stream);
 int gm_env_observe(gm_env* env, const gm_obs_buffers* obs, void* stream);
+/* Agent observation rows (env_var 1: columns [0, 6N+10)) rebuilt from their GEMM-ready copies:
+ * obs_gemm [rows, ld_gemm] (6N+8 columns, gm_obs_buffers.obs_gemm) -> obs [rows, ld_obs]. The
+ * two dropped columns are restored exactly (column N-1 = sum of the target one-hot - the other
+ * position one-hots; column 2N = sum of the next-hop one-hot), so the result equals what the env
+ * kernels write into gm_obs_buffers.obs bit for bit. N even, 16-byte rows. */
+int gm_obs_from_gemm(const float* obs_gemm, int64_t ld_gemm, int64_t rows, int32_t n_nodes, float* obs, int64_t ld_obs,
+                     void* stream);
 /* nbr: int32 [n_env, N, 3] neighbour ids ascending (= order of actions 1..3);
  * node_adj: int8 [n_env, N, N] (I + A); node_aux: float32 [n_env, N, N] APSP weights;
  * topo_seed: int64 [n_env]. Any may be NULL. */

@@ -115,7 +115,7 @@ def test_benched_rollout_long_horizon(form, case, monkeypatch, oracle_mod):
         out = {}
         for e, (g, i) in loc.items():
             env, wenv = ro.envs[g], ro.wenvs[g]
-            out[e] = dict(obs=env.obs_buf[i, :, :od].cpu().numpy(), node_obs=env.node_obs[i].cpu().numpy(),
+            out[e] = dict(obs=env.obs[i, :, :od].cpu().numpy(), node_obs=env.node_obs[i].cpu().numpy(),
                           state=wenv.current_netmon_state[i].cpu().numpy() if RNN else None,
                           readout=wenv.obs[i, :, od:].cpu().numpy() if RNN else None, reward=env.reward[i].cpu().numpy(),
                           done=env.done[i].cpu().numpy().astype(bool),

@@ -31,7 +31,7 @@ def snapshot(ro):
     for env, wenv in zip(ro.envs, ro.wenvs):
         st = env.get_state()
         out.append({"now": st["now"], "target": st["target"], "loads": st["loads"], "rng": st["rng_key"],
-                    "obs": env.obs_buf.cpu().numpy(), "reward": env.reward.cpu().numpy(),
+                    "obs": env.obs.cpu().numpy(), "reward": env.reward.cpu().numpy(),
                     "netmon": wenv.current_netmon_state.cpu().numpy()})
     return out
 
@@ -172,6 +172,44 @@ def test_rollout_orders_after_caller_stream():
     for a, b in zip(g, go(False)):
         assert_same(a, b)
     assert any(not np.array_equal(a["netmon"], b["netmon"]) for a, b in zip(g, go(False, edit=False)))
+
+
+@pytest.mark.parametrize("graph", [False, True])
+def test_lazy_obs_rows_match_written_rows(graph):
+    """The rollout's envs write only the GEMM-ready obs copy (Routing.set_lazy_obs); reading .obs
+    rebuilds the reference rows (gm_obs_from_gemm). They equal, bit for bit, the rows the env kernels
+    write when asked to, at every step, across episode resets, eager and under graph replay; and the
+    two modes give the same trajectories."""
+    RO = importlib.import_module("graph-marl_amd.rollout")
+    ros = []
+    for lazy in (True, False):
+        RO.LAZY_OBS = lazy
+        try:
+            ro = build(groups=2, n_env=64, episode_steps=10)
+        finally:
+            RO.LAZY_OBS = True
+        assert all(e._lazy_obs == lazy for e in ro.envs)
+        ro.reset()
+        ro.run(2)
+        if graph:
+            ro.capture(2)
+        ros.append(ro)
+    for step in range(12):
+        for ro in ros:
+            ro.run(2)
+        torch.cuda.synchronize()
+        for el, ew in zip(ros[0].envs, ros[1].envs):
+            assert el._obs_stale and not ew._obs_stale
+            assert torch.equal(el.obs_gemm, ew.obs_gemm), step
+            assert torch.equal(el.obs, ew.obs), step  # rebuilt vs written
+            assert torch.equal(el.reward, ew.reward) and torch.equal(el.node_obs, ew.node_obs)
+            assert not el._obs_stale
+    # a masked reset on a lazy env, then the obs rows of every env (reset or not)
+    el, ew = ros[0].envs[0], ros[1].envs[0]
+    mask = (torch.arange(el.n_env, device="cuda") % 3 == 0).to(torch.uint8)
+    el.reset_(mask)
+    ew.reset_(mask)
+    assert torch.equal(el.obs, ew.obs)
 
 
 def test_graph_needs_fixed_epsilon():
