@@ -298,9 +298,10 @@ def measure_extras(args, gm, M, RO, timed_region, dev, N, A, x3):
             dq = M.DQN(6 * N + 10 + (nm.get_out_features() if nm is not None else 0), [512, 256], 4).to(dev)
             ro = RO.StreamedRollout(net, A, n_env, nm, dq, groups=args.groups, seed=0, epsilon=args.epsilon,
                                     episode_steps=args.episode_steps, device=dev.index)
-            el, _ = timed_region(5, steps, False, ro=ro)
+            g = args.graph if args.graph and steps % args.graph == 0 else 0  # the headline's launch mode
+            el, _ = timed_region(5, steps, False, ro=ro, graph=g)
             out[name] = {"value": round(n_env * steps / el, 1), "unit": "env-steps/s",
-                         "ms_per_step": round(1e3 * el / steps, 4), "steps": steps, "n_env": n_env,
+                         "ms_per_step": round(1e3 * el / steps, 4), "steps": steps, "n_env": n_env, "graph": g,
                          "resets_in_window": -(-steps // args.episode_steps), "workload": desc}
             del ro, nm, dq
         except Exception as ex:  # an extra configuration must never break the headline line

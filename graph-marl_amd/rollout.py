@@ -111,10 +111,17 @@ class StreamedRollout:
                 self.wenvs[g].reset_()
         self.ep = 0
 
+    def _after_caller(self):
+        """Order every group stream after what the caller's stream holds (weight copies, edits): one
+        event recorded, one wait per group."""
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream())
+        for s in self.streams:
+            s.wait_event(ev)
+
     def _enqueue_step(self):
-        cur = torch.cuda.current_stream()
+        self._after_caller()
         for g in range(self.groups):
-            self.streams[g].wait_stream(cur)  # after whatever the caller enqueued (free when cur is idle)
             with self._on(g):
                 self.policies[g].act_step(self.wenvs[g])
 
@@ -180,9 +187,8 @@ class StreamedRollout:
             if self.ep % self._gsteps:
                 raise RuntimeError("graph replay must start at a multiple of the captured length")
             if self._graphs is not None:
-                cur = torch.cuda.current_stream()
+                self._after_caller()
                 for g, gr in enumerate(self._graphs):
-                    self.streams[g].wait_stream(cur)  # ordered after the caller's stream (weight copies, edits)
                     with self._on(g):
                         gr.replay()
                     self.envs[g].mark_obs_stale()

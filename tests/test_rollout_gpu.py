@@ -13,14 +13,15 @@ pytestmark = pytest.mark.gpu
 N, A, B = 20, 20, 8
 
 
-def build(groups, seed=0, episode_steps=10, n_env=B, K=2, epsilon=0.3):
+def build(groups, seed=0, episode_steps=10, n_env=B, K=2, epsilon=0.3, netmon=True):
+    """netmon False: BASELINE config 2 (no NetMon, the DQN on the env obs, fixed topology)."""
     gm = importlib.import_module("graph-marl_amd")
     M = importlib.import_module("graph-marl_amd.model")
     RO = importlib.import_module("graph-marl_amd.rollout")
-    net = gm.Network(N, random_topology=True, excluded_seeds=gm.EVAL_SEEDS, device=0)
+    net = gm.Network(N, random_topology=netmon, excluded_seeds=gm.EVAL_SEEDS, device=0)
     torch.manual_seed(3)
-    netmon = M.NetMon(4 * N + 8, 128, [512, 256], K).cuda()
-    dqn = M.DQN(6 * N + 10 + netmon.get_out_features(), [512, 256], 4).cuda()
+    netmon = M.NetMon(4 * N + 8, 128, [512, 256], K).cuda() if netmon else None
+    dqn = M.DQN(6 * N + 10 + (netmon.get_out_features() if netmon is not None else 0), [512, 256], 4).cuda()
     return RO.StreamedRollout(net, A, n_env, netmon, dqn, groups=groups, seed=seed, epsilon=epsilon,
                               episode_steps=episode_steps, device=0)
 
@@ -32,7 +33,7 @@ def snapshot(ro):
         st = env.get_state()
         out.append({"now": st["now"], "target": st["target"], "loads": st["loads"], "rng": st["rng_key"],
                     "obs": env.obs.cpu().numpy(), "reward": env.reward.cpu().numpy(),
-                    "netmon": wenv.current_netmon_state.cpu().numpy()})
+                    "netmon": wenv.current_netmon_state.cpu().numpy() if hasattr(wenv, "netmon") else np.zeros(1)})
     return out
 
 
@@ -120,6 +121,24 @@ def test_graph_replay_matches_eager(groups, gsteps, warm, per_group):
     ro.capture(gsteps, per_group=per_group)
     ro.run(40)
     assert (ro._graphs is not None and len(ro._graphs) == groups) if per_group else ro._graph is not None
+    for a, b in zip(snapshot(ro), ref):
+        assert_same(a, b)
+
+
+def test_graph_replay_matches_eager_config2():
+    """BASELINE config 2 (no NetMon: EpsilonGreedy.act on the env obs, the DQN as torch modules over the
+    HIP GEMMs, fixed topology) under per-group graph replay, as bench.py times it: bit-identical to eager."""
+    kw = dict(n_env=1024, epsilon=0.5, episode_steps=50, netmon=False)
+    eager = build(2, **kw)
+    eager.reset()
+    eager.run(10 + 120)
+    ref = snapshot(eager)
+    ro = build(2, **kw)
+    ro.reset()
+    for _ in range(10):
+        ro.step()
+    ro.capture(10, per_group=True)
+    ro.run(120)
     for a, b in zip(snapshot(ro), ref):
         assert_same(a, b)
 

@@ -17,7 +17,7 @@ d = json.loads(s[i:s.index("\n", i)])
 k = {t: round(v["avg_us"], 1) for t, v in (d.get("kernels") or {}).items()}
 print(json.dumps({"lib": sys.argv[1], "rollout": d["value"], "ms": d["ms_per_step"], "frac": (d.get("roofline") or {}).get("frac"),
                   "train": (d.get("rollout_train") or {}).get("value"),
-                  "sl": ((d.get("other_configs") or {}).get("config5_sl") or {}).get("value"), "kernels": k}))
+                  "other": {c: v.get("value") for c, v in (d.get("other_configs") or {}).items()}, "kernels": k}))
 PY
   done
 done

@@ -40,11 +40,11 @@ for s in "$@"; do
         benchst) step bench_stagger 300 python bench.py --no-cpu-baseline --steps 100 --stagger || exit $? ;;
         benchq) step bench 300 python bench.py --no-cpu-baseline --steps 100 || exit $? ;;
         prof) step prof 600 rocprofv3 --kernel-trace --stats -T --output-format csv -d gpurun_out/prof -o bench \
-                  -- python bench.py --steps 100 --groups 1 --no-cpu-baseline --no-train --no-f32-compare --no-extras --graph 0 || exit $? ;;
+                  -- python bench.py --steps 100 --groups 1 --no-cpu-baseline --no-pmc --no-train --no-f32-compare --no-extras --graph 0 || exit $? ;;
         pmc) step pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE -T --output-format csv -d gpurun_out/pmc -o fetch \
-                 -- python bench.py --steps 20 --warmup 5 --groups 1 --no-cpu-baseline --no-kernel-timers --no-train --no-f32-compare --no-extras --graph 0 || exit $?
+                 -- python bench.py --steps 20 --warmup 5 --groups 1 --no-cpu-baseline --no-pmc --no-kernel-timers --no-train --no-f32-compare --no-extras --graph 0 || exit $?
              step pmc_write 600 rocprofv3 --pmc WRITE_SIZE -T --output-format csv -d gpurun_out/pmc -o write \
-                 -- python bench.py --steps 20 --warmup 5 --groups 1 --no-cpu-baseline --no-kernel-timers --no-train --no-f32-compare --no-extras --graph 0 || exit $? ;;
+                 -- python bench.py --steps 20 --warmup 5 --groups 1 --no-cpu-baseline --no-pmc --no-kernel-timers --no-train --no-f32-compare --no-extras --graph 0 || exit $? ;;
         *) echo "unknown step $s"; exit 2 ;;
     esac
 done

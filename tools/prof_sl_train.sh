@@ -9,4 +9,4 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats -T --output-format csv -d gpu
     --iterations 3 --warmup 1 > gpurun_out/slprof/run.log 2>&1 || exit $?
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -T --output-format csv -d gpurun_out/tprof -o t \
     -- python bench.py --steps 4 --warmup 2 --graph 0 --no-extras --no-cpu-baseline --no-f32-compare --no-kernel-timers \
-    --train-steps 4 > gpurun_out/tprof/b.log 2>&1
+    --no-pmc --train-steps 4 > gpurun_out/tprof/b.log 2>&1
