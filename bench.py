@@ -480,7 +480,7 @@ def main():
     RO = importlib.import_module("graph-marl_amd.rollout")
     ro = RO.StreamedRollout(net, A, B, netmon, dqn, groups=args.groups, seed=rank * B, epsilon=args.epsilon,
                             episode_steps=args.episode_steps, device=dev.index,
-                            stagger=args.stagger and not args.graph)
+                            stagger=args.stagger, stagger_quantum=args.graph or 1)
     _GEMM_OBS_ON[0] = ro.envs[0].obs_gemm is not None and not ro.envs[0]._lazy_obs  # both copies written
     if args.unfused:
         for w in ro.wenvs:

@@ -64,12 +64,12 @@ class _PlainEnv:
 
 class StreamedRollout:
     def __init__(self, network, n_data, n_env, netmon, model, groups=1, seed=0, epsilon=0.5, episode_steps=50,
-                 obs_extra=None, device=None, stagger=False, **env_kw):
+                 obs_extra=None, device=None, stagger=False, stagger_quantum=1, **env_kw):
         """netmon None: DQN on the env observation alone (the reference without --netmon).
-        stagger: group g's episodes start g * episode_steps / groups steps into the first one, so
-        the groups' resets (latency-bound, low occupancy) overlap another group's GEMMs instead
-        of all groups resetting on the same step; every env still runs fixed-length episodes
-        (eager stepping only: graph capture needs aligned resets)."""
+        stagger: group g's episodes start about g * episode_steps / groups steps into the first one
+        (rounded down to a multiple of stagger_quantum: the graph length for graph replay), so the
+        groups' resets (latency-bound, low occupancy) overlap another group's GEMMs instead of all
+        groups resetting on the same step; every env still runs fixed-length episodes."""
         assert n_env % groups == 0, "n_env must be divisible by groups"
         self.groups = groups
         self.n_env = n_env
@@ -92,7 +92,8 @@ class StreamedRollout:
             self.streams.append(torch.cuda.Stream(dev))
         self.ep = 0
         self.stagger = stagger and groups > 1
-        self._offs = [(g * episode_steps) // groups if self.stagger else 0 for g in range(groups)]
+        q = max(1, int(stagger_quantum))
+        self._offs = [((g * episode_steps) // groups) // q * q if self.stagger else 0 for g in range(groups)]
         self._graph = None
         self._graphs = None
         self._gsteps = 0
@@ -147,8 +148,9 @@ class StreamedRollout:
         group on its own stream; else every group in one graph. Call after reset() and a few
         eager steps (packed weights and scratch exist)."""
         assert steps % 2 == 0 and self.episode_steps % steps == 0, "steps must be even and divide episode_steps"
-        if self.stagger:
-            raise ValueError("graph replay needs aligned group resets (stagger=False)")
+        if any(o % steps for o in self._offs):
+            raise ValueError("graph replay needs group episode offsets that are multiples of the captured length "
+                             "(StreamedRollout(stagger_quantum=steps))")
         if any(w._eps_changes() for w in self.policies):
             raise ValueError("graph replay needs a fixed epsilon (epsilon_decay = 1.0)")
         torch.cuda.synchronize()
@@ -195,9 +197,11 @@ class StreamedRollout:
                 self.ep += self._gsteps
                 if self.ep >= self.episode_steps:
                     L.check_range()
-                    for g in range(self.groups):
+                for g in range(self.groups):
+                    if (self.ep + self._offs[g]) % self.episode_steps == 0:
                         with self._on(g):
                             self.wenvs[g].reset_()
+                if self.ep >= self.episode_steps:
                     self.ep = 0
                 continue
             self._graph.replay()
@@ -206,13 +210,16 @@ class StreamedRollout:
             self.ep += self._gsteps
             if self.ep >= self.episode_steps:
                 L.check_range()
+            due = [g for g in range(self.groups) if (self.ep + self._offs[g]) % self.episode_steps == 0]
+            if due:
                 cur = torch.cuda.current_stream()  # the replay's stream
-                for g in range(self.groups):
+                for g in due:
                     self.streams[g].wait_stream(cur)
                     with self._on(g):
                         self.wenvs[g].reset_()
-                for s in self.streams:
-                    cur.wait_stream(s)
+                for g in due:
+                    cur.wait_stream(self.streams[g])
+            if self.ep >= self.episode_steps:
                 self.ep = 0
 
     def join(self):

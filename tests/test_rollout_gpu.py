@@ -13,7 +13,7 @@ pytestmark = pytest.mark.gpu
 N, A, B = 20, 20, 8
 
 
-def build(groups, seed=0, episode_steps=10, n_env=B, K=2, epsilon=0.3, netmon=True):
+def build(groups, seed=0, episode_steps=10, n_env=B, K=2, epsilon=0.3, netmon=True, **kw):
     """netmon False: BASELINE config 2 (no NetMon, the DQN on the env obs, fixed topology)."""
     gm = importlib.import_module("graph-marl_amd")
     M = importlib.import_module("graph-marl_amd.model")
@@ -23,7 +23,7 @@ def build(groups, seed=0, episode_steps=10, n_env=B, K=2, epsilon=0.3, netmon=Tr
     netmon = M.NetMon(4 * N + 8, 128, [512, 256], K).cuda() if netmon else None
     dqn = M.DQN(6 * N + 10 + (netmon.get_out_features() if netmon is not None else 0), [512, 256], 4).cuda()
     return RO.StreamedRollout(net, A, n_env, netmon, dqn, groups=groups, seed=seed, epsilon=epsilon,
-                              episode_steps=episode_steps, device=0)
+                              episode_steps=episode_steps, device=0, **kw)
 
 
 def snapshot(ro):
@@ -94,14 +94,33 @@ def test_staggered_groups_match_serial():
     assert_same(got, cat(parts))
 
 
-def test_stagger_refuses_graph():
-    ro = build(2)
-    ro.stagger = True
+def test_stagger_refuses_graph_off_quantum():
+    ro = build(2, stagger=True)  # offsets 0, 5: not multiples of a 2-step graph
+    assert ro._offs == [0, 5]
     ro.reset()
     ro.step()
     ro.step()
     with pytest.raises(ValueError):
         ro.capture(2)
+
+
+@pytest.mark.parametrize("per_group", [True, False])
+def test_staggered_graph_replay_matches_eager(per_group):
+    """Staggered episodes (group 1 resets 4 steps after group 0: offsets quantised to the 2-step graph)
+    under graph replay == the same staggered rollout stepped eagerly, across several resets of each group."""
+    eager = build(2, stagger=True, stagger_quantum=2)
+    assert eager._offs == [0, 4]
+    eager.reset()
+    eager.run(4 + 40)
+    ref = snapshot(eager)
+    ro = build(2, stagger=True, stagger_quantum=2)
+    ro.reset()
+    for _ in range(4):
+        ro.step()
+    ro.capture(2, per_group=per_group)
+    ro.run(40)
+    for a, b in zip(snapshot(ro), ref):
+        assert_same(a, b)
 
 
 @pytest.mark.parametrize("per_group", [True, False])
