@@ -62,6 +62,9 @@
 #ifndef GM_HEAD_STAGES
 #define GM_HEAD_STAGES 2  // LDS stages of the fused DQN layer 2 + Q head (gm_gemm_x3_head)
 #endif
+#ifndef GM_WGRAD_PF2
+#define GM_WGRAD_PF2 1  // k_wgrad_tr (128-wide, 32x32x16): operand loads two k tiles ahead in two register sets
+#endif
 #ifndef GM_K3_ROWPERM
 #define GM_K3_ROWPERM 1  // register-staged k_gemm3: conflict-free LDS stores by a row permutation (see there)
 #endif
@@ -2799,23 +2802,28 @@ __global__ __launch_bounds__(256, BN == 128 ? 2 : 1) void k_wgrad_tr(const float
     // (tid >> 5) + 8 j; B tile 32 x BN: BN / 4 float4 per row
     constexpr int QB = BN / 4, RB_STEP = 256 / QB;
     const int qa = tid & 31, ka0 = tid >> 5, qb = tid % QB, kb0 = tid / QB;
-    float4 va[LA], vb[LB];
-    auto load = [&](int kt) {
+    // NS register sets of staged operands: 2 (GM_WGRAD_PF2, 128-wide 32x32x16 form) loads tile kt + 2 while
+    // tile kt + 1 waits in the other set for its store, so a load has a whole k step plus the MFMAs to land
+    constexpr int NS = (GM_WGRAD_PF2 && MF == 0 && BN == 128) ? 2 : 1;
+    float4 va[NS][LA], vb[NS][LB];
+    auto load = [&](auto SET, int kt) {
+        constexpr int S = decltype(SET)::value;
         const int k0 = kb + kt * BK;
 #pragma unroll
         for (int j = 0; j < LA; j++) {
             const int k = k0 + ka0 + 8 * j, m = m0 + 4 * qa;
             const int off = (k < ke && m < M) ? (int)(((long long)(k - kb) * lda + m) * 4) : OOB;
-            va[j] = bload(ra, off);
+            va[S][j] = bload(ra, off);
         }
 #pragma unroll
         for (int j = 0; j < LB; j++) {
             const int k = k0 + kb0 + RB_STEP * j, n = n0 + 4 * qb;
             const int off = (k < ke && n < N) ? (int)(((long long)(k - kb) * ldb + n) * 4) : OOB;
-            vb[j] = bload(rb, off);
+            vb[S][j] = bload(rb, off);
         }
     };
-    auto store = [&](int buf) {
+    auto store = [&](auto SET, int buf) {
+        constexpr int S = decltype(SET)::value;
         char* ah = smem[buf];
         char* al = ah + BK * RA;
         char* bh = al + BK * RA;
@@ -2824,9 +2832,9 @@ __global__ __launch_bounds__(256, BN == 128 ? 2 : 1) void k_wgrad_tr(const float
         for (int j = 0; j < LA; j++) {
             half4 hi, lo;
 #if GM_SPLIT_LDEXP
-            split4e(va[j], e_a, hi, lo);
+            split4e(va[S][j], e_a, hi, lo);
 #else
-            split4(make_float4(va[j].x * s_a, va[j].y * s_a, va[j].z * s_a, va[j].w * s_a), hi, lo);
+            split4(make_float4(va[S][j].x * s_a, va[S][j].y * s_a, va[S][j].z * s_a, va[S][j].w * s_a), hi, lo);
 #endif
             const int o = (ka0 + 8 * j) * RA + ((8 * qa) ^ (MF ? (((ka0 + 8 * j) >> 3) & 1) << 5 : 0));
             *reinterpret_cast<half4*>(ah + o) = hi;
@@ -2836,9 +2844,9 @@ __global__ __launch_bounds__(256, BN == 128 ? 2 : 1) void k_wgrad_tr(const float
         for (int j = 0; j < LB; j++) {
             half4 hi, lo;
 #if GM_SPLIT_LDEXP
-            split4e(vb[j], e_b, hi, lo);
+            split4e(vb[S][j], e_b, hi, lo);
 #else
-            split4(make_float4(vb[j].x * s_b, vb[j].y * s_b, vb[j].z * s_b, vb[j].w * s_b), hi, lo);
+            split4(make_float4(vb[S][j].x * s_b, vb[S][j].y * s_b, vb[S][j].z * s_b, vb[S][j].w * s_b), hi, lo);
 #endif
             const int o = (kb0 + RB_STEP * j) * RB + ((8 * qb) ^ (MF ? (((kb0 + RB_STEP * j) >> 3) & 1) << 5 : 0));
             *reinterpret_cast<half4*>(bh + o) = hi;
@@ -2940,16 +2948,40 @@ __global__ __launch_bounds__(256, BN == 128 ? 2 : 1) void k_wgrad_tr(const float
                 }
         }
     };
-    if (nk > 0) {
-        load(0);
-        store(0);
-    }
-    __syncthreads();
-    for (int kt = 0; kt < nk; kt++) {
-        if (kt + 1 < nk) load(kt + 1);
-        compute(kt & 1);
-        if (kt + 1 < nk) store((kt + 1) & 1);
+    using W0 = std::integral_constant<int, 0>;
+    using W1 = std::integral_constant<int, NS - 1>;
+    if constexpr (NS == 1) {
+        if (nk > 0) {
+            load(W0{}, 0);
+            store(W0{}, 0);
+        }
         __syncthreads();
+        for (int kt = 0; kt < nk; kt++) {
+            if (kt + 1 < nk) load(W0{}, kt + 1);
+            compute(kt & 1);
+            if (kt + 1 < nk) store(W0{}, (kt + 1) & 1);
+            __syncthreads();
+        }
+    } else {
+        // step kt: load tile kt + 2 into set kt & 1 (its tile kt is in LDS buffer kt & 1), compute buffer
+        // kt & 1, store tile kt + 1 (set (kt + 1) & 1, loaded one step earlier) into the other buffer
+        if (nk > 0) {
+            load(W0{}, 0);
+            if (nk > 1) load(W1{}, 1);
+            store(W0{}, 0);
+        }
+        __syncthreads();
+        auto step = [&](auto SET, int kt) {
+            constexpr int S = decltype(SET)::value;
+            if (kt + 2 < nk) load(SET, kt + 2);
+            compute(S);
+            if (kt + 1 < nk) store(std::integral_constant<int, S ^ 1>{}, S ^ 1);
+            __syncthreads();
+        };
+        for (int kt = 0; kt < nk; kt += 2) {
+            step(W0{}, kt);
+            if (kt + 1 < nk) step(W1{}, kt + 1);
+        }
     }
     const float inv = 1.0f / (s_a * s_b);  // powers of two: exact
     float* Cz = C + (size_t)chunk * cz;
