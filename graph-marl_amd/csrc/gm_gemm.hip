@@ -62,6 +62,9 @@
 #ifndef GM_HEAD_STAGES
 #define GM_HEAD_STAGES 2  // LDS stages of the fused DQN layer 2 + Q head (gm_gemm_x3_head)
 #endif
+#ifndef GM_READOUT_TILE
+#define GM_READOUT_TILE (GM_PINGPONG ? 9 : 10)  // LDS-DMA tile of the readout-sourced DQN layer 1 (9: 3 stages, 144 KB)
+#endif
 #ifndef GM_WGRAD_PF2
 #define GM_WGRAD_PF2 1  // k_wgrad_tr (128-wide, 32x32x16): operand loads two k tiles ahead in two register sets
 #endif
@@ -2141,7 +2144,7 @@ int dispatch(const ASrc& s0, const ASrc& s1, const float* w, long long ldw, unsi
         } else if (tile >= 8)
             gt = tile;
         else if (tile == -1 && s0.mode == GM_A_READOUT && n > 128)
-            gt = GM_PINGPONG ? 9 : 10;  // ping-pong: 3 stages (two tiles in flight) 177 -> 172 us for DQN layer 1
+            gt = GM_READOUT_TILE;  // ping-pong: 3 stages (two tiles in flight) 177 -> 172 us for DQN layer 1
         else if (tile == -1 && s0.mode == GM_A_DENSE && n >= 128 && K >= 256 && m >= 32768)
             gt = 12;  // N = 128 (the encoder's last layer): 25.9 -> 21.4 us at 40 960 rows
 #define GM_GX(WGM, WGN, TM, TN, EP, AXV) \
