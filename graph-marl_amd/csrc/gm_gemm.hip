@@ -62,6 +62,9 @@
 #ifndef GM_HEAD_STAGES
 #define GM_HEAD_STAGES 2  // LDS stages of the fused DQN layer 2 + Q head (gm_gemm_x3_head)
 #endif
+#ifndef GM_HEAD_SPLIT
+#define GM_HEAD_SPLIT 1  // rollout Q head on 128x128 blocks, partial Q per column block added onto a zeroed q
+#endif
 #ifndef GM_READOUT_TILE
 #define GM_READOUT_TILE (GM_PINGPONG ? 9 : 10)  // LDS-DMA tile of the readout-sourced DQN layer 1 (9: 3 stages, 144 KB)
 #endif
@@ -135,6 +138,7 @@ struct Epi {
     const float* bq;
     int nq;
     float* q;
+    int q_atomic;             // EPI_HEAD over several column blocks: each adds its partial Q (block 0 with bq) to q (zeroed)
     long long ldq;
     unsigned* range_flag;     // X3: set to 1 when an accumulator is not finite (host-mapped; nullable)
     int cell;                 // EPI_LSTM tiles: 0 LSTM (i, f, g, o), 1 GRU (r, z, n_x, n_h; c_in = h)
@@ -1201,12 +1205,12 @@ __device__ __forceinline__ void dgrad_epilogue16(floatx4 (&acc)[T2][N2], const E
 // = row 4 (l >> 4) + (e >> 2), head e & 3), the WGN column waves summed through LDS.
 template <int T2, int N2, int WGN, int BM, int A = -1>
 __device__ __forceinline__ void head_epilogue16(floatx4 (&acc)[T2][N2], const Epi& ep, char* lds, int m0, int wr,
-                                                int wc, int M, int N, int lane, int tid) {
+                                                int wc, int M, int N, int lane, int tid, int n0 = 0) {
     const int l16 = lane & 15, rq = 4 * (lane >> 4);
     float bv[N2], wqv[N2][4];
 #pragma unroll
     for (int j = 0; j < N2; j++) {
-        const int col = wc * N2 * 16 + j * 16 + l16;
+        const int col = n0 + wc * N2 * 16 + j * 16 + l16;
         bv[j] = (ep.bias && col < N) ? ep.bias[col] : 0.f;
 #pragma unroll
         for (int a = 0; a < 4; a++) wqv[j][a] = (col < N && a < ep.nq) ? ep.wq[a * ep.ldwq + col] : 0.f;
@@ -1220,7 +1224,7 @@ __device__ __forceinline__ void head_epilogue16(floatx4 (&acc)[T2][N2], const Ep
         for (int e = 0; e < 16; e++) x[e] = 0.f;
 #pragma unroll
         for (int j = 0; j < N2; j++) {
-            const int col = wc * N2 * 16 + j * 16 + l16;
+            const int col = n0 + wc * N2 * 16 + j * 16 + l16;
 #pragma unroll
             for (int r = 0; r < 4; r++) {
                 float y = acc[i][j][r] + bv[j];
@@ -1255,10 +1259,13 @@ __device__ __forceinline__ void head_epilogue16(floatx4 (&acc)[T2][N2], const Ep
     for (int e = tid; e < BM * 4; e += WGN * (BM / T2 / 16) * 64) {
         const int rl = e >> 2, a = e & 3, row = m0 + rl;
         if (a >= ep.nq || row >= M) continue;
-        float v = ep.bq ? ep.bq[a] : 0.f;
+        float v = (ep.bq && n0 == 0) ? ep.bq[a] : 0.f;
 #pragma unroll
         for (int w = 0; w < WGN; w++) v += qp[(w * BM + rl) * 4 + a];
-        ep.q[(long long)row * ep.ldq + a] = v;
+        if (ep.q_atomic)  // two column blocks onto a zeroed q: 0 + x is exact, so x + y is order-free
+            atomicAdd(&ep.q[(long long)row * ep.ldq + a], v);
+        else
+            ep.q[(long long)row * ep.ldq + a] = v;
     }
 }
 
@@ -1957,7 +1964,7 @@ __global__ __launch_bounds__(WGM* WGN * 64, OCC) void k_gemm3g(ASrc a0, ASrc a1,
                                                              N, lane);
         } else if constexpr (EPI == EPI_HEAD)
             act_dispatch(ep.act, [&](auto A) {
-                head_epilogue16<2 * TM, 2 * TN, WGN, BM, decltype(A)::value>(acc4, ep, lds, m0, wr, wc, M, N, lane, tid);
+                head_epilogue16<2 * TM, 2 * TN, WGN, BM, decltype(A)::value>(acc4, ep, lds, m0, wr, wc, M, N, lane, tid, n0);
             });
         else if constexpr (EPI == EPI_DQN)
             act_dispatch(ep.act, [&](auto A) {
@@ -2539,6 +2546,15 @@ extern "C" int gm_gemm_x3_head(const gm_a_src* a0, const void* wp, const float* 
     ep.q = q;
     ep.ldq = ldq;
     if ((rc = range_flag(&ep.range_flag))) return rc;
+    if (GM_HEAD_SPLIT && !s0.amax && n > 128 && g_mfma16 == 2) {  // (the 16x16 epilogue adds partials)
+        // rollout: 128x128 blocks at 2 per CU (the plain layer's faster tile); each of the two column
+        // blocks adds its partial Q to a zeroed q (column block 0 with bq)
+        const hipError_t me = hipMemset2DAsync(q, (size_t)ldq * 4, 0, (size_t)nq * 4, (size_t)m, (hipStream_t)stream);
+        if (me != hipSuccess) return gm_fail(GM_ERR_HIP, std::string("gm_gemm_x3_head: ") + hipGetErrorString(me));
+        ep.q_atomic = 1;
+        return launch_g<4, 1, 1, 4, 2, GM_A_DENSE, EPI_HEAD, 2>(s0, s1, static_cast<const float*>(wp), ldw, (unsigned)wb, m, n,
+                                                                K, ep, (hipStream_t)stream, wscale_inv, g_mfma16 == 2);
+    }
     if (s0.amax)  // training forward: max |A| for the layer's weight gradient
         return launch_g<4, 2, 1, 4, GM_HEAD_STAGES, GM_A_DENSE, EPI_HEAD, 1, 1>(s0, s1, static_cast<const float*>(wp), ldw,
                                                                   (unsigned)wb, m, n, K, ep, (hipStream_t)stream,
