@@ -62,6 +62,9 @@
 #ifndef GM_HEAD_STAGES
 #define GM_HEAD_STAGES 2  // LDS stages of the fused DQN layer 2 + Q head (gm_gemm_x3_head)
 #endif
+#ifndef GM_NARROW_TILE
+#define GM_NARROW_TILE 0  // 1: 128-column layers with K <= 256 (encoder layer 3) on 64x128 blocks, 3 per CU (tile 15)
+#endif
 #ifndef GM_HEAD_SPLIT
 #define GM_HEAD_SPLIT 1  // rollout Q head on 128x128 blocks, partial Q per column block added onto a zeroed q
 #endif
@@ -2153,7 +2156,7 @@ int dispatch(const ASrc& s0, const ASrc& s1, const float* w, long long ldw, unsi
         else if (tile == -1 && s0.mode == GM_A_READOUT && n > 128)
             gt = GM_READOUT_TILE;  // ping-pong: 3 stages (two tiles in flight) 177 -> 172 us for DQN layer 1
         else if (tile == -1 && s0.mode == GM_A_DENSE && n >= 128 && K >= 256 && m >= 32768)
-            gt = 12;  // N = 128 (the encoder's last layer): 25.9 -> 21.4 us at 40 960 rows
+            gt = (GM_NARROW_TILE && n <= 128 && K <= 256 && epilogue != GM_EPI_LSTM) ? 15 : 12;  // N = 128 (the encoder's last layer): 25.9 -> 21.4 us at 40 960 rows
 #define GM_GX(WGM, WGN, TM, TN, EP, AXV) \
     launch_g<WGM, WGN, TM, TN, 2, GM_A_DENSE, EP, 2, AXV>(s0, s1, w, ldw, wb, m, n, K, ep, st, wsi)
         if (gt >= 8 && ax) {
@@ -2189,6 +2192,7 @@ int dispatch(const ASrc& s0, const ASrc& s1, const float* w, long long ldw, unsi
         case 12: return GM_G(4, 1, 1, 4, 2, AM, EPI_BIAS, 2);    \
         case 13: return GM_G(2, 2, 2, 2, 2, AM, EPI_BIAS, 2);    \
         case 14: return GM_G(2, 2, 2, 4, 2, AM, EPI_BIAS, 1);    \
+        case 15: return GM_G(2, 2, 1, 2, 2, AM, EPI_BIAS, 3);    \
         default: return GM_G(8, 1, 1, 4, 2, AM, EPI_BIAS, 1);    \
     }
             if (n > 32) {
@@ -3122,7 +3126,7 @@ extern "C" int gm_gemm_set_mfma(int32_t shape) {
 }
 
 extern "C" int gm_gemm_set_tile(int32_t tile) {
-    if (tile < -1 || tile > 14) return gm_fail(GM_ERR_INVALID_ARG, "gm_gemm_set_tile: tile in [-1, 14]");
+    if (tile < -1 || tile > 15) return gm_fail(GM_ERR_INVALID_ARG, "gm_gemm_set_tile: tile in [-1, 15]");
     g_tile = tile;
     return GM_OK;
 }

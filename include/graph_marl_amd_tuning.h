@@ -13,7 +13,7 @@ extern "C" {
  * blocks/CU); of gm_gemm_x3 (-1/0 = 128x128x16; 1 = 128x256x16 (LSTM: 128x128x32);
  * 2 = 128x128x32 (LSTM: 256x128x16)); 8..14 the LDS-DMA tiles of gm_gemm_x3's dense / readout
  * sources (8 = 256x256, 9 = 128x256 3 stages, 10 = 128x256, 12 = 128x128 2 blocks/CU, 13 = 128x128
- * of 64x64 waves, 14 = 128x256 of 64x128 waves). Process-wide. */
+ * of 64x64 waves, 14 = 128x256 of 64x128 waves, 15 = 64x128 3 blocks/CU). Process-wide. */
 /* Weight-gradient kernel of gm_gemm_x3_wgrad (same arithmetic, diagnostics / A-B timing):
  * -1 (default) or 1 = transposed LDS reads (ds_read_b64_tr_b16) with 128 x 128 tiles, 2 = the same
  * with 128 x 256 tiles, 3 = 128 x 128 tiles on v_mfma_f32_16x16x32_f16, 0 = the dword-load
