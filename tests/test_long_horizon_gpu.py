@@ -37,7 +37,7 @@ pytestmark = pytest.mark.gpu
 A, G, EPS = 20, 2, 0.5
 TOL = 1e-5
 # (N, envs, episode steps, vector steps, NetMon cell (None: no NetMon), --activation-function, random topology
-#  [, --netmon-iterations K, default 1])
+#  [, --netmon-iterations K, default 1 [, --netmon-agg-type, default sum]])
 CASES = [(20, 4096, 50, 120, "lstm", "leaky_relu", True), (10, 512, 30, 70, "lstm", "leaky_relu", True),
          (30, 512, 30, 70, "lstm", "leaky_relu", True), (40, 512, 30, 70, "lstm", "leaky_relu", True),
          (50, 512, 30, 70, "lstm", "leaky_relu", True), (20, 1024, 50, 120, "lnlstm", "leaky_relu", True),
@@ -45,14 +45,15 @@ CASES = [(20, 4096, 50, 120, "lstm", "leaky_relu", True), (10, 512, 30, 70, "lst
          (20, 512, 30, 70, "lstm", "tanh", True),
          (20, 4096, 50, 120, "lstm", "leaky_relu", False),  # config 3: NetMon on the fixed graph
          (20, 1024, 50, 120, None, "leaky_relu", False),    # config 2: no NetMon, fixed graph
-         (20, 1024, 50, 120, "lstm", "leaky_relu", True, 3)]  # the CLI default --netmon-iterations 3
+         (20, 1024, 50, 120, "lstm", "leaky_relu", True, 3),  # the CLI default --netmon-iterations 3
+         (20, 512, 30, 70, "lstm", "leaky_relu", True, 2, "mean")]  # --netmon-agg-type mean
 # LN-LSTM: fixed upper bound of the fp32 envelope (measured 1.9e-3 state / 1.4e-3 readout for the fp32
 # restatement over 120 steps), so a GPU error growing with the envelope still fails
 ENVELOPE_CAP = 8e-3
 
 
 def case_id(c):
-    return f"N{c[0]}-{c[4] or 'no_netmon'}-{c[5]}" + ("" if c[6] else "-fixed") + (f"-K{c[7]}" if len(c) > 7 else "")
+    return f"N{c[0]}-{c[4] or 'no_netmon'}-{c[5]}" + ("" if c[6] else "-fixed") + (f"-K{c[7]}" if len(c) > 7 else "") + (f"-{c[8]}" if len(c) > 8 else "")
 
 
 def adjacency(topo, N):
@@ -71,6 +72,7 @@ def test_benched_rollout_long_horizon(form, case, monkeypatch, oracle_mod):
 
     N, B, EP, STEPS, RNN, ACT, RANDOM = case[:7]
     K = case[7] if len(case) > 7 else 1
+    AGG = case[8] if len(case) > 8 else "sum"
     SAMPLE = sorted({0, 1, B // 5, B // 2 - 1, B // 2, B // 2 + 1, (4 * B) // 5, B - 1})
 
     gm = importlib.import_module("graph-marl_amd")
@@ -80,7 +82,7 @@ def test_benched_rollout_long_horizon(form, case, monkeypatch, oracle_mod):
     gm._lib.range_status(clear=True)
     net = gm.Network(N, random_topology=RANDOM, excluded_seeds=gm.EVAL_SEEDS, device=0)
     torch.manual_seed(0)
-    netmon = M.NetMon(4 * N + 8, 128, [512, 256], K, rnn_type=RNN, activation=ACT).cuda() if RNN else None
+    netmon = M.NetMon(4 * N + 8, 128, [512, 256], K, rnn_type=RNN, activation=ACT, agg_type=AGG).cuda() if RNN else None
     dqn = M.DQN(6 * N + 10 + (netmon.get_out_features() if RNN else 0), [512, 256], 4, activation=ACT).cuda()
     ro = RO.StreamedRollout(net, A, B, netmon, dqn, groups=G, seed=0, epsilon=EPS, episode_steps=EP, device=0)
     per = B // G
@@ -144,13 +146,13 @@ def test_benched_rollout_long_horizon(form, case, monkeypatch, oracle_mod):
         assert (v["adj"] == adj).all(), f"step {t} env {e}: I+A adjacency"
         if not RNN:  # config 2: the DQN reads the env obs alone
             return ob["obs"].astype(np.float64)
-        out, st = netmon_ref.netmon_forward(Wn, ob["node_obs"][None], adj[None], state64.get(e), RNN, "sum", K, act=ACT)
+        out, st = netmon_ref.netmon_forward(Wn, ob["node_obs"][None], adj[None], state64.get(e), RNN, AGG, K, act=ACT)
         state64[e] = st
         ro_ = netmon_ref.to_network_obs(out, ob["node_agent"][None])[0]
         tol_s = tol_r = TOL
         if fp32_envelope:
             out32, st32 = netmon_ref.netmon_forward(Wn32, ob["node_obs"][None].astype(np.float32),
-                                                    adj[None].astype(np.float32), state32.get(e), RNN, "sum", K,
+                                                    adj[None].astype(np.float32), state32.get(e), RNN, AGG, K,
                                                     act=ACT, dtype=np.float32)
             state32[e] = st32
             ro32 = netmon_ref.to_network_obs(out32, ob["node_agent"][None])[0]
@@ -195,6 +197,6 @@ def test_benched_rollout_long_horizon(form, case, monkeypatch, oracle_mod):
         resets += t % EP == 0
     assert resets == STEPS // EP >= 2
     gm._lib.check_range()
-    print(f"N={N} K={K} {RNN} {ACT} {'random' if RANDOM else 'fixed'} form {form}: worst |err| over {STEPS} steps x "
+    print(f"N={N} K={K} {AGG} {RNN} {ACT} {'random' if RANDOM else 'fixed'} form {form}: worst |err| over {STEPS} steps x "
           f"{len(SAMPLE)} envs: {worst}; worst err / tolerance {ratio['worst']:.3g}"
           + (f"; fp32 restatement of the reference formula vs fp64: {worst32}" if fp32_envelope else ""))
