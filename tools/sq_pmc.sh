@@ -6,7 +6,7 @@ mkdir -p gpurun_out/sq
 export TMPDIR=/tmp
 timeout -s KILL 240 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU \
     SQ_INSTS_LDS SQ_INSTS_SALU SQ_WAVES -T --output-format csv -d gpurun_out/sq -o sq -- python bench.py --steps 10 \
-    --warmup 3 --groups 1 --no-cpu-baseline --no-kernel-timers --no-train --no-f32-compare \
+    --warmup 3 --groups 1 --no-cpu-baseline --no-pmc --no-extras --no-kernel-timers --no-train --no-f32-compare \
     > gpurun_out/sq/bench.log 2>&1 || exit $?
 python - <<'PY' > gpurun_out/sq/summary.txt
 import csv, collections
