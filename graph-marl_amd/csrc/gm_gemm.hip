@@ -62,6 +62,12 @@
 #ifndef GM_HEAD_STAGES
 #define GM_HEAD_STAGES 2  // LDS stages of the fused DQN layer 2 + Q head (gm_gemm_x3_head)
 #endif
+#ifndef GM_LO_E
+#define GM_LO_E 12
+#endif
+#ifndef GM_ROLLOUT_LO_UNSCALED
+#define GM_ROLLOUT_LO_UNSCALED 1  // LDS-DMA GEMMs on rollout operands (AX = 0): low split piece without 2^GM_LO_E
+#endif
 #ifndef GM_NARROW_TILE
 #define GM_NARROW_TILE 0  // 1: 128-column layers with K <= 256 (encoder layer 3) on 64x128 blocks, 3 per CU (tile 15)
 #endif
@@ -226,7 +232,8 @@ __device__ __forceinline__ void act_dispatch(int act, F&& f) {
 }
 
 // Range guard of the split-f16 form: an A element whose pieces leave the f16 range (|a| >=
-// 65520, or a low piece (a - a_hi) * 2^12 >= 65520, possible from |a| >= 2^15) makes every
+// 65520, or a low piece (a - a_hi) * 2^12 >= 65520, possible from |a| >= 2^15 where the low piece
+// is scaled: training operands and the register-staged kernels) makes every
 // accumulator of its row inf or NaN, whatever the epilogue does with it afterwards (the LSTM
 // gates would squash inf to a finite h). One wave-wide vote per tile; lane 0 of a wave that saw
 // a non-finite accumulator stores 1 into the host-mapped status word (gm_gemm_range_status).
@@ -242,16 +249,21 @@ __device__ __forceinline__ void range_guard(const floatx16 (&acc)[TM][TN], unsig
             for (int r = 0; r < 16; r++) bad |= !__builtin_isfinite(acc[i][j][r]);
     if (__ballot(bad) != 0ull && lane == 0) *reinterpret_cast<volatile unsigned*>(flag) = 1u;
 }
+// GM_LO_E: the low piece of the split is scaled by 2^GM_LO_E (12: keeps it a normal f16 for |a| >= 2^-3,
+// the w_hi factor 2^-GM_LO_E restores it; 0: unscaled, a denormal f16 below 2^-14, which the f16 MFMA
+// consumes exactly, and no w_hi scaling)
+constexpr float LO_S = (float)(1 << GM_LO_E);
 // a = hi + 2^-12 lo with hi = f16(a) (RNE), lo = f16((a - hi) * 2^12)
 __device__ __forceinline__ void split4(float4 v, half4& hi, half4& lo) {
     const floatx4 a = {v.x, v.y, v.z, v.w};
     hi = __builtin_convertvector(a, half4);
-    lo = __builtin_convertvector((a - __builtin_convertvector(hi, floatx4)) * 4096.0f, half4);
+    lo = __builtin_convertvector((a - __builtin_convertvector(hi, floatx4)) * LO_S, half4);
 }
 
 // lo = f16(fma(hi, -4096, X)) of a pair (hp = the two f16 hi, X = 4096 x): exact in f32, one rounding
+template <int LOE = GM_LO_E>
 __device__ __forceinline__ unsigned split_lo_pair(unsigned hp, float X0, float X1) {
-    const float m4096 = -4096.0f;
+    const float m4096 = -(float)(1 << LOE);
 #if GM_SPLIT_ASM == 2
     unsigned l;
     asm("v_fma_mixlo_f16 %0, %1, %2, %3 op_sel_hi:[1,0,0]" : "=&v"(l) : "v"(hp), "s"(m4096), "v"(X0));
@@ -270,6 +282,7 @@ __device__ __forceinline__ unsigned split_lo_pair(unsigned hp, float X0, float X
 // split_lo_pair).
 // GM_SPLIT_LDEXP: the split of x * 2^e (e = 0, or a device power-of-two operand scale) with 4096 x by
 // v_ldexp_f32 instead of v_pk_mul_f32 (packed f32 VALU beside MFMAs costs extra issue cycles)
+template <int LOE = GM_LO_E>
 __device__ __forceinline__ void split8(floatx4 x0, floatx4 x1, half8& hi, half8& lo, int e = 0) {
     typedef float floatx2 __attribute__((ext_vector_type(2)));
     typedef _Float16 half2_t __attribute__((ext_vector_type(2)));
@@ -278,14 +291,14 @@ __device__ __forceinline__ void split8(floatx4 x0, floatx4 x1, half8& hi, half8&
     for (int q = 0; q < 4; q++) {
         floatx2 x = q < 2 ? floatx2{x0[2 * q], x0[2 * q + 1]} : floatx2{x1[2 * q - 4], x1[2 * q - 3]};
 #if GM_SPLIT_LDEXP
-        const floatx2 X = {__builtin_ldexpf(x[0], e + 12), __builtin_ldexpf(x[1], e + 12)};
+        const floatx2 X = {__builtin_ldexpf(x[0], e + LOE), __builtin_ldexpf(x[1], e + LOE)};
         if (e != 0) x = floatx2{__builtin_ldexpf(x[0], e), __builtin_ldexpf(x[1], e)};
         hp[q] = __builtin_bit_cast(unsigned, __builtin_convertvector(x, half2_t));
 #else
         hp[q] = __builtin_bit_cast(unsigned, __builtin_convertvector(x, half2_t));
-        const floatx2 X = x * 4096.0f;
+        const floatx2 X = x * (float)(1 << LOE);
 #endif
-        lp[q] = split_lo_pair(hp[q], X[0], X[1]);
+        lp[q] = split_lo_pair<LOE>(hp[q], X[0], X[1]);
     }
     typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
     hi = __builtin_bit_cast(half8, u32x4_t{hp[0], hp[1], hp[2], hp[3]});
@@ -304,7 +317,7 @@ __device__ __forceinline__ void split4e(float4 v, int e, half4& hi, half4& lo) {
     for (int q = 0; q < 2; q++) {
         const floatx2 xs = {__builtin_ldexpf(x[2 * q], e), __builtin_ldexpf(x[2 * q + 1], e)};
         hp[q] = __builtin_bit_cast(unsigned, __builtin_convertvector(xs, half2_t));
-        const float X0 = __builtin_ldexpf(x[2 * q], e + 12), X1 = __builtin_ldexpf(x[2 * q + 1], e + 12);
+        const float X0 = __builtin_ldexpf(x[2 * q], e + GM_LO_E), X1 = __builtin_ldexpf(x[2 * q + 1], e + GM_LO_E);
         lp[q] = split_lo_pair(hp[q], X0, X1);
     }
     typedef unsigned u32x2_t __attribute__((ext_vector_type(2)));
@@ -937,7 +950,7 @@ __global__ __launch_bounds__(WGM* WGN * 64, OCC) void k_gemm3(ASrc a0, ASrc a1, 
             for (int r = 0; r < 16; r++) acc[i][j][r] = 0.f;
 
     const int h = lane >> 5, l32 = lane & 31;
-    const _Float16 s12 = (_Float16)(1.0f / 4096.0f);
+    const _Float16 s12 = (_Float16)(1.0f / LO_S);
     auto compute = [&](int buf) {
         const char* ac = As[buf] + (wr * TM * 32 + l32) * ROWB + 16 * h;
         const char* bc = Bs[buf] + (wc * TN * 32 + l32) * ROWB + 16 * h;
@@ -1363,7 +1376,7 @@ __device__ __forceinline__ void dqn_tail(floatx4 (&acc)[T2][N2], const Epi& ep, 
             half4, __builtin_amdgcn_ds_read_tr16_b64_v4f16((__attribute__((address_space(3))) v4fp16*)(a1)));
         return half8{x0[0], x0[1], x0[2], x0[3], x1[0], x1[1], x1[2], x1[3]};
     };
-    const _Float16 s12 = (_Float16)(1.0f / 4096.0f);
+    const _Float16 s12 = (_Float16)(1.0f / LO_S);
     // A fragments double-buffered in registers: tile kt + 1's reads are issued before tile kt's MFMAs
     half8 fah[2][T2], fal[2][T2];
 #pragma unroll
@@ -1634,8 +1647,12 @@ __global__ __launch_bounds__(WGM* WGN * 64, OCC) void k_gemm3g(ASrc a0, ASrc a1,
     }
     half8 sah[2 * TM], sal[2 * TM];  // 16x16 form: split A of the current k tile (both column halves)
     constexpr bool PINGPONG = GM_PINGPONG && MF == 1 && NW == 8 && STAGES <= 3;
+    // the low split piece: unscaled for the rollout's operands (AX = 0: a denormal f16 below 2^-14, consumed
+    // exactly by the f16 MFMA; no w_hi scaling), scaled by 2^GM_LO_E for the training operands (small
+    // gradient entries keep their low bits)
+    constexpr int LOE = (AX == 0 && GM_ROLLOUT_LO_UNSCALED) ? 0 : GM_LO_E;
     const bool late = wave >= NW / 2;  // wave-uniform (readfirstlane)
-    const _Float16 s12 = (_Float16)(1.0f / 4096.0f);
+    const _Float16 s12 = (_Float16)(1.0f / (float)(1 << LOE));  // 1 when LOE = 0: the multiply folds away
     const float ascale = AX == 2 ? *a0.scale : 1.0f;
     const int aexp = __builtin_amdgcn_frexp_expf(ascale) - 1;  // ascale = 2^aexp
     float amx = 0.f;  // AX 1: max |A| over the fragments this lane reads (all A elements of the tile
@@ -1684,7 +1701,7 @@ __global__ __launch_bounds__(WGM* WGN * 64, OCC) void k_gemm3g(ASrc a0, ASrc a1,
             x0 *= ascale;
             x1 *= ascale;
         }
-        split8(x0, x1, h, l, AX == 2 && GM_SPLIT_LDEXP ? aexp : 0);
+        split8<LOE>(x0, x1, h, l, AX == 2 && GM_SPLIT_LDEXP ? aexp : 0);
     };
     // the MFMAs of column half sb of the current tile on a split A held in (ch, cl) (GM_PINGPONG)
     auto mfma16s = [&](const Frag& f, auto SB, half8 (&ch)[2 * TM], half8 (&cl)[2 * TM]) {
@@ -1719,7 +1736,7 @@ __global__ __launch_bounds__(WGM* WGN * 64, OCC) void k_gemm3g(ASrc a0, ASrc a1,
                 sah[i] = __builtin_bit_cast(half8, x0);
                 sal[i] = __builtin_bit_cast(half8, x1);
 #else
-                split8(x0, x1, sah[i], sal[i], AX == 2 && GM_SPLIT_LDEXP ? aexp : 0);
+                split8<LOE>(x0, x1, sah[i], sal[i], AX == 2 && GM_SPLIT_LDEXP ? aexp : 0);
 #endif
             }
         }
@@ -1755,7 +1772,7 @@ __global__ __launch_bounds__(WGM* WGN * 64, OCC) void k_gemm3g(ASrc a0, ASrc a1,
                 x0 *= ascale;
                 x1 *= ascale;
             }
-            split8(x0, x1, ah[i], al[i], AX == 2 && GM_SPLIT_LDEXP ? aexp : 0);
+            split8<LOE>(x0, x1, ah[i], al[i], AX == 2 && GM_SPLIT_LDEXP ? aexp : 0);
 #endif
         }
 #pragma unroll
@@ -2771,7 +2788,7 @@ __global__ __launch_bounds__(256, 2) void k_gemm3_kmajor(const float* __restrict
 #pragma unroll
             for (int r = 0; r < 16; r++) {
                 const int m = m0 + wr * TM * 32 + i * 32 + 4 * h + (r & 3) + 8 * (r >> 2);
-                if (m < M && n < N) Cz[(long long)m * ldc + n] = (acc[i][j][r] + acc2[i][j][r] * (1.0f / 4096.0f)) * inv;
+                if (m < M && n < N) Cz[(long long)m * ldc + n] = (acc[i][j][r] + acc2[i][j][r] * (1.0f / LO_S)) * inv;
             }
         }
 }
@@ -3017,7 +3034,7 @@ __global__ __launch_bounds__(256, BN == 128 ? 2 : 1) void k_wgrad_tr(const float
 #pragma unroll
                 for (int r = 0; r < 4; r++) {
                     const int m = m0 + wr * TM * 32 + i * 16 + 4 * (lane >> 4) + r;
-                    if (m < M && n < N) Cz[(long long)m * ldc + n] = (c4[i][j][r] + c4b[i][j][r] * (1.0f / 4096.0f)) * inv;
+                    if (m < M && n < N) Cz[(long long)m * ldc + n] = (c4[i][j][r] + c4b[i][j][r] * (1.0f / LO_S)) * inv;
                 }
             }
         return;
@@ -3031,7 +3048,7 @@ __global__ __launch_bounds__(256, BN == 128 ? 2 : 1) void k_wgrad_tr(const float
 #pragma unroll
             for (int r = 0; r < 16; r++) {
                 const int m = m0 + wr * TM * 32 + i * 32 + 4 * hh + (r & 3) + 8 * (r >> 2);
-                if (m < M && n < N) Cz[(long long)m * ldc + n] = (acc[i][j][r] + acc2[i][j][r] * (1.0f / 4096.0f)) * inv;
+                if (m < M && n < N) Cz[(long long)m * ldc + n] = (acc[i][j][r] + acc2[i][j][r] * (1.0f / LO_S)) * inv;
             }
         }
 }
