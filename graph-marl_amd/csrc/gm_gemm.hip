@@ -65,6 +65,9 @@
 #ifndef GM_LO_E
 #define GM_LO_E 12
 #endif
+#ifndef GM_FWD_LO_UNSCALED
+#define GM_FWD_LO_UNSCALED 0  // 1: also the training forward GEMMs (AX = 1) with the unscaled low piece
+#endif
 #ifndef GM_ROLLOUT_LO_UNSCALED
 #define GM_ROLLOUT_LO_UNSCALED 1  // LDS-DMA GEMMs on rollout operands (AX = 0): low split piece without 2^GM_LO_E
 #endif
@@ -1650,7 +1653,7 @@ __global__ __launch_bounds__(WGM* WGN * 64, OCC) void k_gemm3g(ASrc a0, ASrc a1,
     // the low split piece: unscaled for the rollout's operands (AX = 0: a denormal f16 below 2^-14, consumed
     // exactly by the f16 MFMA; no w_hi scaling), scaled by 2^GM_LO_E for the training operands (small
     // gradient entries keep their low bits)
-    constexpr int LOE = (AX == 0 && GM_ROLLOUT_LO_UNSCALED) ? 0 : GM_LO_E;
+    constexpr int LOE = ((AX == 0 || (AX == 1 && GM_FWD_LO_UNSCALED)) && GM_ROLLOUT_LO_UNSCALED) ? 0 : GM_LO_E;
     const bool late = wave >= NW / 2;  // wave-uniform (readfirstlane)
     const _Float16 s12 = (_Float16)(1.0f / (float)(1 << LOE));  // 1 when LOE = 0: the multiply folds away
     const float ascale = AX == 2 ? *a0.scale : 1.0f;
