@@ -76,6 +76,9 @@ def parse():
     p.add_argument("--no-extras", action="store_true",
                    help="skip the other BASELINE configurations (K=3, configs 2/3, config 5 SL) timed after the headline")
     p.add_argument("--extra-steps", type=int, default=100, help="timed vector steps of each extra rollout configuration")
+    p.add_argument("--no-config4", action="store_true",
+                   help="skip the config-4 leg (4096 envs in total over the GPUs, N = 10..50, rollout + training)")
+    p.add_argument("--config4-train-steps", type=int, default=2, help="timed rollout + update steps per config-4 size")
     p.add_argument("--no-pmc", action="store_true",
                    help="skip the same-run rocprofv3 PMC passes (HBM bytes of DQN layer 1 and k_env_step)")
     p.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
@@ -337,13 +340,13 @@ def measure_extras(args, gm, M, RO, timed_region, dev, N, A, x3):
     return out
 
 
-def measure_train(args, gm, M, W, P, net, netmon, dqn, dev, world, rank):
+def measure_train(args, gm, M, W, P, net, netmon, dqn, dev, world, rank, n_env=None, steps=None):
     """Rollout + DQN/NetMon training at the reference's replay ratio: every
     vector step of ALL n_env envs of the GPU (one env batch, one stream) stores its n_env
     transitions in the device replay and runs one update of B sequences x L steps
     (B = 32 n_env / 10: the paper's B=32, L=8 update every 10 env-steps, per env), with the
     gradient all-reduce across ranks (src/main.py:667-1026; graph-marl_amd/train.py).
-    Value = env-steps/s of the whole loop (all ranks)."""
+    Value = env-steps/s of the whole loop (all ranks). n_env / steps default to --n-env / --train-steps."""
     import copy
 
     import importlib as il
@@ -351,7 +354,8 @@ def measure_train(args, gm, M, W, P, net, netmon, dqn, dev, world, rank):
     T = il.import_module("graph-marl_amd.train")
     TS = il.import_module("graph-marl_amd.train_seq")
     RB = il.import_module("graph-marl_amd.replaybuffer")
-    B = args.n_env
+    B = n_env or args.n_env
+    n_steps = steps or args.train_steps
     env = gm.Routing(net, args.n_data, n_env=B, seed=rank * B, obs_extra=netmon.get_out_features(),
                      agent_adjacency=False, device=dev.index)
     wenv = W.NetMonWrapper(env, netmon, 1)
@@ -399,7 +403,7 @@ def measure_train(args, gm, M, W, P, net, netmon, dqn, dev, world, rank):
     if world > 1:
         dist.barrier()
     t0 = time.perf_counter()
-    for _ in range(args.train_steps):
+    for _ in range(n_steps):
         vstep(True)
     torch.cuda.synchronize()
     if world > 1:
@@ -410,11 +414,58 @@ def measure_train(args, gm, M, W, P, net, netmon, dqn, dev, world, rank):
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     el = float(t.item())
-    return {"value": round(B * world * args.train_steps / el, 1), "unit": "env-steps/s", "n_env_per_gpu": B,
-            "ms_per_step": round(1e3 * el / args.train_steps, 3), "steps": args.train_steps,
+    return {"value": round(B * world * n_steps / el, 1), "unit": "env-steps/s", "n_env_per_gpu": B,
+            "ms_per_step": round(1e3 * el / n_steps, 3), "steps": n_steps,
             "update": {"sequences": bsz, "seq_len": L_, "graph_steps": bsz * L_,
                        "path": "train_seq (sequence-batched)" if seq_path else "train.dqn_update (autograd)",
                        "per": "vector step of n_env envs (replay ratio 25.6 = reference B=32, L=8 every 10 steps)"}}
+
+
+CONFIG4_NODES = (10, 20, 30, 40, 50)
+CONFIG4_TOTAL_ENVS = 4096
+
+
+def measure_config4(args, gm, M, W, P, RO, timed_region, dev, world, rank):
+    """BASELINE config 4 as defined: --netmon --random-topology 1 at 10-50-node random graphs, 4096 envs IN
+    TOTAL sharded over the ranks (4096 / world per GPU: strong scaling), rollout alone and rollout + training
+    with the gradient all-reduce (src/main.py:840-1006 wrapped by train.allreduce_gradients), one run per
+    node count (scripts/start_routing_netmon_runs.sh:32-50 runs the random-topology NetMon jobs at these
+    sizes). Every rank takes part in every timed region (barriers, max-over-ranks time). The rollout window
+    is one 50-step episode (one topology reset + NetMon start-up, the reference's rate); the training
+    window --config4-train-steps vector steps, each with one update at the reference's replay ratio."""
+    out = {"workload": "config 4: --netmon --random-topology 1, NetMon K=1 H=128 enc 512,256 lstm + DQN 512,256, "
+                       f"{CONFIG4_TOTAL_ENVS} envs in total over {world} GPU(s)",
+           "total_envs": CONFIG4_TOTAL_ENVS, "envs_per_gpu": CONFIG4_TOTAL_ENVS // world, "n_gpus": world,
+           "scaling": "strong (total envs fixed)", "unit": "env-steps/s", "per_n_nodes": {}}
+    B = CONFIG4_TOTAL_ENVS // world
+    for n in CONFIG4_NODES:
+        rec = {}
+        try:
+            net = gm.Network(n, random_topology=True, excluded_seeds=gm.EVAL_SEEDS, device=dev.index)
+            torch.manual_seed(0)
+            nm = M.NetMon(4 * n + 8, 128, [512, 256], 1).to(dev)
+            dq = M.DQN(6 * n + 10 + nm.get_out_features(), [512, 256], 4).to(dev)
+            ro = RO.StreamedRollout(net, args.n_data, B, nm, dq, groups=args.groups, seed=rank * B, epsilon=args.epsilon,
+                                    episode_steps=args.episode_steps, device=dev.index)
+            g = args.graph if args.graph and args.episode_steps % args.graph == 0 else 0
+            el, _ = timed_region(5, args.episode_steps, False, ro=ro, graph=g)
+            rec["rollout"] = round(B * world * args.episode_steps / el, 1)
+            rec["rollout_ms_per_step"] = round(1e3 * el / args.episode_steps, 4)
+            del ro
+            tr = measure_train(args, gm, M, W, P, net, nm, dq, dev, world, rank, n_env=B, steps=args.config4_train_steps)
+            rec["rollout_train"] = tr["value"]
+            rec["rollout_train_ms_per_step"] = tr["ms_per_step"]
+            rec["update_sequences"] = tr["update"]["sequences"]
+            del nm, dq, net
+        except Exception as ex:  # a config-4 size must never break the headline line
+            if os.environ.get("GM_BENCH_RAISE") == "1" or world > 1:
+                raise  # with peers waiting in collectives a rank must not carry on alone
+            rec = {"value": None, "error": repr(ex)[:300]}
+        out["per_n_nodes"][str(n)] = rec
+        torch.cuda.empty_cache()
+    out["rollout_steps"] = args.episode_steps
+    out["train_steps"] = args.config4_train_steps
+    return out
 
 
 def launch_ranks(args, argv=None):
@@ -452,12 +503,15 @@ def main():
     # GM_BENCH_SHARE_GPU=1 rehearses the N-rank path on one GPU (all ranks on cuda:0, gloo)
     share = os.environ.get("GM_BENCH_SHARE_GPU") == "1"
     if world > 1:
+        import datetime
+
         gpu = 0 if share else local
         torch.cuda.set_device(gpu)
+        timeout = datetime.timedelta(seconds=float(os.environ.get("GM_DIST_TIMEOUT", "900")))
         if share:
-            dist.init_process_group("gloo")
+            dist.init_process_group("gloo", timeout=timeout)
         else:
-            dist.init_process_group("nccl", device_id=torch.device("cuda", gpu))
+            dist.init_process_group("nccl", device_id=torch.device("cuda", gpu), timeout=timeout)
     else:
         torch.cuda.set_device(0)
     dev = torch.device("cuda", torch.cuda.current_device())
@@ -619,6 +673,13 @@ def main():
             where = " <- ".join(f"{fs.name}:{fs.lineno}" for fs in traceback.extract_tb(ex.__traceback__)[::-1][:4])
             train = {"value": None, "error": repr(ex)[:300], "where": where}
 
+    config4 = None
+    if not args.no_config4 and netmon is not None and not args.no_extras:
+        config4 = measure_config4(args, gm, M, W, P, RO, timed_region, dev, world, rank)
+        if extras is None:
+            extras = {}
+        extras["config4"] = config4
+
     pmc = None
     if rank == 0 and world == 1 and not args.no_pmc and netmon is not None and args.netmon_rnn_type == "lstm":
         try:
@@ -657,7 +718,8 @@ def main():
             "metric": METRIC, "value": round(value, 1), "unit": "env-steps/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(1e3 * elapsed / args.steps, 4),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
-            "dtype": "f32 (GEMMs: 3xf16-split MFMA, f32 accumulate)" if x3 else "f32",
+            "dtype": (f"f32 (GEMMs: 3xf16-split MFMA, A low piece scaled 2^{L.build_info().get('x3', '?')[2:]}, "
+                      "f32 accumulate)") if x3 else "f32",
             "data": "synthetic: random-init NetMon+DQN weights, on-device random topologies and packets",
             "config": {"workload": ("routing rollout (no NetMon) + " if netmon is None else
                                     f"routing rollout --netmon (NetMon K={K}, H=128, enc 512,256, {args.netmon_rnn_type}, sum) + ") +

@@ -37,7 +37,7 @@ EXPORTS = [
     "gm_act_fwd", "gm_act_bwd_z", "gm_obs_from_gemm",
 ]
 # kernel-form switches (include/graph_marl_amd_tuning.h)
-TUNING_EXPORTS = ["gm_gemm_set_tile", "gm_gemm_set_wgrad", "gm_gemm_set_mfma", "gm_gemm_set_dgrad"]
+TUNING_EXPORTS = ["gm_gemm_set_tile", "gm_gemm_set_wgrad", "gm_gemm_set_mfma", "gm_gemm_set_dgrad", "gm_gemm_form"]
 
 # Arithmetic form of the fused rollout GEMMs (graph-marl_amd/fused.py): "x3" = split-f16
 # MFMA with fp32 accumulation (default), "f32" = exact fp32 MFMA. GM_GEMM=f32 selects the
@@ -187,6 +187,8 @@ def lib():
             getattr(L, name).argtypes = at
     if hasattr(L, "gm_build_info"):
         L.gm_build_info.restype = C.c_char_p
+    if hasattr(L, "gm_gemm_form"):
+        L.gm_gemm_form.restype = C.c_char_p
     if MFMA_SHAPE is not None:
         if L.gm_gemm_set_mfma({"16": 1, "32": 0, "16all": 2}[MFMA_SHAPE]) != 0:
             raise GMError(L.gm_last_error().decode())
@@ -222,6 +224,8 @@ def build_info():
     if not hasattr(L, "gm_build_info"):
         return {"src": None, "matches_tree": None}
     d = dict(kv.split("=", 1) for kv in L.gm_build_info().decode().split())
+    if hasattr(L, "gm_gemm_form"):  # the arithmetic form the GEMM kernels were compiled with
+        d.update(kv.split("=", 1) for kv in L.gm_gemm_form().decode().split())
     try:
         d["matches_tree"] = d.get("src") == source_hash()
     except OSError:

@@ -40,8 +40,9 @@ __device__ __forceinline__ float gm_act(float v, int act) {
 }
 
 // the precise forms of the rarer activations as ONE out-of-line function per code object: inlined into
-// every GEMM epilogue instantiation they quadrupled the library (7.9 -> 30.9 MB)
-__device__ __noinline__ float gm_act_rare(float v, int act) { return gm_act(v, act); }
+// every GEMM epilogue instantiation they quadrupled the library (7.9 -> 30.9 MB); static: internal linkage,
+// one copy per translation unit (no duplicate symbol under relocatable device code)
+static __device__ __noinline__ float gm_act_rare(float v, int act) { return gm_act(v, act); }
 
 // GEMM epilogues (every tile instantiation carries one): leaky_relu / identity stay a select, the rest
 // branch (wave-uniform act) to short hardware-transcendental forms (v_exp_f32 / v_rcp_f32, absolute

@@ -36,61 +36,18 @@
 #include <cstring>
 #include <type_traits>
 
-#ifndef GM_SPLIT_LDEXP
-#define GM_SPLIT_LDEXP 1  // 0: 4096 x by v_pk_mul_f32 in the split (A/B: rollout -0.9 %, training within noise)
-#endif
-#ifndef GM_SPLIT_ASM
-// lo piece of the split: 0 (default) f32 fma + cvt, compiler-visible; 2 v_fma_mix{lo,hi}_f16 as inline asm
-// followed by s_nop 1. The plain asm form (formerly 1) is removed: the compiler's hazard recognizer does
-// not see an asm statement as a VALU write, so an MFMA could read the lo piece one wait state after the
-// v_fma_mixhi wrote it and take the stale register (32x32x16 k_gemm3g with 3 stages: j = 0 accumulators
-// off by ~1e-4, tools/tile_diag2.py); forms 0 and 2 are exact there, and cost ~1 % on DQN layer 1
-#define GM_SPLIT_ASM 0
-#endif
-#if GM_SPLIT_ASM != 0 && GM_SPLIT_ASM != 2
-#error "GM_SPLIT_ASM must be 0 (compiler-visible split) or 2 (asm + s_nop 1): the bare asm form races the MFMA read"
-#endif
-#ifndef GM_PINGPONG
-// 1 (default): 8-wave 16x16x32 LDS-DMA kernels run the k loop as a ping-pong of the two waves of every SIMD:
-// waves 0..3 do [DMA issue, fragment reads, A split] then the tile's MFMAs; waves 4..7 first run the
-// MFMAs of the tile they read in the previous step, then [DMA, reads, split]; after every barrier one
-// wave of each SIMD feeds the matrix pipe while its partner does the rest (in-kernel stamps showed
-// both waves issuing DMAs and reading fragments in lockstep: ~45 % of a k step without an MFMA). DQN layer 1
-// 182 -> 177 us (2 stages) / 172 us (3 stages, the readout default since), bit-identical results
-#define GM_PINGPONG 1
-#endif
-#ifndef GM_HEAD_STAGES
-#define GM_HEAD_STAGES 2  // LDS stages of the fused DQN layer 2 + Q head (gm_gemm_x3_head)
-#endif
-#ifndef GM_LO_E
+// Arithmetic form (one form, no compile-time alternatives since round 5): the A operand's low split
+// piece is scaled by 2^GM_LO_E (a_lo' = f16((a - a_hi) * 2^12): a normal f16 down to |a| ~ 2^-15) and
+// paired with w_hi * 2^-12, in every kernel incl. the rollout's. Round 4's unscaled low piece on rollout
+// operands (a denormal f16 below |a| = 2^-3, absolute error up to 2^-25 per element) measured 2.1e-5 of
+// sum |a w| on rows of 2^-12 activations at the production tile vs 2.5e-7 scaled and 5e-7 for the exact
+// f32 GEMM (tests/test_gemm_precision_gpu.py); it was removed with the other round-4 variant knobs.
 #define GM_LO_E 12
-#endif
-#ifndef GM_FWD_LO_UNSCALED
-#define GM_FWD_LO_UNSCALED 0  // 1: also the training forward GEMMs (AX = 1) with the unscaled low piece
-#endif
-#ifndef GM_ROLLOUT_LO_UNSCALED
-#define GM_ROLLOUT_LO_UNSCALED 1  // LDS-DMA GEMMs on rollout operands (AX = 0): low split piece without 2^GM_LO_E
-#endif
-#ifndef GM_NARROW_TILE
-#define GM_NARROW_TILE 0  // 1: 128-column layers with K <= 256 (encoder layer 3) on 64x128 blocks, 3 per CU (tile 15)
-#endif
-#ifndef GM_HEAD_SPLIT
-#define GM_HEAD_SPLIT 1  // rollout Q head on 128x128 blocks, partial Q per column block added onto a zeroed q
-#endif
-#ifndef GM_READOUT_TILE
-#define GM_READOUT_TILE (GM_PINGPONG ? 9 : 10)  // LDS-DMA tile of the readout-sourced DQN layer 1 (9: 3 stages, 144 KB)
-#endif
-#ifndef GM_WGRAD_PF2
-#define GM_WGRAD_PF2 1  // k_wgrad_tr (128-wide, 32x32x16): operand loads two k tiles ahead in two register sets
-#endif
-#ifndef GM_K3_ROWPERM
-#define GM_K3_ROWPERM 1  // register-staged k_gemm3: conflict-free LDS stores by a row permutation (see there)
-#endif
-#ifndef GM_PRIO
-#define GM_PRIO 0  // 1: waves 4-7 of the 8-wave LDS-DMA blocks at s_setprio 1 for the k loop (guide: static priority)
-#endif
 #ifndef GM_DIAG
-#define GM_DIAG 0  // 1: no A split, 2: no loads/stores in the k loop, 3: as 2 without barriers
+#define GM_DIAG 0  // 30: per-segment s_memtime stamps of the LDS-DMA k loop (diagnostic build, tools/stamp_bench.py)
+#endif
+#if GM_DIAG != 0 && GM_DIAG != 30
+#error "GM_DIAG must be 0 or 30"
 #endif
 #include <string>
 
@@ -252,9 +209,8 @@ __device__ __forceinline__ void range_guard(const floatx16 (&acc)[TM][TN], unsig
             for (int r = 0; r < 16; r++) bad |= !__builtin_isfinite(acc[i][j][r]);
     if (__ballot(bad) != 0ull && lane == 0) *reinterpret_cast<volatile unsigned*>(flag) = 1u;
 }
-// GM_LO_E: the low piece of the split is scaled by 2^GM_LO_E (12: keeps it a normal f16 for |a| >= 2^-3,
-// the w_hi factor 2^-GM_LO_E restores it; 0: unscaled, a denormal f16 below 2^-14, which the f16 MFMA
-// consumes exactly, and no w_hi scaling)
+// GM_LO_E: the low piece of the split is scaled by 2^12 (a normal f16 down to |a| ~ 2^-15); the w_hi
+// factor 2^-12 restores it
 constexpr float LO_S = (float)(1 << GM_LO_E);
 // a = hi + 2^-12 lo with hi = f16(a) (RNE), lo = f16((a - hi) * 2^12)
 __device__ __forceinline__ void split4(float4 v, half4& hi, half4& lo) {
@@ -264,28 +220,21 @@ __device__ __forceinline__ void split4(float4 v, half4& hi, half4& lo) {
 }
 
 // lo = f16(fma(hi, -4096, X)) of a pair (hp = the two f16 hi, X = 4096 x): exact in f32, one rounding
-template <int LOE = GM_LO_E>
+// (compiler-visible f32: the round-3 inline-asm v_fma_mix form raced an MFMA's read of the lo register,
+// DESIGN.md §4a "Hazard")
 __device__ __forceinline__ unsigned split_lo_pair(unsigned hp, float X0, float X1) {
-    const float m4096 = -(float)(1 << LOE);
-#if GM_SPLIT_ASM == 2
-    unsigned l;
-    asm("v_fma_mixlo_f16 %0, %1, %2, %3 op_sel_hi:[1,0,0]" : "=&v"(l) : "v"(hp), "s"(m4096), "v"(X0));
-    asm("v_fma_mixhi_f16 %0, %1, %2, %3 op_sel:[1,0,0] op_sel_hi:[1,0,0]\n\ts_nop 1" : "+v"(l) : "v"(hp), "s"(m4096), "v"(X1));
-    return l;
-#else
+    constexpr float m4096 = -(float)(1 << GM_LO_E);
     typedef _Float16 half2_t __attribute__((ext_vector_type(2)));
     const half2_t h = __builtin_bit_cast(half2_t, hp);
     const half2_t l = {(_Float16)__builtin_fmaf((float)h[0], m4096, X0), (_Float16)__builtin_fmaf((float)h[1], m4096, X1)};
     return __builtin_bit_cast(unsigned, l);
-#endif
 }
 
 // The same split for 8 floats: hi = cvt_pk (RNE), X = 4096 x (exact), lo = f16(fma(hi, -4096, X)) =
 // f16(4096 (x - hi)) (the fma is exact in f32, so one rounding, RNE: the same bits as split4;
 // split_lo_pair).
-// GM_SPLIT_LDEXP: the split of x * 2^e (e = 0, or a device power-of-two operand scale) with 4096 x by
-// v_ldexp_f32 instead of v_pk_mul_f32 (packed f32 VALU beside MFMAs costs extra issue cycles)
-template <int LOE = GM_LO_E>
+// The split of x * 2^e (e = 0, or a device power-of-two operand scale) with 4096 x by v_ldexp_f32 instead
+// of v_pk_mul_f32 (packed f32 VALU beside MFMAs costs extra issue cycles: rollout +0.9 %)
 __device__ __forceinline__ void split8(floatx4 x0, floatx4 x1, half8& hi, half8& lo, int e = 0) {
     typedef float floatx2 __attribute__((ext_vector_type(2)));
     typedef _Float16 half2_t __attribute__((ext_vector_type(2)));
@@ -293,15 +242,10 @@ __device__ __forceinline__ void split8(floatx4 x0, floatx4 x1, half8& hi, half8&
 #pragma unroll
     for (int q = 0; q < 4; q++) {
         floatx2 x = q < 2 ? floatx2{x0[2 * q], x0[2 * q + 1]} : floatx2{x1[2 * q - 4], x1[2 * q - 3]};
-#if GM_SPLIT_LDEXP
-        const floatx2 X = {__builtin_ldexpf(x[0], e + LOE), __builtin_ldexpf(x[1], e + LOE)};
+        const floatx2 X = {__builtin_ldexpf(x[0], e + GM_LO_E), __builtin_ldexpf(x[1], e + GM_LO_E)};
         if (e != 0) x = floatx2{__builtin_ldexpf(x[0], e), __builtin_ldexpf(x[1], e)};
         hp[q] = __builtin_bit_cast(unsigned, __builtin_convertvector(x, half2_t));
-#else
-        hp[q] = __builtin_bit_cast(unsigned, __builtin_convertvector(x, half2_t));
-        const floatx2 X = x * (float)(1 << LOE);
-#endif
-        lp[q] = split_lo_pair<LOE>(hp[q], X[0], X[1]);
+        lp[q] = split_lo_pair(hp[q], X[0], X[1]);
     }
     typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
     hi = __builtin_bit_cast(half8, u32x4_t{hp[0], hp[1], hp[2], hp[3]});
@@ -805,14 +749,13 @@ __global__ __launch_bounds__(WGM* WGN * 64, OCC) void k_gemm3(ASrc a0, ASrc a1, 
 
     // ---- per-thread source byte offsets (fixed over K) ----
     const int c4 = tid % CPR, rbase = tid / CPR;
-    // GM_K3_ROWPERM: rows permuted inside aligned 8-row blocks (a row's CPR chunks stay on consecutive
+    // rows permuted inside aligned 8-row blocks (a row's CPR chunks stay on consecutive
     // lanes, so every load instruction touches the same lines) so that the LDS stores meet distinct banks
     // at the 4 BK + 16 byte row stride: A (ds_write_b64, 16-lane groups, CPR 4) rows {0,2,4,6} / {1,3,5,7}
     // per group, (CPR 8: 2 rows per group, offset 2); B (ds_write_b128, 8-lane groups, CPR 4) rows {r, r+4}
     const int j8 = rbase & 7;
-    const int rba = !GM_K3_ROWPERM ? rbase
-                    : (rbase & ~7) | (CPR == 4 ? ((j8 & 3) << 1) | (j8 >> 2) : CPR == 8 ? (j8 & 4) | ((j8 & 1) << 1) | ((j8 >> 1) & 1) : j8);
-    const int rbb = !GM_K3_ROWPERM || CPR != 4 ? rbase : (rbase & ~7) | ((j8 & 1) << 2) | (j8 >> 1);
+    const int rba = (rbase & ~7) | (CPR == 4 ? ((j8 & 3) << 1) | (j8 >> 2) : CPR == 8 ? (j8 & 4) | ((j8 & 1) << 1) | ((j8 >> 1) & 1) : j8);
+    const int rbb = CPR != 4 ? rbase : (rbase & ~7) | ((j8 & 1) << 2) | (j8 >> 1);
     int off1[AQ];       // src1 row
     int so[AQ][4];      // DENSE: so[q][0] row; AGGREGATE: member rows; READOUT: segment rows (OOB = none)
     float scale[AQ];
@@ -927,15 +870,7 @@ __global__ __launch_bounds__(WGM* WGN * 64, OCC) void k_gemm3(ASrc a0, ASrc a1, 
             }
             if (amax) amx = fmaxf(amx, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
             half4 hi, lo;
-#if GM_DIAG == 1  // diagnostic build: raw bits instead of the split
-            hi = __builtin_bit_cast(half4, make_float2(v.x, v.y));
-            lo = __builtin_bit_cast(half4, make_float2(v.z, v.w));
-#elif GM_SPLIT_LDEXP
             split4e(v, aexp, hi, lo);
-#else
-            if (ascaled) v = make_float4(v.x * ascale, v.y * ascale, v.z * ascale, v.w * ascale);
-            split4(v, hi, lo);
-#endif
             char* row = as + (rba + q * RSTEP) * ROWB;
             *reinterpret_cast<half4*>(row) = hi;
             *reinterpret_cast<half4*>(row + 32) = lo;
@@ -993,17 +928,10 @@ __global__ __launch_bounds__(WGM* WGN * 64, OCC) void k_gemm3(ASrc a0, ASrc a1, 
     // is already in LDS) and stores tile kt+1 (set (kt+1)&1) into the other buffer
     auto step = [&](auto SET, int kt) {
         constexpr int S = decltype(SET)::value;
-#if GM_DIAG >= 2  // diagnostic builds only: no operand traffic inside the loop
-        compute(S);
-#if GM_DIAG == 2
-        __syncthreads();
-#endif
-#else
         if (kt + 2 < nk) gload(SET, (kt + 2) * BK);
         compute(S);
         if (kt + 1 < nk) lstore(std::integral_constant<int, S ^ 1>{}, S ^ 1, (kt + 1) * BK);
         __syncthreads();
-#endif
     };
     for (int kt = 0; kt < nk; kt += 2) {
         step(S0{}, kt);
@@ -1307,10 +1235,6 @@ template <int T2, int N2, int WGN, int BM, int A = -1>
 __device__ __forceinline__ void dqn_tail(floatx4 (&acc)[T2][N2], const Epi& ep, char* lds, int m0, int wc, int M,
                                          int lane, int tid) {
     static_assert(T2 * 16 == BM, "one wave row holds the block's rows");
-#if GM_DIAG == 20  // diagnostic build 20: layer 1 only (timing only, wrong Q)
-    if (acc[0][0][0] == 12345.f) ep.q[m0] = 1.f;
-    return;
-#endif
     constexpr int K2 = WGN * N2 * 16;  // layer-2 K = layer-1 width
     constexpr int RS = BM * 2;         // image row bytes
     constexpr int NK = K2 / 32;        // layer-2 k tiles
@@ -1387,11 +1311,7 @@ __device__ __forceinline__ void dqn_tail(floatx4 (&acc)[T2][N2], const Epi& ep, 
         fah[0][i] = frag(ih, 0, 16 * i);
         fal[0][i] = frag(il, 0, 16 * i);
     }
-#if GM_DIAG == 21  // diagnostic build 21: no layer-2 k loop (timing only, wrong Q)
-    if (acc2[0][0][0] != 0.f) {
-#else
     {
-#endif
 #pragma unroll
     for (int kt = 0; kt < NK; kt++) {
         const int cur = kt & 1, slot = kt % NB2;
@@ -1649,13 +1569,9 @@ __global__ __launch_bounds__(WGM* WGN * 64, OCC) void k_gemm3g(ASrc a0, ASrc a1,
         }
     }
     half8 sah[2 * TM], sal[2 * TM];  // 16x16 form: split A of the current k tile (both column halves)
-    constexpr bool PINGPONG = GM_PINGPONG && MF == 1 && NW == 8 && STAGES <= 3;
-    // the low split piece: unscaled for the rollout's operands (AX = 0: a denormal f16 below 2^-14, consumed
-    // exactly by the f16 MFMA; no w_hi scaling), scaled by 2^GM_LO_E for the training operands (small
-    // gradient entries keep their low bits)
-    constexpr int LOE = ((AX == 0 || (AX == 1 && GM_FWD_LO_UNSCALED)) && GM_ROLLOUT_LO_UNSCALED) ? 0 : GM_LO_E;
+    constexpr bool PINGPONG = MF == 1 && NW == 8 && STAGES <= 3;
     const bool late = wave >= NW / 2;  // wave-uniform (readfirstlane)
-    const _Float16 s12 = (_Float16)(1.0f / (float)(1 << LOE));  // 1 when LOE = 0: the multiply folds away
+    const _Float16 s12 = (_Float16)(1.0f / LO_S);
     const float ascale = AX == 2 ? *a0.scale : 1.0f;
     const int aexp = __builtin_amdgcn_frexp_expf(ascale) - 1;  // ascale = 2^aexp
     float amx = 0.f;  // AX 1: max |A| over the fragments this lane reads (all A elements of the tile
@@ -1700,13 +1616,10 @@ __global__ __launch_bounds__(WGM* WGN * 64, OCC) void k_gemm3g(ASrc a0, ASrc a1,
         if constexpr (AX == 1) {
 #pragma unroll
             for (int e = 0; e < 4; e++) amx = fmaxf(amx, fmaxf(fabsf(x0[e]), fabsf(x1[e])));
-        } else if constexpr (AX == 2 && !GM_SPLIT_LDEXP) {
-            x0 *= ascale;
-            x1 *= ascale;
         }
-        split8<LOE>(x0, x1, h, l, AX == 2 && GM_SPLIT_LDEXP ? aexp : 0);
+        split8(x0, x1, h, l, AX == 2 ? aexp : 0);
     };
-    // the MFMAs of column half sb of the current tile on a split A held in (ch, cl) (GM_PINGPONG)
+    // the MFMAs of column half sb of the current tile on a split A held in (ch, cl) (ping-pong loop)
     auto mfma16s = [&](const Frag& f, auto SB, half8 (&ch)[2 * TM], half8 (&cl)[2 * TM]) {
         constexpr int sb = decltype(SB)::value;
 #pragma unroll
@@ -1731,25 +1644,13 @@ __global__ __launch_bounds__(WGM* WGN * 64, OCC) void k_gemm3g(ASrc a0, ASrc a1,
                 if constexpr (AX == 1) {
 #pragma unroll
                     for (int e = 0; e < 4; e++) amx = fmaxf(amx, fmaxf(fabsf(x0[e]), fabsf(x1[e])));
-                } else if constexpr (AX == 2 && !GM_SPLIT_LDEXP) {
-                    x0 *= ascale;
-                    x1 *= ascale;
                 }
-#if GM_DIAG == 11  // diagnostic build 11: A read as if stored pre-split (timing only)
-                sah[i] = __builtin_bit_cast(half8, x0);
-                sal[i] = __builtin_bit_cast(half8, x1);
-#else
-                split8<LOE>(x0, x1, sah[i], sal[i], AX == 2 && GM_SPLIT_LDEXP ? aexp : 0);
-#endif
+                split8(x0, x1, sah[i], sal[i], AX == 2 ? aexp : 0);
             }
         }
 #pragma unroll
         for (int j = j0; j < j1; j++) {
-#if GM_DIAG == 11 || GM_DIAG == 12  // diagnostic builds 11, 12: no w_hi scaling (timing only)
-            const half8 bs = f.bh[j];
-#else
             const half8 bs = f.bh[j] * s12;  // w_hi * 2^-12, exact
-#endif
 #pragma unroll
             for (int i = 0; i < 2 * TM; i++) {
                 floatx4& c = acc4[i][sb * TN + j];
@@ -1763,28 +1664,16 @@ __global__ __launch_bounds__(WGM* WGN * 64, OCC) void k_gemm3g(ASrc a0, ASrc a1,
         half8 ah[TM], al[TM];
 #pragma unroll
         for (int i = 0; i < TM; i++) {
-#if GM_DIAG == 10
-            ah[i] = __builtin_bit_cast(half8, f.xa[i][0]);
-            al[i] = __builtin_bit_cast(half8, f.xa[i][1]);
-#else
             floatx4 x0 = f.xa[i][0], x1 = f.xa[i][1];
             if constexpr (AX == 1) {
 #pragma unroll
                 for (int e = 0; e < 4; e++) amx = fmaxf(amx, fmaxf(fabsf(x0[e]), fabsf(x1[e])));
-            } else if constexpr (AX == 2 && !GM_SPLIT_LDEXP) {
-                x0 *= ascale;
-                x1 *= ascale;
             }
-            split8<LOE>(x0, x1, ah[i], al[i], AX == 2 && GM_SPLIT_LDEXP ? aexp : 0);
-#endif
+            split8(x0, x1, ah[i], al[i], AX == 2 ? aexp : 0);
         }
 #pragma unroll
         for (int j = 0; j < TN; j++) {
-#if GM_DIAG == 10
-            const half8 bs = f.bh[j];
-#else
             const half8 bs = f.bh[j] * s12;  // w_hi * 2^-12, exact
-#endif
 #pragma unroll
             for (int i = 0; i < TM; i++) {
                 acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[i], bs, acc[i][j], 0, 0, 0);
@@ -1862,9 +1751,6 @@ __global__ __launch_bounds__(WGM* WGN * 64, OCC) void k_gemm3g(ASrc a0, ASrc a1,
             }
             GM_STAMP(kt, 4);
         };
-#if GM_PRIO
-        if (__builtin_amdgcn_readfirstlane(threadIdx.x) >= 256) __builtin_amdgcn_s_setprio(1);
-#endif
         for (int kt = 0; kt < nk; kt += STAGES) {
             pp_step(I0{}, kt);
             if (kt + 1 < nk) pp_step(I1{}, kt + 1);
@@ -1896,17 +1782,9 @@ __global__ __launch_bounds__(WGM* WGN * 64, OCC) void k_gemm3g(ASrc a0, ASrc a1,
     if (ragged && nk == 1) zero_tail(I0{});
     Frag f0, f1;
     read(I0{}, I0{}, f0);
-#if GM_DIAG == 10
-    read(I0{}, I1{}, f1);
-#endif
     auto step = [&](auto ST, int kt) {
         constexpr int S = decltype(ST)::value;
         using SN = std::integral_constant<int, (S + 1) % STAGES>;
-#if GM_DIAG == 10  // diagnostic build 10: MFMAs only in the k loop (timing only)
-        mfma(f0);
-        mfma(f1);
-        if (kt < 0) {
-#else
         GM_STAMP(kt, 0);
         read(ST, I1{}, f1);
         __builtin_amdgcn_sched_barrier(0);
@@ -1917,7 +1795,6 @@ __global__ __launch_bounds__(WGM* WGN * 64, OCC) void k_gemm3g(ASrc a0, ASrc a1,
         __builtin_amdgcn_sched_barrier(0);
         GM_STAMP(kt, 1);
         if (kt + 1 < nk) {
-#endif
             // own DMA of tile kt+1 landed (tiles kt+2 .. kt+STAGES-1 may stay in flight)
             wait_landed(min(STAGES - 2, nk - 2 - kt));
             GM_STAMP(kt, 2);
@@ -1938,13 +1815,6 @@ __global__ __launch_bounds__(WGM* WGN * 64, OCC) void k_gemm3g(ASrc a0, ASrc a1,
             mfma(f1);
         GM_STAMP(kt, 6);
     };
-#if GM_PRIO
-    if constexpr (NW == 8)
-        if (__builtin_amdgcn_readfirstlane(threadIdx.x) >= 256) __builtin_amdgcn_s_setprio(1);
-#endif
-#if GM_DIAG == 7  // diagnostic build 7: prologue + epilogue only (timing only)
-    if (nk < 0)
-#endif
     for (int kt = 0; kt < nk; kt += STAGES) {
         step(I0{}, kt);
         if (kt + 1 < nk) step(I1{}, kt + 1);
@@ -1955,9 +1825,6 @@ __global__ __launch_bounds__(WGM* WGN * 64, OCC) void k_gemm3g(ASrc a0, ASrc a1,
     }
     }  // !PINGPONG
 
-#if GM_PRIO
-    __builtin_amdgcn_s_setprio(0);
-#endif
 #if GM_DIAG == 30
     if (stw && g_stamps && blockIdx.x < 4096)
         for (int i = 0; i < 64; i++) g_stamps[((size_t)blockIdx.x * 2 + (wave != 0)) * 64 + i] = stl[(wave != 0) * 64 + i];
@@ -2174,9 +2041,9 @@ int dispatch(const ASrc& s0, const ASrc& s1, const float* w, long long ldw, unsi
         } else if (tile >= 8)
             gt = tile;
         else if (tile == -1 && s0.mode == GM_A_READOUT && n > 128)
-            gt = GM_READOUT_TILE;  // ping-pong: 3 stages (two tiles in flight) 177 -> 172 us for DQN layer 1
+            gt = 9;  // ping-pong: 3 stages (two tiles in flight) 177 -> 172 us for DQN layer 1
         else if (tile == -1 && s0.mode == GM_A_DENSE && n >= 128 && K >= 256 && m >= 32768)
-            gt = (GM_NARROW_TILE && n <= 128 && K <= 256 && epilogue != GM_EPI_LSTM) ? 15 : 12;  // N = 128 (the encoder's last layer): 25.9 -> 21.4 us at 40 960 rows
+            gt = 12;  // N = 128 (the encoder's last layer): 25.9 -> 21.4 us at 40 960 rows
 #define GM_GX(WGM, WGN, TM, TN, EP, AXV) \
     launch_g<WGM, WGN, TM, TN, 2, GM_A_DENSE, EP, 2, AXV>(s0, s1, w, ldw, wb, m, n, K, ep, st, wsi)
         if (gt >= 8 && ax) {
@@ -2212,7 +2079,6 @@ int dispatch(const ASrc& s0, const ASrc& s1, const float* w, long long ldw, unsi
         case 12: return GM_G(4, 1, 1, 4, 2, AM, EPI_BIAS, 2);    \
         case 13: return GM_G(2, 2, 2, 2, 2, AM, EPI_BIAS, 2);    \
         case 14: return GM_G(2, 2, 2, 4, 2, AM, EPI_BIAS, 1);    \
-        case 15: return GM_G(2, 2, 1, 2, 2, AM, EPI_BIAS, 3);    \
         default: return GM_G(8, 1, 1, 4, 2, AM, EPI_BIAS, 1);    \
     }
             if (n > 32) {
@@ -2570,7 +2436,7 @@ extern "C" int gm_gemm_x3_head(const gm_a_src* a0, const void* wp, const float* 
     ep.q = q;
     ep.ldq = ldq;
     if ((rc = range_flag(&ep.range_flag))) return rc;
-    if (GM_HEAD_SPLIT && !s0.amax && n > 128 && g_mfma16 == 2) {  // (the 16x16 epilogue adds partials)
+    if (!s0.amax && n > 128 && g_mfma16 == 2) {  // (the 16x16 epilogue adds partials)
         // rollout: 128x128 blocks at 2 per CU (the plain layer's faster tile); each of the two column
         // blocks adds its partial Q to a zeroed q (column block 0 with bq)
         const hipError_t me = hipMemset2DAsync(q, (size_t)ldq * 4, 0, (size_t)nq * 4, (size_t)m, (hipStream_t)stream);
@@ -2580,10 +2446,10 @@ extern "C" int gm_gemm_x3_head(const gm_a_src* a0, const void* wp, const float* 
                                                                 K, ep, (hipStream_t)stream, wscale_inv, g_mfma16 == 2);
     }
     if (s0.amax)  // training forward: max |A| for the layer's weight gradient
-        return launch_g<4, 2, 1, 4, GM_HEAD_STAGES, GM_A_DENSE, EPI_HEAD, 1, 1>(s0, s1, static_cast<const float*>(wp), ldw,
+        return launch_g<4, 2, 1, 4, 2, GM_A_DENSE, EPI_HEAD, 1, 1>(s0, s1, static_cast<const float*>(wp), ldw,
                                                                   (unsigned)wb, m, n, K, ep, (hipStream_t)stream,
                                                                   wscale_inv, g_mfma16 == 2);
-    return launch_g<4, 2, 1, 4, GM_HEAD_STAGES, GM_A_DENSE, EPI_HEAD, 1>(s0, s1, static_cast<const float*>(wp), ldw, (unsigned)wb, m,
+    return launch_g<4, 2, 1, 4, 2, GM_A_DENSE, EPI_HEAD, 1>(s0, s1, static_cast<const float*>(wp), ldw, (unsigned)wb, m,
                                                           n, K, ep, (hipStream_t)stream, wscale_inv, g_mfma16 == 2);
 }
 
@@ -2845,9 +2711,9 @@ __global__ __launch_bounds__(256, BN == 128 ? 2 : 1) void k_wgrad_tr(const float
     // (tid >> 5) + 8 j; B tile 32 x BN: BN / 4 float4 per row
     constexpr int QB = BN / 4, RB_STEP = 256 / QB;
     const int qa = tid & 31, ka0 = tid >> 5, qb = tid % QB, kb0 = tid / QB;
-    // NS register sets of staged operands: 2 (GM_WGRAD_PF2, 128-wide 32x32x16 form) loads tile kt + 2 while
+    // NS register sets of staged operands: 2 (128-wide 32x32x16 form) loads tile kt + 2 while
     // tile kt + 1 waits in the other set for its store, so a load has a whole k step plus the MFMAs to land
-    constexpr int NS = (GM_WGRAD_PF2 && MF == 0 && BN == 128) ? 2 : 1;
+    constexpr int NS = (MF == 0 && BN == 128) ? 2 : 1;
     float4 va[NS][LA], vb[NS][LB];
     auto load = [&](auto SET, int kt) {
         constexpr int S = decltype(SET)::value;
@@ -2874,11 +2740,7 @@ __global__ __launch_bounds__(256, BN == 128 ? 2 : 1) void k_wgrad_tr(const float
 #pragma unroll
         for (int j = 0; j < LA; j++) {
             half4 hi, lo;
-#if GM_SPLIT_LDEXP
             split4e(va[S][j], e_a, hi, lo);
-#else
-            split4(make_float4(va[S][j].x * s_a, va[S][j].y * s_a, va[S][j].z * s_a, va[S][j].w * s_a), hi, lo);
-#endif
             const int o = (ka0 + 8 * j) * RA + ((8 * qa) ^ (MF ? (((ka0 + 8 * j) >> 3) & 1) << 5 : 0));
             *reinterpret_cast<half4*>(ah + o) = hi;
             *reinterpret_cast<half4*>(al + o) = lo;
@@ -2886,11 +2748,7 @@ __global__ __launch_bounds__(256, BN == 128 ? 2 : 1) void k_wgrad_tr(const float
 #pragma unroll
         for (int j = 0; j < LB; j++) {
             half4 hi, lo;
-#if GM_SPLIT_LDEXP
             split4e(vb[S][j], e_b, hi, lo);
-#else
-            split4(make_float4(vb[S][j].x * s_b, vb[S][j].y * s_b, vb[S][j].z * s_b, vb[S][j].w * s_b), hi, lo);
-#endif
             const int o = (kb0 + RB_STEP * j) * RB + ((8 * qb) ^ (MF ? (((kb0 + RB_STEP * j) >> 3) & 1) << 5 : 0));
             *reinterpret_cast<half4*>(bh + o) = hi;
             *reinterpret_cast<half4*>(bl + o) = lo;
@@ -3145,8 +3003,14 @@ extern "C" int gm_gemm_set_mfma(int32_t shape) {
     return GM_OK;
 }
 
+#define GM_STR2(x) #x
+#define GM_STR(x) GM_STR2(x)
+extern "C" const char* gm_gemm_form(void) { return "x3=lo" GM_STR(GM_LO_E) " diag=" GM_STR(GM_DIAG); }
+#undef GM_STR
+#undef GM_STR2
+
 extern "C" int gm_gemm_set_tile(int32_t tile) {
-    if (tile < -1 || tile > 15) return gm_fail(GM_ERR_INVALID_ARG, "gm_gemm_set_tile: tile in [-1, 15]");
+    if (tile < -1 || tile > 14) return gm_fail(GM_ERR_INVALID_ARG, "gm_gemm_set_tile: tile in [-1, 14]");
     g_tile = tile;
     return GM_OK;
 }

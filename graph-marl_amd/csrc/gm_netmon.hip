@@ -1321,54 +1321,26 @@ extern "C" int gm_routing_node_encoder_bits(const float* x, int64_t ldx, const i
         (sbits && ldsb < n / 32))
         return gm_fail(GM_ERR_INVALID_ARG, "gm_routing_node_encoder: bad arguments (n % 64 == 0, 16-byte W^T)");
     const int K = 4 * N + 8;
-    // columns per lane: 2 while the block's W^T slice (K x 128 floats) fits 64 KB (N <= 30); GM_RENC_CPL=2
-    // also above that, with the slice up to 160 KB (one block per CU), GM_RENC_CPL=1 always 1 (A-B knob)
-    static const int cpl_env = [] {
-        const char* e = getenv("GM_RENC_CPL");
-        return e ? atoi(e) : 0;
-    }();
-    const bool two_ok = n % 128 == 0 && (size_t)K * 128 * 4 <= 160 * 1024;
-    const int cpl = (cpl_env == 2 && two_ok) ? 2
-                    : (cpl_env == 1 ? 1 : ((n % 128 == 0 && (size_t)K * 128 * 4 <= 65536) ? 2 : 1));
+    // columns per lane: 2 while the block's W^T slice (K x 128 floats) fits 64 KB (N <= 30), else 1 (2 above
+    // N = 30 with a slice of up to 160 KB at one block per CU measured within noise, round 4)
+    const int cpl = (n % 128 == 0 && (size_t)K * 128 * 4 <= 65536) ? 2 : 1;
     const size_t lds = (size_t)K * 64 * cpl * 4;
     if (lds > 160 * 1024) return gm_fail(GM_ERR_UNSUPPORTED, "gm_routing_node_encoder: 4N+8 too large for the LDS slice");
     const long long M = (long long)G * N;
-    // rows per block: the block's W^T slice (K x BN) is staged once for them, so larger graphs take more
-    // rows. Measured per launch (4096 envs): N = 20 256 / 512 / 1024 rows 60.9 / 61.3 / 75.8 us;
-    // N = 30 117 / 103 / 92 us; N = 40 196 / 178 / 160 us. GM_RENC_ROWS overrides (A-B)
-    static const int tpb_env = [] {
-        const char* e = getenv("GM_RENC_TPB");
-        return e ? atoi(e) : 0;
-    }();
-    static const int rows_env = [] {
-        const char* e = getenv("GM_RENC_ROWS");
-        const int v = e ? atoi(e) : 0;
-        return (v >= 256 && v % 256 == 0) ? v : 0;
-    }();
-    // 8 waves per block share the staged slice (round 3, interleaved rollout A/B, per-launch times): N = 20
-    // 512 rows 54.9 vs 63.8 us (256 rows, 4 waves), N = 30 1024 rows 88.9 vs 111.7 us, N = 40 157.5 vs
-    // 170.5 us, N = 50 222 vs 240 us (rollout +0.1 / +1.7 / +0.7 % at N = 20 / 40 / 50); GM_RENC_TPB=256
-    // restores 4 waves with half the rows
-    const int tpb = tpb_env == 256 ? 256 : 512;
-    const int rows = rows_env ? rows_env : (K <= 88 ? 256 : (K <= 128 ? 512 : 1024)) * (tpb == 512 && K <= 128 ? 2 : 1);
+    // 8 waves per block share the staged W^T slice; rows per block grow with the graph size (the slice is
+    // staged once for them). Round 3, interleaved rollout A/B, per-launch times at 4096 envs: N = 20 512
+    // rows 54.9 vs 63.8 us (256 rows, 4 waves), N = 30 1024 rows 88.9 vs 111.7 us, N = 40 157.5 vs 170.5
+    // us, N = 50 222 vs 240 us
+    const int rows = (K <= 88 ? 256 : (K <= 128 ? 512 : 1024)) * (K <= 128 ? 2 : 1);
     dim3 grid((unsigned)((M + rows - 1) / rows), (unsigned)(n / (64 * cpl)));
 #define GM_RENC(C, A)                                                                                               \
     do {                                                                                                            \
-    if (lds > 65536) {                                                                                              \
-        if (tpb == 512)                                                                                             \
+        if (lds > 65536)                                                                                            \
             (void)hipFuncSetAttribute((const void*)(k_routing_enc<C, A, 512>),                                      \
                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);                        \
-        else                                                                                                        \
-            (void)hipFuncSetAttribute((const void*)(k_routing_enc<C, A>), hipFuncAttributeMaxDynamicSharedMemorySize, \
-                                      (int)lds);                                                                    \
-    }                                                                                                               \
-    if (tpb == 512)                                                                                                 \
         hipLaunchKernelGGL((k_routing_enc<C, A, 512>), grid, dim3(512), lds, (hipStream_t)stream, x, (long long)ldx, \
                            nbr, G, N, wt, b, n, act, y, (long long)ldy, rows, reinterpret_cast<unsigned*>(sbits),    \
                            (long long)ldsb);                                                                        \
-    else                                                                                                            \
-        hipLaunchKernelGGL((k_routing_enc<C, A>), grid, dim3(256), lds, (hipStream_t)stream, x, (long long)ldx, nbr, G, \
-                           N, wt, b, n, act, y, (long long)ldy, rows, reinterpret_cast<unsigned*>(sbits), (long long)ldsb); \
     } while (0)
     if (cpl == 2) {
         if (act == GM_ACT_LEAKY_RELU) GM_RENC(2, 1);

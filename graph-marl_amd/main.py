@@ -28,7 +28,10 @@ Differences from the reference, by design:
     (seeded --seed + rank), starts from rank 0's parameters and averages every update's gradients
     with one all-reduce (train.allreduce_gradients), so the replicas stay identical; rank 0 logs,
     writes the checkpoints and evaluates. The reference runs one independent job per GPU instead
-    (scripts/start_routing_netmon_runs.sh:50).
+    (scripts/start_routing_netmon_runs.sh:50). A rank whose training step raises posts the gradient
+    exchange with a failure flag (train.abort_peers): every other rank raises train.PeerFailure at its
+    next exchange or at the end-of-loop sync, so all ranks leave the loop together and exit non-zero
+    (GM_FAULT=rank:step injects such a failure, for the tests).
 """
 import argparse
 import copy
@@ -403,8 +406,12 @@ def _main(args, rank, world):
     iteration = 0
     t0 = time.time()
     exception_training = None
+    fault = os.environ.get("GM_FAULT")  # "rank:step": that rank raises at that step (failure-path tests)
+    fault = tuple(int(v) for v in fault.split(":")) if fault else None
     try:
         for step in range(1, int(args.total_steps) + 1):
+            if fault == (rank, step):
+                raise RuntimeError(f"GM_FAULT: injected failure on rank {rank} at step {step}")
             if episode_step is None or episode_done:
                 if episode_step is not None:
                     L.check_range()  # split-f16 range guard (graph_marl_amd.h gm_gemm_range_status)
@@ -499,6 +506,15 @@ def _main(args, rank, world):
 
         traceback.print_exc()
         exception_training = e
+        dist_err = getattr(T.dist, "DistError", ())
+        if world > 1 and not isinstance(e, (T.PeerFailure, dist_err)):
+            T.abort_peers(params)  # the peers' next gradient exchange raises PeerFailure: every rank stops
+    if world > 1 and exception_training is None:
+        try:  # meets a peer that failed after this rank's last update
+            T.finish_sync(params)
+        except T.PeerFailure as e:
+            print(f"rank {rank}: {e}", flush=True)
+            exception_training = e
     log_print("Performing clean exit")
     del buff
     metrics = None

@@ -193,7 +193,7 @@ class StreamedRollout:
                 for g, gr in enumerate(self._graphs):
                     with self._on(g):
                         gr.replay()
-                    self.envs[g].mark_obs_stale()
+                        self.envs[g].mark_obs_stale()  # on the group stream: sync_obs waits for it
                 self.ep += self._gsteps
                 if self.ep >= self.episode_steps:
                     L.check_range()

@@ -203,14 +203,22 @@ class Routing:
         return self._lazy_obs
 
     def mark_obs_stale(self):
-        """The env kernels ran outside step_ / reset_ (a replayed HIP graph): in lazy mode the obs rows
-        are rebuilt on the next read."""
+        """The env kernels that just ran (step_ / reset_, or a replayed HIP graph) wrote only the GEMM-ready
+        rows: in lazy mode the obs rows are rebuilt on the next read. Call it on the stream those kernels
+        ran on: it records an event there, and sync_obs orders the rebuild after it (the reader's stream
+        may differ, e.g. StreamedRollout's group streams)."""
         if self._lazy_obs:
             self._obs_stale = True
+            if not torch.cuda.is_current_stream_capturing():
+                ev = self._obs_ev = getattr(self, "_obs_ev", None) or torch.cuda.Event()
+                ev.record(torch.cuda.current_stream(self.device))
 
     def sync_obs(self):
         """Rebuild the agent obs rows from the GEMM-ready copy if the last kernels wrote only that."""
         if self._obs_stale:
+            ev = getattr(self, "_obs_ev", None)
+            if ev is not None:
+                torch.cuda.current_stream(self.device).wait_event(ev)
             L.check(L.lib().gm_obs_from_gemm(self.obs_gemm.data_ptr(), self.obs_gemm.stride(1),
                                              self.n_env * self.n_data, self.n_nodes, self.obs_buf.data_ptr(),
                                              self.obs_stride, self._stream()))

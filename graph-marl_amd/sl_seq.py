@@ -56,8 +56,14 @@ def seq_ok(netmon, rows=None, steps=None):
           and not netmon.output_global_hidden and netmon.iterations >= 1 and H % 32 == 0 and H <= 1024
           and len(enc) >= 1 and all(l.act == 1 and l.bias is not None for l in enc))
     if ok and rows is not None and steps is not None:
-        dev = next(netmon.parameters()).device
-        ok = 1.25 * seq_bytes(netmon, rows, steps) < _device_room(dev)
+        # decided once per (module, rows, steps) shape: the allocator's free memory moves from step to
+        # step, and the path (and with it the summation order) must not flip mid-run
+        key = (rows, steps)
+        cache = netmon.__dict__.setdefault("_sl_seq_fits", {})
+        if key not in cache:
+            dev = next(netmon.parameters()).device
+            cache[key] = 1.25 * seq_bytes(netmon, rows, steps) < _device_room(dev)
+        ok = cache[key]
     return ok
 
 

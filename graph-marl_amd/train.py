@@ -21,30 +21,68 @@ import torch.nn.functional as F
 from . import _lib as GL
 
 
-def allreduce_gradients(params, group=None):
-    """Average .grad over the process group with one bucketed all-reduce."""
-    if not dist.is_available() or not dist.is_initialized() or dist.get_world_size(group) == 1:
+class PeerFailure(RuntimeError):
+    """A rank of the data-parallel job failed (raised on EVERY rank by the next gradient exchange or
+    the end-of-training sync, so the ranks leave the training loop together)."""
+
+
+def _distributed(group=None):
+    return dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1
+
+
+def allreduce_gradients(params, group=None, failed=False):
+    """Average .grad over the process group with ONE bucketed all-reduce. The bucket carries one
+    extra element, the number of ranks that failed: a rank whose step raised posts the same
+    collective with its flag set and zero gradients (abort_peers), so its peers, blocked in this
+    all-reduce, raise PeerFailure instead of waiting for the collective timeout. The
+    bucket size is the same on every rank (a parameter without .grad contributes zeros). One host
+    read of the flag per update, only when world > 1."""
+    if not _distributed(group):
         return
-    grads = [p.grad for p in params if p.grad is not None]
-    if not grads:
-        return
-    flat = torch.cat([g.reshape(-1) for g in grads])
+    parts = [(p.grad if (p.grad is not None and not failed) else torch.zeros_like(p)).reshape(-1) for p in params]
+    flag = parts[0].new_full((1,), 1.0 if failed else 0.0)
+    flat = torch.cat(parts + [flag])
     dist.all_reduce(flat, group=group)
-    flat.div_(dist.get_world_size(group))
+    nfail = int(round(float(flat[-1].item())))
+    if nfail:
+        raise PeerFailure(f"{nfail} of {dist.get_world_size(group)} data-parallel ranks failed; every rank stops")
+    flat = flat[:-1].div_(dist.get_world_size(group))
     off = 0
-    for g in grads:
-        n = g.numel()
-        g.copy_(flat[off:off + n].view_as(g))
+    for p in params:
+        n = p.numel()
+        if p.grad is not None:
+            p.grad.copy_(flat[off:off + n].view_as(p.grad))
         off += n
+
+
+def abort_peers(params, group=None):
+    """Called by a rank whose training step raised: posts the gradient exchange its peers wait in (or
+    will reach next) with the failure flag set. Returns without raising; no-op in a single process."""
+    try:
+        allreduce_gradients(params, group, failed=True)
+    except PeerFailure:
+        pass
+
+
+def finish_sync(params, group=None, failed=False):
+    """End of the training loop on every rank: one more exchange of the same shape, so a rank that
+    failed after its peers' last update still meets them (PeerFailure on every rank if any failed)."""
+    allreduce_gradients(params, group, failed=failed)
+
+
+DIST_TIMEOUT_S = float(os.environ.get("GM_DIST_TIMEOUT", "900"))
 
 
 def init_distributed(use_gpu=True):
     """One process per GPU under a launcher (torch.distributed.run sets RANK / WORLD_SIZE /
     LOCAL_RANK; the reference runs independent jobs per GPU, scripts/start_routing_netmon_runs.sh:50).
     Returns (rank, world, local_rank); world 1 initialises nothing. Backend: RCCL ("nccl") with rank
-    r on cuda:LOCAL_RANK; gloo when use_gpu is False (CPU tests), when GM_DIST_SHARE_GPU=1, or when
-    the node shows fewer GPUs than local ranks (every rank then shares cuda:0: a one-GPU rehearsal).
-    Counting devices does not initialise the GPU."""
+    r on cuda:LOCAL_RANK; gloo when use_gpu is False (CPU tests) or when GM_DIST_SHARE_GPU=1 (every
+    rank on cuda:0: a one-GPU rehearsal). A node that shows fewer GPUs than local ranks is an error
+    (round 4 fell back to gloo on one GPU silently). Every collective times out after
+    GM_DIST_TIMEOUT seconds (default 900). Counting devices does not initialise the GPU."""
+    import datetime
+
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", str(rank)))
@@ -53,15 +91,20 @@ def init_distributed(use_gpu=True):
     if dist.is_initialized():
         return dist.get_rank(), dist.get_world_size(), local
     local_world = int(os.environ.get("LOCAL_WORLD_SIZE", str(world)))
-    share = os.environ.get("GM_DIST_SHARE_GPU") == "1" or (use_gpu and torch.cuda.device_count() < local_world)
+    share = os.environ.get("GM_DIST_SHARE_GPU") == "1"
+    timeout = datetime.timedelta(seconds=DIST_TIMEOUT_S)
+    if use_gpu and not share and torch.cuda.device_count() < local_world:
+        raise RuntimeError(f"{local_world} local ranks but {torch.cuda.device_count()} visible GPUs: one rank per GPU "
+                           "(check HIP_VISIBLE_DEVICES / ROCR_VISIBLE_DEVICES), or GM_DIST_SHARE_GPU=1 for a "
+                           "one-GPU rehearsal over gloo")
     if not use_gpu:
-        dist.init_process_group("gloo")
+        dist.init_process_group("gloo", timeout=timeout)
     elif share:
         torch.cuda.set_device(0)
-        dist.init_process_group("gloo")
+        dist.init_process_group("gloo", timeout=timeout)
     else:
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local), timeout=timeout)
     return dist.get_rank(), dist.get_world_size(), local
 
 

@@ -13,7 +13,7 @@ extern "C" {
  * blocks/CU); of gm_gemm_x3 (-1/0 = 128x128x16; 1 = 128x256x16 (LSTM: 128x128x32);
  * 2 = 128x128x32 (LSTM: 256x128x16)); 8..14 the LDS-DMA tiles of gm_gemm_x3's dense / readout
  * sources (8 = 256x256, 9 = 128x256 3 stages, 10 = 128x256, 12 = 128x128 2 blocks/CU, 13 = 128x128
- * of 64x64 waves, 14 = 128x256 of 64x128 waves, 15 = 64x128 3 blocks/CU). Process-wide. */
+ * of 64x64 waves, 14 = 128x256 of 64x128 waves). Process-wide. */
 /* Weight-gradient kernel of gm_gemm_x3_wgrad (same arithmetic, diagnostics / A-B timing):
  * -1 (default) or 1 = transposed LDS reads (ds_read_b64_tr_b16) with 128 x 128 tiles, 2 = the same
  * with 128 x 256 tiles, 3 = 128 x 128 tiles on v_mfma_f32_16x16x32_f16, 0 = the dword-load
@@ -30,6 +30,10 @@ int gm_gemm_set_mfma(int32_t shape);
  * -1 (default) = per-shape choice, 0 = register-staged 128 x 128 tile (k_gemm3), 1 = LDS-DMA
  * 128 x 128 tile (4 waves, 2 blocks/CU), 2 = LDS-DMA 128 x 256 tile (8 waves). Process-wide. */
 int gm_gemm_set_dgrad(int32_t form);
+/* Arithmetic form the GEMM kernels were compiled with, e.g. "x3=lo12 diag=0": x3=lo12 = split-f16
+ * with the A operand's low piece scaled by 2^12 in every kernel (the only form since round 5);
+ * diag = 0 for the product build, 30 for the k-step stamp build (tools/stamp_bench.py). */
+const char* gm_gemm_form(void);
 
 #ifdef __cplusplus
 }

@@ -899,6 +899,78 @@ def gen_sl(out, Network, Routing, EVAL_SEEDS, NetMon, n=20, seeds=None, H=32, en
     print("sl:", out)
 
 
+def gen_sl_prod(out, Network, NetMon, n=100, graphs=328, det_seed=31, topo_seed=17):
+    """BASELINE config 5 at its production tiles: the CLI-default NetMon (H 128,
+    encoder 512,256, K 1, lstm, sum) on `graphs` valid random 100-node topologies (328 x 100 = 32 800 node
+    rows per GEMM: the LDS-DMA k_gemm3g forms), one train iteration of src/sl.py:360-424 with seq_len 2
+    and the regression-all loss. Stored compactly like train_prod: the topology seeds (drawn by the
+    reference's own _create_valid_network from np.random.seed(topo_seed), EVAL_SEEDS excluded) and
+    their neighbour tables; node features, parameters and the initial state regenerated from detparams
+    (not stored); targets (the reference's APSP weights), predictions and gradients at sampled
+    positions plus row / column sums (_store)."""
+    import torch
+    import torch.nn as nn
+    import torch.nn.functional as F
+
+    from env.constants import EVAL_SEEDS
+
+    d = {}
+    np.random.seed(topo_seed)
+    net = Network(n, random_topology=True, excluded_seeds=list(EVAL_SEEDS))
+    seeds, adj, ta = [], [], []
+    for g in range(graphs):
+        net.reset()
+        seeds.append(net.current_topology_seed)
+        adj.append(net.get_nodes_adjacency().astype(np.float32))  # I + A, as gen_sl passes it
+        t = np.zeros((n, n), np.float32)
+        for v in range(n):
+            for w in range(n):
+                t[v, w] = net.shortest_paths_weights[v][w]
+        ta.append(t)
+    a = np.stack(adj)
+    d["seeds"] = np.array(seeds, np.int64)
+    nbr = np.full((graphs, n, 3), -1, np.int16)
+    for g in range(graphs):
+        for v in range(n):
+            nb = [w for w in np.nonzero(a[g, v])[0] if w != v]
+            nbr[g, v, :len(nb)] = nb
+    d["nbr"] = nbr
+    targets_all = np.stack(ta)
+    x = detparams.det_tensor(det_seed, "node_obs", (graphs, n, 4 * n + 8))  # U(-1/sqrt(fan), ..) scaled below
+    x = (x * np.sqrt(4 * n + 8)).astype(np.float32)  # U(-1, 1) node features
+    torch.manual_seed(3)
+    netmon = NetMon(4 * n + 8, 128, [512, 256], 1, activation_fn=F.leaky_relu, rnn_type="lstm", rnn_carryover=True,
+                    agg_type="sum", output_neighbor_hidden=True, output_global_hidden=False)
+    heads = [nn.Linear(netmon.get_out_features(), k) for k in (4, 1, n)]
+    names = [f"netmon.{k}" for k, _ in netmon.named_parameters()] + \
+        [f"{hn}.{k}" for hn, h in zip(("linear", "linear_reg", "linear_reg_all"), heads) for k, _ in h.named_parameters()]
+    params = list(netmon.parameters()) + [p for h in heads for p in h.parameters()]
+    with torch.no_grad():
+        for nme, p in zip(names, params):
+            p.copy_(torch.tensor(detparams.det_tensor(det_seed, nme, p.shape)))
+    xt = torch.tensor(x)
+    at = torch.tensor(a)
+    eye = torch.eye(n).repeat(graphs, 1, 1)
+    tgt = torch.tensor(targets_all)
+    netmon.state = None
+    seq = []
+    for t in range(2):
+        feats = netmon(xt, at, eye)
+        pred_all = heads[2](feats)
+        _store(d, f"pred_all_{t}", pred_all.detach().numpy().reshape(graphs * n, n), True, det_seed)
+        seq.append(F.mse_loss(pred_all, tgt))
+    total = torch.mean(torch.stack(seq))
+    total.backward()
+    d["loss"] = np.float64(total.item())
+    _store(d, "targets_all", targets_all.reshape(graphs * n, n), True, det_seed)
+    for nme, p in zip(names, params):
+        _store(d, "g_" + nme, p.grad.numpy() if p.grad is not None else np.zeros(p.shape, np.float32), True, det_seed)
+    d["param_names"] = np.array(names)
+    d["config"] = np.array([n, 128, 512, 256, graphs, det_seed], np.int64)
+    np.savez_compressed(out, **d)
+    print("sl_prod:", out, flush=True)
+
+
 def gen_replay(out, ReplayBuffer):
     """ReplayBuffer sampling indices (src/replaybuffer.py:101-130): transitions t = 0, 1, ...
     inserted in order (obs = t), then a script of get_batch calls (uniform and sequence) with
@@ -1069,6 +1141,8 @@ def main():
         seeds100 = np.load(os.path.join(HERE, "topology.npz"))["rand_n100_seed"][:4]
         gen_sl(os.path.join(HERE, "sl_n100.npz"), Network, Routing, EVAL_SEEDS, NetMon, n=100, seeds=seeds100,
                H=128, enc=(512, 256))
+    if only is None or "sl_prod" in only:
+        gen_sl_prod(os.path.join(HERE, "sl_prod.npz"), Network, NetMon)
     if only is None or "replay" in only:
         gen_replay(os.path.join(HERE, "replay.npz"), ReplayBuffer)
     if only is None or "simple" in only:

@@ -33,14 +33,25 @@ def test_library_was_built_from_these_sources(gm):
     assert info["src"] == gm._lib.source_hash(), f"library built from other sources: {info}"
 
 
-def test_library_split_form_is_hazard_free(gm):
-    """The A split of the split-f16 GEMMs is the compiler-visible form (0) or the asm form with its
-    s_nop (2); the bare asm form whose lo register an MFMA could read stale (DESIGN.md §4a Hazard)
-    no longer builds (gm_gemm.hip #error) and the library reports which form it carries."""
+def test_library_reports_only_the_supported_forms(gm):
+    """Round 5 pruned the GEMM variant knobs: the library reports the one split
+    form it carries (x3=lo12: the A operand's low piece scaled by 2^12 in every kernel, pinned at the
+    production tiles by tests/test_gemm_precision_gpu.py) and the product build (diag=0); the only
+    compile-time switch left in gm_gemm.hip is the GM_DIAG stamp build, and the removed forms (the
+    bare asm split that raced the MFMA read, the unscaled low piece, the neutral tile / priority /
+    stage variants) are gone from the source."""
     info = gm._lib.build_info()
-    assert info.get("split_asm") in ("0", "2"), info
+    assert info.get("x3") == "lo12" and info.get("diag") == "0", info
+    assert set(info) == {"src", "arch", "hipcc", "x3", "diag", "matches_tree"}, info
     src = open(os.path.join(ROOT, "graph-marl_amd", "csrc", "gm_gemm.hip")).read()
-    assert "#if GM_SPLIT_ASM != 0 && GM_SPLIT_ASM != 2" in src
+    assert set(re.findall(r"#ifndef (GM_\w+)", src)) == {"GM_DIAG"}
+    for gone in ("GM_SPLIT_ASM", "GM_ROLLOUT_LO_UNSCALED", "GM_FWD_LO_UNSCALED", "GM_NARROW_TILE", "GM_PRIO",
+                 "GM_READOUT_TILE", "GM_HEAD_STAGES", "GM_PINGPONG", "asm(\"v_fma_mix"):
+        assert gone not in src, gone
+    for f in ("gm_netmon.hip", "gm_env.hip"):
+        txt = open(os.path.join(ROOT, "graph-marl_amd", "csrc", f)).read()
+        for gone in ("GM_RENC_CPL", "GM_RENC_TPB", "GM_RENC_ROWS"):
+            assert gone not in txt, (f, gone)
 
 
 def test_library_exports_every_declared_symbol(gm):

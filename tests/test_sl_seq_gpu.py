@@ -91,3 +91,61 @@ def test_sl_seq_matches_autograd_path(K, agg, steps):
         scale = float(ga.abs().max()) + 1e-12
         err = float((ga - gb).abs().max()) / scale
         assert err < 2e-4, (s, err)
+
+
+def _sl_prod():
+    """tests/golden/sl_prod.npz (make_golden.py gen_sl_prod): the reference's config-5 iteration at the
+    production tiles (328 graphs x 100 nodes = 32 800 node rows per GEMM, CLI-default NetMon)."""
+    import sys
+
+    sys.path.insert(0, HERE)
+    import detparams
+    import golden_update as GU
+
+    SL, M = _mods()
+    g = np.load(os.path.join(HERE, "sl_prod.npz"))
+    n, H, e0, e1, graphs, det_seed = (int(v) for v in g["config"])
+    model = SL.NetMonSL(_args(n, H, f"{e0},{e1}"), 4 * n + 8, 4, n).cuda()
+    names = [str(s) for s in g["param_names"]]
+    sd = model.state_dict()
+    model.load_state_dict({s: torch.as_tensor(detparams.det_tensor(det_seed, s, sd[s].shape)) for s in names})
+    x = detparams.det_tensor(det_seed, "node_obs", (graphs, n, 4 * n + 8)) * np.float32(np.sqrt(4 * n + 8))
+    data = SL.build_dataset(n, 20, graphs, 0, seeds=[int(s) for s in g["seeds"]])
+    return SL, M, GU, g, n, graphs, names, model, torch.as_tensor(x, device="cuda"), data
+
+
+@pytest.mark.parametrize("path", ["seq", "autograd"])
+def test_sl_prod_matches_reference(path):
+    """Config 5 pinned at its production tiles: the device topologies of the
+    reference's 328 valid 100-node seeds (neighbour tables, APSP targets) and one training iteration
+    (seq_len 2, regression-all loss) on both unroll paths: predictions at 1e-5 (sampled positions, row /
+    column sums), loss at 1e-5 relative, every parameter gradient at 1e-5 + 1e-4 relative."""
+    SL, M, GU, g, n, graphs, names, model, x, data = _sl_prod()
+    np.testing.assert_array_equal(data.nbr.cpu().numpy(), g["nbr"].astype(np.int32))
+    GU.check(g, "targets_all", data.targets_all.reshape(graphs * n, n), 0, 0, "APSP targets")
+    tgt = data.targets_all
+    nbr = data.nbr
+    model.netmon.state = None
+    if path == "seq":
+        assert SL.SQ.seq_ok(model.netmon)
+        pred = model.forward_seq(x, nbr, 2)
+        preds = [pred[t] for t in range(2)]
+        total = (pred - tgt).pow(2).mean(dim=(1, 2, 3)).mean()
+    else:
+        enc = model.netmon.encode_nodes(x, nbr)
+        preds, seq = [], []
+        for _ in range(2):
+            _, _, pa = model(x, nbr, enc)
+            preds.append(pa)
+            seq.append(torch.nn.functional.mse_loss(pa, tgt))
+        total = torch.mean(torch.stack(seq))
+    for t in range(2):
+        GU.check(g, f"pred_all_{t}", preds[t].detach().reshape(graphs * n, n), 1e-5, 0, f"pred_all step {t}")
+    total.backward()
+    np.testing.assert_allclose(total.item(), float(g["loss"]), rtol=1e-5)
+    params = dict(model.named_parameters())
+    for s in names:
+        if s.startswith("linear.") or s.startswith("linear_reg."):
+            assert params[s].grad is None or float(params[s].grad.abs().max()) == 0.0  # not in the loss
+            continue
+        GU.check(g, "g_" + s, params[s].grad, 1e-5, 1e-4, s)
