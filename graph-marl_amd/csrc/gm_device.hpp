@@ -88,12 +88,13 @@ __device__ __forceinline__ void mt_twist_lds(uint32_t* k) {
     }
 }
 
-// numpy's init_genrand (RandomState.seed(int)); serial chain, written by lane 0.
-__device__ __forceinline__ void mt_seed_lds(uint32_t* k, uint32_t seed) {
+// numpy's init_genrand (RandomState.seed(int)); serial chain, written by lane 0. n < MT_N: only the
+// first n state words (a partial block: LocalRng::seed_partial).
+__device__ __forceinline__ void mt_seed_lds(uint32_t* k, uint32_t seed, int n = MT_N) {
     if (lane_id() == 0) {
         uint32_t v = seed;
         k[0] = v;
-        for (int i = 1; i < MT_N; i++) {
+        for (int i = 1; i < n; i++) {
             v = 1812433253u * (v ^ (v >> 30)) + (uint32_t)i;
             k[i] = v;
         }
@@ -179,14 +180,46 @@ struct MainRng {
 struct LocalRng {
     uint32_t* key;
     int pos;
+    int lim = MT_N;     // generated words valid in key[0, lim) (< MT_N after seed_partial)
+    uint32_t sd = 0;    // the seed (to complete a partial block)
     __device__ void seed(uint32_t s) {
         mt_seed_lds(key, s);
         pos = MT_N;
+        lim = MT_N;
+        sd = s;
+    }
+    // Seed and generate only the first w (<= MT_N - MT_M) words of the first block: word i < 227 of a
+    // generation needs state words i, i + 1 and i + 397 only, so the serial seeding stops at 397 + w
+    // instead of 624 (a topology attempt reads 4N + 1 words; 22 % of the chain at N = 20). A read past
+    // word w rebuilds the whole block (same words).
+    __device__ void seed_partial(uint32_t s, int w) {
+        mt_seed_lds(key, s, MT_M + w);
+        const int l = lane_id();
+        for (int c = 0; c < w; c += WAVE) {  // in place, chunk by chunk like mt_twist_lds
+            const int i = c + l;
+            uint32_t a = 0, b = 0, m = 0;
+            if (i < w) {
+                a = key[i];
+                b = key[i + 1];
+                m = key[i + MT_M];
+            }
+            __syncthreads();
+            if (i < w) key[i] = mt_mix(a, b, m);
+            __syncthreads();
+        }
+        pos = 0;
+        lim = w;
+        sd = s;
     }
     __device__ __forceinline__ uint32_t next32() {
         if (pos == MT_N) {
             mt_twist_lds(key);
             pos = 0;
+        }
+        if (pos >= lim) {  // past a partial block: generate it completely
+            mt_seed_lds(key, sd);
+            mt_twist_lds(key);
+            lim = MT_N;
         }
         return mt_temper(key[pos++]);
     }

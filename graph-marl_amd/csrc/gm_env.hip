@@ -386,6 +386,7 @@ __device__ void load_packets_lds(const EnvDev& d, int env, ES& s) {
 // ---------------------------------------------------------------------------
 template <int NC>
 struct TopoLds {
+    static constexpr int NCAP = NC;
     double x[NC], y[NC], d2[NC];
     uint32_t tkey[MT_N];
     int32_t deg[NC];
@@ -416,10 +417,116 @@ __device__ int64_t draw_topology_seed(const EnvDev& d, R& r) {  // network.py:23
     return sd;
 }
 
+// One _create_random_topology attempt (network.py:122-195) for N <= 64, lane v = node v, the whole
+// state in registers (round 5; the LDS form below took ~100 k cycles per attempt at N = 20, and a reset
+// lasts as long as its worst env's attempt chain: ~17 attempts at 4096 envs). Row i's candidates are
+// taken in the reference's stable sort order of (squared distance, index) without sorting: every lane
+// counts the keys below its own over all nodes (its rank) and over the takeable nodes (its position in
+// the candidate list; the rank-0 node, normally i itself, is skipped like sorted index 0), and the row
+// takes the candidates at positions 0 .. need - 1 by ballot. Takeability (degree < 3, not yet linked to
+// i) is evaluated at the start of the row: no candidate's state changes before it is visited, and the
+// row stops when i has 3 neighbours, so this equals the reference's check at visit time. Edge records go
+// to LDS (one writer, read after the caller's barrier); degrees, edge slots and adjacency bits stay in the
+// owning lane's registers and are written to LDS at the end for topology_finish.
+template <class TS>
+__device__ bool topology_attempt_reg(const EnvDev& d, TS& t, LocalRng& tr) {
+    const int l = lane_id();
+    const int N = d.N;
+    if (tr.pos == MT_N) {
+        mt_twist_lds(tr.key);
+        tr.pos = 0;
+    }
+    const bool live = l < N;
+    double x = 0.0, y = 0.0;
+    if (live) {
+        uint32_t w0 = mt_temper(tr.key[tr.pos + 4 * l]), w1 = mt_temper(tr.key[tr.pos + 4 * l + 1]);
+        uint32_t w2 = mt_temper(tr.key[tr.pos + 4 * l + 2]), w3 = mt_temper(tr.key[tr.pos + 4 * l + 3]);
+        x = ((int32_t)(w0 >> 5) * 67108864.0 + (int32_t)(w1 >> 6)) / 9007199254740992.0;
+        y = ((int32_t)(w2 >> 5) * 67108864.0 + (int32_t)(w3 >> 6)) / 9007199254740992.0;
+    }
+    tr.pos += 4 * N;
+    int deg = 0, ne0 = 0, ne1 = 0, ne2 = 0, n_edges = 0;
+    uint64_t adj = 0ull;
+    for (int i = 0; i < N; i++) {
+        const int need = 3 - readlane(deg, i);
+        if (need <= 0) continue;  // the reference's loop breaks at once
+        const double xi = readlane_f64(x, i), yi = readlane_f64(y, i);
+        const double dx = x - xi, dy = y - yi;
+        const double a = dx * dx, b = dy * dy;
+        const double d2 = a + b;  // >= +0: its IEEE bits order like the values
+        const uint64_t key = live ? (uint64_t)__double_as_longlong(d2) : ~0ull;
+        // edge length of every node as a candidate of row i (network.py:173), all lanes at once
+        const double s10 = sqrt(d2) * 10.0;
+        const int32_t len = ((int32_t)s10) / 2 + 1;
+        // the row's takeable nodes (start-of-row state), as a lane mask
+        const uint64_t okm = ballot(live && deg < 3 && !((adj >> i) & 1ull));
+        // ranks over all NC lanes with immediate lane indices (independent readlanes the compiler can
+        // schedule back to back); pads (l >= N) carry the largest key and are below no live key
+        int rank = 0, okpos = 0;
+#pragma unroll
+        for (int k = 0; k < TS::NCAP; k++) {
+            const uint64_t kk = readlane_u64(key, k);
+            const bool below = kk < key || (kk == key && k < l);  // stable sort: ties by index
+            rank += below;
+            okpos += below && ((okm >> k) & 1ull);
+        }
+        // the rank-0 node is sorted index 0 (skipped); it precedes every other key
+        const int r0 = __builtin_ctzll(ballot(live && rank == 0));
+        const bool r0ok = (okm >> r0) & 1ull;
+        const bool cand = live && l != r0 && ((okm >> l) & 1ull);
+        okpos -= r0ok && l != r0;
+        for (int j = 0; j < need; j++) {
+            const uint64_t hit = ballot(cand && okpos == j);
+            if (!hit) break;
+            const int c = __builtin_ctzll(hit);
+            const int e = n_edges++;
+            if (l == c) {  // the candidate's lane records the edge (one writer)
+                t.ea[e] = i < c ? i : c;
+                t.eb[e] = i < c ? c : i;
+                t.elen[e] = len;
+            }
+            // candidate first, then i (network.py:180-181)
+            if (l == c) {
+                ne0 = deg == 0 ? e : ne0;
+                ne1 = deg == 1 ? e : ne1;
+                ne2 = deg == 2 ? e : ne2;
+                deg += 1;
+                adj |= 1ull << i;
+            }
+            if (l == i) {
+                ne0 = deg == 0 ? e : ne0;
+                ne1 = deg == 1 ? e : ne1;
+                ne2 = deg == 2 ? e : ne2;
+                deg += 1;
+                adj |= 1ull << c;
+            }
+        }
+    }
+    if (live) {
+        t.node_edges[l * 3 + 0] = ne0;
+        t.node_edges[l * 3 + 1] = ne1;
+        t.node_edges[l * 3 + 2] = ne2;
+        t.deg[l] = deg;
+        t.adj[l][0] = adj;
+        t.adj[l][1] = 0ull;
+    }
+    if (l == 0) t.n_edges = n_edges;
+    // validity (network.py:197-213): all degrees 3 and connected
+    if (ballot(live && deg != 3)) return false;
+    const uint64_t full = N == 64 ? ~0ull : ((1ull << N) - 1);
+    uint64_t reach = 1ull, prev = 0ull;
+    while (reach != prev) {
+        prev = reach;
+        reach |= wave_or_u64(((prev >> l) & 1ull) && live ? adj : 0ull);
+    }
+    return reach == full;
+}
+
 // One _create_random_topology attempt from the LDS stream t.tkey (fresh after seeding).
-// Node-indexed work runs in lanes v = l and v = l + 64 (N <= 128).
+// Node-indexed work runs in lanes v = l and v = l + 64 (N <= 128); N <= 64: topology_attempt_reg.
 template <class TS>
 __device__ bool topology_attempt(const EnvDev& d, TS& t, LocalRng& tr) {
+    if constexpr (TS::NCAP <= 64) return topology_attempt_reg(d, t, tr);
     const int l = lane_id();
     const int N = d.N;
     // positions: node i draws x then y (network.py:134-138) = tempered words 4i..4i+3
@@ -535,6 +642,55 @@ __device__ bool topology_attempt(const EnvDev& d, TS& t, LocalRng& tr) {
     return reach[0] == full0 && reach[1] == full1;
 }
 
+// Floyd-Warshall for N <= NC <= 64 with the distance matrix in registers: lane j holds column j
+// (dist[i][j], i < NC: static register indices); pivot k broadcasts column k through LDS (col, NC int32)
+// and dist[k][j] = dist[j][k] (symmetric) is entry j of that column. Integer min-plus: the same result as
+// the LDS form in any order. Pads (i or j >= N) hold INF and never shorten a path.
+template <int NC, class TS>
+__device__ void apsp_reg(const EnvDev& d, int env, const TS& t, int32_t* col) {
+    static_assert(NC <= 64 && NC % 4 == 0, "register APSP needs NC <= 64");
+    const int l = lane_id();
+    const int N = d.N;
+    constexpr int INF = 1 << 20;
+    // column j: 0 on the diagonal, the edge lengths at j's three neighbours (a valid topology is simple
+    // and 3-regular), INF elsewhere
+    int nb[3] = {-1, -1, -1}, ln[3] = {0, 0, 0};
+    if (l < N) {
+#pragma unroll
+        for (int q = 0; q < 3; q++) {
+            const int e = t.node_edges[l * 3 + q];
+            nb[q] = t.ea[e] ^ t.eb[e] ^ l;
+            ln[q] = t.elen[e];
+        }
+    }
+    int dc[NC];
+#pragma unroll
+    for (int i = 0; i < NC; i++)
+        dc[i] = (i == l && l < N) ? 0 : i == nb[0] ? ln[0] : i == nb[1] ? ln[1] : i == nb[2] ? ln[2] : INF;
+    for (int k = 0; k < N; k++) {
+        int32_t* ck = col + (k & 1) * NC;  // double-buffered: one barrier per pivot
+        if (l == k) {
+#pragma unroll
+            for (int i = 0; i < NC; i += 4) *reinterpret_cast<int4*>(ck + i) = make_int4(dc[i], dc[i + 1], dc[i + 2], dc[i + 3]);
+        }
+        __syncthreads();
+        const int dkj = l < NC ? ck[l] : INF;
+#pragma unroll
+        for (int i = 0; i < NC; i += 4) {
+            const int4 v = *reinterpret_cast<const int4*>(ck + i);
+            dc[i] = min(dc[i], v.x + dkj);
+            dc[i + 1] = min(dc[i + 1], v.y + dkj);
+            dc[i + 2] = min(dc[i + 2], v.z + dkj);
+            dc[i + 3] = min(dc[i + 3], v.w + dkj);
+        }
+    }
+    if (l < N) {
+#pragma unroll
+        for (int i = 0; i < NC; i++)
+            if (i < N) d.apsp[((size_t)env * N + i) * N + l] = (int16_t)dc[i];
+    }
+}
+
 template <class TS>
 __device__ void topology_finish(const EnvDev& d, int env, TS& t, int16_t* dist, int64_t seed, int reps) {
     const int l = lane_id();
@@ -562,6 +718,9 @@ __device__ void topology_finish(const EnvDev& d, int env, TS& t, int16_t* dist, 
         d.edge_len[(size_t)env * E + e] = t.elen[e];
     }
     // all-pairs shortest path weights (network.py:274-290) by Floyd-Warshall
+    if constexpr (TS::NCAP <= 64) {
+        apsp_reg<TS::NCAP>(d, env, t, reinterpret_cast<int32_t*>(dist));
+    } else {
     const int16_t INF = 0x3fff;
     for (int idx = l; idx < N * N; idx += WAVE) dist[idx] = (idx / N == idx % N) ? 0 : INF;
     __syncthreads();
@@ -580,6 +739,7 @@ __device__ void topology_finish(const EnvDev& d, int env, TS& t, int16_t* dist, 
         __syncthreads();
     }
     for (int idx = l; idx < N * N; idx += WAVE) d.apsp[(size_t)env * N * N + idx] = dist[idx];
+    }
     if (l == 0) {
         d.topo_seed[env] = seed;
         d.topo_reps[env] = reps;
@@ -593,7 +753,17 @@ __device__ void generate_topology(const EnvDev& d, int env, TS& t, int16_t* dist
                                   bool allow_retry) {
     LocalRng tr;
     tr.key = t.tkey;
-    tr.seed((uint32_t)seed);
+    // an attempt reads 4N position words and, when invalid, the next seed (one more word per rare
+    // rejection): partial blocks while those fit the first MT_N - MT_M words
+    const int w = 4 * d.N + 2;
+    const bool part = w <= MT_N - MT_M;
+    auto reseed = [&](int64_t sd) {
+        if (part)
+            tr.seed_partial((uint32_t)sd, w);
+        else
+            tr.seed((uint32_t)sd);
+    };
+    reseed(seed);
     int reps = 0;
     for (;;) {
         bool ok = topology_attempt(d, t, tr);
@@ -604,7 +774,7 @@ __device__ void generate_topology(const EnvDev& d, int env, TS& t, int16_t* dist
             break;
         }
         seed = draw_topology_seed(d, tr);
-        tr.seed((uint32_t)seed);
+        reseed(seed);
     }
     __syncthreads();
     topology_finish(d, env, t, dist, seed, reps);
@@ -615,7 +785,7 @@ template <int NC>
 struct ResetLds {
     EnvLds<NC> env;
     TopoLds<NC> topo;
-    int16_t dist[NC * NC];  // Floyd-Warshall APSP
+    alignas(16) int16_t dist[NC * NC];  // Floyd-Warshall APSP (NC <= 64: the pivot column buffer)
 };
 
 // src/env/routing.py:160-178 (+ network.py:366-371): new topology (per mode), zero
