@@ -417,17 +417,30 @@ __device__ int64_t draw_topology_seed(const EnvDev& d, R& r) {  // network.py:23
     return sd;
 }
 
+// the smallest key over the lanes with `in` (all lanes hold the result); ~0 when no lane has `in`.
+// Butterfly over the whole wave (every lane active): 6 rounds of two 32-bit shuffles and a 64-bit min
+__device__ __forceinline__ uint64_t argmin_key(uint64_t key, bool in) {
+    uint64_t v = in ? key : ~0ull;
+#pragma unroll
+    for (int m = 1; m < WAVE; m <<= 1) {
+        const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)v, m), hi = (uint32_t)__shfl_xor((int)(uint32_t)(v >> 32), m);
+        const uint64_t o = ((uint64_t)hi << 32) | lo;
+        v = o < v ? o : v;
+    }
+    return v;
+}
+
 // One _create_random_topology attempt (network.py:122-195) for N <= 64, lane v = node v, the whole
 // state in registers (round 5; the LDS form below took ~100 k cycles per attempt at N = 20, and a reset
 // lasts as long as its worst env's attempt chain: ~17 attempts at 4096 envs). Row i's candidates are
-// taken in the reference's stable sort order of (squared distance, index) without sorting: every lane
-// counts the keys below its own over all nodes (its rank) and over the takeable nodes (its position in
-// the candidate list; the rank-0 node, normally i itself, is skipped like sorted index 0), and the row
-// takes the candidates at positions 0 .. need - 1 by ballot. Takeability (degree < 3, not yet linked to
-// i) is evaluated at the start of the row: no candidate's state changes before it is visited, and the
-// row stops when i has 3 neighbours, so this equals the reference's check at visit time. Edge records go
-// to LDS (one writer, read after the caller's barrier); degrees, edge slots and adjacency bits stay in the
-// owning lane's registers and are written to LDS at the end for topology_finish.
+// taken in the reference's stable sort order of (squared distance, index) without sorting: the first
+// element (sorted index 0, normally i itself) and then the takeable nodes one by one as wave minima of
+// the distance bits (non-negative doubles order like their bit patterns) with the lowest index among
+// equal keys. Takeability (degree < 3, not yet linked to i) is evaluated at the start of the row: no
+// candidate's state changes before it is visited, and the row stops when i has 3 neighbours, so this
+// equals the reference's check at visit time. Edge records go to LDS (written by the candidate's lane,
+// read after the caller's barrier); degrees, edge slots and adjacency bits stay in the owning lane's
+// registers and are written to LDS at the end for topology_finish.
 template <class TS>
 __device__ bool topology_attempt_reg(const EnvDev& d, TS& t, LocalRng& tr) {
     const int l = lane_id();
@@ -458,27 +471,19 @@ __device__ bool topology_attempt_reg(const EnvDev& d, TS& t, LocalRng& tr) {
         // edge length of every node as a candidate of row i (network.py:173), all lanes at once
         const double s10 = sqrt(d2) * 10.0;
         const int32_t len = ((int32_t)s10) / 2 + 1;
-        // the row's takeable nodes (start-of-row state), as a lane mask
-        const uint64_t okm = ballot(live && deg < 3 && !((adj >> i) & 1ull));
-        // ranks over all NC lanes with immediate lane indices (independent readlanes the compiler can
-        // schedule back to back); pads (l >= N) carry the largest key and are below no live key
-        int rank = 0, okpos = 0;
-#pragma unroll
-        for (int k = 0; k < TS::NCAP; k++) {
-            const uint64_t kk = readlane_u64(key, k);
-            const bool below = kk < key || (kk == key && k < l);  // stable sort: ties by index
-            rank += below;
-            okpos += below && ((okm >> k) & 1ull);
-        }
-        // the rank-0 node is sorted index 0 (skipped); it precedes every other key
-        const int r0 = __builtin_ctzll(ballot(live && rank == 0));
-        const bool r0ok = (okm >> r0) & 1ull;
-        const bool cand = live && l != r0 && ((okm >> l) & 1ull);
-        okpos -= r0ok && l != r0;
-        for (int j = 0; j < need; j++) {
-            const uint64_t hit = ballot(cand && okpos == j);
-            if (!hit) break;
+        // sorted index 0 (skipped: normally i itself) = the first (key, index) of all nodes; then the
+        // candidates in sort order = successive (key, index) minima over the takeable nodes (the row's
+        // start-of-row state, a lane mask), each a wave min + ballot (ties: the lowest index, as the
+        // stable sort keeps them)
+        const uint64_t kmin = argmin_key(key, live);  // outside any condition: every lane takes part
+        const uint64_t r0m = ballot(live && key == kmin);
+        uint64_t cands = ballot(live && deg < 3 && !((adj >> i) & 1ull)) & ~(r0m & (0ull - r0m));
+        for (int j = 0; j < need && cands; j++) {
+            const bool in = (cands >> l) & 1ull;
+            const uint64_t cmin = argmin_key(key, in);
+            const uint64_t hit = ballot(in && key == cmin);
             const int c = __builtin_ctzll(hit);
+            cands &= ~(1ull << c);
             const int e = n_edges++;
             if (l == c) {  // the candidate's lane records the edge (one writer)
                 t.ea[e] = i < c ? i : c;

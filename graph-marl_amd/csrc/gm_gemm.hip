@@ -89,6 +89,8 @@ struct ASrc {
                               // kernels address its rows relative to their block's first row)
     const float* scale;       // k_gemm3 DENSE source: power-of-two A scale (nullable)
     unsigned* amax;           // k_gemm3: max |A| float bits published here (nullable)
+    const float* bias0;       // ROUTING_ENC: the folded encoder layer's bias (nullable) and activation
+    int act0;
 };
 
 struct Epi {
@@ -1396,16 +1398,25 @@ __global__ __launch_bounds__(WGM* WGN * 64, OCC) void k_gemm3g(ASrc a0, ASrc a1,
                                                               Epi ep, const float* __restrict__ wscale_inv) {
     constexpr int BK = 32, NW = WGM * WGN;
     constexpr int BM = WGM * TM * 32, BN = WGN * TN * 32;
+    // ROUTING_ENC (RENC): the A tile is computed in the block from the routing node observations and the
+    // folded encoder layer's W0^T, whose 32-column slice per k tile is DMA'd (RW pieces of 8 rows per wave)
+    constexpr bool RENC = AMODE == GM_A_ROUTING_ENC;
+    constexpr int RW = RENC ? 2 : 0;                     // W0^T slice pieces per wave: 4N + 8 <= 8 NW RW rows
     constexpr int NA = BM / 8 / NW, NB = BN / 8 / NW;  // DMA instructions per wave per tile
-    constexpr int NL = NA + NB;
+    constexpr int NAD = RENC ? 0 : NA;                   // A pieces actually DMA'd
+    constexpr int NL = NAD + NB + RW;
     constexpr int STAGE_B = (BM + BN) * 128;
+    constexpr int W0S_B = 8 * NW * RW * 128;             // one W0^T slice stage
+    constexpr int RENC_B = RENC ? 2 * W0S_B + 4 * 1024 : 0;  // two slice stages + the bias (<= 1024 columns)
     static_assert(BM % (8 * NW) == 0 && BN % (8 * NW) == 0, "tile rows per wave");
     static_assert(AMODE != GM_A_AGGREGATE, "aggregate source uses k_gemm3");
     static_assert(STAGES >= 2 && STAGES <= 4, "stages");
+    static_assert(!RENC || (STAGES == 2 && BM * 4 == NW * 64 && MF == 1 && NW == 8),
+                  "routing-encoder source: 2-stage ping-pong tile, 4 threads per A row");
 #if GM_DIAG == 30
-    __shared__ __attribute__((aligned(16))) char lds[STAGES * STAGE_B + 1024];
+    __shared__ __attribute__((aligned(16))) char lds[STAGES * STAGE_B + RENC_B + 1024];
 #else
-    __shared__ __attribute__((aligned(16))) char lds[STAGES * STAGE_B];
+    __shared__ __attribute__((aligned(16))) char lds[STAGES * STAGE_B + RENC_B];
 #endif
 
     const int tid = threadIdx.x, lane = tid & 63;
@@ -1435,7 +1446,7 @@ __global__ __launch_bounds__(WGM* WGN * 64, OCC) void k_gemm3g(ASrc a0, ASrc a1,
     int so[NA][4];  // DENSE: [0]; READOUT: segment rows (OOB = none)
     int o1[NA];     // second (dense) source
 #pragma unroll
-    for (int j = 0; j < NA; j++) {
+    for (int j = 0; j < NAD; j++) {
         const int R = (wave * NA + j) * 8 + sub;
         const int c = (lane & 7) ^ gswz<MF>((R >> 1) & 7);
         const int row = min(m0 + R, M - 1);
@@ -1444,7 +1455,7 @@ __global__ __launch_bounds__(WGM* WGN * 64, OCC) void k_gemm3g(ASrc a0, ASrc a1,
         for (int s = 0; s < 4; s++) so[j][s] = OOB;
         if (AMODE == GM_A_DENSE) {
             so[j][0] = (int)((row - m0) * a0.ld0) * 4 + 16 * c;
-        } else {  // READOUT: [h_final[v] | h_prev[nbr(v, 0..2)]], v = agent_node[row]
+        } else if constexpr (AMODE == GM_A_READOUT) {  // [h_final[v] | h_prev[nbr(v, 0..2)]], v = agent_node[row]
             const int g = row / a0.rows_per_graph;
             const int v = a0.agent_node[row];
             const int* nb = a0.nbr + ((size_t)g * a0.n_nodes + v) * a0.deg;
@@ -1470,15 +1481,97 @@ __global__ __launch_bounds__(WGM* WGN * 64, OCC) void k_gemm3g(ASrc a0, ASrc a1,
     const __amdgpu_buffer_rsrc_t r1 = a1.p0 ? rsrc_rows(a1.p0, a1.ld0, m0, a1.bytes0) : rsrc(a0.p0, 0u);
     const __amdgpu_buffer_rsrc_t rw = rsrc(reinterpret_cast<const float*>(w), wbytes);
 
-    // DMA of k tile kt into stage ST (all LDS bases wave-uniform)
+    // ---- ROUTING_ENC: this thread's A row (4 threads per row, 8 consecutive k each) and its node-obs
+    // features: A[r][k] = act0(b0[k] + W0^T[v][k] + cnt W0^T[N][k] + load W0^T[N + 1][k] + sum over the
+    // 3 neighbour blocks (W0^T[off + u][k] + len W0^T[off + N][k] + load W0^T[off + N + 1][k])), the
+    // 12 nonzero columns of the node observation [onehot(n) | cnt | load | 3 x (onehot(nbr) | len |
+    // load)] (src/env/routing.py:187-235), in k_routing_enc's order of operations ----
+    const int rr = tid >> 2, rq = tid & 3;
+    int r_oh[4] = {0, 0, 0, 0};
+    float r_sv[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    int wso[RW > 0 ? RW : 1];
+    if constexpr (RENC) {
+        const int Nn = a0.n_nodes;
+        const int row = min(m0 + rr, M - 1);
+        const int g = row / Nn, v = row - g * Nn;
+        const float* xr = a0.p0 + (long long)row * a0.ld0;
+        const int* nb = a0.nbr + ((long long)g * Nn + v) * 3;
+        r_oh[0] = v;
+        r_sv[0] = xr[Nn];
+        r_sv[1] = xr[Nn + 1];
+#pragma unroll
+        for (int k = 0; k < 3; k++) {
+            const int off = Nn + 2 + k * (Nn + 2);
+            r_oh[k + 1] = off + nb[k];
+            r_sv[2 + 2 * k] = xr[off + Nn];
+            r_sv[3 + 2 * k] = xr[off + Nn + 1];
+        }
+        const int K0 = 4 * Nn + 8;
+#pragma unroll
+        for (int j = 0; j < RW; j++) {
+            const int R = (wave * RW + j) * 8 + sub;
+            wso[j] = R < K0 ? (int)(R * a0.ld1) * 4 + 16 * (lane & 7) : OOB;
+        }
+        // the folded layer's bias for all k, once (plain loads: retired before the k loop's counted waits)
+        float* b0s = reinterpret_cast<float*>(lds + STAGES * STAGE_B + 2 * W0S_B);
+        for (int k = tid; k < a0.k; k += NW * 64) b0s[k] = a0.bias0 ? a0.bias0[k] : 0.f;
+    }
+    const __amdgpu_buffer_rsrc_t rw0 = rsrc(RENC ? a0.p1 : a0.p0, RENC ? (unsigned)a0.bytes1 : 0u);
+    // DMA of the W0^T slice of k tile kt (32 columns of every input row) into slice stage kt & 1
+    auto issue_w0 = [&](int kt) {
+        char* base = lds + STAGES * STAGE_B + (kt & 1) * W0S_B + wave * RW * 1024;
+#pragma unroll
+        for (int j = 0; j < RW; j++) dma16(rw0, base + j * 1024, wso[j], kt * BK * 4);
+    };
+    // A tile kt into stage ST from slice stage kt & 1 (landed and published by a barrier)
+    auto renc_a = [&](auto ST, int kt) {
+        const float* wsl = reinterpret_cast<const float*>(lds + STAGES * STAGE_B + (kt & 1) * W0S_B);
+        const float* b0s = reinterpret_cast<const float*>(lds + STAGES * STAGE_B + 2 * W0S_B) + kt * BK;
+        char* adst = lds + decltype(ST)::value * STAGE_B;
+        const int Nn = a0.n_nodes;
+        auto wrow = [&](int r, int c) { return *reinterpret_cast<const float4*>(wsl + r * BK + 4 * c); };
+#pragma unroll
+        for (int h = 0; h < 2; h++) {
+            const int c = 2 * rq + h;  // 16-byte chunk: k = 4c .. 4c + 3 of the tile
+            const float4 bz = *reinterpret_cast<const float4*>(b0s + 4 * c);
+            const float4 e0 = wrow(r_oh[0], c), wa = wrow(Nn, c), wb = wrow(Nn + 1, c);
+            float a[4] = {bz.x + e0.x + r_sv[0] * wa.x + r_sv[1] * wb.x, bz.y + e0.y + r_sv[0] * wa.y + r_sv[1] * wb.y,
+                          bz.z + e0.z + r_sv[0] * wa.z + r_sv[1] * wb.z, bz.w + e0.w + r_sv[0] * wa.w + r_sv[1] * wb.w};
+#pragma unroll
+            for (int k = 0; k < 3; k++) {
+                const int off = Nn + 2 + k * (Nn + 2);
+                const float4 ek = wrow(r_oh[k + 1], c), wl = wrow(off + Nn, c), wd = wrow(off + Nn + 1, c);
+                const float ln = r_sv[2 + 2 * k], ld = r_sv[3 + 2 * k];
+                a[0] += ek.x + ln * wl.x + ld * wd.x;
+                a[1] += ek.y + ln * wl.y + ld * wd.y;
+                a[2] += ek.z + ln * wl.z + ld * wd.z;
+                a[3] += ek.w + ln * wl.w + ld * wd.w;
+            }
+#pragma unroll
+            for (int e = 0; e < 4; e++) a[e] = a0.act0 == 1 ? act_t<1>(a[e], 1) : act_t<-1>(a[e], a0.act0);
+            *reinterpret_cast<float4*>(adst + rr * 128 + ((c ^ gswz<MF>((rr >> 1) & 7)) << 4)) =
+                make_float4(a[0], a[1], a[2], a[3]);
+        }
+    };
+
+    // DMA of k tile kt into stage ST (all LDS bases wave-uniform); ROUTING_ENC: the B tile, the next
+    // W0^T slice, and the A tile computed from this tile's slice
     auto issue = [&](auto ST, int kt) {
         char* base = lds + decltype(ST)::value * STAGE_B + wave * NA * 1024;
         const int k0 = kt * BK;
+        if constexpr (RENC) {
+            char* bbase = lds + decltype(ST)::value * STAGE_B + BM * 128 + wave * NB * 1024;
+#pragma unroll
+            for (int j = 0; j < NB; j++) dma16(rw, bbase + j * 1024, wo[j], k0 * 4);
+            if ((kt + 1) * BK < K) issue_w0(kt + 1);
+            renc_a(ST, kt);
+            return;
+        }
         if (k0 < a0.k) {
             if (AMODE == GM_A_DENSE) {
 #pragma unroll
                 for (int j = 0; j < NA; j++) dma16(r0a, base + j * 1024, so[j][0], k0 * 4);
-            } else {
+            } else if constexpr (AMODE == GM_A_READOUT) {
                 const int seg = k0 / a0.hidden, ko = (k0 - seg * a0.hidden) * 4;
                 // OOB + ko stays out of range, so missing neighbours need no select
                 switch (seg) {
@@ -1715,6 +1808,11 @@ __global__ __launch_bounds__(WGM* WGN * 64, OCC) void k_gemm3g(ASrc a0, ASrc a1,
             mfma16s(fa, I0{}, sah, sal);
             mfma16s(fb, I1{}, sah, sal);
         };
+        if constexpr (RENC) {  // the first slice lands and is published before tile 0's A is computed
+            issue_w0(0);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();
+        }
         issue(I0{}, 0);
         if constexpr (STAGES == 3)
             if (nk > 1) issue(I1{}, 1);
@@ -1913,7 +2011,10 @@ int launch_g(const ASrc& a0, const ASrc& a1, const float* w, long long ldw, unsi
              const Epi& ep, hipStream_t st, const float* wscale_inv, int mf = -1) {
     constexpr int BM = WGM * TM * 32, BN = WGN * TN * 32;
     const int T = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
-    if (mf < 0 ? g_mfma16 : mf)
+    if constexpr (AMODE == GM_A_ROUTING_ENC)  // 16x16x32 only
+        hipLaunchKernelGGL((k_gemm3g<WGM, WGN, TM, TN, STAGES, AMODE, EPI, OCC, AX, 1>), dim3(T), dim3(WGM * WGN * 64), 0,
+                           st, a0, a1, reinterpret_cast<const _Float16*>(w), ldw, wbytes, M, N, K, ep, wscale_inv);
+    else if (mf < 0 ? g_mfma16 : mf)
         hipLaunchKernelGGL((k_gemm3g<WGM, WGN, TM, TN, STAGES, AMODE, EPI, OCC, AX, 1>), dim3(T), dim3(WGM * WGN * 64), 0,
                            st, a0, a1, reinterpret_cast<const _Float16*>(w), ldw, wbytes, M, N, K, ep, wscale_inv);
     else
@@ -1957,7 +2058,7 @@ int g_tile = -1;  // tile configuration override (gm_gemm_set_tile), -1 = per-sh
 
 bool fits(long long bytes) { return bytes >= 0 && bytes < (1ll << 31) - (1 << 24); }
 
-int to_asrc(const gm_a_src* s, int M, ASrc& o) {
+int to_asrc_any(const gm_a_src* s, int M, ASrc& o) {
     memset(&o, 0, sizeof(o));
     if (!s) return GM_OK;
     o.mode = s->mode;
@@ -1975,8 +2076,22 @@ int to_asrc(const gm_a_src* s, int M, ASrc& o) {
     o.hidden = s->hidden;
     o.scale = s->scale;
     o.amax = reinterpret_cast<unsigned*>(s->amax);
+    o.bias0 = s->bias0;
+    o.act0 = s->act0;
     if (s->scale && s->mode != GM_A_DENSE)
         return gm_fail(GM_ERR_INVALID_ARG, "gm_gemm: an A scale needs a DENSE source");
+    if (s->mode == GM_A_ROUTING_ENC) {
+        const long long K0 = 4ll * s->n_nodes + 8;
+        if (!s->p0 || !s->p1 || !s->nbr || s->deg != 3 || s->n_nodes < 4 || K0 > 128 || s->k <= 0 || (s->k % BKMAX) ||
+            s->k > 1024 || s->ld0 < K0 || s->ld1 < s->k || (s->ld1 & 3) || (reinterpret_cast<uintptr_t>(s->p1) & 15) ||
+            (M % s->n_nodes) || s->act0 < GM_ACT_NONE || s->act0 > GM_ACT_LAST || s->amax)
+            return gm_fail(GM_ERR_UNSUPPORTED, "gm_gemm: routing-encoder source needs deg 3, 4N + 8 <= 128, k % 32 == 0, "
+                                               "k <= 1024, ld1 >= k (16-byte W0^T rows), M = G * N");
+        o.bytes0 = ((long long)(M - 1) * s->ld0 + K0) * 4;
+        o.bytes1 = ((K0 - 1) * s->ld1 + s->k) * 4;
+        if (!fits(o.bytes0) || !fits(o.bytes1)) return gm_fail(GM_ERR_UNSUPPORTED, "gm_gemm: routing-encoder source > 2 GB");
+        return GM_OK;
+    }
     if (!s->p0 || s->k <= 0 || (s->ld0 & 3) || (reinterpret_cast<uintptr_t>(s->p0) & 15))
         return gm_fail(GM_ERR_INVALID_ARG, "gm_gemm_f32: A source needs p0, k > 0, ld0 % 4 == 0, 16-byte base");
     long long rows0 = M;
@@ -2009,6 +2124,13 @@ int to_asrc(const gm_a_src* s, int M, ASrc& o) {
     return GM_OK;
 }
 
+// the A sources of every entry but gm_gemm_x3: no ROUTING_ENC
+int to_asrc(const gm_a_src* s, int M, ASrc& o, bool renc_ok = false) {
+    if (s && s->mode == GM_A_ROUTING_ENC && !renc_ok)
+        return gm_fail(GM_ERR_UNSUPPORTED, "routing-encoder A source: gm_gemm_x3 only");
+    return to_asrc_any(s, M, o);
+}
+
 // Tile tables. F32: per-shape default from tools/gemm_bench.py on MI355X (BK=16 for short
 // K, narrow N and the readout layer; BK=32 for K=512, N>=256). X3: 128x128x16 tiles
 // (49 KB of LDS: 3 blocks/CU), LSTM 128 rows x 4 gate tiles.
@@ -2031,6 +2153,13 @@ int dispatch(const ASrc& s0, const ASrc& s1, const float* w, long long ldw, unsi
         // training operands (forward GEMMs publishing max|A|, input-gradient GEMMs on a scaled A):
         // the LDS-DMA kernel's 128x128 tile at 2 blocks/CU for large dense GEMMs, k_gemm3 otherwise
         const int ax = s0.amax ? 1 : (s0.scale ? 2 : 0);
+        if (s0.mode == GM_A_ROUTING_ENC) {  // the A tile computed in the block: 128 x 256 ping-pong tile, 2 stages
+            if (!g_mfma16 || !is_bias_epi(epilogue) || s1.p0)
+                return gm_fail(GM_ERR_UNSUPPORTED, "gm_gemm_x3: routing-encoder source needs the 16x16x32 form, a bias "
+                                                   "epilogue and no second source");
+            ep.act = epi_act(epilogue);
+            return launch_g<4, 2, 1, 4, 2, GM_A_ROUTING_ENC, EPI_BIAS, 1>(s0, s1, w, ldw, wb, m, n, K, ep, st, wsi, 1);
+        }
         int gt = 0;
         if (ax) {
             // tools/train_gemm_bench.py at 262 160 rows: wide forward layers (N >= 256, K >= 512) gain
@@ -2189,7 +2318,7 @@ int gemm_entry(bool x3, const gm_a_src* a0, const gm_a_src* a1, const void* w, i
         (x3 && !wsi))
         return gm_fail(GM_ERR_INVALID_ARG, std::string(fn) + ": bad arguments");
     ASrc s0, s1;
-    int rc = to_asrc(a0, m, s0);
+    int rc = to_asrc(a0, m, s0, x3);
     if (rc) return rc;
     rc = to_asrc(a1, m, s1);
     if (rc) return rc;

@@ -21,7 +21,7 @@ import torch.nn.functional as F
 
 from . import _lib as L
 
-GM_A_DENSE, GM_A_AGGREGATE, GM_A_READOUT = 0, 1, 2
+GM_A_DENSE, GM_A_AGGREGATE, GM_A_READOUT, GM_A_ROUTING_ENC = 0, 1, 2, 3
 GM_EPI_BIAS, GM_EPI_BIAS_LEAKY, GM_EPI_LSTM, GM_EPI_GRU = 0, 1, 2, 3
 
 
@@ -42,7 +42,7 @@ class ASrc(C.Structure):
         ("mode", C.c_int32), ("p0", C.c_void_p), ("p1", C.c_void_p), ("ld0", C.c_int64), ("ld1", C.c_int64),
         ("nbr", C.c_void_p), ("agent_node", C.c_void_p), ("n_nodes", C.c_int32), ("deg", C.c_int32),
         ("mean", C.c_int32), ("rows_per_graph", C.c_int32), ("k", C.c_int32), ("hidden", C.c_int32),
-        ("scale", C.c_void_p), ("amax", C.c_void_p),
+        ("scale", C.c_void_p), ("amax", C.c_void_p), ("bias0", C.c_void_p), ("act0", C.c_int32),
     ]
 
 
@@ -98,6 +98,33 @@ def dense(p, ld, k, scale=None, amax=None):
     s.scale = scale
     s.amax = amax
     return s
+
+
+def routing_enc_src(lin, x, nbr, N):
+    """ROUTING_ENC A source (gm_gemm_x3): the NetMon encoder's first layer `lin` on routing node
+    observations x [G*N, >= 4N+8] computed inside the next layer's A-tile load (no m x k output)."""
+    if not hasattr(lin, "_packed_t"):
+        lin._packed_t = Packed()
+    wt = lin._packed_t.get(_key(lin.weight), lambda: lin.weight.detach().t().contiguous())
+    s = ASrc()
+    s.mode, s.p0, s.ld0, s.p1, s.ld1 = GM_A_ROUTING_ENC, x.data_ptr(), x.stride(0), wt.data_ptr(), wt.stride(0)
+    s.nbr, s.n_nodes, s.deg, s.k = nbr.data_ptr(), N, 3, lin.out_features
+    s.bias0 = None if lin.bias is None else lin.bias.data_ptr()
+    s.act0 = lin.act
+    return s
+
+
+# the rollout folds the NetMon encoder's first layer into the second layer's A-tile load when the split
+# form runs with the 16x16x32 MFMA (gm_gemm_set_mfma != 0) and 4N + 8 <= 128 (GM_A_ROUTING_ENC);
+# False keeps gm_routing_node_encoder + a DENSE second layer
+RENC_FOLD = os.environ.get("GM_RENC_FOLD", "1") != "0"
+
+
+def renc_fold_ok(layers, N, Fd, nbr):
+    return (RENC_FOLD and L.GEMM_MODE == "x3" and len(layers) >= 2 and routing_encoder_ok(layers[0], N, Fd, nbr)
+            and 4 * N + 8 <= 128 and layers[0].out_features % 32 == 0 and layers[0].out_features <= 1024
+            and use_x3(layers[1].out_features) and layers[1].in_features == layers[0].out_features
+            and L.MFMA_SHAPE != "32")
 
 
 def aggregate(p, ld, k, nbr, n_nodes, mean=False):
@@ -476,7 +503,15 @@ def netmon_step(netmon, node_obs, nbr, state, out=None, last_out=None):
     dev = node_obs.device
     x = node_obs.reshape(M, Fd)
     layers = list(netmon.encode.linear_layers)
-    if routing_encoder_ok(layers[0], N, Fd, nbr):
+    if renc_fold_ok(layers, N, Fd, nbr):  # layers 1 and 2 in one GEMM: layer 1 computed in layer 2's A load
+        l0, l1 = layers[0], layers[1]
+        y = torch.empty(M, l1.out_features, device=dev)
+        gemm(routing_enc_src(l0, x, nbr, N), None, None, 0, l1.bias.data_ptr(), M, l1.out_features, _epi(l1.act),
+             y.data_ptr(), y.stride(0), tag=l1.tag and f"linear:{l1.tag}:{M}x{l1.out_features}x{l1.in_features}",
+             x3=pack_x3(l1))
+        x = y
+        layers = layers[2:]
+    elif routing_encoder_ok(layers[0], N, Fd, nbr):
         x = routing_encoder(layers[0], x, nbr, B, N, torch.empty(M, layers[0].out_features, device=dev))
         layers = layers[1:]
     for lin in layers:

@@ -344,7 +344,7 @@ int gm_linear_f32(const float* x, int64_t ldx, const float* w, int64_t ldw, cons
  * Replaces the reference's Linear layers of MLP/DQN (src/model.py:13-42, 187-203) and the
  * LSTMCell gate GEMM (src/model.py:379-382) with the aggregate (206-229) and the readout +
  * agent gather (582-631) folded into the A-operand load. */
-enum { GM_A_DENSE = 0, GM_A_AGGREGATE = 1, GM_A_READOUT = 2 };
+enum { GM_A_DENSE = 0, GM_A_AGGREGATE = 1, GM_A_READOUT = 2, GM_A_ROUTING_ENC = 3 };
 enum { GM_EPI_BIAS = 0, GM_EPI_BIAS_LEAKY = 1, GM_EPI_LSTM = 2, GM_EPI_GRU = 3, GM_EPI_BIAS_RELU = 4,
        GM_EPI_BIAS_ELU = 5, GM_EPI_BIAS_TANH = 6, GM_EPI_BIAS_SIGMOID = 7, GM_EPI_BIAS_ACT = 64 };
 /* Layer activations (--activation-function = any elementwise torch.nn.functional name with its
@@ -371,7 +371,17 @@ typedef struct {
                                /* two s from gm_absmax_scale; A is split as s*A, the result / s    */
     uint32_t* amax;            /* gm_gemm_x3, src0 (nullable): max |A| over [src0 | src1] published */
                                /* as float bits by atomicMax (zero it first; gm_absmax_finish)      */
+    const float* bias0;        /* ROUTING_ENC (nullable): bias of the folded encoder layer          */
+    int32_t act0;              /* ROUTING_ENC: its activation (GM_ACT_*)                            */
 } gm_a_src;
+/* GM_A_ROUTING_ENC (gm_gemm_x3 only, no src1): A = act0(W0 x + b0), the NetMon encoder's first layer
+ * (src/model.py:13-42, 489) on routing node observations x (src/env/routing.py:187-235: [onehot(n) | cnt |
+ * load | 3 x (onehot(nbr_k) | len_k | load_k)], 4N + 8 columns) computed inside the GEMM's A-tile load from
+ * the 12 nonzero columns, so the m x k layer output never reaches HBM: p0 = x rows ([G * n_nodes][ld0]),
+ * p1 = W0^T ([4N + 8][ld1], ld1 >= k), nbr = [G][n_nodes][3] (deg = 3), n_nodes = N with 4N + 8 <= 128,
+ * k = the layer's width (multiple of 32), bias0 / act0. Needs the 16x16x32 MFMA form (gm_gemm_set_mfma
+ * != 0) and a bias epilogue; other cases return GM_ERR_UNSUPPORTED (run gm_routing_node_encoder and a
+ * DENSE source instead). */
 /* src1 (nullable) must be DENSE and src0->k a multiple of 32. W: [n][ldw] (ldw >= K, zero
  * padded to a multiple of 4). GM_EPI_LSTM: W rows packed so that rows [128t, 128t+128) are
  * gates i,f,g,o (32 rows each) of hidden units [32t, 32t+32); n = 4H; writes h' to y, c' to y2,

@@ -578,3 +578,50 @@ def test_dqn_fused_kernel_matches_two_kernels(n_env, gemm_obs, act, monkeypatch)
     Wd = {k: v.detach().double().cpu().numpy() for k, v in dqn.state_dict().items()}
     q64 = netmon_ref.dqn_forward(Wd, joint, act=act)
     assert abs(q1.double().cpu().numpy() - q64).max() < 1e-5
+
+
+@pytest.mark.parametrize("N,B", [(20, 4096), (10, 333), (30, 700)])
+def test_routing_encoder_fold_matches_two_kernels(N, B):
+    """Round 5: the rollout computes NetMon encoder layer 1 inside layer 2's A-tile load (GM_A_ROUTING_ENC,
+    the m x 512 layer-1 output never written) — layer 2's output equals gm_routing_node_encoder + the
+    dense layer-2 GEMM on real routing node observations (random topologies, packets in flight), and the
+    fp64 evaluation of the two layers within the split-f16 rollout tolerance."""
+    gm, M, FU, W = mods()
+    env = gm.Routing(gm.Network(N, random_topology=True, excluded_seeds=gm.EVAL_SEEDS), 20, n_env=B, seed=3,
+                     agent_adjacency=False)
+    env.reset_()
+    for _ in range(3):  # packets on edges: nonzero load / count features
+        env.step_(torch.randint(0, 4, (B, 20), device="cuda", dtype=torch.int32))
+    torch.manual_seed(N)
+    nm = M.NetMon(4 * N + 8, 128, [512, 256], 1).cuda()
+    l0, l1 = list(nm.encode.linear_layers)[:2]
+    x = env.node_obs.reshape(B * N, -1)
+    nbr = env.nbr
+    assert FU.renc_fold_ok(list(nm.encode.linear_layers), N, x.shape[1], nbr)
+    y_fold = torch.empty(B * N, 256, device="cuda")
+    FU.gemm(FU.routing_enc_src(l0, x, nbr, N), None, None, 0, l1.bias.data_ptr(), B * N, 256, FU._epi(l1.act),
+            y_fold.data_ptr(), 256, x3=FU.pack_x3(l1))
+    h1 = FU.routing_encoder(l0, x, nbr, B, N, torch.empty(B * N, 512, device="cuda"))
+    y_two = FU._linear(h1, h1.stride(0), 512, l1, torch.empty(B * N, 256, device="cuda"))
+    ref = F.leaky_relu(F.linear(F.leaky_relu(F.linear(x.double(), l0.weight.double(), l0.bias.double())),
+                                l1.weight.double(), l1.bias.double()))
+    d = (y_fold - y_two).abs().max().item()
+    assert d < 2e-6, d  # same A values up to the encoder's fma contraction, same split-f16 GEMM
+    assert (y_fold.double() - ref).abs().max().item() < 1e-5
+
+
+def test_routing_encoder_fold_refuses_unsupported_cases():
+    """gm_gemm_x3 only (not gm_gemm_f32), 4N + 8 <= 128, and the 16x16x32 MFMA form."""
+    gm, M, FU, W = mods()
+    N, B = 40, 8
+    env = gm.Routing(gm.Network(N, random_topology=True, excluded_seeds=gm.EVAL_SEEDS), 20, n_env=B, seed=1,
+                     agent_adjacency=False)
+    env.reset_()
+    nm = M.NetMon(4 * N + 8, 128, [512, 256], 1).cuda()
+    l0, l1 = list(nm.encode.linear_layers)[:2]
+    x = env.node_obs.reshape(B * N, -1)
+    assert not FU.renc_fold_ok(list(nm.encode.linear_layers), N, x.shape[1], env.nbr)
+    y = torch.empty(B * N, 256, device="cuda")
+    with pytest.raises(gm._lib.GMError, match="4N"):
+        FU.gemm(FU.routing_enc_src(l0, x, env.nbr, N), None, None, 0, l1.bias.data_ptr(), B * N, 256, 1,
+                y.data_ptr(), 256, x3=FU.pack_x3(l1))
