@@ -417,17 +417,27 @@ __device__ int64_t draw_topology_seed(const EnvDev& d, R& r) {  // network.py:23
     return sd;
 }
 
-// the smallest key over the lanes with `in` (all lanes hold the result); ~0 when no lane has `in`.
-// Butterfly over the whole wave (every lane active): 6 rounds of two 32-bit shuffles and a 64-bit min
+// one min step of a wave reduction over 64-bit keys: the partner lane by a DPP pattern (no LDS round trip)
+template <int CTRL>
+__device__ __forceinline__ uint64_t dpp_min_u64(uint64_t v) {
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)v, CTRL, 0xF, 0xF, false);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)(v >> 32), CTRL, 0xF, 0xF, false);
+    const uint64_t o = ((uint64_t)hi << 32) | lo;
+    return o < v ? o : v;
+}
+// the smallest key over the lanes with `in` (uniform result); ~0 when no lane has `in`. Call it with every
+// lane active (outside any lane condition). Inside each 16-lane row by DPP (quad_perm [1,0,3,2], [2,3,0,1],
+// row_half_mirror, row_mirror: every lane ends with its row's minimum), then the four rows by readlane:
+// ~8x shorter than a 6-round shuffle butterfly, whose LDS-path bpermutes dominated an attempt's rows
 __device__ __forceinline__ uint64_t argmin_key(uint64_t key, bool in) {
     uint64_t v = in ? key : ~0ull;
-#pragma unroll
-    for (int m = 1; m < WAVE; m <<= 1) {
-        const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)v, m), hi = (uint32_t)__shfl_xor((int)(uint32_t)(v >> 32), m);
-        const uint64_t o = ((uint64_t)hi << 32) | lo;
-        v = o < v ? o : v;
-    }
-    return v;
+    v = dpp_min_u64<0xB1>(v);
+    v = dpp_min_u64<0x4E>(v);
+    v = dpp_min_u64<0x141>(v);
+    v = dpp_min_u64<0x140>(v);
+    const uint64_t r0 = readlane_u64(v, 0), r1 = readlane_u64(v, 16), r2 = readlane_u64(v, 32), r3 = readlane_u64(v, 48);
+    const uint64_t a = r0 < r1 ? r0 : r1, b = r2 < r3 ? r2 : r3;
+    return a < b ? a : b;
 }
 
 // One _create_random_topology attempt (network.py:122-195) for N <= 64, lane v = node v, the whole
