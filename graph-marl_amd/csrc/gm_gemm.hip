@@ -2153,10 +2153,11 @@ int dispatch(const ASrc& s0, const ASrc& s1, const float* w, long long ldw, unsi
         // training operands (forward GEMMs publishing max|A|, input-gradient GEMMs on a scaled A):
         // the LDS-DMA kernel's 128x128 tile at 2 blocks/CU for large dense GEMMs, k_gemm3 otherwise
         const int ax = s0.amax ? 1 : (s0.scale ? 2 : 0);
-        if (s0.mode == GM_A_ROUTING_ENC) {  // the A tile computed in the block: 128 x 256 ping-pong tile, 2 stages
-            if (!g_mfma16 || !is_bias_epi(epilogue) || s1.p0)
-                return gm_fail(GM_ERR_UNSUPPORTED, "gm_gemm_x3: routing-encoder source needs the 16x16x32 form, a bias "
-                                                   "epilogue and no second source");
+        if (s0.mode == GM_A_ROUTING_ENC) {  // the A tile computed in the block: 128 x 256 ping-pong tile, 2 stages,
+                                            // always on 16x16x32 (whatever gm_gemm_set_mfma selects elsewhere)
+            if (!is_bias_epi(epilogue) || s1.p0)
+                return gm_fail(GM_ERR_UNSUPPORTED, "gm_gemm_x3: routing-encoder source needs a bias epilogue and no "
+                                                   "second source");
             ep.act = epi_act(epilogue);
             return launch_g<4, 2, 1, 4, 2, GM_A_ROUTING_ENC, EPI_BIAS, 1>(s0, s1, w, ldw, wb, m, n, K, ep, st, wsi, 1);
         }

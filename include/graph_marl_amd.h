@@ -379,9 +379,9 @@ typedef struct {
  * load | 3 x (onehot(nbr_k) | len_k | load_k)], 4N + 8 columns) computed inside the GEMM's A-tile load from
  * the 12 nonzero columns, so the m x k layer output never reaches HBM: p0 = x rows ([G * n_nodes][ld0]),
  * p1 = W0^T ([4N + 8][ld1], ld1 >= k), nbr = [G][n_nodes][3] (deg = 3), n_nodes = N with 4N + 8 <= 128,
- * k = the layer's width (multiple of 32), bias0 / act0. Needs the 16x16x32 MFMA form (gm_gemm_set_mfma
- * != 0) and a bias epilogue; other cases return GM_ERR_UNSUPPORTED (run gm_routing_node_encoder and a
- * DENSE source instead). */
+ * k = the layer's width (multiple of 32), bias0 / act0. Runs on v_mfma_f32_16x16x32_f16 (whatever
+ * gm_gemm_set_mfma selects for the other GEMMs) and needs a bias epilogue; other cases return
+ * GM_ERR_UNSUPPORTED (run gm_routing_node_encoder and a DENSE source instead). */
 /* src1 (nullable) must be DENSE and src0->k a multiple of 32. W: [n][ldw] (ldw >= K, zero
  * padded to a multiple of 4). GM_EPI_LSTM: W rows packed so that rows [128t, 128t+128) are
  * gates i,f,g,o (32 rows each) of hidden units [32t, 32t+32); n = 4H; writes h' to y, c' to y2,

@@ -611,7 +611,7 @@ def test_routing_encoder_fold_matches_two_kernels(N, B):
 
 
 def test_routing_encoder_fold_refuses_unsupported_cases():
-    """gm_gemm_x3 only (not gm_gemm_f32), 4N + 8 <= 128, and the 16x16x32 MFMA form."""
+    """gm_gemm_x3 only (not gm_gemm_f32) and 4N + 8 <= 128."""
     gm, M, FU, W = mods()
     N, B = 40, 8
     env = gm.Routing(gm.Network(N, random_topology=True, excluded_seeds=gm.EVAL_SEEDS), 20, n_env=B, seed=1,
