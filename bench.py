@@ -225,7 +225,8 @@ def kernel_cost(tag, n_env, N, A, E, x3=False):
     kind = tag.split(":")[0]
     if kind in ("linear", "lstm", "lstm_agg"):
         m, n, k = (int(v) for v in tag.split(":")[2].split("x"))
-        return ("mfma16" if x3 and n > 32 else "mfma"), (3.0 if x3 and n > 32 else 1.0) * 2.0 * m * n * k
+        macs = m * n * k + (m * 128 * n if "+chain" in tag else 0)  # gm_encoder_x3: + layer 3 (n -> 128)
+        return ("mfma16" if x3 and n > 32 else "mfma"), (3.0 if x3 and n > 32 else 1.0) * 2.0 * macs
     if kind == "dqn_fused":  # gm_dqn_x3: layer 1 (K) + layer 2 (512 -> 256) + Q head, 3 f16 products each
         m, n, k = (int(v) for v in tag.split(":")[2].split("x"))
         return "mfma16", 3.0 * 2.0 * m * (n * k + 256 * n + 4 * 256)

@@ -34,7 +34,7 @@ EXPORTS = [
     "gm_pcg64_seed", "gm_pcg64_choice", "gm_lnlstm_pointwise", "gm_agent_attention", "gm_agent_comm",
     "gm_gemm_x3_dgrad", "gm_lstm_cell_bwd", "gm_qhead_bwd", "gm_netmon_readout_ld", "gm_routing_node_encoder_bits", "gm_gather_records",
     "gm_lnlstm_fwd", "gm_lnlstm_bwd", "gm_gru_pointwise", "gm_gru_bwd", "gm_act_bwd", "gm_dqn_x3", "gm_build_info",
-    "gm_act_fwd", "gm_act_bwd_z", "gm_obs_from_gemm",
+    "gm_act_fwd", "gm_act_bwd_z", "gm_obs_from_gemm", "gm_encoder_x3",
 ]
 # kernel-form switches (include/graph_marl_amd_tuning.h)
 TUNING_EXPORTS = ["gm_gemm_set_tile", "gm_gemm_set_wgrad", "gm_gemm_set_mfma", "gm_gemm_set_dgrad", "gm_gemm_form"]

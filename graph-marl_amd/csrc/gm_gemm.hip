@@ -75,7 +75,7 @@ typedef float floatx4 __attribute__((ext_vector_type(4)));
 
 constexpr int BKMAX = 32;            // largest K tile of any configuration (host-side checks)
 constexpr int OOB = 0x7ff00000;       // byte offset beyond any buffer: load returns 0
-enum { EPI_BIAS = 0, EPI_LSTM = 1, EPI_HEAD = 2, EPI_DGRAD = 3, EPI_DQN = 4 };
+enum { EPI_BIAS = 0, EPI_LSTM = 1, EPI_HEAD = 2, EPI_DGRAD = 3, EPI_DQN = 4, EPI_CHAIN = 5 };
 
 struct ASrc {
     int mode;                 // GM_A_DENSE / GM_A_AGGREGATE / GM_A_READOUT
@@ -1361,6 +1361,141 @@ __device__ __forceinline__ void dqn_tail(floatx4 (&acc)[T2][N2], const Epi& ep, 
     });
 }
 
+// ---- EPI_CHAIN: the next MLP layer in the block that computed this one (the rollout's NetMon encoder
+// layers 2 -> 3, src/model.py:13-42) ----
+// The block (BM rows x the layer's whole width K2 = WGN * N2 * 16) sends its activations through bias +
+// activation and the split (split4: the bits a dense A tile of the next layer would get) into two
+// K-major LDS images ([k][BM rows] f16, dqn_swz slots: EPI_DQN's layout with BM * 2-byte rows), which
+// alias the finished operand stages. The next layer (N3 = WGN * J3 * 16 columns: wave (wr, wc) computes
+// rows 16 T2 wr .., columns 16 J3 wc ..) reads its A fragments transposed from the images
+// (ds_read_b64_tr_b16) and its packed weight fragments straight from L2, two k tiles ahead, and stores
+// act3(. + b3) with epilogue16. The m x K2 activation of the first layer never reaches HBM.
+template <int WGM, int WGN, int T2, int N2, int BM, int J3, int A = -1>
+__device__ __forceinline__ void chain_tail(floatx4 (&acc)[T2][N2], const Epi& ep, char* lds, int m0, int wr, int wc,
+                                           int M, int lane) {
+    static_assert(WGM * T2 * 16 == BM, "the wave rows hold the block's rows");
+    constexpr int K2 = WGN * N2 * 16;  // next layer's K = this layer's width
+    constexpr int N3 = WGN * J3 * 16;  // next layer's width
+    constexpr int RS = BM * 2;         // image row bytes
+    constexpr int NK = K2 / 32;        // next layer's k tiles
+    char* ih = lds;
+    char* il = lds + K2 * RS;
+    const int l16 = lane & 15, rq = 4 * (lane >> 4);
+    __syncthreads();  // every wave is past its last reads of the operand stages
+#pragma unroll
+    for (int j = 0; j < N2; j++) {
+        const int n = wc * N2 * 16 + j * 16 + l16;  // this layer's column = the next layer's k
+        const float bj = ep.bias ? ep.bias[n] : 0.f;
+        const int sw = dqn_swz(n) << 3;
+#pragma unroll
+        for (int i = 0; i < T2; i++) {
+            const int m = wr * T2 * 16 + i * 16 + rq;
+            float4 v;
+            v.x = act_t<A>(acc[i][j][0] + bj, ep.act);
+            v.y = act_t<A>(acc[i][j][1] + bj, ep.act);
+            v.z = act_t<A>(acc[i][j][2] + bj, ep.act);
+            v.w = act_t<A>(acc[i][j][3] + bj, ep.act);
+            half4 hi, lo;
+            split4(v, hi, lo);
+            const int off = n * RS + ((2 * m) ^ sw);
+            *reinterpret_cast<half4*>(ih + off) = hi;
+            *reinterpret_cast<half4*>(il + off) = lo;
+        }
+    }
+    // weight fragments of this wave's 16 J3 columns: row n3 = 16 J3 wc + 16 jb + l16, k 8 q .. 8 q + 7 of
+    // each 32-deep tile (16-k block (q >> 1), halves (q & 1) x 8; hi at +0, lo at +32 of a block's 64 bytes)
+    const int q = lane >> 4;
+    const __amdgpu_buffer_rsrc_t rw = rsrc(reinterpret_cast<const float*>(ep.w2), ep.w2bytes);
+    int wo[J3];
+#pragma unroll
+    for (int jb = 0; jb < J3; jb++)
+        wo[jb] = (int)((wc * J3 * 16 + jb * 16 + l16) * ep.ldw2) + (q >> 1) * 64 + (q & 1) * 16;
+    constexpr int NB3 = 2;  // weight tiles in flight
+    u32x4 pbh[NB3][J3], pbl[NB3][J3];
+    auto bfetch = [&](int slot, int kt) {
+#pragma unroll
+        for (int jb = 0; jb < J3; jb++) {
+            pbh[slot][jb] = __builtin_amdgcn_raw_buffer_load_b128(rw, wo[jb] + kt * 128, 0, 0);
+            pbl[slot][jb] = __builtin_amdgcn_raw_buffer_load_b128(rw, wo[jb] + kt * 128 + 32, 0, 0);
+        }
+    };
+#pragma unroll
+    for (int t = 0; t < NB3; t++) bfetch(t, t);
+    __syncthreads();  // the images are complete
+    floatx4 acc3[T2][J3];
+#pragma unroll
+    for (int i = 0; i < T2; i++)
+#pragma unroll
+        for (int j = 0; j < J3; j++)
+#pragma unroll
+            for (int r = 0; r < 4; r++) acc3[i][j][r] = 0.f;
+    const int g = lane >> 4, qq = (lane >> 2) & 3, p = lane & 3;
+    typedef __fp16 v4fp16 __attribute__((__vector_size__(8)));
+    auto frag = [&](const char* img, int k0, int col0) {  // as dqn_tail: 8 consecutive k of one row
+        const int r0 = k0 + 8 * g + qq, r1 = r0 + 4;
+        const char* a0 = img + r0 * RS + ((2 * (col0 + 4 * p)) ^ (dqn_swz(r0) << 3));
+        const char* a1 = img + r1 * RS + ((2 * (col0 + 4 * p)) ^ (dqn_swz(r1) << 3));
+        const half4 x0 = __builtin_bit_cast(
+            half4, __builtin_amdgcn_ds_read_tr16_b64_v4f16((__attribute__((address_space(3))) v4fp16*)(a0)));
+        const half4 x1 = __builtin_bit_cast(
+            half4, __builtin_amdgcn_ds_read_tr16_b64_v4f16((__attribute__((address_space(3))) v4fp16*)(a1)));
+        return half8{x0[0], x0[1], x0[2], x0[3], x1[0], x1[1], x1[2], x1[3]};
+    };
+    const _Float16 s12 = (_Float16)(1.0f / LO_S);
+    const int row0 = wr * T2 * 16;
+    half8 fah[2][T2], fal[2][T2];
+#pragma unroll
+    for (int i = 0; i < T2; i++) {
+        fah[0][i] = frag(ih, 0, row0 + 16 * i);
+        fal[0][i] = frag(il, 0, row0 + 16 * i);
+    }
+#pragma unroll
+    for (int kt = 0; kt < NK; kt++) {
+        const int cur = kt & 1, slot = kt % NB3;
+        if (kt + 1 < NK) {
+#pragma unroll
+            for (int i = 0; i < T2; i++) {
+                fah[cur ^ 1][i] = frag(ih, (kt + 1) * 32, row0 + 16 * i);
+                fal[cur ^ 1][i] = frag(il, (kt + 1) * 32, row0 + 16 * i);
+            }
+        }
+        half8 bh[J3], bl[J3];
+#pragma unroll
+        for (int jb = 0; jb < J3; jb++) {
+            bh[jb] = __builtin_bit_cast(half8, pbh[slot][jb]);
+            bl[jb] = __builtin_bit_cast(half8, pbl[slot][jb]);
+        }
+        if (kt + NB3 < NK) bfetch(slot, kt + NB3);
+#pragma unroll
+        for (int jb = 0; jb < J3; jb++) {
+            const half8 bs = bh[jb] * s12;
+#pragma unroll
+            for (int i = 0; i < T2; i++) {
+                floatx4& c = acc3[i][jb];
+                c = __builtin_amdgcn_mfma_f32_16x16x32_f16(fal[cur][i], bs, c, 0, 0, 0);
+                c = __builtin_amdgcn_mfma_f32_16x16x32_f16(fah[cur][i], bl[jb], c, 0, 0, 0);
+                c = __builtin_amdgcn_mfma_f32_16x16x32_f16(fah[cur][i], bh[jb], c, 0, 0, 0);
+            }
+        }
+    }
+    const float si = *ep.wsi2;
+#pragma unroll
+    for (int i = 0; i < T2; i++)
+#pragma unroll
+        for (int j = 0; j < J3; j++)
+#pragma unroll
+            for (int r = 0; r < 4; r++) acc3[i][j][r] *= si;
+    range_guard16<T2, J3>(acc3, ep.range_flag, lane);
+    Epi e3 = ep;
+    e3.bias = ep.b2;
+    e3.act = ep.act2;
+    e3.sbits = nullptr;
+    CIn16<T2, EPI_BIAS> none;
+    act_dispatch(e3.act, [&](auto A3) {
+        epilogue16<T2, J3, EPI_BIAS, decltype(A3)::value>(acc3, e3, m0 + row0, wc * J3 * 16, M, N3, lane, none);
+    });
+}
+
 // ---------------------------------------------------------------------------------------
 // X3 kernel with LDS-DMA staging (buffer_load ... lds): both operands go HBM/L2 -> LDS with
 // no VGPR round trip and no ds_write pass. A stays fp32 in LDS (32-deep k tiles = one 128-B
@@ -1413,6 +1548,8 @@ __global__ __launch_bounds__(WGM* WGN * 64, OCC) void k_gemm3g(ASrc a0, ASrc a1,
     static_assert(STAGES >= 2 && STAGES <= 4, "stages");
     static_assert(!RENC || (STAGES == 2 && BM * 4 == NW * 64 && MF == 1 && NW == 8),
                   "routing-encoder source: 2-stage ping-pong tile, 4 threads per A row");
+    static_assert(EPI != EPI_CHAIN || (MF == 1 && STAGES * STAGE_B + RENC_B >= 2 * BN * BM * 2),
+                  "chain epilogue: the next layer's split A images alias the operand stages");
 #if GM_DIAG == 30
     __shared__ __attribute__((aligned(16))) char lds[STAGES * STAGE_B + RENC_B + 1024];
 #else
@@ -1958,6 +2095,10 @@ __global__ __launch_bounds__(WGM* WGN * 64, OCC) void k_gemm3g(ASrc a0, ASrc a1,
             act_dispatch(ep.act, [&](auto A) {
                 dqn_tail<2 * TM, 2 * TN, WGN, BM, decltype(A)::value>(acc4, ep, lds, m0, wc, M, lane, tid);
             });
+        else if constexpr (EPI == EPI_CHAIN)
+            act_dispatch(ep.act, [&](auto A) {
+                chain_tail<WGM, WGN, 2 * TM, 2 * TN, BM, 4, decltype(A)::value>(acc4, ep, lds, m0, wr, wc, M, lane);
+            });
         else
             if constexpr (EPI == EPI_BIAS)
                 act_dispatch(ep.act, [&](auto A) {
@@ -1991,7 +2132,7 @@ __global__ __launch_bounds__(WGM* WGN * 64, OCC) void k_gemm3g(ASrc a0, ASrc a1,
             act_dispatch(ep.act, [&](auto A) {
                 epilogue<TM, TN, EPI, decltype(A)::value>(acc, ep, m0 + wr * TM * 32, n0 + wc * TN * 32, M, N, lane, cin);
             });
-        else if constexpr (EPI != EPI_DQN)  // EPI_DQN runs on the 16x16x32 form only (gm_dqn_x3)
+        else if constexpr (EPI != EPI_DQN && EPI != EPI_CHAIN)  // EPI_DQN / EPI_CHAIN: the 16x16x32 form only
             epilogue<TM, TN, EPI>(acc, ep, m0 + wr * TM * 32, n0 + wc * TN * 32, M, N, lane, cin);
     }
 }
@@ -2490,6 +2631,41 @@ extern "C" int gm_gemm_range_status(int32_t* status, int32_t clear) {
     *status = g_range_host ? (int32_t)*reinterpret_cast<volatile unsigned*>(g_range_host) : 0;
     if (clear && g_range_host) *reinterpret_cast<volatile unsigned*>(g_range_host) = 0u;
     return GM_OK;
+}
+
+// NetMon encoder layers 1-3 of the rollout in one launch (src/model.py:13-42, 489): layer 1 in layer 2's
+// A-tile load (a0: GM_A_ROUTING_ENC), layer 2 (128 x 256 block tiles: the whole width) kept on chip as split
+// f16 images, layer 3 from them (EPI_CHAIN); only y = layer 3's output is written
+extern "C" int gm_encoder_x3(const gm_a_src* a0, const void* w2p, const float* w2sinv, const float* b2, int32_t act2,
+                             const void* w3p, const float* w3sinv, const float* b3, int32_t act3, int32_t m, int32_t n2,
+                             int32_t n3, float* y, int64_t ldy, void* stream) {
+    if (!a0 || a0->mode != GM_A_ROUTING_ENC || !w2p || !w2sinv || !w3p || !w3sinv || !y || m <= 0 || n2 != 256 ||
+        n3 != 128 || ldy < n3 || act2 < GM_ACT_NONE || act2 > GM_ACT_LAST || act3 < GM_ACT_NONE || act3 > GM_ACT_LAST ||
+        (reinterpret_cast<uintptr_t>(w2p) & 15) || (reinterpret_cast<uintptr_t>(w3p) & 15))
+        return gm_fail(GM_ERR_INVALID_ARG, "gm_encoder_x3: bad arguments (routing-encoder source, layers 256, 128 wide)");
+    ASrc s0, s1;
+    int rc = to_asrc(a0, m, s0, true);
+    if (rc) return rc;
+    memset(&s1, 0, sizeof(s1));
+    const int K = s0.k;
+    const long long ldw2 = (long long)K / 16 * 64, wb2 = (long long)n2 * ldw2;
+    const long long ldw3 = (long long)n2 / 16 * 64, wb3 = (long long)n3 * ldw3;  // layer-3 K = n2
+    Epi ep;
+    memset(&ep, 0, sizeof(ep));
+    ep.bias = b2;
+    ep.act = act2;
+    ep.w2 = static_cast<const _Float16*>(w3p);
+    ep.ldw2 = ldw3;
+    ep.w2bytes = (unsigned)wb3;
+    ep.wsi2 = w3sinv;
+    ep.b2 = b3;
+    ep.act2 = act3;
+    ep.y = y;
+    ep.ldy = ldy;
+    if ((rc = range_flag(&ep.range_flag))) return rc;
+    return launch_g<4, 2, 1, 4, 2, GM_A_ROUTING_ENC, EPI_CHAIN, 1>(s0, s1, static_cast<const float*>(w2p), ldw2,
+                                                                  (unsigned)wb2, m, n2, K, ep, (hipStream_t)stream,
+                                                                  w2sinv, 1);
 }
 
 extern "C" int gm_dqn_x3(const gm_a_src* a0, const gm_a_src* a1, const void* w1p, const float* w1sinv, const float* b1,

@@ -67,6 +67,7 @@ def _setup():
         if hasattr(lib, "gm_dqn_x3") or not os.environ.get("GM_LIB"):  # an older GM_LIB build lacks it
             lib.gm_dqn_x3.argtypes = [C.POINTER(ASrc), C.POINTER(ASrc), vp, vp, vp, i32, vp, vp, vp, i32, i32, i32,
                                       i32, vp, i64, vp, i32, vp, i64, vp]
+        lib.gm_encoder_x3.argtypes = [C.POINTER(ASrc), vp, vp, vp, i32, vp, vp, vp, i32, i32, i32, i32, vp, i64, vp]
         lib._gemm_ready = True
     return lib
 
@@ -124,6 +125,30 @@ def renc_fold_ok(layers, N, Fd, nbr):
     return (RENC_FOLD and L.GEMM_MODE == "x3" and len(layers) >= 2 and routing_encoder_ok(layers[0], N, Fd, nbr)
             and 4 * N + 8 <= 128 and layers[0].out_features % 32 == 0 and layers[0].out_features <= 1024
             and use_x3(layers[1].out_features) and layers[1].in_features == layers[0].out_features)
+
+
+# the rollout's NetMon encoder [4N+8 -> k -> 256 -> 128] (the CLI default 512, 256 with H = 128) in one launch
+# (gm_encoder_x3: layer 2's output stays on chip for layer 3); GM_ENC_CHAIN=0 keeps the fold + a layer-3 GEMM
+ENC_CHAIN = os.environ.get("GM_ENC_CHAIN", "1") != "0"
+
+
+def encoder_chain_ok(layers, N, Fd, nbr):
+    return (ENC_CHAIN and len(layers) >= 3 and renc_fold_ok(layers, N, Fd, nbr) and layers[1].out_features == 256
+            and layers[2].in_features == 256 and layers[2].out_features == 128 and layers[1].bias is not None
+            and layers[2].bias is not None and use_x3(128))
+
+
+def encoder_chain(l0, l1, l2, x, nbr, N, out):
+    """out = l2(l1(l0(x))) on routing node observations in one launch (gm_encoder_x3)."""
+    lib = _setup()
+    x1, x2 = pack_x3(l1), pack_x3(l2)
+    M = x.shape[0]
+    with L.timed(l1.tag and f"linear:{l1.tag}+chain:{M}x{l1.out_features}x{l1.in_features}"):
+        L.check(lib.gm_encoder_x3(C.byref(routing_enc_src(l0, x, nbr, N)), x1.wp.data_ptr(), x1.sinv.data_ptr(),
+                                  l1.bias.data_ptr(), l1.act, x2.wp.data_ptr(), x2.sinv.data_ptr(), l2.bias.data_ptr(),
+                                  l2.act, M, l1.out_features, l2.out_features, out.data_ptr(), out.stride(0),
+                                  L.stream_ptr()))
+    return out
 
 
 def aggregate(p, ld, k, nbr, n_nodes, mean=False):
@@ -502,7 +527,11 @@ def netmon_step(netmon, node_obs, nbr, state, out=None, last_out=None):
     dev = node_obs.device
     x = node_obs.reshape(M, Fd)
     layers = list(netmon.encode.linear_layers)
-    if renc_fold_ok(layers, N, Fd, nbr):  # layers 1 and 2 in one GEMM: layer 1 computed in layer 2's A load
+    if encoder_chain_ok(layers, N, Fd, nbr):  # layers 1-3 in one launch (gm_encoder_x3)
+        l0, l1, l2 = layers[:3]
+        x = encoder_chain(l0, l1, l2, x, nbr, N, torch.empty(M, l2.out_features, device=dev))
+        layers = layers[3:]
+    elif renc_fold_ok(layers, N, Fd, nbr):  # layers 1 and 2 in one GEMM: layer 1 computed in layer 2's A load
         l0, l1 = layers[0], layers[1]
         y = torch.empty(M, l1.out_features, device=dev)
         gemm(routing_enc_src(l0, x, nbr, N), None, None, 0, l1.bias.data_ptr(), M, l1.out_features, _epi(l1.act),

@@ -433,6 +433,14 @@ int gm_dqn_x3(const gm_a_src* a0, const gm_a_src* a1, const void* w1p, const flo
               int32_t act1, const void* w2p, const float* w2sinv, const float* b2, int32_t act2, int32_t m, int32_t n1,
               int32_t n2, const float* wq, int64_t ldwq, const float* bq, int32_t nq, float* q, int64_t ldq,
               void* stream);
+/* The rollout's NetMon encoder (src/model.py:13-42 MLP, 489) in ONE launch: layer 1 computed in layer 2's
+ * A-tile load from the routing node observations (a0: GM_A_ROUTING_ENC), layer 2 (n2 = 256) kept on chip
+ * per 128-row block as split-f16 LDS images, layer 3 (n3 = 128) from them; y [m][ldy] = act3(act2(A W2^T +
+ * b2) W3^T + b3). w2p / w2sinv, w3p / w3sinv: gm_gemm_pack_x3 of W2 [256][k] and W3 [128][256]. Neither the
+ * m x k layer-1 nor the m x 256 layer-2 activation is written. */
+int gm_encoder_x3(const gm_a_src* a0, const void* w2p, const float* w2sinv, const float* b2, int32_t act2,
+                  const void* w3p, const float* w3sinv, const float* b3, int32_t act3, int32_t m, int32_t n2, int32_t n3,
+                  float* y, int64_t ldy, void* stream);
 /* Input-gradient GEMM of a layer whose input went through leaky_relu (the reference MLP's
  * F.leaky_relu, src/model.py:13-42, backward of torch autograd, src/main.py:996): D = src0 . W^T
  * in split-f16 form over wp = gm_gemm_pack_x3 of W^T ([n][K], K = src0->k; src0 DENSE, its

@@ -625,3 +625,33 @@ def test_routing_encoder_fold_refuses_unsupported_cases():
     with pytest.raises(gm._lib.GMError, match="4N"):
         FU.gemm(FU.routing_enc_src(l0, x, env.nbr, N), None, None, 0, l1.bias.data_ptr(), B * N, 256, 1,
                 y.data_ptr(), 256, x3=FU.pack_x3(l1))
+
+
+@pytest.mark.parametrize("N,B", [(20, 4096), (10, 333), (30, 700)])
+def test_encoder_chain_matches_layer_by_layer(N, B):
+    """gm_encoder_x3 (round 5: NetMon encoder layers 1-3 of the rollout in one launch, layer 2's output kept
+    on chip as split-f16 images) == the fold (layers 1 + 2) + the dense layer-3 GEMM, and fp64 within the
+    rollout tolerance, on real routing node observations."""
+    gm, M, FU, W = mods()
+    env = gm.Routing(gm.Network(N, random_topology=True, excluded_seeds=gm.EVAL_SEEDS), 20, n_env=B, seed=5,
+                     agent_adjacency=False)
+    env.reset_()
+    for _ in range(3):
+        env.step_(torch.randint(0, 4, (B, 20), device="cuda", dtype=torch.int32))
+    torch.manual_seed(N + 1)
+    nm = M.NetMon(4 * N + 8, 128, [512, 256], 1).cuda()
+    l0, l1, l2 = list(nm.encode.linear_layers)
+    x = env.node_obs.reshape(B * N, -1)
+    nbr = env.nbr
+    assert FU.encoder_chain_ok(list(nm.encode.linear_layers), N, x.shape[1], nbr)
+    y = FU.encoder_chain(l0, l1, l2, x, nbr, N, torch.empty(B * N, 128, device="cuda"))
+    y2 = torch.empty(B * N, 256, device="cuda")
+    FU.gemm(FU.routing_enc_src(l0, x, nbr, N), None, None, 0, l1.bias.data_ptr(), B * N, 256, FU._epi(l1.act),
+            y2.data_ptr(), 256, x3=FU.pack_x3(l1))
+    y3 = FU._linear(y2, 256, 256, l2, torch.empty(B * N, 128, device="cuda"))
+    ref = x.double()
+    for lin in (l0, l1, l2):
+        ref = F.leaky_relu(F.linear(ref, lin.weight.double(), lin.bias.double()))
+    assert (y - y3).abs().max().item() < 1e-6
+    assert (y.double() - ref).abs().max().item() < 1e-5
+    assert FU.L.range_status() == 0
