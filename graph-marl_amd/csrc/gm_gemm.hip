@@ -1547,7 +1547,7 @@ __global__ __launch_bounds__(WGM* WGN * 64, OCC) void k_gemm3g(ASrc a0, ASrc a1,
     static_assert(AMODE != GM_A_AGGREGATE, "aggregate source uses k_gemm3");
     static_assert(STAGES >= 2 && STAGES <= 4, "stages");
     static_assert(!RENC || (STAGES == 2 && BM * 4 == NW * 64 && MF == 1 && NW == 8),
-                  "routing-encoder source: 2-stage ping-pong tile, 4 threads per A row");
+                  "routing-encoder source: 2-stage ping-pong tile, 8 threads x 2 rows per 128 A rows");
     static_assert(EPI != EPI_CHAIN || (MF == 1 && STAGES * STAGE_B + RENC_B >= 2 * BN * BM * 2),
                   "chain epilogue: the next layer's split A images alias the operand stages");
 #if GM_DIAG == 30
@@ -1618,30 +1618,34 @@ __global__ __launch_bounds__(WGM* WGN * 64, OCC) void k_gemm3g(ASrc a0, ASrc a1,
     const __amdgpu_buffer_rsrc_t r1 = a1.p0 ? rsrc_rows(a1.p0, a1.ld0, m0, a1.bytes0) : rsrc(a0.p0, 0u);
     const __amdgpu_buffer_rsrc_t rw = rsrc(reinterpret_cast<const float*>(w), wbytes);
 
-    // ---- ROUTING_ENC: this thread's A row (4 threads per row, 8 consecutive k each) and its node-obs
-    // features: A[r][k] = act0(b0[k] + W0^T[v][k] + cnt W0^T[N][k] + load W0^T[N + 1][k] + sum over the
-    // 3 neighbour blocks (W0^T[off + u][k] + len W0^T[off + N][k] + load W0^T[off + N + 1][k])), the
-    // 12 nonzero columns of the node observation [onehot(n) | cnt | load | 3 x (onehot(nbr) | len |
-    // load)] (src/env/routing.py:187-235), in k_routing_enc's order of operations ----
-    const int rr = tid >> 2, rq = tid & 3;
-    int r_oh[4] = {0, 0, 0, 0};
-    float r_sv[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    // ---- ROUTING_ENC: this thread's 16-byte chunk rq (k = 4 rq .. 4 rq + 3 of every tile) of A rows rr and
+    // rr + BM / 2, and their node-obs features: A[r][k] = act0(b0[k] + W0^T[v][k] + cnt W0^T[N][k] + load
+    // W0^T[N + 1][k] + sum over the 3 neighbour blocks (W0^T[off + u][k] + len W0^T[off + N][k] + load
+    // W0^T[off + N + 1][k])), the 12 nonzero columns of the node observation [onehot(n) | cnt | load | 3 x
+    // (onehot(nbr) | len | load)] (src/env/routing.py:187-235), in k_routing_enc's order of operations. The
+    // 9 row-independent W0^T / bias chunks are read once for both rows ----
+    const int rr = tid >> 3, rq = tid & 7;
+    int r_oh[2][4] = {};
+    float r_sv[2][8] = {};
     int wso[RW > 0 ? RW : 1];
     if constexpr (RENC) {
         const int Nn = a0.n_nodes;
-        const int row = min(m0 + rr, M - 1);
-        const int g = row / Nn, v = row - g * Nn;
-        const float* xr = a0.p0 + (long long)row * a0.ld0;
-        const int* nb = a0.nbr + ((long long)g * Nn + v) * 3;
-        r_oh[0] = v;
-        r_sv[0] = xr[Nn];
-        r_sv[1] = xr[Nn + 1];
 #pragma unroll
-        for (int k = 0; k < 3; k++) {
-            const int off = Nn + 2 + k * (Nn + 2);
-            r_oh[k + 1] = off + nb[k];
-            r_sv[2 + 2 * k] = xr[off + Nn];
-            r_sv[3 + 2 * k] = xr[off + Nn + 1];
+        for (int h = 0; h < 2; h++) {
+            const int row = min(m0 + rr + h * (BM / 2), M - 1);
+            const int g = row / Nn, v = row - g * Nn;
+            const float* xr = a0.p0 + (long long)row * a0.ld0;
+            const int* nb = a0.nbr + ((long long)g * Nn + v) * 3;
+            r_oh[h][0] = v;
+            r_sv[h][0] = xr[Nn];
+            r_sv[h][1] = xr[Nn + 1];
+#pragma unroll
+            for (int k = 0; k < 3; k++) {
+                const int off = Nn + 2 + k * (Nn + 2);
+                r_oh[h][k + 1] = off + nb[k];
+                r_sv[h][2 + 2 * k] = xr[off + Nn];
+                r_sv[h][3 + 2 * k] = xr[off + Nn + 1];
+            }
         }
         const int K0 = 4 * Nn + 8;
 #pragma unroll
@@ -1666,27 +1670,36 @@ __global__ __launch_bounds__(WGM* WGN * 64, OCC) void k_gemm3g(ASrc a0, ASrc a1,
         const float* b0s = reinterpret_cast<const float*>(lds + STAGES * STAGE_B + 2 * W0S_B) + kt * BK;
         char* adst = lds + decltype(ST)::value * STAGE_B;
         const int Nn = a0.n_nodes;
-        auto wrow = [&](int r, int c) { return *reinterpret_cast<const float4*>(wsl + r * BK + 4 * c); };
+        auto wrow = [&](int r) { return *reinterpret_cast<const float4*>(wsl + r * BK + 4 * rq); };
+        const float4 bz = *reinterpret_cast<const float4*>(b0s + 4 * rq);
+        const float4 wa = wrow(Nn), wb = wrow(Nn + 1);
+        float4 wl[3], wd[3];
+#pragma unroll
+        for (int k = 0; k < 3; k++) {
+            const int off = Nn + 2 + k * (Nn + 2);
+            wl[k] = wrow(off + Nn);
+            wd[k] = wrow(off + Nn + 1);
+        }
 #pragma unroll
         for (int h = 0; h < 2; h++) {
-            const int c = 2 * rq + h;  // 16-byte chunk: k = 4c .. 4c + 3 of the tile
-            const float4 bz = *reinterpret_cast<const float4*>(b0s + 4 * c);
-            const float4 e0 = wrow(r_oh[0], c), wa = wrow(Nn, c), wb = wrow(Nn + 1, c);
-            float a[4] = {bz.x + e0.x + r_sv[0] * wa.x + r_sv[1] * wb.x, bz.y + e0.y + r_sv[0] * wa.y + r_sv[1] * wb.y,
-                          bz.z + e0.z + r_sv[0] * wa.z + r_sv[1] * wb.z, bz.w + e0.w + r_sv[0] * wa.w + r_sv[1] * wb.w};
+            const int* oh = r_oh[h];
+            const float* sv = r_sv[h];
+            const float4 e0 = wrow(oh[0]);
+            float a[4] = {bz.x + e0.x + sv[0] * wa.x + sv[1] * wb.x, bz.y + e0.y + sv[0] * wa.y + sv[1] * wb.y,
+                          bz.z + e0.z + sv[0] * wa.z + sv[1] * wb.z, bz.w + e0.w + sv[0] * wa.w + sv[1] * wb.w};
 #pragma unroll
             for (int k = 0; k < 3; k++) {
-                const int off = Nn + 2 + k * (Nn + 2);
-                const float4 ek = wrow(r_oh[k + 1], c), wl = wrow(off + Nn, c), wd = wrow(off + Nn + 1, c);
-                const float ln = r_sv[2 + 2 * k], ld = r_sv[3 + 2 * k];
-                a[0] += ek.x + ln * wl.x + ld * wd.x;
-                a[1] += ek.y + ln * wl.y + ld * wd.y;
-                a[2] += ek.z + ln * wl.z + ld * wd.z;
-                a[3] += ek.w + ln * wl.w + ld * wd.w;
+                const float4 ek = wrow(oh[k + 1]);
+                const float ln = sv[2 + 2 * k], ld = sv[3 + 2 * k];
+                a[0] += ek.x + ln * wl[k].x + ld * wd[k].x;
+                a[1] += ek.y + ln * wl[k].y + ld * wd[k].y;
+                a[2] += ek.z + ln * wl[k].z + ld * wd[k].z;
+                a[3] += ek.w + ln * wl[k].w + ld * wd[k].w;
             }
 #pragma unroll
             for (int e = 0; e < 4; e++) a[e] = a0.act0 == 1 ? act_t<1>(a[e], 1) : act_t<-1>(a[e], a0.act0);
-            *reinterpret_cast<float4*>(adst + rr * 128 + ((c ^ gswz<MF>((rr >> 1) & 7)) << 4)) =
+            const int R = rr + h * (BM / 2);
+            *reinterpret_cast<float4*>(adst + R * 128 + ((rq ^ gswz<MF>((R >> 1) & 7)) << 4)) =
                 make_float4(a[0], a[1], a[2], a[3]);
         }
     };

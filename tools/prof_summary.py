@@ -29,7 +29,10 @@ DQN = ["dqn.enc0(K=642)", "dqn.enc1(K=512)", "dqn.q(K=256)"]
 
 # k_gemm (gm_gemm_f32, fused path): encoder layer 0 runs in k_routing_enc, the LSTM
 # cells carry their gate epilogue, the DQN's first layer gathers the NetMon readout
-NETMON_G = ["netmon.enc1(K=512)", "netmon.enc2(K=256)", "netmon.rnn_obs(K=128+128)", "netmon.rnn_update(K=sum128+128)"]
+# (round 5: encoder layers 1-3 are one launch, gm_encoder_x3; --netmon-layers for older profiles)
+NETMON_G_LAYERS = ["netmon.enc1(K=512)", "netmon.enc2(K=256)", "netmon.rnn_obs(K=128+128)",
+                   "netmon.rnn_update(K=sum128+128)"]
+NETMON_G = ["netmon.enc(layers 1-3 chained)", "netmon.rnn_obs(K=128+128)", "netmon.rnn_update(K=sum128+128)"]
 def dqn_g(env_k=128, fused_head=True):
     """DQN layer labels of the fused rollout; env_k = env-obs columns of layer 1 (128 with the
     GEMM-ready obs copy, 130 without); before gm_gemm_x3_head the head was a third GEMM."""
@@ -55,11 +58,11 @@ def linear_labels(n_dispatch, episode_steps, netmon_iters=1, netmon=NETMON, dqn=
     return out[:n_dispatch]
 
 
-def relabel(rows, episode_steps, dqn_g=DQN_G):
+def relabel(rows, episode_steps, dqn_g=DQN_G, netmon_g=None):
     for r in rows:  # k_gemm3<...> (split-f16 form) and k_gemm<...> (f32) are one call-site sequence
         if "k_gemm3" in r["Kernel_Name"] or r["Kernel_Name"].startswith("k_gemm") or "k_gemmI" in r["Kernel_Name"]:
             r["Kernel_Name"] = "k_gemm"
-    for name, nm, dq in (("k_linear_f32", NETMON, DQN), ("k_gemm", NETMON_G, dqn_g)):
+    for name, nm, dq in (("k_linear_f32", NETMON, DQN), ("k_gemm", netmon_g or NETMON_G, dqn_g)):
         lin = [r for r in rows if r["Kernel_Name"].startswith(name)]
         for r, lab in zip(lin, linear_labels(len(lin), episode_steps, netmon=nm, dqn=dq)):
             r["Kernel_Name"] = f"{name}[{lab}]"
@@ -73,6 +76,7 @@ def bench_tag(name, grid, rows, env_k=128):
     gemm = {
         f"dqn.enc0(K=512 readout+{env_k})": f"linear:dqn.encoder.linear_layers.0:{M}x512x{512 + env_k}",
         "dqn.enc1+q(K=512, Q head fused)": f"linear:dqn.encoder.linear_layers.1+head:{M}x256x512",
+        "netmon.enc(layers 1-3 chained)": f"linear:netmon.encode.linear_layers.1+chain:{M}x256x512",
         "netmon.enc1(K=512)": f"linear:netmon.encode.linear_layers.1:{M}x256x512",
         "netmon.enc2(K=256)": f"linear:netmon.encode.linear_layers.2:{M}x128x256",
         "netmon.rnn_obs(K=128+128)": f"lstm:netmon.rnn_obs:{M}x512x256",
@@ -104,12 +108,14 @@ def main():
     ap.add_argument("--rows", type=int, default=81920, help="GEMM rows of the profiled rollout (n_env * N)")
     ap.add_argument("--env-k", type=int, default=128,
                     help="env-obs columns of DQN layer 1 (128: GEMM-ready obs copy, 130: GM_GEMM_OBS=0 profiles)")
+    ap.add_argument("--netmon-layers", action="store_true", help="profiles taken before gm_encoder_x3 (round 5)")
     a = ap.parse_args()
+    nmg = NETMON_G_LAYERS if a.netmon_layers else NETMON_G
     dqn_g_ = dqn_g(a.env_k, not a.unfused_head)
     dur = defaultdict(list)
     trace = load(a.trace)
     trace.sort(key=lambda r: int(r["Start_Timestamp"]))
-    for r in relabel(trace, a.episode_steps, dqn_g_):
+    for r in relabel(trace, a.episode_steps, dqn_g_, nmg):
         dur[key(r)].append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
     pmc = defaultdict(dict)
     for name, path in (("FETCH_SIZE", a.fetch), ("WRITE_SIZE", a.write)):
@@ -118,7 +124,7 @@ def main():
         acc = defaultdict(list)
         rows = [r for r in load(path) if r["Counter_Name"] == name]
         rows.sort(key=lambda r: int(r["Dispatch_Id"]))
-        for r in relabel(rows, a.episode_steps, dqn_g_):
+        for r in relabel(rows, a.episode_steps, dqn_g_, nmg):
             if r["Counter_Name"] == name:
                 acc[key(r)].append(float(r["Counter_Value"]))
         for k, v in acc.items():
