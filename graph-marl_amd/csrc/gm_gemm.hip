@@ -1664,7 +1664,7 @@ __global__ __launch_bounds__(WGM* WGN * 64, OCC) void k_gemm3g(ASrc a0, ASrc a1,
 #pragma unroll
         for (int j = 0; j < RW; j++) dma16(rw0, base + j * 1024, wso[j], kt * BK * 4);
     };
-    // A tile kt into stage ST from slice stage kt & 1 (landed and published by a barrier)
+    // split-f16 A tile kt into stage ST from slice stage kt & 1 (landed and published by a barrier)
     auto renc_a = [&](auto ST, int kt) {
         const float* wsl = reinterpret_cast<const float*>(lds + STAGES * STAGE_B + (kt & 1) * W0S_B);
         const float* b0s = reinterpret_cast<const float*>(lds + STAGES * STAGE_B + 2 * W0S_B) + kt * BK;
@@ -1680,6 +1680,8 @@ __global__ __launch_bounds__(WGM* WGN * 64, OCC) void k_gemm3g(ASrc a0, ASrc a1,
             wl[k] = wrow(off + Nn);
             wd[k] = wrow(off + Nn + 1);
         }
+        // the folded layer's activation resolved once per tile (act_dispatch), not per element
+        act_dispatch(a0.act0, [&](auto ACT) {
 #pragma unroll
         for (int h = 0; h < 2; h++) {
             const int* oh = r_oh[h];
@@ -1697,11 +1699,21 @@ __global__ __launch_bounds__(WGM* WGN * 64, OCC) void k_gemm3g(ASrc a0, ASrc a1,
                 a[3] += ek.w + ln * wl[k].w + ld * wd[k].w;
             }
 #pragma unroll
-            for (int e = 0; e < 4; e++) a[e] = a0.act0 == 1 ? act_t<1>(a[e], 1) : act_t<-1>(a[e], a0.act0);
+            for (int e = 0; e < 4; e++) a[e] = act_t<decltype(ACT)::value>(a[e], a0.act0);
+            // split once here (the bits of the k loop's split8), stored where the 16x16 read takes its A
+            // chunks: hi of k 8q .. 8q + 7 at logical chunk 2q, lo at 2q + 1 (q = rq / 2, this thread's 4 k
+            // at byte 8 (rq & 1)); even rows store hi first, odd rows lo first, so the two rows of a
+            // 16-lane store group hit disjoint banks
+            half4 hi, lo;
+            split4e(make_float4(a[0], a[1], a[2], a[3]), 0, hi, lo);
             const int R = rr + h * (BM / 2);
-            *reinterpret_cast<float4*>(adst + R * 128 + ((rq ^ gswz<MF>((R >> 1) & 7)) << 4)) =
-                make_float4(a[0], a[1], a[2], a[3]);
+            const int sw = gswz<MF>((R >> 1) & 7), odd = R & 1;
+            char* rowp = adst + R * 128 + 8 * (rq & 1);
+            const half4 first = odd ? lo : hi, second = odd ? hi : lo;
+            *reinterpret_cast<half4*>(rowp + (((2 * (rq >> 1) + odd) ^ sw) << 4)) = first;
+            *reinterpret_cast<half4*>(rowp + (((2 * (rq >> 1) + 1 - odd) ^ sw) << 4)) = second;
         }
+        });
     };
 
     // DMA of k tile kt into stage ST (all LDS bases wave-uniform); ROUTING_ENC: the B tile, the next
@@ -1990,7 +2002,14 @@ __global__ __launch_bounds__(WGM* WGN * 64, OCC) void k_gemm3g(ASrc a0, ASrc a1,
             read(ST, I0{}, fa);
             read(ST, I1{}, fb);
 #pragma unroll
-            for (int i = 0; i < 2 * TM; i++) split_blk(fa, i, sah[i], sal[i]);
+            for (int i = 0; i < 2 * TM; i++) {
+                if constexpr (RENC) {  // stored split (renc_a): hi / lo chunks as read
+                    sah[i] = __builtin_bit_cast(half8, fa.xa[i][0]);
+                    sal[i] = __builtin_bit_cast(half8, fa.xa[i][1]);
+                } else {
+                    split_blk(fa, i, sah[i], sal[i]);
+                }
+            }
             __builtin_amdgcn_sched_barrier(0);
             GM_STAMP(kt, 3);
             if (!late) {
