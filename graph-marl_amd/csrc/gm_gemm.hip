@@ -1366,16 +1366,20 @@ __device__ __forceinline__ void dqn_tail(floatx4 (&acc)[T2][N2], const Epi& ep, 
 // The block (BM rows x the layer's whole width K2 = WGN * N2 * 16) sends its activations through bias +
 // activation and the split (split4: the bits a dense A tile of the next layer would get) into two
 // K-major LDS images ([k][BM rows] f16, dqn_swz slots: EPI_DQN's layout with BM * 2-byte rows), which
-// alias the finished operand stages. The next layer (N3 = WGN * J3 * 16 columns: wave (wr, wc) computes
-// rows 16 T2 wr .., columns 16 J3 wc ..) reads its A fragments transposed from the images
-// (ds_read_b64_tr_b16) and its packed weight fragments straight from L2, two k tiles ahead, and stores
-// act3(. + b3) with epilogue16. The m x K2 activation of the first layer never reaches HBM.
-template <int WGM, int WGN, int T2, int N2, int BM, int J3, int A = -1>
+// alias the finished operand stages. The next layer (N3 columns) has its own wave grid: NW / W3N waves over
+// the rows (T3 16-row blocks each) x W3N over the columns (J3 16-column blocks each), so each weight
+// fragment is fetched by NW / W3N waves (2, not WGM = 4: half the tail's L2 traffic). Each wave reads its A
+// fragments transposed from the images (ds_read_b64_tr_b16) and its packed weight fragments straight from
+// L2, two k tiles ahead, and stores act3(. + b3) with epilogue16. The m x K2 activation of the first layer
+// never reaches HBM.
+template <int WGM, int WGN, int T2, int N2, int BM, int N3, int W3N, int A = -1>
 __device__ __forceinline__ void chain_tail(floatx4 (&acc)[T2][N2], const Epi& ep, char* lds, int m0, int wr, int wc,
                                            int M, int lane) {
     static_assert(WGM * T2 * 16 == BM, "the wave rows hold the block's rows");
+    constexpr int NW = WGM * WGN, W3M = NW / W3N;
+    constexpr int T3 = BM / 16 / W3M, J3 = N3 / 16 / W3N;
+    static_assert(NW % W3N == 0 && T3 * 16 * W3M == BM && J3 * 16 * W3N == N3 && J3 % 2 == 0, "layer-3 wave grid");
     constexpr int K2 = WGN * N2 * 16;  // next layer's K = this layer's width
-    constexpr int N3 = WGN * J3 * 16;  // next layer's width
     constexpr int RS = BM * 2;         // image row bytes
     constexpr int NK = K2 / 32;        // next layer's k tiles
     char* ih = lds;
@@ -1402,14 +1406,15 @@ __device__ __forceinline__ void chain_tail(floatx4 (&acc)[T2][N2], const Epi& ep
             *reinterpret_cast<half4*>(il + off) = lo;
         }
     }
-    // weight fragments of this wave's 16 J3 columns: row n3 = 16 J3 wc + 16 jb + l16, k 8 q .. 8 q + 7 of
+    const int w3 = wr * WGN + wc, w3r = w3 / W3N, w3c = w3 % W3N;  // this wave's layer-3 block
+    // weight fragments of this wave's 16 J3 columns: row n3 = 16 J3 w3c + 16 jb + l16, k 8 q .. 8 q + 7 of
     // each 32-deep tile (16-k block (q >> 1), halves (q & 1) x 8; hi at +0, lo at +32 of a block's 64 bytes)
     const int q = lane >> 4;
     const __amdgpu_buffer_rsrc_t rw = rsrc(reinterpret_cast<const float*>(ep.w2), ep.w2bytes);
     int wo[J3];
 #pragma unroll
     for (int jb = 0; jb < J3; jb++)
-        wo[jb] = (int)((wc * J3 * 16 + jb * 16 + l16) * ep.ldw2) + (q >> 1) * 64 + (q & 1) * 16;
+        wo[jb] = (int)((w3c * J3 * 16 + jb * 16 + l16) * ep.ldw2) + (q >> 1) * 64 + (q & 1) * 16;
     constexpr int NB3 = 2;  // weight tiles in flight
     u32x4 pbh[NB3][J3], pbl[NB3][J3];
     auto bfetch = [&](int slot, int kt) {
@@ -1422,9 +1427,9 @@ __device__ __forceinline__ void chain_tail(floatx4 (&acc)[T2][N2], const Epi& ep
 #pragma unroll
     for (int t = 0; t < NB3; t++) bfetch(t, t);
     __syncthreads();  // the images are complete
-    floatx4 acc3[T2][J3];
+    floatx4 acc3[T3][J3];
 #pragma unroll
-    for (int i = 0; i < T2; i++)
+    for (int i = 0; i < T3; i++)
 #pragma unroll
         for (int j = 0; j < J3; j++)
 #pragma unroll
@@ -1442,10 +1447,10 @@ __device__ __forceinline__ void chain_tail(floatx4 (&acc)[T2][N2], const Epi& ep
         return half8{x0[0], x0[1], x0[2], x0[3], x1[0], x1[1], x1[2], x1[3]};
     };
     const _Float16 s12 = (_Float16)(1.0f / LO_S);
-    const int row0 = wr * T2 * 16;
-    half8 fah[2][T2], fal[2][T2];
+    const int row0 = w3r * T3 * 16;
+    half8 fah[2][T3], fal[2][T3];
 #pragma unroll
-    for (int i = 0; i < T2; i++) {
+    for (int i = 0; i < T3; i++) {
         fah[0][i] = frag(ih, 0, row0 + 16 * i);
         fal[0][i] = frag(il, 0, row0 + 16 * i);
     }
@@ -1454,7 +1459,7 @@ __device__ __forceinline__ void chain_tail(floatx4 (&acc)[T2][N2], const Epi& ep
         const int cur = kt & 1, slot = kt % NB3;
         if (kt + 1 < NK) {
 #pragma unroll
-            for (int i = 0; i < T2; i++) {
+            for (int i = 0; i < T3; i++) {
                 fah[cur ^ 1][i] = frag(ih, (kt + 1) * 32, row0 + 16 * i);
                 fal[cur ^ 1][i] = frag(il, (kt + 1) * 32, row0 + 16 * i);
             }
@@ -1470,7 +1475,7 @@ __device__ __forceinline__ void chain_tail(floatx4 (&acc)[T2][N2], const Epi& ep
         for (int jb = 0; jb < J3; jb++) {
             const half8 bs = bh[jb] * s12;
 #pragma unroll
-            for (int i = 0; i < T2; i++) {
+            for (int i = 0; i < T3; i++) {
                 floatx4& c = acc3[i][jb];
                 c = __builtin_amdgcn_mfma_f32_16x16x32_f16(fal[cur][i], bs, c, 0, 0, 0);
                 c = __builtin_amdgcn_mfma_f32_16x16x32_f16(fah[cur][i], bl[jb], c, 0, 0, 0);
@@ -1480,19 +1485,19 @@ __device__ __forceinline__ void chain_tail(floatx4 (&acc)[T2][N2], const Epi& ep
     }
     const float si = *ep.wsi2;
 #pragma unroll
-    for (int i = 0; i < T2; i++)
+    for (int i = 0; i < T3; i++)
 #pragma unroll
         for (int j = 0; j < J3; j++)
 #pragma unroll
             for (int r = 0; r < 4; r++) acc3[i][j][r] *= si;
-    range_guard16<T2, J3>(acc3, ep.range_flag, lane);
+    range_guard16<T3, J3>(acc3, ep.range_flag, lane);
     Epi e3 = ep;
     e3.bias = ep.b2;
     e3.act = ep.act2;
     e3.sbits = nullptr;
-    CIn16<T2, EPI_BIAS> none;
+    CIn16<T3, EPI_BIAS> none;
     act_dispatch(e3.act, [&](auto A3) {
-        epilogue16<T2, J3, EPI_BIAS, decltype(A3)::value>(acc3, e3, m0 + row0, wc * J3 * 16, M, N3, lane, none);
+        epilogue16<T3, J3, EPI_BIAS, decltype(A3)::value>(acc3, e3, m0 + row0, w3c * J3 * 16, M, N3, lane, none);
     });
 }
 
@@ -2129,7 +2134,7 @@ __global__ __launch_bounds__(WGM* WGN * 64, OCC) void k_gemm3g(ASrc a0, ASrc a1,
             });
         else if constexpr (EPI == EPI_CHAIN)
             act_dispatch(ep.act, [&](auto A) {
-                chain_tail<WGM, WGN, 2 * TM, 2 * TN, BM, 4, decltype(A)::value>(acc4, ep, lds, m0, wr, wc, M, lane);
+                chain_tail<WGM, WGN, 2 * TM, 2 * TN, BM, 128, 4, decltype(A)::value>(acc4, ep, lds, m0, wr, wc, M, lane);
             });
         else
             if constexpr (EPI == EPI_BIAS)
