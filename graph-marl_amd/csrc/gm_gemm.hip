@@ -1565,7 +1565,7 @@ __global__ __launch_bounds__(WGM* WGN * 64, OCC) void k_gemm3g(ASrc a0, ASrc a1,
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: LDS bases in SGPRs
 #if GM_DIAG == 30
     // stamps of k steps 4..11 x 8 points by waves 0 and NW / 2 (one SIMD), kept in LDS until the end
-    unsigned long long* stl = reinterpret_cast<unsigned long long*>(lds + STAGES * STAGE_B);
+    unsigned long long* stl = reinterpret_cast<unsigned long long*>(lds + STAGES * STAGE_B + RENC_B);
     const bool stw = lane == 0 && (wave == 0 || wave == NW / 2);
     auto stamp = [&](int kt, int pt) {
         if (stw && kt >= 4 && kt < 12) stl[((wave != 0) * 8 + (kt - 4)) * 8 + pt] = __builtin_amdgcn_s_memtime();
@@ -1663,15 +1663,18 @@ __global__ __launch_bounds__(WGM* WGN * 64, OCC) void k_gemm3g(ASrc a0, ASrc a1,
         for (int k = tid; k < a0.k; k += NW * 64) b0s[k] = a0.bias0 ? a0.bias0[k] : 0.f;
     }
     const __amdgpu_buffer_rsrc_t rw0 = rsrc(RENC ? a0.p1 : a0.p0, RENC ? (unsigned)a0.bytes1 : 0u);
-    // DMA of the W0^T slice of k tile kt (32 columns of every input row) into slice stage kt & 1
-    auto issue_w0 = [&](int kt) {
-        char* base = lds + STAGES * STAGE_B + (kt & 1) * W0S_B + wave * RW * 1024;
+    // DMA of the W0^T slice of k tile kt (32 columns of every input row) into slice stage kt & 1 = WS (2-stage
+    // tile: compile-time, like every LDS base of the loop)
+    auto issue_w0 = [&](auto WS, int kt) {
+        char* base = lds + STAGES * STAGE_B + decltype(WS)::value * W0S_B + wave * RW * 1024;
 #pragma unroll
         for (int j = 0; j < RW; j++) dma16(rw0, base + j * 1024, wso[j], kt * BK * 4);
     };
     // split-f16 A tile kt into stage ST from slice stage kt & 1 (landed and published by a barrier)
-    auto renc_a = [&](auto ST, int kt) {
-        const float* wsl = reinterpret_cast<const float*>(lds + STAGES * STAGE_B + (kt & 1) * W0S_B);
+    typedef float f32x2 __attribute__((ext_vector_type(2)));
+    auto lo2 = [](const float4& v, int p) { return p == 0 ? f32x2{v.x, v.y} : f32x2{v.z, v.w}; };
+    auto renc_a = [&](auto ST, int kt) {  // (tile kt's slice stage kt & 1 = its operand stage ST)
+        const float* wsl = reinterpret_cast<const float*>(lds + STAGES * STAGE_B + decltype(ST)::value * W0S_B);
         const float* b0s = reinterpret_cast<const float*>(lds + STAGES * STAGE_B + 2 * W0S_B) + kt * BK;
         char* adst = lds + decltype(ST)::value * STAGE_B;
         const int Nn = a0.n_nodes;
@@ -1691,18 +1694,21 @@ __global__ __launch_bounds__(WGM* WGN * 64, OCC) void k_gemm3g(ASrc a0, ASrc a1,
         for (int h = 0; h < 2; h++) {
             const int* oh = r_oh[h];
             const float* sv = r_sv[h];
+            // element pairs on packed f32 (v_pk_fma_f32 / v_pk_add_f32): the same operations, half the issues
             const float4 e0 = wrow(oh[0]);
-            float a[4] = {bz.x + e0.x + sv[0] * wa.x + sv[1] * wb.x, bz.y + e0.y + sv[0] * wa.y + sv[1] * wb.y,
-                          bz.z + e0.z + sv[0] * wa.z + sv[1] * wb.z, bz.w + e0.w + sv[0] * wa.w + sv[1] * wb.w};
+            const f32x2 s0 = {sv[0], sv[0]}, s1 = {sv[1], sv[1]};
+            f32x2 ap[2];
+#pragma unroll
+            for (int p = 0; p < 2; p++)
+                ap[p] = lo2(bz, p) + lo2(e0, p) + s0 * lo2(wa, p) + s1 * lo2(wb, p);
 #pragma unroll
             for (int k = 0; k < 3; k++) {
                 const float4 ek = wrow(oh[k + 1]);
-                const float ln = sv[2 + 2 * k], ld = sv[3 + 2 * k];
-                a[0] += ek.x + ln * wl[k].x + ld * wd[k].x;
-                a[1] += ek.y + ln * wl[k].y + ld * wd[k].y;
-                a[2] += ek.z + ln * wl[k].z + ld * wd[k].z;
-                a[3] += ek.w + ln * wl[k].w + ld * wd[k].w;
+                const f32x2 ln = {sv[2 + 2 * k], sv[2 + 2 * k]}, ld = {sv[3 + 2 * k], sv[3 + 2 * k]};
+#pragma unroll
+                for (int p = 0; p < 2; p++) ap[p] += lo2(ek, p) + ln * lo2(wl[k], p) + ld * lo2(wd[k], p);
             }
+            float a[4] = {ap[0][0], ap[0][1], ap[1][0], ap[1][1]};
 #pragma unroll
             for (int e = 0; e < 4; e++) a[e] = act_t<decltype(ACT)::value>(a[e], a0.act0);
             // split once here (the bits of the k loop's split8), stored where the 16x16 read takes its A
@@ -1721,17 +1727,19 @@ __global__ __launch_bounds__(WGM* WGN * 64, OCC) void k_gemm3g(ASrc a0, ASrc a1,
         });
     };
 
-    // DMA of k tile kt into stage ST (all LDS bases wave-uniform); ROUTING_ENC: the B tile, the next
-    // W0^T slice, and the A tile computed from this tile's slice
+    // DMA of k tile kt into stage ST (all LDS bases wave-uniform); ROUTING_ENC: the A tile computed from
+    // this tile's slice, then the B tile and the next W0^T slice. In that order: LDS reads after an LDS-DMA
+    // whose destination the compiler cannot tell apart wait for it (s_waitcnt vmcnt(0)), which put the DMA
+    // latency in front of the A computation (2.2-3.1 k of a 4.7 k-cycle step, tools/stamp_fold.py)
     auto issue = [&](auto ST, int kt) {
         char* base = lds + decltype(ST)::value * STAGE_B + wave * NA * 1024;
         const int k0 = kt * BK;
         if constexpr (RENC) {
+            renc_a(ST, kt);
             char* bbase = lds + decltype(ST)::value * STAGE_B + BM * 128 + wave * NB * 1024;
 #pragma unroll
             for (int j = 0; j < NB; j++) dma16(rw, bbase + j * 1024, wo[j], k0 * 4);
-            if ((kt + 1) * BK < K) issue_w0(kt + 1);
-            renc_a(ST, kt);
+            if ((kt + 1) * BK < K) issue_w0(std::integral_constant<int, 1 - decltype(ST)::value>{}, kt + 1);
             return;
         }
         if (k0 < a0.k) {
@@ -1976,7 +1984,7 @@ __global__ __launch_bounds__(WGM* WGN * 64, OCC) void k_gemm3g(ASrc a0, ASrc a1,
             mfma16s(fb, I1{}, sah, sal);
         };
         if constexpr (RENC) {  // the first slice lands and is published before tile 0's A is computed
-            issue_w0(0);
+            issue_w0(std::integral_constant<int, 0>{}, 0);
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             __syncthreads();
         }
