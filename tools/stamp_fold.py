@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Where a k step of the fold (routing-encoder A source, NetMon encoder layer 2 at 81 920 x 256 x 512) and of
-the readout-source DQN layer 1 goes in the ping-pong loop (diagnostic build 30: s_memtime stamps of waves 0
+the readout-source DQN layer 1 (tile 9) goes in the ping-pong loop (diagnostic build 30: s_memtime stamps of waves 0
 (early) and 4 (late) of every block, one SIMD, k steps 4..11):
   GM_LIB=graph-marl_amd/lib/vstamp/libgraphmarl_amd.so python tools/stamp_fold.py
 Stamp points of a step: 0 after the barrier, 1 after the late wave's MFMAs of the previous tile, 2 after the
@@ -38,10 +38,23 @@ def main():
     rows = B * N
     y2 = torch.empty(rows, 256, device="cuda")
     y3 = torch.empty(rows, 128, device="cuda")
+    # DQN layer 1 on its READOUT source (as tools/stamp_bench.py): 4096 graphs x 20 agents, K = 512 + 128
+    state, hprev = torch.randn(rows, 256, device="cuda"), torch.randn(rows, 256, device="cuda")
+    nbr = torch.randint(0, N, (B, N, 3), device="cuda", dtype=torch.int32)
+    agent_node = torch.randint(0, N, (B, 20), device="cuda", dtype=torch.int32)
+    obs = torch.randn(B, 20, 128, device="cuda")
+    w = torch.randn(512, 640, device="cuda") / 640 ** 0.5
+    b = torch.randn(512, device="cuda")
+    wp, ldw = FU._pad_cols(w)
+    y = torch.empty(rows, 512, device="cuda")
     shapes = {
         "fold_81920x256x512": lambda: FU.gemm(FU.routing_enc_src(l0, x, env.nbr, N), None, None, 0, l1.bias.data_ptr(),
                                               rows, 256, FU._epi(l1.act), y2.data_ptr(), 256, x3=FU.pack_x3(l1)),
         "chain": lambda: FU.encoder_chain(l0, l1, l2, x, env.nbr, N, y3),
+        "dqn_l1_readout_81920x512x640": lambda: FU.gemm(
+            FU.readout(state.data_ptr(), 256, hprev.data_ptr(), 256, nbr, agent_node, N, 128),
+            FU.dense(obs.data_ptr(), 128, 128), wp.data_ptr(), ldw, b.data_ptr(), rows, 512, 1, y.data_ptr(), 512,
+            x3=FU.X3(wp, ldw, 512, 640)),
     }
     for name, fn in shapes.items():
         for _ in range(20):
@@ -56,8 +69,8 @@ def main():
             s = st[:, wv]
             ok = (s[:, :-1, 0] > 0) & (s[:, 1:, 0] > 0)
             segs = {}
-            for nm_, (a, b) in {"late_mfma": (0, 1), "issue": (1, 2), "reads": (2, 3), "early_mfma": (3, 4)}.items():
-                d = (s[:, :-1, b] - s[:, :-1, a])[ok]
+            for nm_, (p0, p1) in {"late_mfma": (0, 1), "issue": (1, 2), "reads": (2, 3), "early_mfma": (3, 4)}.items():
+                d = (s[:, :-1, p1] - s[:, :-1, p0])[ok]
                 segs[nm_] = int(np.median(d)) if d.size else None
             d = (s[:, 1:, 0] - s[:, :-1, 4])[ok]
             segs["to_next_barrier"] = int(np.median(d)) if d.size else None
