@@ -1654,8 +1654,8 @@ __global__ __launch_bounds__(WGM* WGN * 64, OCC) void k_gemm3g(ASrc a0, ASrc a1,
         }
         const int K0 = 4 * Nn + 8;
 #pragma unroll
-        for (int j = 0; j < RW; j++) {
-            const int R = (wave * RW + j) * 8 + sub;
+        for (int j = 0; j < RW; j++) {  // piece j NW + wave: 8 rows of W0^T (see issue_w0)
+            const int R = (j * NW + wave) * 8 + sub;
             wso[j] = R < K0 ? (int)(R * a0.ld1) * 4 + 16 * (lane & 7) : OOB;
         }
         // the folded layer's bias for all k, once (plain loads: retired before the k loop's counted waits)
@@ -1664,11 +1664,15 @@ __global__ __launch_bounds__(WGM* WGN * 64, OCC) void k_gemm3g(ASrc a0, ASrc a1,
     }
     const __amdgpu_buffer_rsrc_t rw0 = rsrc(RENC ? a0.p1 : a0.p0, RENC ? (unsigned)a0.bytes1 : 0u);
     // DMA of the W0^T slice of k tile kt (32 columns of every input row) into slice stage kt & 1 = WS (2-stage
-    // tile: compile-time, like every LDS base of the loop)
+    // tile: compile-time, like every LDS base of the loop). Wave w issues pieces w and NW + w and skips the
+    // pieces past the 4N + 8 input rows (wave-uniform): at N = 20 the 11 pieces put at most 3 of a SIMD's two
+    // waves' DMA issues in a step instead of 4 (the 2-stage loop waits vmcnt(0), so the count may vary)
+    const int w0rows = RENC ? 4 * a0.n_nodes + 8 : 0;
     auto issue_w0 = [&](auto WS, int kt) {
-        char* base = lds + STAGES * STAGE_B + decltype(WS)::value * W0S_B + wave * RW * 1024;
+        char* base = lds + STAGES * STAGE_B + decltype(WS)::value * W0S_B;
 #pragma unroll
-        for (int j = 0; j < RW; j++) dma16(rw0, base + j * 1024, wso[j], kt * BK * 4);
+        for (int j = 0; j < RW; j++)
+            if ((j * NW + wave) * 8 < w0rows) dma16(rw0, base + (j * NW + wave) * 1024, wso[j], kt * BK * 4);
     };
     // split-f16 A tile kt into stage ST from slice stage kt & 1 (landed and published by a barrier)
     typedef float f32x2 __attribute__((ext_vector_type(2)));
