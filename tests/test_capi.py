@@ -107,3 +107,38 @@ def test_training_entry_points_reject_bad_arguments(gm):
     # Q-head backward with more than 4 heads
     assert L.gm_qhead_bwd(vp(16), 5, 5, vp(16), 8, vp(16), 8, 8, 8, 1, vp(16), 8, vp(16), vp(16), vp(16), 8, None,
                           None) == -1
+
+
+def test_routing_encoder_source_rejects_bad_arguments(gm):
+    """gm_encoder_x3 and the ROUTING_ENC A source (round 5) validate before any device call: the source
+    mode, the layer widths (256 -> 128), degree 3, 4N + 8 <= 128 and whole 32-wide k tiles; gm_gemm_f32
+    refuses the source outright."""
+    import importlib
+
+    FU = importlib.import_module("graph-marl_amd.fused")
+    L = gm._lib.lib()
+    FU._setup()
+    vp = ctypes.c_void_p
+
+    def src(**kw):
+        s = FU.ASrc()
+        s.mode, s.p0, s.p1, s.ld0, s.ld1, s.nbr = FU.GM_A_ROUTING_ENC, 16, 16, 88, 512, 16
+        s.n_nodes, s.deg, s.k, s.bias0, s.act0 = 20, 3, 512, 16, 1
+        for k, v in kw.items():
+            setattr(s, k, v)
+        return s
+
+    def chain(s, n2=256, n3=128, m=81920):
+        return L.gm_encoder_x3(ctypes.byref(s), vp(16), vp(16), vp(16), 1, vp(16), vp(16), vp(16), 1, m, n2, n3,
+                               vp(16), 128, None)
+
+    assert chain(src(), n2=512) == -1 and b"256, 128" in L.gm_last_error()
+    assert chain(src(), n3=64) == -1
+    assert chain(src(mode=FU.GM_A_DENSE)) == -1 and b"routing-encoder" in L.gm_last_error()
+    for bad in (dict(deg=4), dict(n_nodes=31), dict(k=500), dict(nbr=None)):
+        assert chain(src(**bad)) != 0, bad
+        assert b"routing-encoder" in L.gm_last_error(), bad
+    assert chain(src(), m=81919) != 0  # rows not whole graphs
+    s = src()
+    assert L.gm_gemm_f32(ctypes.byref(s), None, vp(16), 512, vp(16), 81920, 256, 1, vp(16), 256, None, 0, None, 0,
+                         None, None) != 0
