@@ -174,6 +174,14 @@ __device__ __forceinline__ float tanh_fast(float x) { return 2.0f * sigm(2.0f * 
 // 1 leaky_relu, -1 any GM_ACT_* at run time (a per-element branch tree: relu / elu / tanh / sigmoid
 // only). act_dispatch calls f with A chosen from the wave-uniform act, so the default epilogues carry
 // no activation branches per element.
+// (up ? b : a, up ? a : b) as a bitwise blend of the two values: written as selects of two elements of a
+// local array, LLVM turns them into one dynamically indexed access, and the array is then lowered to
+// 16-way v_cmp / v_cndmask chains per element (the Q-head reduction cost ~29 us per 81 920-row launch)
+__device__ __forceinline__ void swap_if(bool up, float a, float b, float& mine, float& other) {
+    const unsigned m = up ? ~0u : 0u, ua = __builtin_bit_cast(unsigned, a), ub = __builtin_bit_cast(unsigned, b);
+    mine = __builtin_bit_cast(float, (ua & ~m) | (ub & m));
+    other = __builtin_bit_cast(float, (ub & ~m) | (ua & m));
+}
 template <int A>
 __device__ __forceinline__ float act_t(float v, int act) {
     if constexpr (A == 0)
@@ -408,8 +416,8 @@ __device__ __forceinline__ void head_epilogue(floatx16 (&acc)[TM][TN], const Epi
             const bool up = (l32 & mask) != 0;
 #pragma unroll
             for (int k = 0; k < n; k++) {
-                const float mine = up ? x[n + k] : x[k];
-                const float other = up ? x[k] : x[n + k];
+                float mine, other;
+                swap_if(up, x[k], x[n + k], mine, other);
                 x[k] = mine + __shfl_xor(other, mask);
             }
         }
@@ -1152,17 +1160,27 @@ __device__ __forceinline__ void dgrad_epilogue16(floatx4 (&acc)[T2][N2], const E
 // EPI_HEAD on the 16x16 layout: per row block i, a lane's partial dot products (4 rows x 4 heads)
 // are reduce-scattered over its 16-lane group (xor 8..1: 15 shuffles; lane ends with entry l & 15
 // = row 4 (l >> 4) + (e >> 2), head e & 3), the WGN column waves summed through LDS.
+// hl (optional): the block's bias and Q-head weight columns staged in LDS before the k loop ([5][block
+// width]: bias, wq rows 0..3, zero past N / nq; k_gemm3g head_load / head_store), instead of global loads here
 template <int T2, int N2, int WGN, int BM, int A = -1>
 __device__ __forceinline__ void head_epilogue16(floatx4 (&acc)[T2][N2], const Epi& ep, char* lds, int m0, int wr,
-                                                int wc, int M, int N, int lane, int tid, int n0 = 0) {
+                                                int wc, int M, int N, int lane, int tid, int n0 = 0,
+                                                const float* hl = nullptr) {
+    constexpr int BNH = WGN * N2 * 16;  // the block's columns
     const int l16 = lane & 15, rq = 4 * (lane >> 4);
     float bv[N2], wqv[N2][4];
 #pragma unroll
     for (int j = 0; j < N2; j++) {
-        const int col = n0 + wc * N2 * 16 + j * 16 + l16;
-        bv[j] = (ep.bias && col < N) ? ep.bias[col] : 0.f;
+        const int cl = wc * N2 * 16 + j * 16 + l16, col = n0 + cl;
+        if (hl) {
+            bv[j] = hl[cl];
 #pragma unroll
-        for (int a = 0; a < 4; a++) wqv[j][a] = (col < N && a < ep.nq) ? ep.wq[a * ep.ldwq + col] : 0.f;
+            for (int a = 0; a < 4; a++) wqv[j][a] = hl[(1 + a) * BNH + cl];
+        } else {
+            bv[j] = (ep.bias && col < N) ? ep.bias[col] : 0.f;
+#pragma unroll
+            for (int a = 0; a < 4; a++) wqv[j][a] = (col < N && a < ep.nq) ? ep.wq[a * ep.ldwq + col] : 0.f;
+        }
     }
     float* qp = reinterpret_cast<float*>(lds);  // [WGN][BM][4]
     float red[T2];
@@ -1191,8 +1209,8 @@ __device__ __forceinline__ void head_epilogue16(floatx4 (&acc)[T2][N2], const Ep
             const bool up = (l16 & mask) != 0;
 #pragma unroll
             for (int k = 0; k < n; k++) {
-                const float mine = up ? x[n + k] : x[k];
-                const float other = up ? x[k] : x[n + k];
+                float mine, other;
+                swap_if(up, x[k], x[n + k], mine, other);
                 x[k] = mine + __shfl_xor(other, mask);
             }
         }
@@ -1555,17 +1573,21 @@ __global__ __launch_bounds__(WGM* WGN * 64, OCC) void k_gemm3g(ASrc a0, ASrc a1,
                   "routing-encoder source: 2-stage ping-pong tile, 8 threads x 2 rows per 128 A rows");
     static_assert(EPI != EPI_CHAIN || (MF == 1 && STAGES * STAGE_B + RENC_B >= 2 * BN * BM * 2),
                   "chain epilogue: the next layer's split A images alias the operand stages");
+    // EPI_HEAD: the block's bias and Q-head weight columns, staged once (head_load / head_store) so that the
+    // epilogue does not start with 40 dependent global loads per lane
+    constexpr int HEAD_N = EPI == EPI_HEAD ? 5 * BN : 0;
+    constexpr int HEAD_B = HEAD_N * 4;
 #if GM_DIAG == 30
-    __shared__ __attribute__((aligned(16))) char lds[STAGES * STAGE_B + RENC_B + 1024];
+    __shared__ __attribute__((aligned(16))) char lds[STAGES * STAGE_B + RENC_B + HEAD_B + 1024];
 #else
-    __shared__ __attribute__((aligned(16))) char lds[STAGES * STAGE_B + RENC_B];
+    __shared__ __attribute__((aligned(16))) char lds[STAGES * STAGE_B + RENC_B + HEAD_B];
 #endif
 
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: LDS bases in SGPRs
 #if GM_DIAG == 30
     // stamps of k steps 4..11 x 8 points by waves 0 and NW / 2 (one SIMD), kept in LDS until the end
-    unsigned long long* stl = reinterpret_cast<unsigned long long*>(lds + STAGES * STAGE_B + RENC_B);
+    unsigned long long* stl = reinterpret_cast<unsigned long long*>(lds + STAGES * STAGE_B + RENC_B + HEAD_B);
     const bool stw = lane == 0 && (wave == 0 || wave == NW / 2);
     auto stamp = [&](int kt, int pt) {
         if (stw && kt >= 4 && kt < 12) stl[((wave != 0) * 8 + (kt - 4)) * 8 + pt] = __builtin_amdgcn_s_memtime();
@@ -1663,6 +1685,33 @@ __global__ __launch_bounds__(WGM* WGN * 64, OCC) void k_gemm3g(ASrc a0, ASrc a1,
         for (int k = tid; k < a0.k; k += NW * 64) b0s[k] = a0.bias0 ? a0.bias0[k] : 0.f;
     }
     const __amdgpu_buffer_rsrc_t rw0 = rsrc(RENC ? a0.p1 : a0.p0, RENC ? (unsigned)a0.bytes1 : 0u);
+    // EPI_HEAD staging: loaded into registers before the prologue DMAs, stored to LDS after them (the store's
+    // wait then covers these loads only: they were issued first); published by the k loop's barriers
+    constexpr int HPT = HEAD_N ? (HEAD_N + NW * 64 - 1) / (NW * 64) : 1;
+    float hv[HPT];
+    float* const hlds = reinterpret_cast<float*>(lds + STAGES * STAGE_B + RENC_B);
+    auto head_load = [&]() {
+        if constexpr (EPI == EPI_HEAD) {
+#pragma unroll
+            for (int i = 0; i < HPT; i++) {
+                const int e = tid + i * NW * 64, r = e / BN, col = n0 + (e - r * BN);
+                hv[i] = 0.f;
+                if (e < HEAD_N && col < N) {
+                    if (r == 0)
+                        hv[i] = ep.bias ? ep.bias[col] : 0.f;
+                    else if (r - 1 < ep.nq)
+                        hv[i] = ep.wq[(r - 1) * ep.ldwq + col];
+                }
+            }
+        }
+    };
+    auto head_store = [&]() {
+        if constexpr (EPI == EPI_HEAD) {
+#pragma unroll
+            for (int i = 0; i < HPT; i++)
+                if (tid + i * NW * 64 < HEAD_N) hlds[tid + i * NW * 64] = hv[i];
+        }
+    };
     // DMA of the W0^T slice of k tile kt (32 columns of every input row) into slice stage kt & 1 = WS (2-stage
     // tile: compile-time, like every LDS base of the loop). Wave w issues pieces w and NW + w and skips the
     // pieces past the 4N + 8 input rows (wave-uniform): at N = 20 the 11 pieces put at most 3 of a SIMD's two
@@ -1987,6 +2036,7 @@ __global__ __launch_bounds__(WGM* WGN * 64, OCC) void k_gemm3g(ASrc a0, ASrc a1,
             mfma16s(fa, I0{}, sah, sal);
             mfma16s(fb, I1{}, sah, sal);
         };
+        head_load();
         if constexpr (RENC) {  // the first slice lands and is published before tile 0's A is computed
             issue_w0(std::integral_constant<int, 0>{}, 0);
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1995,6 +2045,7 @@ __global__ __launch_bounds__(WGM* WGN * 64, OCC) void k_gemm3g(ASrc a0, ASrc a1,
         issue(I0{}, 0);
         if constexpr (STAGES == 3)
             if (nk > 1) issue(I1{}, 1);
+        head_store();
         auto pp_step = [&](auto ST, int kt) {
             constexpr int S = decltype(ST)::value;
             using SI = std::integral_constant<int, (S + STAGES - 1) % STAGES>;  // stage of tile kt + STAGES - 1
@@ -2043,12 +2094,14 @@ __global__ __launch_bounds__(WGM* WGN * 64, OCC) void k_gemm3g(ASrc a0, ASrc a1,
         }
         if (late) mfma_all();  // the last tile
     } else {
+    head_load();
     issue(I0{}, 0);
     if (nk > 1) issue(I1{}, 1);
     if constexpr (STAGES >= 3)
         if (nk > 2) issue(I2{}, 2);
     if constexpr (STAGES >= 4)
         if (nk > 3) issue(I3{}, 3);
+    head_store();
     // wait until this wave's DMA of the oldest tile landed, n younger tiles left in flight
     auto wait_landed = [&](int n) {
         if (n >= 3)
@@ -2138,7 +2191,8 @@ __global__ __launch_bounds__(WGM* WGN * 64, OCC) void k_gemm3g(ASrc a0, ASrc a1,
                                                              N, lane);
         } else if constexpr (EPI == EPI_HEAD)
             act_dispatch(ep.act, [&](auto A) {
-                head_epilogue16<2 * TM, 2 * TN, WGN, BM, decltype(A)::value>(acc4, ep, lds, m0, wr, wc, M, N, lane, tid, n0);
+                head_epilogue16<2 * TM, 2 * TN, WGN, BM, decltype(A)::value>(acc4, ep, lds, m0, wr, wc, M, N, lane, tid, n0,
+                                                                             hlds);
             });
         else if constexpr (EPI == EPI_DQN)
             act_dispatch(ep.act, [&](auto A) {

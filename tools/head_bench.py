@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
-"""DQN layer 2 + fused Q head (gm_gemm_x3_head, 81920 x 256 x 512 + 4 heads) per tile form: default,
-tile 10 (128 x 256, 1 block / CU), tile 15 (64 x 256, 2 blocks / CU); Q and hidden output compared
-with the default form. python tools/head_bench.py"""
+"""DQN layer 2 + fused Q head (gm_gemm_x3_head, 81920 x 256 x 512 + 4 heads) per tile form: default
+(128 x 128 blocks, 2 per CU, partial Q per column block onto a zeroed q), tile 10 (128 x 256, 1 block / CU);
+Q and hidden output compared with the default form; against the same GEMM with a plain bias + act store
+(gm_gemm_x3) and the q zeroing alone. python tools/head_bench.py"""
 import ctypes as C
 import importlib
 import json
@@ -47,7 +48,7 @@ def main():
                                            y.data_ptr() if with_y else None, n, FU.L.stream_ptr()))
         ref = None
         r = {}
-        for t in (-1, 10, 15):
+        for t in (-1, 10):
             lib.gm_gemm_set_tile(t)
             run()
             torch.cuda.synchronize()
@@ -58,7 +59,7 @@ def main():
                 r[f"t{t}_qdiff"] = float((o[0] - ref[0]).abs().max())
                 if with_y:
                     r[f"t{t}_ydiff"] = float((o[1] - ref[1]).abs().max())
-        ts = {t: [] for t in (-1, 10, 15)}
+        ts = {t: [] for t in (-1, 10)}
         for _ in range(3):
             for t in ts:
                 lib.gm_gemm_set_tile(t)
@@ -66,7 +67,12 @@ def main():
         lib.gm_gemm_set_tile(-1)
         r.update({f"t{t}_us": round(min(v), 1) for t, v in ts.items()})
         out["with_y" if with_y else "q_only"] = r
-        print(json.dumps(out), flush=True)
+    x3b = FU.X3(wp, ldw, n, k)
+    out["plain_gemm_us"] = round(min(timeit(lambda: FU.gemm(FU.dense(x.data_ptr(), k, k), None, wp.data_ptr(), ldw,
+                                                                 b.data_ptr(), m, n, 1, y.data_ptr(), n, x3=x3b))
+                                     for _ in range(3)), 1)
+    out["q_zero_us"] = round(min(timeit(lambda: q.zero_()) for _ in range(3)), 1)
+    print(json.dumps(out), flush=True)
 
 
 if __name__ == "__main__":
