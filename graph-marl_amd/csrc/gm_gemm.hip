@@ -222,6 +222,8 @@ __device__ __forceinline__ void range_guard(const floatx16 (&acc)[TM][TN], unsig
 // GM_LO_E: the low piece of the split is scaled by 2^12 (a normal f16 down to |a| ~ 2^-15); the w_hi
 // factor 2^-12 restores it
 constexpr float LO_S = (float)(1 << GM_LO_E);
+// routing-encoder (ROUTING_ENC) source: node-obs rows 4N + 8 up to N = 50 (BASELINE config 4's largest graphs)
+#define GM_RENC_ROWS 208
 // a = hi + 2^-12 lo with hi = f16(a) (RNE), lo = f16((a - hi) * 2^12)
 __device__ __forceinline__ void split4(float4 v, half4& hi, half4& lo) {
     const floatx4 a = {v.x, v.y, v.z, v.w};
@@ -1559,12 +1561,14 @@ __global__ __launch_bounds__(WGM* WGN * 64, OCC) void k_gemm3g(ASrc a0, ASrc a1,
     // ROUTING_ENC (RENC): the A tile is computed in the block from the routing node observations and the
     // folded encoder layer's W0^T, whose 32-column slice per k tile is DMA'd (RW pieces of 8 rows per wave)
     constexpr bool RENC = AMODE == GM_A_ROUTING_ENC;
-    constexpr int RW = RENC ? 2 : 0;                     // W0^T slice pieces per wave: 4N + 8 <= 8 NW RW rows
+    // W0^T slice: 4N + 8 <= GM_RENC_ROWS rows (N <= 50) in pieces of 8 rows, piece j NW + wave DMA'd by wave
+    constexpr int W0P = RENC ? (GM_RENC_ROWS + 7) / 8 : 0;  // pieces per slice stage
+    constexpr int RW = RENC ? (W0P + NW - 1) / NW : 0;       // pieces per wave (the last ones skipped past 4N + 8)
     constexpr int NA = BM / 8 / NW, NB = BN / 8 / NW;  // DMA instructions per wave per tile
     constexpr int NAD = RENC ? 0 : NA;                   // A pieces actually DMA'd
     constexpr int NL = NAD + NB + RW;
     constexpr int STAGE_B = (BM + BN) * 128;
-    constexpr int W0S_B = 8 * NW * RW * 128;             // one W0^T slice stage
+    constexpr int W0S_B = W0P * 1024;                     // one W0^T slice stage
     constexpr int RENC_B = RENC ? 2 * W0S_B + 4 * 1024 : 0;  // two slice stages + the bias (<= 1024 columns)
     static_assert(BM % (8 * NW) == 0 && BN % (8 * NW) == 0, "tile rows per wave");
     static_assert(AMODE != GM_A_AGGREGATE, "aggregate source uses k_gemm3");
@@ -2326,10 +2330,10 @@ int to_asrc_any(const gm_a_src* s, int M, ASrc& o) {
         return gm_fail(GM_ERR_INVALID_ARG, "gm_gemm: an A scale needs a DENSE source");
     if (s->mode == GM_A_ROUTING_ENC) {
         const long long K0 = 4ll * s->n_nodes + 8;
-        if (!s->p0 || !s->p1 || !s->nbr || s->deg != 3 || s->n_nodes < 4 || K0 > 128 || s->k <= 0 || (s->k % BKMAX) ||
+        if (!s->p0 || !s->p1 || !s->nbr || s->deg != 3 || s->n_nodes < 4 || K0 > GM_RENC_ROWS || s->k <= 0 || (s->k % BKMAX) ||
             s->k > 1024 || s->ld0 < K0 || s->ld1 < s->k || (s->ld1 & 3) || (reinterpret_cast<uintptr_t>(s->p1) & 15) ||
             (M % s->n_nodes) || s->act0 < GM_ACT_NONE || s->act0 > GM_ACT_LAST || s->amax)
-            return gm_fail(GM_ERR_UNSUPPORTED, "gm_gemm: routing-encoder source needs deg 3, 4N + 8 <= 128, k % 32 == 0, "
+            return gm_fail(GM_ERR_UNSUPPORTED, "gm_gemm: routing-encoder source needs deg 3, 4N + 8 <= 208, k % 32 == 0, "
                                                "k <= 1024, ld1 >= k (16-byte W0^T rows), M = G * N");
         o.bytes0 = ((long long)(M - 1) * s->ld0 + K0) * 4;
         o.bytes1 = ((K0 - 1) * s->ld1 + s->k) * 4;

@@ -116,14 +116,14 @@ def routing_enc_src(lin, x, nbr, N):
 
 
 # the rollout folds the NetMon encoder's first layer into the second layer's A-tile load when the split
-# form runs and 4N + 8 <= 128 (GM_A_ROUTING_ENC, always on 16x16x32 MFMA); GM_RENC_FOLD=0 keeps
+# form runs and 4N + 8 <= 208, N <= 50 (GM_A_ROUTING_ENC, always on 16x16x32 MFMA); GM_RENC_FOLD=0 keeps
 # gm_routing_node_encoder + a DENSE second layer (A-B timing)
 RENC_FOLD = os.environ.get("GM_RENC_FOLD", "1") != "0"
 
 
 def renc_fold_ok(layers, N, Fd, nbr):
     return (RENC_FOLD and L.GEMM_MODE == "x3" and len(layers) >= 2 and routing_encoder_ok(layers[0], N, Fd, nbr)
-            and 4 * N + 8 <= 128 and layers[0].out_features % 32 == 0 and layers[0].out_features <= 1024
+            and 4 * N + 8 <= 208 and layers[0].out_features % 32 == 0 and layers[0].out_features <= 1024
             and use_x3(layers[1].out_features) and layers[1].in_features == layers[0].out_features)
 
 

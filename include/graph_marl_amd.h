@@ -378,7 +378,7 @@ typedef struct {
  * (src/model.py:13-42, 489) on routing node observations x (src/env/routing.py:187-235: [onehot(n) | cnt |
  * load | 3 x (onehot(nbr_k) | len_k | load_k)], 4N + 8 columns) computed inside the GEMM's A-tile load from
  * the 12 nonzero columns, so the m x k layer output never reaches HBM: p0 = x rows ([G * n_nodes][ld0]),
- * p1 = W0^T ([4N + 8][ld1], ld1 >= k), nbr = [G][n_nodes][3] (deg = 3), n_nodes = N with 4N + 8 <= 128,
+ * p1 = W0^T ([4N + 8][ld1], ld1 >= k), nbr = [G][n_nodes][3] (deg = 3), n_nodes = N with 4N + 8 <= 208 (N <= 50),
  * k = the layer's width (multiple of 32), bias0 / act0. Runs on v_mfma_f32_16x16x32_f16 (whatever
  * gm_gemm_set_mfma selects for the other GEMMs) and needs a bias epilogue; other cases return
  * GM_ERR_UNSUPPORTED (run gm_routing_node_encoder and a DENSE source instead). */

@@ -111,7 +111,7 @@ def test_training_entry_points_reject_bad_arguments(gm):
 
 def test_routing_encoder_source_rejects_bad_arguments(gm):
     """gm_encoder_x3 and the ROUTING_ENC A source (round 5) validate before any device call: the source
-    mode, the layer widths (256 -> 128), degree 3, 4N + 8 <= 128 and whole 32-wide k tiles; gm_gemm_f32
+    mode, the layer widths (256 -> 128), degree 3, 4N + 8 <= 208 and whole 32-wide k tiles; gm_gemm_f32
     refuses the source outright."""
     import importlib
 
@@ -135,7 +135,7 @@ def test_routing_encoder_source_rejects_bad_arguments(gm):
     assert chain(src(), n2=512) == -1 and b"256, 128" in L.gm_last_error()
     assert chain(src(), n3=64) == -1
     assert chain(src(mode=FU.GM_A_DENSE)) == -1 and b"routing-encoder" in L.gm_last_error()
-    for bad in (dict(deg=4), dict(n_nodes=31), dict(k=500), dict(nbr=None)):
+    for bad in (dict(deg=4), dict(n_nodes=51), dict(k=500), dict(nbr=None)):
         assert chain(src(**bad)) != 0, bad
         assert b"routing-encoder" in L.gm_last_error(), bad
     assert chain(src(), m=81919) != 0  # rows not whole graphs

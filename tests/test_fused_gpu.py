@@ -580,7 +580,7 @@ def test_dqn_fused_kernel_matches_two_kernels(n_env, gemm_obs, act, monkeypatch)
     assert abs(q1.double().cpu().numpy() - q64).max() < 1e-5
 
 
-@pytest.mark.parametrize("N,B", [(20, 4096), (10, 333), (30, 700)])
+@pytest.mark.parametrize("N,B", [(20, 4096), (10, 333), (30, 700), (40, 512), (50, 1024)])
 def test_routing_encoder_fold_matches_two_kernels(N, B):
     """Round 5: the rollout computes NetMon encoder layer 1 inside layer 2's A-tile load (GM_A_ROUTING_ENC,
     the m x 512 layer-1 output never written) — layer 2's output equals gm_routing_node_encoder + the
@@ -611,9 +611,9 @@ def test_routing_encoder_fold_matches_two_kernels(N, B):
 
 
 def test_routing_encoder_fold_refuses_unsupported_cases():
-    """gm_gemm_x3 only (not gm_gemm_f32) and 4N + 8 <= 128."""
+    """gm_gemm_x3 only (not gm_gemm_f32) and 4N + 8 <= 208 (N <= 50)."""
     gm, M, FU, W = mods()
-    N, B = 40, 8
+    N, B = 52, 8
     env = gm.Routing(gm.Network(N, random_topology=True, excluded_seeds=gm.EVAL_SEEDS), 20, n_env=B, seed=1,
                      agent_adjacency=False)
     env.reset_()
@@ -627,7 +627,7 @@ def test_routing_encoder_fold_refuses_unsupported_cases():
                 y.data_ptr(), 256, x3=FU.pack_x3(l1))
 
 
-@pytest.mark.parametrize("N,B", [(20, 4096), (10, 333), (30, 700)])
+@pytest.mark.parametrize("N,B", [(20, 4096), (10, 333), (30, 700), (40, 512), (50, 1024)])
 def test_encoder_chain_matches_layer_by_layer(N, B):
     """gm_encoder_x3 (round 5: NetMon encoder layers 1-3 of the rollout in one launch, layer 2's output kept
     on chip as split-f16 images) == the fold (layers 1 + 2) + the dense layer-3 GEMM, and fp64 within the
