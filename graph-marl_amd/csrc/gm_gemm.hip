@@ -170,10 +170,6 @@ __device__ __forceinline__ float sigm(float x) {
 }
 __device__ __forceinline__ float tanh_fast(float x) { return 2.0f * sigm(2.0f * x) - 1.0f; }
 
-// Layer activation in the epilogues with the common cases resolved at compile time: A = 0 none,
-// 1 leaky_relu, -1 any GM_ACT_* at run time (a per-element branch tree: relu / elu / tanh / sigmoid
-// only). act_dispatch calls f with A chosen from the wave-uniform act, so the default epilogues carry
-// no activation branches per element.
 // (up ? b : a, up ? a : b) as a bitwise blend of the two values: written as selects of two elements of a
 // local array, LLVM turns them into one dynamically indexed access, and the array is then lowered to
 // 16-way v_cmp / v_cndmask chains per element (the Q-head reduction cost ~29 us per 81 920-row launch)
@@ -182,6 +178,11 @@ __device__ __forceinline__ void swap_if(bool up, float a, float b, float& mine, 
     mine = __builtin_bit_cast(float, (ua & ~m) | (ub & m));
     other = __builtin_bit_cast(float, (ub & ~m) | (ua & m));
 }
+
+// Layer activation in the epilogues with the common cases resolved at compile time: A = 0 none,
+// 1 leaky_relu, -1 any GM_ACT_* at run time (a per-element branch tree: relu / elu / tanh / sigmoid
+// only). act_dispatch calls f with A chosen from the wave-uniform act, so the default epilogues carry
+// no activation branches per element.
 template <int A>
 __device__ __forceinline__ float act_t(float v, int act) {
     if constexpr (A == 0)
@@ -1717,9 +1718,9 @@ __global__ __launch_bounds__(WGM* WGN * 64, OCC) void k_gemm3g(ASrc a0, ASrc a1,
         }
     };
     // DMA of the W0^T slice of k tile kt (32 columns of every input row) into slice stage kt & 1 = WS (2-stage
-    // tile: compile-time, like every LDS base of the loop). Wave w issues pieces w and NW + w and skips the
-    // pieces past the 4N + 8 input rows (wave-uniform): at N = 20 the 11 pieces put at most 3 of a SIMD's two
-    // waves' DMA issues in a step instead of 4 (the 2-stage loop waits vmcnt(0), so the count may vary)
+    // tile: compile-time, like every LDS base of the loop). Wave w issues pieces j NW + w (j < RW) and skips
+    // the pieces past the 4N + 8 input rows (wave-uniform): at N = 20 the 11 pieces put at most 3 of a SIMD's
+    // two waves' DMA issues in a step (the 2-stage loop waits vmcnt(0), so the count may vary per wave)
     const int w0rows = RENC ? 4 * a0.n_nodes + 8 : 0;
     auto issue_w0 = [&](auto WS, int kt) {
         char* base = lds + STAGES * STAGE_B + decltype(WS)::value * W0S_B;
