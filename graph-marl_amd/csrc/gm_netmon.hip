@@ -139,6 +139,51 @@ __global__ __launch_bounds__(256) void k_mp_aggregate(const float* __restrict__ 
     stv<V>(out + row * ldo + (size_t)cv * V, acc);
 }
 
+// forward of k_mp_aggregate for degree-3 graphs with fewer than 2^31 (row, vector) items: 32-bit index
+// math (the 64-bit divisions of the general kernel were most of its instructions) and the members
+// {n} u nbr(n) put in ascending id order by a 4-input sorting network (missing neighbours last) instead of
+// members()'s dynamically indexed local array; the same members, the same summation order
+template <int V>
+__global__ __launch_bounds__(256) void k_mp_aggregate3(const float* __restrict__ h, const int32_t* __restrict__ nbr,
+                                                       unsigned N, unsigned HV, int mode, float* __restrict__ out,
+                                                       long long ldh, long long ldo, unsigned total) {
+    const unsigned gid = xcd_block(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x;
+    if (gid >= total) return;
+    const unsigned row = gid / HV, cv = gid - row * HV;
+    const unsigned g = row / N;
+    const int32_t* nb = nbr + (size_t)row * 3;
+    constexpr int MISSING = 0x7fffffff;
+    int m[4] = {(int)(row - g * N), nb[0] < 0 ? MISSING : nb[0], nb[1] < 0 ? MISSING : nb[1],
+                nb[2] < 0 ? MISSING : nb[2]};
+    const int cnt = 1 + (m[1] != MISSING) + (m[2] != MISSING) + (m[3] != MISSING);
+    auto cswap = [](int& a, int& b) {
+        const int lo = min(a, b), hi = max(a, b);
+        a = lo;
+        b = hi;
+    };
+    cswap(m[0], m[1]);
+    cswap(m[2], m[3]);
+    cswap(m[0], m[2]);
+    cswap(m[1], m[3]);
+    cswap(m[1], m[2]);
+    const float* src = h + (size_t)g * N * ldh + (size_t)cv * V;
+    Vec<V> x[4];
+#pragma unroll
+    for (int q = 0; q < 4; q++) x[q] = q < cnt ? ldv<V>(src + (size_t)m[q] * ldh) : zerov<V>();
+    Vec<V> acc = x[0];
+#pragma unroll
+    for (int q = 1; q < 4; q++)
+        if (q < cnt) {
+#pragma unroll
+            for (int i = 0; i < V; i++) acc.v[i] = acc.v[i] + x[q].v[i];
+        }
+    if (mode == 1) {
+#pragma unroll
+        for (int i = 0; i < V; i++) acc.v[i] = acc.v[i] / cnt;
+    }
+    stv<V>(out + (size_t)row * ldo + (size_t)cv * V, acc);
+}
+
 // readout: out row r of graph g = [h_final[v], h_prev[nbr(v,0..deg-1)]], v = agent_node or r.
 // Output rows may sit inside a wider joint observation (stride); V-wide stores.
 template <int V>
@@ -436,6 +481,10 @@ static int launch_agg(const float* h, const int32_t* nbr, int32_t G, int32_t N, 
     const int V = vec_width(H, ldh, h) < vec_width(H, ldo, out) ? vec_width(H, ldh, h) : vec_width(H, ldo, out);
     long long total = (long long)G * N * (H / V);
     dim3 grid(nblocks(total, 256));
+    if (!BWD && deg == 3 && total < (1ll << 31)) {
+        GM_VLAUNCH(k_mp_aggregate3, V, grid, h, nbr, (unsigned)N, (unsigned)(H / V), mode, out, ldh, ldo, (unsigned)total);
+        return launched();
+    }
     if (V == 4) hipLaunchKernelGGL((k_mp_aggregate<BWD, 4>), grid, dim3(256), 0, (hipStream_t)stream, h, nbr, G, N, deg, H, mode, out, ldh, ldo);
     else if (V == 2) hipLaunchKernelGGL((k_mp_aggregate<BWD, 2>), grid, dim3(256), 0, (hipStream_t)stream, h, nbr, G, N, deg, H, mode, out, ldh, ldo);
     else hipLaunchKernelGGL((k_mp_aggregate<BWD, 1>), grid, dim3(256), 0, (hipStream_t)stream, h, nbr, G, N, deg, H, mode, out, ldh, ldo);
