@@ -281,3 +281,40 @@ def test_netmon_no_carryover_vs_reference_golden():
                             torch.as_tensor(g["node_agent"][t], device="cuda"))
             np.testing.assert_allclose(mapped.cpu().numpy(), g[f"v{vi}_mapped_{t}"], atol=1e-5, rtol=0)
             np.testing.assert_allclose(nm.state.cpu().numpy(), g[f"v{vi}_state_{t}"], atol=1e-5, rtol=0)
+
+
+@pytest.mark.parametrize("mode", [0, 1])
+def test_mp_aggregate_degree3_missing_neighbours(mode):
+    """The degree-3 aggregate kernel (round 5: members in ascending id order by a sorting network) with
+    neighbour tables as dense_to_nbr writes them for graphs of degree <= 3 (ascending ids, -1 padding):
+    bit for bit the fp32 sum over {n} u nbr(n) in ascending id order (the reference bmm's (I + A) order),
+    divided by the member count for mean."""
+    M = model_mod()
+    G, N, H = 16, 20, 128
+    g = torch.Generator().manual_seed(mode)
+    adj = torch.zeros(G, N, N, dtype=torch.int8)
+    for b in range(G):
+        for n in range(N):
+            k = int(torch.randint(0, 4, (1,), generator=g))
+            for v in torch.randperm(N, generator=g)[:k].tolist():
+                if v != n:
+                    adj[b, n, v] = 1
+    nbr = torch.full((G, N, 3), -1, dtype=torch.int32)
+    for b in range(G):
+        for n in range(N):
+            ids = torch.nonzero(adj[b, n]).flatten()[:3]
+            nbr[b, n, :len(ids)] = ids.int()
+    nbr = nbr.cuda()
+    h = torch.randn(G * N, H, device="cuda")
+    out = M.mp_aggregate(h, nbr, mode)
+    hv = h.view(G, N, H)
+    ref = torch.empty_like(hv)
+    for b in range(G):
+        for n in range(N):
+            mem = sorted([n] + [v for v in nbr[b, n].tolist() if v >= 0])
+            acc = hv[b, mem[0]].clone()
+            for v in mem[1:]:
+                acc = acc + hv[b, v]
+            # tensor divisor: torch divides by a Python scalar as a multiply by its reciprocal on the GPU
+            ref[b, n] = acc / torch.full_like(acc, float(len(mem))) if mode == 1 else acc
+    assert torch.equal(out.view(G, N, H), ref)
