@@ -2070,10 +2070,11 @@ __global__ __launch_bounds__(WGM* WGN * 64, OCC) void k_gemm3g(ASrc a0, ASrc a1,
             }
             __builtin_amdgcn_sched_barrier(0);
             GM_STAMP(kt, 1);
-            if (kt + STAGES - 1 < nk) issue(SI{}, kt + STAGES - 1);  // into the stage of tile kt - 1
+            if (RENC && kt + STAGES - 1 < nk) issue(SI{}, kt + STAGES - 1);  // into the stage of tile kt - 1
             GM_STAMP(kt, 2);
             read(ST, I0{}, fa);
             read(ST, I1{}, fb);
+            if (!RENC && kt + STAGES - 1 < nk) issue(SI{}, kt + STAGES - 1);  // behind the reads (guide: cheaper)
 #pragma unroll
             for (int i = 0; i < 2 * TM; i++) {
                 if constexpr (RENC) {  // stored split (renc_a): hi / lo chunks as read
