@@ -1020,7 +1020,7 @@ __device__ __forceinline__ void range_guard16(const floatx4 (&acc)[T2][N2], unsi
 }
 template <int T2, int N2, int EPI, int A = -1>
 __device__ __forceinline__ void epilogue16(floatx4 (&acc)[T2][N2], const Epi& ep, int wm0, int wn0, int M, int N,
-                                           int lane, const CIn16<T2, EPI>& cin) {
+                                           int lane, const CIn16<T2, EPI>& cin, const float* bl = nullptr) {
     const int l16 = lane & 15, rq = 4 * (lane >> 4);
     if constexpr (EPI == EPI_BIAS) {
         static_assert(N2 % 2 == 0, "column blocks in pairs (32-column sign words)");
@@ -1060,7 +1060,9 @@ __device__ __forceinline__ void epilogue16(floatx4 (&acc)[T2][N2], const Epi& ep
             const int unit = (wn0 >> 2) + 16 * b + l16;
             float bgate[4];
 #pragma unroll
-            for (int g = 0; g < 4; g++) bgate[g] = ep.bias ? ep.bias[wn0 + g * 32 + 16 * b + l16] : 0.f;
+            for (int g = 0; g < 4; g++)  // bl: the block's gate biases staged in LDS (k_gemm3g, EPI_LSTM)
+                bgate[g] = bl ? bl[g * 32 + 16 * b + l16]  // (bl at this wave's first column)
+                              : ep.bias ? ep.bias[wn0 + g * 32 + 16 * b + l16] : 0.f;
 #pragma unroll
             for (int i = 0; i < T2; i++)
 #pragma unroll
@@ -1580,7 +1582,7 @@ __global__ __launch_bounds__(WGM* WGN * 64, OCC) void k_gemm3g(ASrc a0, ASrc a1,
                   "chain epilogue: the next layer's split A images alias the operand stages");
     // EPI_HEAD: the block's bias and Q-head weight columns, staged once (head_load / head_store) so that the
     // epilogue does not start with 40 dependent global loads per lane
-    constexpr int HEAD_N = EPI == EPI_HEAD ? 5 * BN : 0;
+    constexpr int HEAD_N = EPI == EPI_HEAD ? 5 * BN : EPI == EPI_LSTM ? BN : 0;  // (LSTM: the gate biases)
     constexpr int HEAD_B = HEAD_N * 4;
 #if GM_DIAG == 30
     __shared__ __attribute__((aligned(16))) char lds[STAGES * STAGE_B + RENC_B + HEAD_B + 1024];
@@ -1696,6 +1698,13 @@ __global__ __launch_bounds__(WGM* WGN * 64, OCC) void k_gemm3g(ASrc a0, ASrc a1,
     float hv[HPT];
     float* const hlds = reinterpret_cast<float*>(lds + STAGES * STAGE_B + RENC_B);
     auto head_load = [&]() {
+        if constexpr (EPI == EPI_LSTM) {
+#pragma unroll
+            for (int i = 0; i < HPT; i++) {
+                const int e = tid + i * NW * 64, col = n0 + e;
+                hv[i] = (e < HEAD_N && col < N && ep.bias) ? ep.bias[col] : 0.f;
+            }
+        }
         if constexpr (EPI == EPI_HEAD) {
 #pragma unroll
             for (int i = 0; i < HPT; i++) {
@@ -1711,7 +1720,7 @@ __global__ __launch_bounds__(WGM* WGN * 64, OCC) void k_gemm3g(ASrc a0, ASrc a1,
         }
     };
     auto head_store = [&]() {
-        if constexpr (EPI == EPI_HEAD) {
+        if constexpr (EPI == EPI_HEAD || EPI == EPI_LSTM) {
 #pragma unroll
             for (int i = 0; i < HPT; i++)
                 if (tid + i * NW * 64 < HEAD_N) hlds[tid + i * NW * 64] = hv[i];
@@ -2215,7 +2224,8 @@ __global__ __launch_bounds__(WGM* WGN * 64, OCC) void k_gemm3g(ASrc a0, ASrc a1,
                                                                         N, lane, cin);
                 });
             else
-                epilogue16<2 * TM, 2 * TN, EPI>(acc4, ep, m0 + wr * TM * 32, n0 + wc * TN * 32, M, N, lane, cin);
+                epilogue16<2 * TM, 2 * TN, EPI>(acc4, ep, m0 + wr * TM * 32, n0 + wc * TN * 32, M, N, lane, cin,
+                                                EPI == EPI_LSTM ? hlds + wc * TN * 32 : nullptr);
     } else {
 #pragma unroll
         for (int i = 0; i < TM; i++)
