@@ -1030,7 +1030,7 @@ __device__ __forceinline__ void epilogue16(floatx4 (&acc)[T2][N2], const Epi& ep
 #pragma unroll
             for (int b = 0; b < 2; b++) {
                 const int col = wn0 + (2 * jp + b) * 16 + l16;
-                bv[b] = (ep.bias && col < N) ? ep.bias[col] : 0.f;
+                bv[b] = bl ? bl[(2 * jp + b) * 16 + l16] : (ep.bias && col < N) ? ep.bias[col] : 0.f;
             }
 #pragma unroll
             for (int i = 0; i < T2; i++)
@@ -1397,7 +1397,7 @@ __device__ __forceinline__ void dqn_tail(floatx4 (&acc)[T2][N2], const Epi& ep, 
 // never reaches HBM.
 template <int WGM, int WGN, int T2, int N2, int BM, int N3, int W3N, int A = -1>
 __device__ __forceinline__ void chain_tail(floatx4 (&acc)[T2][N2], const Epi& ep, char* lds, int m0, int wr, int wc,
-                                           int M, int lane) {
+                                           int M, int lane, const float* bl) {
     static_assert(WGM * T2 * 16 == BM, "the wave rows hold the block's rows");
     constexpr int NW = WGM * WGN, W3M = NW / W3N;
     constexpr int T3 = BM / 16 / W3M, J3 = N3 / 16 / W3N;
@@ -1412,7 +1412,7 @@ __device__ __forceinline__ void chain_tail(floatx4 (&acc)[T2][N2], const Epi& ep
 #pragma unroll
     for (int j = 0; j < N2; j++) {
         const int n = wc * N2 * 16 + j * 16 + l16;  // this layer's column = the next layer's k
-        const float bj = ep.bias ? ep.bias[n] : 0.f;
+        const float bj = bl[n];  // staged before the k loop (k_gemm3g head_load / head_store)
         const int sw = dqn_swz(n) << 3;
 #pragma unroll
         for (int i = 0; i < T2; i++) {
@@ -1582,7 +1582,7 @@ __global__ __launch_bounds__(WGM* WGN * 64, OCC) void k_gemm3g(ASrc a0, ASrc a1,
                   "chain epilogue: the next layer's split A images alias the operand stages");
     // EPI_HEAD: the block's bias and Q-head weight columns, staged once (head_load / head_store) so that the
     // epilogue does not start with 40 dependent global loads per lane
-    constexpr int HEAD_N = EPI == EPI_HEAD ? 5 * BN : EPI == EPI_LSTM ? BN : 0;  // (LSTM: the gate biases)
+    constexpr int HEAD_N = EPI == EPI_HEAD ? 5 * BN : (EPI == EPI_LSTM || EPI == EPI_BIAS || EPI == EPI_CHAIN) ? BN : 0;
     constexpr int HEAD_B = HEAD_N * 4;
 #if GM_DIAG == 30
     __shared__ __attribute__((aligned(16))) char lds[STAGES * STAGE_B + RENC_B + HEAD_B + 1024];
@@ -1698,7 +1698,7 @@ __global__ __launch_bounds__(WGM* WGN * 64, OCC) void k_gemm3g(ASrc a0, ASrc a1,
     float hv[HPT];
     float* const hlds = reinterpret_cast<float*>(lds + STAGES * STAGE_B + RENC_B);
     auto head_load = [&]() {
-        if constexpr (EPI == EPI_LSTM) {
+        if constexpr (EPI == EPI_LSTM || EPI == EPI_BIAS || EPI == EPI_CHAIN) {  // the block's biases
 #pragma unroll
             for (int i = 0; i < HPT; i++) {
                 const int e = tid + i * NW * 64, col = n0 + e;
@@ -1720,7 +1720,7 @@ __global__ __launch_bounds__(WGM* WGN * 64, OCC) void k_gemm3g(ASrc a0, ASrc a1,
         }
     };
     auto head_store = [&]() {
-        if constexpr (EPI == EPI_HEAD || EPI == EPI_LSTM) {
+        if constexpr (HEAD_N > 0) {
 #pragma unroll
             for (int i = 0; i < HPT; i++)
                 if (tid + i * NW * 64 < HEAD_N) hlds[tid + i * NW * 64] = hv[i];
@@ -2215,13 +2215,13 @@ __global__ __launch_bounds__(WGM* WGN * 64, OCC) void k_gemm3g(ASrc a0, ASrc a1,
             });
         else if constexpr (EPI == EPI_CHAIN)
             act_dispatch(ep.act, [&](auto A) {
-                chain_tail<WGM, WGN, 2 * TM, 2 * TN, BM, 128, 4, decltype(A)::value>(acc4, ep, lds, m0, wr, wc, M, lane);
+                chain_tail<WGM, WGN, 2 * TM, 2 * TN, BM, 128, 4, decltype(A)::value>(acc4, ep, lds, m0, wr, wc, M, lane, hlds);
             });
         else
             if constexpr (EPI == EPI_BIAS)
                 act_dispatch(ep.act, [&](auto A) {
                     epilogue16<2 * TM, 2 * TN, EPI, decltype(A)::value>(acc4, ep, m0 + wr * TM * 32, n0 + wc * TN * 32, M,
-                                                                        N, lane, cin);
+                                                                        N, lane, cin, hlds + wc * TN * 32);
                 });
             else
                 epilogue16<2 * TM, 2 * TN, EPI>(acc4, ep, m0 + wr * TM * 32, n0 + wc * TN * 32, M, N, lane, cin,
