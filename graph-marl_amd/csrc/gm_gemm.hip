@@ -1397,7 +1397,7 @@ __device__ __forceinline__ void dqn_tail(floatx4 (&acc)[T2][N2], const Epi& ep, 
 // never reaches HBM.
 template <int WGM, int WGN, int T2, int N2, int BM, int N3, int W3N, int A = -1>
 __device__ __forceinline__ void chain_tail(floatx4 (&acc)[T2][N2], const Epi& ep, char* lds, int m0, int wr, int wc,
-                                           int M, int lane, const float* bl) {
+                                           int M, int lane, const float* bl, float si3) {
     static_assert(WGM * T2 * 16 == BM, "the wave rows hold the block's rows");
     constexpr int NW = WGM * WGN, W3M = NW / W3N;
     constexpr int T3 = BM / 16 / W3M, J3 = N3 / 16 / W3N;
@@ -1506,7 +1506,7 @@ __device__ __forceinline__ void chain_tail(floatx4 (&acc)[T2][N2], const Epi& ep
             }
         }
     }
-    const float si = *ep.wsi2;
+    const float si = si3;  // *ep.wsi2, loaded at kernel start
 #pragma unroll
     for (int i = 0; i < T3; i++)
 #pragma unroll
@@ -1520,7 +1520,8 @@ __device__ __forceinline__ void chain_tail(floatx4 (&acc)[T2][N2], const Epi& ep
     e3.sbits = nullptr;
     CIn16<T3, EPI_BIAS> none;
     act_dispatch(e3.act, [&](auto A3) {
-        epilogue16<T3, J3, EPI_BIAS, decltype(A3)::value>(acc3, e3, m0 + row0, w3c * J3 * 16, M, N3, lane, none);
+        epilogue16<T3, J3, EPI_BIAS, decltype(A3)::value>(acc3, e3, m0 + row0, w3c * J3 * 16, M, N3, lane, none,
+                                                          bl + WGN * N2 * 16 + w3c * J3 * 16);
     });
 }
 
@@ -1582,7 +1583,10 @@ __global__ __launch_bounds__(WGM* WGN * 64, OCC) void k_gemm3g(ASrc a0, ASrc a1,
                   "chain epilogue: the next layer's split A images alias the operand stages");
     // EPI_HEAD: the block's bias and Q-head weight columns, staged once (head_load / head_store) so that the
     // epilogue does not start with 40 dependent global loads per lane
-    constexpr int HEAD_N = EPI == EPI_HEAD ? 5 * BN : (EPI == EPI_LSTM || EPI == EPI_BIAS || EPI == EPI_CHAIN) ? BN : 0;
+    constexpr int HEAD_N = EPI == EPI_HEAD    ? 5 * BN
+                           : EPI == EPI_CHAIN ? BN + 128  // + the layer-3 biases
+                           : (EPI == EPI_LSTM || EPI == EPI_BIAS) ? BN
+                                                                   : 0;
     constexpr int HEAD_B = HEAD_N * 4;
 #if GM_DIAG == 30
     __shared__ __attribute__((aligned(16))) char lds[STAGES * STAGE_B + RENC_B + HEAD_B + 1024];
@@ -1698,11 +1702,22 @@ __global__ __launch_bounds__(WGM* WGN * 64, OCC) void k_gemm3g(ASrc a0, ASrc a1,
     float hv[HPT];
     float* const hlds = reinterpret_cast<float*>(lds + STAGES * STAGE_B + RENC_B);
     auto head_load = [&]() {
-        if constexpr (EPI == EPI_LSTM || EPI == EPI_BIAS || EPI == EPI_CHAIN) {  // the block's biases
+        if constexpr (EPI == EPI_LSTM || EPI == EPI_BIAS) {  // the block's biases
 #pragma unroll
             for (int i = 0; i < HPT; i++) {
                 const int e = tid + i * NW * 64, col = n0 + e;
                 hv[i] = (e < HEAD_N && col < N && ep.bias) ? ep.bias[col] : 0.f;
+            }
+        }
+        if constexpr (EPI == EPI_CHAIN) {  // layer-2 biases (one column block: n0 = 0), then layer 3's
+#pragma unroll
+            for (int i = 0; i < HPT; i++) {
+                const int e = tid + i * NW * 64;
+                hv[i] = 0.f;
+                if (e < BN) {
+                    if (e < N && ep.bias) hv[i] = ep.bias[e];
+                } else if (e < HEAD_N && ep.b2)
+                    hv[i] = ep.b2[e - BN];
             }
         }
         if constexpr (EPI == EPI_HEAD) {
@@ -1909,6 +1924,9 @@ __global__ __launch_bounds__(WGM* WGN * 64, OCC) void k_gemm3g(ASrc a0, ASrc a1,
     const _Float16 s12 = (_Float16)(1.0f / LO_S);
     const float ascale = AX == 2 ? *a0.scale : 1.0f;
     const int aexp = __builtin_amdgcn_frexp_expf(ascale) - 1;  // ascale = 2^aexp
+    // epilogue scales read here, not after the k loop, so their latency hides under it
+    const float wsi0 = *wscale_inv;
+    const float wsi3 = EPI == EPI_CHAIN ? *ep.wsi2 : 1.0f;
     float amx = 0.f;  // AX 1: max |A| over the fragments this lane reads (all A elements of the tile
                       // are read by some lane of every column wave; ragged columns zeroed first)
     // fragments of one 16-deep half (SB) of a k tile: A raw fp32 (split at use), B hi / lo
@@ -2185,7 +2203,7 @@ __global__ __launch_bounds__(WGM* WGN * 64, OCC) void k_gemm3g(ASrc a0, ASrc a1,
         amx = gm_wave_max(amx);
         if (lane == 0) gm_amax_publish(a0.amax, amx);
     }
-    const float si = *wscale_inv / ascale;  // undo the weight and A scales (powers of two: exact)
+    const float si = wsi0 / ascale;  // undo the weight and A scales (powers of two: exact)
     if constexpr (MF == 1) {
 #pragma unroll
         for (int i = 0; i < 2 * TM; i++)
@@ -2215,7 +2233,8 @@ __global__ __launch_bounds__(WGM* WGN * 64, OCC) void k_gemm3g(ASrc a0, ASrc a1,
             });
         else if constexpr (EPI == EPI_CHAIN)
             act_dispatch(ep.act, [&](auto A) {
-                chain_tail<WGM, WGN, 2 * TM, 2 * TN, BM, 128, 4, decltype(A)::value>(acc4, ep, lds, m0, wr, wc, M, lane, hlds);
+                chain_tail<WGM, WGN, 2 * TM, 2 * TN, BM, 128, 4, decltype(A)::value>(acc4, ep, lds, m0, wr, wc, M, lane, hlds,
+                                                                                       wsi3);
             });
         else
             if constexpr (EPI == EPI_BIAS)
