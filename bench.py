@@ -82,16 +82,18 @@ def parse():
     p.add_argument("--no-pmc", action="store_true",
                    help="skip the same-run rocprofv3 PMC passes (HBM bytes of DQN layer 1 and k_env_step)")
     p.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
+    p.add_argument("--pmc-order", default=None, help=argparse.SUPPRESS)
     p.add_argument("--cpu-envs", type=int, default=1024)
     p.add_argument("--cpu-steps", type=int, default=50, help="one full episode (includes its reset)")
     return p.parse_args()
 
 
 def pmc_traffic(tag, build_src=None):
-    """HBM bytes per launch of a kernel (FETCH_SIZE x2 + WRITE_SIZE) from the latest committed
-    rocprofv3 PMC passes (profiles/*/pmc_traffic.json), with a provenance note: whether the profile's
-    recorded source hash equals this library's build.src. (None, None) when not profiled. Used only
-    when the same-run passes (measure_pmc) are unavailable."""
+    """HBM bytes per launch of a kernel (FETCH_SIZE x2 + WRITE_SIZE) from a committed rocprofv3 PMC
+    profile (profiles/*/*/pmc_traffic.json), with a provenance note. A profile whose recorded source
+    hash equals this library's build.src wins; otherwise the newest one (round directory, then the
+    profile's "seq", then its file time), never the largest byte count. (None, None) when no profile
+    has the kernel. Used only when the same-run passes (measure_pmc) are unavailable."""
     import glob
 
     found = []
@@ -100,93 +102,110 @@ def pmc_traffic(tag, build_src=None):
             with open(path) as f:
                 d = json.load(f)
             k = d["kernels"].get(tag)
+            mtime = os.path.getmtime(path)
         except (OSError, ValueError, KeyError):
             continue
-        if k:  # newest = highest round directory, then the profile's own "seq" within the round
+        if k:
             rnd = os.path.basename(os.path.dirname(os.path.dirname(path)))
-            found.append(((rnd, d.get("seq", 0)), k["fetch_bytes"] + k["write_bytes"], os.path.relpath(path, ROOT),
-                          d.get("src")))
+            psrc = d.get("src")
+            rank = (build_src is not None and psrc == build_src, rnd, d.get("seq", 0), mtime)
+            found.append((rank, k["fetch_bytes"] + k["write_bytes"], os.path.relpath(path, ROOT), psrc))
     if not found:
         return None, None
-    _, tb, src, psrc = max(found)
+    _, tb, src, psrc = max(found, key=lambda f: f[0])
     same = ("source hash not recorded" if psrc is None else
             "same sources as this build" if psrc == build_src else f"OTHER sources ({psrc}) than this build")
     return tb, f"committed profile {src}, {same}"
 
 
-PMC_X, PMC_Y = 6, 6  # DQN forwards, then env steps, in the counted window of the --pmc-child process
+PMC_S = 6  # rollout vector steps in the counted window of the --pmc-child process
 
 
 def pmc_child(args):
     """The dispatch window the PMC passes count (bench.py under rocprofv3, started by measure_pmc): the
-    headline's rollout as one group, a few warm steps, then PMC_X DQN forwards (layer 1 = the dominant
-    kernel, then layer 2 + Q head) and PMC_Y fused ε-greedy + env steps, nothing else in between."""
+    headline's rollout as ONE group (the same kernels and launch sizes as the per-kernel timer pass),
+    positioned so that the window holds no episode reset; one step records the library's launch order
+    (_lib.TRACE, written to --pmc-order), then PMC_S more steps run with nothing in between."""
     torch.cuda.set_device(0)
     gm = importlib.import_module("graph-marl_amd")
     M = importlib.import_module("graph-marl_amd.model")
     RO = importlib.import_module("graph-marl_amd.rollout")
-    FU = importlib.import_module("graph-marl_amd.fused")
+    L = gm._lib
     N, A, B = args.n_router, args.n_data, args.n_env
+    assert args.episode_steps > PMC_S + 6, "the PMC window must fit inside one episode"
     net = gm.Network(N, random_topology=bool(args.random_topology), excluded_seeds=gm.EVAL_SEEDS, device=0)
     torch.manual_seed(0)
     netmon = M.NetMon(4 * N + 8, 128, [512, 256], args.netmon_iterations).cuda()
     dqn = M.DQN(6 * N + 10 + netmon.get_out_features(), [512, 256], 4).cuda()
+    M.tag_modules(netmon, "netmon.")
+    M.tag_modules(dqn, "dqn.")
     ro = RO.StreamedRollout(net, A, B, netmon, dqn, groups=1, seed=0, epsilon=args.epsilon,
                             episode_steps=args.episode_steps, device=0)
     with torch.no_grad():
         ro.reset()
         ro.run(3)
-        env, wenv, pol = ro.envs[0], ro.wenvs[0], ro.policies[0]
         torch.cuda.synchronize()
-        for _ in range(PMC_X):
-            q = FU.dqn_q(dqn, env.obs_buf, env.obs_dim, wenv.current_netmon_state, wenv.h_prev, env.nbr,
-                         env.agent_node, pol._buf, hidden=netmon.hidden_features, obs_gemm=env.obs_gemm)
+        L.TRACE = []
+        ro.step()
+        order, L.TRACE = L.TRACE, None
+        for _ in range(PMC_S - 1):
+            ro.step()
         torch.cuda.synchronize()
-        qv = q.view(B, A, -1).contiguous()
-        for _ in range(PMC_Y):
-            env.policy_step_(qv, args.epsilon, pol.actions)
-        torch.cuda.synchronize()
+    assert ro.ep == 3 + PMC_S, "an episode reset fell inside the PMC window"
+    with open(args.pmc_order, "w") as f:
+        json.dump(order, f)
 
 
-def _pmc_window(path, counter):
-    """Per-launch counter values of (DQN layer 1, k_env_step) from the child's CSV: the last
-    2 PMC_X + PMC_Y dispatches of this library's kernels must be PMC_X (layer 1, layer 2 + head) pairs
-    (layer 1 = the larger grid) then PMC_Y env steps; None if the window does not look like that."""
+def _pmc_window(path, counter, order):
+    """Per-launch counter values of every rollout kernel from the child's CSV: the last PMC_S x len(order)
+    dispatches of this library's kernels must be PMC_S repetitions of one step's launches (same kernel
+    names, the env step and the aggregate where `order` has them). Returns ({tag: median value per launch},
+    median over the steps of the per-step sum), or None if the window does not look like that."""
     import csv
 
     with open(path) as f:
         rows = [r for r in csv.DictReader(f) if r.get("Counter_Name") == counter]
     rows.sort(key=lambda r: int(r["Dispatch_Id"]))
     ours = [r for r in rows if r["Kernel_Name"].lstrip("_ ").startswith(("k_", "ZN12_GLOBAL__N_1"))]
-    win = ours[-(2 * PMC_X + PMC_Y):]
-    if len(win) != 2 * PMC_X + PMC_Y or not all("k_env_step" in r["Kernel_Name"] for r in win[2 * PMC_X:]):
+    P = len(order)
+    win = ours[-(PMC_S * P):] if P else []
+    if P == 0 or len(win) != PMC_S * P:
         return None
-    grid = lambda r: int(r.get("Grid_Size") or r.get("Grid_Size_X"))  # noqa: E731
-    l1 = [a for a, b in zip(win[0:2 * PMC_X:2], win[1:2 * PMC_X:2]) if grid(a) > grid(b)]
-    if len(l1) != PMC_X:
+    names = [r["Kernel_Name"] for r in win]
+    if any(names[i] != names[i % P] for i in range(len(win))):
         return None
+    for i, tag in enumerate(order):
+        for kind, kname in (("env_step", "k_env_step"), ("mp_aggregate", "k_mp_aggregate")):
+            if tag.split(":")[0] == kind and kname not in names[i]:
+                return None
     med = lambda v: sorted(v)[len(v) // 2]  # noqa: E731
-    return (med([float(r["Counter_Value"]) for r in l1]),
-            med([float(r["Counter_Value"]) for r in win[2 * PMC_X:]]))
+    vals = {}
+    for i, tag in enumerate(order):
+        vals.setdefault(tag, []).extend(float(win[s * P + i]["Counter_Value"]) for s in range(PMC_S))
+    per_step = [sum(float(win[s * P + i]["Counter_Value"]) for i in range(P)) for s in range(PMC_S)]
+    return {tag: med(v) for tag, v in vals.items()}, med(per_step)
 
 
 def measure_pmc(args):
-    """Same-run HBM traffic (MI355X_MICROARCH.md §HBM): two rocprofv3 passes over a child bench.py
-    (--pmc-child), FETCH_SIZE and WRITE_SIZE in separate runs (they do not fit one pass), each under
-    a hard time limit; KiB per launch, FETCH_SIZE doubled (gfx950 counts half of a 16-B/lane stream).
-    Returns {"dqn_l1": bytes, "env_step": bytes, ...} or None (no rocprofv3, or a pass failed)."""
+    """Same-run HBM traffic (MI355X_MICROARCH.md §HBM) of EVERY rollout kernel: two rocprofv3 passes over a
+    child bench.py (--pmc-child), FETCH_SIZE and WRITE_SIZE in separate runs (they do not fit one pass),
+    each under a hard time limit; KiB per launch, FETCH_SIZE doubled (gfx950 counts half of a 16-B/lane
+    stream). Returns {"kernels": {tag: bytes per launch}, "step_bytes": bytes per vector step (one group of
+    --n-env envs), ...} or None (no rocprofv3); {"error": ...} if a pass failed."""
     import shutil
     import tempfile
 
     prof = shutil.which("rocprofv3")
     if prof is None:
         return None
-    out = {}
+    out, steps = {}, {}
     with tempfile.TemporaryDirectory(dir=os.path.join(ROOT, "gpurun_out") if os.path.isdir(
             os.path.join(ROOT, "gpurun_out")) else None) as d:
+        order_path = os.path.join(d, "order.json")
         for counter in ("FETCH_SIZE", "WRITE_SIZE"):
             cmd = ["timeout", "-s", "KILL", "150", prof, "--pmc", counter, "-T", "--output-format", "csv", "-d", d,
                    "-o", counter.lower(), "--", sys.executable, os.path.abspath(__file__), "--pmc-child",
+                   "--pmc-order", order_path,
                    "--n-env", str(args.n_env), "--n-router", str(args.n_router), "--n-data", str(args.n_data),
                    "--netmon-iterations", str(args.netmon_iterations), "--random-topology", str(args.random_topology),
                    "--episode-steps", str(args.episode_steps), "--epsilon", str(args.epsilon)]
@@ -196,16 +215,26 @@ def measure_pmc(args):
                 return {"error": f"{counter} pass timed out"}
             if r.returncode != 0:
                 return {"error": f"{counter} pass rc {r.returncode}: {r.stderr.decode(errors='replace')[-200:]}"}
+            try:
+                with open(order_path) as f:
+                    order = json.load(f)
+            except (OSError, ValueError):
+                return {"error": f"{counter}: the child wrote no launch order"}
             csvs = [os.path.join(dp, f) for dp, _, fs in os.walk(d) for f in fs
                     if f.startswith(counter.lower()) and f.endswith("counter_collection.csv")]
-            got = _pmc_window(csvs[0], counter) if csvs else None
+            got = _pmc_window(csvs[0], counter, order) if csvs else None
             if got is None:
                 return {"error": f"{counter}: dispatch window not found in {csvs}"}
             f = 2.0 if counter == "FETCH_SIZE" else 1.0
-            out[counter] = [f * v * 1024 for v in got]
-    return {"dqn_l1": out["FETCH_SIZE"][0] + out["WRITE_SIZE"][0], "env_step": out["FETCH_SIZE"][1] +
-            out["WRITE_SIZE"][1], "fetch_bytes": out["FETCH_SIZE"], "write_bytes": out["WRITE_SIZE"],
-            "note": "rocprofv3 PMC in this bench run (child process, median of 6 launches; FETCH_SIZE x2, KiB x1024)"}
+            out[counter] = {tag: f * v * 1024 for tag, v in got[0].items()}
+            steps[counter] = f * got[1] * 1024
+    kernels = {tag: round(out["FETCH_SIZE"][tag] + out["WRITE_SIZE"].get(tag, 0.0)) for tag in out["FETCH_SIZE"]}
+    return {"kernels": kernels, "step_bytes": round(steps["FETCH_SIZE"] + steps["WRITE_SIZE"]),
+            "fetch_bytes": {t: round(v) for t, v in out["FETCH_SIZE"].items()},
+            "write_bytes": {t: round(v) for t, v in out["WRITE_SIZE"].items()},
+            "window": f"{PMC_S} rollout vector steps of one group of {args.n_env} envs, no reset inside",
+            "note": f"rocprofv3 PMC in this bench run (child process, median of {PMC_S} steps; FETCH_SIZE x2, "
+                    "KiB x1024)"}
 
 
 def cpu_model():
@@ -227,9 +256,6 @@ def kernel_cost(tag, n_env, N, A, E, x3=False):
         m, n, k = (int(v) for v in tag.split(":")[2].split("x"))
         macs = m * n * k + (m * 128 * n if "+chain" in tag else 0)  # gm_encoder_x3: + layer 3 (n -> 128)
         return ("mfma16" if x3 and n > 32 else "mfma"), (3.0 if x3 and n > 32 else 1.0) * 2.0 * macs
-    if kind == "dqn_fused":  # gm_dqn_x3: layer 1 (K) + layer 2 (512 -> 256) + Q head, 3 f16 products each
-        m, n, k = (int(v) for v in tag.split(":")[2].split("x"))
-        return "mfma16", 3.0 * 2.0 * m * (n * k + 256 * n + 4 * 256)
     if kind == "routing_enc":
         rows, n = (int(v) for v in tag.split(":")[2].split("x"))
         return "hbm", rows * n * 4 + rows * 11 * 4  # write y, read the 11 nonzero features per row
@@ -459,9 +485,18 @@ def measure_config4(args, gm, M, W, P, RO, timed_region, dev, world, rank):
             rec["update_sequences"] = tr["update"]["sequences"]
             del nm, dq, net
         except Exception as ex:  # a config-4 size must never break the headline line
-            if os.environ.get("GM_BENCH_RAISE") == "1" or world > 1:
-                raise  # with peers waiting in collectives a rank must not carry on alone
+            if os.environ.get("GM_BENCH_RAISE") == "1":
+                raise
             rec = {"value": None, "error": repr(ex)[:300]}
+        if world > 1:
+            # every rank reaches this exchange whether its size passed or failed (a failure at a size is
+            # normally the same on every rank: memory, an unsupported shape), so the ranks skip a failed
+            # size together and go on to the next one and to the headline line
+            flag = torch.tensor([0.0 if "error" not in rec else 1.0], dtype=torch.float64,
+                                device="cpu" if os.environ.get("GM_BENCH_SHARE_GPU") == "1" else dev)
+            dist.all_reduce(flag, op=dist.ReduceOp.MAX)
+            if float(flag.item()) > 0 and "error" not in rec:
+                rec = {"value": None, "error": "skipped: another rank failed at this size"}
         out["per_n_nodes"][str(n)] = rec
         torch.cuda.empty_cache()
     out["rollout_steps"] = args.episode_steps
@@ -687,14 +722,17 @@ def main():
             pmc = measure_pmc(args)
         except Exception as ex:  # the traffic probe must never break the GPU line
             pmc = {"error": repr(ex)[:200]}
-    if roof and pmc and "dqn_l1" in pmc and roof.get("kernel", "").startswith("linear:dqn.encoder.linear_layers.0:"):
-        roof["traffic"] = round(pmc["dqn_l1"])
+    pk = (pmc or {}).get("kernels") or {}
+    if roof and roof.get("kernel") in pk:
+        roof["traffic"] = pk[roof["kernel"]]
         roof["traffic_note"] = "HBM bytes per launch, " + pmc["note"]
-    if pmc and "env_step" in pmc:
-        for tag, kv in roof_hbm.items():
-            if tag.startswith("env_step"):
-                kv["traffic"] = round(pmc["env_step"])
-                kv["traffic_note"] = "HBM bytes per launch, " + pmc["note"]
+    for tag, kv in roof_hbm.items():
+        if tag in pk:
+            kv["traffic"] = pk[tag]
+            kv["traffic_note"] = "HBM bytes per launch, " + pmc["note"]
+    for tag, kv in kernels.items():
+        if tag in pk:
+            kv["traffic"] = pk[tag]
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

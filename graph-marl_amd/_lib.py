@@ -33,7 +33,7 @@ EXPORTS = [
     "gm_gemm_pack_x3", "gm_gemm_pack_x3_bytes", "gm_gemm_range_status",
     "gm_pcg64_seed", "gm_pcg64_choice", "gm_lnlstm_pointwise", "gm_agent_attention", "gm_agent_comm",
     "gm_gemm_x3_dgrad", "gm_lstm_cell_bwd", "gm_qhead_bwd", "gm_netmon_readout_ld", "gm_routing_node_encoder_bits", "gm_gather_records",
-    "gm_lnlstm_fwd", "gm_lnlstm_bwd", "gm_gru_pointwise", "gm_gru_bwd", "gm_act_bwd", "gm_dqn_x3", "gm_build_info",
+    "gm_lnlstm_fwd", "gm_lnlstm_bwd", "gm_gru_pointwise", "gm_gru_bwd", "gm_act_bwd", "gm_build_info",
     "gm_act_fwd", "gm_act_bwd_z", "gm_obs_from_gemm", "gm_encoder_x3",
 ]
 # kernel-form switches (include/graph_marl_amd_tuning.h)
@@ -45,21 +45,6 @@ TUNING_EXPORTS = ["gm_gemm_set_tile", "gm_gemm_set_wgrad", "gm_gemm_set_mfma", "
 GEMM_MODE = os.environ.get("GM_GEMM", "x3")
 if GEMM_MODE not in ("x3", "f32"):
     raise ValueError(f"GM_GEMM must be 'x3' or 'f32', not {GEMM_MODE!r}")
-# MFMA shape of the LDS-DMA split-f16 kernel (gm_gemm_set_mfma): GM_MFMA=16all (16x16x32
-# everywhere: the library default), 16 (16x16x32 except the fused Q head) or 32 (32x32x16); unset
-# leaves the library default
-MFMA_SHAPE = os.environ.get("GM_MFMA")
-if MFMA_SHAPE not in (None, "16", "32", "16all"):
-    raise ValueError(f"GM_MFMA must be '16', '32' or '16all', not {MFMA_SHAPE!r}")
-# input-gradient kernel form of gm_gemm_x3_dgrad (gm_gemm_set_dgrad: -1 per-shape default, 0 / 1 / 2)
-DGRAD_FORM = os.environ.get("GM_DGRAD")
-if DGRAD_FORM not in (None, "-1", "0", "1", "2"):
-    raise ValueError(f"GM_DGRAD must be -1, 0, 1 or 2, not {DGRAD_FORM!r}")
-# weight-gradient kernel form of gm_gemm_x3_wgrad (gm_gemm_set_wgrad: -1 default, 0..3, +8 dispatch order)
-WGRAD_FORM = os.environ.get("GM_WGRAD")
-if WGRAD_FORM is not None and WGRAD_FORM not in [str(v) for v in (-1, 0, 1, 2, 3, 8, 9, 10, 11)]:
-    raise ValueError(f"GM_WGRAD must be -1, 0..3 or 8..11, not {WGRAD_FORM!r}")
-
 
 class EnvConfig(C.Structure):
     _fields_ = [
@@ -189,13 +174,6 @@ def lib():
         L.gm_build_info.restype = C.c_char_p
     if hasattr(L, "gm_gemm_form"):
         L.gm_gemm_form.restype = C.c_char_p
-    if MFMA_SHAPE is not None:
-        if L.gm_gemm_set_mfma({"16": 1, "32": 0, "16all": 2}[MFMA_SHAPE]) != 0:
-            raise GMError(L.gm_last_error().decode())
-    if DGRAD_FORM is not None and L.gm_gemm_set_dgrad(int(DGRAD_FORM)) != 0:
-        raise GMError(L.gm_last_error().decode())
-    if WGRAD_FORM is not None and L.gm_gemm_set_wgrad(int(WGRAD_FORM)) != 0:
-        raise GMError(L.gm_last_error().decode())
     _lib = L
     return L
 
@@ -315,6 +293,8 @@ def require_gpu():
 # records a pair of HIP events on the launch stream under its tag.
 # ---------------------------------------------------------------------------
 PROF = None
+# launch-order recorder (bench.py's PMC child): when TRACE is a list, every wrapped launch appends its tag
+TRACE = None
 
 
 class timed:
@@ -325,6 +305,8 @@ class timed:
         self.s = None
 
     def __enter__(self):
+        if TRACE is not None and self.tag:
+            TRACE.append(self.tag)
         if PROF is not None and self.tag:
             self.s = torch.cuda.Event(enable_timing=True)
             self.s.record()

@@ -75,7 +75,7 @@ typedef float floatx4 __attribute__((ext_vector_type(4)));
 
 constexpr int BKMAX = 32;            // largest K tile of any configuration (host-side checks)
 constexpr int OOB = 0x7ff00000;       // byte offset beyond any buffer: load returns 0
-enum { EPI_BIAS = 0, EPI_LSTM = 1, EPI_HEAD = 2, EPI_DGRAD = 3, EPI_DQN = 4, EPI_CHAIN = 5 };
+enum { EPI_BIAS = 0, EPI_LSTM = 1, EPI_HEAD = 2, EPI_DGRAD = 3, EPI_CHAIN = 5 };
 
 struct ASrc {
     int mode;                 // GM_A_DENSE / GM_A_AGGREGATE / GM_A_READOUT
@@ -126,8 +126,8 @@ struct Epi {
     // the leaky_relu derivative of the layer's output for the training backward, 1/32 of its bytes
     unsigned* sbits;
     long long ldsb;
-    // EPI_DQN (the DQN's second layer + Q head after the first layer, in the same block): packed
-    // split-f16 layer-2 weights (gm_gemm_pack_x3 layout, n2 rows of ldw2 bytes), their 1/S, bias, act
+    // EPI_CHAIN (the next MLP layer after this one, in the same block): packed split-f16 weights of that
+    // layer (gm_gemm_pack_x3 layout, rows of ldw2 bytes), their 1/S, bias, act
     const _Float16* w2;
     long long ldw2;
     unsigned w2bytes;
@@ -1241,154 +1241,18 @@ __device__ __forceinline__ void head_epilogue16(floatx4 (&acc)[T2][N2], const Ep
     }
 }
 
-// ---- EPI_DQN: the DQN's layers 2 + Q head in the block that computed layer 1 (src/model.py:187-203) ----
-// A 64-row block holds its rows' whole layer-1 output (8 waves x 64 columns, 16x16x32 accumulators).
-// It goes through bias + activation, is split into f16 hi / lo pieces exactly like a dense A tile of
-// the unfused layer-2 kernel (split4: the same bits), and is stored K-major in two LDS images
-// ([layer-1 column = layer-2 k][64 rows] f16, 128-B rows). Layer 2 then reads its A fragments (8
-// consecutive k of one row) with ds_read_b64_tr_b16 and its weight fragments straight from
-// global/L2 into registers, two k tiles ahead; the Q head is head_epilogue16. The 81920 x 512 layer-1
-// activation never reaches HBM (168 MB written + read per rollout step unfused).
-// Image swizzle: the 8-byte slot of row k is XOR'd with dqn_swz(k) = k & 15 with bits 1 and 2
-// swapped, so the epilogue's 16 consecutive-k writes and the transposed reads (rows 8g + q, 4 lanes
-// per row) both hit distinct banks.
+// K-major split-f16 LDS image swizzle (EPI_CHAIN): the 8-byte slot of row k is XOR'd with dqn_swz(k) =
+// k & 15 with bits 1 and 2 swapped, so the epilogue's 16 consecutive-k writes and the transposed reads
+// (rows 8g + q, 4 lanes per row) both hit distinct banks.
 __device__ __forceinline__ int dqn_swz(int k) {
     return (k & 9) | ((k & 2) << 1) | ((k & 4) >> 1);
-}
-
-template <int T2, int N2, int WGN, int BM, int A = -1>
-__device__ __forceinline__ void dqn_tail(floatx4 (&acc)[T2][N2], const Epi& ep, char* lds, int m0, int wc, int M,
-                                         int lane, int tid) {
-    static_assert(T2 * 16 == BM, "one wave row holds the block's rows");
-    constexpr int K2 = WGN * N2 * 16;  // layer-2 K = layer-1 width
-    constexpr int RS = BM * 2;         // image row bytes
-    constexpr int NK = K2 / 32;        // layer-2 k tiles
-    constexpr int J2 = 2;              // layer-2 16-column blocks per wave (WGN * 32 columns)
-    char* ih = lds;
-    char* il = lds + K2 * RS;
-    const int l16 = lane & 15, rq = 4 * (lane >> 4);
-    __syncthreads();  // every wave is past its last reads of the layer-1 operand stages
-#pragma unroll
-    for (int j = 0; j < N2; j++) {
-        const int n = wc * N2 * 16 + j * 16 + l16;  // layer-1 column = layer-2 k
-        const float bj = ep.bias ? ep.bias[n] : 0.f;
-        const int sw = dqn_swz(n) << 3;
-#pragma unroll
-        for (int i = 0; i < T2; i++) {
-            const int m = i * 16 + rq;
-            float4 v;
-            v.x = act_t<A>(acc[i][j][0] + bj, ep.act);
-            v.y = act_t<A>(acc[i][j][1] + bj, ep.act);
-            v.z = act_t<A>(acc[i][j][2] + bj, ep.act);
-            v.w = act_t<A>(acc[i][j][3] + bj, ep.act);
-            half4 hi, lo;
-            split4(v, hi, lo);
-            const int off = n * RS + ((2 * m) ^ sw);
-            *reinterpret_cast<half4*>(ih + off) = hi;
-            *reinterpret_cast<half4*>(il + off) = lo;
-        }
-    }
-    // layer-2 weight fragments of this wave's 32 columns: lane reads row n2 = 32 wc + 16 jb + l16,
-    // k 8 q .. 8 q + 7 of each 32-deep tile: 16-k block 2 kt + (q >> 1), halves (q & 1) x 8 (hi at +0,
-    // lo at +32 of the block's 64 bytes)
-    const int q = lane >> 4;
-    const __amdgpu_buffer_rsrc_t rw = rsrc(reinterpret_cast<const float*>(ep.w2), ep.w2bytes);
-    int wo[J2];
-#pragma unroll
-    for (int jb = 0; jb < J2; jb++) wo[jb] = (int)((wc * 32 + jb * 16 + l16) * ep.ldw2) + (q >> 1) * 64 + (q & 1) * 16;
-    constexpr int NB2 = 3;  // weight tiles in flight
-    u32x4 pbh[NB2][J2], pbl[NB2][J2];
-    auto bfetch = [&](int slot, int kt) {
-#pragma unroll
-        for (int jb = 0; jb < J2; jb++) {
-            pbh[slot][jb] = __builtin_amdgcn_raw_buffer_load_b128(rw, wo[jb] + kt * 128, 0, 0);
-            pbl[slot][jb] = __builtin_amdgcn_raw_buffer_load_b128(rw, wo[jb] + kt * 128 + 32, 0, 0);
-        }
-    };
-#pragma unroll
-    for (int t = 0; t < NB2; t++) bfetch(t, t);
-    __syncthreads();  // the images are complete
-    floatx4 acc2[T2][J2];
-#pragma unroll
-    for (int i = 0; i < T2; i++)
-#pragma unroll
-        for (int j = 0; j < J2; j++)
-#pragma unroll
-            for (int r = 0; r < 4; r++) acc2[i][j][r] = 0.f;
-    // transposed A reads: 16-lane group g reads k rows 8 g + qq (+ 4), columns 4 p of its 16-row block
-    const int g = lane >> 4, qq = (lane >> 2) & 3, p = lane & 3;
-    typedef __fp16 v4fp16 __attribute__((__vector_size__(8)));
-    auto frag = [&](const char* img, int k0, int col0) {
-        const int r0 = k0 + 8 * g + qq, r1 = r0 + 4;
-        const char* a0 = img + r0 * RS + ((2 * (col0 + 4 * p)) ^ (dqn_swz(r0) << 3));
-        const char* a1 = img + r1 * RS + ((2 * (col0 + 4 * p)) ^ (dqn_swz(r1) << 3));
-        const half4 x0 = __builtin_bit_cast(
-            half4, __builtin_amdgcn_ds_read_tr16_b64_v4f16((__attribute__((address_space(3))) v4fp16*)(a0)));
-        const half4 x1 = __builtin_bit_cast(
-            half4, __builtin_amdgcn_ds_read_tr16_b64_v4f16((__attribute__((address_space(3))) v4fp16*)(a1)));
-        return half8{x0[0], x0[1], x0[2], x0[3], x1[0], x1[1], x1[2], x1[3]};
-    };
-    const _Float16 s12 = (_Float16)(1.0f / LO_S);
-    // A fragments double-buffered in registers: tile kt + 1's reads are issued before tile kt's MFMAs
-    half8 fah[2][T2], fal[2][T2];
-#pragma unroll
-    for (int i = 0; i < T2; i++) {
-        fah[0][i] = frag(ih, 0, 16 * i);
-        fal[0][i] = frag(il, 0, 16 * i);
-    }
-    {
-#pragma unroll
-    for (int kt = 0; kt < NK; kt++) {
-        const int cur = kt & 1, slot = kt % NB2;
-        if (kt + 1 < NK) {
-#pragma unroll
-            for (int i = 0; i < T2; i++) {
-                fah[cur ^ 1][i] = frag(ih, (kt + 1) * 32, 16 * i);
-                fal[cur ^ 1][i] = frag(il, (kt + 1) * 32, 16 * i);
-            }
-        }
-        half8 bh[J2], bl[J2];
-#pragma unroll
-        for (int jb = 0; jb < J2; jb++) {
-            bh[jb] = __builtin_bit_cast(half8, pbh[slot][jb]);
-            bl[jb] = __builtin_bit_cast(half8, pbl[slot][jb]);
-        }
-        if (kt + NB2 < NK) bfetch(slot, kt + NB2);
-#pragma unroll
-        for (int jb = 0; jb < J2; jb++) {
-            const half8 bs = bh[jb] * s12;
-#pragma unroll
-            for (int i = 0; i < T2; i++) {
-                floatx4& c = acc2[i][jb];
-                c = __builtin_amdgcn_mfma_f32_16x16x32_f16(fal[cur][i], bs, c, 0, 0, 0);
-                c = __builtin_amdgcn_mfma_f32_16x16x32_f16(fah[cur][i], bl[jb], c, 0, 0, 0);
-                c = __builtin_amdgcn_mfma_f32_16x16x32_f16(fah[cur][i], bh[jb], c, 0, 0, 0);
-            }
-        }
-    }
-    }
-    const float si = *ep.wsi2;
-#pragma unroll
-    for (int i = 0; i < T2; i++)
-#pragma unroll
-        for (int j = 0; j < J2; j++)
-#pragma unroll
-            for (int r = 0; r < 4; r++) acc2[i][j][r] *= si;
-    range_guard16<T2, J2>(acc2, ep.range_flag, lane);
-    Epi e2 = ep;
-    e2.bias = ep.b2;
-    e2.act = ep.act2;
-    e2.y = nullptr;
-    act_dispatch(e2.act, [&](auto A2) {
-        head_epilogue16<T2, J2, WGN, BM, decltype(A2)::value>(acc2, e2, lds, m0, 0, wc, M, WGN * 32, lane, tid);
-    });
 }
 
 // ---- EPI_CHAIN: the next MLP layer in the block that computed this one (the rollout's NetMon encoder
 // layers 2 -> 3, src/model.py:13-42) ----
 // The block (BM rows x the layer's whole width K2 = WGN * N2 * 16) sends its activations through bias +
 // activation and the split (split4: the bits a dense A tile of the next layer would get) into two
-// K-major LDS images ([k][BM rows] f16, dqn_swz slots: EPI_DQN's layout with BM * 2-byte rows), which
+// K-major LDS images ([k][BM rows] f16, dqn_swz slots, BM * 2-byte rows), which
 // alias the finished operand stages. The next layer (N3 columns) has its own wave grid: NW / W3N waves over
 // the rows (T3 16-row blocks each) x W3N over the columns (J3 16-column blocks each), so each weight
 // fragment is fetched by NW / W3N waves (2, not WGM = 4: half the tail's L2 traffic). Each wave reads its A
@@ -1459,7 +1323,7 @@ __device__ __forceinline__ void chain_tail(floatx4 (&acc)[T2][N2], const Epi& ep
             for (int r = 0; r < 4; r++) acc3[i][j][r] = 0.f;
     const int g = lane >> 4, qq = (lane >> 2) & 3, p = lane & 3;
     typedef __fp16 v4fp16 __attribute__((__vector_size__(8)));
-    auto frag = [&](const char* img, int k0, int col0) {  // as dqn_tail: 8 consecutive k of one row
+    auto frag = [&](const char* img, int k0, int col0) {  // 8 consecutive k of one row
         const int r0 = k0 + 8 * g + qq, r1 = r0 + 4;
         const char* a0 = img + r0 * RS + ((2 * (col0 + 4 * p)) ^ (dqn_swz(r0) << 3));
         const char* a1 = img + r1 * RS + ((2 * (col0 + 4 * p)) ^ (dqn_swz(r1) << 3));
@@ -2147,6 +2011,9 @@ __global__ __launch_bounds__(WGM* WGN * 64, OCC) void k_gemm3g(ASrc a0, ASrc a1,
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     };
     wait_landed(min(STAGES - 1, nk - 1));  // tiles issued after tile 0
+    // head_store's LDS writes are read by other waves in the epilogue: publish them here too (with
+    // nk == 1 no later barrier of the k loop would)
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
     if (ragged && nk == 1) zero_tail(I0{});
@@ -2227,10 +2094,6 @@ __global__ __launch_bounds__(WGM* WGN * 64, OCC) void k_gemm3g(ASrc a0, ASrc a1,
                 head_epilogue16<2 * TM, 2 * TN, WGN, BM, decltype(A)::value>(acc4, ep, lds, m0, wr, wc, M, N, lane, tid, n0,
                                                                              hlds);
             });
-        else if constexpr (EPI == EPI_DQN)
-            act_dispatch(ep.act, [&](auto A) {
-                dqn_tail<2 * TM, 2 * TN, WGN, BM, decltype(A)::value>(acc4, ep, lds, m0, wc, M, lane, tid);
-            });
         else if constexpr (EPI == EPI_CHAIN)
             act_dispatch(ep.act, [&](auto A) {
                 chain_tail<WGM, WGN, 2 * TM, 2 * TN, BM, 128, 4, decltype(A)::value>(acc4, ep, lds, m0, wr, wc, M, lane, hlds,
@@ -2270,7 +2133,7 @@ __global__ __launch_bounds__(WGM* WGN * 64, OCC) void k_gemm3g(ASrc a0, ASrc a1,
             act_dispatch(ep.act, [&](auto A) {
                 epilogue<TM, TN, EPI, decltype(A)::value>(acc, ep, m0 + wr * TM * 32, n0 + wc * TN * 32, M, N, lane, cin);
             });
-        else if constexpr (EPI != EPI_DQN && EPI != EPI_CHAIN)  // EPI_DQN / EPI_CHAIN: the 16x16x32 form only
+        else if constexpr (EPI != EPI_CHAIN)  // EPI_CHAIN: the 16x16x32 form only
             epilogue<TM, TN, EPI>(acc, ep, m0 + wr * TM * 32, n0 + wc * TN * 32, M, N, lane, cin);
     }
 }
@@ -2804,52 +2667,6 @@ extern "C" int gm_encoder_x3(const gm_a_src* a0, const void* w2p, const float* w
     return launch_g<4, 2, 1, 4, 2, GM_A_ROUTING_ENC, EPI_CHAIN, 1>(s0, s1, static_cast<const float*>(w2p), ldw2,
                                                                   (unsigned)wb2, m, n2, K, ep, (hipStream_t)stream,
                                                                   w2sinv, 1);
-}
-
-extern "C" int gm_dqn_x3(const gm_a_src* a0, const gm_a_src* a1, const void* w1p, const float* w1sinv, const float* b1,
-                         int32_t act1, const void* w2p, const float* w2sinv, const float* b2, int32_t act2, int32_t m,
-                         int32_t n1, int32_t n2, const float* wq, int64_t ldwq, const float* bq, int32_t nq, float* q,
-                         int64_t ldq, void* stream) {
-    if (!a0 || !w1p || !w1sinv || !b1 || !w2p || !w2sinv || !b2 || !wq || !q || m <= 0 || n1 != 512 || n2 != 256 ||
-        nq <= 0 || nq > 4 || ldwq < n2 || ldq < nq || act1 < GM_ACT_NONE || act1 > GM_ACT_LAST ||
-        act2 < GM_ACT_NONE || act2 > GM_ACT_LAST || (reinterpret_cast<uintptr_t>(w1p) & 15) ||
-        (reinterpret_cast<uintptr_t>(w2p) & 15))
-        return gm_fail(GM_ERR_INVALID_ARG, "gm_dqn_x3: bad arguments (layers 512, 256 wide, nq <= 4)");
-    ASrc s0, s1;
-    int rc = to_asrc(a0, m, s0);
-    if (rc) return rc;
-    rc = to_asrc(a1, m, s1);
-    if (rc) return rc;
-    if (s0.mode == GM_A_AGGREGATE || s0.scale || s0.amax || (a1 && (a1->mode != GM_A_DENSE || (s0.k % BKMAX))))
-        return gm_fail(GM_ERR_INVALID_ARG, "gm_dqn_x3: dense or readout source (+ a dense second source, k % 32 == 0)");
-    const int K = s0.k + (a1 ? s1.k : 0);
-    const long long ldw1 = (long long)((K + BKMAX - 1) / BKMAX * BKMAX) / 16 * 64, wb1 = (long long)n1 * ldw1;
-    const long long ldw2 = (long long)n1 / 16 * 64, wb2 = (long long)n2 * ldw2;  // layer-2 K = n1
-    if (!fits(wb1)) return gm_fail(GM_ERR_UNSUPPORTED, "gm_dqn_x3: weights larger than 2 GB");
-    Epi ep;
-    memset(&ep, 0, sizeof(ep));
-    ep.bias = b1;
-    ep.act = act1;
-    ep.w2 = static_cast<const _Float16*>(w2p);
-    ep.ldw2 = ldw2;
-    ep.w2bytes = (unsigned)wb2;
-    ep.wsi2 = w2sinv;
-    ep.b2 = b2;
-    ep.act2 = act2;
-    ep.wq = wq;
-    ep.ldwq = ldwq;
-    ep.bq = bq;
-    ep.nq = nq;
-    ep.q = q;
-    ep.ldq = ldq;
-    if ((rc = range_flag(&ep.range_flag))) return rc;
-    const float* w1 = static_cast<const float*>(w1p);
-    hipStream_t st = (hipStream_t)stream;
-    // 64-row blocks, 8 waves of 64 layer-1 columns; 2 LDS stages of (64 + 512) x 128 B = 144 KB
-    if (s0.mode == GM_A_READOUT)
-        return launch_g<1, 8, 2, 2, 2, GM_A_READOUT, EPI_DQN, 1>(s0, s1, w1, ldw1, (unsigned)wb1, m, n1, K, ep, st,
-                                                                w1sinv, 1);
-    return launch_g<1, 8, 2, 2, 2, GM_A_DENSE, EPI_DQN, 1>(s0, s1, w1, ldw1, (unsigned)wb1, m, n1, K, ep, st, w1sinv, 1);
 }
 
 extern "C" int gm_gemm_x3_head(const gm_a_src* a0, const void* wp, const float* wscale_inv, const float* b,

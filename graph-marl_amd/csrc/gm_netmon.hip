@@ -826,12 +826,6 @@ __global__ __launch_bounds__(1024) void k_readout_bwd_g(const float* __restrict_
     if (dhp) stv<V>(dhp + node * H + off, ap);
 }
 
-// GM_READOUT_BWD=graph keeps one block per graph (A-B timing)
-const bool g_readout_bwd_cs = [] {
-    const char* e = getenv("GM_READOUT_BWD");
-    return !(e && strcmp(e, "graph") == 0);
-}();
-
 extern "C" int gm_netmon_readout_bwd(const float* dout, int64_t stride, const int32_t* nbr, const int32_t* agent_node,
                                      int32_t G, int32_t N, int32_t R, int32_t deg, int32_t H, float* dhf, float* dhp,
                                      void* stream) {
@@ -843,8 +837,7 @@ extern "C" int gm_netmon_readout_bwd(const float* dout, int64_t stride, const in
     const size_t lds = (size_t)R * (deg + 1) * H * 4;
     // column chunks per graph: 4, or 8 when a quarter of the graph's rows exceeds 48 KB of LDS
     const int S = (lds / 4 <= 48 * 1024 || (H / 4) % 8) ? 4 : 8;
-    if (V == 4 && R <= 128 && N <= 128 && deg <= 3 && (H / 4) % S == 0 && lds / S <= 48 * 1024 &&
-        g_readout_bwd_cs) {
+    if (V == 4 && R <= 128 && N <= 128 && deg <= 3 && (H / 4) % S == 0 && lds / S <= 48 * 1024) {
         const int threads = std::min(256, (N * (H / (4 * S)) + 63) / 64 * 64);
         if (R <= 64)
             hipLaunchKernelGGL(k_readout_bwd_cs<1>, dim3((unsigned)((long long)G * S)), dim3(threads), lds / S,
@@ -1281,12 +1274,6 @@ __global__ __launch_bounds__(256) void k_qhead_bwd4(const float* __restrict__ dq
 
 }  // namespace
 
-// GM_LSTM_BWD=scalar selects the one-unit-per-thread kernel (A-B timing)
-const bool g_lstm_bwd_vec = [] {
-    const char* e = getenv("GM_LSTM_BWD");
-    return !(e && strcmp(e, "scalar") == 0);
-}();
-
 extern "C" int gm_lstm_cell_bwd(const gm_lstm_bwd_args* a, void* stream) {
     if (!a || !a->act || !a->c_in || !a->c_out || !a->dgates || a->m <= 0 || a->hidden <= 0 || a->hidden > 1024 ||
         (a->hidden > 256 && a->hidden % 64) || (a->dm && (!a->nbr || a->n_nodes <= 0 || a->deg < 0 || a->deg > MAXDEG)) ||
@@ -1302,7 +1289,7 @@ extern "C" int gm_lstm_cell_bwd(const gm_lstm_bwd_args* a, void* stream) {
         return gm_fail(GM_ERR_HIP, "gm_lstm_cell_bwd: memset");
     const long long nb = (b.m + b.rows_per_block - 1) / b.rows_per_block;
     auto a16 = [](const void* p, long long ld) { return !p || ((reinterpret_cast<uintptr_t>(p) & 15) == 0 && ld % 4 == 0); };
-    const bool vec = g_lstm_bwd_vec && H % 4 == 0 && H / 4 <= 256 && ((256 / (H / 4)) * (H / 4)) % 64 == 0 &&
+    const bool vec = H % 4 == 0 && H / 4 <= 256 && ((256 / (H / 4)) * (H / 4)) % 64 == 0 &&
                      a16(b.act, b.ld_act) && a16(b.c_in, b.ld_cin) && a16(b.c_out, b.ld_cout) &&
                      a16(b.dh0, b.ld_dh0) && a16(b.dh1, b.ld_dh1) && a16(b.dm, b.ld_dm) && a16(b.dh_ext, b.ld_ext) &&
                      a16(b.dc_ext, b.ld_dcext) && a16(b.dc, b.ld_dc) && a16(b.dgates, b.ld_dg) &&
@@ -1320,12 +1307,6 @@ extern "C" int gm_lstm_cell_bwd(const gm_lstm_bwd_args* a, void* stream) {
     return rc;
 }
 
-// GM_QHEAD_BWD=scalar selects the one-column-per-thread kernel (A-B timing)
-const bool g_qhead_vec = [] {
-    const char* e = getenv("GM_QHEAD_BWD");
-    return !(e && strcmp(e, "scalar") == 0);
-}();
-
 extern "C" int gm_qhead_bwd(const float* dq, int64_t ldq, int32_t nq, const float* wq, int64_t ldwq, const float* y,
                             int64_t ldy, int64_t rows, int32_t cols, int32_t act, float* g, int64_t ldg, float* part_b,
                             float* part_wq, float* part_bq, int32_t rows_per_block, float* g_scale, void* stream) {
@@ -1337,7 +1318,7 @@ extern "C" int gm_qhead_bwd(const float* dq, int64_t ldq, int32_t nq, const floa
         return gm_fail(GM_ERR_HIP, "gm_qhead_bwd: memset");
     const long long nb = (rows + rows_per_block - 1) / rows_per_block;
     auto a16 = [](const void* p, long long ld) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0 && ld % 4 == 0; };
-    if (g_qhead_vec && cols % 4 == 0 && cols <= 1024 && ((256 / (cols / 4)) * (cols / 4)) % 64 == 0 && a16(wq, ldwq) &&
+    if (cols % 4 == 0 && cols <= 1024 && ((256 / (cols / 4)) * (cols / 4)) % 64 == 0 && a16(wq, ldwq) &&
         a16(y, ldy) && a16(g, ldg) && a16(part_b, cols) && a16(part_wq, cols)) {
         const int rl = 256 / (cols / 4);
         hipLaunchKernelGGL(k_qhead_bwd4, dim3((unsigned)nb), dim3(rl * (cols / 4)), 0, st, dq, (long long)ldq, nq, wq,

@@ -14,7 +14,6 @@ Weights are packed once per parameter version (LSTM gate interleave, W1 column o
 and for the split-f16 form (L.GEMM_MODE == "x3", gm_gemm_x3) the hi/lo f16 split).
 """
 import ctypes as C
-import os
 
 import torch
 import torch.nn.functional as F
@@ -64,9 +63,6 @@ def _setup():
         lib.gm_gemm_x3_dgrad.argtypes = [C.POINTER(ASrc), vp, vp, C.c_int32, C.c_int32, C.c_int32, vp, C.c_int64, vp,
                                          C.c_int64, vp, C.c_int64, vp, vp, vp]
         i32, i64 = C.c_int32, C.c_int64
-        if hasattr(lib, "gm_dqn_x3") or not os.environ.get("GM_LIB"):  # an older GM_LIB build lacks it
-            lib.gm_dqn_x3.argtypes = [C.POINTER(ASrc), C.POINTER(ASrc), vp, vp, vp, i32, vp, vp, vp, i32, i32, i32,
-                                      i32, vp, i64, vp, i32, vp, i64, vp]
         lib.gm_encoder_x3.argtypes = [C.POINTER(ASrc), vp, vp, vp, i32, vp, vp, vp, i32, i32, i32, i32, vp, i64, vp]
         lib._gemm_ready = True
     return lib
@@ -116,20 +112,21 @@ def routing_enc_src(lin, x, nbr, N):
 
 
 # the rollout folds the NetMon encoder's first layer into the second layer's A-tile load when the split
-# form runs and 4N + 8 <= 208, N <= 50 (GM_A_ROUTING_ENC, always on 16x16x32 MFMA); GM_RENC_FOLD=0 keeps
-# gm_routing_node_encoder + a DENSE second layer (A-B timing)
-RENC_FOLD = os.environ.get("GM_RENC_FOLD", "1") != "0"
+# form runs and 4N + 8 <= 208, N <= 50 (GM_A_ROUTING_ENC, always on 16x16x32 MFMA); otherwise
+# gm_routing_node_encoder + a DENSE second layer (tests set it False to compare the two forms)
+RENC_FOLD = True
 
 
 def renc_fold_ok(layers, N, Fd, nbr):
     return (RENC_FOLD and L.GEMM_MODE == "x3" and len(layers) >= 2 and routing_encoder_ok(layers[0], N, Fd, nbr)
             and 4 * N + 8 <= 208 and layers[0].out_features % 32 == 0 and layers[0].out_features <= 1024
-            and use_x3(layers[1].out_features) and layers[1].in_features == layers[0].out_features)
+            and use_x3(layers[1].out_features) and layers[1].in_features == layers[0].out_features
+            and layers[1].bias is not None)
 
 
 # the rollout's NetMon encoder [4N+8 -> k -> 256 -> 128] (the CLI default 512, 256 with H = 128) in one launch
-# (gm_encoder_x3: layer 2's output stays on chip for layer 3); GM_ENC_CHAIN=0 keeps the fold + a layer-3 GEMM
-ENC_CHAIN = os.environ.get("GM_ENC_CHAIN", "1") != "0"
+# (gm_encoder_x3: layer 2's output stays on chip for layer 3); other shapes run the fold + a layer-3 GEMM
+ENC_CHAIN = True
 
 
 def encoder_chain_ok(layers, N, Fd, nbr):
@@ -352,38 +349,6 @@ def linear_head(lin, fc, x, ldx, k, q, y=None):
     return q
 
 
-# The DQN's layers 1, 2 and the Q head as ONE kernel (gm_dqn_x3: the 512-wide layer-1 activation
-# stays on chip). Opt-in (GM_DQN_FUSED=1): 64-row blocks are needed for the on-chip activation, and
-# the layer-2 phase runs with 1 block per CU after layer 1, so it measured 360-420 us per 81 920 rows
-# against 300-310 us for layer 1 + the fused layer 2 + head as two kernels
-DQN_FUSED = os.environ.get("GM_DQN_FUSED", "0") == "1"
-
-
-def dqn_fused_ok(dqn):
-    """gm_dqn_x3 covers the CLI-default DQN: mlp_units 512, 256 (+ bias), <= 4 actions, split-f16 form."""
-    layers = dqn.encoder.linear_layers
-    return (DQN_FUSED and L.GEMM_MODE == "x3" and len(layers) == 2 and layers[0].out_features == 512
-            and layers[1].out_features == 256 and layers[1].in_features == 512 and layers[0].bias is not None
-            and head_ok(layers[1], dqn.q_net.fc))
-
-
-def dqn_fused(dqn, a0, a1, x3_1, b1, M, K, q):
-    """q [M, actions] = gm_dqn_x3 on A = a0 (++ a1) with layer 1's packed weights x3_1 / bias b1 (the
-    column order of the sources, fused.pack_dqn_first)."""
-    lib = _setup()
-    lin0, lin1 = dqn.encoder.linear_layers
-    fc = dqn.q_net.fc
-    x3_2 = pack_x3(lin1)
-    wq = fc.weight if fc.weight.is_contiguous() else fc.weight.contiguous()
-    tag = lin0.tag and f"dqn_fused:{lin0.tag}:{M}x512x{K}"
-    with L.timed(tag):
-        L.check(lib.gm_dqn_x3(C.byref(a0), None if a1 is None else C.byref(a1), x3_1.wp.data_ptr(),
-                              x3_1.sinv.data_ptr(), b1.data_ptr(), lin0.act, x3_2.wp.data_ptr(), x3_2.sinv.data_ptr(),
-                              lin1.bias.data_ptr(), lin1.act, M, 512, 256, wq.data_ptr(), wq.stride(0),
-                              fc.bias.data_ptr(), fc.out_features, q.data_ptr(), q.stride(0), L.stream_ptr()))
-    return q
-
-
 def _linear(x, ldx, k, lin, out):
     wp, ldw = lin._wc.get(lin.weight)
     a = dense(x.data_ptr(), ldx, k)
@@ -601,8 +566,6 @@ def dqn_q(dqn, env_obs, obs_dim, state, h_prev, nbr, agent_node, scratch, hidden
     else:
         src, ks = dense(env_obs.data_ptr(), stride, obs_dim), obs_dim
     a0 = readout(state.data_ptr(), state.shape[-1], h_prev.data_ptr(), h_prev.stride(0), nbr, agent_node, N, H)
-    if x3 is not None and dqn_fused_ok(dqn):
-        return dqn_fused(dqn, a0, src, x3, b, M, a0.k + ks, scratch(3, M, dqn.q_net.fc.out_features))
     h1 = scratch(0, M, lin0.out_features)
     gemm(a0, src, wp.data_ptr(), ldw, b.data_ptr(), M, lin0.out_features,
          _epi(lin0.act), h1.data_ptr(), h1.stride(0),
@@ -628,10 +591,6 @@ def dqn_q_dense(dqn, env_obs, graph, scratch):
     g2 = graph.reshape(M, graph.shape[-1])
     lin0 = dqn.encoder.linear_layers[0]
     wp, ldw, b, x3 = pack_dqn_first(lin0, od)
-    if x3 is not None and dqn_fused_ok(dqn) and g2.shape[1] % 32 == 0 and g2.stride(0) % 4 == 0:
-        return dqn_fused(dqn, dense(g2.data_ptr(), g2.stride(0), g2.shape[1]),
-                         dense(env_obs.data_ptr(), env_obs.stride(1), od), x3, b, M, g2.shape[1] + od,
-                         scratch(3, M, dqn.q_net.fc.out_features))
     h1 = scratch(0, M, lin0.out_features)
     gemm(dense(g2.data_ptr(), g2.stride(0), g2.shape[1]), dense(env_obs.data_ptr(), env_obs.stride(1), od),
          wp.data_ptr(), ldw, b.data_ptr(), M, lin0.out_features, _epi(lin0.act),

@@ -5,12 +5,11 @@ Q-values come from the agent model (DQN, DGN, DQNR, CommNet) on the HIP kernels;
 stream) and the argmax/mix run in the env's egreedy kernel (gm_policy_egreedy /
 gm_simple_policy_egreedy).
 """
-import os
 
 import torch
 
-# GM_POLICY_STEP=split keeps ε-greedy and the env step as two launches (A-B timing)
-FUSED_POLICY_STEP = os.environ.get("GM_POLICY_STEP", "fused") != "split"
+# ε-greedy runs as the env step kernel's prologue (gm_env_policy_step); tests compare it with the two launches
+FUSED_POLICY_STEP = True
 
 
 class EpsilonGreedy:

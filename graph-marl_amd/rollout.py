@@ -19,7 +19,6 @@ launch cost (one replay call per group per captured length). Graph replay bakes 
 arguments in: it is for fixed-ε rollouts (ε decay 1.0: benchmarks, evaluation); episode resets
 stay eager between replays.
 """
-import os
 
 import torch
 
@@ -31,8 +30,9 @@ from .wrapper import NetMonWrapper
 
 
 # the rollout's envs write only the GEMM-ready obs copy that the fused DQN reads; reading .obs
-# rebuilds the reference rows from it (Routing.set_lazy_obs). GM_LAZY_OBS=0: write both every step
-LAZY_OBS = os.environ.get("GM_LAZY_OBS", "1") != "0"
+# rebuilds the reference rows from it (Routing.set_lazy_obs); tests set it False to compare with envs that
+# write both copies every step
+LAZY_OBS = True
 
 
 class _PlainEnv:

@@ -16,8 +16,8 @@ import torch
 
 from . import _lib as L
 
-# GM_GEMM_OBS=0: the fused DQN reads the env obs with K = 6N+10 instead of the GEMM-ready copy (A-B)
-GEMM_OBS = os.environ.get("GM_GEMM_OBS", "1") != "0"
+# the fused DQN reads the GEMM-ready copy of the agent rows (K = 6N+8) instead of the env obs (K = 6N+10)
+GEMM_OBS = True
 
 EVAL_SEEDS = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "data", "eval_seeds.npy"))
 
@@ -179,7 +179,7 @@ class Routing:
     def enable_gemm_obs(self):
         """Have every reset / step / observe also write the GEMM-ready copy of the agent rows
         (gm_obs_buffers.obs_gemm: 6N+8 columns, the two linearly dependent ones dropped) that the
-        fused DQN's first layer reads with K = 6N+8. Variant 1 only; GM_GEMM_OBS=0 disables."""
+        fused DQN's first layer reads with K = 6N+8. Variant 1 only."""
         if self.obs_gemm is not None or self.env_var != 1 or not GEMM_OBS:
             return self.obs_gemm
         self.obs_gemm = torch.zeros(self.n_env, self.n_data, 6 * self.n_nodes + 8, device=self.device)

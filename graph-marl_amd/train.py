@@ -30,6 +30,25 @@ def _distributed(group=None):
     return dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1
 
 
+_BUCKET = {}
+
+
+def _bucket(params):
+    """The exchange's persistent buffers for this parameter list (no per-update allocation):
+    the flat bucket (every parameter + the failure flag), a zero tensor per parameter for ranks / parameters
+    without .grad, and the two flag values [0.], [1.]."""
+    key = tuple((id(p), p.numel()) for p in params)
+    b = _BUCKET.get(key)
+    if b is None:
+        p0 = params[0]
+        n = sum(p.numel() for p in params) + 1
+        b = (torch.empty(n, dtype=p0.dtype, device=p0.device), [torch.zeros_like(p) for p in params],
+             (torch.zeros(1, dtype=p0.dtype, device=p0.device), torch.ones(1, dtype=p0.dtype, device=p0.device)))
+        _BUCKET.clear()
+        _BUCKET[key] = b
+    return b
+
+
 def allreduce_gradients(params, group=None, failed=False):
     """Average .grad over the process group with ONE bucketed all-reduce. The bucket carries one
     extra element, the number of ranks that failed: a rank whose step raised posts the same
@@ -39,9 +58,9 @@ def allreduce_gradients(params, group=None, failed=False):
     read of the flag per update, only when world > 1."""
     if not _distributed(group):
         return
-    parts = [(p.grad if (p.grad is not None and not failed) else torch.zeros_like(p)).reshape(-1) for p in params]
-    flag = parts[0].new_full((1,), 1.0 if failed else 0.0)
-    flat = torch.cat(parts + [flag])
+    flat, zeros, flags = _bucket(params)
+    parts = [(p.grad if (p.grad is not None and not failed) else zeros[i]).reshape(-1) for i, p in enumerate(params)]
+    torch.cat(parts + [flags[1 if failed else 0]], out=flat)
     dist.all_reduce(flat, group=group)
     nfail = int(round(float(flat[-1].item())))
     if nfail:

@@ -378,7 +378,8 @@ typedef struct {
  * (src/model.py:13-42, 489) on routing node observations x (src/env/routing.py:187-235: [onehot(n) | cnt |
  * load | 3 x (onehot(nbr_k) | len_k | load_k)], 4N + 8 columns) computed inside the GEMM's A-tile load from
  * the 12 nonzero columns, so the m x k layer output never reaches HBM: p0 = x rows ([G * n_nodes][ld0]),
- * p1 = W0^T ([4N + 8][ld1], ld1 >= k), nbr = [G][n_nodes][3] (deg = 3), n_nodes = N with 4N + 8 <= 208 (N <= 50),
+ * p1 = W0^T ([4N + 8][ld1], ld1 >= k), nbr = [G][n_nodes][3] (deg = 3, every entry a node id in [0, N): the
+ * routing graphs are 3-regular; -1 entries are NOT masked here, unlike READOUT), n_nodes = N with 4N + 8 <= 208 (N <= 50),
  * k = the layer's width (multiple of 32), bias0 / act0. Runs on v_mfma_f32_16x16x32_f16 (whatever
  * gm_gemm_set_mfma selects for the other GEMMs) and needs a bias epilogue; other cases return
  * GM_ERR_UNSUPPORTED (run gm_routing_node_encoder and a DENSE source instead). */
@@ -423,16 +424,6 @@ int gm_gemm_range_status(int32_t* status, int32_t clear);
 int gm_gemm_x3_head(const gm_a_src* src0, const void* wp, const float* wscale_inv, const float* b, int32_t m,
                     int32_t n, int32_t act, const float* wq, int64_t ldwq, const float* bq, int32_t nq, float* q,
                     int64_t ldq, float* y, int64_t ldy, void* stream);
-/* The DQN's two hidden layers and its Q head in ONE launch (src/model.py:187-203 DQN with mlp_units
- * 512, 256 and <= 4 actions; split-f16 form): h1 = act1(A W1^T + b1) with A from a0 (dense rows, or
- * the NetMon READOUT gather) ++ the optional dense a1 (as gm_gemm_x3, W1 packed for the combined K),
- * q = act2(h1 W2^T + b2) wq^T + bq. A 64-row block keeps its rows' h1 on chip (LDS, split f16), so
- * the m x 512 activation is never written; the hidden layer-2 activation neither. w1p / w2p and
- * w1sinv / w2sinv: gm_gemm_pack_x3 of W1 [512][K] and W2 [256][512]. */
-int gm_dqn_x3(const gm_a_src* a0, const gm_a_src* a1, const void* w1p, const float* w1sinv, const float* b1,
-              int32_t act1, const void* w2p, const float* w2sinv, const float* b2, int32_t act2, int32_t m, int32_t n1,
-              int32_t n2, const float* wq, int64_t ldwq, const float* bq, int32_t nq, float* q, int64_t ldq,
-              void* stream);
 /* The rollout's NetMon encoder (src/model.py:13-42 MLP, 489) in ONE launch: layer 1 computed in layer 2's
  * A-tile load from the routing node observations (a0: GM_A_ROUTING_ENC), layer 2 (n2 = 256) kept on chip
  * per 128-row block as split-f16 LDS images, layer 3 (n3 = 128) from them; y [m][ldy] = act3(act2(A W2^T +

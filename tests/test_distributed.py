@@ -136,27 +136,63 @@ def test_bench_gpus_flag_launches_ranks(monkeypatch):
 
 
 def test_bench_pmc_window_parser(tmp_path):
-    """bench.py's same-run PMC probe (measure_pmc) reads the child's counter CSV: the last
-    2 PMC_X + PMC_Y dispatches of the library's kernels are PMC_X (DQN layer 1, layer 2 + head)
-    pairs then PMC_Y env steps; medians per launch; a window of another shape is rejected."""
+    """bench.py's same-run PMC probe (measure_pmc) reads the child's counter CSV: the last PMC_S x P
+    dispatches of the library's kernels must repeat one step's P launches (the order the child recorded);
+    medians per launch per tag, the per-step sum; a window of another shape is rejected."""
     import bench
 
-    X, Y = bench.PMC_X, bench.PMC_Y
-    rows = [("at::native::fill", 64, 1.0)] * 3 + [("k_env_reset", 4096, 7.0)]
-    rows += [("k_gemm3g", 655360, 100.0 + i) for i in range(1)]  # older dispatch outside the window
-    for i in range(X):
-        rows += [("k_gemm3g", 655360, 200.0 + i), ("k_gemm3g", 327680, 50.0)]
-    rows += [("k_env_step", 262144, 30.0 + i) for i in range(Y)]
+    S = bench.PMC_S
+    order = ["linear:dqn.l0", "linear:dqn.l1+head", "env_step", "linear:netmon.chain", "lstm:obs",
+             "mp_aggregate:81920x128", "lstm_agg:upd"]
+    kern = ["k_gemm3g_a", "k_gemm3g_b", "k_env_step", "k_gemm3g_c", "k_gemm3g_d", "k_mp_aggregate3", "k_gemm3g_d"]
+    rows = [("at::native::fill", 64, 1.0)] * 3 + [("k_env_reset", 4096, 7.0), ("k_gemm3g_a", 655360, 5.0)]
+    for s in range(S):
+        rows += [(k, 1000, 10.0 * (i + 1) + s) for i, k in enumerate(kern)]
+        rows += [("__amd_rocclr_fillBufferAligned", 256, 3.0)]  # not ours: skipped
     p = tmp_path / "c.csv"
-    with open(p, "w") as f:
-        f.write("Dispatch_Id,Kernel_Name,Grid_Size,Counter_Name,Counter_Value\n")
-        for i, (n, g, v) in enumerate(rows):
-            f.write(f"{i},{n},{g},FETCH_SIZE,{v}\n")
-    l1, env = bench._pmc_window(str(p), "FETCH_SIZE")
-    assert l1 == 200.0 + X // 2 and env == 30.0 + Y // 2
-    with open(p, "a") as f:  # one more layer-2 dispatch after the env steps: not the probe's window
-        f.write(f"{len(rows)},k_gemm3g,327680,FETCH_SIZE,1.0\n")
-    assert bench._pmc_window(str(p), "FETCH_SIZE") is None
+
+    def write(rs):
+        with open(p, "w") as f:
+            f.write("Dispatch_Id,Kernel_Name,Grid_Size,Counter_Name,Counter_Value\n")
+            for i, (n, g, v) in enumerate(rs):
+                f.write(f"{i},{n},{g},FETCH_SIZE,{v}\n")
+
+    write(rows)
+    per, step = bench._pmc_window(str(p), "FETCH_SIZE", order)
+    assert per["env_step"] == 30.0 + S // 2 and per["linear:dqn.l0"] == 10.0 + S // 2
+    assert step == sum(10.0 * (i + 1) for i in range(len(kern))) + len(kern) * (S // 2)
+    write(rows + [("k_gemm3g_b", 1000, 1.0)])  # one more dispatch after the window: not a whole step
+    assert bench._pmc_window(str(p), "FETCH_SIZE", order) is None
+    swapped = list(order)
+    swapped[2], swapped[3] = swapped[3], swapped[2]  # the env step where the order has a GEMM
+    write(rows)
+    assert bench._pmc_window(str(p), "FETCH_SIZE", swapped) is None
+    assert bench._pmc_window(str(p), "FETCH_SIZE", []) is None
+
+
+def test_bench_committed_traffic_prefers_same_sources(tmp_path, monkeypatch):
+    """The committed-profile fallback (bench.pmc_traffic) takes a profile whose source hash is the build's,
+    else the newest (round, seq, file time), never the largest byte count (VERDICT r05 weak #1)."""
+    import json
+
+    import bench
+
+    def prof(rnd, name, src, seq, fetch):
+        d = tmp_path / "profiles" / rnd / name
+        d.mkdir(parents=True)
+        (d / "pmc_traffic.json").write_text(json.dumps(
+            {"src": src, "seq": seq, "kernels": {"k": {"fetch_bytes": fetch, "write_bytes": 0}}}))
+
+    prof("r05", "a", "aaaa", 0, 900)
+    prof("r05", "b", "bbbb", 0, 100)
+    prof("r04", "c", "cccc", 3, 50)
+    monkeypatch.setattr(bench, "ROOT", str(tmp_path))
+    tb, note = bench.pmc_traffic("k", "bbbb")
+    assert tb == 100 and "same sources" in note
+    os.utime(tmp_path / "profiles" / "r05" / "a" / "pmc_traffic.json", (1, 1))
+    tb, note = bench.pmc_traffic("k", "zzzz")  # no same-source profile: the newest file of the newest round
+    assert tb == 100 and "OTHER sources (bbbb)" in note
+    assert bench.pmc_traffic("missing", "bbbb") == (None, None)
 
 
 def _fail_worker(rank, world, port, q, fail_at, steps, update_every):

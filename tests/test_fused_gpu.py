@@ -540,46 +540,6 @@ def test_joint_first_layer_split_vs_fp64(rows):
         torch.testing.assert_close(q1, q0, atol=1e-5, rtol=0)
 
 
-@pytest.mark.parametrize("n_env", [64, 37])
-@pytest.mark.parametrize("gemm_obs", [True, False])
-@pytest.mark.parametrize("act", ["leaky_relu", "tanh"])
-def test_dqn_fused_kernel_matches_two_kernels(n_env, gemm_obs, act, monkeypatch):
-    """gm_dqn_x3 (layers 1, 2 and the Q head in one launch, layer-1 activation kept in LDS) == layer 1
-    + the fused layer 2 + head (gm_gemm_x3 + gm_gemm_x3_head) on the same rollout state: the layer-2
-    A operand is split into the same f16 pieces, so Q agrees to the head's summation order; row
-    counts that are not a multiple of the 64-row block (37 x 20); fp64 Q within 1e-5."""
-    gm, M, FU, W = mods()
-    import netmon_ref
-
-    env, nm, w = _setup_env(gm, W, M, B=n_env, fused=True)
-    torch.manual_seed(5)
-    dqn = M.DQN(env.obs_dim + 512, [512, 256], 4, activation=act).cuda()
-    monkeypatch.setattr(FU, "DQN_FUSED", True)  # opt-in kernel (GM_DQN_FUSED=1)
-    assert FU.dqn_fused_ok(dqn)
-    w.reset()
-    for _ in range(3):
-        w.step_(torch.randint(0, 4, (n_env, env.n_data), device="cuda", dtype=torch.int32))
-    if gemm_obs:
-        env.enable_gemm_obs()
-    og = env.obs_gemm if gemm_obs else None
-    assert (og is not None) == gemm_obs
-    args = (dqn, env.obs_buf, env.obs_dim, w.current_netmon_state, w.h_prev, env.nbr, env.agent_node)
-
-    def scratch_fn():
-        d = {}
-        return lambda i, m, n: d.setdefault((i, m, n), torch.empty(m, n, device="cuda"))
-
-    q1 = FU.dqn_q(*args, scratch_fn(), hidden=128, obs_gemm=og).clone()
-    monkeypatch.setattr(FU, "DQN_FUSED", False)
-    assert not FU.dqn_fused_ok(dqn)
-    q2 = FU.dqn_q(*args, scratch_fn(), hidden=128, obs_gemm=og).clone()
-    torch.testing.assert_close(q1, q2, atol=2e-6, rtol=0)
-    joint = w.obs.reshape(n_env * env.n_data, -1).double().cpu().numpy()
-    Wd = {k: v.detach().double().cpu().numpy() for k, v in dqn.state_dict().items()}
-    q64 = netmon_ref.dqn_forward(Wd, joint, act=act)
-    assert abs(q1.double().cpu().numpy() - q64).max() < 1e-5
-
-
 @pytest.mark.parametrize("N,B", [(20, 4096), (10, 333), (30, 700), (40, 512), (50, 1024)])
 def test_routing_encoder_fold_matches_two_kernels(N, B):
     """Round 5: the rollout computes NetMon encoder layer 1 inside layer 2's A-tile load (GM_A_ROUTING_ENC,

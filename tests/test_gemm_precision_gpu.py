@@ -10,7 +10,9 @@ small activations is what a denormal low split piece would hurt) and weight rows
 and bounds the error of every output against fp64, relative to sum |a * w| of that output (the error
 measure of an fp32 dot product), for both the split-f16 form and the exact-f32 form on the same inputs.
 
-Stated bound: split-f16 <= max(4e-6, 4 x the exact-f32 GEMM's own error). The dropped a_lo * w_lo term
+Stated bound (round 6, VERDICT r05 item 7): split-f16 <= max(1e-6, 2 x the exact-f32 GEMM's own error);
+measured 2.5-6.4e-7 against 3.5-10.2e-7 for the exact-f32 form (round 5: max(4e-6, 4x), which a 6-15x
+regression would have passed). Every case prints its error / tolerance ratio. The dropped a_lo * w_lo term
 and the 22-bit pieces put the split form at ~2^-22 of sum |a * w|; the exact f32 MFMA chain at ~2^-24 * a
 small K-dependent factor. A low piece that rounds to an f16 denormal (|a| < 2^-3 without the 2^12 scale)
 has an absolute error up to 2^-25 per element and fails this bound on the 2^-12 rows."""
@@ -22,8 +24,14 @@ import torch.nn.functional as F
 
 pytestmark = pytest.mark.gpu
 
-BOUND_ABS = 4e-6
-BOUND_X_F32 = 4.0
+BOUND_ABS = 1e-6
+BOUND_X_F32 = 2.0
+
+
+def _check(name, e_x3, e_f32):
+    tol = max(BOUND_ABS, BOUND_X_F32 * e_f32)
+    print(f"{name}: split {e_x3:.3g}, exact-f32 {e_f32:.3g}, tolerance {tol:.3g}, worst/tolerance {e_x3 / tol:.3f}")
+    assert e_x3 <= tol, (name, e_x3, e_f32)
 
 
 def mods():
@@ -73,7 +81,7 @@ def test_split_gemm_error_at_production_tile(name, m, n, k, tile):
         lib.gm_gemm_set_tile(-1)
     print(f"{name}: relative error vs fp64 (of sum |a w|): {errs}")
     assert errs["f32"] < 2e-6, errs  # the exact-f32 MFMA chain itself, K <= 640
-    assert errs["x3"] <= max(BOUND_ABS, BOUND_X_F32 * errs["f32"]), errs
+    _check(name, errs["x3"], errs["f32"])
 
 
 def test_split_readout_layer_error_at_production_tile():
@@ -118,7 +126,7 @@ def test_split_readout_layer_error_at_production_tile():
         errs[form] = _rel(y, ref, mag)
     print(f"dqn_layer1_readout_tile9: relative error vs fp64 (of sum |a w|): {errs}")
     assert errs["f32"] < 2e-6, errs  # the exact-f32 MFMA chain itself, K <= 640
-    assert errs["x3"] <= max(BOUND_ABS, BOUND_X_F32 * errs["f32"]), errs
+    _check("dqn_layer1_readout_tile9", errs["x3"], errs["f32"])
 
 
 def test_split_head_error_at_production_tile():
@@ -146,5 +154,5 @@ def test_split_head_error_at_production_tile():
     y32 = _gemm(FU, x, *FU._pad_cols(w), n, k, "f32")
     e32 = _rel(y32, hid, mag)
     print(f"head: hidden {e_hid:.3g}, q {e_q:.3g}, exact-f32 hidden {e32:.3g}")
-    assert e_hid <= max(BOUND_ABS, BOUND_X_F32 * e32), (e_hid, e32)
-    assert e_q <= max(BOUND_ABS, BOUND_X_F32 * e32), (e_q, e32)
+    _check("head hidden", e_hid, e32)
+    _check("head q", e_q, e32)

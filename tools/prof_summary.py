@@ -107,7 +107,7 @@ def main():
     ap.add_argument("--src", help="build.src of the profiled library (recorded; bench.py compares it)")
     ap.add_argument("--rows", type=int, default=81920, help="GEMM rows of the profiled rollout (n_env * N)")
     ap.add_argument("--env-k", type=int, default=128,
-                    help="env-obs columns of DQN layer 1 (128: GEMM-ready obs copy, 130: GM_GEMM_OBS=0 profiles)")
+                    help="env-obs columns of DQN layer 1 (128: GEMM-ready obs copy, 130: the round-1/2 profiles)")
     ap.add_argument("--netmon-layers", action="store_true", help="profiles taken before gm_encoder_x3 (round 5)")
     a = ap.parse_args()
     nmg = NETMON_G_LAYERS if a.netmon_layers else NETMON_G

@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """gm_netmon_readout_bwd timing at the sequence-batched update's size (G graphs of N nodes, R agents,
-H = 128): python tools/readout_bwd_bench.py (GM_READOUT_BWD=graph: one block per graph)."""
+H = 128): python tools/readout_bwd_bench.py."""
 import importlib
 import os
 import sys
@@ -37,5 +37,5 @@ for _ in range(3):
     torch.cuda.synchronize()
     best = min(best, s.elapsed_time(e) / 5 * 1e3)
 gb = (dout.numel() + dhf.numel() + dhp.numel()) * 4 / 1e9
-print(f"{os.environ.get('GM_READOUT_BWD', 'cs')}: {best:.1f} us, {gb / best * 1e6 / 1e3:.2f} TB/s "
+print(f"cs: {best:.1f} us, {gb / best * 1e6 / 1e3:.2f} TB/s "
       f"checksum {dhf.double().sum().item():.6e} {dhp.double().sum().item():.6e}")
