@@ -670,6 +670,124 @@ def gen_train(out, Network, Routing, EVAL_SEEDS, NetMon, DQN, interpolate_model,
     print(os.path.basename(out), "done", flush=True)
 
 
+def gen_train_models(out, Network, Routing, EVAL_SEEDS, DGN, DQNR, CommNet, interpolate_model, name, att_coeff=0.0,
+                     B=4, L=3, n=20, a=20, seed=400):
+    """One update of a non-default model (src/main.py:840-1026 with netmon None, src/model.py:45-184,
+    653-794) on real routing agent observations and agent adjacency: DGN with the attention-KL
+    regulariser (att_coeff, src/main.py:920-954: the target model runs on the next observation, its
+    attention weights are the KL target), DQNR / CommNet with the agent state loaded from the replayed
+    start state at t = 0 (src/main.py:847-849), handed to the target model (899-902) and masked by done /
+    episode_done after it (956-964). Records q, q_target, loss (and loss_q / loss_att), the raw and
+    clipped gradients, the AdamW step and the soft target update, like gen_train."""
+    import torch
+    import torch.nn.functional as F
+    import torch.optim as optim
+
+    d = {}
+    obs_l, adj_l = [], []
+    envs = []
+    for b in range(B):
+        net = Network(n_nodes=n, random_topology=True, topology_init_seed=476, excluded_seeds=EVAL_SEEDS)
+        env = Routing(net, a, 1)
+        np.random.seed(seed + b)
+        envs.append((env, env.reset()))
+    rs = np.random.RandomState(seed)
+    for t in range(L + 1):
+        ob, ad = [], []
+        for b, (env, (o, g)) in enumerate(envs):
+            ob.append(o.astype(np.float32))
+            ad.append(g.astype(np.float32))
+            o2, g2, _, _, _ = env.step(rs.randint(4, size=a))
+            envs[b] = (env, (o2, g2))
+        obs_l.append(np.stack(ob))
+        adj_l.append(np.stack(ad))
+    agent_obs, agent_adj = np.stack(obs_l), np.stack(adj_l)
+    D = agent_obs.shape[-1]
+    act_fn = F.leaky_relu
+    torch.manual_seed(seed + 1)
+    make = {"dgn": lambda: DGN(D, [64, 48], 4, 4, 2, act_fn),
+            "dqnr": lambda: DQNR(D, [64, 48], 4, act_fn),
+            "commnet": lambda: CommNet(D, [64, 48], 4, 2, act_fn)}[name]
+    model = make()
+    model_tar = copy.deepcopy(model)
+    with torch.no_grad():  # DGN: the attention query / key weights perturbed more, so that the KL is not ~0
+        for k, p in model_tar.named_parameters():
+            p.add_((0.3 if att_coeff > 0 and ("fc_q" in k or "fc_k" in k) else 0.01) * torch.randn_like(p))
+    sd_to_npz("model_", model.state_dict(), d)
+    sd_to_npz("target_", model_tar.state_dict(), d)
+    rng = np.random.RandomState(seed + 2)
+    has_state = hasattr(model, "state")
+    if has_state:
+        d["agent_state0"] = (0.1 * rng.standard_normal((B, a, model.get_state_len()))).astype(np.float32)
+    actions = rng.randint(4, size=(L, B, a))
+    reward = rng.choice(np.array([0.0, -0.2, 10.0, -10.0, 9.8], dtype=np.float32), size=(L, B, a)).astype(np.float32)
+    done = rng.rand(L, B, a) < 0.15
+    episode_done = rng.rand(L, B) < 0.3
+    d.update(agent_obs=agent_obs, agent_adj=agent_adj.astype(np.int8), actions=actions.astype(np.int8), reward=reward,
+             done=done.astype(np.int8), episode_done=episode_done.astype(np.int8))
+    gamma, lr, tau = 0.9, 1e-3, 0.01
+    d["gamma"], d["lr"], d["tau"], d["att_coeff"] = np.float64(gamma), np.float64(lr), np.float64(tau), np.float64(att_coeff)
+    d["arch_model"] = np.array(name)
+    parameters = list(model.parameters())
+    optimizer = optim.AdamW(parameters, lr=lr)
+    model.train()
+    loss_q = torch.zeros(1)
+    loss_att = torch.zeros(1)
+    for t in range(L):
+        obs, adj = torch.tensor(agent_obs[t]), torch.tensor(agent_adj[t])
+        next_obs, next_adj = torch.tensor(agent_obs[t + 1]), torch.tensor(agent_adj[t + 1])
+        bdone, bep = torch.tensor(done[t]), torch.tensor(episode_done[t])
+        if has_state and t == 0:
+            model.state = torch.tensor(d["agent_state0"])
+        q_values = model(obs, adj)
+        with torch.no_grad():
+            if has_state:
+                model_tar.state = model.state.detach()
+            next_q = model_tar(next_obs, next_adj)
+            next_q_max = next_q.max(dim=2)[0]
+        if has_state:
+            state_mask = ~bdone * (~bep).view(-1, 1)
+            model.state = model.state * state_mask.unsqueeze(-1)
+        tgt = torch.tensor(reward[t]) + (~bdone) * gamma * next_q_max
+        q_target = torch.scatter(q_values.detach(), -1, torch.tensor(actions[t]).long().unsqueeze(-1),
+                                 tgt.unsqueeze(-1))
+        loss_q = loss_q + torch.mean((q_values - q_target).pow(2)) / L
+        if hasattr(model, "att_weights") and att_coeff > 0:
+            attention = F.log_softmax(torch.stack(model.att_weights), dim=-1)
+            target_attention = F.softmax(torch.stack(model_tar.att_weights), dim=-1)
+            shape = attention.shape
+            kl = F.kl_div(attention.view(-1, a), target_attention.view(-1, a), reduction="none").view(shape)
+            kl = kl.transpose(0, -2).transpose(0, 1).sum(dim=(-1, -2, -3))
+            kl = (kl * ~bdone).sum() / torch.clamp((~bdone).sum(), min=1)
+            loss_att = loss_att + kl / L
+        d[f"q_{t}"] = q_values.detach().numpy()
+        d[f"qtarget_{t}"] = q_target.numpy()
+    loss = loss_q + att_coeff * loss_att
+    optimizer.zero_grad()
+    names = [f"model_{k}" for k, _ in model.named_parameters()]
+    if att_coeff > 0:  # the regulariser's own gradient, so that its sign and scale are pinned apart from the TD term
+        ga = torch.autograd.grad(att_coeff * loss_att.sum(), parameters, retain_graph=True, allow_unused=True)
+        for nm_, g_ in zip(names, ga):
+            d["grad_att_" + nm_] = (torch.zeros_like(p) if g_ is None else g_).detach().numpy().copy()
+    loss.backward()
+    d["loss"], d["loss_q"], d["loss_att"] = loss.detach().numpy(), loss_q.detach().numpy(), loss_att.detach().numpy()
+    for nm_, p in zip(names, parameters):
+        d["grad_raw_" + nm_] = p.grad.detach().numpy().copy()
+    torch.nn.utils.clip_grad_value_(parameters, 0.5)
+    d["clip_total_norm"] = np.float64(torch.nn.utils.clip_grad_norm_(parameters, 1.0).item())
+    for nm_, p in zip(names, parameters):
+        d["grad_clip_" + nm_] = p.grad.detach().numpy().copy()
+    optimizer.step()
+    for nm_, p in zip(names, parameters):
+        d["param_after_" + nm_] = p.detach().numpy().copy()
+    interpolate_model(model, model_tar, tau, model_tar)
+    for k, v in model_tar.state_dict().items():
+        d["target_after_" + k] = v.detach().numpy().copy()
+    d["param_names"] = np.array(names)
+    np.savez_compressed(out, **d)
+    print(os.path.basename(out), "done", flush=True)
+
+
 # ---------------------------------------------------------------------------
 # SimpleEnvironment traces (src/env/simple_environment.py) with EpsilonGreedy
 # draws (src/policy.py:44-50) on the same global stream
@@ -1126,6 +1244,12 @@ def main():
         if only is None or f"train_{act}" in only:
             gen_train(os.path.join(HERE, f"train_{act}.npz"), Network, Routing, EVAL_SEEDS, NetMon, DQN,
                       interpolate_model, K=2, B=4, act=act)
+    # the non-default models' updates: DGN with the attention-KL regulariser, DQNR / CommNet
+    # with the replayed agent state
+    for mname, coeff in (("dgn", 0.03), ("dqnr", 0.0), ("commnet", 0.0)):
+        if only is None or f"train_{mname}" in only:
+            gen_train_models(os.path.join(HERE, f"train_{mname}.npz"), Network, Routing, EVAL_SEEDS, DGN, DQNR, CommNet,
+                             interpolate_model, mname, att_coeff=coeff)
     if only is None or "checkpoint" in only:
         gen_checkpoint(os.path.join(HERE, "ref_checkpoint.pt"), os.path.join(HERE, "ref_checkpoint.npz"), args.ref,
                        Network, Routing, EVAL_SEEDS, NetMon, DQN, get_state_dict)

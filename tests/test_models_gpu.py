@@ -169,3 +169,70 @@ def test_training_update_runs_and_reduces_loss(name):
         losses.append(loss.item())
     assert all(np.isfinite(losses))
     assert losses[-1] < losses[0]
+
+
+def _upd_model(M, g):
+    name = str(g["arch_model"])
+    D = g["agent_obs"].shape[-1]
+    make = {"dgn": lambda: M.DGN(D, [64, 48], 4, 4, 2), "dqnr": lambda: M.DQNR(D, [64, 48], 4),
+            "commnet": lambda: M.CommNet(D, [64, 48], 4, 2)}[name]
+    sd = lambda p: {k[len(p):]: torch.as_tensor(g[k]) for k in g.files  # noqa: E731
+                    if k.startswith(p) and not k.startswith(p + "after_")}
+    m, tar = make(), make()
+    m.load_state_dict(sd("model_"))
+    tar.load_state_dict(sd("target_"))
+    return m.cuda(), tar.cuda()
+
+
+@pytest.mark.parametrize("name", ["dgn", "dqnr", "commnet"])
+def test_model_update_matches_reference_golden(name):
+    """one update of the non-default models against the reference's own
+    (tests/golden/train_{dgn,dqnr,commnet}.npz, make_golden.py gen_train_models; src/main.py:840-1026):
+    DGN with --att-regularization-coeff 0.03 (the attention KL against the target model's weights on the
+    next observation, 920-954), DQNR / CommNet from the replayed agent state (847-849), the target model
+    continuing from the online state (899-902), the state masked by done / episode_done after it
+    (956-964). q, q_target, the loss terms, the KL's own gradient (sign and scale), raw and clipped
+    gradients, the AdamW step and the soft target update at the tolerances of the NetMon goldens."""
+    import golden_update as GU
+    from test_train_gpu import check_update
+
+    M, T = mods()
+    RB = importlib.import_module("graph-marl_amd.replaybuffer")
+    g = np.load(os.path.join(R.GOLDEN, f"train_{name}.npz"))
+    m, tar = _upd_model(M, g)
+    dev = torch.device("cuda")
+    f = lambda a: torch.as_tensor(a, device=dev)  # noqa: E731
+    Lq = g["actions"].shape[0]
+    st0 = f(g["agent_state0"]) if "agent_state0" in g.files else None
+    batches = [RB.TransitionBatch(None, f(g["agent_obs"][t]), f(g["actions"][t]).long(), f(g["reward"][t]),
+                                  f(g["agent_obs"][t + 1]), f(g["done"][t]).bool(), f(g["episode_done"][t]).bool(),
+                                  None, None, None, None, None, None, f(g["agent_adj"][t]).float(),
+                                  f(g["agent_adj"][t + 1]).float(), st0 if t == 0 else None) for t in range(Lq)]
+    params = list(m.parameters())
+    names = [f"model_{k}" for k, _ in m.named_parameters()]
+    assert names == list(g["param_names"])
+    opt = torch.optim.AdamW(params, lr=float(g["lr"]))
+    m.train()
+    coeff = float(g["att_coeff"])
+    parts = {}
+    loss, qs, qts = T.dqn_loss(None, m, tar, batches, float(g["gamma"]), att_coeff=coeff, parts=parts)
+    for t in range(Lq):
+        np.testing.assert_allclose(qs[t].detach().cpu().numpy(), g[f"q_{t}"], atol=1e-5, rtol=0, err_msg=f"q_{t}")
+        np.testing.assert_allclose(qts[t].cpu().numpy(), g[f"qtarget_{t}"], atol=1e-5, rtol=0, err_msg=f"qtarget_{t}")
+    np.testing.assert_allclose(parts["loss_q"].item(), g["loss_q"].item(), rtol=1e-5, atol=1e-6)
+    np.testing.assert_allclose(loss.item(), g["loss"].item(), rtol=1e-5, atol=1e-6)
+    if coeff > 0:
+        np.testing.assert_allclose(parts["loss_att"].item(), g["loss_att"].item(), rtol=1e-4, atol=1e-7)
+        ga = torch.autograd.grad(coeff * parts["loss_att"], params, retain_graph=True, allow_unused=True)
+        worst = 0.0
+        for n, p, gr in zip(names, params, ga):
+            ref = g["grad_att_" + n]
+            got = np.zeros_like(ref) if gr is None else gr.detach().cpu().numpy()
+            scale = max(np.abs(ref).max(), 1e-12)
+            worst = max(worst, np.abs(got - ref).max() / scale)
+            # relative to the tensor's largest element: a wrong sign or scale of the KL gradient is O(1) here
+            assert np.abs(got - ref).max() <= 1e-3 * scale + 1e-10, (n, np.abs(got - ref).max(), scale)
+        print(f"{name}: attention-KL gradient worst error / max |g| = {worst:.3g}")
+    opt.zero_grad()
+    loss.backward()
+    check_update(g, names, params, opt, m, tar, T)

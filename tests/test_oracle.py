@@ -199,6 +199,56 @@ def test_agent_model_restatement_matches_reference(name):
         np.testing.assert_allclose(q, g[f"{name}_q_{t}"], atol=5e-6, rtol=0)
 
 
+def _log_softmax(x):
+    m = x.max(-1, keepdims=True)
+    return x - m - np.log(np.exp(x - m).sum(-1, keepdims=True))
+
+
+@pytest.mark.parametrize("name", ["dgn", "dqnr", "commnet"])
+def test_model_update_golden_reproduced_by_fp64_restatement(name):
+    """Pins tests/golden/train_{dgn,dqnr,commnet}.npz (make_golden.py gen_train_models):
+    the fp64 restatement (oracle/models_ref.py) replays the reference's update loop (src/main.py:840-964
+    with netmon None) on the fixture's inputs: q, q_target, the TD loss and DGN's attention KL (KL(softmax
+    target || softmax online) per source agent, summed over layers / heads / destinations, averaged over the
+    agents that are not done)."""
+    import models_ref as MR
+
+    g = np.load(os.path.join(R.GOLDEN, f"train_{name}.npz"))
+    W = lambda p: {k[len(p):]: g[k].astype(np.float64) for k in g.files  # noqa: E731
+                   if k.startswith(p) and not k.startswith(p + "after_")}
+    Wm, Wt = W("model_"), W("target_")
+    L, gamma = g["actions"].shape[0], float(g["gamma"])
+    state = g["agent_state0"].astype(np.float64) if "agent_state0" in g.files else None
+    loss_q = loss_att = 0.0
+    for t in range(L):
+        x, adj = g["agent_obs"][t].astype(np.float64), g["agent_adj"][t].astype(np.float64)
+        xn, adjn = g["agent_obs"][t + 1].astype(np.float64), g["agent_adj"][t + 1].astype(np.float64)
+        done = g["done"][t].astype(bool)
+        if name == "dgn":
+            q, att = MR.dgn(Wm, x, adj, 4)
+            qn, att_t = MR.dgn(Wt, xn, adjn, 4)
+            lp = _log_softmax(np.stack(att))
+            pt = np.exp(_log_softmax(np.stack(att_t)))
+            kl = (pt * (np.log(np.maximum(pt, 1e-300)) - lp)).sum(-1).sum(axis=(0, 2))  # (B, A)
+            loss_att += (kl * ~done).sum() / max(int((~done).sum()), 1) / L
+        else:
+            f = MR.dqnr if name == "dqnr" else MR.commnet
+            q, st = f(Wm, x, state) if name == "dqnr" else f(Wm, x, adj, state)
+            qn, _ = f(Wt, xn, st) if name == "dqnr" else f(Wt, xn, adjn, st)
+            state = st * (~done * ~g["episode_done"][t].astype(bool)[:, None])[..., None]
+        tgt = g["reward"][t] + (~done) * gamma * qn.max(-1)
+        qt = q.copy()
+        np.put_along_axis(qt, g["actions"][t].astype(np.int64)[..., None], tgt[..., None], -1)
+        np.testing.assert_allclose(q, g[f"q_{t}"], atol=1e-5, rtol=0)
+        np.testing.assert_allclose(qt, g[f"qtarget_{t}"], atol=1e-5, rtol=0)
+        loss_q += ((q - qt) ** 2).mean() / L
+    np.testing.assert_allclose(loss_q, g["loss_q"].item(), rtol=1e-5)
+    np.testing.assert_allclose(loss_att, g["loss_att"].item(), rtol=1e-4, atol=1e-9)
+    np.testing.assert_allclose(loss_q + float(g["att_coeff"]) * loss_att, g["loss"].item(), rtol=1e-5)
+    if name == "dgn":
+        assert loss_att > 1e-3  # the fixture exercises the regulariser (perturbed target attention)
+
+
 def test_netmon_global_restatement_matches_reference():
     """--netmon-global readout of the fp64 restatement vs the reference (netmon_global.npz)."""
     g = np.load(os.path.join(R.GOLDEN, "netmon_global.npz"))
