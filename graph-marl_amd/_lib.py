@@ -29,7 +29,7 @@ EXPORTS = [
     "gm_netmon_readout_bwd", "gm_lstm_pointwise", "gm_lstm_pointwise_bwd", "gm_linear_f32", "gm_gemm_f32",
     "gm_simple_create", "gm_simple_destroy", "gm_simple_reset", "gm_simple_step",
     "gm_simple_observe", "gm_simple_policy_egreedy", "gm_simple_get_state", "gm_env_set_topology",
-    "gm_policy_shortest_path", "gm_env_first_hops", "gm_routing_node_encoder", "gm_gemm_x3", "gm_gemm_x3_head", "gm_absmax_scale", "gm_absmax_scale_rows", "gm_gemm_x3_wgrad", "gm_absmax_finish",
+    "gm_policy_shortest_path", "gm_env_first_hops", "gm_routing_node_encoder", "gm_gemm_x3", "gm_gemm_x3_head", "gm_absmax_scale", "gm_absmax_scale_rows", "gm_gemm_x3_wgrad", "gm_gemm_x3_wgrad2", "gm_absmax_finish",
     "gm_gemm_pack_x3", "gm_gemm_pack_x3_bytes", "gm_gemm_range_status",
     "gm_pcg64_seed", "gm_pcg64_choice", "gm_lnlstm_pointwise", "gm_agent_attention", "gm_agent_comm",
     "gm_gemm_x3_dgrad", "gm_lstm_cell_bwd", "gm_qhead_bwd", "gm_netmon_readout_ld", "gm_routing_node_encoder_bits", "gm_gather_records",
@@ -92,6 +92,12 @@ class LSTMBwdArgs(C.Structure):
         ("dc_out", C.c_void_p), ("ld_dco", C.c_int64), ("bias_part", C.c_void_p), ("rows_per_block", C.c_int32),
         ("dg_scale", C.c_void_p), ("dg_max", C.c_void_p),
     ]
+
+
+class WgradSrc(C.Structure):
+    """gm_wgrad_src (include/graph_marl_amd.h): one B source of gm_gemm_x3_wgrad2 with its row map."""
+    _fields_ = [("p", C.c_void_p), ("ld", C.c_int64), ("scale", C.c_void_p), ("period", C.c_int64),
+                ("shift", C.c_int64), ("rows", C.c_int64)]
 
 
 class GMError(RuntimeError):

@@ -2939,13 +2939,20 @@ __global__ __launch_bounds__(256, 2) void k_gemm3_kmajor(const float* __restrict
 // every tile of a k chunk on one XCD (workgroups go to the 8 XCDs round-robin by linear id), so the
 // chunk's A and B rows are fetched into that XCD's L2 once and reused by all its tiles there
 // (identity order: the tiles of a chunk spread over the 8 XCDs and each L2 fetches its own copy)
+struct WgB {  // one K-major B source of k_wgrad_tr (gm_wgrad_src): batch row r reads source row
+                // (period ? r % period : r) + shift, zero outside [0, rows); a k chunk maps to one run of rows
+    const float* p;
+    long long ld;
+    const float* s;
+    long long period, shift, rows;
+};
+
 template <int BN, int MF = 0>
 __global__ __launch_bounds__(256, BN == 128 ? 2 : 1) void k_wgrad_tr(const float* __restrict__ A, long long lda,
-                                                                   unsigned abytes, const float* __restrict__ B,
-                                                                   long long ldb, unsigned bbytes, int M, int N, int K,
-                                                                   int kchunk, const float* __restrict__ sa,
-                                                                   const float* __restrict__ sb, float* __restrict__ C,
-                                                                   long long ldc, long long cz, int xcd) {
+                                                                   unsigned abytes, WgB b1, WgB b2, int nsplit, int M,
+                                                                   int N, int K, int kchunk, const float* __restrict__ sa,
+                                                                   float* __restrict__ C, long long ldc, long long cz,
+                                                                   int xcd) {
     constexpr int BM = 128, BK = 32, TM = 2, TN = BN / 64;
     constexpr int RA = BM * 2 + 64, RB = BN * 2 + 64;  // image row strides (bytes)
     constexpr int LA = BM / 4 * BK / 256, LB = BN / 4 * BK / 256;  // float4 loads per thread
@@ -2963,11 +2970,22 @@ __global__ __launch_bounds__(256, BN == 128 ? 2 : 1) void k_wgrad_tr(const float
     const int m0 = (tile / nN) * BM, n0 = (tile % nN) * BN;
     const int kb = chunk * kchunk, ke = min(K, kb + kchunk);
     const int nk = (ke - kb + BK - 1) / BK;
-    const float s_a = *sa, s_b = *sb;
+    // B source of this tile: output columns [0, nsplit) from b1, [nsplit, N) from b2 (nsplit % BN == 0, so a tile
+    // lies in one source); nb0 / nlim: the tile's first column and the column count inside its source. The k
+    // chunk's batch rows map to source rows brow0 .. brow0 + kchunk - 1 (host: kchunk divides every period and
+    // shift), zero where they fall outside the source
+    const bool sec = n0 >= nsplit;
+    const WgB& bs = sec ? b2 : b1;
+    const int nb0 = sec ? n0 - nsplit : n0, nlim = sec ? N - nsplit : min(N, nsplit);
+    const long long brow0 = (bs.period ? kb % bs.period : kb) + bs.shift;
+    const long long bav = (brow0 < 0 || brow0 >= bs.rows) ? 0 : min((long long)kchunk, bs.rows - brow0);
+    const long long ldb = bs.ld;
+    const float s_a = *sa, s_b = *bs.s;
     const int e_a = __builtin_amdgcn_frexp_expf(s_a) - 1, e_b = __builtin_amdgcn_frexp_expf(s_b) - 1;  // 2^e = scale
     // buffer resources over this block's k chunk only: 32-bit offsets stay small whatever the batch
     // (abytes / bbytes: the bytes of one chunk of rows, host-checked)
-    const __amdgpu_buffer_rsrc_t ra = rsrc(A + (long long)kb * lda, abytes), rb = rsrc(B + (long long)kb * ldb, bbytes);
+    const __amdgpu_buffer_rsrc_t ra = rsrc(A + (long long)kb * lda, abytes),
+                                 rb = rsrc(bs.p + (bav ? brow0 : 0) * ldb, (unsigned)(bav * ldb * 4));
     // loader map: A tile 32 k x 128 m = 32 float4 per k row -> lane q = tid & 31 (m = 4q), rows
     // (tid >> 5) + 8 j; B tile 32 x BN: BN / 4 float4 per row
     constexpr int QB = BN / 4, RB_STEP = 256 / QB;
@@ -2987,8 +3005,8 @@ __global__ __launch_bounds__(256, BN == 128 ? 2 : 1) void k_wgrad_tr(const float
         }
 #pragma unroll
         for (int j = 0; j < LB; j++) {
-            const int k = k0 + kb0 + RB_STEP * j, n = n0 + 4 * qb;
-            const int off = (k < ke && n < N) ? (int)(((long long)(k - kb) * ldb + n) * 4) : OOB;
+            const int k = k0 + kb0 + RB_STEP * j, n = nb0 + 4 * qb;
+            const int off = (k < ke && n < nlim) ? (int)(((long long)(k - kb) * ldb + n) * 4) : OOB;
             vb[S][j] = bload(rb, off);
         }
     };
@@ -3178,46 +3196,71 @@ __global__ __launch_bounds__(256, BN == 128 ? 2 : 1) void k_wgrad_tr(const float
 int g_wgrad = -1;  // weight-gradient kernel: -1 / 1 transposed reads 128 x 128 (default), 2 the same 128 x 256, 0 dword form
 int g_wgrad_xcd = 1;  // XCD-grouped k chunks (k_wgrad_tr xcd), when the grid is a multiple of 8
 
-extern "C" int gm_gemm_x3_wgrad(const float* a, int64_t lda, const float* b, int64_t ldb, int32_t m, int32_t n, int32_t k,
-                                int32_t kchunk, const float* sa, const float* sb, float* c, int64_t ldc, void* stream) {
-    if (!a || !b || !sa || !sb || !c || m <= 0 || n <= 0 || k <= 0 || kchunk <= 0 || (kchunk % 16) || (m % 4) ||
-        (n % 4) || lda < m || ldb < n || (lda % 4) || (ldb % 4) || ldc < n || (reinterpret_cast<uintptr_t>(a) & 15) ||
-        (reinterpret_cast<uintptr_t>(b) & 15))
-        return gm_fail(GM_ERR_INVALID_ARG, "gm_gemm_x3_wgrad: bad arguments (m, n, ld multiples of 4, 16-B bases, "
-                                           "kchunk % 16 == 0)");
+// launcher of both entry points: n1 columns from source 1, n2 from source 2 (n2 = 0: none)
+static int wgrad_launch(const float* a, int64_t lda, const gm_wgrad_src& s1, int32_t n1, const gm_wgrad_src* s2,
+                        int32_t n2, int32_t m, int32_t k, int32_t kchunk, const float* sa, float* c, int64_t ldc,
+                        void* stream, const char* what) {
+    const int n = n1 + n2;
+    auto src_ok = [&](const gm_wgrad_src& b, int nb) {
+        return b.p && b.scale && nb > 0 && (nb % 4) == 0 && b.ld >= nb && (b.ld % 4) == 0 &&
+               !(reinterpret_cast<uintptr_t>(b.p) & 15) && b.period >= 0 && b.rows > 0 &&
+               (b.period == 0 || b.period % kchunk == 0) && (b.shift % kchunk) == 0;
+    };
+    if (!a || !sa || !c || m <= 0 || n1 <= 0 || n2 < 0 || k <= 0 || kchunk <= 0 || (kchunk % 16) || (m % 4) ||
+        lda < m || (lda % 4) || ldc < n || (reinterpret_cast<uintptr_t>(a) & 15) || !src_ok(s1, n1) ||
+        (n2 > 0 && (!s2 || !src_ok(*s2, n2))))
+        return gm_fail(GM_ERR_INVALID_ARG, std::string(what) + ": bad arguments (m, n, ld multiples of 4, 16-B bases, "
+                                                               "kchunk % 16 == 0 and dividing every period / shift)");
     const int S = (k + kchunk - 1) / kchunk;
+    const bool plain = n2 == 0 && s1.period == 0 && s1.shift == 0;
+    if (!plain && (g_wgrad == 0 || g_wgrad == 2 || (n2 > 0 && n1 % 128)))
+        return gm_fail(GM_ERR_UNSUPPORTED, std::string(what) + ": two sources / row maps need the 128-column "
+                                                               "transposed-read forms and n1 % 128 == 0");
     if (g_wgrad == 0) {
         const int T = ((m + 127) / 128) * ((n + 127) / 128);
-        hipLaunchKernelGGL(k_gemm3_kmajor, dim3(T, S), dim3(256), 0, (hipStream_t)stream, a, (long long)lda, b,
-                           (long long)ldb, m, n, k, kchunk, sa, sb, c, (long long)ldc, (long long)m * ldc);
+        hipLaunchKernelGGL(k_gemm3_kmajor, dim3(T, S), dim3(256), 0, (hipStream_t)stream, a, (long long)lda, s1.p,
+                           (long long)s1.ld, m, n, k, kchunk, sa, s1.scale, c, (long long)ldc, (long long)m * ldc);
     } else {
         // per-block buffer resources cover one k chunk (any batch size; a chunk below 2 GB)
         const long long kc = std::min<long long>(kchunk, k);
-        const long long ab = kc * lda * 4, bb = kc * ldb * 4;
-        if (ab >= 0x7ff00000LL || bb >= 0x7ff00000LL)
-            return gm_fail(GM_ERR_UNSUPPORTED, "gm_gemm_x3_wgrad: one k chunk of an operand larger than 2 GB");
+        const long long ab = kc * lda * 4;
+        if (ab >= 0x7ff00000LL || kc * s1.ld * 4 >= 0x7ff00000LL || (n2 > 0 && kc * s2->ld * 4 >= 0x7ff00000LL))
+            return gm_fail(GM_ERR_UNSUPPORTED, std::string(what) + ": one k chunk of an operand larger than 2 GB");
+        const WgB w1{s1.p, s1.ld, s1.scale, s1.period, s1.shift, s1.rows};
+        const WgB w2 = n2 > 0 ? WgB{s2->p, s2->ld, s2->scale, s2->period, s2->shift, s2->rows} : w1;
         const int T128 = ((m + 127) / 128) * ((n + 127) / 128);
         const int xcd = g_wgrad_xcd && (T128 * S) % 8 == 0;
         if (g_wgrad == 3) {  // 16x16x32 MFMA
-            const int T = T128;
-            hipLaunchKernelGGL((k_wgrad_tr<128, 1>), dim3(T, S), dim3(256), 0, (hipStream_t)stream, a, (long long)lda,
-                               (unsigned)ab, b, (long long)ldb, (unsigned)bb, m, n, k, kchunk, sa, sb, c, (long long)ldc,
+            hipLaunchKernelGGL((k_wgrad_tr<128, 1>), dim3(T128, S), dim3(256), 0, (hipStream_t)stream, a,
+                               (long long)lda, (unsigned)ab, w1, w2, n1, m, n, k, kchunk, sa, c, (long long)ldc,
                                (long long)m * ldc, xcd);
         } else if (g_wgrad != 2) {  // 128 x 128 tiles at 2 blocks/CU: 8-24 % faster than 128 x 256 at 1 block/CU
-            const int T = T128;
-            hipLaunchKernelGGL(k_wgrad_tr<128>, dim3(T, S), dim3(256), 0, (hipStream_t)stream, a, (long long)lda,
-                               (unsigned)ab, b, (long long)ldb, (unsigned)bb, m, n, k, kchunk, sa, sb, c, (long long)ldc,
-                               (long long)m * ldc, xcd);
+            hipLaunchKernelGGL(k_wgrad_tr<128>, dim3(T128, S), dim3(256), 0, (hipStream_t)stream, a, (long long)lda,
+                               (unsigned)ab, w1, w2, n1, m, n, k, kchunk, sa, c, (long long)ldc, (long long)m * ldc,
+                               xcd);
         } else {
             const int T = ((m + 127) / 128) * ((n + 255) / 256);
             hipLaunchKernelGGL(k_wgrad_tr<256>, dim3(T, S), dim3(256), 0, (hipStream_t)stream, a, (long long)lda,
-                               (unsigned)ab, b, (long long)ldb, (unsigned)bb, m, n, k, kchunk, sa, sb, c, (long long)ldc,
-                               (long long)m * ldc, (int)(g_wgrad_xcd && (T * S) % 8 == 0));
+                               (unsigned)ab, w1, w2, n1, m, n, k, kchunk, sa, c, (long long)ldc, (long long)m * ldc,
+                               (int)(g_wgrad_xcd && (T * S) % 8 == 0));
         }
     }
     hipError_t e = hipGetLastError();
-    if (e != hipSuccess) return gm_fail(GM_ERR_HIP, std::string("gm_gemm_x3_wgrad: ") + hipGetErrorString(e));
+    if (e != hipSuccess) return gm_fail(GM_ERR_HIP, std::string(what) + ": " + hipGetErrorString(e));
     return GM_OK;
+}
+
+extern "C" int gm_gemm_x3_wgrad(const float* a, int64_t lda, const float* b, int64_t ldb, int32_t m, int32_t n, int32_t k,
+                                int32_t kchunk, const float* sa, const float* sb, float* c, int64_t ldc, void* stream) {
+    const gm_wgrad_src s1{b, ldb, sb, 0, 0, k};
+    return wgrad_launch(a, lda, s1, n, nullptr, 0, m, k, kchunk, sa, c, ldc, stream, "gm_gemm_x3_wgrad");
+}
+
+extern "C" int gm_gemm_x3_wgrad2(const float* a, int64_t lda, const gm_wgrad_src* b1, int32_t n1, const gm_wgrad_src* b2,
+                                 int32_t n2, int32_t m, int32_t k, int32_t kchunk, const float* sa, float* c, int64_t ldc,
+                                 void* stream) {
+    if (!b1) return gm_fail(GM_ERR_INVALID_ARG, "gm_gemm_x3_wgrad2: no first source");
+    return wgrad_launch(a, lda, *b1, n1, b2, b2 ? n2 : 0, m, k, kchunk, sa, c, ldc, stream, "gm_gemm_x3_wgrad2");
 }
 
 extern "C" int64_t gm_gemm_pack_x3_bytes(int32_t n, int32_t k) {

@@ -58,6 +58,8 @@ def _setup():
         lib.gm_absmax_scale_rows.argtypes = [vp, C.c_int64, C.c_int32, C.c_int64, vp, vp]
         lib.gm_gemm_x3_wgrad.argtypes = [vp, C.c_int64, vp, C.c_int64, C.c_int32, C.c_int32, C.c_int32, C.c_int32,
                                          vp, vp, vp, C.c_int64, vp]
+        lib.gm_gemm_x3_wgrad2.argtypes = [vp, C.c_int64, C.POINTER(L.WgradSrc), C.c_int32, C.POINTER(L.WgradSrc),
+                                          C.c_int32, C.c_int32, C.c_int32, C.c_int32, vp, vp, C.c_int64, vp]
         lib.gm_gemm_x3_head.argtypes = [C.POINTER(ASrc), vp, vp, vp, C.c_int32, C.c_int32, C.c_int32, vp, C.c_int64,
                                         vp, C.c_int32, vp, C.c_int64, vp, C.c_int64, vp]
         lib.gm_gemm_x3_dgrad.argtypes = [C.POINTER(ASrc), vp, vp, C.c_int32, C.c_int32, C.c_int32, vp, C.c_int64, vp,

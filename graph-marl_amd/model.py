@@ -227,14 +227,77 @@ def _wgrad(gy, x, k, sa=None, sb=None):
         # scale from the k real columns; the up to 3 padding columns only reach output columns >= k
         sb = torch.empty(1, device=dev)
         L.check(lib.gm_absmax_scale_rows(x.data_ptr(), Mb, k, ldx, sb.data_ptr(), L.stream_ptr()))
-    tiles = ((o + 127) // 128) * ((N + 127) // 128)
-    splits = max(1, min(Mb // 2048, (1024 + tiles - 1) // tiles))
-    kchunk = ((Mb + splits - 1) // splits + 31) // 32 * 32  # the kernel's k tile is 32 deep
-    splits = (Mb + kchunk - 1) // kchunk
+    kchunk, splits = _wgrad_chunk(Mb, ((o + 127) // 128) * ((N + 127) // 128))
     part = torch.empty(splits, o, N, device=dev)
     L.check(lib.gm_gemm_x3_wgrad(gy.data_ptr(), o, x.data_ptr(), ldx, o, N, Mb, kchunk, sa.data_ptr(), sb.data_ptr(),
                                  part.data_ptr(), N, L.stream_ptr()))
     return part.sum(0)[:, :k]
+
+
+def _wgrad_chunk(Mb, tiles, period=0):
+    """Split-K plan of the weight-gradient kernel: (kchunk, splits). About 1024 blocks (two rounds of the 512
+    resident 128 x 128 blocks; rounding the split count DOWN, so no partial third round), k chunks a multiple
+    of the 32-deep k tile and, with a row map (period > 0), dividing the period."""
+    splits = max(1, min(Mb // 2048, 1024 // max(1, tiles)))
+    while splits > 1 and (tiles * splits) % 8:  # XCD-grouped chunks need tiles * splits % 8 == 0
+        splits -= 1
+    q = -(-(-(-Mb // splits)) // 32)  # ceil(ceil(Mb / splits) / 32)
+    if period:
+        if period % 32:
+            return None, None
+        while (period // 32) % q:
+            q += 1
+    kchunk = 32 * q
+    return kchunk, -(-Mb // kchunk)
+
+
+def _wgrad2(gy, srcs, sa):
+    """Weight gradients gy^T @ x[:, :k] of one or two K-major sources that share the gradient operand gy, in ONE
+    split-K launch (gm_gemm_x3_wgrad2: gy is read once per k chunk for both): srcs = [(x, k, sb, period, shift),
+    ...] with sb the source's operand scale and the row map of gm_wgrad_src (batch row r reads x row (period ? r
+    % period : r) + shift, zero outside x; period / shift 0: plain). The first source's k must be a multiple of
+    128 when a second is given. Returns the gradients; None when the shapes do not fit the kernel (the caller
+    then runs _wgrad per source)."""
+    from . import fused as FU
+
+    Mb, o = gy.shape
+    gy = gy.contiguous()
+    Ns = [(k + 3) // 4 * 4 for _, k, _, _, _ in srcs]
+    ok = (Mb >= 4096 and o % 4 == 0 and gy.data_ptr() % 16 == 0 and len(srcs) in (1, 2)
+          and (len(srcs) == 1 or srcs[0][1] % 128 == 0))
+    for (x, k, _, _, _), N in zip(srcs, Ns):
+        ok = ok and FU.use_x3(k) and N <= x.stride(0) and x.stride(0) % 4 == 0 and x.stride(1) == 1 \
+            and x.data_ptr() % 16 == 0
+    if not ok:
+        return None
+    N = sum(Ns)
+    tiles = ((o + 127) // 128) * ((N + 127) // 128)
+    period = 0
+    for _, _, _, per, sh in srcs:
+        period = per or period
+        if sh:
+            period = period or abs(sh)
+    kchunk, splits = _wgrad_chunk(Mb, tiles, period)
+    if kchunk is None or any((per and per % kchunk) or (sh % kchunk) for _, _, _, per, sh in srcs):
+        return None
+    lib = FU._setup()
+    part = torch.empty(splits, o, N, device=gy.device)
+    spec = [L.WgradSrc(x.data_ptr(), x.stride(0), sb.data_ptr(), per, sh, x.shape[0]) for x, _, sb, per, sh in srcs]
+    L.check(lib.gm_gemm_x3_wgrad2(gy.data_ptr(), o, C.byref(spec[0]), Ns[0],
+                                  C.byref(spec[1]) if len(spec) > 1 else None, Ns[1] if len(spec) > 1 else 0, o, Mb,
+                                  kchunk, sa.data_ptr(), part.data_ptr(), N, L.stream_ptr()))
+    tot = part.sum(0)
+    out, c0 = [], 0
+    for (_, k, _, _, _), n in zip(srcs, Ns):
+        out.append(tot[:, c0:c0 + k])
+        c0 += n
+    return out
+
+
+def _wgrad_pair(gy, x1, k1, x2, k2, sa, sb1, sb2):
+    """(gy^T x1[:, :k1], gy^T x2[:, :k2]) in one launch when possible (_wgrad2), else two _wgrad calls."""
+    r = _wgrad2(gy, [(x1, k1, sb1, 0, 0), (x2, k2, sb2, 0, 0)], sa)
+    return tuple(r) if r is not None else (_wgrad(gy, x1, k1, sa, sb1), _wgrad(gy, x2, k2, sa, sb2))
 
 
 class LinearFn(torch.autograd.Function):

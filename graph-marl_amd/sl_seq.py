@@ -233,12 +233,17 @@ def _backward(p, dR):
     sa_obs, sa_upd = TS._finish(gmax_obs), TS._finish(gmax_upd)
     E = p.enc_out[-1]
     cell = netmon.rnn_obs
-    # W_ih: every step's x is the same encoder output E
-    gw = None
-    for t in range(Ls):
-        w_t = TS._wgrad(dG[0, t], sa_obs, E, H, p.s_obs)
-        gw = w_t if gw is None else gw.add_(w_t)
-    grads[cell.weight_ih] = gw
+    # W_ih: every step's x is the same encoder output E: ONE launch over all L steps' gate gradients with E's
+    # rows repeated (row map period M), instead of L launches of M rows (each at ~0.35 of the large-batch rate)
+    r = TS.MD._wgrad2(dG[0].reshape(Ls * M, 4 * H), [(E, H, p.s_obs, M, 0)], sa_obs) if Ls > 1 else None
+    if r is not None:
+        grads[cell.weight_ih] = r[0]
+    else:
+        gw = None
+        for t in range(Ls):
+            w_t = TS._wgrad(dG[0, t], sa_obs, E, H, p.s_obs)
+            gw = w_t if gw is None else gw.add_(w_t)
+        grads[cell.weight_ih] = gw
     # W_hh: step 0's h is zero; step t's is S[K, t-1] (contiguous over t = 1..L-1)
     if Ls > 1:
         grads[cell.weight_hh] = TS._wgrad(dG[0, 1:].reshape(-1, 4 * H), sa_obs, S[K, :Ls - 1].reshape(-1, S2), H,
@@ -250,8 +255,9 @@ def _backward(p, dR):
     grads[cell.bias_hh] = bg.clone()
     cell = netmon.rnn_update
     gs = dG[1:].reshape(-1, 4 * H)
-    grads[cell.weight_ih] = TS._wgrad(gs, sa_upd, p.agg.reshape(K * Ls * M, H), H, p.s_upd)
-    grads[cell.weight_hh] = TS._wgrad(gs, sa_upd, S[:K].reshape(K * Ls * M, S2), H, p.s_upd)
+    grads[cell.weight_ih], grads[cell.weight_hh] = TS.MD._wgrad_pair(gs, p.agg.reshape(K * Ls * M, H), H,
+                                                                  S[:K].reshape(K * Ls * M, S2), H, sa_upd, p.s_upd,
+                                                                  p.s_upd)
     bg = bpart[1:].reshape(-1, 4 * H).sum(0)
     grads[cell.bias_ih] = bg
     grads[cell.bias_hh] = bg.clone()

@@ -339,7 +339,8 @@ def _backward(p, dq):
         g, sc = gn, _finish(gmax)
     lin0 = dl[0]
     s_in0 = p.d_in_scale[0]
-    grads[lin0.weight] = torch.cat([_wgrad(g, sc, p.env, od, s_in0), _wgrad(g, sc, p.R, 4 * H, s_in0)], 1)
+    w_r, w_env = MD._wgrad_pair(g, p.R, 4 * H, p.env, od, sc, s_in0, s_in0)  # one launch: g read once per k chunk
+    grads[lin0.weight] = torch.cat([w_env, w_r], 1)
     dR = torch.empty(LMa, 4 * H, device=dev)
     _dgrad(g, lin0.out_features, lin0.out_features, sc, _lin_x3t(lin0, slice(od, od + 4 * H)), LMa, 4 * H, 4 * H,
            None, 0, dR, 4 * H)
@@ -425,8 +426,7 @@ def _backward(p, dq):
                                        p.S[:K].reshape(K * LM, S2))):
         gs = dG[j0:j0 + (1 if j0 == 0 else K)].reshape(-1, 4 * H)
         sa = _finish(gm_)
-        grads[cell.weight_ih] = _wgrad(gs, sa, xs, H, sx)
-        grads[cell.weight_hh] = _wgrad(gs, sa, hs, H, sx)
+        grads[cell.weight_ih], grads[cell.weight_hh] = MD._wgrad_pair(gs, xs, H, hs, H, sa, sx, sx)
         bg = bpart[j0:j0 + (1 if j0 == 0 else K)].reshape(-1, 4 * H).sum(0)
         grads[cell.bias_ih] = bg
         grads[cell.bias_hh] = bg.clone()

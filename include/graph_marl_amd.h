@@ -26,7 +26,7 @@
  *   gm_gemm_x3 / gm_gemm_pack_x3     the same GEMMs in split-f16 form (f16 MFMA, fp32 accumulate)
  *   gm_gemm_x3_head                  last DQN layer + Q head in one kernel
  *   gm_absmax_scale(_rows/_finish)   power-of-two operand scale for gm_gemm_x3 (input gradients)
- *   gm_gemm_x3_wgrad                 split-K weight-gradient GEMM over K-major operands
+ *   gm_gemm_x3_wgrad(2)              split-K weight-gradient GEMM over K-major operands (two B sources)
  *   gm_gemm_x3_dgrad / gm_lstm_cell_bwd / gm_qhead_bwd   backward of Linear+leaky_relu, LSTMCell and
  *                                    Q_Net.fc (torch autograd of the update, src/main.py:996)
  *   gm_agent_attention               AttModel attention core (DGN)          src/model.py:86-117
@@ -453,6 +453,24 @@ int gm_gemm_x3_dgrad(const gm_a_src* src0, const void* wp, const float* wscale_i
  * gradients of the reference's Linear / LSTMCell layers (torch autograd, src/main.py:840-1026). */
 int gm_gemm_x3_wgrad(const float* a, int64_t lda, const float* b, int64_t ldb, int32_t m, int32_t n, int32_t k,
                      int32_t kchunk, const float* sa, const float* sb, float* c, int64_t ldc, void* stream);
+/* One K-major B source of gm_gemm_x3_wgrad2: n columns of p (row stride ld floats, 16-byte base), operand scale
+ * (device power of two, as sb); batch row r of a reads source row (period ? r % period : r) + shift, and zeros
+ * where that row lies outside [0, rows) (period / shift: multiples of kchunk). E.g. the config-5 obs cell, whose
+ * input x = E [M][H] is the same at every one of the L steps: period = M; its h input of step t is step t-1's
+ * state [(L-1) M rows]: shift = -M (zero at t = 0). */
+typedef struct {
+    const float* p;
+    int64_t ld;
+    const float* scale;
+    int64_t period, shift, rows;
+} gm_wgrad_src;
+/* The weight gradients of two B sources that share the gradient operand a, in ONE launch: c = a^T [b1 | b2]
+ * (n1 columns of b1, n2 of b2; b2 nullable), split-K partials [k / kchunk][m][ldc >= n1 + n2]; each k chunk of a
+ * is fetched once into the XCD's L2 for both (the LSTM cell's W_ih / W_hh, the DQN's first layer over [readout |
+ * env obs]). n1 % 128 == 0 when b2 is given. */
+int gm_gemm_x3_wgrad2(const float* a, int64_t lda, const gm_wgrad_src* b1, int32_t n1, const gm_wgrad_src* b2,
+                      int32_t n2, int32_t m, int32_t k, int32_t kchunk, const float* sa, float* c, int64_t ldc,
+                      void* stream);
 /* s = 2^(14 - e) with max|x| in [2^(e-1), 2^e) (1 when x is all zero): the power-of-two scale
  * that brings a gm_gemm_x3 A operand of small magnitude (e.g. gradients) into the range where
  * both f16 pieces of the split are normal. x: n floats; scale: one device float. */

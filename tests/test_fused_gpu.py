@@ -1,6 +1,7 @@
 """GPU parity of the fused GEMM path (gm_gemm_f32): dense/ragged GEMMs and the LSTM
 epilogue vs torch fp32, the fused NetMon step and DQN readout-gather vs the unfused
 (golden-validated) path, and the reference goldens through the fused path."""
+import ctypes as C
 import importlib
 
 import numpy as np
@@ -298,6 +299,70 @@ def test_weight_gradient_kmajor(Mb, o, k, ldx, mag):
             assert rel < 4e-6, (form, rel)
     finally:
         lib.gm_gemm_set_wgrad(-1)
+
+
+@pytest.mark.parametrize("Mb,o,k1,ld1,k2,ld2", [(131072, 512, 128, 128, 128, 256), (65536, 512, 512, 512, 130, 132),
+                                               (20001, 256, 128, 256, 256, 256)])
+def test_weight_gradient_two_sources(Mb, o, k1, ld1, k2, ld2):
+    """gm_gemm_x3_wgrad2 (round 6): the two weight gradients that share a gradient operand (LSTM W_ih / W_hh on
+    [x] and the h half of the [h | c] state rows, DQN layer 1 on [readout | env obs]) from ONE launch, each with
+    its own operand scale: fp32-order error vs fp64 like gm_gemm_x3_wgrad, on both 128-column forms."""
+    gm, M_, FU, W = mods()
+    torch.manual_seed(Mb + k2)
+    gy = torch.randn(Mb, o, device="cuda") * 1e-5
+    x1 = torch.randn(Mb, ld1, device="cuda")
+    x2 = torch.randn(Mb, ld2, device="cuda") * 3e-3
+    s = [torch.empty(1, device="cuda") for _ in range(3)]
+    lib = FU._setup()
+    L = FU.L
+    L.check(lib.gm_absmax_scale(gy.data_ptr(), gy.numel(), s[0].data_ptr(), L.stream_ptr()))
+    L.check(lib.gm_absmax_scale_rows(x1.data_ptr(), Mb, k1, ld1, s[1].data_ptr(), L.stream_ptr()))
+    L.check(lib.gm_absmax_scale_rows(x2.data_ptr(), Mb, k2, ld2, s[2].data_ptr(), L.stream_ptr()))
+    try:
+        for form in (-1, 3):
+            lib.gm_gemm_set_wgrad(form)
+            r = M_._wgrad2(gy, [(x1, k1, s[1], 0, 0), (x2, k2, s[2], 0, 0)], s[0])
+            assert r is not None
+            for got, x, k in zip(r, (x1, x2), (k1, k2)):
+                assert got.shape == (o, k)
+                ref = gy.double().t() @ x[:, :k].double()
+                mag = gy.abs().double().t() @ x[:, :k].abs().double()
+                rel = ((got.double() - ref).abs() / mag.clamp_min(1e-300)).max().item()
+                assert rel < 4e-6, (form, k, rel)
+    finally:
+        lib.gm_gemm_set_wgrad(-1)
+    bad = L.WgradSrc(x1.data_ptr(), ld1, s[1].data_ptr(), 0, 0, Mb)  # n1 = 100: a column tile would straddle
+    assert lib.gm_gemm_x3_wgrad2(gy.data_ptr(), o, C.byref(bad), 100, C.byref(bad), 4, o, Mb, 4096, s[0].data_ptr(),
+                                 gy.data_ptr(), 104, None) != 0
+
+
+def test_weight_gradient_row_maps():
+    """gm_wgrad_src row maps (round 6, config 5): the obs cell's x is the same encoder output E [M][H] at every one
+    of L steps, so W_ih's gradient over all L steps' gate gradients reads E with period M in ONE launch; W_hh's
+    reads step t-1's state (shift -M, zero at t = 0). Both against fp64 sums over the steps."""
+    gm, M_, FU, W = mods()
+    Ls, M, H, o = 4, 20480, 128, 512
+    torch.manual_seed(3)
+    dG = torch.randn(Ls * M, o, device="cuda") * 1e-4
+    E = torch.randn(M, H, device="cuda")
+    Sprev = torch.randn((Ls - 1) * M, 2 * H, device="cuda")  # states of steps 0..L-2, [h | c] rows
+    s = [torch.empty(1, device="cuda") for _ in range(3)]
+    lib = FU._setup()
+    L = FU.L
+    L.check(lib.gm_absmax_scale(dG.data_ptr(), dG.numel(), s[0].data_ptr(), L.stream_ptr()))
+    L.check(lib.gm_absmax_scale_rows(E.data_ptr(), M, H, H, s[1].data_ptr(), L.stream_ptr()))
+    L.check(lib.gm_absmax_scale_rows(Sprev.data_ptr(), (Ls - 1) * M, H, 2 * H, s[2].data_ptr(), L.stream_ptr()))
+    r = M_._wgrad2(dG, [(E, H, s[1], M, 0), (Sprev, H, s[2], 0, -M)], s[0])
+    assert r is not None
+    d64 = dG.double().view(Ls, M, o)
+    ref_ih = sum(d64[t].t() @ E.double() for t in range(Ls))
+    mag_ih = sum(d64[t].abs().t() @ E.abs().double() for t in range(Ls))
+    hp = Sprev[:, :H].double().view(Ls - 1, M, H)
+    ref_hh = sum(d64[t].t() @ hp[t - 1] for t in range(1, Ls))
+    mag_hh = sum(d64[t].abs().t() @ hp[t - 1].abs() for t in range(1, Ls))
+    for got, ref, mag in ((r[0], ref_ih, mag_ih), (r[1], ref_hh, mag_hh)):
+        rel = ((got.double() - ref).abs() / mag.clamp_min(1e-300)).max().item()
+        assert rel < 4e-6, rel
 
 
 @pytest.mark.parametrize("rows,k,n,act", [(8192, 642, 512, 1), (5000, 256, 128, 1), (4096, 512, 4, 0),

