@@ -1746,6 +1746,15 @@ __global__ __launch_bounds__(WGM* WGN * 64, OCC) void k_gemm3g(ASrc a0, ASrc a1,
         cin_load<TM, EPI>(cin, ep, m0 + wr * TM * 32, n0 + wc * TN * 32, M, lane);
     floatx16 acc[TM][TN];
     floatx4 acc4[2 * TM][2 * TN];
+    // LOACC (ping-pong loop, not the chain: it would spill): the a_lo' w_hi products in their own accumulators
+    constexpr bool LOACC = MF == 1 && NW == 8 && STAGES <= 3 && EPI != EPI_CHAIN;
+    floatx4 acc4l[LOACC ? 2 * TM : 1][LOACC ? 2 * TN : 1];
+#pragma unroll
+    for (int i = 0; i < (LOACC ? 2 * TM : 1); i++)
+#pragma unroll
+        for (int j = 0; j < (LOACC ? 2 * TN : 1); j++)
+#pragma unroll
+            for (int r = 0; r < 4; r++) acc4l[i][j][r] = 0.f;
 #pragma unroll
     for (int i = 0; i < TM; i++)
 #pragma unroll
@@ -1841,6 +1850,18 @@ __global__ __launch_bounds__(WGM* WGN * 64, OCC) void k_gemm3g(ASrc a0, ASrc a1,
         constexpr int sb = decltype(SB)::value;
 #pragma unroll
         for (int j = 0; j < TN; j++) {
+            if constexpr (LOACC) {
+            // a_lo' w_hi (scaled 2^12 by the split) into its own accumulators, scaled once after the k loop:
+            // no per-tile w_hi * 2^-12 VALU
+#pragma unroll
+            for (int i = 0; i < 2 * TM; i++) {
+                floatx4& c = acc4[i][sb * TN + j];
+                floatx4& cl4 = acc4l[i][sb * TN + j];
+                cl4 = __builtin_amdgcn_mfma_f32_16x16x32_f16(cl[i], f.bh[j], cl4, 0, 0, 0);
+                c = __builtin_amdgcn_mfma_f32_16x16x32_f16(ch[i], f.bl[j], c, 0, 0, 0);
+                c = __builtin_amdgcn_mfma_f32_16x16x32_f16(ch[i], f.bh[j], c, 0, 0, 0);
+            }
+            } else {
             const half8 bs = f.bh[j] * s12;  // w_hi * 2^-12, exact
 #pragma unroll
             for (int i = 0; i < 2 * TM; i++) {
@@ -1848,6 +1869,7 @@ __global__ __launch_bounds__(WGM* WGN * 64, OCC) void k_gemm3g(ASrc a0, ASrc a1,
                 c = __builtin_amdgcn_mfma_f32_16x16x32_f16(cl[i], bs, c, 0, 0, 0);
                 c = __builtin_amdgcn_mfma_f32_16x16x32_f16(ch[i], f.bl[j], c, 0, 0, 0);
                 c = __builtin_amdgcn_mfma_f32_16x16x32_f16(ch[i], f.bh[j], c, 0, 0, 0);
+            }
             }
         }
     };
@@ -2071,6 +2093,14 @@ __global__ __launch_bounds__(WGM* WGN * 64, OCC) void k_gemm3g(ASrc a0, ASrc a1,
         if (lane == 0) gm_amax_publish(a0.amax, amx);
     }
     const float si = wsi0 / ascale;  // undo the weight and A scales (powers of two: exact)
+    if constexpr (LOACC) {
+#pragma unroll
+        for (int i = 0; i < 2 * TM; i++)
+#pragma unroll
+            for (int j = 0; j < 2 * TN; j++)
+#pragma unroll
+                for (int r = 0; r < 4; r++) acc4[i][j][r] += acc4l[i][j][r] * (1.0f / LO_S);
+    }
     if constexpr (MF == 1) {
 #pragma unroll
         for (int i = 0; i < 2 * TM; i++)

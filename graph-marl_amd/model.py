@@ -12,6 +12,7 @@ checkpoints load unchanged. The forward arithmetic runs in libgraphmarl_amd:
 Backward passes use the matching HIP backward kernels; weight/input gradients of
 the dense layers use library GEMMs (torch.mm -> hipBLASLt).
 """
+import ctypes as C
 import math
 
 import torch

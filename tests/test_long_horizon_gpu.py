@@ -49,9 +49,11 @@ CASES = [(20, 4096, 50, 120, "lstm", "leaky_relu", True), (10, 512, 30, 70, "lst
          (20, 512, 30, 70, "lstm", "leaky_relu", True, 2, "mean")]  # --netmon-agg-type mean
 # LN-LSTM: the GPU must stay within ENVELOPE_X times the fp32 restatement's own drift from fp64 so far
 # (floor ENVELOPE_FLOOR), never above ENVELOPE_CAP (measured 1.9e-3 state / 1.4e-3 readout for the fp32 restatement
-# over 120 steps, GPU 1.6e-3 / 6.2e-4). Round 6: 1.5x and 3e-3 instead
-# of 4x and 8e-3, which a 4x regression would have passed
-ENVELOPE_X = 1.5
+# over 120 steps, GPU 1.6e-3 / 6.2e-4). Round 6: 2x and 3e-3 instead
+# of 4x and 8e-3, which a 4x regression would have passed. 1.5x was tried: the GPU is a second fp32
+# evaluation whose error vs fp64 reached 0.96x (split form) and 1.6x (f32 form, step 22: readout 3.1e-5
+# against a restatement drift of 1.9e-5) of the restatement's own drift
+ENVELOPE_X = 2.0
 ENVELOPE_CAP = 3e-3
 # floor of the envelope: in the first steps the fp32 restatement's own drift is ~1e-5 and the GPU's error is another
 # draw of the same size (a first 1.5x run failed at step 7 with 1.76e-5 against 1.5 x 1.0e-5)
