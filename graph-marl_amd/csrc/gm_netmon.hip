@@ -753,6 +753,36 @@ __global__ __launch_bounds__(256) void k_readout_bwd_cs(const float* __restrict_
     }
 }
 
+// Readout backward without an agent map (every node reads itself out: config 5's all-nodes readout,
+// src/sl.py:132-168): row v of dout is [dh_final(v) | dh_prev(nbr(v, 0)) | ... ], so dhf(u) is row u's
+// segment 0 and dhp(u) = sum over the neighbours v of u, ascending, of row v's segment 1 + (slot of u in v's
+// ascending list) (symmetric adjacency: u is in v's list once). A gather per (node, 16-B chunk) instead of the
+// per-graph LDS staging of k_readout_bwd_cs; the same ascending-row order, so the same fp32 sums
+__global__ __launch_bounds__(256) void k_readout_bwd_nodes(const float* __restrict__ dout, long long stride,
+                                                           const int32_t* __restrict__ nbr, long long nodes, int N,
+                                                           int deg, int H, float* __restrict__ dhf,
+                                                           float* __restrict__ dhp) {
+    const int C4 = H >> 2;
+    const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= nodes * C4) return;
+    const long long u = t / C4;
+    const int c = (int)(t - u * C4);
+    const long long g0 = (u / N) * N;
+    const int ul = (int)(u - g0);
+    if (dhf) *reinterpret_cast<float4*>(dhf + u * H + 4 * c) = *reinterpret_cast<const float4*>(dout + u * stride + 4 * c);
+    if (!dhp) return;
+    float4 ap = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int k = 0; k < deg; k++) {
+        const int v = nbr[u * deg + k];
+        if (v < 0 || v >= N) continue;
+        int slot = -1;
+        for (int j = 0; j < deg; j++)
+            if (nbr[(g0 + v) * deg + j] == ul) slot = j;
+        if (slot >= 0) ap = f4add(ap, *reinterpret_cast<const float4*>(dout + (g0 + v) * stride + (1 + slot) * H + 4 * c));
+    }
+    *reinterpret_cast<float4*>(dhp + u * H + 4 * c) = ap;
+}
+
 extern "C" int gm_netmon_readout_ld(const float* hf, int64_t ldf, const float* hp, int64_t ldp, const int32_t* nbr,
                                     const int32_t* agent_node, int32_t G, int32_t N, int32_t R, int32_t deg, int32_t H,
                                     float* out, int64_t stride, void* stream) {
@@ -834,6 +864,12 @@ extern "C" int gm_netmon_readout_bwd(const float* dout, int64_t stride, const in
     int V = vec_width(H, stride, dout);
     if (dhf) { int v = vec_width(H, H, dhf); V = V < v ? V : v; }
     if (dhp) { int v = vec_width(H, H, dhp); V = V < v ? V : v; }
+    if (!agent_node && R == N && V == 4 && deg <= MAXDEG) {  // every node read out: a gather per node
+        const long long total = (long long)G * N * (H / 4);
+        hipLaunchKernelGGL(k_readout_bwd_nodes, dim3(nblocks(total, 256)), dim3(256), 0, (hipStream_t)stream, dout,
+                           (long long)stride, nbr, (long long)G * N, N, deg, H, dhf, dhp);
+        return launched();
+    }
     const size_t lds = (size_t)R * (deg + 1) * H * 4;
     // column chunks per graph: 4, or 8 when a quarter of the graph's rows exceeds 48 KB of LDS
     const int S = (lds / 4 <= 48 * 1024 || (H / 4) % 8) ? 4 : 8;

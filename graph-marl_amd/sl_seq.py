@@ -159,13 +159,12 @@ def _backward(p, dR):
     grads = {}
     dR = dR.reshape(Ls * M, 4 * H).contiguous()
 
-    # ---- readout, every step ----
-    dhf = torch.empty(Ls * M, H, device=dev)
+    # ---- readout, every step: dh_final of node v is row v's first segment of dR (read in place by the
+    # cell backward, ld 4H); dh_prev gathered from the neighbours' segments (gm_netmon_readout_bwd, no agent map)
     dhp = torch.empty(Ls * M, H, device=dev)
     for t in range(Ls):
         L.check(lib.gm_netmon_readout_bwd(dR[t * M:(t + 1) * M].data_ptr(), 4 * H, nbr.data_ptr(), None, B, N, N, deg,
-                                          H, dhf[t * M:(t + 1) * M].data_ptr(), dhp[t * M:(t + 1) * M].data_ptr(),
-                                          L.stream_ptr()))
+                                          H, None, dhp[t * M:(t + 1) * M].data_ptr(), L.stream_ptr()))
 
     # ---- LSTM cells, per step, in reverse ----
     S, act, Z = p.S, p.act, p.Z
@@ -195,7 +194,7 @@ def _backward(p, dR):
             a.c_in, a.ld_cin = cin.data_ptr() + 4 * H, S2
             a.c_out, a.ld_cout = S[j, t].data_ptr() + 4 * H, S2
             if j == K:
-                a.dh0, a.ld_dh0 = dhf[t * M:(t + 1) * M].data_ptr(), H
+                a.dh0, a.ld_dh0 = dR[t * M:(t + 1) * M].data_ptr(), 4 * H  # dh_final: segment 0 of dR
             else:
                 a.dh0, a.ld_dh0 = D.data_ptr() + 4 * H, S2  # h part of the next cell's input gradient
                 a.dm, a.ld_dm = D.data_ptr(), S2            # its aggregate part, transposed

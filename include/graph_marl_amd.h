@@ -277,6 +277,10 @@ int gm_mp_aggregate_bwd(const float* dout, const int32_t* nbr, int32_t n_graphs,
 int gm_netmon_readout(const float* h_final, const float* h_prev, const int32_t* nbr, const int32_t* agent_node,
                       int32_t n_graphs, int32_t n_nodes, int32_t n_rows, int32_t deg, int32_t hidden, float* out,
                       int64_t out_stride, void* stream);
+/* Its backward: dh_final[v] / dh_prev[u] = the sums of the dout segments that read them (either output
+ * nullable). Without an agent map (agent_node NULL, n_rows = n_nodes: every node read out, config 5) the
+ * neighbour table must be symmetric (u in nbr(v) <=> v in nbr(u): the routing graphs are), and dh_prev[u] is
+ * gathered from u's neighbours' rows (ascending, the same fp32 sums as the general form). */
 int gm_netmon_readout_bwd(const float* dout, int64_t dout_stride, const int32_t* nbr, const int32_t* agent_node,
                           int32_t n_graphs, int32_t n_nodes, int32_t n_rows, int32_t deg, int32_t hidden,
                           float* dh_final, float* dh_prev, void* stream);
