@@ -2337,13 +2337,20 @@ int dispatch(const ASrc& s0, const ASrc& s1, const float* w, long long ldw, unsi
         if (ax) {
             // tools/train_gemm_bench.py at 262 160 rows: wide forward layers (N >= 256, K >= 512) gain
             // 3-5 % on the 128x128 LDS-DMA tile, short-K and input-gradient GEMMs do not
-            if (s0.mode == GM_A_DENSE &&
-                (tile == 12 || tile == 13 || (tile == -1 && ax == 1 && m >= 32768 && n >= 256 && K >= 512)))
+            // round 6: wide bias layers on the 8-wave ping-pong tile 9 (second accumulator set), tools/gemm_bench.py
+            // SHAPES=train at 1 M rows: DQN layer 1 (K = 642) 2 397 vs 2 630 us, K = 512 layers -4 %
+            if (s0.mode == GM_A_DENSE && epilogue != GM_EPI_LSTM &&
+                (tile == 9 || tile == 10 || (tile == -1 && m >= 32768 && n >= 256 && K >= 512)))
+                gt = tile == 10 ? 10 : 9;
+            else if (s0.mode == GM_A_DENSE &&
+                     (tile == 12 || tile == 13 || (tile == -1 && ax == 1 && m >= 32768 && n >= 256 && K >= 512)))
                 gt = tile == 13 && epilogue != GM_EPI_LSTM ? 13 : 12;
         } else if (tile >= 8)
             gt = tile;
         else if (tile == -1 && s0.mode == GM_A_READOUT && n > 128)
             gt = 9;  // ping-pong: 3 stages (two tiles in flight) 177 -> 172 us for DQN layer 1
+        else if (tile == -1 && s0.mode == GM_A_DENSE && n >= 256 && K >= 512 && m >= 32768 && is_bias_epi(epilogue))
+            gt = 9;  // wide bias layers (the update's target DQN layer 1, config 5's encoder): as above
         else if (tile == -1 && s0.mode == GM_A_DENSE && n >= 128 && K >= 256 && m >= 32768)
             gt = 12;  // N = 128 (the encoder's last layer): 25.9 -> 21.4 us at 40 960 rows
 #define GM_GX(WGM, WGN, TM, TN, EP, AXV) \
@@ -2354,6 +2361,12 @@ int dispatch(const ASrc& s0, const ASrc& s1, const float* w, long long ldw, unsi
                 return ax == 1 ? GM_GX(4, 1, 1, 4, EPI_LSTM, 1) : GM_GX(4, 1, 1, 4, EPI_LSTM, 2);
             }
             ep.act = epi_act(epilogue);
+            if (gt == 9)
+                return ax == 1 ? launch_g<4, 2, 1, 4, 3, GM_A_DENSE, EPI_BIAS, 1, 1>(s0, s1, w, ldw, wb, m, n, K, ep, st, wsi)
+                               : launch_g<4, 2, 1, 4, 3, GM_A_DENSE, EPI_BIAS, 1, 2>(s0, s1, w, ldw, wb, m, n, K, ep, st, wsi);
+            if (gt == 10)
+                return ax == 1 ? launch_g<4, 2, 1, 4, 2, GM_A_DENSE, EPI_BIAS, 1, 1>(s0, s1, w, ldw, wb, m, n, K, ep, st, wsi)
+                               : launch_g<4, 2, 1, 4, 2, GM_A_DENSE, EPI_BIAS, 1, 2>(s0, s1, w, ldw, wb, m, n, K, ep, st, wsi);
             if (gt == 13) return ax == 1 ? GM_GX(2, 2, 2, 2, EPI_BIAS, 1) : GM_GX(2, 2, 2, 2, EPI_BIAS, 2);
             return ax == 1 ? GM_GX(4, 1, 1, 4, EPI_BIAS, 1) : GM_GX(4, 1, 1, 4, EPI_BIAS, 2);
         }
