@@ -6,7 +6,7 @@ mkdir -p gpurun_out/tsq
 export TMPDIR=/tmp
 timeout -s KILL 300 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_INST_LDS \
     SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_VALU_MFMA_BUSY_CYCLES -T --output-format csv -d gpurun_out/tsq -o sq \
-    -- python bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-kernel-timers --no-f32-compare --train-steps 2 \
+    -- python bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-kernel-timers --no-f32-compare --train-steps 2 --graph 0 --no-pmc --no-extras \
     > gpurun_out/tsq/bench.log 2>&1 || exit $?
 python - <<'PY' > gpurun_out/tsq/summary.txt
 import csv, collections
