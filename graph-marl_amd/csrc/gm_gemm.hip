@@ -314,10 +314,15 @@ __device__ __forceinline__ void epilogue(floatx16 (&acc)[TM][TN], const Epi& ep,
                                          int lane, const CIn<TM, EPI>& cin) {
     const int h = lane >> 5, l32 = lane & 31;
     if constexpr (EPI == EPI_BIAS) {
+        // buffer stores on a resource over the wave's rows [wm0, M) (rows past M dropped by its extent), columns
+        // past N at the OOB offset: no per-element branches or 64-bit addresses
+        const __amdgpu_buffer_rsrc_t rs = rsrc_rows(ep.y + wn0, ep.ldy, wm0, (long long)M * ep.ldy * 4);
+        const unsigned ld4 = (unsigned)ep.ldy * 4u;
 #pragma unroll
         for (int j = 0; j < TN; j++) {
             const int col = wn0 + j * 32 + l32;
             const float bv = (ep.bias && col < N) ? ep.bias[col] : 0.f;
+            const unsigned vb = col < N ? 4u * h * ld4 + 4u * (j * 32 + l32) : (unsigned)OOB;
 #pragma unroll
             for (int i = 0; i < TM; i++) {
                 const int rb0 = wm0 + i * 32 + 4 * h;
@@ -326,7 +331,8 @@ __device__ __forceinline__ void epilogue(floatx16 (&acc)[TM][TN], const Epi& ep,
                     const int row = rb0 + (r & 3) + 8 * (r >> 2);
                     float v = acc[i][j][r] + bv;
                     v = act_t<A>(v, ep.act);
-                    if (row < M && col < N) ep.y[(long long)row * ep.ldy + col] = v;
+                    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), rs,
+                                                          (int)(vb + (unsigned)(i * 32 + (r & 3) + 8 * (r >> 2)) * ld4), 0, 0);
                     if (ep.sbits) {  // lanes 0-31 / 32-63: 32 columns of rows row(h = 0) / row(h = 1)
                         const unsigned long long b = __ballot(v > 0.f && col < N);
                         if (l32 == 0 && row < M && wn0 + j * 32 < N)
@@ -341,18 +347,30 @@ __device__ __forceinline__ void epilogue(floatx16 (&acc)[TM][TN], const Epi& ep,
         float bgate[4];
 #pragma unroll
         for (int g = 0; g < 4; g++) bgate[g] = ep.bias ? ep.bias[wn0 + g * 32 + l32] : 0.f;
+        // buffer stores on resources over the wave's rows [wm0, M) (rows past M dropped by their extent), units
+        // past H at the OOB offset: no per-element branches or 64-bit addresses
+        const bool in = unit < H;
+        const unsigned ly = (unsigned)ep.ldy * 4u, lc = (unsigned)ep.ldy2 * 4u, la = (unsigned)H * 16u;
+        const __amdgpu_buffer_rsrc_t ry = rsrc_rows(ep.y + (wn0 >> 2), ep.ldy, wm0, (long long)M * ep.ldy * 4);
+        const __amdgpu_buffer_rsrc_t rc =
+            rsrc_rows(ep.y2 ? ep.y2 + (wn0 >> 2) : ep.y, ep.ldy2, wm0, ep.y2 ? (long long)M * ep.ldy2 * 4 : 0);
+        const __amdgpu_buffer_rsrc_t ra =
+            rsrc_rows(ep.act_out ? ep.act_out + (wn0 >> 2) : ep.y, 4LL * H, wm0, ep.act_out ? (long long)M * H * 16 : 0);
+        const unsigned vy = in ? 4u * h * ly + 4u * l32 : (unsigned)OOB, vc = in ? 4u * h * lc + 4u * l32 : (unsigned)OOB;
+        const unsigned va = in ? 4u * h * la + 4u * l32 : (unsigned)OOB;
+        auto st = [](float v, __amdgpu_buffer_rsrc_t rr, unsigned off) {
+            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), rr, (int)off, 0, 0);
+        };
 #pragma unroll
         for (int i = 0; i < TM; i++) {
-            const int rb0 = wm0 + i * 32 + 4 * h;
 #pragma unroll
             for (int r = 0; r < 16; r++) {
-                const int row = rb0 + (r & 3) + 8 * (r >> 2);
-                if (row >= M || unit >= H) continue;
+                const unsigned rl = (unsigned)(i * 32 + (r & 3) + 8 * (r >> 2));  // row - wm0 - 4 h
                 if (ep.cell == 1) {  // GRU (torch.nn.GRUCell): the 4th tile is W_hn h, kept apart for r * (.)
                     const float rg = sigm(acc[i][0][r] + bgate[0]);
                     const float zg = sigm(acc[i][1][r] + bgate[1]);
                     const float ng = tanh_fast(acc[i][2][r] + bgate[2] + rg * (acc[i][3][r] + bgate[3]));
-                    ep.y[(long long)row * ep.ldy + unit] = (1.f - zg) * ng + zg * cin.v[i][r];
+                    st((1.f - zg) * ng + zg * cin.v[i][r], ry, vy + rl * ly);
                     continue;
                 }
                 float gi = sigm(acc[i][0][r] + bgate[0]);
@@ -361,14 +379,14 @@ __device__ __forceinline__ void epilogue(floatx16 (&acc)[TM][TN], const Epi& ep,
                 float go = sigm(acc[i][3][r] + bgate[3]);
                 float cn = gf * cin.v[i][r] + gi * gg;
                 float hn = go * tanh_fast(cn);
-                ep.y[(long long)row * ep.ldy + unit] = hn;
-                ep.y2[(long long)row * ep.ldy2 + unit] = cn;
+                st(hn, ry, vy + rl * ly);
+                st(cn, rc, vc + rl * lc);
                 if (ep.act_out) {
-                    float* ao = ep.act_out + (long long)row * 4 * H;
-                    ao[unit] = gi;
-                    ao[H + unit] = gf;
-                    ao[2 * H + unit] = gg;
-                    ao[3 * H + unit] = go;
+                    const unsigned ao = va + rl * la;
+                    st(gi, ra, ao);
+                    st(gf, ra, ao + 4u * H);
+                    st(gg, ra, ao + 8u * H);
+                    st(go, ra, ao + 12u * H);
                 }
             }
         }
@@ -1024,6 +1042,13 @@ __device__ __forceinline__ void epilogue16(floatx4 (&acc)[T2][N2], const Epi& ep
     const int l16 = lane & 15, rq = 4 * (lane >> 4);
     if constexpr (EPI == EPI_BIAS) {
         static_assert(N2 % 2 == 0, "column blocks in pairs (32-column sign words)");
+        // buffer stores on a resource over the wave's rows [wm0, M) (rows past M dropped by its extent), columns
+        // past N at the OOB offset: no per-element branches or 64-bit addresses
+        const __amdgpu_buffer_rsrc_t rs = rsrc_rows(ep.y + wn0, ep.ldy, wm0, (long long)M * ep.ldy * 4);
+        const unsigned ld4 = (unsigned)ep.ldy * 4u;
+        unsigned vb[N2];
+#pragma unroll
+        for (int j = 0; j < N2; j++) vb[j] = wn0 + 16 * j + l16 < N ? (unsigned)rq * ld4 + 4u * (16 * j + l16) : (unsigned)OOB;
 #pragma unroll
         for (int jp = 0; jp < N2 / 2; jp++) {
             float bv[2];
@@ -1043,7 +1068,8 @@ __device__ __forceinline__ void epilogue16(floatx4 (&acc)[T2][N2], const Epi& ep
                         const int col = wn0 + (2 * jp + b) * 16 + l16;
                         float v = acc[i][2 * jp + b][r] + bv[b];
                         v = act_t<A>(v, ep.act);
-                        if (row < M && col < N) ep.y[(long long)row * ep.ldy + col] = v;
+                        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), rs,
+                                                              (int)(vb[2 * jp + b] + (unsigned)(i * 16 + r) * ld4), 0, 0);
                         bb[b] = ep.sbits ? __ballot(v > 0.f && col < N) : 0ull;
                     }
                     if (ep.sbits && l16 == 0 && row < M && wn0 + jp * 32 < N) {  // group q: 16 columns of row 4q + r
@@ -1055,9 +1081,24 @@ __device__ __forceinline__ void epilogue16(floatx4 (&acc)[T2][N2], const Epi& ep
         }
     } else {  // EPI_LSTM: N2 == 8 blocks, gate g of unit 16 b + l16 in block 2 g + b
         const int H = ep.hidden;
+        // buffer stores on resources over the wave's rows [wm0, M) (rows past M dropped by their extent), units
+        // past H at the OOB offset: no per-element branches or 64-bit addresses
+        const unsigned ly = (unsigned)ep.ldy * 4u, lc = (unsigned)ep.ldy2 * 4u, la = (unsigned)H * 16u;
+        const __amdgpu_buffer_rsrc_t ry = rsrc_rows(ep.y + (wn0 >> 2), ep.ldy, wm0, (long long)M * ep.ldy * 4);
+        const __amdgpu_buffer_rsrc_t rc =
+            rsrc_rows(ep.y2 ? ep.y2 + (wn0 >> 2) : ep.y, ep.ldy2, wm0, ep.y2 ? (long long)M * ep.ldy2 * 4 : 0);
+        const __amdgpu_buffer_rsrc_t ra =
+            rsrc_rows(ep.act_out ? ep.act_out + (wn0 >> 2) : ep.y, 4LL * H, wm0, ep.act_out ? (long long)M * H * 16 : 0);
+        auto st = [](float v, __amdgpu_buffer_rsrc_t rr, unsigned off) {
+            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), rr, (int)off, 0, 0);
+        };
 #pragma unroll
         for (int b = 0; b < 2; b++) {
             const int unit = (wn0 >> 2) + 16 * b + l16;
+            const bool in = unit < H;
+            const unsigned u4 = 4u * (16 * b + l16);
+            const unsigned vy = in ? rq * ly + u4 : (unsigned)OOB, vc = in ? rq * lc + u4 : (unsigned)OOB;
+            const unsigned va = in ? rq * la + u4 : (unsigned)OOB;
             float bgate[4];
 #pragma unroll
             for (int g = 0; g < 4; g++)  // bl: the block's gate biases staged in LDS (k_gemm3g, EPI_LSTM)
@@ -1067,27 +1108,26 @@ __device__ __forceinline__ void epilogue16(floatx4 (&acc)[T2][N2], const Epi& ep
             for (int i = 0; i < T2; i++)
 #pragma unroll
                 for (int r = 0; r < 4; r++) {
-                    const int row = wm0 + i * 16 + rq + r;
-                    if (row >= M || unit >= H) continue;
+                    const unsigned rl = (unsigned)(i * 16 + r);  // row - wm0 - rq
                     const float a0 = acc[i][b][r] + bgate[0], a1 = acc[i][2 + b][r] + bgate[1];
                     const float a2 = acc[i][4 + b][r] + bgate[2], a3 = acc[i][6 + b][r] + bgate[3];
                     if (ep.cell == 1) {  // GRU: r, z, n_x, n_h tiles
                         const float rg = sigm(a0), zg = sigm(a1);
                         const float ng = tanh_fast(a2 + rg * a3);
-                        ep.y[(long long)row * ep.ldy + unit] = (1.f - zg) * ng + zg * cin.v[i][b][r];
+                        st((1.f - zg) * ng + zg * cin.v[i][b][r], ry, vy + rl * ly);
                         continue;
                     }
                     const float gi = sigm(a0), gf = sigm(a1), gg = tanh_fast(a2), go = sigm(a3);
                     const float cn = gf * cin.v[i][b][r] + gi * gg;
                     const float hn = go * tanh_fast(cn);
-                    ep.y[(long long)row * ep.ldy + unit] = hn;
-                    ep.y2[(long long)row * ep.ldy2 + unit] = cn;
+                    st(hn, ry, vy + rl * ly);
+                    st(cn, rc, vc + rl * lc);
                     if (ep.act_out) {
-                        float* ao = ep.act_out + (long long)row * 4 * H;
-                        ao[unit] = gi;
-                        ao[H + unit] = gf;
-                        ao[2 * H + unit] = gg;
-                        ao[3 * H + unit] = go;
+                        const unsigned ao = va + rl * la;
+                        st(gi, ra, ao);
+                        st(gf, ra, ao + 4u * H);
+                        st(gg, ra, ao + 8u * H);
+                        st(go, ra, ao + 12u * H);
                     }
                 }
         }
@@ -1114,6 +1154,50 @@ __device__ __forceinline__ void dgrad_epilogue16(floatx4 (&acc)[T2][N2], const E
     }
     float mx = 0.f;
     float cs[N2];
+    const int sp = ep.split;
+    const bool blk_lo = n0 + BN <= sp, blk_hi = n0 >= sp;  // block-uniform
+    if (n0 + BN <= N && (blk_lo || blk_hi)) {
+        // the block's columns all on one side of the split and inside N: buffer stores on a resource over
+        // the wave's rows [wm0, M) (rows past M dropped by its extent), the row offset in the VGPR and the
+        // column block in the instruction's offset; no per-element bounds branches or 64-bit addresses
+        const long long ld = blk_lo ? ep.ldy : ep.ldy2;
+        float* yb = blk_lo ? ep.y + wn0 : ep.y2 + (wn0 - sp);
+        const __amdgpu_buffer_rsrc_t rs = rsrc_rows(yb, ld, wm0, (long long)M * ld * 4);
+        const int voff = (rq * (int)ld + l16) * 4, ld4 = (int)ld * 4;
+        if (blk_lo) {
+#pragma unroll
+            for (int j = 0; j < N2; j++) {
+                const int bit = (j & 1) * 16 + l16, wofs = (wn0 - n0 + 16 * j) >> 5;
+                float s = 0.f;
+#pragma unroll
+                for (int i = 0; i < T2; i++)
+#pragma unroll
+                    for (int r = 0; r < 4; r++) {
+                        const int row = wm0 + i * 16 + rq + r;
+                        float v = acc[i][j][r];
+                        if (ep.mbits && !((smb[(row - m0) * WPR + wofs] >> bit) & 1u)) v *= 0.01f;
+                        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), rs, voff + (i * 16 + r) * ld4 + j * 64,
+                                                              0, 0);
+                        const bool in = row < M;
+                        s += in ? v : 0.f;
+                        mx = in ? fmaxf(mx, fabsf(v)) : mx;
+                    }
+                s += __shfl_xor(s, 16);
+                cs[j] = s + __shfl_xor(s, 32);
+            }
+        } else {
+#pragma unroll
+            for (int j = 0; j < N2; j++) {
+#pragma unroll
+                for (int i = 0; i < T2; i++)
+#pragma unroll
+                    for (int r = 0; r < 4; r++)
+                        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(acc[i][j][r]), rs,
+                                                              voff + (i * 16 + r) * ld4 + j * 64, 0, 0);
+                cs[j] = 0.f;
+            }
+        }
+    } else {
 #pragma unroll
     for (int j = 0; j < N2; j++) {
         const int col = wn0 + j * 16 + l16;
@@ -1138,6 +1222,7 @@ __device__ __forceinline__ void dgrad_epilogue16(floatx4 (&acc)[T2][N2], const E
             }
         s += __shfl_xor(s, 16);
         cs[j] = s + __shfl_xor(s, 32);
+    }
     }
     if (ep.gmax) {
         mx = gm_wave_max(mx);
