@@ -2427,8 +2427,11 @@ int dispatch(const ASrc& s0, const ASrc& s1, const float* w, long long ldw, unsi
             if (s0.mode == GM_A_DENSE && epilogue != GM_EPI_LSTM &&
                 (tile == 9 || tile == 10 || (tile == -1 && m >= 32768 && n >= 256 && K >= 512)))
                 gt = tile == 10 ? 10 : 9;
+            // round 6 (row-bounded epilogue stores): the LSTM cells at K = 256 too, 437.5 vs 453.3 us at 262 160 rows
             else if (s0.mode == GM_A_DENSE &&
-                     (tile == 12 || tile == 13 || (tile == -1 && ax == 1 && m >= 32768 && n >= 256 && K >= 512)))
+                     (tile == 12 || tile == 13 ||
+                      (tile == -1 && ax == 1 && m >= 32768 && n >= 256 &&
+                       (K >= 512 || (epilogue == GM_EPI_LSTM && K >= 256)))))
                 gt = tile == 13 && epilogue != GM_EPI_LSTM ? 13 : 12;
         } else if (tile >= 8)
             gt = tile;
