@@ -34,7 +34,8 @@ EXPORTS = [
     "gm_pcg64_seed", "gm_pcg64_choice", "gm_lnlstm_pointwise", "gm_agent_attention", "gm_agent_comm",
     "gm_gemm_x3_dgrad", "gm_lstm_cell_bwd", "gm_qhead_bwd", "gm_netmon_readout_ld", "gm_routing_node_encoder_bits", "gm_gather_records",
     "gm_lnlstm_fwd", "gm_lnlstm_bwd", "gm_gru_pointwise", "gm_gru_bwd", "gm_act_bwd", "gm_build_info",
-    "gm_act_fwd", "gm_act_bwd_z", "gm_obs_from_gemm", "gm_encoder_x3",
+    "gm_act_fwd", "gm_act_bwd_z", "gm_obs_from_gemm", "gm_encoder_x3", "gm_step_mse_blocks", "gm_step_mse",
+    "gm_step_mse_bwd",
 ]
 # kernel-form switches (include/graph_marl_amd_tuning.h)
 TUNING_EXPORTS = ["gm_gemm_set_tile", "gm_gemm_set_wgrad", "gm_gemm_set_mfma", "gm_gemm_set_dgrad", "gm_gemm_form"]
@@ -172,10 +173,15 @@ def lib():
         "gm_act_fwd": [vp, C.c_int64, i32, i32, vp, vp],
         "gm_act_bwd_z": [vp, vp, C.c_int64, i32, i32, vp, vp, i32, vp, vp],
         "gm_obs_from_gemm": [vp, i64, i64, i32, vp, i64, vp],
+        "gm_step_mse_blocks": [i64],
+        "gm_step_mse": [vp, vp, i64, i32, vp, vp],
+        "gm_step_mse_bwd": [vp, vp, i64, i32, vp, C.c_float, vp, vp],
     }
     for name, at in newer.items():
         if hasattr(L, name) or not os.environ.get("GM_LIB"):
             getattr(L, name).argtypes = at
+    if hasattr(L, "gm_step_mse_blocks"):
+        L.gm_step_mse_blocks.restype = i32
     if hasattr(L, "gm_build_info"):
         L.gm_build_info.restype = C.c_char_p
     if hasattr(L, "gm_gemm_form"):

@@ -1812,3 +1812,108 @@ extern "C" int gm_gru_bwd(const float* gi, int64_t ldgi, const float* gh, int64_
     if (e != hipSuccess) return gm_fail(GM_ERR_HIP, std::string("gm_gru_bwd: ") + hipGetErrorString(e));
     return GM_OK;
 }
+
+// ---- per-step mean squared error of the SL unroll (src/sl.py:396-400: mse_loss(pred_all, targets_all) after
+// every unroll step, averaged over the steps) ----
+// pred [L][n] (every step's prediction), tgt [n] (the same target at every step), n % 4 == 0, 16-byte
+// bases. Block b owns float4 indices [b * 256 * V, (b + 1) * 256 * V) of a step; its target elements are loaded
+// once and stay in registers while the block walks the L steps (the target is not re-read per step).
+namespace {
+constexpr int MSE_V = 4;
+
+__global__ __launch_bounds__(256) void k_step_mse_fwd(const float4* __restrict__ pred, const float4* __restrict__ tgt,
+                                                      long long n4, int L, float* __restrict__ part) {
+    __shared__ float wsum[4];
+    const long long base = (long long)blockIdx.x * (256 * MSE_V) + threadIdx.x;
+    float4 t[MSE_V];
+#pragma unroll
+    for (int v = 0; v < MSE_V; v++) {
+        const long long i = base + (long long)v * 256;
+        t[v] = i < n4 ? tgt[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+    for (int l = 0; l < L; l++) {
+        const float4* pl = pred + (long long)l * n4;
+        float4 p[MSE_V];
+#pragma unroll
+        for (int v = 0; v < MSE_V; v++) {
+            const long long i = base + (long long)v * 256;
+            p[v] = i < n4 ? pl[i] : t[v];  // past the end: d = 0
+        }
+        float s = 0.f;
+#pragma unroll
+        for (int v = 0; v < MSE_V; v++) {
+            const float dx = p[v].x - t[v].x, dy = p[v].y - t[v].y, dz = p[v].z - t[v].z, dw = p[v].w - t[v].w;
+            s = fmaf(dx, dx, s);
+            s = fmaf(dy, dy, s);
+            s = fmaf(dz, dz, s);
+            s = fmaf(dw, dw, s);
+        }
+        for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+        if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = s;
+        __syncthreads();
+        if (threadIdx.x == 0) part[(long long)l * gridDim.x + blockIdx.x] = (wsum[0] + wsum[1]) + (wsum[2] + wsum[3]);
+        __syncthreads();
+    }
+}
+
+// grad[l][i] = (pred[l][i] - tgt[i]) * (g[l] * two_over_n): torch's d * (g * (2 / n)) in fp32, element for element
+__global__ __launch_bounds__(256) void k_step_mse_bwd(const float4* __restrict__ pred, const float4* __restrict__ tgt,
+                                                      long long n4, int L, const float* __restrict__ g,
+                                                      float two_over_n, float4* __restrict__ grad) {
+    const long long base = (long long)blockIdx.x * (256 * MSE_V) + threadIdx.x;
+    float4 t[MSE_V];
+#pragma unroll
+    for (int v = 0; v < MSE_V; v++) {
+        const long long i = base + (long long)v * 256;
+        t[v] = i < n4 ? tgt[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+    for (int l = 0; l < L; l++) {
+        const float s = g[l] * two_over_n;
+        const float4* pl = pred + (long long)l * n4;
+        float4* gl = grad + (long long)l * n4;
+        float4 p[MSE_V];
+#pragma unroll
+        for (int v = 0; v < MSE_V; v++) {
+            const long long i = base + (long long)v * 256;
+            p[v] = i < n4 ? pl[i] : t[v];
+        }
+#pragma unroll
+        for (int v = 0; v < MSE_V; v++) {
+            const long long i = base + (long long)v * 256;
+            if (i < n4)
+                gl[i] = make_float4((p[v].x - t[v].x) * s, (p[v].y - t[v].y) * s, (p[v].z - t[v].z) * s,
+                                    (p[v].w - t[v].w) * s);
+        }
+    }
+}
+
+bool mse_args_ok(const float* pred, const float* tgt, int64_t n, int32_t L) {
+    auto a16 = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
+    return pred && tgt && n > 0 && n % 4 == 0 && L > 0 && a16(pred) && a16(tgt) && n / 4 <= (1ll << 40);
+}
+}  // namespace
+
+extern "C" int32_t gm_step_mse_blocks(int64_t n) {
+    return n > 0 ? (int32_t)((n / 4 + 256 * MSE_V - 1) / (256 * MSE_V)) : 0;
+}
+
+extern "C" int gm_step_mse(const float* pred, const float* tgt, int64_t n, int32_t L, float* part, void* stream) {
+    if (!mse_args_ok(pred, tgt, n, L) || !part)
+        return gm_fail(GM_ERR_INVALID_ARG, "gm_step_mse: bad arguments (n % 4 == 0, 16-byte pred / tgt)");
+    const int nb = gm_step_mse_blocks(n);
+    hipLaunchKernelGGL(k_step_mse_fwd, dim3((unsigned)nb), dim3(256), 0, (hipStream_t)stream,
+                       reinterpret_cast<const float4*>(pred), reinterpret_cast<const float4*>(tgt), (long long)(n / 4),
+                       L, part);
+    return launched();
+}
+
+extern "C" int gm_step_mse_bwd(const float* pred, const float* tgt, int64_t n, int32_t L, const float* g,
+                               float two_over_n, float* grad, void* stream) {
+    if (!mse_args_ok(pred, tgt, n, L) || !g || !grad || (reinterpret_cast<uintptr_t>(grad) & 15))
+        return gm_fail(GM_ERR_INVALID_ARG, "gm_step_mse_bwd: bad arguments (n % 4 == 0, 16-byte pred / tgt / grad)");
+    const int nb = gm_step_mse_blocks(n);
+    hipLaunchKernelGGL(k_step_mse_bwd, dim3((unsigned)nb), dim3(256), 0, (hipStream_t)stream,
+                       reinterpret_cast<const float4*>(pred), reinterpret_cast<const float4*>(tgt), (long long)(n / 4),
+                       L, g, two_over_n, reinterpret_cast<float4*>(grad));
+    return launched();
+}

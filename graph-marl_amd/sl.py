@@ -201,18 +201,42 @@ class _StepMSE(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, pred, tgt):
+        steps, n = pred.shape[0], pred[0].numel()
+        ctx.n = n
+        ctx.fused = _step_mse_fits(pred, tgt)
+        if ctx.fused:
+            # one pass over pred with the target held in registers across the steps (gm_step_mse); the
+            # difference is not stored: backward recomputes it from pred and tgt (gm_step_mse_bwd)
+            part = torch.empty(steps, L.lib().gm_step_mse_blocks(n), device=pred.device)
+            L.check(L.lib().gm_step_mse(pred.data_ptr(), tgt.data_ptr(), n, steps, part.data_ptr(), L.stream_ptr()))
+            ctx.save_for_backward(pred, tgt)
+            return part.sum(1) / n
         d = pred - tgt
-        steps, n = d.shape[0], d[0].numel()
         c = next(c for c in (4096, 1024, 256, 64, 16, 4, 1) if n % c == 0)
         per = d.reshape(steps, c, n // c).pow(2).sum(2).sum(1) / n
         ctx.save_for_backward(d)
-        ctx.n = n
         return per
 
     @staticmethod
     def backward(ctx, g):
+        if ctx.fused:
+            pred, tgt = ctx.saved_tensors
+            g = g.contiguous()
+            grad = torch.empty_like(pred)
+            L.check(L.lib().gm_step_mse_bwd(pred.data_ptr(), tgt.data_ptr(), ctx.n, pred.shape[0], g.data_ptr(),
+                                            2.0 / ctx.n, grad.data_ptr(), L.stream_ptr()))
+            return grad, None
         (d,) = ctx.saved_tensors
         return d * (g.view((-1,) + (1,) * (d.dim() - 1)) * (2.0 / ctx.n)), None
+
+
+def _step_mse_fits(pred, tgt):
+    """gm_step_mse covers fp32 device tensors with contiguous rows of a multiple of 4 elements per step and
+    16-byte bases (the config-5 loss: pred_all [L, B, N, N] against targets_all [B, N, N]); other shapes
+    (a --num-targets slice, fp64 host tensors in the CPU tests) take the torch expression."""
+    return (pred.is_cuda and pred.dtype == torch.float32 and tgt.dtype == torch.float32 and pred.is_contiguous()
+            and tgt.is_contiguous() and tgt.shape == pred.shape[1:] and pred[0].numel() % 4 == 0
+            and pred.data_ptr() % 16 == 0 and tgt.data_ptr() % 16 == 0)
 
 
 def train_step(args, model, optim, data, batch_idx):

@@ -267,6 +267,16 @@ int gm_act_bwd(const float* dy, const float* y, int64_t rows, int32_t cols, int3
 int gm_act_fwd(const float* z, int64_t rows, int32_t cols, int32_t act, float* y, void* stream);
 int gm_act_bwd_z(const float* dy, const float* z, int64_t rows, int32_t cols, int32_t act, float* g, float* part,
                  int32_t rows_per_block, float* g_scale, void* stream);
+/* SL regression loss at every unroll step (src/sl.py:396-400: mse_loss(pred_all, targets_all) after each
+ * of the L steps; replaces torch's mse_loss and its autograd): pred [L][n] contiguous, tgt [n] (the same
+ * target at every step), n % 4 == 0, 16-byte bases. gm_step_mse writes per-block partial sums of squared
+ * differences, part [L][gm_step_mse_blocks(n)] (the caller sums each row in order and divides by n);
+ * gm_step_mse_bwd writes grad[l][i] = (pred[l][i] - tgt[i]) * (g[l] * two_over_n) with g the L upstream
+ * gradients of the per-step losses and two_over_n = 2 / n rounded to float. */
+int32_t gm_step_mse_blocks(int64_t n);
+int gm_step_mse(const float* pred, const float* tgt, int64_t n, int32_t L, float* part, void* stream);
+int gm_step_mse_bwd(const float* pred, const float* tgt, int64_t n, int32_t L, const float* g, float two_over_n,
+                    float* grad, void* stream);
 /* Backward of gm_mp_aggregate for symmetric adjacency: dh[j] = Σ_{n ∈ {j} ∪ nbr(j)} dout[n] / cnt(n). */
 int gm_mp_aggregate_bwd(const float* dout, const int32_t* nbr, int32_t n_graphs, int32_t n_nodes, int32_t deg,
                         int32_t hidden, int32_t mode, float* dh, void* stream);

@@ -149,3 +149,23 @@ def test_sl_prod_matches_reference(path):
             assert params[s].grad is None or float(params[s].grad.abs().max()) == 0.0  # not in the loss
             continue
         GU.check(g, "g_" + s, params[s].grad, 1e-5, 1e-4, s)
+
+
+@pytest.mark.parametrize("shape", [(8, 64, 100, 100), (3, 5, 7, 4), (1, 1, 1, 4), (2, 333, 20, 20)])
+def test_step_mse_kernel_matches_torch(shape):
+    """gm_step_mse / gm_step_mse_bwd (the config-5 loss of sl.train_step) vs the per-step mse_loss in fp64
+    (losses at 1e-6 relative) and vs torch's fp32 expression d * (g * (2 / n)) (gradient bit for bit),
+    including element counts that leave a partial last block."""
+    SL, _ = _mods()
+    torch.manual_seed(0)
+    pred = torch.randn(*shape, device="cuda", requires_grad=True)
+    tgt = torch.randn(*shape[1:], device="cuda")
+    assert SL._step_mse_fits(pred, tgt)
+    per = SL._StepMSE.apply(pred, tgt)
+    ref = ((pred.detach().double() - tgt.double()) ** 2).reshape(shape[0], -1).mean(1)
+    torch.testing.assert_close(per.double(), ref, rtol=1e-6, atol=0)
+    w = torch.randn(shape[0], device="cuda")
+    g, = torch.autograd.grad((per * w).sum(), pred)
+    n = pred[0].numel()
+    expect = (pred.detach() - tgt) * (w.view((-1,) + (1,) * (pred.dim() - 1)) * (2.0 / n))
+    assert torch.equal(g, expect)

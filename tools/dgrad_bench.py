@@ -28,7 +28,10 @@ def timeit(fn, reps=5):
 
 m = int(os.environ.get("ROWS", "1040384"))
 out = {}
-for n, k in ((512, 256), (512, 512), (256, 128), (256, 512)):
+SH = ((512, 256), (512, 512), (256, 128), (256, 512))
+if os.environ.get("DSHAPES"):  # n:k,... (output columns : gradient columns; e.g. 512:100, config 5's head)
+    SH = tuple(tuple(int(v) for v in x.split(":")) for x in os.environ["DSHAPES"].split(","))
+for n, k in SH:
     g = torch.randn(m, k, device="cuda") * 1e-6
     w = torch.randn(k, n, device="cuda") / k ** 0.5
     mask = torch.randint(-2 ** 31, 2 ** 31 - 1, (m, (n + 31) // 32), dtype=torch.int32, device="cuda")  # sign words

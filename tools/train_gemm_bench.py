@@ -19,6 +19,8 @@ M = int(os.environ.get("ROWS", "262160"))
 SHAPES = [("fwd.dqn1", 256, 512, "fwd"), ("fwd.enc2", 128, 256, "fwd"), ("fwd.dqn0", 512, 642, "fwd"),
           ("dgrad.dqn1", 512, 256, "dgrad"), ("dgrad.enc2", 256, 128, "dgrad"), ("dgrad.lstm", 256, 512, "dgrad"),
           ("dgrad.dqn0", 512, 512, "dgrad"), ("lstm", 512, 256, "lstm")]
+if os.environ.get("SHAPES"):  # name:N:K:kind,... (e.g. fwd.slhead:100:512:fwd, config 5's output head)
+    SHAPES = [(f[0], int(f[1]), int(f[2]), f[3]) for f in (x.split(":") for x in os.environ["SHAPES"].split(","))]
 
 
 def timeit(fn, reps=10):
