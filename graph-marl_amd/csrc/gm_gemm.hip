@@ -2428,10 +2428,12 @@ int dispatch(const ASrc& s0, const ASrc& s1, const float* w, long long ldw, unsi
                 (tile == 9 || tile == 10 || (tile == -1 && m >= 32768 && n >= 256 && K >= 512)))
                 gt = tile == 10 ? 10 : 9;
             // round 6 (row-bounded epilogue stores): the LSTM cells at K = 256 too, 437.5 vs 453.3 us at 262 160 rows
+            // config 5's output head (N = 100, K = 512, 6.55 M rows): 4242 -> 3620 us on tile 12 (tools/train_gemm_bench.py)
             else if (s0.mode == GM_A_DENSE &&
                      (tile == 12 || tile == 13 ||
-                      (tile == -1 && ax == 1 && m >= 32768 && n >= 256 &&
-                       (K >= 512 || (epilogue == GM_EPI_LSTM && K >= 256)))))
+                      (tile == -1 && ax == 1 && m >= 32768 &&
+                       ((n >= 256 && (K >= 512 || (epilogue == GM_EPI_LSTM && K >= 256))) ||
+                        (n > 64 && K >= 512 && epilogue != GM_EPI_LSTM)))))
                 gt = tile == 13 && epilogue != GM_EPI_LSTM ? 13 : 12;
         } else if (tile >= 8)
             gt = tile;
@@ -2742,8 +2744,10 @@ extern "C" int gm_gemm_x3_dgrad(const gm_a_src* a0, const void* wp, const float*
     const float* w = static_cast<const float*>(wp);
     hipStream_t st = (hipStream_t)stream;
     // tools/dgrad_bench.py at 1.04 M rows: the LDS-DMA tile gains 13-15 % at K = 512 and 2-3 % at
-    // K = 256; the register-staged tile stays ahead at K = 128 (four k tiles)
-    const int form = g_dgrad >= 0 ? g_dgrad : (m >= 32768 && K >= 256 ? 1 : 0);
+    // K = 256; since the row-bounded epilogue stores (round 6) also at K = 128: 256 x 128 with mask, bias partials
+    // and max 615 -> 517 us (128x128), 512 x 128 1070 -> 1010 us (128x256), config 5's head (512 x 100 at
+    // 6.55 M rows, bare) 6179 -> 5193 us (128x256)
+    const int form = g_dgrad >= 0 ? g_dgrad : (m >= 32768 && K >= 64 ? (K < 256 && n >= 512 ? 2 : 1) : 0);
     if (form == 1)  // LDS-DMA 128x128, 4 waves, 2 blocks/CU
         return s0.scale ? launch_g<4, 1, 1, 4, 2, GM_A_DENSE, EPI_DGRAD, 2, 2>(s0, s1, w, ldw, (unsigned)wb, m, n, K, ep,
                                                                                st, wscale_inv)
