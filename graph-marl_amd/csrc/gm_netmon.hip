@@ -758,29 +758,44 @@ __global__ __launch_bounds__(256) void k_readout_bwd_cs(const float* __restrict_
 // segment 0 and dhp(u) = sum over the neighbours v of u, ascending, of row v's segment 1 + (slot of u in v's
 // ascending list) (symmetric adjacency: u is in v's list once). A gather per (node, 16-B chunk) instead of the
 // per-graph LDS staging of k_readout_bwd_cs; the same ascending-row order, so the same fp32 sums
+template <typename I>
 __global__ __launch_bounds__(256) void k_readout_bwd_nodes(const float* __restrict__ dout, long long stride,
                                                            const int32_t* __restrict__ nbr, long long nodes, int N,
                                                            int deg, int H, float* __restrict__ dhf,
                                                            float* __restrict__ dhp) {
-    const int C4 = H >> 2;
-    const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= nodes * C4) return;
-    const long long u = t / C4;
+    // I: the index type of the (node, chunk) decomposition, 32-bit when nodes * H / 4 fits (no 64-bit division)
+    const I C4 = (I)(H >> 2);
+    const I t = (I)blockIdx.x * (I)blockDim.x + (I)threadIdx.x;
+    if ((long long)t >= nodes * C4) return;
+    const I u = t / C4;
     const int c = (int)(t - u * C4);
-    const long long g0 = (u / N) * N;
+    const I g0 = (u / (I)N) * (I)N;
     const int ul = (int)(u - g0);
-    if (dhf) *reinterpret_cast<float4*>(dhf + u * H + 4 * c) = *reinterpret_cast<const float4*>(dout + u * stride + 4 * c);
+    const long long U = (long long)u, G0 = (long long)g0;
+    if (dhf) *reinterpret_cast<float4*>(dhf + U * H + 4 * c) = *reinterpret_cast<const float4*>(dout + U * stride + 4 * c);
     if (!dhp) return;
-    float4 ap = make_float4(0.f, 0.f, 0.f, 0.f);
-    for (int k = 0; k < deg; k++) {
-        const int v = nbr[u * deg + k];
-        if (v < 0 || v >= N) continue;
-        int slot = -1;
-        for (int j = 0; j < deg; j++)
-            if (nbr[(g0 + v) * deg + j] == ul) slot = j;
-        if (slot >= 0) ap = f4add(ap, *reinterpret_cast<const float4*>(dout + (g0 + v) * stride + (1 + slot) * H + 4 * c));
+    // all neighbour ids, then all their lists, then all gradient loads in flight together; summed in ascending k
+    // as before (the same fp32 sums)
+    int v[MAXDEG], slot[MAXDEG];
+#pragma unroll
+    for (int k = 0; k < MAXDEG; k++) v[k] = k < deg ? nbr[U * deg + k] : -1;
+#pragma unroll
+    for (int k = 0; k < MAXDEG; k++) {
+        slot[k] = -1;
+        if (v[k] >= 0 && v[k] < N)
+            for (int j = 0; j < deg; j++)
+                if (nbr[(G0 + v[k]) * deg + j] == ul) slot[k] = j;
     }
-    *reinterpret_cast<float4*>(dhp + u * H + 4 * c) = ap;
+    float4 x[MAXDEG];
+#pragma unroll
+    for (int k = 0; k < MAXDEG; k++)
+        x[k] = slot[k] >= 0 ? *reinterpret_cast<const float4*>(dout + (G0 + v[k]) * stride + (1 + slot[k]) * H + 4 * c)
+                            : make_float4(0.f, 0.f, 0.f, 0.f);
+    float4 ap = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+    for (int k = 0; k < MAXDEG; k++)
+        if (slot[k] >= 0) ap = f4add(ap, x[k]);
+    *reinterpret_cast<float4*>(dhp + U * H + 4 * c) = ap;
 }
 
 extern "C" int gm_netmon_readout_ld(const float* hf, int64_t ldf, const float* hp, int64_t ldp, const int32_t* nbr,
@@ -866,8 +881,12 @@ extern "C" int gm_netmon_readout_bwd(const float* dout, int64_t stride, const in
     if (dhp) { int v = vec_width(H, H, dhp); V = V < v ? V : v; }
     if (!agent_node && R == N && V == 4 && deg <= MAXDEG) {  // every node read out: a gather per node
         const long long total = (long long)G * N * (H / 4);
-        hipLaunchKernelGGL(k_readout_bwd_nodes, dim3(nblocks(total, 256)), dim3(256), 0, (hipStream_t)stream, dout,
-                           (long long)stride, nbr, (long long)G * N, N, deg, H, dhf, dhp);
+        if (total + 256 < (1ll << 31))
+            hipLaunchKernelGGL(k_readout_bwd_nodes<unsigned>, dim3(nblocks(total, 256)), dim3(256), 0,
+                               (hipStream_t)stream, dout, (long long)stride, nbr, (long long)G * N, N, deg, H, dhf, dhp);
+        else
+            hipLaunchKernelGGL(k_readout_bwd_nodes<long long>, dim3(nblocks(total, 256)), dim3(256), 0,
+                               (hipStream_t)stream, dout, (long long)stride, nbr, (long long)G * N, N, deg, H, dhf, dhp);
         return launched();
     }
     const size_t lds = (size_t)R * (deg + 1) * H * 4;
